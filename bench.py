@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark: ELBO inner-steps/sec of the coreset-weighted inner loop on MI355X.
+
+Workload (BASELINE.json north star / SURVEY.md §8(d)): fn2 = make_fc2net
+(VILinearMultivariateNormal 64 -> 40 -> 40 -> 2, full-covariance Gaussian
+posterior, P = 4,730,326 parameters), M = 100 pseudopoints, S = 128 MC
+samples PER GPU (C3 on one GPU; weak scaling: S = 128 N on N GPUs, the
+N = 8 point being the C4 sample count).  One step = fresh eps draw (Philox),
+reparameterised sampling x_s = mean + L eps_s, batched forward over S x M,
+coreset-weighted NLL + KL, hand-derived backward, higher-Adam update of all
+parameters.  Inputs are synthetic (make_synthetic-shaped: X ~ N(0, I_64),
+labels ~ Bernoulli(sigmoid(5 sum x))), parameters at the reference init
+(mean = 0, sd = softplus^-1(1e-6), corr = 0), N_data = 800, v = 0.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "blackbox-coresets-vi_amd"))
+
+import torch  # noqa: E402
+
+LAYERS = [(64, 40), (40, 40), (40, 2)]
+S_PER_GPU = 128
+M = 100
+N_DATA = 800
+LR = 1e-3
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense peak (spec)
+
+
+def synthetic_inputs(device, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randn(M, LAYERS[0][0], generator=g)
+    p = torch.sigmoid(5.0 * u.sum(1))
+    z = (torch.rand(M, generator=g) < p).to(torch.int32)
+    w = torch.full((M,), N_DATA / M)  # N * softmax(v = 0)
+    return u.to(device), z.to(device), w.to(device)
+
+
+def reference_init_params(n_layers_sizes, device):
+    parts = []
+    isp = math.log(math.expm1(1e-6))
+    for din, dout in n_layers_sizes:
+        n = din * dout + dout
+        parts += [torch.zeros(n), torch.full((n,), isp), torch.zeros((n - 1) * (n - 2) // 2)]
+    return torch.cat(parts).to(device)
+
+
+def algorithmic_work(S, rows_frac=1.0):
+    """Per-launch algorithmic bytes / flops of the two dominant kernels
+    (SURVEY.md §8(d)); rows_frac = this rank's share of the rows (nnz)."""
+    n = [i * o + o for i, o in LAYERS]
+    n_tot = sum(n)
+    nc = sum((k - 1) * (k - 2) // 2 for k in n)
+    upd_bytes = (24 * (nc + 2 * n_tot)) * rows_frac + 8 * S * n_tot * rows_frac + 4 * S * n_tot
+    upd_flops = 2.0 * S * nc * rows_frac
+    fwd_flops = 2.0 * S * nc * rows_frac
+    fwd_bytes = 4 * (nc + 2 * n_tot) * rows_frac + 4 * S * n_tot + 4 * S * n_tot * rows_frac
+    return dict(update=dict(bytes=upd_bytes, flops=upd_flops),
+                sample=dict(bytes=fwd_bytes, flops=fwd_flops))
+
+
+def cpu_baseline(budget_s=12.0):
+    """Op-faithful torch CPU restatement of the reference inner step
+    (oracle/cpu_reference.py) on a bounded number of C3 steps."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from cpu_reference import RefInnerStep, reference_init
+
+    torch.manual_seed(0)
+    r = RefInnerStep("mvn", LAYERS, S_PER_GPU)
+    p0 = reference_init("mvn", LAYERS)
+    u, z, w = synthetic_inputs("cpu")
+    z = z.float()
+    r.run(p0, u, z, w, 2, LR)  # warm-up
+    t0 = time.perf_counter()
+    r.run(p0, u, z, w, 3, LR)
+    per = (time.perf_counter() - t0) / 3
+    n = max(3, min(60, int(budget_s / max(per, 1e-3))))
+    t0 = time.perf_counter()
+    r.run(p0, u, z, w, n, LR)
+    dt = time.perf_counter() - t0
+    try:
+        model = open("/proc/cpuinfo").read().split("model name")[1].split(":")[1].split("\n")[0].strip()
+    except Exception:
+        model = "unknown"
+    return dict(value=n / dt, unit="inner-steps/s", cores=torch.get_num_threads(), kind="port",
+                sample=(f"C3 fn2 S=128 M=100: one nested inner loop of {n} steps "
+                        f"(autograd.grad create_graph=True + higher-Adam, anomaly off) "
+                        f"in {dt:.1f} s on {torch.get_num_threads()} threads of {model}"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from psvi.runtime import InnerLoopPlan, randn_
+    from psvi.runtime.sharded import ShardedInnerLoop, TorchDistComm
+
+    S = S_PER_GPU * world
+    u, z, w = synthetic_inputs(dev)
+    if world == 1:
+        plan = InnerLoopPlan("fullcov", LAYERS, S, M)
+        loop = None
+        rows_frac = 1.0
+    else:
+        loop = ShardedInnerLoop("fullcov", LAYERS, S, M, world, rank, device=dev,
+                                comm=TorchDistComm())
+        plan = loop.plan
+        n = [i * o + o for i, o in LAYERS]
+        info = loop.info[rank]
+        nnz_own = 0
+        for l, k in enumerate(n):
+            lo, hi = info["row_lo"][l], info["row_lo"][l] + info["row_cnt"][l]
+            nnz_own += sum(min(r, k - 1) for r in range(lo, hi))
+        rows_frac = nnz_own / sum((k - 1) * (k - 2) // 2 for k in n)
+    params = reference_init_params(LAYERS, dev)
+    m = torch.zeros_like(params)
+    v = torch.zeros_like(params)
+    eps = torch.empty(plan.eps_count, device=dev)
+    eps_stride = (plan.eps_count + 3) // 4 * 4
+    f32 = dict(dtype=torch.float32, device=dev)
+    if world == 1:
+        xs = torch.empty(plan.xshard_count, **f32)
+        gs = torch.empty(plan.xshard_count, **f32)
+    total_steps = args.warmup + args.steps
+    parts = torch.zeros(total_steps, 2, **f32)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+
+    def one_step(k, timed):
+        randn_(eps, seed=20251015, offset=k * eps_stride)
+        t = k + 1  # Adam step of one long inner loop (never reset here)
+        e = ev[k - args.warmup] if timed else None
+        if world == 1:
+            if e: e[0].record()
+            plan.mvn_sample(eps, params, xs)
+            if e: e[1].record()
+            plan.mvn_net(u, z, w, xs, gs, parts[k, 0:1])
+            if e: e[2].record()
+            plan.mvn_update(eps, gs, params, m, v, step=t, lr=LR, kl_out=parts[k, 1:2])
+            if e: e[3].record()
+        else:
+            if e: e[0].record()
+            loop.phase_sample(eps, params)
+            if e: e[1].record()
+            loop.comm.all_to_all(loop.x_recv, loop.x_shard, loop.x_out, loop.x_in)
+            loop.phase_net(u, z, w)
+            loop.comm.all_to_all(loop.g_shard, loop.g_send, loop.g_out, loop.g_in)
+            if e: e[2].record()
+            loop.phase_update(eps, params, m, v, t, LR, "higher")
+            if e: e[3].record()
+            parts[k].copy_(loop.parts)
+
+    for k in range(args.warmup):
+        one_step(k, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total_steps):
+        one_step(k, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # per-phase device time (HIP events on the launch stream)
+    ph = {"sample": [], "exchange+net": [], "update": []}
+    for e in ev:
+        ph["sample"].append(e[0].elapsed_time(e[1]))
+        ph["exchange+net"].append(e[1].elapsed_time(e[2]))
+        ph["update"].append(e[2].elapsed_time(e[3]))
+    avg_ms = {k: sum(x) / len(x) for k, x in ph.items()}
+    elbo = parts.sum(-1)
+    if world > 1:
+        dist.all_reduce(elbo)
+    finite = bool(torch.isfinite(elbo).all().item())
+
+    steps_per_s = args.steps / elapsed
+    value = steps_per_s * (S / S_PER_GPU)
+    work = algorithmic_work(S, rows_frac)
+    upd_s = avg_ms["update"] * 1e-3
+    smp_s = avg_ms["sample"] * 1e-3
+    kernels = {
+        "mvn_update_kernel": dict(avg_us=avg_ms["update"] * 1e3,
+                                  gbs=work["update"]["bytes"] / upd_s / 1e9,
+                                  tflops=work["update"]["flops"] / upd_s / 1e12),
+        "mvn_fwd_kernel": dict(avg_us=avg_ms["sample"] * 1e3,
+                               gbs=work["sample"]["bytes"] / smp_s / 1e9,
+                               tflops=work["sample"]["flops"] / smp_s / 1e12),
+        "net_kernel(+exchange)": dict(avg_us=avg_ms["exchange+net"] * 1e3),
+    }
+    achieved = work["update"]["bytes"] / upd_s / 1e9
+    roofline = dict(bound="hbm", kernel="mvn_update_kernel", achieved=round(achieved, 1),
+                    peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
+                    traffic=None,
+                    algorithmic_bytes_per_launch=int(work["update"]["bytes"]),
+                    kernels={k: {kk: round(vv, 2) for kk, vv in d.items()}
+                             for k, d in kernels.items()},
+                    mfma_frac_fwd=round(kernels["mvn_fwd_kernel"]["tflops"] /
+                                        FP32_MFMA_PEAK_TFLOPS, 4))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_budget)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        out = {
+            "metric": "ELBO inner-steps/sec (S MC samples x M pseudopoints) at 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "inner-steps/s (S=128 x M=100 fn2 C3 shards; S = 128 x n_gpus)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (make_synthetic-shaped X~N(0,I64), Bernoulli labels; reference init)",
+            "config": {"workload": "C3 fn2 full-cov MLP 64-40-40-2 per GPU (C4 sample count at 8 GPUs)",
+                       "S_total": S, "S_per_gpu": S_PER_GPU, "M": M, "D": 64, "H": 40, "C": 2,
+                       "params": plan.param_count, "parallelism": f"rows-of-L x samples sharded over {world}",
+                       "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

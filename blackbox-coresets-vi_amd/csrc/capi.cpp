@@ -1,0 +1,405 @@
+// capi.cpp -- extern "C" boundary of libpsvi_hip.so (declared in include/psvi_hip.h).
+//
+// Plans hold the immutable geometry of one (family, layer sizes, S, M, world,
+// rank) configuration: sample shards, nnz-balanced row shards of every
+// full-cov layer, and the device work lists of the packed-triangular kernels.
+// Steps are pure stream-ordered kernel launches + hipMemsetAsync (graph
+// capturable: no allocation, no synchronisation).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "psvi_internal.hpp"
+
+namespace psvi {
+size_t net_plan_geometry(psvi_plan& p);  // kernels_net.hip
+void net_set_lds_limit();                // kernels_net.hip
+}  // namespace psvi
+
+using namespace psvi;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    g_err = std::string(where) + ": " + hipGetErrorString(e);
+    return (int)e;
+}
+
+#define HIP_TRY(expr)                                      \
+    do {                                                   \
+        hipError_t e_ = (expr);                            \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+    } while (0)
+
+constexpr int kFwdKChunk = 512;  // columns of L per forward work item
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// nnz-balanced contiguous split of rows [0, n) of a full-cov layer: row r
+// owns r strict-lower corr entries (r <= n-2) plus mean and sd.
+void split_rows(int n, int world, int* lo, int* hi) {
+    std::vector<double> cum(n + 1, 0.0);
+    for (int r = 0; r < n; ++r) cum[r + 1] = cum[r] + (r <= n - 2 ? r : 0) + 2.0;
+    const double tot = cum[n];
+    int start = 0;
+    for (int q = 0; q < world; ++q) {
+        int end = n;
+        if (q < world - 1) {
+            const double target = tot * (q + 1) / world;
+            end = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+            end = std::max(start, std::min(end, n));
+        }
+        lo[q] = start;
+        hi[q] = end;
+        start = end;
+    }
+}
+
+template <class T>
+int upload(const std::vector<T>& v, T** dst) {
+    *dst = nullptr;
+    if (v.empty()) return 0;
+    HIP_TRY(hipMalloc((void**)dst, sizeof(T) * v.size()));
+    HIP_TRY(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int check_desc(const psvi_net_desc* d) {
+    if (!d) return fail(PSVI_EINVAL, "null descriptor");
+    if (d->n_layers < 1 || d->n_layers > PSVI_MAX_LAYERS)
+        return fail(PSVI_EINVAL, "n_layers out of range [1, 8]");
+    for (int l = 0; l <= d->n_layers; ++l)
+        if (d->dims[l] < 1) return fail(PSVI_EINVAL, "layer dims must be >= 1");
+    if (d->S < 1) return fail(PSVI_EINVAL, "S must be >= 1");
+    if (d->M < 1) return fail(PSVI_EINVAL, "M must be >= 1");
+    if (!(d->prior_sd > 0.f)) return fail(PSVI_EINVAL, "prior_sd must be > 0");
+    return 0;
+}
+
+int build_plan(psvi_plan& p) {
+    const psvi_net_desc& d = p.d;
+    p.L = d.n_layers;
+    int64_t po = 0, eo = 0;
+    int wo = 0;
+    for (int l = 0; l < p.L; ++l) {
+        LayerInfo& li = p.lay[l];
+        li.din = d.dims[l];
+        li.dout = d.dims[l + 1];
+        li.n = li.din * li.dout + li.dout;
+        li.nc = (int64_t)(li.n - 1) * (li.n - 2) / 2;
+        li.poff = po;
+        li.eoff = eo;
+        li.woff = wo;
+        po += p.family == PSVI_FAMILY_MEANFIELD ? 2 * (int64_t)li.n : 2 * (int64_t)li.n + li.nc;
+        eo += (int64_t)d.S * li.n;
+        wo += li.n;
+    }
+    p.P = po;
+    p.Peps = eo;
+    p.n_tot = wo;
+    // sample shards
+    for (int q = 0; q < p.world; ++q) {
+        const int base = d.S / p.world, rem = d.S % p.world;
+        p.s_cnt[q] = base + (q < rem ? 1 : 0);
+        p.s_off[q] = q * base + std::min(q, rem);
+    }
+    // row shards
+    for (int q = 0; q < p.world; ++q) p.rows_tot[q] = 0;
+    for (int l = 0; l < p.L; ++l) {
+        int lo[kMaxWorld], hi[kMaxWorld];
+        if (p.family == PSVI_FAMILY_FULLCOV) {
+            split_rows(p.lay[l].n, p.world, lo, hi);
+        } else {
+            for (int q = 0; q < p.world; ++q) { lo[q] = 0; hi[q] = p.lay[l].n; }
+        }
+        for (int q = 0; q < p.world; ++q) {
+            p.row_lo[q][l] = lo[q];
+            p.row_hi[q][l] = hi[q];
+            p.xcol_l[q][l] = p.rows_tot[q];
+            p.rows_tot[q] += hi[q] - lo[q];
+        }
+    }
+    p.acc_count = 4 + 2 * (int64_t)p.n_tot;
+    net_plan_geometry(p);
+    if (p.net_lds > 160 * 1024)
+        return fail(PSVI_EUNSUP, "layer too wide for the per-sample LDS network kernel");
+
+    const int S = d.S, r = p.rank;
+    if (p.family == PSVI_FAMILY_FULLCOV) {
+        std::vector<FwdItem> fwd;
+        std::vector<BwdTile> bwd;
+        std::vector<DiagBlock> diag;
+        for (int l = 0; l < p.L; ++l) {
+            const int n = p.lay[l].n, lo = p.row_lo[r][l], hi = p.row_hi[r][l];
+            const int xc = p.xcol_l[r][l];
+            for (int r0 = lo; r0 < hi; r0 += 32) {
+                const int r1 = std::min(r0 + 32, hi);
+                const int kmax = std::max(0, std::min(r1 - 1, n - 2));
+                const int nit = std::max(1, (kmax + kFwdKChunk - 1) / kFwdKChunk);
+                // even split, multiples of 32 columns
+                const int steps = (kmax + 31) / 32;
+                for (int i = 0; i < nit; ++i) {
+                    const int k0 = std::min(kmax, 32 * (int)((int64_t)steps * i / nit));
+                    const int k1 = std::min(kmax, 32 * (int)((int64_t)steps * (i + 1) / nit));
+                    if (i > 0 && k0 >= k1) continue;
+                    fwd.push_back(FwdItem{l, r0, r1, k0, k1, xc + (r0 - lo)});
+                }
+            }
+            const int thi = std::min(hi, n - 1);
+            for (int r0 = lo; r0 < thi; r0 += 64) {
+                const int cmax = std::min(r0 + 63, n - 2);  // c < r <= cmax
+                for (int c0 = 0; c0 < cmax; c0 += 64)
+                    bwd.push_back(BwdTile{l, r0, c0, lo, thi, xc - lo});
+            }
+            for (int r0 = lo; r0 < hi; r0 += 256)
+                diag.push_back(DiagBlock{l, r0, hi, xc - lo});
+        }
+        // longest forward items first
+        std::stable_sort(fwd.begin(), fwd.end(), [](const FwdItem& a, const FwdItem& b) {
+            return (a.k1 - a.k0) > (b.k1 - b.k0);
+        });
+        p.h_fwd = fwd;
+        p.h_bwd = bwd;
+        p.h_diag = diag;
+        p.n_fwd = (int)fwd.size();
+        p.n_bwd = (int)bwd.size();
+        p.n_diag = (int)diag.size();
+        const size_t xs = sizeof(float) * (size_t)S * p.rows_tot[r];
+        p.ws_bytes = align256(xs) * 2 + 256;
+    } else {
+        p.ws_bytes = align256(sizeof(float) * (size_t)p.acc_count);
+    }
+    return 0;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+const char* psvi_last_error(void) { return g_err.c_str(); }
+const char* psvi_version(void) { return "psvi_hip 0.1.0 (gfx950)"; }
+
+int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int32_t rank,
+                     psvi_plan** out) {
+    if (!out) return fail(PSVI_EINVAL, "null out");
+    *out = nullptr;
+    if (int rc = check_desc(d)) return rc;
+    if (family != PSVI_FAMILY_MEANFIELD && family != PSVI_FAMILY_FULLCOV)
+        return fail(PSVI_EINVAL, "unknown family");
+    if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world)
+        return fail(PSVI_EINVAL, "world/rank out of range (world <= 8)");
+    int ndev = 0;
+    const bool have_dev = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
+    if (have_dev) {
+        static std::once_flag once;
+        std::call_once(once, net_set_lds_limit);
+    }
+    psvi_plan* p = new psvi_plan();
+    p->family = family;
+    p->d = *d;
+    p->world = world;
+    p->rank = rank;
+    int rc = build_plan(*p);
+    if (!rc && have_dev) {
+        // the only device allocations of the library: immutable work lists
+        if (!(rc = upload(p->h_fwd, &p->d_fwd)) && !(rc = upload(p->h_bwd, &p->d_bwd)))
+            rc = upload(p->h_diag, &p->d_diag);
+        p->on_device = rc == 0;
+    }
+    if (rc) {
+        psvi_plan_destroy(p);
+        return rc;
+    }
+    *out = p;
+    return 0;
+}
+
+int psvi_plan_destroy(psvi_plan* p) {
+    if (!p) return 0;
+    if (p->d_fwd) (void)hipFree(p->d_fwd);
+    if (p->d_bwd) (void)hipFree(p->d_bwd);
+    if (p->d_diag) (void)hipFree(p->d_diag);
+    delete p;
+    return 0;
+}
+
+int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
+    if (!p || !value) return fail(PSVI_EINVAL, "null argument");
+    const int r = p->rank;
+    switch (key) {
+        case PSVI_Q_PARAM_COUNT: *value = p->P; break;
+        case PSVI_Q_EPS_COUNT: *value = p->Peps; break;
+        case PSVI_Q_WS_BYTES: *value = (int64_t)p->ws_bytes; break;
+        case PSVI_Q_S_LOCAL: *value = p->s_cnt[r]; break;
+        case PSVI_Q_S_OFFSET: *value = p->s_off[r]; break;
+        case PSVI_Q_ACC_COUNT: *value = p->acc_count; break;
+        case PSVI_Q_ROWS_LOCAL: *value = p->rows_tot[r]; break;
+        case PSVI_Q_XSHARD_COUNT: *value = (int64_t)p->d.S * p->rows_tot[r]; break;
+        case PSVI_Q_XRECV_COUNT: *value = (int64_t)p->s_cnt[r] * p->n_tot; break;
+        default: return fail(PSVI_EINVAL, "unknown query key");
+    }
+    return 0;
+}
+
+int psvi_plan_shard_info(const psvi_plan* p, int32_t r, int64_t* out) {
+    if (!p || !out) return fail(PSVI_EINVAL, "null argument");
+    if (r < 0 || r >= p->world) return fail(PSVI_EINVAL, "rank out of range");
+    out[0] = p->s_off[r];
+    out[1] = p->s_cnt[r];
+    out[2] = p->rows_tot[r];
+    for (int l = 0; l < PSVI_MAX_LAYERS; ++l) {
+        out[3 + l] = l < p->L ? p->row_lo[r][l] : 0;
+        out[3 + PSVI_MAX_LAYERS + l] = l < p->L ? p->row_hi[r][l] - p->row_lo[r][l] : 0;
+    }
+    return 0;
+}
+
+static int check_step(const psvi_plan* p, const void* u, const void* z, const void* w,
+                      const void* eps, size_t ws_bytes, const void* ws) {
+    if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (p->world != 1) return fail(PSVI_ESTATE, "fused step needs world == 1 (use phases)");
+    if (!u || !z || !w || !eps) return fail(PSVI_EINVAL, "null input pointer");
+    if (!ws || ws_bytes < p->ws_bytes) return fail(PSVI_ENOSPC, "workspace too small");
+    return 0;
+}
+
+static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                     const float* eps, float* params, float* m, float* v,
+                     const psvi_adam_hp* hp, float* elbo_out, float* grad_out,
+                     int include_kl, void* ws, hipStream_t st) {
+    HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(float), st));
+    char* wsb = (char*)ws;
+    if (p->family == PSVI_FAMILY_MEANFIELD) {
+        float* acc = (float*)wsb;
+        HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
+        HIP_TRY(launch_net(*p, u, z, w, params, eps, acc + 4, acc + 4 + p->n_tot, nullptr,
+                           nullptr, acc, st));
+        HIP_TRY(launch_mf_update(*p, acc, params, m, v, hp, elbo_out, grad_out, include_kl, st));
+    } else {
+        const size_t xs = sizeof(float) * (size_t)p->d.S * p->rows_tot[0];
+        float* x = (float*)wsb;
+        float* g = (float*)(wsb + align256(xs));
+        HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
+        if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
+        HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x, g, elbo_out, st));
+        HIP_TRY(launch_mvn_update(*p, eps, g, params, m, v, hp, elbo_out, grad_out, include_kl,
+                                  st));
+    }
+    return 0;
+}
+
+int psvi_inner_step(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                    const float* eps, float* params, float* adam_m, float* adam_v,
+                    const psvi_adam_hp* hp, float* elbo_out, void* ws, size_t ws_bytes,
+                    void* stream) {
+    if (int rc = check_step(p, u, z, w, eps, ws_bytes, ws)) return rc;
+    if (!params || !adam_m || !adam_v || !hp || !elbo_out)
+        return fail(PSVI_EINVAL, "null state pointer");
+    if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    return step_impl(p, u, z, w, eps, params, adam_m, adam_v, hp, elbo_out, nullptr, 1, ws,
+                     as_stream(stream));
+}
+
+int psvi_elbo_grad(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                   const float* eps, const float* params, int32_t include_kl, float* elbo_out,
+                   float* grad_out, void* ws, size_t ws_bytes, void* stream) {
+    if (int rc = check_step(p, u, z, w, eps, ws_bytes, ws)) return rc;
+    if (!params || !elbo_out || !grad_out) return fail(PSVI_EINVAL, "null pointer");
+    return step_impl(p, u, z, w, eps, const_cast<float*>(params), nullptr, nullptr, nullptr,
+                     elbo_out, grad_out, include_kl ? 1 : 0, ws, as_stream(stream));
+}
+
+int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* z,
+                             const float* w, const float* eps, const float* params, float* acc,
+                             void* stream) {
+    if (!p || p->family != PSVI_FAMILY_MEANFIELD) return fail(PSVI_ESTATE, "not a mean-field plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!u || !z || !w || !eps || !params || !acc) return fail(PSVI_EINVAL, "null pointer");
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
+    HIP_TRY(launch_net(*p, u, z, w, params, eps, acc + 4, acc + 4 + p->n_tot, nullptr, nullptr,
+                       acc, st));
+    return 0;
+}
+
+int psvi_mf_phase_update(const psvi_plan* p, const float* acc, float* params, float* adam_m,
+                         float* adam_v, const psvi_adam_hp* hp, float* elbo_out,
+                         float* grad_out, void* stream) {
+    if (!p || p->family != PSVI_FAMILY_MEANFIELD) return fail(PSVI_ESTATE, "not a mean-field plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!acc || !params) return fail(PSVI_EINVAL, "null pointer");
+    if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
+    if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    hipStream_t st = as_stream(stream);
+    if (elbo_out) HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(float), st));
+    HIP_TRY(launch_mf_update(*p, acc, params, adam_m, adam_v, hp, elbo_out, grad_out, 1, st));
+    return 0;
+}
+
+int psvi_mvn_phase_sample(const psvi_plan* p, const float* eps, const float* params,
+                          float* x_shard, void* stream) {
+    if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!eps || !params || !x_shard) return fail(PSVI_EINVAL, "null pointer");
+    HIP_TRY(launch_mvn_fwd(*p, eps, params, x_shard, as_stream(stream)));
+    return 0;
+}
+
+int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                       const float* x_recv, float* g_send, float* nll_out, void* stream) {
+    if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!u || !z || !w || !x_recv || !g_send || !nll_out) return fail(PSVI_EINVAL, "null pointer");
+    hipStream_t st = as_stream(stream);
+    if (p->mchunks > 1)
+        HIP_TRY(hipMemsetAsync(g_send, 0,
+                               sizeof(float) * (size_t)p->s_cnt[p->rank] * p->n_tot, st));
+    HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x_recv, g_send, nll_out,
+                       st));
+    return 0;
+}
+
+int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_shard,
+                          float* params, float* adam_m, float* adam_v, const psvi_adam_hp* hp,
+                          float* kl_out, float* grad_out, int32_t include_kl, void* stream) {
+    if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!eps || !g_shard || !params) return fail(PSVI_EINVAL, "null pointer");
+    if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
+    if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, grad_out,
+                              include_kl ? 1 : 0, as_stream(stream)));
+    return 0;
+}
+
+int psvi_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, void* stream) {
+    if (!out || n < 0) return fail(PSVI_EINVAL, "bad randn arguments");
+    if (offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");
+    HIP_TRY(launch_randn(out, n, seed, offset, as_stream(stream)));
+    return 0;
+}
+
+int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m, float* adam_v,
+                     const psvi_adam_hp* hp, void* stream) {
+    if (n < 0 || !params || !grad || !adam_m || !adam_v || !hp)
+        return fail(PSVI_EINVAL, "bad adam arguments");
+    if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    HIP_TRY(launch_adam(n, params, grad, adam_m, adam_v, hp, as_stream(stream)));
+    return 0;
+}
+
+}  // extern "C"

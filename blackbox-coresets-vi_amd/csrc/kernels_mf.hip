@@ -1,0 +1,208 @@
+// kernels_mf.hip -- mean-field (VILinear) KL + gradient assembly + Adam, the
+// generic fused Adam, and the Philox normal generator.
+//
+// Reference (/root/reference):
+//   VIMixin.kl              psvi/models/neural_net.py:101-108 (-> torch
+//                           _kl_normal_normal: 0.5(vr + t1 - 1 - log vr))
+//   softplus sigma          neural_net.py:133-135, 150-153
+//   DifferentiableAdam      psvi/robust_higher/optim.py:299-367
+//   hypergrad adam_step     psvi/hypergrad/diff_optimizers.py:184-213
+// Gradient: d mu = sum_s dW_s + mu/s0^2,
+//   d rho = (sum_s dW_s*eps_s + sp/s0^2 - 1/sp) * sigmoid(rho).
+#include "psvi_internal.hpp"
+
+namespace psvi {
+
+AdamC make_adam(const psvi_adam_hp* hp) {
+    AdamC a{};
+    a.lr = hp->lr;
+    a.b1 = hp->beta1;
+    a.b2 = hp->beta2;
+    a.eps = hp->eps;
+    a.omb1 = 1.f - hp->beta1;
+    a.omb2 = 1.f - hp->beta2;
+    const double bc1 = 1.0 - std::pow((double)hp->beta1, (double)hp->step);
+    const double bc2 = 1.0 - std::pow((double)hp->beta2, (double)hp->step);
+    a.inv_bc1 = (float)(1.0 / bc1);
+    a.inv_sqrt_bc2 = (float)(1.0 / std::sqrt(bc2));
+    a.lr_bc1 = (float)(hp->lr / bc1);
+    a.inv_bc2 = (float)(1.0 / bc2);
+    a.kind = hp->kind;
+    return a;
+}
+
+struct MfUpdArgs {
+    int L;
+    int woff[kMaxL + 1];
+    int64_t poff[kMaxL];
+    int n[kMaxL];
+    const float* acc;   // [nll pad(4) | sum dW (n_tot) | sum dW*eps (n_tot)]
+    int n_tot;
+    float* params;
+    float* m;
+    float* v;
+    float* grad_out;
+    float* elbo_out;
+    int include_kl;
+    float inv_s0sq, log_s0;
+    AdamC adam;
+};
+
+__device__ __forceinline__ void mf_upd(const MfUpdArgs& a, int64_t pidx, float g) {
+    if (a.grad_out) {
+        a.grad_out[pidx] = g;
+    } else {
+        float mm = a.m[pidx], vv = a.v[pidx];
+        a.params[pidx] = adam_apply(a.adam, a.params[pidx], g, mm, vv);
+        a.m[pidx] = mm;
+        a.v[pidx] = vv;
+    }
+}
+
+__global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
+    __shared__ float red[8];
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    float klp = 0.f;
+    if (e < a.n_tot) {
+        int l = 0;
+        while (l + 1 < a.L && e >= a.woff[l + 1]) ++l;
+        const int idx = e - a.woff[l];
+        const int64_t pmu = a.poff[l] + idx, prho = pmu + a.n[l];
+        const float mu = a.params[pmu], rho = a.params[prho];
+        const float sp = softplus_f(rho), sg = sigmoid_f(rho);
+        const float* accMu = a.acc + 4;
+        const float* accRho = accMu + a.n_tot;
+        float gmu = accMu[e], grho = accRho[e] * sg;
+        if (a.include_kl) {
+            gmu += mu * a.inv_s0sq;
+            grho += (sp * a.inv_s0sq - 1.f / sp) * sg;
+            // _kl_normal_normal with q = N(0, s0): 0.5(vr + mu^2/s0^2 - 1 - log vr)
+            const float vr = sp * sp * a.inv_s0sq;
+            klp = 0.5f * (vr + mu * mu * a.inv_s0sq - 1.f - logf(vr));
+        }
+        mf_upd(a, pmu, gmu);
+        mf_upd(a, prho, grho);
+    }
+    if (a.elbo_out) {
+        float tot = block_sum(klp, red);
+        if (threadIdx.x == 0) {
+            if (blockIdx.x == 0) tot += a.acc[0];
+            atomicAdd(a.elbo_out, tot);
+        }
+    }
+}
+
+hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params, float* m,
+                            float* v, const psvi_adam_hp* hp, float* elbo_out,
+                            float* grad_out, int include_kl, hipStream_t st) {
+    MfUpdArgs a{};
+    a.L = p.L;
+    for (int l = 0; l < p.L; ++l) {
+        a.woff[l] = p.lay[l].woff;
+        a.poff[l] = p.lay[l].poff;
+        a.n[l] = p.lay[l].n;
+    }
+    a.woff[p.L] = p.n_tot;
+    a.acc = acc;
+    a.n_tot = p.n_tot;
+    a.params = params;
+    a.m = m;
+    a.v = v;
+    a.grad_out = grad_out;
+    a.elbo_out = elbo_out;
+    a.include_kl = include_kl;
+    const float s0 = p.d.prior_sd;
+    a.inv_s0sq = 1.f / (s0 * s0);
+    a.log_s0 = logf(s0);
+    if (hp) a.adam = make_adam(hp);
+    const int nb = (p.n_tot + 255) / 256;
+    hipLaunchKernelGGL(mf_update_kernel, dim3(nb), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ generic Adam
+__global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p,
+                                                   const float* __restrict__ g,
+                                                   float* __restrict__ m,
+                                                   float* __restrict__ v, AdamC a) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float mm = m[i], vv = v[i];
+        p[i] = adam_apply(a, p[i], g[i], mm, vv);
+        m[i] = mm;
+        v[i] = vv;
+    }
+}
+
+hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
+                       const psvi_adam_hp* hp, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t nb = std::min<int64_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nb), dim3(256), 0, st, n, p, g, m, v,
+                       make_adam(hp));
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------- Philox4x32-10 randn
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+    const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    c[0] = hi1 ^ c[1] ^ k0;
+    c[1] = lo1;
+    c[2] = hi0 ^ c[3] ^ k1;
+    c[3] = lo0;
+}
+
+__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        philox_round(c, k0, k1);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void randn_kernel(float* __restrict__ out, int64_t n,
+                                                    uint64_t seed, uint64_t offset) {
+    const int64_t nq = (n + 3) / 4;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t ctr = offset / 4 + (uint64_t)q;
+        uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u};
+        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        float r[4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            // u1 in (0, 1], u2 in [0, 1)
+            const float u1 = ((float)(c[2 * j] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+            const float u2 = (float)(c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
+            const float rad = sqrtf(-2.0f * logf(u1));
+            float sn, cs;
+            sincosf(6.283185307179586f * u2, &sn, &cs);
+            r[2 * j] = rad * cs;
+            r[2 * j + 1] = rad * sn;
+        }
+        const int64_t base = q * 4;
+        if (VEC && base + 3 < n) {
+            *reinterpret_cast<float4*>(out + base) = make_float4(r[0], r[1], r[2], r[3]);
+        } else {
+            for (int j = 0; j < 4 && base + j < n; ++j) out[base + j] = r[j];
+        }
+    }
+}
+
+hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t nb = std::min<int64_t>(((n + 3) / 4 + 255) / 256, 4096);
+    if (((uintptr_t)out & 15) == 0)
+        hipLaunchKernelGGL(randn_kernel<true>, dim3((unsigned)nb), dim3(256), 0, st, out, n, seed,
+                           offset);
+    else
+        hipLaunchKernelGGL(randn_kernel<false>, dim3((unsigned)nb), dim3(256), 0, st, out, n,
+                           seed, offset);
+    return hipGetLastError();
+}
+
+}  // namespace psvi

@@ -1,0 +1,148 @@
+// psvi_internal.hpp -- shared host/device definitions of libpsvi_hip.so.
+// Written for gfx950 (CDNA4, wave64) only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "psvi_hip.h"
+
+namespace psvi {
+
+constexpr int kMaxL = PSVI_MAX_LAYERS;
+constexpr int kMaxWorld = 8;      // ranks per node (xGMI)
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- numerics
+// torch.nn.functional.softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplus_f(float x) {
+    return x > 20.f ? x : log1pf(__expf(x));
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// Block-wide sum; `red` is >= blockDim/64 floats of LDS.  All threads call.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    float t = 0.f;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    return t;  // valid in thread 0
+}
+
+// Adam, both reference variants; returns new p, updates m, v in place.
+struct AdamC {
+    float lr, b1, b2, eps, omb1, omb2;
+    float inv_bc1, inv_sqrt_bc2;  // 1/(1-b1^t), 1/sqrt(1-b2^t)
+    float lr_bc1;                 // lr/(1-b1^t)
+    float inv_bc2;                // 1/(1-b2^t)
+    int kind;
+};
+
+__device__ __forceinline__ float adam_apply(const AdamC& a, float p, float g, float& m,
+                                            float& v) {
+    m = a.b1 * m + a.omb1 * g;
+    if (a.kind == PSVI_ADAM_HIGHER) {
+        // optim.py:339-367: v stored without the 1e-8; denom = sqrt(v+1e-8)/sqrt(bc2)+eps
+        v = a.b2 * v + a.omb2 * g * g;
+        const float denom = sqrtf(v + 1e-8f) * a.inv_sqrt_bc2 + a.eps;
+        return p - a.lr_bc1 * (m / denom);
+    } else {
+        // diff_optimizers.py:197-213: v += 1e-12 stored; denom = sqrt(v/bc2)+eps
+        v = a.b2 * v + a.omb2 * g * g + 1e-12f;
+        const float denom = sqrtf(v * a.inv_bc2) + a.eps;
+        return p - a.lr * ((m * a.inv_bc1) / denom);
+    }
+}
+
+// ------------------------------------------------------------- plan layout
+struct LayerInfo {
+    int din, dout;
+    int n;          // out*in + out (sampled elements per layer and sample)
+    int64_t nc;     // full-cov: packed corr count (n-1)(n-2)/2
+    int64_t poff;   // offset of the layer in the flat parameter vector
+    int64_t eoff;   // offset of the layer in the flat eps vector (all S)
+    int woff;       // offset of the layer in the per-sample weight space [0, n_tot)
+};
+
+// Full-cov forward work item: rows [r0, r0+32) of layer `layer` (global row
+// ids, clipped to the rank's row range), columns c in [k0, k1) of L.
+struct FwdItem {
+    int layer, r0, r1, k0, k1, xcol;  // xcol: x_shard column of row r0
+};
+// Full-cov backward tile: rows [r0, r0+64) x cols [c0, c0+64) of the strict
+// lower triangle of layer `layer`, rows clipped to [rlo, rhi).
+struct BwdTile {
+    int layer, r0, c0, rlo, rhi, xcol;  // xcol: g_shard column of row rlo
+};
+// Full-cov per-row (mean, sd) block: rows [r0, r0+256) of layer, clipped.
+struct DiagBlock {
+    int layer, r0, rhi, xcol;
+};
+
+struct NetArgs;  // kernels_net.hip
+
+}  // namespace psvi
+
+struct psvi_plan {
+    int family = 0;
+    psvi_net_desc d{};
+    int world = 1, rank = 0;
+    int L = 0;
+    psvi::LayerInfo lay[psvi::kMaxL];
+    int64_t P = 0;        // parameter count
+    int64_t Peps = 0;     // eps floats for all S
+    int n_tot = 0;        // per-sample weight-space size (sum n)
+    // sample shards
+    int s_off[psvi::kMaxWorld], s_cnt[psvi::kMaxWorld];
+    // full-cov row shards: rows [row_lo, row_hi) of each layer per rank
+    int row_lo[psvi::kMaxWorld][psvi::kMaxL], row_hi[psvi::kMaxWorld][psvi::kMaxL];
+    int rows_tot[psvi::kMaxWorld];
+    int xcol_l[psvi::kMaxWorld][psvi::kMaxL];  // column of layer l's first row in a shard
+    // work lists (host copies, then device)
+    std::vector<psvi::FwdItem> h_fwd;
+    std::vector<psvi::BwdTile> h_bwd;
+    std::vector<psvi::DiagBlock> h_diag;
+    bool on_device = false;
+    psvi::FwdItem* d_fwd = nullptr;
+    int n_fwd = 0;
+    psvi::BwdTile* d_bwd = nullptr;
+    int n_bwd = 0;
+    psvi::DiagBlock* d_diag = nullptr;
+    int n_diag = 0;
+    // net kernel geometry
+    int mchunks = 1, mc = 0;
+    size_t net_lds = 0;
+    size_t ws_bytes = 0;
+    int64_t acc_count = 0;
+};
+
+namespace psvi {
+// launchers (defined in the .hip translation units)
+hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
+                      const float* params, const float* eps, float* accMu, float* accRho,
+                      const float* xrecv, float* gsend, float* nll_out, hipStream_t st);
+hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
+                            float* m, float* v, const psvi_adam_hp* hp, float* elbo_out,
+                            float* grad_out, int include_kl, hipStream_t st);
+hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
+                          float* x_shard, hipStream_t st);
+hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
+                             float* params, float* m, float* v, const psvi_adam_hp* hp,
+                             float* kl_out, float* grad_out, int include_kl, hipStream_t st);
+hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
+hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
+                       const psvi_adam_hp* hp, hipStream_t st);
+AdamC make_adam(const psvi_adam_hp* hp);
+}  // namespace psvi

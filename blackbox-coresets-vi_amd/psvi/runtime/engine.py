@@ -1,0 +1,210 @@
+"""Host wrapper around one libpsvi_hip plan.
+
+``InnerLoopPlan`` owns a ``psvi_plan`` (geometry + device work lists) and
+launches the fused HIP inner step, the autograd-boundary ELBO/gradient, or the
+sharded phases on torch's current HIP stream.  All tensors are caller-owned
+torch tensors on the GPU; this module only checks shapes and passes pointers.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import AdamHP, NetDesc, check
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need(t, name, numel, dtype=torch.float32):
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device})")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} has {t.numel()} elements, expected {numel}")
+
+
+def make_adam(lr, step, kind="higher", betas=(0.9, 0.999), eps=1e-8):
+    k = {"higher": _lib.ADAM_HIGHER, "hypergrad": _lib.ADAM_HYPERGRAD}[kind]
+    return AdamHP(float(lr), float(betas[0]), float(betas[1]), float(eps), int(step), k)
+
+
+class InnerLoopPlan:
+    """family: 'meanfield' (VILinear stack) or 'fullcov' (VILinearMultivariateNormal
+    stack); layers: [(in, out), ...]; S: global MC samples; M: pseudopoints."""
+
+    def __init__(self, family, layers, S, M, prior_sd=1.0, world=1, rank=0):
+        self.lib = _lib.load()
+        self.family = family
+        fam = {"meanfield": _lib.FAMILY_MEANFIELD, "fullcov": _lib.FAMILY_FULLCOV}[family]
+        layers = [tuple(int(x) for x in l) for l in layers]
+        for a, b in zip(layers[:-1], layers[1:]):
+            if a[1] != b[0]:
+                raise ValueError(f"layer sizes do not chain: {layers}")
+        if not 1 <= len(layers) <= _lib.MAX_LAYERS:
+            raise ValueError("1..8 layers supported")
+        self.layers = layers
+        self.S, self.M, self.world, self.rank = int(S), int(M), int(world), int(rank)
+        d = NetDesc()
+        d.n_layers = len(layers)
+        dims = [layers[0][0]] + [o for _, o in layers]
+        for i, v in enumerate(dims):
+            d.dims[i] = v
+        d.S, d.M, d.prior_sd = self.S, self.M, float(prior_sd)
+        self.desc = d
+        h = ctypes.c_void_p()
+        check(self.lib.psvi_plan_create(fam, ctypes.byref(d), self.world, self.rank,
+                                        ctypes.byref(h)), "psvi_plan_create")
+        self.handle = h
+        q = self._query
+        self.param_count = q(_lib.Q_PARAM_COUNT)
+        self.eps_count = q(_lib.Q_EPS_COUNT)
+        self.ws_bytes = q(_lib.Q_WS_BYTES)
+        self.s_local = q(_lib.Q_S_LOCAL)
+        self.s_offset = q(_lib.Q_S_OFFSET)
+        self.acc_count = q(_lib.Q_ACC_COUNT)
+        self.rows_local = q(_lib.Q_ROWS_LOCAL)
+        self.xshard_count = q(_lib.Q_XSHARD_COUNT)
+        self.xrecv_count = q(_lib.Q_XRECV_COUNT)
+        self.n_tot = sum(i * o + o for i, o in layers)
+
+    def _query(self, key):
+        v = ctypes.c_int64()
+        check(self.lib.psvi_plan_query(self.handle, key, ctypes.byref(v)), "psvi_plan_query")
+        return v.value
+
+    def shard_info(self, r):
+        out = (ctypes.c_int64 * (3 + 2 * _lib.MAX_LAYERS))()
+        check(self.lib.psvi_plan_shard_info(self.handle, r, out), "psvi_plan_shard_info")
+        L = len(self.layers)
+        return dict(s_offset=out[0], s_count=out[1], rows=out[2],
+                    row_lo=[out[3 + l] for l in range(L)],
+                    row_cnt=[out[3 + _lib.MAX_LAYERS + l] for l in range(L)])
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.psvi_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    # ----------------------------------------------------------- buffers
+    def workspace(self, device="cuda"):
+        return torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
+
+    def _inputs(self, u, z, w, eps):
+        _need(u, "u", self.M * self.layers[0][0])
+        _need(z, "z", self.M, torch.int32)
+        _need(w, "w", self.M)
+        _need(eps, "eps", self.eps_count)
+
+    # --------------------------------------------------------- world == 1
+    def inner_step(self, u, z, w, eps, params, adam_m, adam_v, step, lr, kind="higher",
+                   elbo_out=None, ws=None):
+        """One fused inner step (psvi_inner_step); params/m/v updated in place.
+        Returns the (device) negative ELBO at the incoming params."""
+        self._inputs(u, z, w, eps)
+        for t, n in ((params, "params"), (adam_m, "adam_m"), (adam_v, "adam_v")):
+            _need(t, n, self.param_count)
+        if elbo_out is None:
+            elbo_out = torch.empty(1, dtype=torch.float32, device=params.device)
+        if ws is None:
+            ws = self.workspace(params.device)
+        hp = make_adam(lr, step, kind)
+        check(self.lib.psvi_inner_step(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps),
+                                       _ptr(params), _ptr(adam_m), _ptr(adam_v),
+                                       ctypes.byref(hp), _ptr(elbo_out), _ptr(ws),
+                                       ws.numel(), _stream()), "psvi_inner_step")
+        return elbo_out
+
+    def elbo_grad(self, u, z, w, eps, params, include_kl=True, ws=None):
+        self._inputs(u, z, w, eps)
+        _need(params, "params", self.param_count)
+        elbo = torch.empty(1, dtype=torch.float32, device=params.device)
+        grad = torch.empty(self.param_count, dtype=torch.float32, device=params.device)
+        if ws is None:
+            ws = self.workspace(params.device)
+        check(self.lib.psvi_elbo_grad(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps),
+                                      _ptr(params), int(bool(include_kl)), _ptr(elbo),
+                                      _ptr(grad), _ptr(ws), ws.numel(), _stream()),
+              "psvi_elbo_grad")
+        return elbo, grad
+
+    # ------------------------------------------------------------ phases
+    def mf_accumulate(self, u, z, w, eps, params, acc):
+        self._inputs(u, z, w, eps)
+        _need(params, "params", self.param_count)
+        _need(acc, "acc", self.acc_count)
+        check(self.lib.psvi_mf_phase_accumulate(self.handle, _ptr(u), _ptr(z), _ptr(w),
+                                                _ptr(eps), _ptr(params), _ptr(acc), _stream()),
+              "psvi_mf_phase_accumulate")
+
+    def mf_update(self, acc, params, adam_m=None, adam_v=None, step=1, lr=1e-3,
+                  kind="higher", elbo_out=None, grad_out=None):
+        _need(acc, "acc", self.acc_count)
+        _need(params, "params", self.param_count)
+        hp = make_adam(lr, step, kind)
+        check(self.lib.psvi_mf_phase_update(self.handle, _ptr(acc), _ptr(params), _ptr(adam_m),
+                                            _ptr(adam_v), ctypes.byref(hp), _ptr(elbo_out),
+                                            _ptr(grad_out), _stream()), "psvi_mf_phase_update")
+
+    def mvn_sample(self, eps, params, x_shard):
+        _need(eps, "eps", self.eps_count)
+        _need(params, "params", self.param_count)
+        _need(x_shard, "x_shard", self.xshard_count)
+        check(self.lib.psvi_mvn_phase_sample(self.handle, _ptr(eps), _ptr(params),
+                                             _ptr(x_shard), _stream()), "psvi_mvn_phase_sample")
+
+    def mvn_net(self, u, z, w, x_recv, g_send, nll_out):
+        _need(u, "u", self.M * self.layers[0][0])
+        _need(z, "z", self.M, torch.int32)
+        _need(w, "w", self.M)
+        _need(x_recv, "x_recv", self.xrecv_count)
+        _need(g_send, "g_send", self.xrecv_count)
+        _need(nll_out, "nll_out", 1)
+        check(self.lib.psvi_mvn_phase_net(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv),
+                                          _ptr(g_send), _ptr(nll_out), _stream()),
+              "psvi_mvn_phase_net")
+
+    def mvn_update(self, eps, g_shard, params, adam_m=None, adam_v=None, step=1, lr=1e-3,
+                   kind="higher", kl_out=None, grad_out=None, include_kl=True):
+        _need(eps, "eps", self.eps_count)
+        _need(g_shard, "g_shard", self.xshard_count)
+        _need(params, "params", self.param_count)
+        hp = make_adam(lr, step, kind)
+        check(self.lib.psvi_mvn_phase_update(self.handle, _ptr(eps), _ptr(g_shard),
+                                             _ptr(params), _ptr(adam_m), _ptr(adam_v),
+                                             ctypes.byref(hp), _ptr(kl_out), _ptr(grad_out),
+                                             int(bool(include_kl)), _stream()),
+              "psvi_mvn_phase_update")
+
+
+def randn_(out, seed, offset=0):
+    """Fill a float32 device tensor with N(0,1) (Philox4x32-10 + Box-Muller)."""
+    _need(out, "out", None)
+    lib = _lib.load()
+    check(lib.psvi_randn(_ptr(out), out.numel(), int(seed) & (2**64 - 1),
+                         int(offset), _stream()), "psvi_randn")
+    return out
+
+
+def adam_update_(params, grad, adam_m, adam_v, step, lr, kind="higher"):
+    n = params.numel()
+    for t, nm in ((params, "params"), (grad, "grad"), (adam_m, "adam_m"), (adam_v, "adam_v")):
+        _need(t, nm, n)
+    hp = make_adam(lr, step, kind)
+    lib = _lib.load()
+    check(lib.psvi_adam_update(n, _ptr(params), _ptr(grad), _ptr(adam_m), _ptr(adam_v),
+                               ctypes.byref(hp), _stream()), "psvi_adam_update")

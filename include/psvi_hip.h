@@ -1,0 +1,174 @@
+/*
+ * psvi_hip.h -- C ABI of the MI355X (gfx950) coreset-ELBO inner-loop library
+ * (libpsvi_hip.so).  Plain C: no HIP, torch or C++ types, so ctypes / cgo /
+ * JNI / N-API can bind it directly (binding stubs: INTEGRATION.md).
+ *
+ * What it replaces (reference = souravc83/Blackbox-Coresets-VI, paths relative
+ * to its repo root):
+ *   one inner step of PSVI.nested_step / PSVI.hyper_step, i.e.
+ *     PSVI.inner_elbo                     psvi/inference/psvi_classes.py:488-511
+ *       -> VILinear.forward / rsample      psvi/models/neural_net.py:155-179
+ *       -> VILinearMultivariateNormal      neural_net.py:408-491
+ *       -> Categorical.log_prob, .matmul(N f(v)), sum, + sum(m.kl())
+ *     DifferentiableOptimizer.step         psvi/robust_higher/optim.py:152-257
+ *       -> DifferentiableAdam._update      optim.py:299-367      (trainer nested)
+ *     hypergrad DifferentiableAdam.step    psvi/hypergrad/diff_optimizers.py:107-154
+ *       -> adam_step                       diff_optimizers.py:184-213 (trainer hyper)
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer (fp32 unless stated) owned by
+ *     the caller; the library never allocates device memory inside a step
+ *     (only psvi_plan_create allocates its small immutable work lists).
+ *   - Steps are stream-ordered and asynchronous on `stream` (a hipStream_t
+ *     passed as void*; NULL = default stream); no host synchronisation inside.
+ *   - Return 0 on success, <0 for an invalid argument / shape (PSVI_E*),
+ *     >0 for a hipError_t.  psvi_last_error() gives a thread-local message.
+ *   - Parameter vectors use the reference's parameters_to_vector order:
+ *       mean-field layer (in,out): [mu_W (out*in), mu_b (out), rho_W (out*in), rho_b (out)]
+ *       full-cov   layer (in,out): n = out*in + out;
+ *                                  [mean (n), sd (n), corr ((n-1)(n-2)/2)]
+ *     corr is the packed row-major strict lower triangle of the top-left
+ *     (n-1)x(n-1) block of L (neural_net.py:452-461): row r starts at r(r-1)/2.
+ *   - Noise `eps` uses the reference draw order (Normal/MultivariateNormal
+ *     rsample in forward order): mean-field per layer eps_W (S,out,in) then
+ *     eps_b (S,out); full-cov per layer eps (S, n).  S is the GLOBAL sample
+ *     count of the plan; every rank passes the full eps.
+ *   - z holds int32 class ids; w holds the coreset weights N*f(v) (M floats,
+ *     psvi_classes.py:505).
+ */
+#ifndef PSVI_HIP_H
+#define PSVI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSVI_MAX_LAYERS 8
+
+/* error codes (<0) */
+#define PSVI_EINVAL   (-1)   /* bad descriptor / shape / pointer            */
+#define PSVI_ENOSPC   (-2)   /* workspace too small                         */
+#define PSVI_EUNSUP   (-3)   /* configuration not supported by the kernels  */
+#define PSVI_ESTATE   (-4)   /* call not valid for this plan (family/world) */
+
+/* model families */
+#define PSVI_FAMILY_MEANFIELD 0   /* VILinear stack: logistic_regression, fn   */
+#define PSVI_FAMILY_FULLCOV   1   /* VILinearMultivariateNormal stack: fn2,
+                                     logistic_regression_fullcov              */
+
+/* Adam variants */
+#define PSVI_ADAM_HIGHER    0   /* robust_higher DifferentiableAdam (optim.py:318-367):
+                                   denom = sqrt(v + 1e-8)/sqrt(bc2) + eps            */
+#define PSVI_ADAM_HYPERGRAD 1   /* hypergrad adam_step (diff_optimizers.py:197-213):
+                                   v += 1e-12 stored; denom = sqrt(v/bc2) + eps      */
+
+typedef struct psvi_net_desc {
+    int32_t n_layers;                     /* affine VI layers                     */
+    int32_t dims[PSVI_MAX_LAYERS + 1];    /* dims[0] = D ... dims[n_layers] = C   */
+    int32_t S;                            /* GLOBAL Monte-Carlo samples           */
+    int32_t M;                            /* pseudopoints                         */
+    float   prior_sd;                     /* sigma_0 (neural_net.py:61, 409)      */
+} psvi_net_desc;
+
+typedef struct psvi_adam_hp {
+    float   lr;
+    float   beta1;
+    float   beta2;
+    float   eps;
+    int32_t step;      /* 1-based Adam step t (bias corrections 1 - beta^t) */
+    int32_t kind;      /* PSVI_ADAM_HIGHER | PSVI_ADAM_HYPERGRAD            */
+} psvi_adam_hp;
+
+typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
+
+/* psvi_plan_query keys */
+#define PSVI_Q_PARAM_COUNT   1  /* floats in params / adam_m / adam_v / grad          */
+#define PSVI_Q_EPS_COUNT     2  /* floats of eps for all S (reference draw order)     */
+#define PSVI_Q_WS_BYTES      3  /* workspace bytes for psvi_inner_step/elbo_grad      */
+#define PSVI_Q_S_LOCAL       4  /* samples owned by this rank                         */
+#define PSVI_Q_S_OFFSET      5  /* first global sample owned by this rank             */
+#define PSVI_Q_ACC_COUNT     6  /* mean-field: floats in the all-reduced accumulator  */
+#define PSVI_Q_ROWS_LOCAL    7  /* full-cov: x/g columns owned (sum over layers)      */
+#define PSVI_Q_XSHARD_COUNT  8  /* full-cov: floats of x_shard / g_shard = S*ROWS_LOCAL */
+#define PSVI_Q_XRECV_COUNT   9  /* full-cov: floats of x_recv / g_send = S_LOCAL*n_tot */
+
+/* Create a plan for `family` over `world` ranks, this process being `rank`.
+ * Samples are split in contiguous blocks; for FULLCOV the rows of every
+ * layer's L are split in nnz-balanced contiguous ranges (ranks own the
+ * matching mean/sd/corr slices and their Adam state). */
+int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world,
+                     int32_t rank, psvi_plan** out);
+int psvi_plan_destroy(psvi_plan* plan);
+int psvi_plan_query(const psvi_plan* plan, int32_t key, int64_t* value);
+/* rows (full-cov) and samples owned by rank `r` of the plan's world:
+ * out[0] = s_offset, out[1] = s_count, out[2] = rows_total,
+ * out[3 + l] = first row of layer l, out[3 + PSVI_MAX_LAYERS + l] = row count. */
+int psvi_plan_shard_info(const psvi_plan* plan, int32_t r, int64_t* out);
+
+/* ---- single-process fused step (world == 1) --------------------------------
+ * One inner step = reparameterise, batched forward over (S x M), weighted NLL
+ * + KL, hand-derived backward, Adam update of params/adam_m/adam_v in place.
+ * elbo_out[0] <- negative inner ELBO (the value inner_elbo returns) evaluated
+ * at the incoming params.  eps == NULL is invalid (use psvi_randn first). */
+int psvi_inner_step(const psvi_plan* plan, const float* u, const int32_t* z,
+                    const float* w, const float* eps, float* params,
+                    float* adam_m, float* adam_v, const psvi_adam_hp* hp,
+                    float* elbo_out, void* ws, size_t ws_bytes, void* stream);
+
+/* Same objective without the update: grad_out (PARAM_COUNT floats) <- d elbo
+ * / d params, elbo_out[0] <- elbo.  Used by the autograd.Function boundary.
+ * include_kl = 0 drops the KL term (and its gradient). */
+int psvi_elbo_grad(const psvi_plan* plan, const float* u, const int32_t* z,
+                   const float* w, const float* eps, const float* params,
+                   int32_t include_kl, float* elbo_out, float* grad_out,
+                   void* ws, size_t ws_bytes, void* stream);
+
+/* ---- sharded phases (any world; the caller runs the collectives) ------------
+ * MEANFIELD (sample-parallel, replicated params):
+ *   acc (ACC_COUNT floats) <- [sum_m,s w NLL | sum_s dW | sum_s dW*eps] over
+ *   this rank's samples;  caller all-reduces acc (sum);  update applies KL +
+ *   Adam identically on every rank; elbo_out[0] <- full elbo. */
+int psvi_mf_phase_accumulate(const psvi_plan* plan, const float* u,
+                             const int32_t* z, const float* w, const float* eps,
+                             const float* params, float* acc, void* stream);
+int psvi_mf_phase_update(const psvi_plan* plan, const float* acc, float* params,
+                         float* adam_m, float* adam_v, const psvi_adam_hp* hp,
+                         float* elbo_out, float* grad_out, void* stream);
+
+/* FULLCOV (rows of L sharded, samples sharded):
+ *   sample: x_shard[S][ROWS_LOCAL] <- mean + L eps for this rank's rows, all S
+ *   (all_to_all: rank r sends rows s in shard q to q -> x_recv)
+ *   net:    x_recv[S_LOCAL][n_tot, blocked by source rank] -> g_send (same
+ *           layout) = per-sample gradients; nll_out[0] += local weighted NLL
+ *   (all_to_all back -> g_shard[S][ROWS_LOCAL])
+ *   update: corr/mean/sd Adam for owned rows; kl_out[0] += owned KL part.
+ *           grad_out != NULL writes the gradient instead of updating. */
+int psvi_mvn_phase_sample(const psvi_plan* plan, const float* eps,
+                          const float* params, float* x_shard, void* stream);
+int psvi_mvn_phase_net(const psvi_plan* plan, const float* u, const int32_t* z,
+                       const float* w, const float* x_recv, float* g_send,
+                       float* nll_out, void* stream);
+int psvi_mvn_phase_update(const psvi_plan* plan, const float* eps,
+                          const float* g_shard, float* params, float* adam_m,
+                          float* adam_v, const psvi_adam_hp* hp, float* kl_out,
+                          float* grad_out, int32_t include_kl, void* stream);
+
+/* ---- utilities ----------------------------------------------------------- */
+/* out[i] ~ N(0,1), Philox4x32-10 counter (seed, offset + i) + Box-Muller.
+ * Throughput-mode replacement for torch's normal_() draw (not bit-identical
+ * to torch's generator; parity mode passes torch-drawn eps instead). */
+int psvi_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, void* stream);
+/* Generic fused Adam over n floats (either variant). */
+int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m,
+                     float* adam_v, const psvi_adam_hp* hp, void* stream);
+
+const char* psvi_last_error(void);
+const char* psvi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSVI_HIP_H */

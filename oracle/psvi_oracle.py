@@ -1,0 +1,273 @@
+"""CPU oracle for the coreset-ELBO inner step -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker.  The product path (the HIP library behind
+blackbox-coresets-vi_amd/psvi) never calls into oracle/.
+
+Float64 numpy restatement of the reference hot path, hand-derived backward
+included.  Parity pinned by tests/golden/*.npz, generated from the reference
+itself by tools/gen_golden.py (see tests/test_oracle_golden.py).
+
+Reference anchors (paths relative to /root/reference):
+  inner objective      psvi/inference/psvi_classes.py:488-511 (sum over S, w = N f(v))
+  f(v)                 psvi_classes.py:1358-1360 (softmax), 1486-1488 (exp(a) softmax)
+  mean-field layer     psvi/models/neural_net.py:60-179 (rsample 155-170, kl 101-108)
+  full-cov layer       neural_net.py:408-491 (scale_tril 452-461, rsample 467-476, kl 435-436)
+  higher Adam          psvi/robust_higher/optim.py:299-367
+  hypergrad adam_step  psvi/hypergrad/diff_optimizers.py:184-213
+
+Flat layouts (identical to torch.nn.utils.parameters_to_vector on the reference
+modules, i.e. module registration order):
+  mean-field layer (in, out): [mu_W (out*in), mu_b (out), rho_W (out*in), rho_b (out)]
+  full-cov layer   (in, out): n = out*in + out; [mean (n), sd (n), corr ((n-1)(n-2)/2)]
+Noise, per layer in forward order: mean-field eps_W (S,out,in) then eps_b (S,out);
+full-cov eps (S, n).
+"""
+import numpy as np
+
+
+# ---------------------------------------------------------------- helpers
+def softplus(x):
+    """torch.nn.functional.softplus(beta=1, threshold=20)."""
+    x = np.asarray(x, dtype=np.float64)
+    return np.where(x > 20.0, x, np.log1p(np.exp(np.minimum(x, 20.0))))
+
+
+def sigmoid(x):
+    x = np.asarray(x, dtype=np.float64)
+    return 0.5 * (1.0 + np.tanh(0.5 * x))
+
+
+def coreset_weights(v, N, f="softmax", alpha=None):
+    """w = N * f(v): PSVI identity (psvi_classes.py:111), PSVILearnV softmax
+    (1358-1360), PSVIAV exp(alpha)*softmax (1486-1488)."""
+    v = np.asarray(v, dtype=np.float64)
+    if f == "identity":
+        return N * v
+    e = np.exp(v - v.max())
+    sm = e / e.sum()
+    if f == "softmax":
+        return N * sm
+    if f == "exp_alpha_softmax":
+        return N * np.exp(alpha) * sm
+    raise ValueError(f)
+
+
+def mf_sizes(layers):
+    out = []
+    for din, dout in layers:
+        out.append(dict(nw=din * dout, nb=dout))
+    return out
+
+
+def mf_param_count(layers):
+    return sum(2 * (i * o + o) for i, o in layers)
+
+
+def mf_eps_count(layers, S):
+    return sum(S * (i * o + o) for i, o in layers)
+
+
+def mvn_n(din, dout):
+    return din * dout + dout
+
+
+def mvn_ncorr(n):
+    return (n - 1) * (n - 2) // 2
+
+
+def mvn_param_count(layers):
+    return sum(2 * mvn_n(i, o) + mvn_ncorr(mvn_n(i, o)) for i, o in layers)
+
+
+def mvn_eps_count(layers, S):
+    return sum(S * mvn_n(i, o) for i, o in layers)
+
+
+def tril_rows_cols(n):
+    """Row-major strict-lower indices of the (n-1)x(n-1) block
+    (torch.tril_indices(n-1, n-1, -1), neural_net.py:458-460)."""
+    r, c = np.tril_indices(n - 1, -1)
+    return r, c
+
+
+# ------------------------------------------------------------ per-sample net
+def net_forward_backward(u, z, w, Ws, bs):
+    """Batched-over-S MLP forward + weighted NLL + hand-derived backward.
+
+    u (M, D); z (M,) int; w (M,); Ws[l] (S, out, in); bs[l] (S, out).
+    Returns (data_term, dWs, dbs) with data_term = sum_s sum_m w_m NLL_sm
+    (psvi_classes.py:495-505,511) and dWs[l] = d data / d W_s (S, out, in).
+    """
+    S = Ws[0].shape[0]
+    M = u.shape[0]
+    L = len(Ws)
+    hs = [np.broadcast_to(u[None], (S,) + u.shape)]
+    acts = []
+    for l in range(L):
+        a = np.einsum("smi,soi->smo", hs[-1], Ws[l]) + bs[l][:, None, :]
+        acts.append(a)
+        hs.append(np.maximum(a, 0.0) if l < L - 1 else a)
+    logits = hs[-1]
+    mx = logits.max(-1, keepdims=True)
+    lse = (mx + np.log(np.exp(logits - mx).sum(-1, keepdims=True)))[..., 0]
+    zi = z.astype(np.int64)
+    picked = logits[:, np.arange(M), zi]
+    nll = lse - picked
+    data = float((nll * w[None]).sum())
+    p = np.exp(logits - lse[..., None])
+    p[:, np.arange(M), zi] -= 1.0
+    g = p * w[None, :, None]
+    dWs = [None] * L
+    dbs = [None] * L
+    for l in range(L - 1, -1, -1):
+        dWs[l] = np.einsum("smo,smi->soi", g, hs[l])
+        dbs[l] = g.sum(1)
+        if l > 0:
+            g = np.einsum("smo,soi->smi", g, Ws[l]) * (acts[l - 1] > 0)
+    return data, dWs, dbs
+
+
+# --------------------------------------------------------------- Adam steps
+def adam_higher(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """robust_higher DifferentiableAdam._update (optim.py:318-367), t 1-based."""
+    m = beta1 * m + (1.0 - beta1) * g
+    v = beta2 * v + (1.0 - beta2) * g * g
+    bc1 = 1.0 - beta1 ** t
+    bc2 = 1.0 - beta2 ** t
+    denom = np.sqrt(v + 1e-8) / np.sqrt(bc2) + eps
+    p = p - (lr / bc1) * m / denom
+    return p, m, v
+
+
+def adam_hypergrad(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """hypergrad adam_step (diff_optimizers.py:184-213): v stores +1e-12."""
+    m = beta1 * m + (1.0 - beta1) * g
+    v = beta2 * v + (1.0 - beta2) * g * g + 1e-12
+    p = p - lr * (m / (1.0 - beta1 ** t)) / (np.sqrt(v / (1.0 - beta2 ** t)) + eps)
+    return p, m, v
+
+
+def adam(kind, *a, **k):
+    return (adam_higher if kind == "higher" else adam_hypergrad)(*a, **k)
+
+
+# ------------------------------------------------------------ mean-field MLP
+def mf_elbo_grad(layers, params, u, z, w, eps, S, prior_sd=1.0):
+    """Negative inner ELBO and its gradient for a VILinear stack
+    (make_fcnet / logistic_regression)."""
+    params = np.asarray(params, dtype=np.float64)
+    eps = np.asarray(eps, dtype=np.float64)
+    Ws, bs, sW, sb, eW, eb, views = [], [], [], [], [], [], []
+    po = 0
+    eo = 0
+    kl = 0.0
+    s0 = float(prior_sd)
+    for din, dout in layers:
+        nw, nb = din * dout, dout
+        muW = params[po:po + nw].reshape(dout, din)
+        mub = params[po + nw:po + nw + nb]
+        rW = params[po + nw + nb:po + 2 * nw + nb].reshape(dout, din)
+        rb = params[po + 2 * nw + nb:po + 2 * nw + 2 * nb]
+        views.append((po, nw, nb, muW, mub, rW, rb))
+        po += 2 * (nw + nb)
+        e_w = eps[eo:eo + S * nw].reshape(S, dout, din)
+        eo += S * nw
+        e_b = eps[eo:eo + S * nb].reshape(S, dout)
+        eo += S * nb
+        sdW, sdb = softplus(rW), softplus(rb)
+        Ws.append(muW[None] + sdW[None] * e_w)
+        bs.append(mub[None] + sdb[None] * e_b)
+        eW.append(e_w)
+        eb.append(e_b)
+        sW.append(sdW)
+        sb.append(sdb)
+        for mu, sd in ((muW, sdW), (mub, sdb)):
+            vr = (sd / s0) ** 2
+            kl += float((0.5 * (vr + (mu / s0) ** 2 - 1.0 - np.log(vr))).sum())
+    data, dWs, dbs = net_forward_backward(np.asarray(u, np.float64), np.asarray(z),
+                                          np.asarray(w, np.float64), Ws, bs)
+    grad = np.zeros_like(params)
+    for l, (po, nw, nb, muW, mub, rW, rb) in enumerate(views):
+        gW = dWs[l].sum(0) + muW / s0 ** 2
+        gb = dbs[l].sum(0) + mub / s0 ** 2
+        grW = ((dWs[l] * eW[l]).sum(0) + sW[l] / s0 ** 2 - 1.0 / sW[l]) * sigmoid(rW)
+        grb = ((dbs[l] * eb[l]).sum(0) + sb[l] / s0 ** 2 - 1.0 / sb[l]) * sigmoid(rb)
+        grad[po:po + nw] = gW.reshape(-1)
+        grad[po + nw:po + nw + nb] = gb
+        grad[po + nw + nb:po + 2 * nw + nb] = grW.reshape(-1)
+        grad[po + 2 * nw + nb:po + 2 * (nw + nb)] = grb
+    return data + kl, grad
+
+
+# ------------------------------------------------------------- full-cov MLP
+def mvn_dense_L(sd, corr, n):
+    L = np.zeros((n, n))
+    L[np.arange(n), np.arange(n)] = softplus(sd)
+    r, c = tril_rows_cols(n)
+    L[r, c] = corr
+    return L
+
+
+def mvn_elbo_grad(layers, params, u, z, w, eps, S, prior_sd=1.0):
+    """Negative inner ELBO and gradient for a VILinearMultivariateNormal stack
+    (make_fc2net / logistic_regression_fullcov)."""
+    params = np.asarray(params, dtype=np.float64)
+    eps = np.asarray(eps, dtype=np.float64)
+    s0 = float(prior_sd)
+    Ws, bs, Es, views = [], [], [], []
+    po = eo = 0
+    kl = 0.0
+    for din, dout in layers:
+        n = mvn_n(din, dout)
+        nc = mvn_ncorr(n)
+        mean = params[po:po + n]
+        sd = params[po + n:po + 2 * n]
+        corr = params[po + 2 * n:po + 2 * n + nc]
+        views.append((po, n, nc, mean, sd, corr))
+        po += 2 * n + nc
+        E = eps[eo:eo + S * n].reshape(S, n)
+        eo += S * n
+        L = mvn_dense_L(sd, corr, n)
+        X = mean[None] + E @ L.T
+        Ws.append(X[:, :din * dout].reshape(S, dout, din))
+        bs.append(X[:, din * dout:])
+        Es.append(E)
+        spd = softplus(sd)
+        kl += (n * np.log(s0) - np.log(spd).sum()
+               + 0.5 * ((spd ** 2).sum() / s0 ** 2 + (corr ** 2).sum() / s0 ** 2
+                        + (mean ** 2).sum() / s0 ** 2 - n))
+    data, dWs, dbs = net_forward_backward(np.asarray(u, np.float64), np.asarray(z),
+                                          np.asarray(w, np.float64), Ws, bs)
+    grad = np.zeros_like(params)
+    for l, (po, n, nc, mean, sd, corr) in enumerate(views):
+        G = np.concatenate([dWs[l].reshape(S, -1), dbs[l]], axis=1)  # (S, n)
+        E = Es[l]
+        spd = softplus(sd)
+        grad[po:po + n] = G.sum(0) + mean / s0 ** 2
+        dsd = (G * E).sum(0)
+        grad[po + n:po + 2 * n] = (dsd + spd / s0 ** 2 - 1.0 / spd) * sigmoid(sd)
+        r, c = tril_rows_cols(n)
+        dL = G.T @ E
+        grad[po + 2 * n:po + 2 * n + nc] = dL[r, c] + corr / s0 ** 2
+    return data + kl, grad
+
+
+# --------------------------------------------------------------- trajectory
+def run_inner_loop(family, layers, params0, u, z, w, eps_steps, S, lr, adam_kind,
+                   prior_sd=1.0, t0=1):
+    """T inner steps (one per eps_steps row): returns (elbos, grads, params, m, v).
+    nested trainer: fresh higher-Adam state at t=1 (psvi_classes.py:549-555);
+    hyper trainer: hypergrad step_cnt from 1 (psvi_classes.py:622-647)."""
+    f = mf_elbo_grad if family == "mf" else mvn_elbo_grad
+    p = np.asarray(params0, dtype=np.float64).copy()
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    elbos, grads, traj = [], [], []
+    for k, e in enumerate(eps_steps):
+        val, g = f(layers, p, u, z, w, e, S, prior_sd)
+        elbos.append(val)
+        grads.append(g)
+        p, m, v = adam(adam_kind, p, g, m, v, t0 + k, lr)
+        traj.append(p.copy())
+    return np.array(elbos), grads, traj, m, v

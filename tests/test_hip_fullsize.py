@@ -1,0 +1,91 @@
+"""HIP vs oracle at BASELINE.json sizes (C2, C3, C4 on one GPU) and on ragged
+shapes (S, M not multiples of the kernels' tiles; single layer; M = 1, S = 1).
+Inputs are seeded synthetic draws of the configs' shapes; params are
+perturbed away from the reference init so every term is exercised."""
+import numpy as np
+import pytest
+import torch
+
+import psvi_oracle as O
+from golden_util import assert_grad_close, l2rel, rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def make_case(family, layers, S, M, seed, N=800):
+    rng = np.random.default_rng(seed)
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        if family == "meanfield":
+            parts += [0.3 * rng.standard_normal(n), rng.uniform(-4, -1, n)]
+        else:
+            parts += [0.1 * rng.standard_normal(n), rng.uniform(-5, -3, n),
+                      (0.15 / np.sqrt(n)) * rng.standard_normal((n - 1) * (n - 2) // 2)]
+    params = np.concatenate(parts).astype(np.float32)
+    u = rng.standard_normal((M, layers[0][0])).astype(np.float32)
+    C = layers[-1][1]
+    z = rng.integers(0, C, M).astype(np.int32)
+    w = O.coreset_weights(0.3 * rng.standard_normal(M), N).astype(np.float32)
+    neps = sum(S * (i * o + o) for i, o in layers)
+    eps = rng.standard_normal(neps).astype(np.float32)
+    return params, u, z, w, eps
+
+
+def check(family, layers, S, M, seed=0, l2tol=1e-4):
+    from psvi.runtime import InnerLoopPlan
+
+    params, u, z, w, eps = make_case(family, layers, S, M, seed)
+    plan = InnerLoopPlan(family, layers, S, M)
+    assert plan.param_count == params.size and plan.eps_count == eps.size
+    t = lambda x, d=torch.float32: torch.tensor(x, dtype=d, device=DEV)
+    elbo, grad = plan.elbo_grad(t(u), t(z, torch.int32), t(w), t(eps), t(params))
+    fn = O.mf_elbo_grad if family == "meanfield" else O.mvn_elbo_grad
+    val, g = fn(layers, params, u, z, w, eps, S)
+    assert np.isfinite(elbo.item())
+    assert rel(elbo.item(), val) < 1e-5, (elbo.item(), val)
+    assert_grad_close(grad.cpu().numpy(), g, l2tol=l2tol, what=f"{family}{layers} S={S} M={M}")
+    # one fused step == oracle Adam on the oracle gradient
+    p = t(params)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    plan.inner_step(t(u), t(z, torch.int32), t(w), t(eps), p, m, v, step=1, lr=1e-3)
+    p_o, _, _ = O.adam_higher(params.astype(np.float64), g, 0 * g, 0 * g, 1, 1e-3)
+    assert np.abs(p.cpu().numpy() - p_o).max() < 5e-4
+    assert l2rel(p.cpu().numpy(), p_o) < 1e-5
+
+
+def test_c2_fn_four_blobs_shape():
+    check("meanfield", [(2, 100), (100, 4)], S=32, M=50)
+
+
+def test_c1_logreg_shape():
+    check("meanfield", [(2, 2)], S=4, M=10)
+
+
+def test_c3_fn2_shape():
+    check("fullcov", [(64, 40), (40, 40), (40, 2)], S=128, M=100)
+
+
+def test_c4_fn2_shape_single_gpu():
+    check("fullcov", [(64, 40), (40, 40), (40, 2)], S=1024, M=200, seed=3)
+
+
+@pytest.mark.parametrize("S,M", [(1, 1), (33, 7), (130, 129), (5, 300)])
+def test_ragged_fullcov(S, M):
+    check("fullcov", [(9, 5), (5, 3)], S=S, M=M, seed=S + M)
+
+
+@pytest.mark.parametrize("S,M", [(1, 1), (33, 7), (130, 129), (3, 1000)])
+def test_ragged_meanfield(S, M):
+    check("meanfield", [(7, 33), (33, 5), (5, 3)], S=S, M=M, seed=S * M)
+
+
+def test_lenet_fc_head_shape():
+    # LeNet's fully connected stack (400 -> 120 -> 84 -> 10) with M = 500
+    check("meanfield", [(400, 120), (120, 84), (84, 10)], S=8, M=500, seed=7)
+
+
+def test_wide_fullcov_layer():
+    # a single wide full-cov layer (n = 1300): many forward split-K items per row tile
+    check("fullcov", [(64, 20)], S=64, M=40, seed=11)
