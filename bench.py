@@ -148,7 +148,7 @@ def main():
         xs = torch.empty(plan.xshard_count, **f32)
         gs = torch.empty(plan.xshard_count, **f32)
     total_steps = args.warmup + args.steps
-    parts = torch.zeros(total_steps, 2, **f32)
+    parts = torch.zeros(total_steps, 2, dtype=torch.float64, device=dev)
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
 
     def one_step(k, timed):

@@ -130,7 +130,7 @@ int build_plan(psvi_plan& p) {
             p.rows_tot[q] += hi[q] - lo[q];
         }
     }
-    p.acc_count = 4 + 2 * (int64_t)p.n_tot;
+    p.acc_count = 2 * (int64_t)p.n_tot;
     net_plan_geometry(p);
     if (p.net_lds > 160 * 1024)
         return fail(PSVI_EUNSUP, "layer too wide for the per-sample LDS network kernel");
@@ -147,11 +147,11 @@ int build_plan(psvi_plan& p) {
                 const int r1 = std::min(r0 + 32, hi);
                 const int kmax = std::max(0, std::min(r1 - 1, n - 2));
                 const int nit = std::max(1, (kmax + kFwdKChunk - 1) / kFwdKChunk);
-                // even split, multiples of 32 columns
-                const int steps = (kmax + 31) / 32;
+                // even split, multiples of 64 columns (the kernel's LDS stage)
+                const int steps = (kmax + 63) / 64;
                 for (int i = 0; i < nit; ++i) {
-                    const int k0 = std::min(kmax, 32 * (int)((int64_t)steps * i / nit));
-                    const int k1 = std::min(kmax, 32 * (int)((int64_t)steps * (i + 1) / nit));
+                    const int k0 = std::min(kmax, 64 * (int)((int64_t)steps * i / nit));
+                    const int k1 = std::min(kmax, 64 * (int)((int64_t)steps * (i + 1) / nit));
                     if (i > 0 && k0 >= k1) continue;
                     fwd.push_back(FwdItem{l, r0, r1, k0, k1, xc + (r0 - lo)});
                 }
@@ -162,7 +162,7 @@ int build_plan(psvi_plan& p) {
                 for (int c0 = 0; c0 < cmax; c0 += 64)
                     bwd.push_back(BwdTile{l, r0, c0, lo, thi, xc - lo});
             }
-            for (int r0 = lo; r0 < hi; r0 += 256)
+            for (int r0 = lo; r0 < hi; r0 += 64)
                 diag.push_back(DiagBlock{l, r0, hi, xc - lo});
         }
         // longest forward items first
@@ -279,15 +279,15 @@ static int check_step(const psvi_plan* p, const void* u, const void* z, const vo
 
 static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
                      const float* eps, float* params, float* m, float* v,
-                     const psvi_adam_hp* hp, float* elbo_out, float* grad_out,
+                     const psvi_adam_hp* hp, double* elbo_out, float* grad_out,
                      int include_kl, void* ws, hipStream_t st) {
-    HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(float), st));
+    HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double), st));
     char* wsb = (char*)ws;
     if (p->family == PSVI_FAMILY_MEANFIELD) {
         float* acc = (float*)wsb;
         HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
-        HIP_TRY(launch_net(*p, u, z, w, params, eps, acc + 4, acc + 4 + p->n_tot, nullptr,
-                           nullptr, acc, st));
+        HIP_TRY(launch_net(*p, u, z, w, params, eps, acc, acc + p->n_tot, nullptr, nullptr,
+                           elbo_out, st));
         HIP_TRY(launch_mf_update(*p, acc, params, m, v, hp, elbo_out, grad_out, include_kl, st));
     } else {
         const size_t xs = sizeof(float) * (size_t)p->d.S * p->rows_tot[0];
@@ -304,7 +304,7 @@ static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const
 
 int psvi_inner_step(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
                     const float* eps, float* params, float* adam_m, float* adam_v,
-                    const psvi_adam_hp* hp, float* elbo_out, void* ws, size_t ws_bytes,
+                    const psvi_adam_hp* hp, double* elbo_out, void* ws, size_t ws_bytes,
                     void* stream) {
     if (int rc = check_step(p, u, z, w, eps, ws_bytes, ws)) return rc;
     if (!params || !adam_m || !adam_v || !hp || !elbo_out)
@@ -315,7 +315,7 @@ int psvi_inner_step(const psvi_plan* p, const float* u, const int32_t* z, const 
 }
 
 int psvi_elbo_grad(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
-                   const float* eps, const float* params, int32_t include_kl, float* elbo_out,
+                   const float* eps, const float* params, int32_t include_kl, double* elbo_out,
                    float* grad_out, void* ws, size_t ws_bytes, void* stream) {
     if (int rc = check_step(p, u, z, w, eps, ws_bytes, ws)) return rc;
     if (!params || !elbo_out || !grad_out) return fail(PSVI_EINVAL, "null pointer");
@@ -325,28 +325,28 @@ int psvi_elbo_grad(const psvi_plan* p, const float* u, const int32_t* z, const f
 
 int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* z,
                              const float* w, const float* eps, const float* params, float* acc,
-                             void* stream) {
+                             double* nll_out, void* stream) {
     if (!p || p->family != PSVI_FAMILY_MEANFIELD) return fail(PSVI_ESTATE, "not a mean-field plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
-    if (!u || !z || !w || !eps || !params || !acc) return fail(PSVI_EINVAL, "null pointer");
+    if (!u || !z || !w || !eps || !params || !acc || !nll_out)
+        return fail(PSVI_EINVAL, "null pointer");
     hipStream_t st = as_stream(stream);
     HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
-    HIP_TRY(launch_net(*p, u, z, w, params, eps, acc + 4, acc + 4 + p->n_tot, nullptr, nullptr,
-                       acc, st));
+    HIP_TRY(launch_net(*p, u, z, w, params, eps, acc, acc + p->n_tot, nullptr, nullptr, nll_out,
+                       st));
     return 0;
 }
 
 int psvi_mf_phase_update(const psvi_plan* p, const float* acc, float* params, float* adam_m,
-                         float* adam_v, const psvi_adam_hp* hp, float* elbo_out,
-                         float* grad_out, void* stream) {
+                         float* adam_v, const psvi_adam_hp* hp, double* kl_out,
+                         float* grad_out, int32_t include_kl, void* stream) {
     if (!p || p->family != PSVI_FAMILY_MEANFIELD) return fail(PSVI_ESTATE, "not a mean-field plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!acc || !params) return fail(PSVI_EINVAL, "null pointer");
     if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
     if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
-    hipStream_t st = as_stream(stream);
-    if (elbo_out) HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(float), st));
-    HIP_TRY(launch_mf_update(*p, acc, params, adam_m, adam_v, hp, elbo_out, grad_out, 1, st));
+    HIP_TRY(launch_mf_update(*p, acc, params, adam_m, adam_v, hp, kl_out, grad_out,
+                             include_kl ? 1 : 0, as_stream(stream)));
     return 0;
 }
 
@@ -360,7 +360,7 @@ int psvi_mvn_phase_sample(const psvi_plan* p, const float* eps, const float* par
 }
 
 int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
-                       const float* x_recv, float* g_send, float* nll_out, void* stream) {
+                       const float* x_recv, float* g_send, double* nll_out, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!u || !z || !w || !x_recv || !g_send || !nll_out) return fail(PSVI_EINVAL, "null pointer");
@@ -375,7 +375,7 @@ int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, con
 
 int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_shard,
                           float* params, float* adam_m, float* adam_v, const psvi_adam_hp* hp,
-                          float* kl_out, float* grad_out, int32_t include_kl, void* stream) {
+                          double* kl_out, float* grad_out, int32_t include_kl, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!eps || !g_shard || !params) return fail(PSVI_EINVAL, "null pointer");

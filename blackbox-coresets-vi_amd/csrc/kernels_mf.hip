@@ -36,20 +36,21 @@ struct MfUpdArgs {
     int woff[kMaxL + 1];
     int64_t poff[kMaxL];
     int n[kMaxL];
-    const float* acc;   // [nll pad(4) | sum dW (n_tot) | sum dW*eps (n_tot)]
+    const float* acc;   // [sum_s dW (n_tot) | sum_s dW*eps (n_tot)]
     int n_tot;
     float* params;
     float* m;
     float* v;
     float* grad_out;
-    float* elbo_out;
+    double* kl_out;
     int include_kl;
     float inv_s0sq, log_s0;
     AdamC adam;
 };
 
+template <bool GRAD>
 __device__ __forceinline__ void mf_upd(const MfUpdArgs& a, int64_t pidx, float g) {
-    if (a.grad_out) {
+    if (GRAD) {
         a.grad_out[pidx] = g;
     } else {
         float mm = a.m[pidx], vv = a.v[pidx];
@@ -59,6 +60,7 @@ __device__ __forceinline__ void mf_upd(const MfUpdArgs& a, int64_t pidx, float g
     }
 }
 
+template <bool GRAD>
 __global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
     __shared__ float red[8];
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
         const int64_t pmu = a.poff[l] + idx, prho = pmu + a.n[l];
         const float mu = a.params[pmu], rho = a.params[prho];
         const float sp = softplus_f(rho), sg = sigmoid_f(rho);
-        const float* accMu = a.acc + 4;
+        const float* accMu = a.acc;
         const float* accRho = accMu + a.n_tot;
         float gmu = accMu[e], grho = accRho[e] * sg;
         if (a.include_kl) {
@@ -80,20 +82,17 @@ __global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
             const float vr = sp * sp * a.inv_s0sq;
             klp = 0.5f * (vr + mu * mu * a.inv_s0sq - 1.f - logf(vr));
         }
-        mf_upd(a, pmu, gmu);
-        mf_upd(a, prho, grho);
+        mf_upd<GRAD>(a, pmu, gmu);
+        mf_upd<GRAD>(a, prho, grho);
     }
-    if (a.elbo_out) {
-        float tot = block_sum(klp, red);
-        if (threadIdx.x == 0) {
-            if (blockIdx.x == 0) tot += a.acc[0];
-            atomicAdd(a.elbo_out, tot);
-        }
+    if (a.kl_out && a.include_kl) {
+        const float tot = block_sum(klp, red);
+        if (threadIdx.x == 0) atomicAdd(a.kl_out, (double)tot);
     }
 }
 
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params, float* m,
-                            float* v, const psvi_adam_hp* hp, float* elbo_out,
+                            float* v, const psvi_adam_hp* hp, double* kl_out,
                             float* grad_out, int include_kl, hipStream_t st) {
     MfUpdArgs a{};
     a.L = p.L;
@@ -109,14 +108,17 @@ hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
     a.m = m;
     a.v = v;
     a.grad_out = grad_out;
-    a.elbo_out = elbo_out;
+    a.kl_out = kl_out;
     a.include_kl = include_kl;
     const float s0 = p.d.prior_sd;
     a.inv_s0sq = 1.f / (s0 * s0);
     a.log_s0 = logf(s0);
     if (hp) a.adam = make_adam(hp);
     const int nb = (p.n_tot + 255) / 256;
-    hipLaunchKernelGGL(mf_update_kernel, dim3(nb), dim3(256), 0, st, a);
+    if (grad_out)
+        hipLaunchKernelGGL(mf_update_kernel<true>, dim3(nb), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(mf_update_kernel<false>, dim3(nb), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

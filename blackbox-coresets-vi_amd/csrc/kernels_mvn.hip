@@ -29,7 +29,7 @@ struct MvnLayerArgs {
 };
 
 // ----------------------------------------------------------------- forward
-constexpr int FBK = 32;    // k (columns of L) per LDS stage
+constexpr int FBK = 64;    // k (columns of L) per LDS stage
 constexpr int FST = 128;   // samples per pass: 4 waves x 32
 
 struct FwdArgs {
@@ -51,6 +51,8 @@ __global__ __launch_bounds__(256) void mvn_fwd_kernel(FwdArgs a) {
     const float* corr = mean + 2 * n;
     const float* E = a.eps + a.lay[it.layer].eoff;   // [S][n]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const rsrc_t rsL = make_rsrc(corr, ((int64_t)(n - 1) * (n - 2) / 2) * 4);
+    const rsrc_t rsE = make_rsrc(E, (int64_t)a.S * n * 4);
 
     for (int sb = 0; sb < a.S; sb += FST) {
         floatx16 acc;
@@ -58,35 +60,32 @@ __global__ __launch_bounds__(256) void mvn_fwd_kernel(FwdArgs a) {
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
         const bool wave_live = sb + 32 * wv < a.S;
         // register prefetch of stage kb
-        float lreg[4], ereg[16];
+        float lreg[FBK / 8], ereg[FBK / 2];
+        // L rows of this item and eps rows of this pass; loads outside the
+        // triangle / past S read 0 through the buffer range check.  eps
+        // columns past k1 need no mask: they meet zero L entries.
+        const int kk = tid % FBK, rq = tid / FBK;
         auto fetch = [&](int kb) {
+            const int c = kb + kk;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int e = tid + 256 * j, rr = e >> 5, kk = e & 31;
-                const int r = it.r0 + rr, c = kb + kk;
-                lreg[j] = (r < it.r1 && c < r && c < it.k1 && r <= n - 2)
-                              ? corr[(int64_t)r * (r - 1) / 2 + c] : 0.f;
+            for (int j = 0; j < FBK / 8; ++j) {
+                const int r = it.r0 + rq + 4 * j;
+                const bool ok = r < it.r1 && c < r && c < it.k1 && r <= n - 2;
+                lreg[j] = bload(rsL, ok ? (uint32_t)(((int64_t)r * (r - 1) / 2 + c) * 4) : kOOB);
             }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int e = tid + 256 * j, ss = e >> 5, kk = e & 31;
-                const int s = sb + ss, c = kb + kk;
-                ereg[j] = (s < a.S && c < it.k1) ? E[(int64_t)s * n + c] : 0.f;
+            for (int j = 0; j < FBK / 2; ++j) {
+                const int srow = sb + rq + 4 * j;
+                ereg[j] = bload(rsE, (uint32_t)(((int64_t)srow * n + c) * 4));
             }
         };
         if (it.k0 < it.k1) fetch(it.k0);
         for (int kb = it.k0; kb < it.k1; kb += FBK) {
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int e = tid + 256 * j;
-                Ls[e >> 5][e & 31] = lreg[j];
-            }
+            for (int j = 0; j < FBK / 8; ++j) Ls[rq + 4 * j][kk] = lreg[j];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int e = tid + 256 * j;
-                Es[e >> 5][e & 31] = ereg[j];
-            }
+            for (int j = 0; j < FBK / 2; ++j) Es[rq + 4 * j][kk] = ereg[j];
             __syncthreads();
             if (kb + FBK < it.k1) fetch(kb + FBK);
             if (wave_live) {
@@ -122,28 +121,30 @@ __global__ __launch_bounds__(256) void mvn_fwd_kernel(FwdArgs a) {
 
 // ---------------------------------------------------------------- backward
 constexpr int BT = 64;    // output tile 64 (rows r) x 64 (cols c)
-constexpr int BKS = 32;   // samples per LDS stage
+constexpr int BKS = 128;  // samples staged per pass (K of the dL GEMM); S <= 128: one pass
 
 struct UpdArgs {
     const BwdTile* tiles;
     const DiagBlock* diag;
-    int n_tiles;
+    int n_tiles, n_diag;
     const float* eps;
     const float* g;    // g_shard [S][ldg]
     int ldg, S;
     float* params;
     float* m;
     float* v;
-    float* grad_out;   // nullable
-    float* kl_out;     // nullable
+    float* grad_out;   // GRAD mode output
+    double* kl_out;    // nullable
+    int64_t pcount;    // parameter vector length
     int include_kl;
     float inv_s0sq, log_s0;
     AdamC adam;
     MvnLayerArgs lay[kMaxL];
 };
 
+template <bool GRAD>
 __device__ __forceinline__ void upd_elem(const UpdArgs& a, int64_t pidx, float gval) {
-    if (a.grad_out) {
+    if (GRAD) {
         a.grad_out[pidx] = gval;
     } else {
         float mm = a.m[pidx], vv = a.v[pidx];
@@ -154,76 +155,131 @@ __device__ __forceinline__ void upd_elem(const UpdArgs& a, int64_t pidx, float g
     }
 }
 
+// Tiles: dL[r0:r0+64, c0:c0+64] = G^T eps over all S samples (4 waves, 32x32
+// each), then the fused corr update.  Memory schedule per tile: issue the
+// G / eps loads of the first sample chunk, THEN the epilogue's corr/m/v loads
+// (vmcnt retires in order, so the GEMM operands are not held behind them),
+// stage the chunk in LDS, run the MFMAs while the corr/m/v loads land, update.
+// Diag blocks (blockIdx < n_diag, scheduled first): mean and sd of 64 rows each.
+template <bool GRAD>
 __global__ __launch_bounds__(256) void mvn_update_kernel(UpdArgs a) {
     __shared__ float Gs[BKS][BT + 1];
     __shared__ float Xs[BKS][BT + 1];
     __shared__ float red[8];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
     float klp = 0.f;
-    if ((int)blockIdx.x < a.n_tiles) {
-        const BwdTile t = a.tiles[blockIdx.x];
+    if ((int)blockIdx.x >= a.n_diag) {
+        const BwdTile t = a.tiles[(int)blockIdx.x - a.n_diag];
         const int n = a.lay[t.layer].n;
         const float* E = a.eps + a.lay[t.layer].eoff;
         const int64_t corr_off = a.lay[t.layer].poff + 2 * n;
         const int wr = wv >> 1, wc = wv & 1;
+        const int c = t.c0 + 32 * wc + l32;
+        const int rb = t.r0 + 32 * wr + 4 * h;
+        const int cc = tid & 63, s0 = tid >> 6;   // staging: column, first sample row
+        // Out-of-tile rows / columns of G and eps only feed dL entries the
+        // epilogue masks, so staging needs no predicate; rows past S read 0.
+        const rsrc_t rsG = make_rsrc(a.g, (int64_t)a.S * a.ldg * 4);
+        const rsrc_t rsE = make_rsrc(E, (int64_t)a.S * n * 4);
+        const rsrc_t rsP = make_rsrc(a.params, a.pcount * 4);
+        const rsrc_t rsM = make_rsrc(a.m, GRAD ? 0 : a.pcount * 4);
+        const rsrc_t rsV = make_rsrc(a.v, GRAD ? 0 : a.pcount * 4);
+        const uint32_t gcol = (uint32_t)(t.xcol + t.r0 + cc) * 4;
+        const uint32_t xcol = (uint32_t)(t.c0 + cc) * 4;
         floatx16 acc;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-        float greg[8], xreg[8];
-        auto fetch = [&](int sb) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int e = tid + 256 * j, ss = e >> 6, cc = e & 63;
-                const int s = sb + ss;
-                const int r = t.r0 + cc, c = t.c0 + cc;
-                greg[j] = (s < a.S && r < t.rhi) ? a.g[(int64_t)s * a.ldg + t.xcol + r] : 0.f;
-                xreg[j] = (s < a.S && c < n) ? E[(int64_t)s * n + c] : 0.f;
-            }
-        };
-        fetch(0);
+        float pq[16], mq[16], vq[16];
         for (int sb = 0; sb < a.S; sb += BKS) {
-            __syncthreads();
+            float greg[BKS / 4], xreg[BKS / 4];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int e = tid + 256 * j;
-                Gs[e >> 6][e & 63] = greg[j];
-                Xs[e >> 6][e & 63] = xreg[j];
+            for (int j = 0; j < BKS / 4; ++j) {
+                const uint32_t s = sb + s0 + 4 * j;
+                greg[j] = bload(rsG, gcol + s * (uint32_t)a.ldg * 4);
+                xreg[j] = bload(rsE, xcol + s * (uint32_t)n * 4);
+            }
+            if (sb == 0) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int r = rb + (q & 3) + 8 * (q >> 2);
+                    const bool ok = r >= t.rlo && r < t.rhi && c < r;
+                    const uint32_t off =
+                        ok ? (uint32_t)((corr_off + (int64_t)r * (r - 1) / 2 + c) * 4) : kOOB;
+                    pq[q] = bload(rsP, off);
+                    if (!GRAD) {
+                        mq[q] = bload(rsM, off);
+                        vq[q] = bload(rsV, off);
+                    }
+                }
+            } else {
+                __syncthreads();  // previous chunk fully consumed
+            }
+#pragma unroll
+            for (int j = 0; j < BKS / 4; ++j) {
+                Gs[s0 + 4 * j][cc] = greg[j];
+                Xs[s0 + 4 * j][cc] = xreg[j];
             }
             __syncthreads();
-            if (sb + BKS < a.S) fetch(sb + BKS);
-#pragma unroll
-            for (int kk = 0; kk < BKS; kk += 2) {
+            const int kend = min(BKS, a.S - sb);
+            for (int kk = 0; kk < kend; kk += 2) {
                 const float av = Gs[kk + h][32 * wr + l32];
                 const float bv = Xs[kk + h][32 * wc + l32];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
             }
         }
         // D[i = r][j = c]: j = lane&31, i = (q&3) + 8(q>>2) + 4h
-        const int c = t.c0 + 32 * wc + l32;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const int r = t.r0 + 32 * wr + (q & 3) + 8 * (q >> 2) + 4 * h;
+            const int r = rb + (q & 3) + 8 * (q >> 2);
             if (r >= t.rlo && r < t.rhi && c < r) {
                 const int64_t pidx = corr_off + (int64_t)r * (r - 1) / 2 + c;
-                const float p = a.params[pidx];
+                const float p = pq[q];
                 klp += p * p;
-                upd_elem(a, pidx, a.include_kl ? acc[q] + p * a.inv_s0sq : acc[q]);
+                const float gval = a.include_kl ? acc[q] + p * a.inv_s0sq : acc[q];
+                if (GRAD) {
+                    a.grad_out[pidx] = gval;
+                } else {
+                    float mm = mq[q], vv = vq[q];
+                    a.params[pidx] = adam_apply(a.adam, p, gval, mm, vv);
+                    a.m[pidx] = mm;
+                    a.v[pidx] = vv;
+                }
             }
         }
         klp *= 0.5f * a.inv_s0sq;
     } else {
-        const DiagBlock db = a.diag[blockIdx.x - a.n_tiles];
+        // 64 rows per block; the 4 waves split the samples, partial sums meet
+        // in LDS (reusing the staging arrays); loads batched 8 deep.
+        const DiagBlock db = a.diag[blockIdx.x];
         const int n = a.lay[db.layer].n;
         const float* E = a.eps + a.lay[db.layer].eoff;
-        const int r = db.r0 + tid;
-        if (r < db.rhi) {
-            float gm = 0.f, gs = 0.f;
-            const float* gcol = a.g + db.xcol + r;
-            for (int s = 0; s < a.S; ++s) {
-                const float gv = gcol[(int64_t)s * a.ldg];
-                gm += gv;
-                gs = fmaf(gv, E[(int64_t)s * n + r], gs);
+        const int r = db.r0 + (tid & 63);
+        const bool rv = r < db.rhi;
+        const int rr = rv ? r : db.r0;
+        const rsrc_t rsG = make_rsrc(a.g, (int64_t)a.S * a.ldg * 4);
+        const rsrc_t rsE = make_rsrc(E, (int64_t)a.S * n * 4);
+        const uint32_t gofs = (uint32_t)(db.xcol + rr) * 4, eofs = (uint32_t)rr * 4;
+        float gm = 0.f, gs = 0.f;
+        for (int s0 = wv; s0 < a.S; s0 += 32) {
+            float gv[8], ev[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t s = s0 + 4 * k;   // past S: range check -> 0
+                gv[k] = bload(rsG, gofs + s * (uint32_t)a.ldg * 4);
+                ev[k] = bload(rsE, eofs + s * (uint32_t)n * 4);
             }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                gm += gv[k];
+                gs = fmaf(gv[k], ev[k], gs);
+            }
+        }
+        Gs[wv][tid & 63] = gm;
+        Xs[wv][tid & 63] = gs;
+        __syncthreads();
+        if (tid < 64 && rv) {
+            gm = Gs[0][tid] + Gs[1][tid] + Gs[2][tid] + Gs[3][tid];
+            gs = Xs[0][tid] + Xs[1][tid] + Xs[2][tid] + Xs[3][tid];
             const int64_t pm = a.lay[db.layer].poff + r, ps = pm + n;
             const float mu = a.params[pm], sdr = a.params[ps];
             const float sp = softplus_f(sdr), sg = sigmoid_f(sdr);
@@ -233,13 +289,13 @@ __global__ __launch_bounds__(256) void mvn_update_kernel(UpdArgs a) {
                 gsd += (sp * a.inv_s0sq - 1.f / sp) * sg;
                 klp = a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
             }
-            upd_elem(a, pm, gmean);
-            upd_elem(a, ps, gsd);
+            upd_elem<GRAD>(a, pm, gmean);
+            upd_elem<GRAD>(a, ps, gsd);
         }
     }
     if (a.kl_out && a.include_kl) {
         const float tot = block_sum(klp, red);
-        if (tid == 0) atomicAdd(a.kl_out, tot);
+        if (tid == 0) atomicAdd(a.kl_out, (double)tot);
     }
 }
 
@@ -270,11 +326,12 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
-                             float* kl_out, float* grad_out, int include_kl, hipStream_t st) {
+                             double* kl_out, float* grad_out, int include_kl, hipStream_t st) {
     UpdArgs a{};
     a.tiles = p.d_bwd;
     a.diag = p.d_diag;
     a.n_tiles = p.n_bwd;
+    a.n_diag = p.n_diag;
     a.eps = eps;
     a.g = g_shard;
     a.ldg = p.rows_tot[p.rank];
@@ -285,6 +342,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
     a.grad_out = grad_out;
     a.kl_out = kl_out;
     a.include_kl = include_kl;
+    a.pcount = p.P;
     const float s0 = p.d.prior_sd;
     a.inv_s0sq = 1.f / (s0 * s0);
     a.log_s0 = logf(s0);
@@ -292,7 +350,10 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
     fill_layers(p, a.lay);
     const int nb = p.n_bwd + p.n_diag;
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(mvn_update_kernel, dim3(nb), dim3(256), 0, st, a);
+    if (grad_out)
+        hipLaunchKernelGGL(mvn_update_kernel<true>, dim3(nb), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(mvn_update_kernel<false>, dim3(nb), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

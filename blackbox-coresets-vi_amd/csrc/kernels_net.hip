@@ -11,8 +11,8 @@
 //
 // One workgroup = one MC sample x one chunk of pseudopoints.  Everything the
 // sample needs (its weights, the pseudo-input chunk, every layer's
-// activations) is staged in LDS with odd row strides (conflict-free b32
-// column walks); the contractions are 4x4 register-tiled VALU FMA chains.
+// activations) is staged in LDS with odd row strides; the per-sample
+// contractions run on fp32 MFMA (16x16x4) tiles.
 //  MEANFIELD: W_s = mu + softplus(rho) * eps formed in LDS; per-sample dW and
 //             dW*eps go to the [sum_s dW | sum_s dW*eps] accumulators
 //             (fp32 atomics, S adders per address).
@@ -32,7 +32,7 @@ struct NetArgs {
     const float* u;
     const int32_t* z;
     const float* w;
-    float* nll_out;
+    double* nll_out;   // fp64 accumulator (many similar-size adds)
     // MEANFIELD
     const float* params;
     const float* eps;
@@ -48,49 +48,70 @@ struct NetArgs {
     int src_lo[kMaxWorld][kMaxL], src_hi[kMaxWorld][kMaxL], src_col[kMaxWorld][kMaxL];
 };
 
-// C[p][q] = sum_k A(p,k) B(q,k), A(p,k)=A[p*sap+k*sak], B(q,k)=B[q*sbq+k*sbk].
-// Thread t owns p in {pt + i*tp}, q in {qt + j*tq}: consecutive lanes walk
-// consecutive q, so unit-stride operands are conflict-free.
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// C[p][q] = sum_k A(p,k) B(q,k), A(p,k)=A[p*sap+k*sak], B(q,k)=B[q*sbq+k*sbk],
+// all operands in LDS.  16x16 output tiles on v_mfma_f32_16x16x4_f32 (exact
+// fp32), dealt round-robin to the workgroup's waves; lane l feeds
+// A[p0 + (l&15)][k + (l>>4)] and B[q0 + (l&15)][k + (l>>4)] and holds
+// D[p0 + 4(l>>4) + r][q0 + (l&15)], r = 0..3.  Out-of-range rows / k read 0.
+// (LDS reads are predicated selects, not branches: LDS, unlike VMEM, has no
+// in-order counter to drain.)
 template <bool RELU_A, bool RELU_B, class Epi>
 __device__ __forceinline__ void lds_gemm(int P, int Q, int K, const float* __restrict__ A,
                                          int sap, int sak, const float* __restrict__ B,
                                          int sbq, int sbk, Epi epi) {
-    const int tp = (P + 3) >> 2, tq = (Q + 3) >> 2;
-    for (int t = threadIdx.x; t < tp * tq; t += blockDim.x) {
-        const int pt = t / tq, qt = t - pt * tq;
-        const float* Ap[4];
-        const float* Bp[4];
+    // Work unit = one 16-row block of P x TWO adjacent 16-column blocks of Q:
+    // two independent accumulator chains (hides the 40-cycle dependent
+    // latency of 16x16x4) sharing the A fragment (3 LDS reads per 2 MFMAs).
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const int i16 = lane & 15, k4 = lane >> 4;
+    const int tp = (P + 15) >> 4, tq2 = (Q + 31) >> 5;
+    for (int t = wid; t < tp * tq2; t += nwv) {
+        const int p0 = (t / tq2) << 4, q0 = (t - (t / tq2) * tq2) << 5;
+        const int p = p0 + i16, qa = q0 + i16, qb = qa + 16;
+        const bool pv = p < P, qav = qa < Q, qbv = qb < Q;
+        const float* Ap = A + (pv ? p : 0) * sap;
+        const float* Ba = B + (qav ? qa : 0) * sbq;
+        const float* Bb = B + (qbv ? qb : 0) * sbq;
+        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        int kb = 0;  // wave-uniform k base
+        for (; kb + 16 <= K; kb += 16) {
+            float av[4], b0[4], b1[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            Ap[i] = A + min(pt + i * tp, P - 1) * sap;
-            Bp[i] = B + min(qt + i * tq, Q - 1) * sbq;
-        }
-        float acc[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-        for (int k = 0; k < K; ++k) {
-            float av[4], bv[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                av[i] = Ap[i][k * sak];
-                if (RELU_A) av[i] = fmaxf(av[i], 0.f);
-                bv[i] = Bp[i][k * sbk];
-                if (RELU_B) bv[i] = fmaxf(bv[i], 0.f);
+            for (int u = 0; u < 4; ++u) {
+                const int kk = kb + 4 * u + k4;
+                av[u] = pv ? Ap[kk * sak] : 0.f;
+                b0[u] = qav ? Ba[kk * sbk] : 0.f;
+                b1[u] = qbv ? Bb[kk * sbk] : 0.f;
+                if (RELU_A) av[u] = fmaxf(av[u], 0.f);
+                if (RELU_B) { b0[u] = fmaxf(b0[u], 0.f); b1[u] = fmaxf(b1[u], 0.f); }
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+            for (int u = 0; u < 4; ++u) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b0[u], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b1[u], acc1, 0, 0, 0);
+            }
+        }
+        for (; kb < K; kb += 4) {
+            const int kk = kb + k4;
+            const bool kv = kk < K;
+            float av = (pv && kv) ? Ap[kk * sak] : 0.f;
+            float b0 = (qav && kv) ? Ba[kk * sbk] : 0.f;
+            float b1 = (qbv && kv) ? Bb[kk * sbk] : 0.f;
+            if (RELU_A) av = fmaxf(av, 0.f);
+            if (RELU_B) { b0 = fmaxf(b0, 0.f); b1 = fmaxf(b1, 0.f); }
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc1, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int p = pt + i * tp, q = qt + j * tq;
-                if (p < P && q < Q) epi(p, q, acc[i][j]);
+        for (int r = 0; r < 4; ++r) {
+            const int pp = p0 + 4 * k4 + r;
+            if (pp < P) {
+                if (qav) epi(pp, qa, acc0[r]);
+                if (qbv) epi(pp, qb, acc1[r]);
             }
+        }
     }
 }
 
@@ -111,10 +132,15 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
     const int L = a.L;
 
     // ---- 1. this sample's weights into LDS ------------------------------
+    // Global -> LDS copies issue kB independent loads per thread before any
+    // LDS store (a load-then-store loop would expose one memory latency per
+    // element); indices are clamped so every load is unconditional.
+    constexpr int kB = 8;
     for (int l = 0; l < L; ++l) {
         const int din = a.din[l], dout = a.dout[l], nw = din * dout, n = nw + dout;
         float* W = sm + a.lw[l];
         float* Bv = sm + a.lb[l];
+        const int ldw = a.ldw[l];
         if (FAM == PSVI_FAMILY_MEANFIELD) {
             const float* mu = a.params + a.poff[l];
             const float* rho = mu + n;
@@ -122,31 +148,51 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
             const float* eB = a.eps + a.eoff[l] + (int64_t)a.S_total * nw + (int64_t)sg * dout;
             float* E = sm + a.le[l];
             float* EB = sm + a.leb[l];
-            for (int idx = threadIdx.x; idx < n; idx += blockDim.x) {
-                const float e = idx < nw ? eW[idx] : eB[idx - nw];
-                // Normal.rsample: loc + eps * scale (torch/distributions/normal.py)
-                const float val = mu[idx] + e * softplus_f(rho[idx]);
-                if (idx < nw) {
-                    const int j = idx / din, i = idx - j * din;
-                    W[j * a.ldw[l] + i] = val;
-                    E[j * a.ldw[l] + i] = e;
-                } else {
-                    Bv[idx - nw] = val;
-                    EB[idx - nw] = e;
+            for (int base = threadIdx.x; base < n; base += kB * blockDim.x) {
+                float vm[kB], vr[kB], ve[kB];
+#pragma unroll
+                for (int k = 0; k < kB; ++k) {
+                    const int idx = min(base + k * (int)blockDim.x, n - 1);
+                    vm[k] = mu[idx];
+                    vr[k] = rho[idx];
+                    ve[k] = idx < nw ? eW[idx] : eB[idx - nw];
+                }
+#pragma unroll
+                for (int k = 0; k < kB; ++k) {
+                    const int idx = base + k * (int)blockDim.x;
+                    if (idx >= n) break;
+                    // Normal.rsample: loc + eps * scale (torch/distributions/normal.py)
+                    const float val = vm[k] + ve[k] * softplus_f(vr[k]);
+                    if (idx < nw) {
+                        const int j = idx / din, i = idx - j * din;
+                        W[j * ldw + i] = val;
+                        E[j * ldw + i] = ve[k];
+                    } else {
+                        Bv[idx - nw] = val;
+                        EB[idx - nw] = ve[k];
+                    }
                 }
             }
         } else {
             for (int p = 0; p < a.nsrc; ++p) {
                 const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
+                if (hi <= lo) continue;
                 const float* src = a.xrecv + a.src_base[p] + (int64_t)s * a.src_stride[p] +
                                    a.src_col[p][l] - lo;
-                for (int r = lo + threadIdx.x; r < hi; r += blockDim.x) {
-                    const float val = src[r];
-                    if (r < nw) {
-                        const int j = r / din, i = r - j * din;
-                        W[j * a.ldw[l] + i] = val;
-                    } else {
-                        Bv[r - nw] = val;
+                for (int base = lo + threadIdx.x; base < hi; base += kB * blockDim.x) {
+                    float v[kB];
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) v[k] = src[min(base + k * (int)blockDim.x, hi - 1)];
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) {
+                        const int r = base + k * (int)blockDim.x;
+                        if (r >= hi) break;
+                        if (r < nw) {
+                            const int j = r / din, i = r - j * din;
+                            W[j * ldw + i] = v[k];
+                        } else {
+                            Bv[r - nw] = v[k];
+                        }
                     }
                 }
             }
@@ -154,11 +200,20 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
     }
     // ---- 2. pseudo-input chunk -------------------------------------------
     {
-        const int D = a.din[0];
+        const int D = a.din[0], nU = mcnt * D;
         float* U = sm + a.lu;
-        for (int idx = threadIdx.x; idx < mcnt * D; idx += blockDim.x) {
-            const int m = idx / D, i = idx - m * D;
-            U[m * a.ldu + i] = a.u[(int64_t)(m0 + m) * D + i];
+        const float* src = a.u + (int64_t)m0 * D;
+        for (int base = threadIdx.x; base < nU; base += kB * blockDim.x) {
+            float v[kB];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) v[k] = src[min(base + k * (int)blockDim.x, nU - 1)];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                const int idx = base + k * (int)blockDim.x;
+                if (idx >= nU) break;
+                const int m = idx / D, i = idx - m * D;
+                U[m * a.ldu + i] = v[k];
+            }
         }
     }
     __syncthreads();
@@ -191,18 +246,18 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
             float mx = row[0];
             for (int k = 1; k < C; ++k) mx = fmaxf(mx, row[k]);
             float se = 0.f;
-            for (int k = 0; k < C; ++k) se += __expf(row[k] - mx);
-            const float lse = mx + __logf(se);
+            for (int k = 0; k < C; ++k) se += expf(row[k] - mx);
+            const float lse = mx + logf(se);
             const int zm = a.z[m0 + m];
             const float wm = a.w[m0 + m];
             part += wm * (lse - row[zm]);
             for (int k = 0; k < C; ++k) {
-                const float pk = __expf(row[k] - lse);
+                const float pk = expf(row[k] - lse);
                 row[k] = wm * (pk - (k == zm ? 1.f : 0.f));
             }
         }
         const float tot = block_sum(part, sm + a.lred);
-        if (threadIdx.x == 0) atomicAdd(a.nll_out, tot);
+        if (threadIdx.x == 0) atomicAdd(a.nll_out, (double)tot);
         __syncthreads();
     }
 
@@ -331,7 +386,7 @@ void net_set_lds_limit() {
 
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* accMu, float* accRho,
-                      const float* xrecv, float* gsend, float* nll_out, hipStream_t st) {
+                      const float* xrecv, float* gsend, double* nll_out, hipStream_t st) {
     NetArgs a{};
     a.L = p.L;
     a.M = p.d.M;

@@ -18,9 +18,9 @@ constexpr int kWave = 64;
 // ---------------------------------------------------------------- numerics
 // torch.nn.functional.softplus(beta=1, threshold=20)
 __device__ __forceinline__ float softplus_f(float x) {
-    return x > 20.f ? x : log1pf(__expf(x));
+    return x > 20.f ? x : log1pf(expf(x));
 }
-__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -39,6 +39,23 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     if (threadIdx.x == 0)
         for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
     return t;  // valid in thread 0
+}
+
+// ------------------------------------------------------- buffer loads (T8)
+// 128-bit SRD in SGPRs + 32-bit per-lane byte offset; the hardware range
+// check returns 0 for any offset >= `bytes`, which is how the kernels mask
+// ragged / triangular tiles without exec-mask branches around the loads.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // byte offset past every buffer we map
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
+    const uint32_t nb = bytes > 0x7fffffff ? 0x7fffffffu : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nb,
+                                             0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
+    // the builtin returns the raw 32 bits as an integer
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
 // Adam, both reference variants; returns new p, updates m, v in place.
@@ -86,7 +103,7 @@ struct FwdItem {
 struct BwdTile {
     int layer, r0, c0, rlo, rhi, xcol;  // xcol: g_shard column of row rlo
 };
-// Full-cov per-row (mean, sd) block: rows [r0, r0+256) of layer, clipped.
+// Full-cov per-row (mean, sd) block: rows [r0, r0+64) of layer, clipped.
 struct DiagBlock {
     int layer, r0, rhi, xcol;
 };
@@ -132,15 +149,15 @@ namespace psvi {
 // launchers (defined in the .hip translation units)
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* accMu, float* accRho,
-                      const float* xrecv, float* gsend, float* nll_out, hipStream_t st);
+                      const float* xrecv, float* gsend, double* nll_out, hipStream_t st);
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
-                            float* m, float* v, const psvi_adam_hp* hp, float* elbo_out,
+                            float* m, float* v, const psvi_adam_hp* hp, double* kl_out,
                             float* grad_out, int include_kl, hipStream_t st);
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
                           float* x_shard, hipStream_t st);
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
-                             float* kl_out, float* grad_out, int include_kl, hipStream_t st);
+                             double* kl_out, float* grad_out, int include_kl, hipStream_t st);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);

@@ -65,8 +65,9 @@ SIGNATURES = {
     "psvi_inner_step": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P,
                                _SZ, _P]),
     "psvi_elbo_grad": (_I32, [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
-    "psvi_mf_phase_accumulate": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P]),
-    "psvi_mf_phase_update": (_I32, [_P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P, _P]),
+    "psvi_mf_phase_accumulate": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "psvi_mf_phase_update": (_I32, [_P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P, _I32,
+                                    _P]),
     "psvi_mvn_phase_sample": (_I32, [_P, _P, _P, _P, _P]),
     "psvi_mvn_phase_net": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "psvi_mvn_phase_update": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P,

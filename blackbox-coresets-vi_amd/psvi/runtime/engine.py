@@ -114,12 +114,13 @@ class InnerLoopPlan:
     def inner_step(self, u, z, w, eps, params, adam_m, adam_v, step, lr, kind="higher",
                    elbo_out=None, ws=None):
         """One fused inner step (psvi_inner_step); params/m/v updated in place.
-        Returns the (device) negative ELBO at the incoming params."""
+        Returns the (device, float64) negative ELBO at the incoming params."""
         self._inputs(u, z, w, eps)
         for t, n in ((params, "params"), (adam_m, "adam_m"), (adam_v, "adam_v")):
             _need(t, n, self.param_count)
         if elbo_out is None:
-            elbo_out = torch.empty(1, dtype=torch.float32, device=params.device)
+            elbo_out = torch.empty(1, dtype=torch.float64, device=params.device)
+        _need(elbo_out, "elbo_out", 1, torch.float64)
         if ws is None:
             ws = self.workspace(params.device)
         hp = make_adam(lr, step, kind)
@@ -132,7 +133,7 @@ class InnerLoopPlan:
     def elbo_grad(self, u, z, w, eps, params, include_kl=True, ws=None):
         self._inputs(u, z, w, eps)
         _need(params, "params", self.param_count)
-        elbo = torch.empty(1, dtype=torch.float32, device=params.device)
+        elbo = torch.empty(1, dtype=torch.float64, device=params.device)
         grad = torch.empty(self.param_count, dtype=torch.float32, device=params.device)
         if ws is None:
             ws = self.workspace(params.device)
@@ -143,22 +144,28 @@ class InnerLoopPlan:
         return elbo, grad
 
     # ------------------------------------------------------------ phases
-    def mf_accumulate(self, u, z, w, eps, params, acc):
+    def mf_accumulate(self, u, z, w, eps, params, acc, nll_out):
+        """acc <- [sum_s dW | sum_s dW*eps] (this rank's samples); nll_out += NLL."""
         self._inputs(u, z, w, eps)
         _need(params, "params", self.param_count)
         _need(acc, "acc", self.acc_count)
+        _need(nll_out, "nll_out", 1, torch.float64)
         check(self.lib.psvi_mf_phase_accumulate(self.handle, _ptr(u), _ptr(z), _ptr(w),
-                                                _ptr(eps), _ptr(params), _ptr(acc), _stream()),
+                                                _ptr(eps), _ptr(params), _ptr(acc),
+                                                _ptr(nll_out), _stream()),
               "psvi_mf_phase_accumulate")
 
     def mf_update(self, acc, params, adam_m=None, adam_v=None, step=1, lr=1e-3,
-                  kind="higher", elbo_out=None, grad_out=None):
+                  kind="higher", kl_out=None, grad_out=None, include_kl=True):
         _need(acc, "acc", self.acc_count)
         _need(params, "params", self.param_count)
+        if kl_out is not None:
+            _need(kl_out, "kl_out", 1, torch.float64)
         hp = make_adam(lr, step, kind)
         check(self.lib.psvi_mf_phase_update(self.handle, _ptr(acc), _ptr(params), _ptr(adam_m),
-                                            _ptr(adam_v), ctypes.byref(hp), _ptr(elbo_out),
-                                            _ptr(grad_out), _stream()), "psvi_mf_phase_update")
+                                            _ptr(adam_v), ctypes.byref(hp), _ptr(kl_out),
+                                            _ptr(grad_out), int(bool(include_kl)), _stream()),
+              "psvi_mf_phase_update")
 
     def mvn_sample(self, eps, params, x_shard):
         _need(eps, "eps", self.eps_count)
@@ -173,7 +180,7 @@ class InnerLoopPlan:
         _need(w, "w", self.M)
         _need(x_recv, "x_recv", self.xrecv_count)
         _need(g_send, "g_send", self.xrecv_count)
-        _need(nll_out, "nll_out", 1)
+        _need(nll_out, "nll_out", 1, torch.float64)
         check(self.lib.psvi_mvn_phase_net(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv),
                                           _ptr(g_send), _ptr(nll_out), _stream()),
               "psvi_mvn_phase_net")
@@ -183,6 +190,8 @@ class InnerLoopPlan:
         _need(eps, "eps", self.eps_count)
         _need(g_shard, "g_shard", self.xshard_count)
         _need(params, "params", self.param_count)
+        if kl_out is not None:
+            _need(kl_out, "kl_out", 1, torch.float64)
         hp = make_adam(lr, step, kind)
         check(self.lib.psvi_mvn_phase_update(self.handle, _ptr(eps), _ptr(g_shard),
                                              _ptr(params), _ptr(adam_m), _ptr(adam_v),

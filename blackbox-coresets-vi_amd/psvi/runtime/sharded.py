@@ -65,7 +65,8 @@ class ShardedInnerLoop:
             self.g_out = list(self.x_in)
         else:
             self.acc = torch.empty(self.plan.acc_count, **f32)
-        self.parts = torch.zeros(2, **f32)  # [local NLL, local KL] of the last step
+        # [local NLL, local KL] of the last step (fp64 accumulators)
+        self.parts = torch.zeros(2, dtype=torch.float64, device=device)
 
     # -------------------------------------------------------------- phases
     def phase_sample(self, eps, params):
@@ -81,7 +82,7 @@ class ShardedInnerLoop:
 
     # ---------------------------------------------------------------- step
     def step(self, u, z, w, eps, params, m, v, step, lr, kind="higher", elbo_parts=None):
-        """One inner step on this rank.  elbo_parts (2 floats, optional)
+        """One inner step on this rank.  elbo_parts (2 doubles, optional)
         receives this rank's [NLL, KL] contributions; their sum over ranks
         (see reduce_elbo) is the negative inner ELBO."""
         if self.family == "fullcov":
@@ -93,15 +94,14 @@ class ShardedInnerLoop:
             if elbo_parts is not None:
                 elbo_parts.copy_(self.parts)
         else:
-            self.plan.mf_accumulate(u, z, w, eps, params, self.acc)
+            self.parts.zero_()
+            self.plan.mf_accumulate(u, z, w, eps, params, self.acc, self.parts[0:1])
             self.comm.all_reduce(self.acc)
-            out = elbo_parts[0:1] if elbo_parts is not None else None
+            # replicated update; the KL value is counted on rank 0 only
             self.plan.mf_update(self.acc, params, m, v, step=step, lr=lr, kind=kind,
-                                elbo_out=out)
-            if elbo_parts is not None and self.rank != 0:
-                elbo_parts.zero_()  # replicated: count the ELBO once
-            elif elbo_parts is not None:
-                elbo_parts[1:2].zero_()
+                                kl_out=self.parts[1:2] if self.rank == 0 else None)
+            if elbo_parts is not None:
+                elbo_parts.copy_(self.parts)
 
     def reduce_elbo(self, elbo_parts):
         """elbo_parts (T, 2) stacked per step -> negative ELBO per step (all ranks)."""

@@ -35,6 +35,11 @@
  *     count of the plan; every rank passes the full eps.
  *   - z holds int32 class ids; w holds the coreset weights N*f(v) (M floats,
  *     psvi_classes.py:505).
+ *   - Scalar objective outputs (elbo_out, nll_out, kl_out) are DOUBLE device
+ *     accumulators: the kernels add thousands of per-block partials into them
+ *     and fp32 accumulation would bias the sum (rounding of similar-size adds
+ *     into a large running total).  They are accumulated into (+=) unless a
+ *     call documents that it zeroes them.
  */
 #ifndef PSVI_HIP_H
 #define PSVI_HIP_H
@@ -90,7 +95,8 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_WS_BYTES      3  /* workspace bytes for psvi_inner_step/elbo_grad      */
 #define PSVI_Q_S_LOCAL       4  /* samples owned by this rank                         */
 #define PSVI_Q_S_OFFSET      5  /* first global sample owned by this rank             */
-#define PSVI_Q_ACC_COUNT     6  /* mean-field: floats in the all-reduced accumulator  */
+#define PSVI_Q_ACC_COUNT     6  /* mean-field: floats in the all-reduced accumulator
+                                   [sum_s dW | sum_s dW*eps] = 2 * sum_l n_l         */
 #define PSVI_Q_ROWS_LOCAL    7  /* full-cov: x/g columns owned (sum over layers)      */
 #define PSVI_Q_XSHARD_COUNT  8  /* full-cov: floats of x_shard / g_shard = S*ROWS_LOCAL */
 #define PSVI_Q_XRECV_COUNT   9  /* full-cov: floats of x_recv / g_send = S_LOCAL*n_tot */
@@ -111,32 +117,38 @@ int psvi_plan_shard_info(const psvi_plan* plan, int32_t r, int64_t* out);
 /* ---- single-process fused step (world == 1) --------------------------------
  * One inner step = reparameterise, batched forward over (S x M), weighted NLL
  * + KL, hand-derived backward, Adam update of params/adam_m/adam_v in place.
- * elbo_out[0] <- negative inner ELBO (the value inner_elbo returns) evaluated
- * at the incoming params.  eps == NULL is invalid (use psvi_randn first). */
+ * elbo_out[0] (double, zeroed by the call) <- negative inner ELBO (the value
+ * inner_elbo returns) at the incoming params.  eps == NULL is invalid (draw
+ * it with psvi_randn, or pass the reference-order draws). */
 int psvi_inner_step(const psvi_plan* plan, const float* u, const int32_t* z,
                     const float* w, const float* eps, float* params,
                     float* adam_m, float* adam_v, const psvi_adam_hp* hp,
-                    float* elbo_out, void* ws, size_t ws_bytes, void* stream);
+                    double* elbo_out, void* ws, size_t ws_bytes, void* stream);
 
 /* Same objective without the update: grad_out (PARAM_COUNT floats) <- d elbo
- * / d params, elbo_out[0] <- elbo.  Used by the autograd.Function boundary.
- * include_kl = 0 drops the KL term (and its gradient). */
+ * / d params, elbo_out[0] (double, zeroed by the call) <- elbo.  Used by the
+ * autograd.Function boundary.  include_kl = 0 drops the KL term and its
+ * gradient. */
 int psvi_elbo_grad(const psvi_plan* plan, const float* u, const int32_t* z,
                    const float* w, const float* eps, const float* params,
-                   int32_t include_kl, float* elbo_out, float* grad_out,
+                   int32_t include_kl, double* elbo_out, float* grad_out,
                    void* ws, size_t ws_bytes, void* stream);
 
 /* ---- sharded phases (any world; the caller runs the collectives) ------------
  * MEANFIELD (sample-parallel, replicated params):
- *   acc (ACC_COUNT floats) <- [sum_m,s w NLL | sum_s dW | sum_s dW*eps] over
- *   this rank's samples;  caller all-reduces acc (sum);  update applies KL +
- *   Adam identically on every rank; elbo_out[0] <- full elbo. */
+ *   acc (ACC_COUNT floats, zeroed by the call) <- [sum_s dW | sum_s dW*eps]
+ *   over this rank's samples, nll_out[0] += their weighted NLL;  caller
+ *   all-reduces acc (sum);  update applies KL gradient + Adam identically on
+ *   every rank (grad_out != NULL: write the gradient instead), kl_out[0] +=
+ *   KL (nullable; count it on one rank). */
 int psvi_mf_phase_accumulate(const psvi_plan* plan, const float* u,
                              const int32_t* z, const float* w, const float* eps,
-                             const float* params, float* acc, void* stream);
+                             const float* params, float* acc, double* nll_out,
+                             void* stream);
 int psvi_mf_phase_update(const psvi_plan* plan, const float* acc, float* params,
                          float* adam_m, float* adam_v, const psvi_adam_hp* hp,
-                         float* elbo_out, float* grad_out, void* stream);
+                         double* kl_out, float* grad_out, int32_t include_kl,
+                         void* stream);
 
 /* FULLCOV (rows of L sharded, samples sharded):
  *   sample: x_shard[S][ROWS_LOCAL] <- mean + L eps for this rank's rows, all S
@@ -150,10 +162,10 @@ int psvi_mvn_phase_sample(const psvi_plan* plan, const float* eps,
                           const float* params, float* x_shard, void* stream);
 int psvi_mvn_phase_net(const psvi_plan* plan, const float* u, const int32_t* z,
                        const float* w, const float* x_recv, float* g_send,
-                       float* nll_out, void* stream);
+                       double* nll_out, void* stream);
 int psvi_mvn_phase_update(const psvi_plan* plan, const float* eps,
                           const float* g_shard, float* params, float* adam_m,
-                          float* adam_v, const psvi_adam_hp* hp, float* kl_out,
+                          float* adam_v, const psvi_adam_hp* hp, double* kl_out,
                           float* grad_out, int32_t include_kl, void* stream);
 
 /* ---- utilities ----------------------------------------------------------- */

@@ -128,6 +128,60 @@ def net_forward_backward(u, z, w, Ws, bs):
     return data, dWs, dbs
 
 
+def relu_margin(u, Ws, bs):
+    """Per-sample min over hidden pre-activations of |a| / (sum_i |h_i W_ji| + |b_j|):
+    how far each sample sits from a ReLU kink in units of its own fp32 rounding
+    scale.  Samples with a margin below ~1e-5 can legitimately flip a mask
+    between an fp32 and an fp64 evaluation."""
+    S = Ws[0].shape[0]
+    h = np.broadcast_to(u[None], (S,) + u.shape)
+    marg = np.full(S, np.inf)
+    for l in range(len(Ws) - 1):
+        a = np.einsum("smi,soi->smo", h, Ws[l]) + bs[l][:, None, :]
+        scale = np.einsum("smi,soi->smo", np.abs(h), np.abs(Ws[l])) + np.abs(bs[l])[:, None, :]
+        marg = np.minimum(marg, (np.abs(a) / np.maximum(scale, 1e-300)).reshape(S, -1).min(1))
+        h = np.maximum(a, 0.0)
+    return marg
+
+
+def mvn_split_x(layers, X):
+    """(S, n_tot) per-sample weight vectors -> per-layer W_s, b_s."""
+    Ws, bs, col = [], [], 0
+    S = X.shape[0]
+    for din, dout in layers:
+        n = din * dout + dout
+        Ws.append(X[:, col:col + din * dout].reshape(S, dout, din))
+        bs.append(X[:, col + din * dout:col + n])
+        col += n
+    return Ws, bs
+
+
+def mvn_grad_from_G(layers, params, G, eps, S, prior_sd=1.0):
+    """Update-phase restatement: gradient of the full-cov parameters from the
+    per-sample weight gradients G (S, n_tot)."""
+    params = np.asarray(params, np.float64)
+    eps = np.asarray(eps, np.float64)
+    G = np.asarray(G, np.float64)
+    s0 = float(prior_sd)
+    grad = np.zeros_like(params)
+    po = eo = col = 0
+    for din, dout in layers:
+        n = mvn_n(din, dout)
+        nc = mvn_ncorr(n)
+        mean, sd, corr = params[po:po + n], params[po + n:po + 2 * n], params[po + 2 * n:po + 2 * n + nc]
+        E = eps[eo:eo + S * n].reshape(S, n)
+        Gl = G[:, col:col + n]
+        spd = softplus(sd)
+        grad[po:po + n] = Gl.sum(0) + mean / s0 ** 2
+        grad[po + n:po + 2 * n] = ((Gl * E).sum(0) + spd / s0 ** 2 - 1.0 / spd) * sigmoid(sd)
+        r, c = tril_rows_cols(n)
+        grad[po + 2 * n:po + 2 * n + nc] = (Gl.T @ E)[r, c] + corr / s0 ** 2
+        po += 2 * n + nc
+        eo += S * n
+        col += n
+    return grad
+
+
 # --------------------------------------------------------------- Adam steps
 def adam_higher(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     """robust_higher DifferentiableAdam._update (optim.py:318-367), t 1-based."""

@@ -17,7 +17,14 @@ if [[ $STEPS == *smoke* ]]; then
   echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
   ok $rc || exit $rc
 fi
-if [[ $STEPS == *bench* ]]; then
+if [[ $STEPS == *kbench* ]]; then
+  for c in ${KB_CFGS:-c3}; do
+    timeout -k 10 300 python tools/kernel_bench.py $c ${KB_ITERS:-200} >> gpurun_out/kbench.log 2>&1; rc=$?
+    echo "kbench $c rc=$rc"; tail -1 gpurun_out/kbench.log
+    ok $rc || exit $rc
+  done
+fi
+if [[ $STEPS == *bench* && $STEPS != *kbench* ]] || [[ $STEPS == *,bench* ]]; then
   timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?
   echo "bench rc=$rc"; tail -2 gpurun_out/bench.log
   ok $rc || exit $rc
