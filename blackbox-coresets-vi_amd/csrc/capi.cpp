@@ -18,6 +18,10 @@
 namespace psvi {
 size_t net_plan_geometry(psvi_plan& p);  // kernels_net.hip
 void net_set_lds_limit();                // kernels_net.hip
+extern int g_net_ablation;               // kernels_net.hip
+extern unsigned long long* g_net_stamps; // kernels_net.hip
+extern int g_upd_ablation;               // kernels_mvn.hip
+extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
 }  // namespace psvi
 
 using namespace psvi;
@@ -134,12 +138,24 @@ int build_plan(psvi_plan& p) {
     net_plan_geometry(p);
     if (p.net_lds > 160 * 1024)
         return fail(PSVI_EUNSUP, "layer too wide for the per-sample LDS network kernel");
+    // the kernels address parameters, eps and the x / g shards with 32-bit offsets
+    const int64_t kMaxOff = (int64_t(1) << 31) - 4096;
+    if (p.P > kMaxOff || p.Peps > kMaxOff || (int64_t)d.S * p.rows_tot[0] > kMaxOff ||
+        (int64_t)d.S * p.n_tot > kMaxOff)
+        return fail(PSVI_EUNSUP, "buffers beyond 2^31 floats are not supported");
 
     const int S = d.S, r = p.rank;
     if (p.family == PSVI_FAMILY_FULLCOV) {
         std::vector<FwdItem> fwd;
-        std::vector<BwdTile> bwd;
-        std::vector<DiagBlock> diag;
+        std::vector<UpdChunk> upd;
+        // c-blocks per update chunk: about two chunks per CU slot (256 CUs x
+        // 2 resident workgroups), at least one
+        int tiles = 0;
+        for (int l = 0; l < p.L; ++l) {
+            const int lo = p.row_lo[r][l], hi = p.row_hi[r][l];
+            for (int b = lo / 64; 64 * b < hi; ++b) tiles += b + 1;
+        }
+        const int ch = std::max(1, (tiles + 511) / 512);
         for (int l = 0; l < p.L; ++l) {
             const int n = p.lay[l].n, lo = p.row_lo[r][l], hi = p.row_hi[r][l];
             const int xc = p.xcol_l[r][l];
@@ -156,25 +172,27 @@ int build_plan(psvi_plan& p) {
                     fwd.push_back(FwdItem{l, r0, r1, k0, k1, xc + (r0 - lo)});
                 }
             }
-            const int thi = std::min(hi, n - 1);
-            for (int r0 = lo; r0 < thi; r0 += 64) {
-                const int cmax = std::min(r0 + 63, n - 2);  // c < r <= cmax
-                for (int c0 = 0; c0 < cmax; c0 += 64)
-                    bwd.push_back(BwdTile{l, r0, c0, lo, thi, xc - lo});
+            // bands of 64 absolute rows; c-blocks 0..b, the last one diagonal
+            for (int b = lo / 64; 64 * b < hi; ++b) {
+                for (int k0 = 0; k0 <= b; k0 += ch) {
+                    const int k1 = std::min(b + 1, k0 + ch);
+                    upd.push_back(UpdChunk{l, 64 * b, k0, k1, lo, hi, xc - lo, k1 == b + 1});
+                }
             }
-            for (int r0 = lo; r0 < hi; r0 += 64)
-                diag.push_back(DiagBlock{l, r0, hi, xc - lo});
         }
         // longest forward items first
         std::stable_sort(fwd.begin(), fwd.end(), [](const FwdItem& a, const FwdItem& b) {
             return (a.k1 - a.k0) > (b.k1 - b.k0);
         });
         p.h_fwd = fwd;
-        p.h_bwd = bwd;
-        p.h_diag = diag;
+        // bigger chunks first (diagonal chunks carry the mean / sd work)
+        std::stable_sort(upd.begin(), upd.end(), [](const UpdChunk& a, const UpdChunk& b) {
+            return (a.k1 - a.k0) + a.diag > (b.k1 - b.k0) + b.diag;
+        });
+        p.h_upd = upd;
+        p.upd_tiles = tiles;
         p.n_fwd = (int)fwd.size();
-        p.n_bwd = (int)bwd.size();
-        p.n_diag = (int)diag.size();
+        p.n_upd = (int)upd.size();
         const size_t xs = sizeof(float) * (size_t)S * p.rows_tot[r];
         p.ws_bytes = align256(xs) * 2 + 256;
     } else {
@@ -191,6 +209,22 @@ extern "C" {
 
 const char* psvi_last_error(void) { return g_err.c_str(); }
 const char* psvi_version(void) { return "psvi_hip 0.1.0 (gfx950)"; }
+
+int psvi_debug_set(int32_t key, int32_t value) {
+    switch (key) {
+        case PSVI_DBG_NET_ABLATION: g_net_ablation = value; return 0;
+        case PSVI_DBG_UPD_ABLATION: g_upd_ablation = value; return 0;
+        default: return fail(PSVI_EINVAL, "unknown debug key");
+    }
+}
+
+int psvi_debug_set_ptr(int32_t key, void* ptr) {
+    switch (key) {
+        case PSVI_DBG_NET_STAMPS: g_net_stamps = (unsigned long long*)ptr; return 0;
+        case PSVI_DBG_UPD_STAMPS: g_upd_stamps = (unsigned long long*)ptr; return 0;
+        default: return fail(PSVI_EINVAL, "unknown debug key");
+    }
+}
 
 int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int32_t rank,
                      psvi_plan** out) {
@@ -215,8 +249,7 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
     int rc = build_plan(*p);
     if (!rc && have_dev) {
         // the only device allocations of the library: immutable work lists
-        if (!(rc = upload(p->h_fwd, &p->d_fwd)) && !(rc = upload(p->h_bwd, &p->d_bwd)))
-            rc = upload(p->h_diag, &p->d_diag);
+        if (!(rc = upload(p->h_fwd, &p->d_fwd))) rc = upload(p->h_upd, &p->d_upd);
         p->on_device = rc == 0;
     }
     if (rc) {
@@ -230,8 +263,7 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
 int psvi_plan_destroy(psvi_plan* p) {
     if (!p) return 0;
     if (p->d_fwd) (void)hipFree(p->d_fwd);
-    if (p->d_bwd) (void)hipFree(p->d_bwd);
-    if (p->d_diag) (void)hipFree(p->d_diag);
+    if (p->d_upd) (void)hipFree(p->d_upd);
     delete p;
     return 0;
 }

@@ -120,16 +120,16 @@ __global__ __launch_bounds__(256) void mvn_fwd_kernel(FwdArgs a) {
 }
 
 // ---------------------------------------------------------------- backward
-constexpr int BT = 64;    // output tile 64 (rows r) x 64 (cols c)
-constexpr int BKS = 128;  // samples staged per pass (K of the dL GEMM); S <= 128: one pass
+constexpr int UB = 64;    // band rows = c-block columns
+constexpr int USB = 128;  // samples staged per pass (K of the dL GEMM)
+constexpr int ULD = 68;   // LDS row stride: 16-byte aligned rows for float4 stores
 
 struct UpdArgs {
-    const BwdTile* tiles;
-    const DiagBlock* diag;
-    int n_tiles, n_diag;
+    const UpdChunk* chunks;
     const float* eps;
     const float* g;    // g_shard [S][ldg]
     int ldg, S;
+    int64_t g_total, e_total;  // floats in g_shard / eps (load guards)
     float* params;
     float* m;
     float* v;
@@ -137,10 +137,41 @@ struct UpdArgs {
     double* kl_out;    // nullable
     int64_t pcount;    // parameter vector length
     int include_kl;
+    int abl;                       // diagnostics ablation mask (0 in production)
+    unsigned long long* stamps;    // diagnostics: 16 slots per workgroup (nullptr in production)
     float inv_s0sq, log_s0;
     AdamC adam;
     MvnLayerArgs lay[kMaxL];
 };
+
+// Branch-free 16-byte loads.  gfx950 global loads need only 4-byte
+// alignment, so a float4 may start at any float offset; the offset is clamped
+// into the buffer [lo, hi) (hi - lo >= 4) so the load is unconditional (loads
+// under divergent branches make the compiler's vmcnt bookkeeping fall back to
+// vmcnt(0), which would drain every prefetch), and fix4 -- applied where the
+// value is consumed -- shifts the clamped vector back, zeroing elements
+// outside [lo, hi).  Offsets are 32-bit (the plan rejects larger buffers).
+__device__ __forceinline__ int clamp4(int off, int lo, int hi) {
+    return off < lo ? lo : (off > hi - 4 ? hi - 4 : off);
+}
+__device__ __forceinline__ float4 ld4u(const float* base, int off, int lo, int hi) {
+    return *reinterpret_cast<const float4*>(base + clamp4(off, lo, hi));
+}
+__device__ __forceinline__ float4 fix4(float4 v, int off, int lo, int hi) {
+    const int d = off - clamp4(off, lo, hi);
+    if (d == 0) return v;  // VALU-only branch
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = i + d;
+        r[i] = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : k == 3 ? x[3] : 0.f;
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+}
+__device__ __forceinline__ float f4get(const float4& v, int i) {
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
 
 template <bool GRAD>
 __device__ __forceinline__ void upd_elem(const UpdArgs& a, int64_t pidx, float gval) {
@@ -155,149 +186,280 @@ __device__ __forceinline__ void upd_elem(const UpdArgs& a, int64_t pidx, float g
     }
 }
 
-// Tiles: dL[r0:r0+64, c0:c0+64] = G^T eps over all S samples (4 waves, 32x32
-// each), then the fused corr update.  Memory schedule per tile: issue the
-// G / eps loads of the first sample chunk, THEN the epilogue's corr/m/v loads
-// (vmcnt retires in order, so the GEMM operands are not held behind them),
-// stage the chunk in LDS, run the MFMAs while the corr/m/v loads land, update.
-// Diag blocks (blockIdx < n_diag, scheduled first): mean and sd of 64 rows each.
-template <bool GRAD>
-__global__ __launch_bounds__(256) void mvn_update_kernel(UpdArgs a) {
-    __shared__ float Gs[BKS][BT + 1];
-    __shared__ float Xs[BKS][BT + 1];
-    __shared__ float red[8];
+#define UPD_STAMP(k, val)                                                          \
+    do {                                                                           \
+        if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 16 + (k)] = (val); \
+    } while (0)
+
+// One chunk: for each of its c-blocks, dL^T[c][r] = sum_s eps[s][c] G[s][r]
+// (v_mfma_f32_32x32x2_f32, 4 waves = 2 x 2 sub-tiles of 32 x 32), then
+//   corr <- Adam(corr, dL + corr/s0^2)         (or grad_out in GRAD mode).
+// The accumulator tile goes through LDS (into the eps stage, free after the
+// MFMAs) so the corr / m / v / grad traffic moves in 256-byte row runs, four
+// rows per wave instruction.
+// Pipeline: after each staging barrier the next step's operand loads (eps,
+// and G when S > 128; clamped to the last step rather than skipped) and, on a
+// c-block's last sample pass, its corr/m/v loads are issued; the MFMAs run
+// while they land.  Every global load is unconditional: a load under a
+// branch makes the compiler's vmcnt bookkeeping fall back to vmcnt(0).
+// The diagonal c-block (columns = the band's rows) also yields sum_s G and
+// sum_s G*eps per row: the mean / sd update.
+constexpr int TLD = 68;   // LDS stride of the transposed accumulator tile
+struct UpdShared {
+    float Gs[USB * ULD];
+    float Es[USB * ULD];
+    float red[2 * 4 * 64];
+};
+
+template <bool GRAD, bool MULTI>
+__device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, UpdShared& sh) {
+    float* Gs = sh.Gs;
+    float* Es = sh.Es;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
-    float klp = 0.f;
-    if ((int)blockIdx.x >= a.n_diag) {
-        const BwdTile t = a.tiles[(int)blockIdx.x - a.n_diag];
-        const int n = a.lay[t.layer].n;
-        const float* E = a.eps + a.lay[t.layer].eoff;
-        const int64_t corr_off = a.lay[t.layer].poff + 2 * n;
-        const int wr = wv >> 1, wc = wv & 1;
-        const int c = t.c0 + 32 * wc + l32;
-        const int rb = t.r0 + 32 * wr + 4 * h;
-        const int cc = tid & 63, s0 = tid >> 6;   // staging: column, first sample row
-        // Out-of-tile rows / columns of G and eps only feed dL entries the
-        // epilogue masks, so staging needs no predicate; rows past S read 0.
-        const rsrc_t rsG = make_rsrc(a.g, (int64_t)a.S * a.ldg * 4);
-        const rsrc_t rsE = make_rsrc(E, (int64_t)a.S * n * 4);
-        const rsrc_t rsP = make_rsrc(a.params, a.pcount * 4);
-        const rsrc_t rsM = make_rsrc(a.m, GRAD ? 0 : a.pcount * 4);
-        const rsrc_t rsV = make_rsrc(a.v, GRAD ? 0 : a.pcount * 4);
-        const uint32_t gcol = (uint32_t)(t.xcol + t.r0 + cc) * 4;
-        const uint32_t xcol = (uint32_t)(t.c0 + cc) * 4;
-        floatx16 acc;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int n = a.lay[ch.layer].n;
+    const int eoff = (int)a.lay[ch.layer].eoff;
+    const float* E = a.eps + eoff;  // [S][n]; the whole eps buffer is [-eoff, e_rem)
+    const int e_rem = (int)a.e_total - eoff;
+    const int g_total = (int)a.g_total, pcount = (int)a.pcount;
+    const int poff = (int)a.lay[ch.layer].poff, corr_off = poff + 2 * n;
+    const int np = MULTI ? (a.S + USB - 1) / USB : 1;
+    const int nt = ch.k1 - ch.k0;
+    const int kd = ch.diag ? ch.r0 / UB - ch.k0 : -1;  // diagonal c-block index in the chunk
+
+    // staging / epilogue map: 16 lanes x float4 = one 64-column row, rows srow + 16 j
+    const int col4 = tid & 15, srow = tid >> 4;
+    const int gcol = ch.xcol + ch.r0 + 4 * col4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 greg[8], ereg[8];
+    // sample row s is clamped to S-1 (rows >= S are zeroed at the LDS write)
+    auto goff = [&](int s) { return min(s, a.S - 1) * a.ldg + gcol; };
+    auto eofs = [&](int s, int ti) { return min(s, a.S - 1) * n + (ch.k0 + ti) * UB + 4 * col4; };
+    auto load_G = [&](int pi) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) greg[j] = ld4u(a.g, goff(pi * USB + srow + 16 * j), 0, g_total);
+    };
+    auto load_E = [&](int ti, int pi) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            ereg[j] = ld4u(E, eofs(pi * USB + srow + 16 * j, ti), -eoff, e_rem);
+    };
+    auto stage = [&](bool withG, int ti, int pi) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int o = (srow + 16 * j) * ULD + 4 * col4;
+            const int sr = pi * USB + srow + 16 * j;
+            const bool live = sr < a.S && !(a.abl & 1);
+            if (withG)
+                *reinterpret_cast<float4*>(&Gs[o]) = live ? fix4(greg[j], goff(sr), 0, g_total) : z4;
+            *reinterpret_cast<float4*>(&Es[o]) =
+                live ? fix4(ereg[j], eofs(sr, ti), -eoff, e_rem) : z4;
+        }
+    };
+
+    // epilogue rows: r_j = r0 + srow + 16 j, columns c0 + 4 col4 + (0..3)
+    int rowp[4];
+    bool rown[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = ch.r0 + srow + 16 * j;
+        rown[j] = r >= ch.rlo && r < ch.rhi && r >= 1 && r <= n - 2;
+        rowp[j] = corr_off + (int)((int64_t)r * (r - 1) / 2);
+    }
+    float4 pq[4], mq[4], vq[4];
+    auto load_pmv = [&](int ti) {
+        const int cl = (ch.k0 + ti) * UB + 4 * col4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // rows off the band's corr rows load something valid, never stored
+            pq[j] = ld4u(a.params, rowp[j] + cl, 0, pcount);
+            if (!GRAD) {
+                mq[j] = ld4u(a.m, rowp[j] + cl, 0, pcount);
+                vq[j] = ld4u(a.v, rowp[j] + cl, 0, pcount);
+            }
+        }
+    };
+
+    floatx16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    float dgm = 0.f, dgs = 0.f, klp = 0.f;
+
+    auto compute = [&](int ti, int pi) {
+        const int kend = (a.abl & 2) ? 0 : min(USB, a.S - pi * USB);
+        if (ti == kd) {
+            // diagonal c-block: column j of Es is row r0 + j of the band
+            for (int s = 32 * wv; s < 32 * wv + 32 && s < kend; ++s) {
+                const float gv = Gs[s * ULD + lane];
+                dgm += gv;
+                dgs = fmaf(gv, Es[s * ULD + lane], dgs);
+            }
+        }
+        // 16 samples per group (rows past S are staged as zeros up to USB)
+        const float* Ea = Es + h * ULD + 32 * wc + l32;
+        const float* Gb = Gs + h * ULD + 32 * wr + l32;
+        for (int kk = 0; kk < kend; kk += 16) {
+            float av[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                av[u] = Ea[(kk + 2 * u) * ULD];
+                bv[u] = Gb[(kk + 2 * u) * ULD];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+        }
+    };
+
+    // call after a barrier that ends every wave's reads of Es
+    auto epilogue = [&](int ti) {
+        // D[i = c][j = r]: j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h  ->  T[r][c] in Es
+        float* T = Es;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(&T[(32 * wr + l32) * TLD + 32 * wc + 8 * g + 4 * h]) =
+                make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-        float pq[16], mq[16], vq[16];
-        for (int sb = 0; sb < a.S; sb += BKS) {
-            float greg[BKS / 4], xreg[BKS / 4];
+        __syncthreads();
+        const int cb = (ch.k0 + ti) * UB + 4 * col4;
 #pragma unroll
-            for (int j = 0; j < BKS / 4; ++j) {
-                const uint32_t s = sb + s0 + 4 * j;
-                greg[j] = bload(rsG, gcol + s * (uint32_t)a.ldg * 4);
-                xreg[j] = bload(rsE, xcol + s * (uint32_t)n * 4);
+        for (int j = 0; j < 4; ++j) {
+            const int r = ch.r0 + srow + 16 * j;
+            if (!rown[j] || cb >= r || (a.abl & 8)) continue;
+            const int o = rowp[j] + cb;
+            const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
+            const float4 p4 = (a.abl & 4) ? z4 : fix4(pq[j], o, 0, pcount);
+            float4 m4 = z4, v4 = z4;
+            if (!GRAD) {
+                m4 = (a.abl & 4) ? z4 : fix4(mq[j], o, 0, pcount);
+                v4 = (a.abl & 4) ? z4 : fix4(vq[j], o, 0, pcount);
             }
-            if (sb == 0) {
+            float pn[4], mn[4], vn[4];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int r = rb + (q & 3) + 8 * (q >> 2);
-                    const bool ok = r >= t.rlo && r < t.rhi && c < r;
-                    const uint32_t off =
-                        ok ? (uint32_t)((corr_off + (int64_t)r * (r - 1) / 2 + c) * 4) : kOOB;
-                    pq[q] = bload(rsP, off);
-                    if (!GRAD) {
-                        mq[q] = bload(rsM, off);
-                        vq[q] = bload(rsV, off);
-                    }
+            for (int i = 0; i < 4; ++i) {
+                const float p = f4get(p4, i);
+                klp += cb + i < r ? p * p : 0.f;
+                const float gval = a.include_kl ? f4get(d4, i) + p * a.inv_s0sq : f4get(d4, i);
+                if (GRAD) {
+                    pn[i] = gval;
+                } else {
+                    float mm = f4get(m4, i), vv = f4get(v4, i);
+                    pn[i] = adam_apply_fast(a.adam, p, gval, mm, vv);
+                    mn[i] = mm;
+                    vn[i] = vv;
+                }
+            }
+            float* dp = GRAD ? a.grad_out : a.params;
+            if (cb + 3 < r) {
+                *reinterpret_cast<float4*>(dp + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
+                if (!GRAD) {
+                    *reinterpret_cast<float4*>(a.m + o) = make_float4(mn[0], mn[1], mn[2], mn[3]);
+                    *reinterpret_cast<float4*>(a.v + o) = make_float4(vn[0], vn[1], vn[2], vn[3]);
                 }
             } else {
-                __syncthreads();  // previous chunk fully consumed
-            }
 #pragma unroll
-            for (int j = 0; j < BKS / 4; ++j) {
-                Gs[s0 + 4 * j][cc] = greg[j];
-                Xs[s0 + 4 * j][cc] = xreg[j];
-            }
-            __syncthreads();
-            const int kend = min(BKS, a.S - sb);
-            for (int kk = 0; kk < kend; kk += 2) {
-                const float av = Gs[kk + h][32 * wr + l32];
-                const float bv = Xs[kk + h][32 * wc + l32];
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-            }
-        }
-        // D[i = r][j = c]: j = lane&31, i = (q&3) + 8(q>>2) + 4h
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int r = rb + (q & 3) + 8 * (q >> 2);
-            if (r >= t.rlo && r < t.rhi && c < r) {
-                const int64_t pidx = corr_off + (int64_t)r * (r - 1) / 2 + c;
-                const float p = pq[q];
-                klp += p * p;
-                const float gval = a.include_kl ? acc[q] + p * a.inv_s0sq : acc[q];
-                if (GRAD) {
-                    a.grad_out[pidx] = gval;
-                } else {
-                    float mm = mq[q], vv = vq[q];
-                    a.params[pidx] = adam_apply(a.adam, p, gval, mm, vv);
-                    a.m[pidx] = mm;
-                    a.v[pidx] = vv;
+                for (int i = 0; i < 3; ++i) {
+                    if (cb + i < r) {
+                        dp[o + i] = pn[i];
+                        if (!GRAD) {
+                            a.m[o + i] = mn[i];
+                            a.v[o + i] = vn[i];
+                        }
+                    }
                 }
             }
         }
-        klp *= 0.5f * a.inv_s0sq;
-    } else {
-        // 64 rows per block; the 4 waves split the samples, partial sums meet
-        // in LDS (reusing the staging arrays); loads batched 8 deep.
-        const DiagBlock db = a.diag[blockIdx.x];
-        const int n = a.lay[db.layer].n;
-        const float* E = a.eps + a.lay[db.layer].eoff;
-        const int r = db.r0 + (tid & 63);
-        const bool rv = r < db.rhi;
-        const int rr = rv ? r : db.r0;
-        const rsrc_t rsG = make_rsrc(a.g, (int64_t)a.S * a.ldg * 4);
-        const rsrc_t rsE = make_rsrc(E, (int64_t)a.S * n * 4);
-        const uint32_t gofs = (uint32_t)(db.xcol + rr) * 4, eofs = (uint32_t)rr * 4;
-        float gm = 0.f, gs = 0.f;
-        for (int s0 = wv; s0 < a.S; s0 += 32) {
-            float gv[8], ev[8];
+    };
+
+    if (!MULTI) {
+        // all samples in one pass: the band's G slice stays in LDS
+        load_G(0);
+        load_E(0, 0);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t s = s0 + 4 * k;   // past S: range check -> 0
-                gv[k] = bload(rsG, gofs + s * (uint32_t)a.ldg * 4);
-                ev[k] = bload(rsE, eofs + s * (uint32_t)n * 4);
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                gm += gv[k];
-                gs = fmaf(gv[k], ev[k], gs);
-            }
+        for (int j = 0; j < 8; ++j) {  // G slice once (its registers die here)
+            const int sr = srow + 16 * j;
+            *reinterpret_cast<float4*>(&Gs[sr * ULD + 4 * col4]) =
+                sr < a.S && !(a.abl & 1) ? fix4(greg[j], goff(sr), 0, g_total) : z4;
         }
-        Gs[wv][tid & 63] = gm;
-        Xs[wv][tid & 63] = gs;
+        for (int ti = 0; ti < nt; ++ti) {
+            stage(false, ti, 0);
+            __syncthreads();
+            if (ti == 0) UPD_STAMP(1, __builtin_amdgcn_s_memtime());
+            load_E(min(ti + 1, nt - 1), 0);
+            load_pmv(ti);
+            compute(ti, 0);
+            __syncthreads();  // every wave done with Es: it takes the accumulator tile
+            epilogue(ti);
+            __syncthreads();  // tile read before the next staging overwrites Es
+        }
+    } else {
+        load_G(0);
+        load_E(0, 0);
+        for (int ti = 0; ti < nt; ++ti) {
+            for (int pi = 0; pi < np - 1; ++pi) {
+                stage(true, ti, pi);
+                __syncthreads();
+                load_G(pi + 1);
+                load_E(ti, pi + 1);
+                compute(ti, pi);
+                __syncthreads();
+            }
+            stage(true, ti, np - 1);
+            __syncthreads();
+            load_G(0);
+            load_E(min(ti + 1, nt - 1), 0);
+            load_pmv(ti);
+            compute(ti, np - 1);
+            __syncthreads();
+            epilogue(ti);
+            __syncthreads();
+        }
+    }
+    UPD_STAMP(2, __builtin_amdgcn_s_memtime());
+    klp *= 0.5f * a.inv_s0sq;
+    if (ch.diag) {
+        sh.red[wv * 64 + lane] = dgm;
+        sh.red[256 + wv * 64 + lane] = dgs;
         __syncthreads();
-        if (tid < 64 && rv) {
-            gm = Gs[0][tid] + Gs[1][tid] + Gs[2][tid] + Gs[3][tid];
-            gs = Xs[0][tid] + Xs[1][tid] + Xs[2][tid] + Xs[3][tid];
-            const int64_t pm = a.lay[db.layer].poff + r, ps = pm + n;
+        const int rr = ch.r0 + tid;
+        if (tid < 64 && rr >= ch.rlo && rr < ch.rhi && rr < n) {
+            const float* red = sh.red;
+            const float gm = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+            const float gs = red[256 + tid] + red[320 + tid] + red[384 + tid] + red[448 + tid];
+            const int pm = poff + rr, ps = pm + n;
             const float mu = a.params[pm], sdr = a.params[ps];
             const float sp = softplus_f(sdr), sg = sigmoid_f(sdr);
             float gmean = gm, gsd = gs * sg;
             if (a.include_kl) {
                 gmean += mu * a.inv_s0sq;
                 gsd += (sp * a.inv_s0sq - 1.f / sp) * sg;
-                klp = a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
+                klp += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
             }
             upd_elem<GRAD>(a, pm, gmean);
             upd_elem<GRAD>(a, ps, gsd);
         }
+        __syncthreads();
     }
     if (a.kl_out && a.include_kl) {
-        const float tot = block_sum(klp, red);
+        const float tot = block_sum(klp, sh.red);
         if (tid == 0) atomicAdd(a.kl_out, (double)tot);
     }
 }
+
+template <bool GRAD, bool MULTI>
+__global__ __launch_bounds__(256, 2) void mvn_update_kernel(UpdArgs a) {
+    __shared__ __attribute__((aligned(16))) UpdShared sh;
+    UPD_STAMP(0, __builtin_amdgcn_s_memtime());
+    UPD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+    UPD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
+    const UpdChunk ch = a.chunks[blockIdx.x];
+    upd_chunk<GRAD, MULTI>(a, ch, sh);
+    UPD_STAMP(3, __builtin_amdgcn_s_memtime());
+}
+
+int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
+unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
 
 static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
     for (int l = 0; l < p.L; ++l) {
@@ -328,32 +490,37 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl, hipStream_t st) {
     UpdArgs a{};
-    a.tiles = p.d_bwd;
-    a.diag = p.d_diag;
-    a.n_tiles = p.n_bwd;
-    a.n_diag = p.n_diag;
+    a.chunks = p.d_upd;
     a.eps = eps;
     a.g = g_shard;
     a.ldg = p.rows_tot[p.rank];
     a.S = p.d.S;
+    a.g_total = (int64_t)p.d.S * p.rows_tot[p.rank];
+    a.e_total = p.Peps;
     a.params = params;
     a.m = m;
     a.v = v;
     a.grad_out = grad_out;
     a.kl_out = kl_out;
     a.include_kl = include_kl;
+    a.abl = g_upd_ablation;
+    a.stamps = g_upd_stamps;
     a.pcount = p.P;
     const float s0 = p.d.prior_sd;
     a.inv_s0sq = 1.f / (s0 * s0);
     a.log_s0 = logf(s0);
     if (hp) a.adam = make_adam(hp);
     fill_layers(p, a.lay);
-    const int nb = p.n_bwd + p.n_diag;
-    if (nb == 0) return hipSuccess;
-    if (grad_out)
-        hipLaunchKernelGGL(mvn_update_kernel<true>, dim3(nb), dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL(mvn_update_kernel<false>, dim3(nb), dim3(256), 0, st, a);
+    if (p.n_upd == 0) return hipSuccess;
+    const dim3 grid(p.n_upd), block(256);
+    const bool multi = a.S > USB;  // more samples than one LDS pass holds
+    if (grad_out) {
+        if (multi) hipLaunchKernelGGL((mvn_update_kernel<true, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((mvn_update_kernel<true, false>), grid, block, 0, st, a);
+    } else {
+        if (multi) hipLaunchKernelGGL((mvn_update_kernel<false, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((mvn_update_kernel<false, false>), grid, block, 0, st, a);
+    }
     return hipGetLastError();
 }
 

@@ -11,24 +11,36 @@
 //
 // One workgroup = one MC sample x one chunk of pseudopoints.  Everything the
 // sample needs (its weights, the pseudo-input chunk, every layer's
-// activations) is staged in LDS with odd row strides; the per-sample
-// contractions run on fp32 MFMA (16x16x4) tiles.
-//  MEANFIELD: W_s = mu + softplus(rho) * eps formed in LDS; per-sample dW and
-//             dW*eps go to the [sum_s dW | sum_s dW*eps] accumulators
-//             (fp32 atomics, S adders per address).
-//  FULLCOV:   W_s gathered from x_recv (blocked by source rank); dW written
-//             to g_send in the same blocked layout (atomics when the sample's
-//             pseudopoints are split over several workgroups).
+// activations, two gradient buffers, one dW accumulation tile) lives in LDS
+// with odd row strides.  The contractions run on fp32 MFMA (16x16x4) "units"
+// of 16 rows x 32 columns with software-pipelined operand loads; units are
+// dealt round-robin to the waves.  Backward, per layer, in ONE phase:
+//   dW_l = g_l^T [h_{l-1} | 1]  (the ones column makes the last output column
+//          the bias gradient), K = pseudopoints split over waves, partial
+//          tiles summed with LDS float atomics into the dW tile;
+//   g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0]  into the other gradient buffer;
+// then the dW tile leaves LDS as contiguous rows:
+//  MEANFIELD: [sum_s dW | sum_s dW*eps] accumulators (fp32 atomics, S adders);
+//  FULLCOV:   g_send in the blocked-by-source-rank layout (plain stores, or
+//             atomics when a sample's pseudopoints span several workgroups).
+#include <algorithm>
+
 #include "psvi_internal.hpp"
 
 namespace psvi {
 
 struct NetArgs {
     int L, M, mc, S_total, s_goff, atomic_g;
+    int abl;  // diagnostics ablation mask (0 in production): 1 loads, 2 fwd
+              // GEMMs, 4 NLL, 8 bwd GEMMs, 16 global dW writes,
+              // 128 g-propagation GEMMs
+    unsigned long long* stamps;  // diagnostics: s_memtime per phase (nullptr in production)
     int din[kMaxL], dout[kMaxL], woff[kMaxL];
     // LDS carve (float offsets) and row strides
     int lw[kMaxL], ldw[kMaxL], lb[kMaxL], le[kMaxL], leb[kMaxL], la[kMaxL], lda[kMaxL];
-    int lu, ldu, lred;
+    int lu, ldu, lred, lg0, lg1, ldgb, ldwt, lds_f4;
+    int lstage_f4;                // float4 index where the late regions (and the DMA stage) start
+    int stage_off[kMaxWorld], stage_u;  // DMA stage: per-source x rows, then the u chunk
     const float* u;
     const int32_t* z;
     const float* w;
@@ -50,67 +62,141 @@ struct NetArgs {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// C[p][q] = sum_k A(p,k) B(q,k), A(p,k)=A[p*sap+k*sak], B(q,k)=B[q*sbq+k*sbk],
-// all operands in LDS.  16x16 output tiles on v_mfma_f32_16x16x4_f32 (exact
-// fp32), dealt round-robin to the workgroup's waves; lane l feeds
-// A[p0 + (l&15)][k + (l>>4)] and B[q0 + (l&15)][k + (l>>4)] and holds
-// D[p0 + 4(l>>4) + r][q0 + (l&15)], r = 0..3.  Out-of-range rows / k read 0.
-// (LDS reads are predicated selects, not branches: LDS, unlike VMEM, has no
-// in-order counter to drain.)
+// One MFMA work unit of C[p][q] = sum_k A(p,k) B(q,k) with
+// A(p,k) = A[p*sap + k*sak], B(q,k) = B[q*sbq + k*sbk] in LDS: rows
+// [p0, p0+16) x columns [q0, q0+32) (two 16x16 tiles on v_mfma_f32_16x16x4_f32,
+// exact fp32, two independent accumulator chains sharing the A fragment),
+// k in [k0, k0 + 16*ceil((k1-k0)/16)).  Lane l feeds A[p0+(l&15)][k+(l>>4)],
+// B[q+(l&15)][k+(l>>4)] and holds D[p0+4(l>>4)+r][q+(l&15)].
+// No masks: the LDS layout (net_lds_floats) zero-fills and pads every
+// operand so that any k >= k1 meets a zero in A or B, and rows / columns
+// past P / Q only feed outputs the epilogue drops.  The next 16-k group's
+// operands are read before the current group's MFMAs.
+template <int NQ, bool RELU_A, bool RELU_B, class Epi>
+__device__ __forceinline__ void gemm_unit(int P, int Q, int k0, int k1, int p0, int q0,
+                                          const float* __restrict__ A, int sap, int sak,
+                                          const float* __restrict__ B, int sbq, int sbk,
+                                          Epi epi) {
+    const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+    const float* Ap = A + (p0 + i16) * sap + k4 * sak;
+    const float* Bp = B + (q0 + i16) * sbq + k4 * sbk;
+    floatx4 acc[NQ];
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float a[4], b[NQ][4];
+    auto load = [&](int kb, float (&x)[4], float (&y)[NQ][4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int kk = kb + 4 * u;
+            x[u] = Ap[kk * sak];
+            if (RELU_A) x[u] = fmaxf(x[u], 0.f);
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) {
+                y[c][u] = Bp[16 * c * sbq + kk * sbk];
+                if (RELU_B) y[c][u] = fmaxf(y[c][u], 0.f);
+            }
+        }
+    };
+    if (k0 < k1) load(k0, a, b);
+    for (int kb = k0; kb < k1; kb += 16) {  // wave-uniform
+        float na[4], nb[NQ][4];
+        if (kb + 16 < k1) load(kb + 16, na, nb);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int c = 0; c < NQ; ++c)
+                acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[c][u], acc[c], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[u] = na[u];
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) b[c][u] = nb[c][u];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int pp = p0 + 4 * k4 + r;
+        if (pp < P) {
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) {
+                const int q = q0 + 16 * c + i16;
+                if (q < Q) epi(pp, q, acc[c][r]);
+            }
+        }
+    }
+}
+
+// Degenerate shapes (a side < 8, or K <= 4: the classifier layer) on VALU.
+// K >= 16: one output per 16-lane group, lanes split k, xor-shuffle reduce;
+// short K: one output per thread.
 template <bool RELU_A, bool RELU_B, class Epi>
-__device__ __forceinline__ void lds_gemm(int P, int Q, int K, const float* __restrict__ A,
-                                         int sap, int sak, const float* __restrict__ B,
-                                         int sbq, int sbk, Epi epi) {
-    // Work unit = one 16-row block of P x TWO adjacent 16-column blocks of Q:
-    // two independent accumulator chains (hides the 40-cycle dependent
-    // latency of 16x16x4) sharing the A fragment (3 LDS reads per 2 MFMAs).
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-    const int i16 = lane & 15, k4 = lane >> 4;
-    const int tp = (P + 15) >> 4, tq2 = (Q + 31) >> 5;
-    for (int t = wid; t < tp * tq2; t += nwv) {
-        const int p0 = (t / tq2) << 4, q0 = (t - (t / tq2) * tq2) << 5;
-        const int p = p0 + i16, qa = q0 + i16, qb = qa + 16;
-        const bool pv = p < P, qav = qa < Q, qbv = qb < Q;
-        const float* Ap = A + (pv ? p : 0) * sap;
-        const float* Ba = B + (qav ? qa : 0) * sbq;
-        const float* Bb = B + (qbv ? qb : 0) * sbq;
-        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        int kb = 0;  // wave-uniform k base
-        for (; kb + 16 <= K; kb += 16) {
-            float av[4], b0[4], b1[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int kk = kb + 4 * u + k4;
-                av[u] = pv ? Ap[kk * sak] : 0.f;
-                b0[u] = qav ? Ba[kk * sbk] : 0.f;
-                b1[u] = qbv ? Bb[kk * sbk] : 0.f;
-                if (RELU_A) av[u] = fmaxf(av[u], 0.f);
-                if (RELU_B) { b0[u] = fmaxf(b0[u], 0.f); b1[u] = fmaxf(b1[u], 0.f); }
+__device__ __forceinline__ void valu_gemm(int P, int Q, int K, const float* A, int sap, int sak,
+                                          const float* B, int sbq, int sbk, Epi epi) {
+    const int PQ = P * Q;
+    if (K >= 16) {
+        const int g = threadIdx.x >> 4, ng = blockDim.x >> 4, l16 = threadIdx.x & 15;
+        for (int base = 0; base < PQ; base += ng) {  // uniform trip count: shuffles converge
+            const int idx = min(base + g, PQ - 1);
+            const int p = idx / Q, q = idx - p * Q;
+            const float* Ap = A + p * sap;
+            const float* Bp = B + q * sbq;
+            float acc = 0.f;
+            for (int k = l16; k < K; k += 16) {
+                float x = Ap[k * sak], y = Bp[k * sbk];
+                if (RELU_A) x = fmaxf(x, 0.f);
+                if (RELU_B) y = fmaxf(y, 0.f);
+                acc = fmaf(x, y, acc);
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b0[u], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b1[u], acc1, 0, 0, 0);
-            }
+            acc += __shfl_xor(acc, 8, 16);
+            acc += __shfl_xor(acc, 4, 16);
+            acc += __shfl_xor(acc, 2, 16);
+            acc += __shfl_xor(acc, 1, 16);
+            if (l16 == 0 && base + g < PQ) epi(p, q, acc);
         }
-        for (; kb < K; kb += 4) {
-            const int kk = kb + k4;
-            const bool kv = kk < K;
-            float av = (pv && kv) ? Ap[kk * sak] : 0.f;
-            float b0 = (qav && kv) ? Ba[kk * sbk] : 0.f;
-            float b1 = (qbv && kv) ? Bb[kk * sbk] : 0.f;
-            if (RELU_A) av = fmaxf(av, 0.f);
-            if (RELU_B) { b0 = fmaxf(b0, 0.f); b1 = fmaxf(b1, 0.f); }
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc1, 0, 0, 0);
+        return;
+    }
+    for (int idx = threadIdx.x; idx < PQ; idx += blockDim.x) {
+        const int p = idx / Q, q = idx - p * Q;
+        const float* Ap = A + p * sap;
+        const float* Bp = B + q * sbq;
+        float acc = 0.f;
+        for (int k = 0; k < K; ++k) {
+            float x = Ap[k * sak], y = Bp[k * sbk];
+            if (RELU_A) x = fmaxf(x, 0.f);
+            if (RELU_B) y = fmaxf(y, 0.f);
+            acc = fmaf(x, y, acc);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int pp = p0 + 4 * k4 + r;
-            if (pp < P) {
-                if (qav) epi(pp, qa, acc0[r]);
-                if (qbv) epi(pp, qb, acc1[r]);
-            }
+        epi(p, q, acc);
+    }
+}
+
+// Whole GEMM: VALU for degenerate shapes, else MFMA units of 16 rows x
+// 16*NQ columns (NQ matched to Q) dealt round-robin to the waves.
+template <bool RELU_A, bool RELU_B, class Epi>
+__device__ __forceinline__ void lds_gemm(int P, int Q, int K, const float* A, int sap, int sak,
+                                         const float* B, int sbq, int sbk, Epi epi) {
+    if (P < 8 || Q < 8 || K <= 4) {
+        valu_gemm<RELU_A, RELU_B>(P, Q, K, A, sap, sak, B, sbq, sbk, epi);
+        return;
+    }
+    const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const int tp = (P + 15) >> 4;
+    if (Q <= 16) {
+        for (int t = wid; t < tp; t += nwv)
+            gemm_unit<1, RELU_A, RELU_B>(P, Q, 0, K, t << 4, 0, A, sap, sak, B, sbq, sbk, epi);
+    } else if (Q <= 32 || (Q > 48 && Q <= 64)) {
+        const int tq = (Q + 31) >> 5;
+        for (int t = wid; t < tp * tq; t += nwv) {
+            const int pt = t / tq;
+            gemm_unit<2, RELU_A, RELU_B>(P, Q, 0, K, pt << 4, (t - pt * tq) << 5, A, sap, sak, B,
+                                         sbq, sbk, epi);
+        }
+    } else {
+        const int tq = (Q + 47) / 48;
+        for (int t = wid; t < tp * tq; t += nwv) {
+            const int pt = t / tq;
+            gemm_unit<3, RELU_A, RELU_B>(P, Q, 0, K, pt << 4, (t - pt * tq) * 48, A, sap, sak, B,
+                                         sbq, sbk, epi);
         }
     }
 }
@@ -122,8 +208,17 @@ __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int l, int r, int s
     return a.src_base[p] + (int64_t)s * a.src_stride[p] + a.src_col[p][l] + (r - a.src_lo[p][l]);
 }
 
+// diagnostics: one wave-0 lane of every workgroup records the shader clock at
+// phase boundaries (slot k of its row); costs nothing when stamps == nullptr
+#define NET_STAMP(k)                                                                   \
+    do {                                                                               \
+        if (a.stamps && threadIdx.x == 0)                                              \
+            a.stamps[(blockIdx.x + blockIdx.y * gridDim.x) * 16 + (k)] =               \
+                __builtin_amdgcn_s_memtime();                                          \
+    } while (0)
+
 template <int FAM>
-__global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
+__global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
@@ -135,13 +230,83 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
     // Global -> LDS copies issue kB independent loads per thread before any
     // LDS store (a load-then-store loop would expose one memory latency per
     // element); indices are clamped so every load is unconditional.
-    constexpr int kB = 8;
-    for (int l = 0; l < L; ++l) {
-        const int din = a.din[l], dout = a.dout[l], nw = din * dout, n = nw + dout;
-        float* W = sm + a.lw[l];
-        float* Bv = sm + a.lb[l];
-        const int ldw = a.ldw[l];
-        if (FAM == PSVI_FAMILY_MEANFIELD) {
+    NET_STAMP(0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    float4* z4 = reinterpret_cast<float4*>(sm);
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float* dWt = sm + a.lg0 - a.ldwt;  // dW tile [dout][din + 1]
+    const int D = a.din[0], nU = mcnt * D;
+    float* U = sm + a.lu;
+    if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
+        // LDS-DMA (global_load_lds_dword): this sample's x rows (one contiguous
+        // run per source rank) and the u chunk land in the stage with no VGPR
+        // round trip; the resident regions are zeroed while they are in flight.
+        float* stage = sm + 4 * a.lstage_f4;
+        if (!(a.abl & 1)) {
+            for (int p = 0; p < a.nsrc; ++p) {
+                const int len = a.src_stride[p];
+                const float* src = a.xrecv + a.src_base[p] + (int64_t)s * len;
+                float* dst = stage + a.stage_off[p];
+                for (int c = wid; c * 64 < len; c += nwv)
+                    __builtin_amdgcn_global_load_lds(
+                        (const void*)(src + min(c * 64 + lane, len - 1)),
+                        (__attribute__((address_space(3))) void*)(dst + c * 64), 4, 0, 0);
+            }
+            const float* usrc = a.u + (int64_t)m0 * D;
+            float* udst = stage + a.stage_u;
+            for (int c = wid; c * 64 < nU; c += nwv)
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(usrc + min(c * 64 + lane, nU - 1)),
+                    (__attribute__((address_space(3))) void*)(udst + c * 64), 4, 0, 0);
+        }
+        for (int i = threadIdx.x; i < a.lstage_f4; i += blockDim.x) z4[i] = zero4;
+        __syncthreads();  // drains the DMA (vmcnt(0)) and the zeroing
+        if (!(a.abl & 1)) {
+            for (int p = 0; p < a.nsrc; ++p) {
+                const float* st = stage + a.stage_off[p];
+                for (int l = 0; l < L; ++l) {
+                    const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
+                    const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l];
+                    const float rdin = 1.f / (float)din;
+                    const float* sl = st + a.src_col[p][l] - lo;
+                    float* W = sm + a.lw[l];
+                    float* Bv = sm + a.lb[l];
+                    for (int r = lo + threadIdx.x; r < hi; r += blockDim.x) {
+                        const float v = sl[r];
+                        if (r < nw) {
+                            // exact for r < 2^21: (r + 0.5) / din is >= 0.5/din from an integer
+                            const int j = (int)(((float)r + 0.5f) * rdin), i = r - j * din;
+                            W[j * ldw + i] = v;
+                        } else {
+                            Bv[r - nw] = v;
+                        }
+                    }
+                }
+            }
+            const float* us = stage + a.stage_u;
+            const float rD = 1.f / (float)D;
+            for (int idx = threadIdx.x; idx < nU; idx += blockDim.x) {
+                const int m = (int)(((float)idx + 0.5f) * rD), i = idx - m * D;
+                U[m * a.ldu + i] = us[idx];
+            }
+        }
+        for (int m = threadIdx.x; m < mcnt; m += blockDim.x) U[m * a.ldu + D] = 1.f;
+        __syncthreads();
+        for (int i = a.lstage_f4 + threadIdx.x; i < a.lds_f4; i += blockDim.x) z4[i] = zero4;
+        __syncthreads();
+        // ones column of every hidden activation (read from fwd layer 1 on,
+        // past the barrier that ends fwd layer 0)
+        for (int m = threadIdx.x; m < mcnt; m += blockDim.x)
+            for (int l = 0; l + 1 < L; ++l) sm[a.la[l] + m * a.lda[l] + a.dout[l]] = 1.f;
+    } else {
+        for (int i = threadIdx.x; i < a.lds_f4; i += blockDim.x) z4[i] = zero4;
+        __syncthreads();
+        constexpr int kB = 16;
+        for (int l = 0; l < L && !(a.abl & 1); ++l) {
+            const int din = a.din[l], dout = a.dout[l], nw = din * dout, n = nw + dout;
+            float* W = sm + a.lw[l];
+            float* Bv = sm + a.lb[l];
+            const int ldw = a.ldw[l];
             const float* mu = a.params + a.poff[l];
             const float* rho = mu + n;
             const float* eW = a.eps + a.eoff[l] + (int64_t)sg * nw;
@@ -173,53 +338,34 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
                     }
                 }
             }
-        } else {
-            for (int p = 0; p < a.nsrc; ++p) {
-                const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
-                if (hi <= lo) continue;
-                const float* src = a.xrecv + a.src_base[p] + (int64_t)s * a.src_stride[p] +
-                                   a.src_col[p][l] - lo;
-                for (int base = lo + threadIdx.x; base < hi; base += kB * blockDim.x) {
-                    float v[kB];
+        }
+        if (!(a.abl & 1)) {
+            const float* src = a.u + (int64_t)m0 * D;
+            for (int base = threadIdx.x; base < nU; base += kB * blockDim.x) {
+                float v[kB];
 #pragma unroll
-                    for (int k = 0; k < kB; ++k) v[k] = src[min(base + k * (int)blockDim.x, hi - 1)];
+                for (int k = 0; k < kB; ++k) v[k] = src[min(base + k * (int)blockDim.x, nU - 1)];
 #pragma unroll
-                    for (int k = 0; k < kB; ++k) {
-                        const int r = base + k * (int)blockDim.x;
-                        if (r >= hi) break;
-                        if (r < nw) {
-                            const int j = r / din, i = r - j * din;
-                            W[j * ldw + i] = v[k];
-                        } else {
-                            Bv[r - nw] = v[k];
-                        }
-                    }
+                for (int k = 0; k < kB; ++k) {
+                    const int idx = base + k * (int)blockDim.x;
+                    if (idx >= nU) break;
+                    const int m = idx / D, i = idx - m * D;
+                    U[m * a.ldu + i] = v[k];
                 }
             }
         }
-    }
-    // ---- 2. pseudo-input chunk -------------------------------------------
-    {
-        const int D = a.din[0], nU = mcnt * D;
-        float* U = sm + a.lu;
-        const float* src = a.u + (int64_t)m0 * D;
-        for (int base = threadIdx.x; base < nU; base += kB * blockDim.x) {
-            float v[kB];
-#pragma unroll
-            for (int k = 0; k < kB; ++k) v[k] = src[min(base + k * (int)blockDim.x, nU - 1)];
-#pragma unroll
-            for (int k = 0; k < kB; ++k) {
-                const int idx = base + k * (int)blockDim.x;
-                if (idx >= nU) break;
-                const int m = idx / D, i = idx - m * D;
-                U[m * a.ldu + i] = v[k];
-            }
+        // ones column (index dim) of u and of every hidden activation: the dW
+        // GEMM over [h | 1] then yields the bias gradient as its last column.
+        for (int m = threadIdx.x; m < mcnt; m += blockDim.x) {
+            U[m * a.ldu + D] = 1.f;
+            for (int l = 0; l + 1 < L; ++l) sm[a.la[l] + m * a.lda[l] + a.dout[l]] = 1.f;
         }
     }
     __syncthreads();
+    NET_STAMP(1);
 
     // ---- 3. forward --------------------------------------------------------
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l < L && !(a.abl & 2); ++l) {
         const float* H = l == 0 ? sm + a.lu : sm + a.la[l - 1];
         const int ldh = l == 0 ? a.ldu : a.lda[l - 1];
         float* Aout = sm + a.la[l];
@@ -235,13 +381,14 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
         __syncthreads();
     }
 
+    NET_STAMP(2);
     // ---- 4. weighted NLL, dlogits ------------------------------------------
     {
         const int C = a.dout[L - 1];
         float* G = sm + a.la[L - 1];
         const int ldg = a.lda[L - 1];
         float part = 0.f;
-        for (int m = threadIdx.x; m < mcnt; m += blockDim.x) {
+        for (int m = threadIdx.x; m < mcnt && !(a.abl & 4); m += blockDim.x) {
             float* row = G + m * ldg;
             float mx = row[0];
             for (int k = 1; k < C; ++k) mx = fmaxf(mx, row[k]);
@@ -261,120 +408,170 @@ __global__ __launch_bounds__(256) void net_kernel(NetArgs a) {
         __syncthreads();
     }
 
+    NET_STAMP(3);
     // ---- 5. backward -------------------------------------------------------
-    for (int l = L - 1; l >= 0; --l) {
-        const int din = a.din[l], dout = a.dout[l], nw = din * dout;
-        const float* G = sm + a.la[l];
-        const int ldg = a.lda[l];
+    float sink = 0.f;
+    for (int l = L - 1; l >= 0 && !(a.abl & 8); --l) {
+        const int din = a.din[l], dout = a.dout[l], nw = din * dout, qw = din + 1;
+        // g_l: dlogits in the last activation buffer, else a ping-pong buffer
+        const float* G = l == L - 1 ? sm + a.la[L - 1] : sm + (((L - 1 - l) & 1) ? a.lg0 : a.lg1);
+        const int ldg = l == L - 1 ? a.lda[L - 1] : a.ldgb;
+        float* Gn = sm + (((L - l) & 1) ? a.lg0 : a.lg1);  // g_{l-1}
         const float* H = l == 0 ? sm + a.lu : sm + a.la[l - 1];
         const int ldh = l == 0 ? a.ldu : a.lda[l - 1];
-        // dW[j][i] = sum_m g[m][j] h[m][i]
+        // dW_l = g_l^T [h_{l-1} | 1] into the LDS dW tile, and
+        // g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] into the other gradient buffer
+        {
+            auto epi = [&](int j, int i, float v) { dWt[j * qw + i] = v; };
+            if (l == 0)
+                lds_gemm<false, false>(dout, qw, mcnt, G, 1, ldg, H, 1, ldh, epi);
+            else
+                lds_gemm<false, true>(dout, qw, mcnt, G, 1, ldg, H, 1, ldh, epi);
+        }
+        if (l > 0 && !(a.abl & 128)) {
+            const float* Ap = sm + a.la[l - 1];
+            const int ldp = a.lda[l - 1];
+            auto epi = [&](int m, int i, float v) {
+                Gn[m * a.ldgb + i] = Ap[m * ldp + i] > 0.f ? v : 0.f;
+            };
+            lds_gemm<false, false>(mcnt, din, dout, G, ldg, 1, sm + a.lw[l], 1, a.ldw[l], epi);
+        }
+        __syncthreads();
+        NET_STAMP(4 + 2 * (L - 1 - l));
+        // dW tile -> global as contiguous rows; re-zero the tile
+        const int nt = dout * qw;
         if (FAM == PSVI_FAMILY_MEANFIELD) {
             float* accMu = a.accMu + a.woff[l];
             float* accRho = a.accRho + a.woff[l];
             const float* E = sm + a.le[l];
-            const int ldw = a.ldw[l];
-            auto epi = [&](int j, int i, float dw) {
-                atomicAdd(accMu + j * din + i, dw);
-                atomicAdd(accRho + j * din + i, dw * E[j * ldw + i]);
-            };
-            if (l == 0)
-                lds_gemm<false, false>(dout, din, mcnt, G, 1, ldg, H, 1, ldh, epi);
-            else
-                lds_gemm<false, true>(dout, din, mcnt, G, 1, ldg, H, 1, ldh, epi);
             const float* EB = sm + a.leb[l];
-            for (int j = threadIdx.x; j < dout; j += blockDim.x) {
-                float db = 0.f;
-                for (int m = 0; m < mcnt; ++m) db += G[m * ldg + j];
-                atomicAdd(accMu + nw + j, db);
-                atomicAdd(accRho + nw + j, db * EB[j]);
+            for (int idx = threadIdx.x; idx < nt; idx += blockDim.x) {
+                const int j = idx / qw, i = idx - j * qw;
+                const float dw = dWt[idx];
+                const int o = i < din ? j * din + i : nw + j;
+                const float e = i < din ? E[j * a.ldw[l] + i] : EB[j];
+                if (a.abl & 16) { sink += dw; continue; }
+                atomicAdd(accMu + o, dw);
+                atomicAdd(accRho + o, dw * e);
             }
         } else {
             const bool at = a.atomic_g != 0;
-            auto epi = [&](int j, int i, float dw) {
-                float* dst = a.gsend + fc_addr(a, l, j * din + i, s);
+            for (int idx = threadIdx.x; idx < nt; idx += blockDim.x) {
+                const int j = idx / qw, i = idx - j * qw;
+                const float dw = dWt[idx];
+                if (a.abl & 16) { sink += dw; continue; }
+                // column din of [h | 1] is the bias gradient
+                float* dst = a.gsend + fc_addr(a, l, i < din ? j * din + i : nw + j, s);
                 if (at) atomicAdd(dst, dw); else *dst = dw;
-            };
-            if (l == 0)
-                lds_gemm<false, false>(dout, din, mcnt, G, 1, ldg, H, 1, ldh, epi);
-            else
-                lds_gemm<false, true>(dout, din, mcnt, G, 1, ldg, H, 1, ldh, epi);
-            for (int j = threadIdx.x; j < dout; j += blockDim.x) {
-                float db = 0.f;
-                for (int m = 0; m < mcnt; ++m) db += G[m * ldg + j];
-                float* dst = a.gsend + fc_addr(a, l, nw + j, s);
-                if (at) atomicAdd(dst, db); else *dst = db;
             }
         }
-        if (l == 0) break;
-        __syncthreads();  // dW read h_{l-1}; g_{l-1} overwrites it in place
-        {
-            float* Hp = sm + a.la[l - 1];
-            const int ldp = a.lda[l - 1];
-            auto epi = [&](int m, int i, float acc) {
-                float* e = Hp + m * ldp + i;
-                *e = *e > 0.f ? acc : 0.f;
-            };
-            // g_{l-1}[m][i] = sum_j g[m][j] W[j][i]
-            lds_gemm<false, false>(mcnt, din, dout, G, ldg, 1, sm + a.lw[l], 1, a.ldw[l], epi);
-        }
         __syncthreads();
+        NET_STAMP(5 + 2 * (L - 1 - l));
     }
+    asm volatile("" ::"v"(sink));
 }
 
 static inline int odd_ld(int x) { return (x & 1) ? x : x + 1; }
+static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 
-// LDS floats needed for a chunk of `mc` points.
+// LDS floats needed for a chunk of `mc` points.  Padding contract of
+// gemm_unit (everything zero-filled at kernel start):
+//   W_l: rup(dout,32) rows (rows >= dout stay 0), odd stride >= rup(din,16)
+//        (columns din.. stay 0): k past din / dout meets zeros;
+//   h buffers (u, activations, gradients): rup(mc,16) rows (rows >= mcnt
+//        stay 0: k past the pseudopoint count meets zeros), odd stride with a
+//        ones column at index dim for u / hidden activations;
+//   every region is followed by 64 floats of zero slack for the row-wrap
+//   reads of out-of-range rows / columns (whose outputs are dropped).
+//   Resident regions (weights, u) come first; the late regions (activations,
+//   dW tile, gradient buffers) follow from lstage and double as the landing
+//   area of the full-cov LDS-DMA loads before they are zeroed.
 static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     size_t off = 0;
     auto take = [&](size_t nfl) {
         size_t o = off;
-        off += (nfl + 3) & ~size_t(3);  // keep 16-B alignment of every region
+        off += ((nfl + 3) & ~size_t(3)) + 64;
         return (int)o;
     };
+    const int mcr = rup(mc, 16);
+    int maxh = 1, wt = 1;
     for (int l = 0; l < p.L; ++l) {
         const int din = p.lay[l].din, dout = p.lay[l].dout;
-        const int ldw = odd_ld(din);
-        if (a) a->ldw[l] = ldw;
-        int lw = take((size_t)dout * ldw), lb = take(dout);
+        if (l > 0) maxh = std::max(maxh, din);
+        wt = std::max(wt, dout * (din + 1));
+        const int ldw = odd_ld(rup(din, 16));
+        int lw = take((size_t)rup(dout, 32) * ldw), lb = take(dout);
         int le = 0, leb = 0;
         if (p.family == PSVI_FAMILY_MEANFIELD) {
             le = take((size_t)dout * ldw);
             leb = take(dout);
         }
-        const int lda = odd_ld(dout);
-        int la = take((size_t)mc * lda);
         if (a) {
-            a->lw[l] = lw; a->lb[l] = lb; a->le[l] = le; a->leb[l] = leb;
-            a->la[l] = la; a->lda[l] = lda;
+            a->ldw[l] = ldw; a->lw[l] = lw; a->lb[l] = lb; a->le[l] = le; a->leb[l] = leb;
         }
     }
-    const int ldu = odd_ld(p.lay[0].din);
-    int lu = take((size_t)mc * ldu);
+    const int ldu = odd_ld(p.lay[0].din + 1);
+    int lu = take((size_t)mcr * ldu);
     int lred = take(16);
-    if (a) { a->lu = lu; a->ldu = ldu; a->lred = lred; }
+    const size_t lstage = off;
+    for (int l = 0; l < p.L; ++l) {
+        const int lda = odd_ld(p.lay[l].dout + 1);
+        int la = take((size_t)mcr * lda);
+        if (a) { a->la[l] = la; a->lda[l] = lda; }
+    }
+    const int wt4 = (wt + 3) & ~3;
+    const int ldgb = odd_ld(maxh);
+    // the dW tile sits directly in front of the first gradient buffer
+    off += wt4;
+    int lg0 = take((size_t)mcr * ldgb);
+    int lg1 = take((size_t)mcr * ldgb);
+    if (p.family == PSVI_FAMILY_FULLCOV) {
+        // DMA stage: whole-wave (64-float) pieces per source, then u
+        size_t st = lstage;
+        for (int q = 0; q < p.world; ++q) {
+            if (a) a->stage_off[q] = (int)(st - lstage);
+            st += (size_t)rup(p.rows_tot[q], 64);
+        }
+        if (a) a->stage_u = (int)(st - lstage);
+        st += (size_t)rup(mc * p.lay[0].din, 64);
+        off = std::max(off, st);
+    }
+    off = (off + 3) & ~size_t(3);
+    if (a) {
+        a->lu = lu; a->ldu = ldu; a->lred = lred;
+        a->lg0 = lg0; a->lg1 = lg1; a->ldgb = ldgb; a->ldwt = wt4;
+        a->lds_f4 = (int)(off / 4);
+        a->lstage_f4 = (int)(lstage / 4);
+    }
     return off;
 }
 
 size_t net_plan_geometry(psvi_plan& p) {
-    // Enough workgroups to cover the CUs, and LDS <= 80 KiB (2 WGs / CU)
-    // when possible, <= 160 KiB always.
-    const int S_local = p.s_cnt[p.rank];
+    // One workgroup per sample and all M pseudopoints when the samples alone
+    // fill the chip (G gets plain stores: no memset, no atomics); otherwise
+    // split the pseudopoints over workgroups (partial dW summed with atomics).
+    // LDS <= 160 KiB per workgroup.
+    const int S_local = std::max(1, p.s_cnt[p.rank]);
     const int M = p.d.M;
     int mchunks = 1;
-    while (S_local * mchunks < 256 && (M + mchunks) / (mchunks + 1) >= 16) ++mchunks;
+    if (S_local < 96)
+        while (S_local * mchunks < 256 && (M + mchunks) / (mchunks + 1) >= 16) ++mchunks;
     for (;;) {
         const int mc = (M + mchunks - 1) / mchunks;
         const size_t bytes = net_lds_floats(p, mc, nullptr) * 4;
-        if (bytes <= 80 * 1024 || (bytes <= 160 * 1024 && mc <= 16) || mc == 1) {
+        if (bytes <= 160 * 1024 || mc == 1) {
             p.mchunks = (M + mc - 1) / mc;
             p.mc = mc;
             p.net_lds = bytes;
+            p.net_threads = mc > 32 ? 512 : 256;
             return bytes;
         }
         ++mchunks;
     }
 }
+
+int g_net_ablation = 0;  // psvi_debug_set(PSVI_DBG_NET_ABLATION, mask)
+unsigned long long* g_net_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_NET_STAMPS, buf)
 
 void net_set_lds_limit() {
     // gfx950: up to 160 KiB of LDS per workgroup
@@ -394,6 +591,8 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     a.S_total = p.d.S;
     a.s_goff = p.s_off[p.rank];
     a.atomic_g = p.mchunks > 1;
+    a.abl = g_net_ablation;
+    a.stamps = g_net_stamps;
     for (int l = 0; l < p.L; ++l) {
         a.din[l] = p.lay[l].din;
         a.dout[l] = p.lay[l].dout;
@@ -420,7 +619,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
             base += (int64_t)S_local * p.rows_tot[q];
         }
     }
-    dim3 grid(p.s_cnt[p.rank], p.mchunks), block(256);
+    dim3 grid(p.s_cnt[p.rank], p.mchunks), block(p.net_threads);
     if (p.s_cnt[p.rank] == 0) return hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL(net_kernel<PSVI_FAMILY_MEANFIELD>, grid, block, p.net_lds, st, a);

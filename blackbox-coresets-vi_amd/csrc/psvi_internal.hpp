@@ -83,6 +83,22 @@ __device__ __forceinline__ float adam_apply(const AdamC& a, float p, float g, fl
     }
 }
 
+// Same update with the raw v_sqrt_f32 / v_rcp_f32 (1 ulp each) instead of the
+// IEEE-exact expansions: the full-cov update runs it on 4.7 M entries per step.
+__device__ __forceinline__ float adam_apply_fast(const AdamC& a, float p, float g, float& m,
+                                                 float& v) {
+    m = a.b1 * m + a.omb1 * g;
+    if (a.kind == PSVI_ADAM_HIGHER) {
+        v = a.b2 * v + a.omb2 * g * g;
+        const float denom = __builtin_amdgcn_sqrtf(v + 1e-8f) * a.inv_sqrt_bc2 + a.eps;
+        return p - a.lr_bc1 * m * __builtin_amdgcn_rcpf(denom);
+    } else {
+        v = a.b2 * v + a.omb2 * g * g + 1e-12f;
+        const float denom = __builtin_amdgcn_sqrtf(v * a.inv_bc2) + a.eps;
+        return p - a.lr * (m * a.inv_bc1) * __builtin_amdgcn_rcpf(denom);
+    }
+}
+
 // ------------------------------------------------------------- plan layout
 struct LayerInfo {
     int din, dout;
@@ -98,14 +114,13 @@ struct LayerInfo {
 struct FwdItem {
     int layer, r0, r1, k0, k1, xcol;  // xcol: x_shard column of row r0
 };
-// Full-cov backward tile: rows [r0, r0+64) x cols [c0, c0+64) of the strict
-// lower triangle of layer `layer`, rows clipped to [rlo, rhi).
-struct BwdTile {
-    int layer, r0, c0, rlo, rhi, xcol;  // xcol: g_shard column of row rlo
-};
-// Full-cov per-row (mean, sd) block: rows [r0, r0+64) of layer, clipped.
-struct DiagBlock {
-    int layer, r0, rhi, xcol;
+// Full-cov update work item: the 64-row band [r0, r0+64) of layer `layer`
+// (r0 a multiple of 64; the rank owns rows [rlo, rhi)) against the c-blocks
+// [k0, k1) (columns [64 k0, 64 k1)).  The band's G slice is staged once and
+// reused across the chunk's c-blocks; the chunk holding c-block r0/64 (diag)
+// also updates the band's mean and sd.  xcol: g_shard column of row r is xcol + r.
+struct UpdChunk {
+    int layer, r0, k0, k1, rlo, rhi, xcol, diag;
 };
 
 struct NetArgs;  // kernels_net.hip
@@ -129,17 +144,15 @@ struct psvi_plan {
     int xcol_l[psvi::kMaxWorld][psvi::kMaxL];  // column of layer l's first row in a shard
     // work lists (host copies, then device)
     std::vector<psvi::FwdItem> h_fwd;
-    std::vector<psvi::BwdTile> h_bwd;
-    std::vector<psvi::DiagBlock> h_diag;
+    std::vector<psvi::UpdChunk> h_upd;
     bool on_device = false;
     psvi::FwdItem* d_fwd = nullptr;
     int n_fwd = 0;
-    psvi::BwdTile* d_bwd = nullptr;
-    int n_bwd = 0;
-    psvi::DiagBlock* d_diag = nullptr;
-    int n_diag = 0;
+    psvi::UpdChunk* d_upd = nullptr;
+    int n_upd = 0;
+    int upd_tiles = 0;  // c-blocks over all chunks (work measure)
     // net kernel geometry
-    int mchunks = 1, mc = 0;
+    int mchunks = 1, mc = 0, net_threads = 256;
     size_t net_lds = 0;
     size_t ws_bytes = 0;
     int64_t acc_count = 0;

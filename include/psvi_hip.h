@@ -180,6 +180,23 @@ int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m,
 const char* psvi_last_error(void);
 const char* psvi_version(void);
 
+/* ---- diagnostics (profiling builds of a run; never needed for results) ---- */
+#define PSVI_DBG_NET_ABLATION 1  /* value: mask of network-kernel parts to skip
+                                    (1 loads, 2 fwd GEMMs, 4 NLL, 8 bwd GEMMs,
+                                    16 global dW writes); 0 = full kernel      */
+int psvi_debug_set(int32_t key, int32_t value);
+#define PSVI_DBG_NET_STAMPS 2    /* ptr: device uint64 buffer, 16 slots per
+                                    network-kernel workgroup: s_memtime at
+                                    phase boundaries; NULL = off               */
+#define PSVI_DBG_UPD_ABLATION 3  /* value: mask of full-cov update-kernel parts to
+                                    skip (1 G/eps loads, 2 MFMAs, 4 epilogue
+                                    loads, 8 epilogue stores)                  */
+#define PSVI_DBG_UPD_STAMPS 4    /* ptr: device uint64 buffer, 16 slots per
+                                    update-kernel workgroup (start, staged,
+                                    MFMA done, end, HW_ID, XCC_ID, tile read,
+                                    loads issued, LDS written)                 */
+int psvi_debug_set_ptr(int32_t key, void* ptr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,12 @@ def main():
         gs = torch.zeros(plan.xshard_count, device=dev)
         out["sample(memset+fwd)"] = timeit(lambda: plan.mvn_sample(eps, params, xs), iters)
         out["net(+memset)"] = timeit(lambda: plan.mvn_net(u, z, w, xs, gs, nll), iters)
+        if os.environ.get("NET_ABLATION"):
+            lib = plan.lib
+            for mask in (1, 2, 4, 8, 16, 2 | 8, 1 | 2 | 4 | 8):
+                lib.psvi_debug_set(1, mask)
+                out[f"net abl={mask}"] = timeit(lambda: plan.mvn_net(u, z, w, xs, gs, nll), iters)
+            lib.psvi_debug_set(1, 0)
         st = [1]
 
         def upd():
