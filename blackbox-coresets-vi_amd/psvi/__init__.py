@@ -1,6 +1,9 @@
-"""psvi (MI355X-native): coreset-weighted ELBO inner loop on hand-written HIP kernels.
+"""psvi (MI355X-native): the coreset-weighted ELBO inner loop of
+souravc83/Blackbox-Coresets-VI on hand-written HIP kernels (gfx950).
 
-Mirrors the reference package layout (psvi.models, psvi.inference,
-psvi.robust_higher, psvi.hypergrad, psvi.experiments) for the hot path; the
-arithmetic of the inner loop runs in blackbox-coresets-vi_amd/csrc (gfx950).
+  psvi.models     variational layers with the reference's parameter layout
+                  (VILinear, VILinearMultivariateNormal, make_fcnet, make_fc2net)
+  psvi.inference  PSVI classes: inner_elbo / inner_loop on the HIP library
+  psvi.runtime    ctypes boundary to libpsvi_hip.so (C ABI: include/psvi_hip.h),
+                  single-GPU plans and the multi-GPU sharded driver
 """

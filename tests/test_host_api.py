@@ -1,0 +1,144 @@
+"""Host-side mirror of the reference API (psvi.models / psvi.inference) on CPU:
+parameter layout, model specs, coreset weights and KL closed forms.  The HIP
+calls behind inner_elbo / inner_loop are exercised in test_host_api_gpu.py."""
+import numpy as np
+import pytest
+import torch
+import torch.distributions as dist
+import torch.nn as nn
+
+import psvi_oracle as O
+from golden_util import family_of, fixture_names, load_fixture
+
+
+def build_model(cfg, params0):
+    """The reference module stack a fixture was generated from, at params0."""
+    from psvi.models import VILinear, VILinearMultivariateNormal
+
+    cls = VILinear if family_of(cfg) == "meanfield" else VILinearMultivariateNormal
+    mods = []
+    for i, (a, b) in enumerate(cfg["layers"]):
+        mods.append(cls(a, b, mc_samples=cfg["S"], prior_sd=cfg["prior_sd"]))
+        if i + 1 < len(cfg["layers"]):
+            mods.append(nn.ReLU())
+    net = nn.Sequential(*mods)
+    with torch.no_grad():
+        nn.utils.vector_to_parameters(torch.tensor(params0, dtype=torch.float32),
+                                      net.parameters())
+    return net
+
+
+def fixture_model(name):
+    f = load_fixture(name)
+    return f, build_model(f["cfg"], f["params0"])
+
+
+def make_psvi(f, model, device="cpu"):
+    from psvi.inference import PSVIAV, PSVILearnV
+
+    cfg = f["cfg"]
+    cls = PSVIAV if cfg["f"] == "exp_alpha_softmax" else PSVILearnV
+    u = torch.tensor(f["u"], dtype=torch.float32, device=device)
+    z = torch.tensor(f["z"], dtype=torch.float32, device=device)
+    ps = cls(u=u, z=z, N=cfg["N"], model=model, mc_samples=cfg["S"], lr0net=cfg["lr"],
+             device_id=0 if device == "cuda" else None)
+    ps.device = torch.device(device)
+    with torch.no_grad():
+        ps.v = torch.tensor(f["v"], dtype=torch.float32, device=device)
+        if cfg["f"] == "exp_alpha_softmax":
+            ps.alpha = torch.tensor([cfg["alpha"]], dtype=torch.float32, device=device)
+    return ps
+
+
+def test_builders_match_reference_layout():
+    from psvi.models import make_fc2net, make_fcnet, make_logreg, model_spec
+    from psvi.runtime import InnerLoopPlan
+
+    net = make_fc2net(64, 40, 2, mc_samples=128, init_sd=1e-6)
+    assert [n for n, _ in net.named_parameters()][:3] == ["lin0.mean", "lin0._sd", "lin0._corr"]
+    fam, layers, prior, S = model_spec(net)
+    assert (fam, layers, prior, S) == ("fullcov", [(64, 40), (40, 40), (40, 2)], 1.0, 128)
+    plan = InnerLoopPlan(fam, layers, S, 100)
+    assert sum(p.numel() for p in net.parameters()) == plan.param_count == 4_730_326
+    # init: mean 0, corr 0, sd = softplus^-1(init_sd)
+    assert torch.all(net[0].mean == 0) and torch.all(net[0]._corr == 0)
+    assert torch.allclose(torch.nn.functional.softplus(net[0]._sd), torch.full((2600,), 1e-6))
+
+    net = make_fcnet(2, 100, 4, n_layers=1, mc_samples=32)
+    assert [n for n, _ in net.named_parameters()] == [
+        "lin0.weight", "lin0.bias", "lin0._weight_sd", "lin0._bias_sd",
+        "classifier.weight", "classifier.bias", "classifier._weight_sd", "classifier._bias_sd"]
+    fam, layers, prior, S = model_spec(net)
+    assert sum(p.numel() for p in net.parameters()) == \
+        InnerLoopPlan(fam, layers, S, 50).param_count == 1408
+    assert model_spec(make_logreg(2, 2, mc_samples=4))[1] == [(2, 2)]
+    assert model_spec(make_logreg(2, 2, fullcov=True, mc_samples=4))[0] == "fullcov"
+
+
+def test_model_spec_rejects_unsupported_stacks():
+    from psvi.models import VILinear, VILinearMultivariateNormal, model_spec
+
+    with pytest.raises(ValueError):
+        model_spec(nn.Sequential(VILinear(2, 3), nn.Tanh(), VILinear(3, 2)))
+    with pytest.raises(ValueError):
+        model_spec(nn.Sequential(VILinear(2, 3), nn.ReLU(), VILinearMultivariateNormal(3, 2)))
+    with pytest.raises(ValueError):
+        model_spec(nn.Sequential(VILinear(2, 3), nn.ReLU()))
+    with pytest.raises(ValueError):
+        model_spec(nn.Sequential(nn.Linear(2, 3)))
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_fixture_params_roundtrip_and_weights(name):
+    f, model = fixture_model(name)
+    vec = nn.utils.parameters_to_vector(model.parameters()).detach().numpy()
+    assert np.array_equal(vec, f["params0"].astype(np.float32))
+    ps = make_psvi(f, model)
+    w = ps.coreset_weights().numpy()
+    assert np.allclose(w, f["w"], rtol=1e-6, atol=0), (w[:4], f["w"][:4])
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_module_kl_matches_oracle_closed_form(name):
+    f, model = fixture_model(name)
+    cfg = f["cfg"]
+    kl = float(sum(m.kl().detach() for m in model if not isinstance(m, nn.ReLU)))
+    # the oracle's ELBO minus its data term is the KL; evaluate with w = 0
+    fn = O.mf_elbo_grad if cfg["family"] == "mf" else O.mvn_elbo_grad
+    val, _ = fn(cfg["layers"], f["params0"], f["u"], f["z"], np.zeros_like(f["w"]),
+                f["eps"][0], cfg["S"], prior_sd=cfg["prior_sd"])
+    assert abs(kl - val) <= 1e-4 * max(1.0, abs(val)), (kl, val)
+
+
+def test_fullcov_kl_closed_form_equals_torch_triangular_solve():
+    from psvi.models import VILinearMultivariateNormal
+
+    torch.manual_seed(0)
+    layer = VILinearMultivariateNormal(3, 2, prior_sd=0.7, init_sd=0.3).double()
+    with torch.no_grad():
+        layer.mean.normal_()
+        layer._sd.normal_()
+        layer._corr.normal_(std=0.2)
+    ref = dist.kl_divergence(layer.param_dist, layer.prior_dist)
+    assert torch.allclose(layer.kl(), ref, rtol=1e-10), (layer.kl(), ref)
+
+
+def test_inner_loop_refuses_cpu_tensors():
+    """No CPU fallback: without a HIP device the product path raises."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    f, model = fixture_model("g3r_fn2_tiny_rand")
+    ps = make_psvi(f, model)
+    with pytest.raises(ValueError, match="device tensor"):
+        ps.inner_elbo(eps=torch.zeros(10))
+    with pytest.raises(ValueError, match="device tensor"):
+        ps.inner_loop(T=1)
+
+
+def test_outer_loop_entry_points_raise():
+    f, model = fixture_model("g1_logreg_c1")
+    ps = make_psvi(f, model)
+    for fn in (lambda: ps.psvi_elbo(None, None), lambda: ps.nested_step(None, None),
+               lambda: ps.hyper_step(None, None), lambda: ps.run_psvi()):
+        with pytest.raises(NotImplementedError):
+            fn()

@@ -1,0 +1,60 @@
+"""psvi.inference on the GPU: PSVI.inner_elbo (autograd boundary over
+psvi_elbo_grad) and PSVI.inner_loop (T fused psvi_inner_step calls) against
+the reference's own numbers in the golden fixtures, through the reference-
+shaped API (modules, coreset weights, parameter write-back)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import adam_kind, assert_grad_close, fixture_names, l2rel, rel
+from test_host_api import fixture_model, make_psvi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_inner_elbo_backward_matches_reference(name):
+    f, model = fixture_model(name)
+    model = model.cuda()
+    ps = make_psvi(f, model, "cuda")
+    eps = torch.tensor(f["eps"][0], dtype=torch.float32, device="cuda")
+    loss = ps.inner_elbo(eps=eps)
+    assert loss.dim() == 0
+    assert rel(loss.item(), f["elbo"][0]) < 1e-5, (loss.item(), f["elbo"][0])
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in model.parameters()]).cpu().numpy()
+    if name == "g4_fn2_mid":  # cancelling classifier-bias entries (see test_hip_parity)
+        assert l2rel(g, f["grad0"]) < 1e-4
+    else:
+        assert_grad_close(g, f["grad0"], l2tol=1e-4, what=name)
+    with pytest.raises(RuntimeError):  # first order only: no double backward
+        p = next(model.parameters())
+        gg = torch.autograd.grad(ps.inner_elbo(eps=eps), p, create_graph=True)[0]
+        gg.sum().backward()
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_inner_loop_matches_reference_trajectory(name):
+    f, model = fixture_model(name)
+    cfg = f["cfg"]
+    model = model.cuda()
+    ps = make_psvi(f, model, "cuda")
+    ps.log_every = 1
+    eps = torch.tensor(f["eps"], dtype=torch.float32, device="cuda")
+    elbos = ps.inner_loop(T=cfg["T"], lr=cfg["lr"], kind=adam_kind(cfg), eps=eps)
+    assert np.allclose(elbos.cpu().numpy(), f["elbo"], rtol=1e-5, atol=0)
+    assert [e[0] for e in ps.elbos] == [1] * cfg["T"]
+    p = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
+    assert l2rel(p, f["params"][-1]) < 1e-5
+    assert np.abs(p - f["params"][-1]).max() < 0.5 * cfg["lr"]
+
+
+def test_inner_loop_philox_is_deterministic_and_advances():
+    f, model = fixture_model("g2r_fn_c2_rand_av")
+    a = make_psvi(f, model.cuda(), "cuda")
+    e1 = a.inner_loop(T=2).cpu()
+    e2 = a.inner_loop(T=2).cpu()
+    assert not torch.equal(e1, e2)  # fresh noise, moved parameters
+    f, model = fixture_model("g2r_fn_c2_rand_av")
+    b = make_psvi(f, model.cuda(), "cuda")
+    assert torch.equal(b.inner_loop(T=2).cpu(), e1)

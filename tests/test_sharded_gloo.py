@@ -1,0 +1,186 @@
+"""Multi-rank inner step on CPU: world_size 2 and 3 over gloo.
+
+The sharded driver (psvi.runtime.sharded.ShardedInnerLoop: split sizes,
+blocked-by-source layouts, the two all_to_all exchanges per full-cov step, the
+mean-field all-reduce, reduce_elbo, owned_mask, gather_params) runs for real
+over torch.distributed; only its three HIP phases are replaced by oracle
+emulations that read and write the same buffers in the same layouts.  One
+sharded step must reproduce the world-1 oracle step (negative ELBO, updated
+params and Adam state)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _layer_cols(info, layers):
+    """column of each layer's first owned row inside a rank's shard row"""
+    cols, c = [], 0
+    for l in range(len(layers)):
+        cols.append(c)
+        c += info["row_cnt"][l]
+    return cols
+
+
+def _emulate_fullcov(loop, O, layers, S, prior_sd):
+    """Install oracle versions of the three full-cov phases on `loop`."""
+    infos, r = loop.info, loop.rank
+    me = infos[r]
+    n_l = [a * b + b for a, b in layers]
+    woff = np.concatenate([[0], np.cumsum(n_l)]).astype(int)
+    cols = [_layer_cols(i, layers) for i in infos]
+    s0 = prior_sd
+
+    def layer_views(params, eps):
+        po = eo = 0
+        for l, n in enumerate(n_l):
+            nc = (n - 1) * (n - 2) // 2
+            mean, sd, corr = params[po:po + n], params[po + n:po + 2 * n], params[po + 2 * n:po + 2 * n + nc]
+            yield l, n, mean, sd, corr, eps[eo:eo + S * n].reshape(S, n)
+            po += 2 * n + nc
+            eo += S * n
+
+    def phase_sample(eps, params):
+        p = params.double().numpy()
+        e = eps.double().numpy()
+        X = np.zeros((S, me["rows"]))
+        for l, n, mean, sd, corr, E in layer_views(p, e):
+            lo, cnt = me["row_lo"][l], me["row_cnt"][l]
+            L = O.mvn_dense_L(sd, corr, n)
+            X[:, cols[r][l]:cols[r][l] + cnt] = mean[lo:lo + cnt] + E @ L[lo:lo + cnt].T
+        loop.x_shard.copy_(torch.from_numpy(X.ravel()).float())
+
+    def recv_to_full(buf):
+        s_cnt = me["s_count"]
+        full = np.zeros((s_cnt, woff[-1]))
+        off = 0
+        for p, q in enumerate(infos):
+            blk = buf[off:off + s_cnt * q["rows"]].reshape(s_cnt, q["rows"])
+            for l in range(len(layers)):
+                lo, cnt = q["row_lo"][l], q["row_cnt"][l]
+                full[:, woff[l] + lo:woff[l] + lo + cnt] = blk[:, cols[p][l]:cols[p][l] + cnt]
+            off += s_cnt * q["rows"]
+        return full
+
+    def full_to_send(full):
+        s_cnt = me["s_count"]
+        out = []
+        for p, q in enumerate(infos):
+            blk = np.zeros((s_cnt, q["rows"]))
+            for l in range(len(layers)):
+                lo, cnt = q["row_lo"][l], q["row_cnt"][l]
+                blk[:, cols[p][l]:cols[p][l] + cnt] = full[:, woff[l] + lo:woff[l] + lo + cnt]
+            out.append(blk.ravel())
+        return np.concatenate(out)
+
+    def phase_net(u, z, w):
+        loop.parts.zero_()
+        X = recv_to_full(loop.x_recv.double().numpy())
+        Ws, bs = O.mvn_split_x(layers, X)
+        data, dWs, dbs = O.net_forward_backward(u.double().numpy(), z.numpy(),
+                                                w.double().numpy(), Ws, bs)
+        G = np.concatenate([np.concatenate([dWs[l].reshape(X.shape[0], -1), dbs[l]], 1)
+                            for l in range(len(layers))], 1)
+        loop.g_send.copy_(torch.from_numpy(full_to_send(G)).float())
+        loop.parts[0] = data
+
+    def phase_update(eps, params, m, v, step, lr, kind, grad_out=None):
+        p = params.double().numpy()
+        e = eps.double().numpy()
+        Gs = loop.g_shard.double().numpy().reshape(S, me["rows"])
+        G = np.zeros((S, woff[-1]))
+        kl = 0.0
+        for l, n, mean, sd, corr, E in layer_views(p, e):
+            lo, cnt = me["row_lo"][l], me["row_cnt"][l]
+            G[:, woff[l] + lo:woff[l] + lo + cnt] = Gs[:, cols[r][l]:cols[r][l] + cnt]
+            L = O.mvn_dense_L(sd, corr, n)[lo:lo + cnt]
+            sp = O.softplus(sd[lo:lo + cnt])
+            kl += float(np.sum(np.log(s0) - np.log(sp) - 0.5
+                               + 0.5 * ((L * L).sum(1) + mean[lo:lo + cnt] ** 2) / s0 ** 2))
+        g = O.mvn_grad_from_G(layers, p, G, e, S, prior_sd=s0)
+        own = loop.owned_mask().numpy()
+        pn, mn, vn = O.adam(kind, p, g, m.double().numpy(), v.double().numpy(), step, lr)
+        for t, new in ((params, pn), (m, mn), (v, vn)):
+            cur = t.double().numpy()
+            cur[own] = new[own]
+            t.copy_(torch.from_numpy(cur).to(t.dtype))
+        loop.parts[1] = kl
+
+    loop.phase_sample, loop.phase_net, loop.phase_update = phase_sample, phase_net, phase_update
+
+
+def _rank_main(rank, world, port, name, kind_override, out):
+    import sys
+    for p in (os.path.join(ROOT, "blackbox-coresets-vi_amd"), os.path.join(ROOT, "oracle"),
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import psvi_oracle as O
+    from golden_util import adam_kind, load_fixture
+    from psvi.runtime.sharded import ShardedInnerLoop, TorchDistComm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        f = load_fixture(name)
+        cfg = f["cfg"]
+        layers, S, M = cfg["layers"], cfg["S"], cfg["M"]
+        kind = kind_override or adam_kind(cfg)
+        loop = ShardedInnerLoop("fullcov", layers, S, M, world, rank, prior_sd=cfg["prior_sd"],
+                                device="cpu", comm=TorchDistComm())
+        _emulate_fullcov(loop, O, layers, S, cfg["prior_sd"])
+        t = lambda x, d=torch.float32: torch.tensor(np.ascontiguousarray(x), dtype=d)
+        params = t(f["params0"]).double()
+        m = torch.zeros_like(params)
+        v = torch.zeros_like(params)
+        parts = torch.zeros(1, 2, dtype=torch.float64)
+        loop.step(t(f["u"]), t(f["z"].astype(np.int32), torch.int32), t(f["w"]), t(f["eps"][0]),
+                  params, m, v, step=1, lr=cfg["lr"], kind=kind, elbo_parts=parts[0])
+        negelbo = loop.reduce_elbo(parts)
+        loop.gather_params(params, m, v)
+        if rank == 0:
+            out.put((float(negelbo[0]), params.numpy(), m.numpy(), v.numpy()))
+        else:
+            out.put(None)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name,kind", [("g3r_fn2_tiny_rand", None), ("g4h_fn2_mid_hyper", None)])
+def test_sharded_fullcov_step_matches_world1(world, name, kind):
+    import psvi_oracle as O
+    from golden_util import adam_kind, l2rel, load_fixture, rel
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, kind, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    negelbo, params, m, v = next(x for x in res if x is not None)
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    o_elbo, _, o_traj, o_m, o_v = O.run_inner_loop(
+        "mvn", cfg["layers"], f["params0"], f["u"], f["z"], f["w"], f["eps"][:1], cfg["S"],
+        cfg["lr"], kind or adam_kind(cfg), prior_sd=cfg["prior_sd"])
+    assert rel(negelbo, o_elbo[0]) < 1e-6, (negelbo, o_elbo[0])
+    assert l2rel(params, o_traj[0]) < 1e-6
+    assert l2rel(m, o_m) < 1e-5 and l2rel(v, o_v) < 1e-5
