@@ -57,16 +57,30 @@ def reference_init_params(n_layers_sizes, device):
 
 def algorithmic_work(S, rows_frac=1.0):
     """Per-launch algorithmic bytes / flops of the two dominant kernels
-    (SURVEY.md §8(d)); rows_frac = this rank's share of the rows (nnz)."""
+    (SURVEY.md §8(d)); rows_frac = this rank's share of the rows (nnz).
+    update: p, m, v of the owned parameters read + written once (24 B each),
+    G of the owned rows and eps (all columns) read once (4 B each), dL = G^T eps
+    over the strict lower triangle (2 flops per MAC)."""
     n = [i * o + o for i, o in LAYERS]
     n_tot = sum(n)
     nc = sum((k - 1) * (k - 2) // 2 for k in n)
-    upd_bytes = (24 * (nc + 2 * n_tot)) * rows_frac + 8 * S * n_tot * rows_frac + 4 * S * n_tot
+    upd_bytes = 24 * (nc + 2 * n_tot) * rows_frac + 4 * S * n_tot * rows_frac + 4 * S * n_tot
     upd_flops = 2.0 * S * nc * rows_frac
     fwd_flops = 2.0 * S * nc * rows_frac
     fwd_bytes = 4 * (nc + 2 * n_tot) * rows_frac + 4 * S * n_tot + 4 * S * n_tot * rows_frac
     return dict(update=dict(bytes=upd_bytes, flops=upd_flops),
                 sample=dict(bytes=fwd_bytes, flops=fwd_flops))
+
+
+def pmc_traffic(kernel, path=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_session.sh -> tools/pmc_report.py --json: separate FETCH_SIZE /
+    WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction), or None."""
+    try:
+        d = json.load(open(path))
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
 
 
 def cpu_baseline(budget_s=12.0):
@@ -223,7 +237,7 @@ def main():
     achieved = work["update"]["bytes"] / upd_s / 1e9
     roofline = dict(bound="hbm", kernel="mvn_update_kernel", achieved=round(achieved, 1),
                     peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                    traffic=None,
+                    traffic=pmc_traffic("mvn_update_kernel"),
                     algorithmic_bytes_per_launch=int(work["update"]["bytes"]),
                     kernels={k: {kk: round(vv, 2) for kk, vv in d.items()}
                              for k, d in kernels.items()},

@@ -57,4 +57,5 @@ def test_inner_loop_philox_is_deterministic_and_advances():
     assert not torch.equal(e1, e2)  # fresh noise, moved parameters
     f, model = fixture_model("g2r_fn_c2_rand_av")
     b = make_psvi(f, model.cuda(), "cuda")
-    assert torch.equal(b.inner_loop(T=2).cpu(), e1)
+    # same Philox stream; mean-field sums use fp32 atomics (order-nondeterministic last bits)
+    assert torch.allclose(b.inner_loop(T=2).cpu(), e1, rtol=1e-7, atol=0)

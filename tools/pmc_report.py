@@ -1,22 +1,58 @@
 #!/usr/bin/env python3
-"""Summarise gpurun_out/pmc: mean kernel duration + per-dispatch counter means."""
+"""Summarise a tools/pmc_session.sh run: mean kernel durations (kernel trace)
+and per-dispatch counter means (one rocprofv3 --pmc pass per group).
+
+  python tools/pmc_report.py [gpurun_out/pmc] [--json out.json]
+
+--json writes per-kernel HBM traffic per launch: FETCH_SIZE and WRITE_SIZE are
+kilobytes; on gfx950 FETCH_SIZE counts half the bytes of 16-byte-per-lane
+streaming reads (MI355X_MICROARCH.md, HBM section), so reads are doubled.
+"""
 import csv
 import glob
+import json
 import os
+import re
 import sys
 from collections import defaultdict
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-stats = glob.glob(os.path.join(root, "trace", "**", "*kernel_stats.csv"), recursive=True)
-for f in stats:
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+root = args[0] if args else "gpurun_out/pmc"
+jout = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+
+
+def short(name):
+    m = re.search(r"psvi::(\w+)", name)
+    return m.group(1) if m else name[:50]
+
+
+durs = {}
+for f in glob.glob(os.path.join(root, "trace", "**", "*kernel_stats.csv"), recursive=True):
     print("== kernel stats", f)
     for r in csv.DictReader(open(f)):
-        print(f"  {r['Name'][:60]:60s} calls={r['Calls']:>5s} avg_us={float(r['AverageNs'])/1e3:9.2f} {float(r['Percentage']):6.2f}%")
+        print(f"  {r['Name'][:70]:70s} calls={r['Calls']:>6s} "
+              f"avg_us={float(r['AverageNs']) / 1e3:9.2f} {float(r['Percentage']):6.2f}%")
+        durs.setdefault(short(r["Name"]), []).append(float(r["AverageNs"]) / 1e3)
 agg = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"][:50]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, d in agg.items():
+        agg[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {}
+for k, d in sorted(agg.items()):
     print("==", k)
     for c, v in sorted(d.items()):
-        print(f"  {c:28s} {sum(v)/len(v):16.1f}  (n={len(v)})")
+        print(f"  {c:28s} {sum(v) / len(v):16.1f}  (n={len(v)})")
+    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+        fetch = 2.0 * 1024 * sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
+        write = 1024.0 * sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
+        out[k] = dict(hbm_bytes_per_launch=round(fetch + write), read_bytes=round(fetch),
+                      write_bytes=round(write), dispatches=len(d["FETCH_SIZE"]),
+                      avg_us=(sum(durs[k]) / len(durs[k]) if k in durs else None))
+        print(f"  -> HBM bytes/launch {fetch + write:.4g} (read x2 {fetch:.4g}, write {write:.4g})")
+if jout:
+    json.dump(dict(source=os.path.abspath(root),
+                   method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                          "KB -> bytes; FETCH_SIZE doubled (gfx950 16-B/lane streaming-read "
+                          "correction, MI355X_MICROARCH.md HBM section)",
+                   kernels=out), open(jout, "w"), indent=1)
+    print("wrote", jout)

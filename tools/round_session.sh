@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-end evidence in one gpurun call: GPU tests, smoke, bench (JSON line),
+# rocprofv3 kernel trace of the bench, PMC HBM-traffic passes of the bench.
+# Stops at the first crash / abort / timeout (rc not in {0,1}).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+R=${ROUND:-r01}
+STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
+if [[ $STEPS == *tests* ]]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 300 > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
+fi
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+  echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; ok $rc || exit $rc
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 600 python bench.py > gpurun_out/bench_${R}.log 2>&1; rc=$?
+  echo "bench rc=$rc"; tail -1 gpurun_out/bench_${R}.log; ok $rc || exit $rc
+fi
+BCMD="python3 bench.py --no-cpu-baseline --steps 200 --warmup 20"
+if [[ $STEPS == *prof* ]]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${R} -o bench -- $BCMD > gpurun_out/prof_${R}.log 2>&1; rc=$?
+  echo "prof rc=$rc"; ok $rc || exit $rc
+fi
+if [[ $STEPS == *pmc* ]]; then
+  CMD="python3 bench.py --no-cpu-baseline --steps 50 --warmup 5" \
+  PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS|SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY|SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
+    bash tools/pmc_session.sh; rc=$?
+  echo "pmc rc=$rc"; ok $rc || exit $rc
+  python3 tools/pmc_report.py gpurun_out/pmc --json gpurun_out/pmc_traffic_${R}.json > gpurun_out/pmc_report_${R}.txt 2>&1
+  tail -30 gpurun_out/pmc_report_${R}.txt
+fi
+exit 0
