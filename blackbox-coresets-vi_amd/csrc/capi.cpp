@@ -21,6 +21,9 @@ void net_set_lds_limit();                // kernels_net.hip
 extern int g_net_ablation;               // kernels_net.hip
 extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
+extern int g_net_split_below;            // kernels_net.hip
+extern int g_fwd_ablation;               // kernels_mvn.hip
+extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
 }  // namespace psvi
 
@@ -46,7 +49,7 @@ int hip_fail(hipError_t e, const char* where) {
         if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
     } while (0)
 
-constexpr int kFwdKChunk = 512;  // columns of L per forward work item
+constexpr int kFwdKChunk = 256;  // columns of L per forward work item
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -89,6 +92,48 @@ int check_desc(const psvi_net_desc* d) {
     if (d->M < 1) return fail(PSVI_EINVAL, "M must be >= 1");
     if (!(d->prior_sd > 0.f)) return fail(PSVI_EINVAL, "prior_sd must be > 0");
     return 0;
+}
+
+// Workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8), each with
+// its own L2.  Keep every band's chunks on one XCD (its G slice and the eps
+// blocks it shares with neighbouring bands then stay in that L2): bands go
+// greedily, largest first, to the least-loaded XCD; each XCD's chunks run
+// largest first; the per-XCD queues are interleaved at stride 8 and padded
+// with empty chunks (k0 == k1, no work).
+static std::vector<UpdChunk> xcd_order(const std::vector<UpdChunk>& in) {
+    constexpr int kXcd = 8;
+    auto work = [](const UpdChunk& c) { return (c.k1 - c.k0) + c.diag; };
+    std::vector<std::vector<UpdChunk>> band;  // chunks of one (layer, r0)
+    for (const UpdChunk& c : in) {
+        if (band.empty() || band.back()[0].layer != c.layer || band.back()[0].r0 != c.r0)
+            band.emplace_back();
+        band.back().push_back(c);
+    }
+    std::vector<int> bw(band.size());
+    for (size_t i = 0; i < band.size(); ++i)
+        for (const UpdChunk& c : band[i]) bw[i] += work(c);
+    std::vector<size_t> idx(band.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return bw[a] > bw[b]; });
+    std::vector<std::vector<UpdChunk>> q(kXcd);
+    std::vector<long> load(kXcd, 0);
+    for (size_t i : idx) {
+        const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[x] += bw[i];
+        q[x].insert(q[x].end(), band[i].begin(), band[i].end());
+    }
+    size_t len = 0;
+    for (auto& v : q) {
+        std::stable_sort(v.begin(), v.end(),
+                         [&](const UpdChunk& a, const UpdChunk& b) { return work(a) > work(b); });
+        len = std::max(len, v.size());
+    }
+    std::vector<UpdChunk> out;
+    out.reserve(len * kXcd);
+    const UpdChunk empty{0, 0, 0, 0, 0, 0, 0, 0};
+    for (size_t j = 0; j < len; ++j)
+        for (int x = 0; x < kXcd; ++x) out.push_back(j < q[x].size() ? q[x][j] : empty);
+    return out;
 }
 
 int build_plan(psvi_plan& p) {
@@ -148,8 +193,9 @@ int build_plan(psvi_plan& p) {
     if (p.family == PSVI_FAMILY_FULLCOV) {
         std::vector<FwdItem> fwd;
         std::vector<UpdChunk> upd;
-        // c-blocks per update chunk: about two chunks per CU slot (256 CUs x
-        // 2 resident workgroups), at least one
+        std::vector<FwdRowBlock> frb;
+        // c-blocks per update chunk: about one chunk per workgroup slot
+        // (256 CUs x 3 resident update workgroups), at least one
         int tiles = 0;
         for (int l = 0; l < p.L; ++l) {
             const int lo = p.row_lo[r][l], hi = p.row_hi[r][l];
@@ -159,18 +205,20 @@ int build_plan(psvi_plan& p) {
         for (int l = 0; l < p.L; ++l) {
             const int n = p.lay[l].n, lo = p.row_lo[r][l], hi = p.row_hi[r][l];
             const int xc = p.xcol_l[r][l];
-            for (int r0 = lo; r0 < hi; r0 += 32) {
-                const int r1 = std::min(r0 + 32, hi);
+            for (int r0 = lo; r0 < hi; r0 += kFwdRows) {
+                const int r1 = std::min(r0 + kFwdRows, hi);
                 const int kmax = std::max(0, std::min(r1 - 1, n - 2));
                 const int nit = std::max(1, (kmax + kFwdKChunk - 1) / kFwdKChunk);
                 // even split, multiples of 64 columns (the kernel's LDS stage)
                 const int steps = (kmax + 63) / 64;
+                const int slot0 = (int)fwd.size();
                 for (int i = 0; i < nit; ++i) {
                     const int k0 = std::min(kmax, 64 * (int)((int64_t)steps * i / nit));
                     const int k1 = std::min(kmax, 64 * (int)((int64_t)steps * (i + 1) / nit));
                     if (i > 0 && k0 >= k1) continue;
-                    fwd.push_back(FwdItem{l, r0, r1, k0, k1, xc + (r0 - lo)});
+                    fwd.push_back(FwdItem{l, r0, r1, k0, k1, xc + (r0 - lo), (int)fwd.size()});
                 }
+                frb.push_back(FwdRowBlock{slot0, (int)fwd.size() - slot0, r1 - r0, xc + (r0 - lo), l, r0});
             }
             // bands of 64 absolute rows; c-blocks 0..b, the last one diagonal
             for (int b = lo / 64; 64 * b < hi; ++b) {
@@ -185,14 +233,12 @@ int build_plan(psvi_plan& p) {
             return (a.k1 - a.k0) > (b.k1 - b.k0);
         });
         p.h_fwd = fwd;
-        // bigger chunks first (diagonal chunks carry the mean / sd work)
-        std::stable_sort(upd.begin(), upd.end(), [](const UpdChunk& a, const UpdChunk& b) {
-            return (a.k1 - a.k0) + a.diag > (b.k1 - b.k0) + b.diag;
-        });
-        p.h_upd = upd;
+        p.h_frb = frb;
+        p.n_frb = (int)frb.size();
+        p.h_upd = xcd_order(upd);
         p.upd_tiles = tiles;
         p.n_fwd = (int)fwd.size();
-        p.n_upd = (int)upd.size();
+        p.n_upd = (int)p.h_upd.size();
         const size_t xs = sizeof(float) * (size_t)S * p.rows_tot[r];
         p.ws_bytes = align256(xs) * 2 + 256;
     } else {
@@ -214,6 +260,8 @@ int psvi_debug_set(int32_t key, int32_t value) {
     switch (key) {
         case PSVI_DBG_NET_ABLATION: g_net_ablation = value; return 0;
         case PSVI_DBG_UPD_ABLATION: g_upd_ablation = value; return 0;
+        case PSVI_DBG_NET_SPLIT_BELOW: g_net_split_below = value; return 0;
+        case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }
 }
@@ -222,6 +270,7 @@ int psvi_debug_set_ptr(int32_t key, void* ptr) {
     switch (key) {
         case PSVI_DBG_NET_STAMPS: g_net_stamps = (unsigned long long*)ptr; return 0;
         case PSVI_DBG_UPD_STAMPS: g_upd_stamps = (unsigned long long*)ptr; return 0;
+        case PSVI_DBG_FWD_STAMPS: g_fwd_stamps = (unsigned long long*)ptr; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }
 }
@@ -249,7 +298,14 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
     int rc = build_plan(*p);
     if (!rc && have_dev) {
         // the only device allocations of the library: immutable work lists
-        if (!(rc = upload(p->h_fwd, &p->d_fwd))) rc = upload(p->h_upd, &p->d_upd);
+        if (!(rc = upload(p->h_fwd, &p->d_fwd)) && !(rc = upload(p->h_frb, &p->d_frb)))
+            rc = upload(p->h_upd, &p->d_upd);
+        if (!rc && p->n_fwd > 0) {
+            // split-K scratch of the sample phase (plan-owned, reused every step)
+            const size_t bytes = sizeof(float) * (size_t)p->n_fwd * p->d.S * kFwdRows;
+            if (hipMalloc((void**)&p->d_fwd_part, bytes) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the sample-phase scratch");
+        }
         p->on_device = rc == 0;
     }
     if (rc) {
@@ -263,6 +319,8 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
 int psvi_plan_destroy(psvi_plan* p) {
     if (!p) return 0;
     if (p->d_fwd) (void)hipFree(p->d_fwd);
+    if (p->d_frb) (void)hipFree(p->d_frb);
+    if (p->d_fwd_part) (void)hipFree(p->d_fwd_part);
     if (p->d_upd) (void)hipFree(p->d_upd);
     delete p;
     return 0;

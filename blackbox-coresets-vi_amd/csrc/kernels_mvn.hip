@@ -31,93 +31,192 @@ struct MvnLayerArgs {
 // ----------------------------------------------------------------- forward
 constexpr int FBK = 64;    // k (columns of L) per LDS stage
 constexpr int FST = 128;   // samples per pass: 4 waves x 32
+constexpr int FLD = FBK + 4;  // LDS row stride: 16-byte rows (float4 stores, ds_read_b128)
 
 struct FwdArgs {
     const FwdItem* items;
     const float* params;
     const float* eps;
-    float* x;         // x_shard [S][ldx]
+    float* part;      // split-K partial slots [n_items][S][32]
     int ldx, S;
+    int64_t e_total;  // floats in eps (load guards)
+    int abl;                     // diagnostics ablation mask (0 in production):
+                                 // 1 loads, 2 MFMAs, 4 x atomics
+    unsigned long long* stamps;  // diagnostics: 16 slots per workgroup
     MvnLayerArgs lay[kMaxL];
 };
 
-__global__ __launch_bounds__(256) void mvn_fwd_kernel(FwdArgs a) {
-    __shared__ float Es[FST][FBK + 1];  // eps  [s][k]
-    __shared__ float Ls[32][FBK + 1];   // corr [r][k]
+// Branch-free 16-byte loads (see the update kernel below for the rationale):
+// clamp the offset into the buffer for the load, shift back at consumption.
+__device__ __forceinline__ int fclamp4(int off, int lo, int hi) {
+    return off < lo ? lo : (off > hi - 4 ? hi - 4 : off);
+}
+__device__ __forceinline__ float4 fld4(const float* base, int off, int lo, int hi) {
+    return *reinterpret_cast<const float4*>(base + fclamp4(off, lo, hi));
+}
+__device__ __forceinline__ float4 ffix4(float4 v, int off, int lo, int hi) {
+    const int d = off - fclamp4(off, lo, hi);
+    if (d == 0) return v;  // VALU-only branch
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = i + d;
+        r[i] = k == 0 ? x[0] : k == 1 ? x[1] : k == 2 ? x[2] : k == 3 ? x[3] : 0.f;
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+}
+
+#define FWD_STAMP(k, val)                                                          \
+    do {                                                                           \
+        if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 16 + (k)] = (val); \
+    } while (0)
+
+// One item: rows [r0, r1) (<= kFwdRows) of L against columns [k0, k1) for all
+// samples: D[s][r] = sum_c eps[s][c] L[r][c] on v_mfma_f32_32x32x2_f32; wave w
+// owns 32 samples x all kFwdRows rows (FT = kFwdRows/32 accumulators), so one
+// eps fragment feeds FT MFMAs and the eps block (L2-resident, shared by every
+// item of the column range) is read once per kFwdRows rows.  Stages of 64 columns:
+// L rows (packed triangle, 256-byte runs) and eps rows go global -> registers
+// (float4) -> LDS, the next stage's loads in flight during this stage's
+// MFMAs.  k-permuted operand feed: one ds_read_b128 per operand per 4 MFMAs.
+// Each item stores its partial sums in its own slot; mvn_fwd_reduce_kernel
+// adds a row block's slots and mean + softplus(sd) eps into x (split-K
+// without atomics; float atomics from the k-chunks of a row block contend on
+// the same addresses).
+__global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float Es[FST * FLD];       // eps  [s][k]
+    __shared__ __attribute__((aligned(16))) float Ls[kFwdRows * FLD];  // corr [r][k]
+    FWD_STAMP(0, __builtin_amdgcn_s_memtime());
+    FWD_STAMP(6, __builtin_amdgcn_s_memrealtime());  // chip-wide 100 MHz clock
+    FWD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+    FWD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const FwdItem it = a.items[blockIdx.x];
     const int n = a.lay[it.layer].n;
-    const float* mean = a.params + a.lay[it.layer].poff;
-    const float* sd = mean + n;
-    const float* corr = mean + 2 * n;
-    const float* E = a.eps + a.lay[it.layer].eoff;   // [S][n]
+    const float* corr = a.params + a.lay[it.layer].poff + 2 * n;
+    const int corr_len = (int)((int64_t)(n - 1) * (n - 2) / 2);
+    const int eoff = (int)a.lay[it.layer].eoff;
+    const float* E = a.eps + eoff;   // [S][n]; the whole eps buffer is [-eoff, e_rem)
+    const int e_rem = (int)a.e_total - eoff;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
-    const rsrc_t rsL = make_rsrc(corr, ((int64_t)(n - 1) * (n - 2) / 2) * 4);
-    const rsrc_t rsE = make_rsrc(E, (int64_t)a.S * n * 4);
+    const int col4 = tid & 15, srow = tid >> 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int FT = kFwdRows / 32, LJ = kFwdRows / 16;
+    // this thread's staged L rows
+    int lrp[LJ];
+#pragma unroll
+    for (int j = 0; j < LJ; ++j) {
+        const int r = it.r0 + srow + 16 * j;
+        lrp[j] = r >= 1 ? (int)((int64_t)r * (r - 1) / 2) : 0;
+    }
+    const int klast = it.k0 + ((it.k1 - it.k0 - 1) / FBK) * FBK;  // last stage start
 
     for (int sb = 0; sb < a.S; sb += FST) {
-        floatx16 acc;
+        floatx16 acc[FT];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        for (int t = 0; t < FT; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
         const bool wave_live = sb + 32 * wv < a.S;
-        // register prefetch of stage kb
-        float lreg[FBK / 8], ereg[FBK / 2];
-        // L rows of this item and eps rows of this pass; loads outside the
-        // triangle / past S read 0 through the buffer range check.  eps
-        // columns past k1 need no mask: they meet zero L entries.
-        const int kk = tid % FBK, rq = tid / FBK;
+        float4 lreg[LJ], ereg[8];
+        auto eofs = [&](int j, int kb) { return min(sb + srow + 16 * j, a.S - 1) * n + kb + 4 * col4; };
         auto fetch = [&](int kb) {
-            const int c = kb + kk;
 #pragma unroll
-            for (int j = 0; j < FBK / 8; ++j) {
-                const int r = it.r0 + rq + 4 * j;
-                const bool ok = r < it.r1 && c < r && c < it.k1 && r <= n - 2;
-                lreg[j] = bload(rsL, ok ? (uint32_t)(((int64_t)r * (r - 1) / 2 + c) * 4) : kOOB);
+            for (int j = 0; j < LJ; ++j)
+                lreg[j] = fld4(corr, (a.abl & 1) ? 0 : lrp[j] + kb + 4 * col4, 0, corr_len);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ereg[j] = fld4(E, (a.abl & 1) ? 0 : eofs(j, kb), -eoff, e_rem);
+        };
+        auto stage = [&](int kb) {
+            const int c = kb + 4 * col4;
+#pragma unroll
+            for (int j = 0; j < LJ; ++j) {
+                // entries outside the item / triangle / column range are 0
+                const int r = it.r0 + srow + 16 * j;
+                const float4 v = ffix4(lreg[j], lrp[j] + c, 0, corr_len);
+                const bool rok = r < it.r1 && r <= n - 2;
+                float4 o;
+                o.x = rok && c + 0 < r && c + 0 < it.k1 ? v.x : 0.f;
+                o.y = rok && c + 1 < r && c + 1 < it.k1 ? v.y : 0.f;
+                o.z = rok && c + 2 < r && c + 2 < it.k1 ? v.z : 0.f;
+                o.w = rok && c + 3 < r && c + 3 < it.k1 ? v.w : 0.f;
+                *reinterpret_cast<float4*>(&Ls[(srow + 16 * j) * FLD + 4 * col4]) = o;
             }
 #pragma unroll
-            for (int j = 0; j < FBK / 2; ++j) {
-                const int srow = sb + rq + 4 * j;
-                ereg[j] = bload(rsE, (uint32_t)(((int64_t)srow * n + c) * 4));
+            for (int j = 0; j < 8; ++j) {
+                const bool live = sb + srow + 16 * j < a.S;
+                *reinterpret_cast<float4*>(&Es[(srow + 16 * j) * FLD + 4 * col4]) =
+                    live ? ffix4(ereg[j], eofs(j, kb), -eoff, e_rem) : z4;
             }
         };
         if (it.k0 < it.k1) fetch(it.k0);
         for (int kb = it.k0; kb < it.k1; kb += FBK) {
+            __syncthreads();  // previous stage's MFMAs done with the LDS
+            stage(kb);
             __syncthreads();
+            fetch(min(kb + FBK, klast));  // unconditional: keeps the vmcnt bookkeeping exact
+            if (kb == it.k0 && sb == 0) FWD_STAMP(1, __builtin_amdgcn_s_memtime());
+            if (wave_live && !(a.abl & 2)) {
+                // k permutation: per 8 columns, lane half h feeds k = kk + 4h + j to
+                // MFMA j (j = 0..3) for BOTH operands -- the same sum over k
+                const float* Ea = Es + (32 * wv + l32) * FLD + 4 * h;
+                const float* Lb = Ls + l32 * FLD + 4 * h;
 #pragma unroll
-            for (int j = 0; j < FBK / 8; ++j) Ls[rq + 4 * j][kk] = lreg[j];
+                for (int kk = 0; kk < FBK; kk += 8) {
+                    const float4 av = *reinterpret_cast<const float4*>(Ea + kk);
+                    float4 bv[FT];
 #pragma unroll
-            for (int j = 0; j < FBK / 2; ++j) Es[rq + 4 * j][kk] = ereg[j];
-            __syncthreads();
-            if (kb + FBK < it.k1) fetch(kb + FBK);
-            if (wave_live) {
+                    for (int t = 0; t < FT; ++t)
+                        bv[t] = *reinterpret_cast<const float4*>(Lb + 32 * t * FLD + kk);
 #pragma unroll
-                for (int kk = 0; kk < FBK; kk += 2) {
-                    const float av = Es[32 * wv + l32][kk + h];
-                    const float bv = Ls[l32][kk + h];
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+                    for (int t = 0; t < FT; ++t) {
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[t].x, acc[t], 0, 0, 0);
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[t].y, acc[t], 0, 0, 0);
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[t].z, acc[t], 0, 0, 0);
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[t].w, acc[t], 0, 0, 0);
+                    }
                 }
             }
         }
+        FWD_STAMP(2, __builtin_amdgcn_s_memtime());
         // D[i = s][j = r]: j = lane&31, i = (q&3) + 8(q>>2) + 4h
-        const int r = it.r0 + l32;
-        if (wave_live && r < it.r1) {
-            float base_m = 0.f, base_sd = 0.f;
-            if (it.k0 == 0) {
-                base_m = mean[r];
-                base_sd = softplus_f(sd[r]);
-            }
-            float* xrow = a.x + it.xcol + l32;
+        if (wave_live && !(a.abl & 4)) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int s = sb + 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * h;
-                if (s < a.S) {
-                    float val = acc[q];
-                    if (it.k0 == 0) val += base_m + base_sd * E[(int64_t)s * n + r];
-                    atomicAdd(xrow + (int64_t)s * a.ldx, val);
+            for (int t = 0; t < FT; ++t) {
+                if (it.r0 + 32 * t + l32 >= it.r1) continue;
+                float* slot = a.part + (size_t)it.slot * a.S * kFwdRows + 32 * t + l32;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int s = sb + 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * h;
+                    if (s < a.S) slot[(size_t)s * kFwdRows] = acc[t][q];
                 }
             }
         }
     }
+    FWD_STAMP(3, __builtin_amdgcn_s_memtime());
+    FWD_STAMP(7, __builtin_amdgcn_s_memrealtime());
 }
+
+// x[s][xcol + rr] = mean[r] + softplus(sd[r]) eps[s][r] + sum over the row
+// block's slots (r = r0 + rr); one workgroup per (row block, 256/kFwdRows
+// samples), coalesced along the rows.
+__global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* rbs,
+                                                             const float* part, FwdArgs a,
+                                                             float* x) {
+    const FwdRowBlock rb = rbs[blockIdx.x];
+    const int rr = threadIdx.x & (kFwdRows - 1);
+    const int s = blockIdx.y * (256 / kFwdRows) + threadIdx.x / kFwdRows;
+    if (s >= a.S || rr >= rb.R) return;
+    const int n = a.lay[rb.layer].n, r = rb.r0 + rr;
+    const float* mean = a.params + a.lay[rb.layer].poff;
+    float sum = mean[r] + softplus_f(mean[n + r]) * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
+    const float* p = part + (size_t)rb.slot0 * a.S * kFwdRows + (size_t)s * kFwdRows + rr;
+    for (int k = 0; k < rb.nk; ++k) sum += p[(size_t)k * a.S * kFwdRows];
+    x[(int64_t)s * a.ldx + rb.xcol + rr] = sum;
+}
+
+int g_fwd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_FWD_ABLATION, mask)
+unsigned long long* g_fwd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_FWD_STAMPS, buf)
 
 // ---------------------------------------------------------------- backward
 constexpr int UB = 64;    // band rows = c-block columns
@@ -205,14 +304,21 @@ __device__ __forceinline__ void upd_elem(const UpdArgs& a, int64_t pidx, float g
 // The diagonal c-block (columns = the band's rows) also yields sum_s G and
 // sum_s G*eps per row: the mean / sd update.
 constexpr int TLD = 68;   // LDS stride of the transposed accumulator tile
+// S <= 128: G resident (all samples), eps staged in halves of UEH samples
+// (52 KB of LDS: three workgroups per CU); S > 128: both staged per pass.
+constexpr int UEH = 64;
+template <bool MULTI>
 struct UpdShared {
     float Gs[USB * ULD];
-    float Es[USB * ULD];
+    float Es[(MULTI ? USB : UEH) * ULD];
     float red[2 * 4 * 64];
 };
 
-template <bool GRAD, bool MULTI>
-__device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, UpdShared& sh) {
+// MODE: 0 = S <= 64 (one eps half), 1 = S <= 128 (two halves), 2 = S > 128
+template <bool GRAD, int MODE>
+__device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
+                                          UpdShared<MODE == 2>& sh) {
+    constexpr bool MULTI = MODE == 2, TWOH = MODE == 1;
     float* Gs = sh.Gs;
     float* Es = sh.Es;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
@@ -257,6 +363,23 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, 
         }
     };
 
+    // S <= 128: eps halves of UEH samples (4 float4 per thread)
+    float4 ehreg[4];
+    auto load_Eh = [&](int ti, int hh) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            ehreg[j] = ld4u(E, eofs(hh * UEH + srow + 16 * j, ti), -eoff, e_rem);
+    };
+    auto stage_Eh = [&](int ti, int hh) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int sr = hh * UEH + srow + 16 * j;
+            const bool live = sr < a.S && !(a.abl & 1);
+            *reinterpret_cast<float4*>(&Es[(srow + 16 * j) * ULD + 4 * col4]) =
+                live ? fix4(ehreg[j], eofs(sr, ti), -eoff, e_rem) : z4;
+        }
+    };
+
     // epilogue rows: r_j = r0 + srow + 16 j, columns c0 + 4 col4 + (0..3)
     int rowp[4];
     bool rown[4];
@@ -298,6 +421,31 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, 
         // 16 samples per group (rows past S are staged as zeros up to USB)
         const float* Ea = Es + h * ULD + 32 * wc + l32;
         const float* Gb = Gs + h * ULD + 32 * wr + l32;
+        for (int kk = 0; kk < kend; kk += 16) {
+            float av[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                av[u] = Ea[(kk + 2 * u) * ULD];
+                bv[u] = Gb[(kk + 2 * u) * ULD];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+        }
+    };
+
+    // one eps half against the resident G (rows hh*UEH ..)
+    auto compute_h = [&](int ti, int hh) {
+        const int kend = (a.abl & 2) ? 0 : min(UEH, a.S - hh * UEH);
+        if (ti == kd) {
+            for (int s = 16 * wv; s < 16 * wv + 16 && s < kend; ++s) {
+                const float gv = Gs[(hh * UEH + s) * ULD + lane];
+                dgm += gv;
+                dgs = fmaf(gv, Es[s * ULD + lane], dgs);
+            }
+        }
+        const float* Ea = Es + h * ULD + 32 * wc + l32;
+        const float* Gb = Gs + (hh * UEH + h) * ULD + 32 * wr + l32;
         for (int kk = 0; kk < kend; kk += 16) {
             float av[8], bv[8];
 #pragma unroll
@@ -373,9 +521,13 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, 
     };
 
     if (!MULTI) {
-        // all samples in one pass: the band's G slice stays in LDS
+        // all samples in one pass: the band's G slice stays in LDS, eps
+        // comes in halves.  Loads are issued in the order they are consumed
+        // (vmcnt retires in order): second eps half, this c-block's corr/m/v,
+        // next c-block's first eps half -- the corr/m/v get both MFMA halves
+        // to land.
         load_G(0);
-        load_E(0, 0);
+        load_Eh(0, 0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {  // G slice once (its registers die here)
             const int sr = srow + 16 * j;
@@ -383,12 +535,23 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, 
                 sr < a.S && !(a.abl & 1) ? fix4(greg[j], goff(sr), 0, g_total) : z4;
         }
         for (int ti = 0; ti < nt; ++ti) {
-            stage(false, ti, 0);
+            stage_Eh(ti, 0);
             __syncthreads();
             if (ti == 0) UPD_STAMP(1, __builtin_amdgcn_s_memtime());
-            load_E(min(ti + 1, nt - 1), 0);
-            load_pmv(ti);
-            compute(ti, 0);
+            if (TWOH) {
+                load_Eh(ti, 1);
+                load_pmv(ti);
+                compute_h(ti, 0);
+                __syncthreads();
+                stage_Eh(ti, 1);
+                __syncthreads();
+                load_Eh(min(ti + 1, nt - 1), 0);
+                compute_h(ti, 1);
+            } else {
+                load_pmv(ti);
+                load_Eh(min(ti + 1, nt - 1), 0);
+                compute_h(ti, 0);
+            }
             __syncthreads();  // every wave done with Es: it takes the accumulator tile
             epilogue(ti);
             __syncthreads();  // tile read before the next staging overwrites Es
@@ -447,14 +610,14 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch, 
     }
 }
 
-template <bool GRAD, bool MULTI>
-__global__ __launch_bounds__(256, 2) void mvn_update_kernel(UpdArgs a) {
-    __shared__ __attribute__((aligned(16))) UpdShared sh;
+template <bool GRAD, int MODE>
+__global__ __launch_bounds__(256, MODE == 2 ? 2 : 3) void mvn_update_kernel(UpdArgs a) {
+    __shared__ __attribute__((aligned(16))) UpdShared<MODE == 2> sh;
     UPD_STAMP(0, __builtin_amdgcn_s_memtime());
     UPD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
     UPD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const UpdChunk ch = a.chunks[blockIdx.x];
-    upd_chunk<GRAD, MULTI>(a, ch, sh);
+    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE>(a, ch, sh);  // XCD padding chunks are empty
     UPD_STAMP(3, __builtin_amdgcn_s_memtime());
 }
 
@@ -475,14 +638,19 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     a.items = p.d_fwd;
     a.params = params;
     a.eps = eps;
-    a.x = x_shard;
+    a.part = p.d_fwd_part;
     a.ldx = p.rows_tot[p.rank];
     a.S = p.d.S;
+    a.e_total = p.Peps;
+    a.abl = g_fwd_ablation;
+    a.stamps = g_fwd_stamps;
     fill_layers(p, a.lay);
-    hipError_t e = hipMemsetAsync(x_shard, 0, sizeof(float) * (size_t)a.S * a.ldx, st);
-    if (e != hipSuccess) return e;
     if (p.n_fwd == 0) return hipSuccess;
+    // every x element is written by exactly one reduce thread: no memset
     hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd), dim3(256), 0, st, a);
+    constexpr int spb = 256 / kFwdRows;  // samples per reduce workgroup
+    hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb), dim3(256), 0,
+                       st, p.d_frb, p.d_fwd_part, a, x_shard);
     return hipGetLastError();
 }
 
@@ -513,13 +681,15 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
     fill_layers(p, a.lay);
     if (p.n_upd == 0) return hipSuccess;
     const dim3 grid(p.n_upd), block(256);
-    const bool multi = a.S > USB;  // more samples than one LDS pass holds
+    const int mode = a.S > USB ? 2 : a.S > UEH ? 1 : 0;  // samples per LDS pass
     if (grad_out) {
-        if (multi) hipLaunchKernelGGL((mvn_update_kernel<true, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((mvn_update_kernel<true, false>), grid, block, 0, st, a);
+        if (mode == 2) hipLaunchKernelGGL((mvn_update_kernel<true, 2>), grid, block, 0, st, a);
+        else if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<true, 1>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((mvn_update_kernel<true, 0>), grid, block, 0, st, a);
     } else {
-        if (multi) hipLaunchKernelGGL((mvn_update_kernel<false, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((mvn_update_kernel<false, false>), grid, block, 0, st, a);
+        if (mode == 2) hipLaunchKernelGGL((mvn_update_kernel<false, 2>), grid, block, 0, st, a);
+        else if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((mvn_update_kernel<false, 0>), grid, block, 0, st, a);
     }
     return hipGetLastError();
 }

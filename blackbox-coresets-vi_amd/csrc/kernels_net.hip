@@ -546,6 +546,8 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     return off;
 }
 
+int g_net_split_below = 96;  // diagnostics: psvi_debug_set(PSVI_DBG_NET_SPLIT_BELOW, n)
+
 size_t net_plan_geometry(psvi_plan& p) {
     // One workgroup per sample and all M pseudopoints when the samples alone
     // fill the chip (G gets plain stores: no memset, no atomics); otherwise
@@ -554,7 +556,7 @@ size_t net_plan_geometry(psvi_plan& p) {
     const int S_local = std::max(1, p.s_cnt[p.rank]);
     const int M = p.d.M;
     int mchunks = 1;
-    if (S_local < 96)
+    if (S_local < g_net_split_below)
         while (S_local * mchunks < 256 && (M + mchunks) / (mchunks + 1) >= 16) ++mchunks;
     for (;;) {
         const int mc = (M + mchunks - 1) / mchunks;

@@ -109,10 +109,18 @@ struct LayerInfo {
     int woff;       // offset of the layer in the per-sample weight space [0, n_tot)
 };
 
-// Full-cov forward work item: rows [r0, r0+32) of layer `layer` (global row
-// ids, clipped to the rank's row range), columns c in [k0, k1) of L.
+// Full-cov forward work item: rows [r0, r1) (<= kFwdRows) of layer `layer`
+// (global row ids, clipped to the rank's row range), columns c in [k0, k1) of L.
+constexpr int kFwdRows = 64;
 struct FwdItem {
     int layer, r0, r1, k0, k1, xcol;  // xcol: x_shard column of row r0
+    int slot;                         // partial-sum slot ([S][kFwdRows] floats) of this item
+};
+// Rows [r0, r0 + R) (R <= kFwdRows) of one layer: their x = sum of the nk partial
+// slots slot0 .. slot0 + nk - 1 (split-K over the columns of L, no atomics).
+struct FwdRowBlock {
+    int slot0, nk, R, xcol;
+    int layer, r0;  // absolute first row (the reduce adds mean + softplus(sd) eps)
 };
 // Full-cov update work item: the 64-row band [r0, r0+64) of layer `layer`
 // (r0 a multiple of 64; the rank owns rows [rlo, rhi)) against the c-blocks
@@ -148,6 +156,10 @@ struct psvi_plan {
     bool on_device = false;
     psvi::FwdItem* d_fwd = nullptr;
     int n_fwd = 0;
+    std::vector<psvi::FwdRowBlock> h_frb;
+    psvi::FwdRowBlock* d_frb = nullptr;
+    int n_frb = 0;
+    float* d_fwd_part = nullptr;  // split-K partial slots: n_fwd x S x 32 floats (plan-owned)
     psvi::UpdChunk* d_upd = nullptr;
     int n_upd = 0;
     int upd_tiles = 0;  // c-blocks over all chunks (work measure)

@@ -18,7 +18,9 @@
  * Conventions
  *   - Every pointer argument is a DEVICE pointer (fp32 unless stated) owned by
  *     the caller; the library never allocates device memory inside a step
- *     (only psvi_plan_create allocates its small immutable work lists).
+ *     (psvi_plan_create allocates its immutable work lists and the plan-owned
+ *     split-K scratch of the full-cov sample phase; a plan's calls must not
+ *     run concurrently on different streams).
  *   - Steps are stream-ordered and asynchronous on `stream` (a hipStream_t
  *     passed as void*; NULL = default stream); no host synchronisation inside.
  *   - Return 0 on success, <0 for an invalid argument / shape (PSVI_E*),
@@ -195,6 +197,15 @@ int psvi_debug_set(int32_t key, int32_t value);
                                     update-kernel workgroup (start, staged,
                                     MFMA done, end, HW_ID, XCC_ID, tile read,
                                     loads issued, LDS written)                 */
+#define PSVI_DBG_NET_SPLIT_BELOW 5 /* value: split each sample's pseudopoints over
+                                    several network workgroups when a rank has
+                                    fewer samples than this (plans created
+                                    afterwards; default 96)                    */
+#define PSVI_DBG_FWD_ABLATION 6  /* value: mask of full-cov sample-kernel parts to
+                                    skip (1 loads, 2 MFMAs, 4 x atomics)       */
+#define PSVI_DBG_FWD_STAMPS 7    /* ptr: device uint64 buffer, 16 slots per
+                                    sample-kernel workgroup (start, first stage,
+                                    MFMAs done, end, HW_ID, XCC_ID)            */
 int psvi_debug_set_ptr(int32_t key, void* ptr);
 
 #ifdef __cplusplus

@@ -60,6 +60,13 @@ def main():
         gs = torch.zeros(plan.xshard_count, device=dev)
         out["sample(memset+fwd)"] = timeit(lambda: plan.mvn_sample(eps, params, xs), iters)
         out["net(+memset)"] = timeit(lambda: plan.mvn_net(u, z, w, xs, gs, nll), iters)
+        if os.environ.get("NET_SPLIT"):
+            # pseudopoint split over workgroups: plans built after setting the knob
+            for below in (1000,):
+                plan.lib.psvi_debug_set(5, below)
+                p2 = InnerLoopPlan(fam, layers, S, M)
+                out[f"net split(<{below})"] = timeit(lambda: p2.mvn_net(u, z, w, xs, gs, nll), iters)
+                plan.lib.psvi_debug_set(5, 96)
         if os.environ.get("NET_ABLATION"):
             lib = plan.lib
             for mask in (1, 2, 4, 8, 16, 2 | 8, 1 | 2 | 4 | 8):
