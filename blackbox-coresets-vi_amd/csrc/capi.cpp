@@ -130,7 +130,7 @@ static std::vector<UpdChunk> xcd_order(const std::vector<UpdChunk>& in) {
     }
     std::vector<UpdChunk> out;
     out.reserve(len * kXcd);
-    const UpdChunk empty{0, 0, 0, 0, 0, 0, 0, 0};
+    const UpdChunk empty{0, 0, 0, 0, 0, 0, 0, 0, -1};
     for (size_t j = 0; j < len; ++j)
         for (int x = 0; x < kXcd; ++x) out.push_back(j < q[x].size() ? q[x][j] : empty);
     return out;
@@ -193,7 +193,8 @@ int build_plan(psvi_plan& p) {
     if (p.family == PSVI_FAMILY_FULLCOV) {
         std::vector<FwdItem> fwd;
         std::vector<UpdChunk> upd;
-        std::vector<FwdRowBlock> frb;
+        std::vector<FwdRowBlock> frb, ufrb;
+        int nslots = 0;
         // c-blocks per update chunk: about one chunk per workgroup slot
         // (256 CUs x 3 resident update workgroups), at least one
         int tiles = 0;
@@ -220,12 +221,17 @@ int build_plan(psvi_plan& p) {
                 }
                 frb.push_back(FwdRowBlock{slot0, (int)fwd.size() - slot0, r1 - r0, xc + (r0 - lo), l, r0});
             }
-            // bands of 64 absolute rows; c-blocks 0..b, the last one diagonal
+            // bands of 64 absolute rows; c-blocks 0..b, the last one diagonal.
+            // Each band is also a row block of the fused next-step sample: its
+            // chunks' partial slots are consecutive.
             for (int b = lo / 64; 64 * b < hi; ++b) {
+                const int slot0 = nslots;
                 for (int k0 = 0; k0 <= b; k0 += ch) {
                     const int k1 = std::min(b + 1, k0 + ch);
-                    upd.push_back(UpdChunk{l, 64 * b, k0, k1, lo, hi, xc - lo, k1 == b + 1});
+                    upd.push_back(UpdChunk{l, 64 * b, k0, k1, lo, hi, xc - lo, k1 == b + 1, nslots++});
                 }
+                const int r0 = std::max(64 * b, lo), r1 = std::min(64 * b + 64, hi);
+                ufrb.push_back(FwdRowBlock{slot0, nslots - slot0, r1 - r0, xc + (r0 - lo), l, r0});
             }
         }
         // longest forward items first
@@ -236,6 +242,12 @@ int build_plan(psvi_plan& p) {
         p.h_frb = frb;
         p.n_frb = (int)frb.size();
         p.h_upd = xcd_order(upd);
+        // fusion needs band-aligned row blocks (rank row ranges start at 0) and
+        // one LDS pass of samples
+        p.fuse_sample = p.world == 1 && S <= 128;
+        p.h_ufrb = ufrb;
+        p.n_ufrb = (int)ufrb.size();
+        p.n_uslots = nslots;
         p.upd_tiles = tiles;
         p.n_fwd = (int)fwd.size();
         p.n_upd = (int)p.h_upd.size();
@@ -306,6 +318,12 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
             if (hipMalloc((void**)&p->d_fwd_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the sample-phase scratch");
         }
+        if (!rc && p->fuse_sample && p->n_uslots > 0) {
+            const size_t bytes = sizeof(float) * (size_t)p->n_uslots * p->d.S * 64;
+            if ((rc = upload(p->h_ufrb, &p->d_ufrb)) == 0 &&
+                hipMalloc((void**)&p->d_upd_part, bytes) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the fused-sample scratch");
+        }
         p->on_device = rc == 0;
     }
     if (rc) {
@@ -321,10 +339,14 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_fwd) (void)hipFree(p->d_fwd);
     if (p->d_frb) (void)hipFree(p->d_frb);
     if (p->d_fwd_part) (void)hipFree(p->d_fwd_part);
+    if (p->d_ufrb) (void)hipFree(p->d_ufrb);
+    if (p->d_upd_part) (void)hipFree(p->d_upd_part);
     if (p->d_upd) (void)hipFree(p->d_upd);
     delete p;
     return 0;
 }
+
+static size_t loop_ws_bytes(const psvi_plan* p);
 
 int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
     if (!p || !value) return fail(PSVI_EINVAL, "null argument");
@@ -338,6 +360,7 @@ int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
         case PSVI_Q_ACC_COUNT: *value = p->acc_count; break;
         case PSVI_Q_ROWS_LOCAL: *value = p->rows_tot[r]; break;
         case PSVI_Q_XSHARD_COUNT: *value = (int64_t)p->d.S * p->rows_tot[r]; break;
+        case PSVI_Q_LOOP_WS_BYTES: *value = (int64_t)loop_ws_bytes(p); break;
         case PSVI_Q_XRECV_COUNT: *value = (int64_t)p->s_cnt[r] * p->n_tot; break;
         default: return fail(PSVI_EINVAL, "unknown query key");
     }
@@ -387,7 +410,7 @@ static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const
         if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
         HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x, g, elbo_out, st));
         HIP_TRY(launch_mvn_update(*p, eps, g, params, m, v, hp, elbo_out, grad_out, include_kl,
-                                  st));
+                                  nullptr, nullptr, st));
     }
     return 0;
 }
@@ -472,7 +495,88 @@ int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_s
     if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
     if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
     HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, grad_out,
-                              include_kl ? 1 : 0, as_stream(stream)));
+                              include_kl ? 1 : 0, nullptr, nullptr, as_stream(stream)));
+    return 0;
+}
+
+int psvi_mvn_phase_update_sample(const psvi_plan* p, const float* eps, const float* g_shard,
+                                 float* params, float* adam_m, float* adam_v,
+                                 const psvi_adam_hp* hp, double* kl_out, int32_t include_kl,
+                                 const float* eps_next, float* x_next, void* stream) {
+    if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!eps || !g_shard || !params || !eps_next || !x_next) return fail(PSVI_EINVAL, "null pointer");
+    if (!adam_m || !adam_v || !hp) return fail(PSVI_EINVAL, "null adam state");
+    if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, nullptr,
+                              include_kl ? 1 : 0, eps_next, x_next, as_stream(stream)));
+    return 0;
+}
+
+static int64_t eps_stride(const psvi_plan* p) { return (p->Peps + 3) / 4 * 4; }
+
+static size_t loop_ws_bytes(const psvi_plan* p) {
+    return align256(p->ws_bytes) + 2 * align256(sizeof(float) * (size_t)eps_stride(p));
+}
+
+int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                    const float* eps, uint64_t seed, uint64_t offset, int32_t T, float* params,
+                    float* adam_m, float* adam_v, const psvi_adam_hp* hp, double* elbo_out,
+                    void* ws, size_t ws_bytes, void* stream) {
+    if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (p->world != 1) return fail(PSVI_ESTATE, "inner loop needs world == 1 (use phases)");
+    if (!u || !z || !w || !params || !adam_m || !adam_v || !hp || !elbo_out)
+        return fail(PSVI_EINVAL, "null pointer");
+    if (T < 0) return fail(PSVI_EINVAL, "T must be >= 0");
+    if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (!eps && offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");
+    if (!ws || ws_bytes < loop_ws_bytes(p)) return fail(PSVI_ENOSPC, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    char* wsb = (char*)ws;
+    const int64_t es = eps_stride(p);
+    float* ebuf[2] = {(float*)(wsb + align256(p->ws_bytes)),
+                      (float*)(wsb + align256(p->ws_bytes) + align256(sizeof(float) * (size_t)es))};
+    // eps of step t: the caller's [T][EPS_COUNT] array, or Philox (seed, offset + t * stride)
+    auto eps_t = [&](int t) -> const float* {
+        if (eps) return eps + (size_t)t * p->Peps;
+        float* b = ebuf[t & 1];
+        return launch_randn(b, p->Peps, seed, offset + (uint64_t)t * es, st) == hipSuccess ? b
+                                                                                         : nullptr;
+    };
+    psvi_adam_hp h = *hp;
+    if (p->family == PSVI_FAMILY_MEANFIELD) {
+        for (int t = 0; t < T; ++t) {
+            const float* e = eps_t(t);
+            if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
+            h.step = hp->step + t;
+            if (int rc = step_impl(p, u, z, w, e, params, adam_m, adam_v, &h, elbo_out + t,
+                                   nullptr, 1, ws, st))
+                return rc;
+        }
+        return 0;
+    }
+    // full-cov: sample x_0, then per step net + update, the update also sampling
+    // the next step's x from the updated parameters (fused where the plan allows)
+    const size_t xs = sizeof(float) * (size_t)p->d.S * p->rows_tot[0];
+    float* x = (float*)wsb;
+    float* g = (float*)(wsb + align256(xs));
+    if (T == 0) return 0;
+    const float* e = eps_t(0);
+    if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
+    HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
+    for (int t = 0; t < T; ++t) {
+        h.step = hp->step + t;
+        HIP_TRY(hipMemsetAsync(elbo_out + t, 0, sizeof(double), st));
+        if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
+        HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x, g, elbo_out + t,
+                           st));
+        const float* en = t + 1 < T ? eps_t(t + 1) : nullptr;
+        if (t + 1 < T && !en) return fail(PSVI_EUNSUP, "randn launch failed");
+        HIP_TRY(launch_mvn_update(*p, e, g, params, adam_m, adam_v, &h, elbo_out + t, nullptr, 1,
+                                  en, en ? x : nullptr, st));
+        e = en;
+    }
     return 0;
 }
 

@@ -240,6 +240,9 @@ struct UpdArgs {
     unsigned long long* stamps;    // diagnostics: 16 slots per workgroup (nullptr in production)
     float inv_s0sq, log_s0;
     AdamC adam;
+    // fused next-step sample (FUSE kernels): partial x_next per chunk slot
+    const float* eps_next;
+    float* part;
     MvnLayerArgs lay[kMaxL];
 };
 
@@ -314,11 +317,16 @@ struct UpdShared {
     float red[2 * 4 * 64];
 };
 
-// MODE: 0 = S <= 64 (one eps half), 1 = S <= 128 (two halves), 2 = S > 128
-template <bool GRAD, int MODE>
+// MODE: 0 = S <= 64 (one eps half), 1 = S <= 128 (two halves), 2 = S > 128.
+// FUSE (Adam, MODE < 2): also the next step's sample from the updated L --
+// per c-block, x_next[s][r] += sum_c eps_next[s][c] L_new[r][c] on a second
+// MFMA GEMM (L_new tile through the LDS tile region, eps_next fragments
+// straight from L2 into registers), partial sums to the chunk's slot.
+template <bool GRAD, int MODE, bool FUSE>
 __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                                           UpdShared<MODE == 2>& sh) {
     constexpr bool MULTI = MODE == 2, TWOH = MODE == 1;
+    static_assert(!FUSE || (!GRAD && !MULTI), "fused sample: Adam mode, S <= 128");
     float* Gs = sh.Gs;
     float* Es = sh.Es;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
@@ -408,6 +416,42 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
     float dgm = 0.f, dgs = 0.f, klp = 0.f;
 
+    // ---- fused next-step sample state
+    floatx16 acc2[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc2[t][q] = 0.f;
+    float4 enreg[FUSE ? 8 : 1];
+    const bool wave_s = 32 * wv < a.S;  // this wave owns samples of the fused GEMM
+    const int es = min(32 * wv + l32, a.S - 1);
+    auto enofs = [&](int ti, int g) { return es * n + (ch.k0 + ti) * UB + 8 * g + 4 * h; };
+    auto load_En = [&](int ti) {
+        if (FUSE) {
+#pragma unroll
+            for (int g = 0; g < 8; ++g) enreg[g] = ld4u(a.eps_next + eoff, enofs(ti, g), -eoff, e_rem);
+        }
+    };
+    // x_next partial over one c-block: A = eps_next[s][c] (registers, k-permuted:
+    // lane half h holds c = 8g + 4h + j for MFMA j), B = L_new[r][c] from the tile
+    auto gemm2 = [&](int ti) {
+        if (FUSE && wave_s) {
+            const float* Lb = Es + l32 * TLD + 4 * h;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const float4 av = fix4(enreg[g], enofs(ti, g), -eoff, e_rem);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const float4 bv = *reinterpret_cast<const float4*>(Lb + 32 * t * TLD + 8 * g);
+                    acc2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc2[t], 0, 0, 0);
+                    acc2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc2[t], 0, 0, 0);
+                    acc2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc2[t], 0, 0, 0);
+                    acc2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc2[t], 0, 0, 0);
+                }
+            }
+        }
+    };
+
     auto compute = [&](int ti, int pi) {
         const int kend = (a.abl & 2) ? 0 : min(USB, a.S - pi * USB);
         if (ti == kd) {
@@ -474,7 +518,11 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int r = ch.r0 + srow + 16 * j;
-            if (!rown[j] || cb >= r || (a.abl & 8)) continue;
+            if (!rown[j] || cb >= r || (a.abl & 8)) {
+                if (FUSE)  // no L entries here: zeros for the fused sample GEMM
+                    *reinterpret_cast<float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]) = z4;
+                continue;
+            }
             const int o = rowp[j] + cb;
             const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
             const float4 p4 = (a.abl & 4) ? z4 : fix4(pq[j], o, 0, pcount);
@@ -499,6 +547,14 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                 }
             }
             float* dp = GRAD ? a.grad_out : a.params;
+            if (FUSE) {  // L_new row segment (strict lower part only)
+                float4 lv;
+                lv.x = cb + 0 < r ? pn[0] : 0.f;
+                lv.y = cb + 1 < r ? pn[1] : 0.f;
+                lv.z = cb + 2 < r ? pn[2] : 0.f;
+                lv.w = cb + 3 < r ? pn[3] : 0.f;
+                *reinterpret_cast<float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]) = lv;
+            }
             if (cb + 3 < r) {
                 *reinterpret_cast<float4*>(dp + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
                 if (!GRAD) {
@@ -541,6 +597,7 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
             if (TWOH) {
                 load_Eh(ti, 1);
                 load_pmv(ti);
+                load_En(ti);
                 compute_h(ti, 0);
                 __syncthreads();
                 stage_Eh(ti, 1);
@@ -549,11 +606,16 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                 compute_h(ti, 1);
             } else {
                 load_pmv(ti);
+                load_En(ti);
                 load_Eh(min(ti + 1, nt - 1), 0);
                 compute_h(ti, 0);
             }
             __syncthreads();  // every wave done with Es: it takes the accumulator tile
             epilogue(ti);
+            if (FUSE) {
+                __syncthreads();  // L_new tile complete
+                gemm2(ti);
+            }
             __syncthreads();  // tile read before the next staging overwrites Es
         }
     } else {
@@ -580,6 +642,17 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
         }
     }
     UPD_STAMP(2, __builtin_amdgcn_s_memtime());
+    if (FUSE && wave_s && ch.slot >= 0) {
+        // D2[i = s][j = r]: j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h
+        float* slot = a.part + (size_t)ch.slot * a.S * 64 + l32;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int s = 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (s < a.S) slot[(size_t)s * 64 + 32 * t] = acc2[t][q];
+            }
+    }
     klp *= 0.5f * a.inv_s0sq;
     if (ch.diag) {
         sh.red[wv * 64 + lane] = dgm;
@@ -610,14 +683,14 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     }
 }
 
-template <bool GRAD, int MODE>
-__global__ __launch_bounds__(256, MODE == 2 ? 2 : 3) void mvn_update_kernel(UpdArgs a) {
+template <bool GRAD, int MODE, bool FUSE = false>
+__global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_kernel(UpdArgs a) {
     __shared__ __attribute__((aligned(16))) UpdShared<MODE == 2> sh;
     UPD_STAMP(0, __builtin_amdgcn_s_memtime());
     UPD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
     UPD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const UpdChunk ch = a.chunks[blockIdx.x];
-    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE>(a, ch, sh);  // XCD padding chunks are empty
+    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE, FUSE>(a, ch, sh);  // XCD padding chunks are empty
     UPD_STAMP(3, __builtin_amdgcn_s_memtime());
 }
 
@@ -656,7 +729,8 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
-                             double* kl_out, float* grad_out, int include_kl, hipStream_t st) {
+                             double* kl_out, float* grad_out, int include_kl,
+                             const float* eps_next, float* x_next, hipStream_t st) {
     UpdArgs a{};
     a.chunks = p.d_upd;
     a.eps = eps;
@@ -682,6 +756,29 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
     if (p.n_upd == 0) return hipSuccess;
     const dim3 grid(p.n_upd), block(256);
     const int mode = a.S > USB ? 2 : a.S > UEH ? 1 : 0;  // samples per LDS pass
+    if (eps_next && !grad_out) {
+        if (!(p.fuse_sample && mode < 2)) {
+            // no fusion for this plan: update, then sample from the new params
+            hipError_t e = launch_mvn_update(p, eps, g_shard, params, m, v, hp, kl_out, nullptr,
+                                             include_kl, nullptr, nullptr, st);
+            return e != hipSuccess ? e : launch_mvn_fwd(p, eps_next, params, x_next, st);
+        }
+        a.eps_next = eps_next;
+        a.part = p.d_upd_part;
+        if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((mvn_update_kernel<false, 0, true>), grid, block, 0, st, a);
+        // x_next = mean' + softplus(sd') eps_next + sum of the band's chunk slots
+        FwdArgs f{};
+        f.params = params;
+        f.eps = eps_next;
+        f.ldx = p.rows_tot[p.rank];
+        f.S = p.d.S;
+        fill_layers(p, f.lay);
+        constexpr int spb = 256 / kFwdRows;
+        hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb), dim3(256),
+                           0, st, p.d_ufrb, p.d_upd_part, f, x_next);
+        return hipGetLastError();
+    }
     if (grad_out) {
         if (mode == 2) hipLaunchKernelGGL((mvn_update_kernel<true, 2>), grid, block, 0, st, a);
         else if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<true, 1>), grid, block, 0, st, a);

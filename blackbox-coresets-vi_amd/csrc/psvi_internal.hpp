@@ -129,6 +129,7 @@ struct FwdRowBlock {
 // also updates the band's mean and sd.  xcol: g_shard column of row r is xcol + r.
 struct UpdChunk {
     int layer, r0, k0, k1, rlo, rhi, xcol, diag;
+    int slot;  // fused next-step sample: partial-sum slot ([S][64] floats), -1 if none
 };
 
 struct NetArgs;  // kernels_net.hip
@@ -161,6 +162,13 @@ struct psvi_plan {
     int n_frb = 0;
     float* d_fwd_part = nullptr;  // split-K partial slots: n_fwd x S x 32 floats (plan-owned)
     psvi::UpdChunk* d_upd = nullptr;
+    // fused update + next-step sample (world == 1, S <= 128): one row block
+    // per 64-row band, one partial slot per chunk
+    bool fuse_sample = false;
+    std::vector<psvi::FwdRowBlock> h_ufrb;
+    psvi::FwdRowBlock* d_ufrb = nullptr;
+    int n_ufrb = 0, n_uslots = 0;
+    float* d_upd_part = nullptr;
     int n_upd = 0;
     int upd_tiles = 0;  // c-blocks over all chunks (work measure)
     // net kernel geometry
@@ -182,7 +190,8 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
                           float* x_shard, hipStream_t st);
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
-                             double* kl_out, float* grad_out, int include_kl, hipStream_t st);
+                             double* kl_out, float* grad_out, int include_kl,
+                             const float* eps_next, float* x_next, hipStream_t st);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);

@@ -26,6 +26,7 @@ Q_ACC_COUNT = 6
 Q_ROWS_LOCAL = 7
 Q_XSHARD_COUNT = 8
 Q_XRECV_COUNT = 9
+Q_LOOP_WS_BYTES = 10
 
 ERRORS = {-1: "PSVI_EINVAL", -2: "PSVI_ENOSPC", -3: "PSVI_EUNSUP", -4: "PSVI_ESTATE"}
 
@@ -72,6 +73,10 @@ SIGNATURES = {
     "psvi_mvn_phase_net": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "psvi_mvn_phase_update": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P,
                                      _I32, _P]),
+    "psvi_mvn_phase_update_sample": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P,
+                                            _I32, _P, _P, _P]),
+    "psvi_inner_loop": (_I32, [_P, _P, _P, _P, _P, _U64, _U64, _I32, _P, _P, _P,
+                               ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),
     "psvi_adam_update": (_I32, [_I64, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P]),
     "psvi_debug_set": (_I32, [_I32, _I32]),

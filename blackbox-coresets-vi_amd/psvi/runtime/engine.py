@@ -76,6 +76,8 @@ class InnerLoopPlan:
         self.rows_local = q(_lib.Q_ROWS_LOCAL)
         self.xshard_count = q(_lib.Q_XSHARD_COUNT)
         self.xrecv_count = q(_lib.Q_XRECV_COUNT)
+        self.loop_ws_bytes = q(_lib.Q_LOOP_WS_BYTES)
+        self.eps_stride = (self.eps_count + 3) // 4 * 4   # Philox offset per loop step
         self.n_tot = sum(i * o + o for i, o in layers)
 
     def _query(self, key):
@@ -129,6 +131,34 @@ class InnerLoopPlan:
                                        ctypes.byref(hp), _ptr(elbo_out), _ptr(ws),
                                        ws.numel(), _stream()), "psvi_inner_step")
         return elbo_out
+
+    def inner_loop(self, u, z, w, params, adam_m, adam_v, T, lr, kind="higher", step0=1,
+                   eps=None, seed=0, offset=0, elbo_out=None, ws=None):
+        """T chained inner steps (psvi_inner_loop).  eps: (T, eps_count) device
+        tensor, or None for in-library Philox draws (seed, offset + t * eps_stride).
+        Returns the (T,) float64 device tensor of negative ELBOs before each step."""
+        _need(u, "u", self.M * self.layers[0][0])
+        _need(z, "z", self.M, torch.int32)
+        _need(w, "w", self.M)
+        for t, n in ((params, "params"), (adam_m, "adam_m"), (adam_v, "adam_v")):
+            _need(t, n, self.param_count)
+        T = int(T)
+        if eps is not None:
+            _need(eps, "eps", T * self.eps_count)
+        if elbo_out is None:
+            elbo_out = torch.empty(max(T, 1), dtype=torch.float64, device=params.device)
+        _need(elbo_out, "elbo_out", None, torch.float64)
+        if elbo_out.numel() < T:
+            raise ValueError("elbo_out holds fewer than T doubles")
+        if ws is None or ws.numel() < self.loop_ws_bytes:
+            ws = torch.empty(self.loop_ws_bytes, dtype=torch.uint8, device=params.device)
+        hp = make_adam(lr, step0, kind)
+        check(self.lib.psvi_inner_loop(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps),
+                                       int(seed) & (2**64 - 1), int(offset), T, _ptr(params),
+                                       _ptr(adam_m), _ptr(adam_v), ctypes.byref(hp),
+                                       _ptr(elbo_out), _ptr(ws), ws.numel(), _stream()),
+              "psvi_inner_loop")
+        return elbo_out[:T]
 
     def elbo_grad(self, u, z, w, eps, params, include_kl=True, ws=None):
         self._inputs(u, z, w, eps)
@@ -186,13 +216,26 @@ class InnerLoopPlan:
               "psvi_mvn_phase_net")
 
     def mvn_update(self, eps, g_shard, params, adam_m=None, adam_v=None, step=1, lr=1e-3,
-                   kind="higher", kl_out=None, grad_out=None, include_kl=True):
+                   kind="higher", kl_out=None, grad_out=None, include_kl=True, eps_next=None,
+                   x_next=None):
+        """Full-cov update phase; with eps_next / x_next also the next step's
+        sample from the updated parameters (psvi_mvn_phase_update_sample)."""
         _need(eps, "eps", self.eps_count)
         _need(g_shard, "g_shard", self.xshard_count)
         _need(params, "params", self.param_count)
         if kl_out is not None:
             _need(kl_out, "kl_out", 1, torch.float64)
         hp = make_adam(lr, step, kind)
+        if eps_next is not None or x_next is not None:
+            if grad_out is not None:
+                raise ValueError("the fused next-step sample runs with the Adam update only")
+            _need(eps_next, "eps_next", self.eps_count)
+            _need(x_next, "x_next", self.xshard_count)
+            check(self.lib.psvi_mvn_phase_update_sample(
+                self.handle, _ptr(eps), _ptr(g_shard), _ptr(params), _ptr(adam_m), _ptr(adam_v),
+                ctypes.byref(hp), _ptr(kl_out), int(bool(include_kl)), _ptr(eps_next),
+                _ptr(x_next), _stream()), "psvi_mvn_phase_update_sample")
+            return
         check(self.lib.psvi_mvn_phase_update(self.handle, _ptr(eps), _ptr(g_shard),
                                              _ptr(params), _ptr(adam_m), _ptr(adam_v),
                                              ctypes.byref(hp), _ptr(kl_out), _ptr(grad_out),

@@ -102,6 +102,7 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_ROWS_LOCAL    7  /* full-cov: x/g columns owned (sum over layers)      */
 #define PSVI_Q_XSHARD_COUNT  8  /* full-cov: floats of x_shard / g_shard = S*ROWS_LOCAL */
 #define PSVI_Q_XRECV_COUNT   9  /* full-cov: floats of x_recv / g_send = S_LOCAL*n_tot */
+#define PSVI_Q_LOOP_WS_BYTES 10 /* workspace bytes for psvi_inner_loop                 */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
  * Samples are split in contiguous blocks; for FULLCOV the rows of every
@@ -136,6 +137,22 @@ int psvi_elbo_grad(const psvi_plan* plan, const float* u, const int32_t* z,
                    int32_t include_kl, double* elbo_out, float* grad_out,
                    void* ws, size_t ws_bytes, void* stream);
 
+/* T chained inner steps (world == 1): the loop the reference runs as
+ *   for t in range(T): diffopt.step(inner_elbo(fmodel))   (psvi_classes.py:549-555)
+ * with Adam steps hp->step .. hp->step + T - 1 on params/adam_m/adam_v in place.
+ * elbo_out[t] (T doubles) <- negative inner ELBO before step t.  eps: the T
+ * steps' noise as [T][EPS_COUNT] floats, or NULL to draw step t's noise in the
+ * library with psvi_randn(seed, offset + t * round_up(EPS_COUNT, 4)).  For
+ * full-cov plans each update also samples the next step's weights from the
+ * updated parameters (one fused kernel when S <= 128; the separate sample
+ * phase otherwise): the same numbers as T psvi_inner_step calls up to fp32
+ * summation order.  ws: PSVI_Q_LOOP_WS_BYTES. */
+int psvi_inner_loop(const psvi_plan* plan, const float* u, const int32_t* z,
+                    const float* w, const float* eps, uint64_t seed, uint64_t offset,
+                    int32_t T, float* params, float* adam_m, float* adam_v,
+                    const psvi_adam_hp* hp, double* elbo_out, void* ws, size_t ws_bytes,
+                    void* stream);
+
 /* ---- sharded phases (any world; the caller runs the collectives) ------------
  * MEANFIELD (sample-parallel, replicated params):
  *   acc (ACC_COUNT floats, zeroed by the call) <- [sum_s dW | sum_s dW*eps]
@@ -169,6 +186,14 @@ int psvi_mvn_phase_update(const psvi_plan* plan, const float* eps,
                           const float* g_shard, float* params, float* adam_m,
                           float* adam_v, const psvi_adam_hp* hp, double* kl_out,
                           float* grad_out, int32_t include_kl, void* stream);
+/* update (Adam) followed by the next step's sample phase from the updated
+ * parameters: x_next[S][ROWS_LOCAL] <- mean' + L' eps_next for this rank's
+ * rows.  One fused kernel when the plan allows (world == 1, S <= 128). */
+int psvi_mvn_phase_update_sample(const psvi_plan* plan, const float* eps,
+                                 const float* g_shard, float* params, float* adam_m,
+                                 float* adam_v, const psvi_adam_hp* hp, double* kl_out,
+                                 int32_t include_kl, const float* eps_next,
+                                 float* x_next, void* stream);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] ~ N(0,1), Philox4x32-10 counter (seed, offset + i) + Box-Muller.

@@ -182,3 +182,88 @@ def test_randn_moments_and_determinism():
     d = torch.empty((1 << 22) - 1024, device=DEV)
     randn_(d, seed=1234, offset=1024)
     assert torch.equal(d, a[1024:])
+
+
+@pytest.mark.parametrize("name", [n for n in NAMES if load_fixture(n)["cfg"]["family"] == "mvn"])
+def test_fused_update_sample_equals_separate(name):
+    """psvi_mvn_phase_update_sample == update, then sample from the new params."""
+    f = load_fixture(name)
+    cfg, plan, u, z, w = _setup(f)
+    eps0, eps1 = _t(f["eps"][0]), _t(f["eps"][1])
+    p1 = _t(f["params0"])
+    xs = torch.empty(plan.xshard_count, device=DEV)
+    gs = torch.empty(plan.xshard_count, device=DEV)
+    nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.mvn_sample(eps0, p1, xs)
+    plan.mvn_net(u, z, w, xs, gs, nll)
+    p2 = p1.clone()
+    m1, v1 = torch.zeros_like(p1), torch.zeros_like(p1)
+    m2, v2 = torch.zeros_like(p1), torch.zeros_like(p1)
+    k1 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    k2 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.mvn_update(eps0, gs, p1, m1, v1, step=1, lr=cfg["lr"], kl_out=k1)
+    x1 = torch.empty_like(xs)
+    plan.mvn_sample(eps1, p1, x1)
+    x2 = torch.full_like(xs, float("nan"))
+    plan.mvn_update(eps0, gs, p2, m2, v2, step=1, lr=cfg["lr"], kl_out=k2, eps_next=eps1,
+                    x_next=x2)
+    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    assert rel(k1.item(), k2.item()) < 1e-12
+    assert torch.isfinite(x2).all()
+    assert l2rel(x2.cpu().numpy(), x1.cpu().numpy()) < 1e-6
+    assert (x2 - x1).abs().max().item() <= 1e-5 * x1.abs().max().item()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_inner_loop_api_matches_oracle(name):
+    """psvi_inner_loop (T chained steps, fused next-step sampling) with the
+    reference's eps == the oracle trajectory and the reference's ELBOs."""
+    f = load_fixture(name)
+    cfg, plan, u, z, w = _setup(f)
+    params = _t(f["params0"])
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    eps = _t(np.ascontiguousarray(f["eps"]).reshape(-1))
+    elbos = plan.inner_loop(u, z, w, params, m, v, cfg["T"], cfg["lr"], adam_kind(cfg), eps=eps)
+    o_elbo, _, o_traj, _, _ = O.run_inner_loop(
+        cfg["family"], cfg["layers"], f["params0"], f["u"], f["z"], f["w"], f["eps"], cfg["S"],
+        cfg["lr"], adam_kind(cfg))
+    e = elbos.cpu().numpy()
+    for t in range(cfg["T"]):
+        assert rel(e[t], o_elbo[t]) < 1e-5 and rel(e[t], f["elbo"][t]) < 1e-5, t
+    p = params.cpu().numpy()
+    assert np.abs(p - o_traj[-1]).max() < 0.5 * cfg["lr"]
+    assert l2rel(p, o_traj[-1]) < 1e-5 and l2rel(p, f["params"][-1]) < 1e-5
+
+
+@pytest.mark.parametrize("family,layers,S,M", [
+    ("fullcov", [(64, 40), (40, 40), (40, 2)], 128, 100),
+    ("fullcov", [(9, 5), (5, 3)], 40, 7),
+    ("meanfield", [(2, 100), (100, 4)], 32, 50)])
+def test_inner_loop_philox_equals_stepwise(family, layers, S, M):
+    """Philox-drawn loop == the same draws fed step by step through psvi_inner_step."""
+    from psvi.runtime import InnerLoopPlan, randn_
+
+    plan = InnerLoopPlan(family, layers, S, M)
+    g = torch.Generator().manual_seed(S + M)
+    u = torch.randn(M, layers[0][0], generator=g).to(DEV)
+    z = torch.randint(0, layers[-1][1], (M,), generator=g).to(torch.int32).to(DEV)
+    w = torch.full((M,), 8.0, device=DEV)
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        parts += [0.1 * torch.randn(n, generator=g), torch.full((n,), -3.0)]
+        if family == "fullcov":
+            parts.append(1e-3 * torch.randn((n - 1) * (n - 2) // 2, generator=g))
+    p0 = torch.cat(parts).to(DEV)
+    T = 4
+    pa, ma, va = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+    ea = plan.inner_loop(u, z, w, pa, ma, va, T, 1e-3, seed=7, offset=0)
+    pb, mb, vb = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+    eps = torch.empty(plan.eps_count, device=DEV)
+    ws = plan.workspace()
+    eb = []
+    for t in range(T):
+        randn_(eps, 7, t * plan.eps_stride)
+        eb.append(plan.inner_step(u, z, w, eps, pb, mb, vb, step=t + 1, lr=1e-3, ws=ws).item())
+    assert np.allclose(ea.cpu().numpy(), eb, rtol=1e-6, atol=0)
+    assert l2rel(pa.cpu().numpy(), pb.cpu().numpy()) < 1e-6

@@ -79,6 +79,21 @@ def main():
             plan.mvn_update(eps, gs, params, m, v, step=st[0], lr=1e-3, kl_out=nll)
             st[0] += 1
         out["update"] = timeit(upd, iters)
+        eps2 = torch.empty_like(eps)
+        randn_(eps2, 2)
+        x2 = torch.empty_like(xs)
+
+        def upd_smp():
+            plan.mvn_update(eps, gs, params, m, v, step=st[0], lr=1e-3, kl_out=nll, eps_next=eps2,
+                            x_next=x2)
+            st[0] += 1
+        out["update+next sample (fused)"] = timeit(upd_smp, iters)
+        T = 20
+        elb = torch.empty(T, dtype=torch.float64, device=dev)
+        lws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+        out["inner_loop per step (T=20, Philox)"] = timeit(
+            lambda: plan.inner_loop(u, z, w, params, m, v, T, 1e-3, seed=3, elbo_out=elb, ws=lws),
+            max(5, iters // T)) / T
         grad = torch.empty_like(params)
         out["update(grad mode)"] = timeit(
             lambda: plan.mvn_update(eps, gs, params, grad_out=grad, kl_out=nll), iters)
