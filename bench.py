@@ -55,6 +55,16 @@ def reference_init_params(n_layers_sizes, device):
     return torch.cat(parts).to(device)
 
 
+def algorithmic_work_fused(S):
+    """update kernel with the fused next-step sample (world == 1): the update's
+    traffic plus eps_next read and x_next written, and a second triangular GEMM
+    (x_next = L' eps_next)."""
+    w = algorithmic_work(S)
+    n_tot = sum(i * o + o for i, o in LAYERS)
+    return dict(bytes=w["update"]["bytes"] + 8 * S * n_tot,
+                flops=w["update"]["flops"] + w["sample"]["flops"])
+
+
 def algorithmic_work(S, rows_frac=1.0):
     """Per-launch algorithmic bytes / flops of the two dominant kernels
     (SURVEY.md §8(d)); rows_frac = this rank's share of the rows (nnz).
@@ -72,13 +82,14 @@ def algorithmic_work(S, rows_frac=1.0):
                 sample=dict(bytes=fwd_bytes, flops=fwd_flops))
 
 
-def pmc_traffic(kernel, path=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")):
+    """HBM bytes per launch of the listed kernels (summed: the phase the
+    roofline times) from the committed rocprofv3 PMC summary
     (tools/pmc_session.sh -> tools/pmc_report.py --json: separate FETCH_SIZE /
     WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction), or None."""
     try:
-        d = json.load(open(path))
-        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+        d = json.load(open(path))["kernels"]
+        return int(sum(d[k]["hbm_bytes_per_launch"] for k in kernels))
     except Exception:
         return None
 
@@ -156,6 +167,7 @@ def main():
     m = torch.zeros_like(params)
     v = torch.zeros_like(params)
     eps = torch.empty(plan.eps_count, device=dev)
+    eps_b = [eps, torch.empty(plan.eps_count, device=dev)]  # this step / next step (world 1)
     eps_stride = (plan.eps_count + 3) // 4 * 4
     f32 = dict(dtype=torch.float32, device=dev)
     if world == 1:
@@ -166,18 +178,23 @@ def main():
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
 
     def one_step(k, timed):
-        randn_(eps, seed=20251015, offset=k * eps_stride)
         t = k + 1  # Adam step of one long inner loop (never reset here)
         e = ev[k - args.warmup] if timed else None
         if world == 1:
+            # steady state of psvi_inner_loop: this step's x was sampled by the
+            # previous update (fused); draw the next step's eps, net, update +
+            # next sample
+            cur, nxt = eps_b[k & 1], eps_b[(k + 1) & 1]
             if e: e[0].record()
-            plan.mvn_sample(eps, params, xs)
+            randn_(nxt, seed=20251015, offset=(k + 1) * eps_stride)
             if e: e[1].record()
             plan.mvn_net(u, z, w, xs, gs, parts[k, 0:1])
             if e: e[2].record()
-            plan.mvn_update(eps, gs, params, m, v, step=t, lr=LR, kl_out=parts[k, 1:2])
+            plan.mvn_update(cur, gs, params, m, v, step=t, lr=LR, kl_out=parts[k, 1:2],
+                            eps_next=nxt, x_next=xs)
             if e: e[3].record()
         else:
+            randn_(eps, seed=20251015, offset=k * eps_stride)
             if e: e[0].record()
             loop.phase_sample(eps, params)
             if e: e[1].record()
@@ -189,6 +206,9 @@ def main():
             if e: e[3].record()
             parts[k].copy_(loop.parts)
 
+    if world == 1:  # x_0 of the loop
+        randn_(eps_b[0], seed=20251015, offset=0)
+        plan.mvn_sample(eps_b[0], params, xs)
     for k in range(args.warmup):
         one_step(k, False)
     torch.cuda.synchronize()
@@ -209,9 +229,10 @@ def main():
         elapsed = float(tt.item())
 
     # per-phase device time (HIP events on the launch stream)
-    ph = {"sample": [], "exchange+net": [], "update": []}
+    first = "randn(next eps)" if world == 1 else "sample"
+    ph = {first: [], "exchange+net": [], "update": []}
     for e in ev:
-        ph["sample"].append(e[0].elapsed_time(e[1]))
+        ph[first].append(e[0].elapsed_time(e[1]))
         ph["exchange+net"].append(e[1].elapsed_time(e[2]))
         ph["update"].append(e[2].elapsed_time(e[3]))
     avg_ms = {k: sum(x) / len(x) for k, x in ph.items()}
@@ -222,27 +243,42 @@ def main():
 
     steps_per_s = args.steps / elapsed
     value = steps_per_s * (S / S_PER_GPU)
-    work = algorithmic_work(S, rows_frac)
     upd_s = avg_ms["update"] * 1e-3
-    smp_s = avg_ms["sample"] * 1e-3
-    kernels = {
-        "mvn_update_kernel": dict(avg_us=avg_ms["update"] * 1e3,
-                                  gbs=work["update"]["bytes"] / upd_s / 1e9,
-                                  tflops=work["update"]["flops"] / upd_s / 1e12),
-        "mvn_fwd_kernel": dict(avg_us=avg_ms["sample"] * 1e3,
-                               gbs=work["sample"]["bytes"] / smp_s / 1e9,
-                               tflops=work["sample"]["flops"] / smp_s / 1e12),
-        "net_kernel(+exchange)": dict(avg_us=avg_ms["exchange+net"] * 1e3),
-    }
-    achieved = work["update"]["bytes"] / upd_s / 1e9
-    roofline = dict(bound="hbm", kernel="mvn_update_kernel", achieved=round(achieved, 1),
-                    peak=HBM_PEAK_GBS, unit="GB/s", frac=round(achieved / HBM_PEAK_GBS, 4),
-                    traffic=pmc_traffic("mvn_update_kernel"),
-                    algorithmic_bytes_per_launch=int(work["update"]["bytes"]),
+    if world == 1:
+        # dominant kernel: the update with the fused next-step sample (plus its
+        # small slot-reduce kernel, inside the same event pair)
+        wk = algorithmic_work_fused(S)
+        hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+        kname = "mvn_update_kernel<fused next-step sample> + mvn_fwd_reduce_kernel"
+        kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
+                               tflops=wk["flops"] / upd_s / 1e12),
+                   "net_kernel": dict(avg_us=avg_ms["exchange+net"] * 1e3),
+                   "randn_kernel": dict(avg_us=avg_ms[first] * 1e3)}
+    else:
+        work = algorithmic_work(S, rows_frac)
+        wk = work["update"]
+        hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+        kname = "mvn_update_kernel"
+        smp_s = avg_ms["sample"] * 1e-3
+        kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
+                               tflops=wk["flops"] / upd_s / 1e12),
+                   "mvn_fwd_kernel+reduce": dict(avg_us=avg_ms["sample"] * 1e3,
+                                                 tflops=work["sample"]["flops"] / smp_s / 1e12),
+                   "net_kernel(+exchange)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
+    if hbm_s >= mfma_s:
+        roofline = dict(bound="hbm", achieved=round(wk["bytes"] / upd_s / 1e9, 1),
+                        peak=HBM_PEAK_GBS, unit="GB/s")
+    else:
+        roofline = dict(bound="mfma", achieved=round(wk["flops"] / upd_s / 1e12, 2),
+                        peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s")
+    roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
+                    traffic=pmc_traffic(["mvn_update_kernel", "mvn_fwd_reduce_kernel"]
+                                        if world == 1 else ["mvn_update_kernel"]),
+                    kernel=kname, algorithmic_bytes_per_launch=int(wk["bytes"]),
+                    algorithmic_flops_per_launch=int(wk["flops"]),
+                    floors_us=dict(hbm=round(hbm_s * 1e6, 2), mfma=round(mfma_s * 1e6, 2)),
                     kernels={k: {kk: round(vv, 2) for kk, vv in d.items()}
-                             for k, d in kernels.items()},
-                    mfma_frac_fwd=round(kernels["mvn_fwd_kernel"]["tflops"] /
-                                        FP32_MFMA_PEAK_TFLOPS, 4))
+                             for k, d in kernels.items()})
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_budget)

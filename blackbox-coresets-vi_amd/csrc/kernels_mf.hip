@@ -177,14 +177,14 @@ __global__ __launch_bounds__(256) void randn_kernel(float* __restrict__ out, int
         float r[4];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            // u1 in (0, 1], u2 in [0, 1)
+            // Box-Muller on the native transcendentals: u1 in (0, 1], u2 in [0, 1);
+            // v_log_f32 is log2, v_sin/v_cos_f32 take revolutions (sin(2 pi u2))
             const float u1 = ((float)(c[2 * j] >> 8) + 1.0f) * (1.0f / 16777216.0f);
             const float u2 = (float)(c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
-            const float rad = sqrtf(-2.0f * logf(u1));
-            float sn, cs;
-            sincosf(6.283185307179586f * u2, &sn, &cs);
-            r[2 * j] = rad * cs;
-            r[2 * j + 1] = rad * sn;
+            const float rad =
+                __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+            r[2 * j] = rad * __builtin_amdgcn_cosf(u2);
+            r[2 * j + 1] = rad * __builtin_amdgcn_sinf(u2);
         }
         const int64_t base = q * 4;
         if (VEC && base + 3 < n) {

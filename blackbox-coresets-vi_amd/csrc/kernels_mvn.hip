@@ -211,8 +211,17 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
     const float* mean = a.params + a.lay[rb.layer].poff;
     float sum = mean[r] + softplus_f(mean[n + r]) * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
     const float* p = part + (size_t)rb.slot0 * a.S * kFwdRows + (size_t)s * kFwdRows + rr;
-    for (int k = 0; k < rb.nk; ++k) sum += p[(size_t)k * a.S * kFwdRows];
-    x[(int64_t)s * a.ldx + rb.xcol + rr] = sum;
+    const size_t st = (size_t)a.S * kFwdRows;
+    // 4 independent loads in flight per thread; summation order k = 0, 1, ... kept per
+    // partial so the result does not depend on the unroll
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 4 <= rb.nk; k += 4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s4[i] += p[(k + i) * st];
+    }
+    for (int i = 0; k + i < rb.nk; ++i) s4[i] += p[(k + i) * st];
+    x[(int64_t)s * a.ldx + rb.xcol + rr] = sum + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
 }
 
 int g_fwd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_FWD_ABLATION, mask)

@@ -546,7 +546,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     return off;
 }
 
-int g_net_split_below = 96;  // diagnostics: psvi_debug_set(PSVI_DBG_NET_SPLIT_BELOW, n)
+int g_net_split_below = 256;  // split when a rank has fewer samples than CUs (psvi_debug_set(PSVI_DBG_NET_SPLIT_BELOW, n))
 
 size_t net_plan_geometry(psvi_plan& p) {
     // One workgroup per sample and all M pseudopoints when the samples alone

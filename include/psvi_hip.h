@@ -225,7 +225,7 @@ int psvi_debug_set(int32_t key, int32_t value);
 #define PSVI_DBG_NET_SPLIT_BELOW 5 /* value: split each sample's pseudopoints over
                                     several network workgroups when a rank has
                                     fewer samples than this (plans created
-                                    afterwards; default 96)                    */
+                                    afterwards; default 256)                   */
 #define PSVI_DBG_FWD_ABLATION 6  /* value: mask of full-cov sample-kernel parts to
                                     skip (1 loads, 2 MFMAs, 4 x atomics)       */
 #define PSVI_DBG_FWD_STAMPS 7    /* ptr: device uint64 buffer, 16 slots per

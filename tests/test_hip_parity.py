@@ -175,6 +175,11 @@ def test_randn_moments_and_determinism():
     assert torch.equal(a, b)
     assert torch.isfinite(a).all()
     assert abs(a.mean().item()) < 3e-3 and abs(a.std().item() - 1) < 3e-3
+    # N(0,1) shape: tail probabilities and the fourth moment
+    for k, p in ((1.0, 0.3173105), (2.0, 0.0455003), (3.0, 0.0026998)):
+        frac = (a.abs() > k).float().mean().item()
+        assert abs(frac - p) < 5 * (p * (1 - p) / a.numel()) ** 0.5 + 1e-5, (k, frac)
+    assert abs((a.double() ** 4).mean().item() - 3.0) < 0.02
     c = torch.empty(1 << 22, device=DEV)
     randn_(c, seed=1235, offset=0)
     assert not torch.equal(a, c)
