@@ -156,6 +156,14 @@ int build_plan(psvi_plan& p) {
     }
     p.P = po;
     p.Peps = eo;
+    int64_t tb = 0;
+    for (int l = 0; l < p.L; ++l) {
+        LayerInfo& li = p.lay[l];
+        li.nb = p.family == PSVI_FAMILY_FULLCOV ? (li.n - 1) / 64 + 1 : 0;
+        li.tbase = tb;
+        tb += (int64_t)li.nb * (li.nb + 1) / 2;
+    }
+    p.tiles_total = tb;
     p.n_tot = wo;
     // sample shards
     for (int q = 0; q < p.world; ++q) {
@@ -347,6 +355,7 @@ int psvi_plan_destroy(psvi_plan* p) {
 }
 
 static size_t loop_ws_bytes(const psvi_plan* p);
+static size_t tiled_floats(const psvi_plan* p);
 
 int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
     if (!p || !value) return fail(PSVI_EINVAL, "null argument");
@@ -361,6 +370,7 @@ int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
         case PSVI_Q_ROWS_LOCAL: *value = p->rows_tot[r]; break;
         case PSVI_Q_XSHARD_COUNT: *value = (int64_t)p->d.S * p->rows_tot[r]; break;
         case PSVI_Q_LOOP_WS_BYTES: *value = (int64_t)loop_ws_bytes(p); break;
+        case PSVI_Q_TILED_FLOATS: *value = (int64_t)tiled_floats(p); break;
         case PSVI_Q_XRECV_COUNT: *value = (int64_t)p->s_cnt[r] * p->n_tot; break;
         default: return fail(PSVI_EINVAL, "unknown query key");
     }
@@ -515,8 +525,42 @@ int psvi_mvn_phase_update_sample(const psvi_plan* p, const float* eps, const flo
 
 static int64_t eps_stride(const psvi_plan* p) { return (p->Peps + 3) / 4 * 4; }
 
+// tiled corr/m/v state: full-cov, world 1, one LDS pass of samples
+static bool tiled_ok(const psvi_plan* p) {
+    return p->family == PSVI_FAMILY_FULLCOV && p->fuse_sample && p->tiles_total > 0;
+}
+static size_t tiled_floats(const psvi_plan* p) {
+    return tiled_ok(p) ? 3 * (size_t)p->tiles_total * 4096 : 0;
+}
+
 static size_t loop_ws_bytes(const psvi_plan* p) {
-    return align256(p->ws_bytes) + 2 * align256(sizeof(float) * (size_t)eps_stride(p));
+    return align256(p->ws_bytes) + 2 * align256(sizeof(float) * (size_t)eps_stride(p)) +
+           align256(sizeof(float) * tiled_floats(p));
+}
+
+int psvi_mvn_tiled_convert(const psvi_plan* p, float* params, float* adam_m, float* adam_v,
+                           float* tstate, int32_t to_tiled, void* stream) {
+    if (!p || !tiled_ok(p)) return fail(PSVI_EUNSUP, "plan has no tiled state (full-cov, world 1, S <= 128)");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!params || !adam_m || !adam_v || !tstate) return fail(PSVI_EINVAL, "null pointer");
+    HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, tstate, to_tiled != 0,
+                                    as_stream(stream)));
+    return 0;
+}
+
+int psvi_mvn_phase_update_tiled(const psvi_plan* p, const float* eps, const float* g_shard,
+                                float* params, float* adam_m, float* adam_v, float* tstate,
+                                const psvi_adam_hp* hp, double* kl_out, int32_t include_kl,
+                                const float* eps_next, float* x_next, void* stream) {
+    if (!p || !tiled_ok(p)) return fail(PSVI_EUNSUP, "plan has no tiled state (full-cov, world 1, S <= 128)");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!eps || !g_shard || !params || !adam_m || !adam_v || !tstate || !hp)
+        return fail(PSVI_EINVAL, "null pointer");
+    if (!eps_next != !x_next) return fail(PSVI_EINVAL, "eps_next and x_next go together");
+    if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, nullptr,
+                              include_kl ? 1 : 0, eps_next, x_next, as_stream(stream), tstate));
+    return 0;
 }
 
 int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
@@ -561,10 +605,15 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     const size_t xs = sizeof(float) * (size_t)p->d.S * p->rows_tot[0];
     float* x = (float*)wsb;
     float* g = (float*)(wsb + align256(xs));
+    // corr / m / v live in the tiled layout for the whole loop when the plan allows
+    float* ts = tiled_ok(p) ? (float*)(wsb + align256(p->ws_bytes) +
+                                       2 * align256(sizeof(float) * (size_t)es))
+                            : nullptr;
     if (T == 0) return 0;
     const float* e = eps_t(0);
     if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
     HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
+    if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st));
     for (int t = 0; t < T; ++t) {
         h.step = hp->step + t;
         HIP_TRY(hipMemsetAsync(elbo_out + t, 0, sizeof(double), st));
@@ -574,9 +623,10 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         const float* en = t + 1 < T ? eps_t(t + 1) : nullptr;
         if (t + 1 < T && !en) return fail(PSVI_EUNSUP, "randn launch failed");
         HIP_TRY(launch_mvn_update(*p, e, g, params, adam_m, adam_v, &h, elbo_out + t, nullptr, 1,
-                                  en, en ? x : nullptr, st));
+                                  en, en ? x : nullptr, st, ts));
         e = en;
     }
+    if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, false, st));
     return 0;
 }
 

@@ -26,7 +26,18 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 struct MvnLayerArgs {
     int n;
     int64_t poff, eoff;
+    int64_t tbase;  // tiled layout: first tile of the layer
 };
+
+// Tiled corr/m/v (world == 1 inner loops): tile (b, k <= b) of a layer holds
+// rows [64b, 64b+64) x columns [64k, 64k+64) of L's strict lower part (0
+// elsewhere) in the update MFMA's fragment order: wave w = 2 wr + wc, column
+// group g, lane = 32 h + l32 hold the float4 of row 64b + 32 wr + l32, columns
+// 64k + 32 wc + 8 g + 4 h .. +3, at ((w * 4 + g) * 64 + lane) * 4.  Every
+// wave instruction of the update then moves 1 KB of contiguous memory.
+__device__ __forceinline__ int64_t tile_index(const MvnLayerArgs& l, int b, int k) {
+    return l.tbase + (int64_t)b * (b + 1) / 2 + k;
+}
 
 // ----------------------------------------------------------------- forward
 constexpr int FBK = 64;    // k (columns of L) per LDS stage
@@ -252,6 +263,10 @@ struct UpdArgs {
     // fused next-step sample (FUSE kernels): partial x_next per chunk slot
     const float* eps_next;
     float* part;
+    // tiled corr / m / v (TILED kernels)
+    float* tp;
+    float* tm;
+    float* tv;
     MvnLayerArgs lay[kMaxL];
 };
 
@@ -331,11 +346,12 @@ struct UpdShared {
 // per c-block, x_next[s][r] += sum_c eps_next[s][c] L_new[r][c] on a second
 // MFMA GEMM (L_new tile through the LDS tile region, eps_next fragments
 // straight from L2 into registers), partial sums to the chunk's slot.
-template <bool GRAD, int MODE, bool FUSE>
+template <bool GRAD, int MODE, bool FUSE, bool TILED>
 __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                                           UpdShared<MODE == 2>& sh) {
     constexpr bool MULTI = MODE == 2, TWOH = MODE == 1;
     static_assert(!FUSE || (!GRAD && !MULTI), "fused sample: Adam mode, S <= 128");
+    static_assert(!TILED || (!GRAD && !MULTI), "tiled state: Adam mode, S <= 128");
     float* Gs = sh.Gs;
     float* Es = sh.Es;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
@@ -407,7 +423,22 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
         rowp[j] = corr_off + (int)((int64_t)r * (r - 1) / 2);
     }
     float4 pq[4], mq[4], vq[4];
+    // tiled state: this lane's 4 fragment float4s of a tile (contiguous per wave)
+    auto tile_off = [&](int ti, int g) {
+        return tile_index(a.lay[ch.layer], ch.r0 / UB, ch.k0 + ti) * 4096 +
+               (int64_t)((wv * 4 + g) * 64 + lane) * 4;
+    };
     auto load_pmv = [&](int ti) {
+        if (TILED) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int64_t o = tile_off(ti, g);
+                pq[g] = *reinterpret_cast<const float4*>(a.tp + o);
+                mq[g] = *reinterpret_cast<const float4*>(a.tm + o);
+                vq[g] = *reinterpret_cast<const float4*>(a.tv + o);
+            }
+            return;
+        }
         const int cl = (ch.k0 + ti) * UB + 4 * col4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -514,6 +545,44 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
 
     // call after a barrier that ends every wave's reads of Es
     auto epilogue = [&](int ti) {
+        if (TILED) {
+            // D[i = c][j = r] (j = lane & 31, i = (q&3) + 8(q>>2) + 4h) is already the
+            // tile's fragment order: Adam on the accumulators, float4 in / out
+            const int r = ch.r0 + 32 * wr + l32;
+            const bool rv = r >= 1 && r <= n - 2 && !(a.abl & 8);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int cb = (ch.k0 + ti) * UB + 32 * wc + 8 * g + 4 * h;
+                const int64_t o = tile_off(ti, g);
+                float pn[4], mn[4], vn[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    // entries outside the strict lower part stay exactly 0: zero
+                    // gradient, zero state (both Adam variants keep p = 0)
+                    const float p = f4get(pq[g], i);
+                    klp += p * p;
+                    const bool ok = rv && cb + i < r;
+                    const float gval = ok ? (a.include_kl ? acc[4 * g + i] + p * a.inv_s0sq
+                                                          : acc[4 * g + i])
+                                          : 0.f;
+                    float mm = f4get(mq[g], i), vv = f4get(vq[g], i);
+                    pn[i] = adam_apply_fast(a.adam, p, gval, mm, vv);
+                    mn[i] = mm;
+                    vn[i] = vv;
+                }
+                if (!(a.abl & 8)) {
+                    *reinterpret_cast<float4*>(a.tp + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
+                    *reinterpret_cast<float4*>(a.tm + o) = make_float4(mn[0], mn[1], mn[2], mn[3]);
+                    *reinterpret_cast<float4*>(a.tv + o) = make_float4(vn[0], vn[1], vn[2], vn[3]);
+                }
+                if (FUSE)  // L_new fragment -> the [r][c] tile for the sample GEMM
+                    *reinterpret_cast<float4*>(&Es[(32 * wr + l32) * TLD + 32 * wc + 8 * g + 4 * h]) =
+                        make_float4(pn[0], pn[1], pn[2], pn[3]);
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+            return;
+        }
         // D[i = c][j = r]: j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h  ->  T[r][c] in Es
         float* T = Es;
 #pragma unroll
@@ -692,14 +761,14 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     }
 }
 
-template <bool GRAD, int MODE, bool FUSE = false>
+template <bool GRAD, int MODE, bool FUSE = false, bool TILED = false>
 __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_kernel(UpdArgs a) {
     __shared__ __attribute__((aligned(16))) UpdShared<MODE == 2> sh;
     UPD_STAMP(0, __builtin_amdgcn_s_memtime());
     UPD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
     UPD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const UpdChunk ch = a.chunks[blockIdx.x];
-    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE, FUSE>(a, ch, sh);  // XCD padding chunks are empty
+    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE, FUSE, TILED>(a, ch, sh);  // XCD padding chunks are empty
     UPD_STAMP(3, __builtin_amdgcn_s_memtime());
 }
 
@@ -711,7 +780,76 @@ static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
         la[l].n = p.lay[l].n;
         la[l].poff = p.lay[l].poff;
         la[l].eoff = p.lay[l].eoff;
+        la[l].tbase = p.lay[l].tbase;
     }
+}
+
+// packed <-> tiled corr / m / v: one thread per tiled float4 of each array
+struct ConvArgs {
+    float* params;
+    float* m;
+    float* v;
+    float* tstate;      // [3][tiles_total * 4096]: p, m, v
+    int64_t tfloats;    // tiles_total * 4096
+    int L;
+    MvnLayerArgs lay[kMaxL];
+    int nb[kMaxL];
+};
+
+template <bool TO_TILED>
+__global__ __launch_bounds__(256) void mvn_tile_convert_kernel(ConvArgs c) {
+    const int64_t q = blockIdx.x * (int64_t)256 + threadIdx.x;  // float4 index
+    if (q * 4 >= c.tfloats) return;
+    const int64_t tile = q / 1024;
+    const int f = (int)(q % 1024), w = f / 256, g = (f / 64) & 3, lane = f & 63;
+    int l = 0;
+    while (l + 1 < c.L && tile >= c.lay[l + 1].tbase) ++l;
+    const int64_t tb = tile - c.lay[l].tbase;
+    int b = (int)((sqrtf(8.f * (float)tb + 1.f) - 1.f) * 0.5f);
+    while ((int64_t)(b + 1) * (b + 2) / 2 <= tb) ++b;
+    while ((int64_t)b * (b + 1) / 2 > tb) --b;
+    const int k = (int)(tb - (int64_t)b * (b + 1) / 2);
+    const int n = c.lay[l].n;
+    const int r = 64 * b + 32 * (w >> 1) + (lane & 31);
+    const int c0 = 64 * k + 32 * (w & 1) + 8 * g + 4 * (lane >> 5);
+    const int64_t rowp = c.lay[l].poff + 2 * (int64_t)n + (int64_t)r * (r - 1) / 2;
+    const bool rv = r >= 1 && r <= n - 2;
+    float* arr[3] = {c.params, c.m, c.v};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float4* t = reinterpret_cast<float4*>(c.tstate + a * c.tfloats) + q;
+        if (TO_TILED) {
+            float e[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) e[i] = rv && c0 + i < r ? arr[a][rowp + c0 + i] : 0.f;
+            *t = make_float4(e[0], e[1], e[2], e[3]);
+        } else {
+            const float4 v4 = *t;
+            const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (rv && c0 + i < r) arr[a][rowp + c0 + i] = e[i];
+        }
+    }
+}
+
+hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
+                                   float* tstate, bool to_tiled, hipStream_t st) {
+    ConvArgs c{};
+    c.params = params;
+    c.m = m;
+    c.v = v;
+    c.tstate = tstate;
+    c.tfloats = p.tiles_total * 4096;
+    c.L = p.L;
+    fill_layers(p, c.lay);
+    if (c.tfloats == 0) return hipSuccess;
+    const dim3 grid((unsigned)((c.tfloats / 4 + 255) / 256));
+    if (to_tiled)
+        hipLaunchKernelGGL(mvn_tile_convert_kernel<true>, grid, dim3(256), 0, st, c);
+    else
+        hipLaunchKernelGGL(mvn_tile_convert_kernel<false>, grid, dim3(256), 0, st, c);
+    return hipGetLastError();
 }
 
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
@@ -739,7 +877,8 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
-                             const float* eps_next, float* x_next, hipStream_t st) {
+                             const float* eps_next, float* x_next, hipStream_t st,
+                             float* tstate) {
     UpdArgs a{};
     a.chunks = p.d_upd;
     a.eps = eps;
@@ -765,11 +904,37 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
     if (p.n_upd == 0) return hipSuccess;
     const dim3 grid(p.n_upd), block(256);
     const int mode = a.S > USB ? 2 : a.S > UEH ? 1 : 0;  // samples per LDS pass
+    if (tstate) {
+        // tiled state (psvi_inner_loop on a fusable plan): corr / m / v in tstate
+        const int64_t tf = p.tiles_total * 4096;
+        a.tp = tstate;
+        a.tm = tstate + tf;
+        a.tv = tstate + 2 * tf;
+        if (eps_next) {
+            a.eps_next = eps_next;
+            a.part = p.d_upd_part;
+            if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1, true, true>), grid, block, 0, st, a);
+            else hipLaunchKernelGGL((mvn_update_kernel<false, 0, true, true>), grid, block, 0, st, a);
+            FwdArgs f{};
+            f.params = params;
+            f.eps = eps_next;
+            f.ldx = p.rows_tot[p.rank];
+            f.S = p.d.S;
+            fill_layers(p, f.lay);
+            constexpr int spb = 256 / kFwdRows;
+            hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb),
+                               dim3(256), 0, st, p.d_ufrb, p.d_upd_part, f, x_next);
+        } else {
+            if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1, false, true>), grid, block, 0, st, a);
+            else hipLaunchKernelGGL((mvn_update_kernel<false, 0, false, true>), grid, block, 0, st, a);
+        }
+        return hipGetLastError();
+    }
     if (eps_next && !grad_out) {
         if (!(p.fuse_sample && mode < 2)) {
             // no fusion for this plan: update, then sample from the new params
             hipError_t e = launch_mvn_update(p, eps, g_shard, params, m, v, hp, kl_out, nullptr,
-                                             include_kl, nullptr, nullptr, st);
+                                             include_kl, nullptr, nullptr, st, nullptr);
             return e != hipSuccess ? e : launch_mvn_fwd(p, eps_next, params, x_next, st);
         }
         a.eps_next = eps_next;

@@ -107,6 +107,8 @@ struct LayerInfo {
     int64_t poff;   // offset of the layer in the flat parameter vector
     int64_t eoff;   // offset of the layer in the flat eps vector (all S)
     int woff;       // offset of the layer in the per-sample weight space [0, n_tot)
+    int64_t tbase;  // full-cov tiled layout: first 64x64 tile of the layer
+    int nb;         // full-cov: 64-row bands covering rows 0 .. n-1
 };
 
 // Full-cov forward work item: rows [r0, r1) (<= kFwdRows) of layer `layer`
@@ -165,6 +167,9 @@ struct psvi_plan {
     // fused update + next-step sample (world == 1, S <= 128): one row block
     // per 64-row band, one partial slot per chunk
     bool fuse_sample = false;
+    // tiled corr/m/v (world == 1, S <= 128 inner loops): 64x64 tiles (b, k <= b)
+    // per layer in MFMA fragment order, tiles_total * 4096 floats per array
+    int64_t tiles_total = 0;
     std::vector<psvi::FwdRowBlock> h_ufrb;
     psvi::FwdRowBlock* d_ufrb = nullptr;
     int n_ufrb = 0, n_uslots = 0;
@@ -191,7 +196,10 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
-                             const float* eps_next, float* x_next, hipStream_t st);
+                             const float* eps_next, float* x_next, hipStream_t st,
+                             float* tstate = nullptr);
+hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
+                                   float* tstate, bool to_tiled, hipStream_t st);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);

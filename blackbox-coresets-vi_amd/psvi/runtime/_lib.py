@@ -27,6 +27,7 @@ Q_ROWS_LOCAL = 7
 Q_XSHARD_COUNT = 8
 Q_XRECV_COUNT = 9
 Q_LOOP_WS_BYTES = 10
+Q_TILED_FLOATS = 11
 
 ERRORS = {-1: "PSVI_EINVAL", -2: "PSVI_ENOSPC", -3: "PSVI_EUNSUP", -4: "PSVI_ESTATE"}
 
@@ -75,6 +76,9 @@ SIGNATURES = {
                                      _I32, _P]),
     "psvi_mvn_phase_update_sample": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P,
                                             _I32, _P, _P, _P]),
+    "psvi_mvn_tiled_convert": (_I32, [_P, _P, _P, _P, _P, _I32, _P]),
+    "psvi_mvn_phase_update_tiled": (_I32, [_P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P,
+                                           _I32, _P, _P, _P]),
     "psvi_inner_loop": (_I32, [_P, _P, _P, _P, _P, _U64, _U64, _I32, _P, _P, _P,
                                ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),

@@ -77,6 +77,7 @@ class InnerLoopPlan:
         self.xshard_count = q(_lib.Q_XSHARD_COUNT)
         self.xrecv_count = q(_lib.Q_XRECV_COUNT)
         self.loop_ws_bytes = q(_lib.Q_LOOP_WS_BYTES)
+        self.tiled_floats = q(_lib.Q_TILED_FLOATS)  # 0: no tiled state for this plan
         self.eps_stride = (self.eps_count + 3) // 4 * 4   # Philox offset per loop step
         self.n_tot = sum(i * o + o for i, o in layers)
 
@@ -203,6 +204,40 @@ class InnerLoopPlan:
         _need(x_shard, "x_shard", self.xshard_count)
         check(self.lib.psvi_mvn_phase_sample(self.handle, _ptr(eps), _ptr(params),
                                              _ptr(x_shard), _stream()), "psvi_mvn_phase_sample")
+
+    def tiled_state(self, device="cuda"):
+        if not self.tiled_floats:
+            raise ValueError("this plan has no tiled state (full-cov, world 1, S <= 128)")
+        return torch.empty(self.tiled_floats, dtype=torch.float32, device=device)
+
+    def tiled_convert(self, params, adam_m, adam_v, tstate, to_tiled):
+        for t, n in ((params, "params"), (adam_m, "adam_m"), (adam_v, "adam_v")):
+            _need(t, n, self.param_count)
+        _need(tstate, "tstate", self.tiled_floats)
+        check(self.lib.psvi_mvn_tiled_convert(self.handle, _ptr(params), _ptr(adam_m),
+                                              _ptr(adam_v), _ptr(tstate), int(bool(to_tiled)),
+                                              _stream()), "psvi_mvn_tiled_convert")
+
+    def mvn_update_tiled(self, eps, g_shard, params, adam_m, adam_v, tstate, step, lr,
+                         kind="higher", kl_out=None, include_kl=True, eps_next=None,
+                         x_next=None):
+        _need(eps, "eps", self.eps_count)
+        _need(g_shard, "g_shard", self.xshard_count)
+        for t, n in ((params, "params"), (adam_m, "adam_m"), (adam_v, "adam_v")):
+            _need(t, n, self.param_count)
+        _need(tstate, "tstate", self.tiled_floats)
+        if kl_out is not None:
+            _need(kl_out, "kl_out", 1, torch.float64)
+        if (eps_next is None) != (x_next is None):
+            raise ValueError("eps_next and x_next go together")
+        if eps_next is not None:
+            _need(eps_next, "eps_next", self.eps_count)
+            _need(x_next, "x_next", self.xshard_count)
+        hp = make_adam(lr, step, kind)
+        check(self.lib.psvi_mvn_phase_update_tiled(
+            self.handle, _ptr(eps), _ptr(g_shard), _ptr(params), _ptr(adam_m), _ptr(adam_v),
+            _ptr(tstate), ctypes.byref(hp), _ptr(kl_out), int(bool(include_kl)), _ptr(eps_next),
+            _ptr(x_next), _stream()), "psvi_mvn_phase_update_tiled")
 
     def mvn_net(self, u, z, w, x_recv, g_send, nll_out):
         _need(u, "u", self.M * self.layers[0][0])

@@ -103,6 +103,8 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_XSHARD_COUNT  8  /* full-cov: floats of x_shard / g_shard = S*ROWS_LOCAL */
 #define PSVI_Q_XRECV_COUNT   9  /* full-cov: floats of x_recv / g_send = S_LOCAL*n_tot */
 #define PSVI_Q_LOOP_WS_BYTES 10 /* workspace bytes for psvi_inner_loop                 */
+#define PSVI_Q_TILED_FLOATS  11 /* floats of the tiled corr/m/v state (0: the plan has
+                                   none -- it needs full-cov, world 1, S <= 128)      */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
  * Samples are split in contiguous blocks; for FULLCOV the rows of every
@@ -194,6 +196,26 @@ int psvi_mvn_phase_update_sample(const psvi_plan* plan, const float* eps,
                                  float* adam_v, const psvi_adam_hp* hp, double* kl_out,
                                  int32_t include_kl, const float* eps_next,
                                  float* x_next, void* stream);
+
+/* Tiled corr / m / v state for a run of inner steps (full-cov, world 1,
+ * S <= 128): the packed triangles re-laid as 64x64 tiles in the update
+ * kernel's fragment order, so every corr/m/v access is a contiguous 1 KB
+ * wave transaction (the packed rows' scattered 256-byte runs stream at about
+ * two thirds of that rate).  tstate: PSVI_Q_TILED_FLOATS floats.
+ * to_tiled = 1 copies the corr parts of params / adam_m / adam_v in; 0 copies
+ * them back (the mean / sd parts always stay in params / adam_m / adam_v).
+ * psvi_inner_loop does this itself. */
+int psvi_mvn_tiled_convert(const psvi_plan* plan, float* params, float* adam_m,
+                           float* adam_v, float* tstate, int32_t to_tiled, void* stream);
+/* psvi_mvn_phase_update with corr and its Adam state in tstate (mean / sd
+ * and theirs stay in params / adam_m / adam_v; the packed corr parts are
+ * neither read nor written until psvi_mvn_tiled_convert(..., 0)); with
+ * eps_next / x_next also the next step's sample (fused). */
+int psvi_mvn_phase_update_tiled(const psvi_plan* plan, const float* eps,
+                                const float* g_shard, float* params, float* adam_m,
+                                float* adam_v, float* tstate, const psvi_adam_hp* hp,
+                                double* kl_out, int32_t include_kl,
+                                const float* eps_next, float* x_next, void* stream);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] ~ N(0,1), Philox4x32-10 counter (seed, offset + i) + Box-Muller.

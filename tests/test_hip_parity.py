@@ -272,3 +272,74 @@ def test_inner_loop_philox_equals_stepwise(family, layers, S, M):
         eb.append(plan.inner_step(u, z, w, eps, pb, mb, vb, step=t + 1, lr=1e-3, ws=ws).item())
     assert np.allclose(ea.cpu().numpy(), eb, rtol=1e-6, atol=0)
     assert l2rel(pa.cpu().numpy(), pb.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("layers,S", [([(64, 40), (40, 40), (40, 2)], 128),
+                                      ([(9, 5), (5, 3)], 40), ([(8, 6), (6, 6), (6, 3)], 16)])
+def test_tiled_state_roundtrip(layers, S):
+    from psvi.runtime import InnerLoopPlan
+
+    plan = InnerLoopPlan("fullcov", layers, S, 10)
+    assert plan.tiled_floats > 0
+    g = torch.Generator().manual_seed(1)
+    p, m, v = (torch.randn(plan.param_count, generator=g).to(DEV) for _ in range(3))
+    ts = plan.tiled_state()
+    plan.tiled_convert(p, m, v, ts, True)
+    q, mq, vq = (torch.zeros_like(p) for _ in range(3))
+    plan.tiled_convert(q, mq, vq, ts, False)
+    po = 0
+    for din, dout in layers:
+        n = din * dout + dout
+        nc = (n - 1) * (n - 2) // 2
+        sl = slice(po + 2 * n, po + 2 * n + nc)
+        for a, b in ((p, q), (m, mq), (v, vq)):
+            assert torch.equal(a[sl], b[sl])
+            assert torch.count_nonzero(b[po:po + 2 * n]) == 0  # mean / sd untouched
+        po += 2 * n + nc
+    # the tiled copy holds each corr entry exactly once, zeros elsewhere
+    tf = plan.tiled_floats // 3
+    assert torch.count_nonzero(ts[:tf]) == torch.count_nonzero(
+        torch.cat([p[po2 + 2 * n2: po2 + 2 * n2 + (n2 - 1) * (n2 - 2) // 2]
+                   for po2, n2 in _layer_offsets(layers)]))
+
+
+def _layer_offsets(layers):
+    po, out = 0, []
+    for din, dout in layers:
+        n = din * dout + dout
+        out.append((po, n))
+        po += 2 * n + (n - 1) * (n - 2) // 2
+    return out
+
+
+@pytest.mark.parametrize("name", [n for n in NAMES if load_fixture(n)["cfg"]["family"] == "mvn"])
+@pytest.mark.parametrize("fused", [False, True])
+def test_tiled_update_equals_packed(name, fused):
+    f = load_fixture(name)
+    cfg, plan, u, z, w = _setup(f)
+    eps0, eps1 = _t(f["eps"][0]), _t(f["eps"][1])
+    p1 = _t(f["params0"])
+    xs = torch.empty(plan.xshard_count, device=DEV)
+    gs = torch.empty(plan.xshard_count, device=DEV)
+    nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.mvn_sample(eps0, p1, xs)
+    plan.mvn_net(u, z, w, xs, gs, nll)
+    p2 = p1.clone()
+    m1, v1 = torch.zeros_like(p1), torch.zeros_like(p1)
+    m2, v2 = torch.zeros_like(p1), torch.zeros_like(p1)
+    k1 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    k2 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    x1, x2 = torch.empty_like(xs), torch.full_like(xs, float("nan"))
+    kw = dict(eps_next=eps1, x_next=x1) if fused else {}
+    plan.mvn_update(eps0, gs, p1, m1, v1, step=1, lr=cfg["lr"], kind=adam_kind(cfg), kl_out=k1, **kw)
+    ts = plan.tiled_state()
+    plan.tiled_convert(p2, m2, v2, ts, True)
+    kw = dict(eps_next=eps1, x_next=x2) if fused else {}
+    plan.mvn_update_tiled(eps0, gs, p2, m2, v2, ts, step=1, lr=cfg["lr"], kind=adam_kind(cfg),
+                          kl_out=k2, **kw)
+    plan.tiled_convert(p2, m2, v2, ts, False)
+    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    assert rel(k1.item(), k2.item()) < 1e-6  # fp32 per-thread partial sums, other order
+    if fused:
+        assert torch.isfinite(x2).all()
+        assert l2rel(x2.cpu().numpy(), x1.cpu().numpy()) < 1e-6

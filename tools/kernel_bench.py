@@ -88,6 +88,19 @@ def main():
                             x_next=x2)
             st[0] += 1
         out["update+next sample (fused)"] = timeit(upd_smp, iters)
+        ts = plan.tiled_state()
+        plan.tiled_convert(params, m, v, ts, True)
+
+        def upd_t(fused):
+            kw = dict(eps_next=eps2, x_next=x2) if fused else {}
+            plan.mvn_update_tiled(eps, gs, params, m, v, ts, step=st[0], lr=1e-3, kl_out=nll, **kw)
+            st[0] += 1
+        out["update (tiled)"] = timeit(lambda: upd_t(False), iters)
+        out["update+next sample (tiled, fused)"] = timeit(lambda: upd_t(True), iters)
+        plan.tiled_convert(params, m, v, ts, False)
+        out["tiled convert (both ways)"] = timeit(
+            lambda: (plan.tiled_convert(params, m, v, ts, True),
+                     plan.tiled_convert(params, m, v, ts, False)), 20)
         T = 20
         elb = torch.empty(T, dtype=torch.float64, device=dev)
         lws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
