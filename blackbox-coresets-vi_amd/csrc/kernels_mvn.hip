@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
     const int eoff = (int)a.lay[it.layer].eoff;
     const float* E = a.eps + eoff;   // [S][n]; the whole eps buffer is [-eoff, e_rem)
     const int e_rem = (int)a.e_total - eoff;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int col4 = tid & 15, srow = tid >> 4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr int FT = kFwdRows / 32, LJ = kFwdRows / 16;
@@ -354,7 +354,7 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     static_assert(!TILED || (!GRAD && !MULTI), "tiled state: Adam mode, S <= 128");
     float* Gs = sh.Gs;
     float* Es = sh.Es;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int wr = wv >> 1, wc = wv & 1;
     const int n = a.lay[ch.layer].n;
     const int eoff = (int)a.lay[ch.layer].eoff;
@@ -372,8 +372,12 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 greg[8], ereg[8];
     // sample row s is clamped to S-1 (rows >= S are zeroed at the LDS write)
-    auto goff = [&](int s) { return min(s, a.S - 1) * a.ldg + gcol; };
-    auto eofs = [&](int s, int ti) { return min(s, a.S - 1) * n + (ch.k0 + ti) * UB + 4 * col4; };
+    // (ablation 1: every G / eps load from one cached address)
+    const int ab1 = (a.abl & 1) ? 0 : 1;
+    auto goff = [&](int s) { return ab1 * (min(s, a.S - 1) * a.ldg + gcol); };
+    auto eofs = [&](int s, int ti) {
+        return ab1 * (min(s, a.S - 1) * n + (ch.k0 + ti) * UB + 4 * col4);
+    };
     auto load_G = [&](int pi) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) greg[j] = ld4u(a.g, goff(pi * USB + srow + 16 * j), 0, g_total);
@@ -428,11 +432,12 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
         return tile_index(a.lay[ch.layer], ch.r0 / UB, ch.k0 + ti) * 4096 +
                (int64_t)((wv * 4 + g) * 64 + lane) * 4;
     };
+    const int64_t ab4 = (a.abl & 4) ? 0 : 1;  // ablation 4: corr/m/v loads from one address
     auto load_pmv = [&](int ti) {
         if (TILED) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int64_t o = tile_off(ti, g);
+                const int64_t o = ab4 * tile_off(ti, g);
                 pq[g] = *reinterpret_cast<const float4*>(a.tp + o);
                 mq[g] = *reinterpret_cast<const float4*>(a.tm + o);
                 vq[g] = *reinterpret_cast<const float4*>(a.tv + o);
@@ -465,7 +470,8 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     float4 enreg[FUSE ? 8 : 1];
     const bool wave_s = 32 * wv < a.S;  // this wave owns samples of the fused GEMM
     const int es = min(32 * wv + l32, a.S - 1);
-    auto enofs = [&](int ti, int g) { return es * n + (ch.k0 + ti) * UB + 8 * g + 4 * h; };
+    const int ab32 = (a.abl & 32) ? 0 : 1;  // ablation 32: eps_next loads from one address
+    auto enofs = [&](int ti, int g) { return ab32 * (es * n + (ch.k0 + ti) * UB + 8 * g + 4 * h); };
     auto load_En = [&](int ti) {
         if (FUSE) {
 #pragma unroll
@@ -475,7 +481,7 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     // x_next partial over one c-block: A = eps_next[s][c] (registers, k-permuted:
     // lane half h holds c = 8g + 4h + j for MFMA j), B = L_new[r][c] from the tile
     auto gemm2 = [&](int ti) {
-        if (FUSE && wave_s) {
+        if (FUSE && wave_s && !(a.abl & 16)) {
             const float* Lb = Es + l32 * TLD + 4 * h;
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
@@ -566,7 +572,8 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                                                           : acc[4 * g + i])
                                           : 0.f;
                     float mm = f4get(mq[g], i), vv = f4get(vq[g], i);
-                    pn[i] = adam_apply_fast(a.adam, p, gval, mm, vv);
+                    pn[i] = (a.abl & 64) ? p + gval + mm + vv
+                                         : adam_apply_fast(a.adam, p, gval, mm, vv);
                     mn[i] = mm;
                     vn[i] = vv;
                 }
@@ -668,18 +675,32 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
             *reinterpret_cast<float4*>(&Gs[sr * ULD + 4 * col4]) =
                 sr < a.S && !(a.abl & 1) ? fix4(greg[j], goff(sr), 0, g_total) : z4;
         }
+        // diagnostics: shader-clock time per loop phase, summed over c-blocks
+        // (slots 6..11: stage 1, MFMA half 1, stage 2, MFMA half 2, epilogue, gemm2)
+        unsigned long long tph[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+        auto ph = [&](int k) {
+            if (a.stamps && tid == 0) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                if (k >= 0) tph[k] += t - tlast;
+                tlast = t;
+            }
+        };
+        ph(-1);
         for (int ti = 0; ti < nt; ++ti) {
             stage_Eh(ti, 0);
             __syncthreads();
             if (ti == 0) UPD_STAMP(1, __builtin_amdgcn_s_memtime());
+            ph(0);
             if (TWOH) {
                 load_Eh(ti, 1);
                 load_pmv(ti);
                 load_En(ti);
                 compute_h(ti, 0);
                 __syncthreads();
+                ph(1);
                 stage_Eh(ti, 1);
                 __syncthreads();
+                ph(2);
                 load_Eh(min(ti + 1, nt - 1), 0);
                 compute_h(ti, 1);
             } else {
@@ -689,13 +710,18 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                 compute_h(ti, 0);
             }
             __syncthreads();  // every wave done with Es: it takes the accumulator tile
+            ph(3);
             epilogue(ti);
             if (FUSE) {
                 __syncthreads();  // L_new tile complete
+                ph(4);
                 gemm2(ti);
             }
             __syncthreads();  // tile read before the next staging overwrites Es
+            ph(FUSE ? 5 : 4);
         }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) UPD_STAMP(6 + k, tph[k]);
     } else {
         load_G(0);
         load_E(0, 0);
@@ -765,11 +791,13 @@ template <bool GRAD, int MODE, bool FUSE = false, bool TILED = false>
 __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_kernel(UpdArgs a) {
     __shared__ __attribute__((aligned(16))) UpdShared<MODE == 2> sh;
     UPD_STAMP(0, __builtin_amdgcn_s_memtime());
+    UPD_STAMP(12, __builtin_amdgcn_s_memrealtime());  // chip-wide 100 MHz clock
     UPD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
     UPD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const UpdChunk ch = a.chunks[blockIdx.x];
     if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE, FUSE, TILED>(a, ch, sh);  // XCD padding chunks are empty
     UPD_STAMP(3, __builtin_amdgcn_s_memtime());
+    UPD_STAMP(13, __builtin_amdgcn_s_memrealtime());
 }
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)

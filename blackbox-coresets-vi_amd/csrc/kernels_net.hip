@@ -1,5 +1,5 @@
-// kernels_net.hip -- per-(sample, pseudopoint-chunk) MLP forward + weighted NLL
-// + hand-derived backward, for both VI families.
+// kernels_net.hip -- per-(sample, role, pseudopoint-chunk) MLP forward + weighted
+// NLL + hand-derived backward, for both VI families.
 //
 // Reference (psvi/..., /root/reference):
 //   VILinear.forward        models/neural_net.py:176-179   a = h W_s^T + b_s
@@ -9,38 +9,54 @@
 // Backward: g = w_m (softmax - onehot); dW_s = g^T h;
 // db_s = sum_m g; g <- (g W_s) * 1[a > 0].
 //
-// One workgroup = one MC sample x one chunk of pseudopoints.  Everything the
-// sample needs (its weights, the pseudo-input chunk, every layer's
-// activations, two gradient buffers, one dW accumulation tile) lives in LDS
-// with odd row strides.  The contractions run on fp32 MFMA (16x16x4) "units"
-// of 16 rows x 32 columns with software-pipelined operand loads; units are
-// dealt round-robin to the waves.  Backward, per layer, in ONE phase:
-//   dW_l = g_l^T [h_{l-1} | 1]  (the ones column makes the last output column
-//          the bias gradient), K = pseudopoints split over waves, partial
-//          tiles summed with LDS float atomics into the dW tile;
-//   g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0]  into the other gradient buffer;
-// then the dW tile leaves LDS as contiguous rows:
-//  MEANFIELD: [sum_s dW | sum_s dW*eps] accumulators (fp32 atomics, S adders);
-//  FULLCOV:   g_send in the blocked-by-source-rank layout (plain stores, or
-//             atomics when a sample's pseudopoints span several workgroups).
+// One workgroup = one MC sample x one ROLE x one chunk of pseudopoints.
+// When a rank has fewer samples than CUs, each sample gets two workgroups
+// with different roles instead of a split of its pseudopoints: both run the
+// forward pass and the loss head; role 0 then produces layer 0's weight
+// gradient (and the gradient chain down to it), role 1 every other layer's.
+// Each gradient element has exactly one writer -- plain stores into g_send,
+// no zeroing pass, no atomics, deterministic.  (Pseudopoint chunks, whose
+// partial dW are added with atomics onto a zeroed g_send, remain for shapes
+// whose buffers exceed the LDS, and for ranks with very few samples.)
+//
+// LDS holds everything a workgroup touches.  Every matrix is row-major with
+// a row stride of 4 x odd floats: the MFMA operand reads -- float4 along k for
+// k-contiguous operands, single floats down k for k-strided ones -- are then
+// free of bank conflicts in both orientations (every buffer is read both
+// ways: activations by the forward GEMM and by the dW GEMM, gradients by the
+// propagation GEMM and by the dW GEMM, weights by the forward and the
+// propagation GEMM).  Contractions run on v_mfma_f32_16x16x4_f32 tiles (exact
+// fp32) with double-buffered operand reads, tiles dealt round-robin to the
+// waves (wave w sits on SIMD w % 4).
+// Padding contract: W rows / columns past dout / din are zero; activation and
+// gradient rows past the chunk's pseudopoints are zero and their columns up
+// to the next multiple of 16 (within the row stride) too (epilogues write
+// them); a k-loop that runs past a row's end reads the next row's (finite)
+// values against zero weights; every region is followed by zeroed slack.
+// The loss head runs on VALU with 4 lanes per pseudopoint (logits in
+// registers up to kMaxC classes, through LDS beyond), fused with the
+// softmax / NLL / dlogits and the first gradient propagation.  Weight
+// gradients leave straight from the MFMA accumulators.
 #include <algorithm>
 
 #include "psvi_internal.hpp"
 
 namespace psvi {
 
+constexpr int kMaxC = 16;  // classes the VALU loss head keeps in registers
+
 struct NetArgs {
-    int L, M, mc, S_total, s_goff, atomic_g;
+    int L, M, mc, S_total, s_goff, atomic_g, nroles, Mp;
     int abl;  // diagnostics ablation mask (0 in production): 1 loads, 2 fwd
-              // GEMMs, 4 NLL, 8 bwd GEMMs, 16 global dW writes,
-              // 128 g-propagation GEMMs
+              // GEMMs, 4 loss head, 8 bwd GEMMs, 16 global gradient writes
     unsigned long long* stamps;  // diagnostics: s_memtime per phase (nullptr in production)
     int din[kMaxL], dout[kMaxL], woff[kMaxL];
-    // LDS carve (float offsets) and row strides
-    int lw[kMaxL], ldw[kMaxL], lb[kMaxL], le[kMaxL], leb[kMaxL], la[kMaxL], lda[kMaxL];
-    int lu, ldu, lred, lg0, lg1, ldgb, ldwt, lds_f4;
-    int lstage_f4;                // float4 index where the late regions (and the DMA stage) start
-    int stage_off[kMaxWorld], stage_u;  // DMA stage: per-source x rows, then the u chunk
+    // LDS carve (float offsets) and row strides: W_l, b_l, X_l (input of layer l:
+    // X_0 = u chunk, X_l = relu(a_{l-1})), two gradient buffers, dlogits
+    int lw[kMaxL], ldw[kMaxL], lb[kMaxL], lx[kMaxL], ldx[kMaxL];
+    int lg[2], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // ldl: dlogits [Mp][lddl]; lzw: z, w
+    int nslack, nslack_early, slack[4 * kMaxL + 8];  // float offsets of the 64-float zero slacks
+    int lstage, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, staged by source
     const float* u;
     const int32_t* z;
     const float* w;
@@ -62,159 +78,157 @@ struct NetArgs {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// One MFMA work unit of C[p][q] = sum_k A(p,k) B(q,k) with
-// A(p,k) = A[p*sap + k*sak], B(q,k) = B[q*sbq + k*sbk] in LDS: rows
-// [p0, p0+16) x columns [q0, q0+32) (two 16x16 tiles on v_mfma_f32_16x16x4_f32,
-// exact fp32, two independent accumulator chains sharing the A fragment),
-// k in [k0, k0 + 16*ceil((k1-k0)/16)).  Lane l feeds A[p0+(l&15)][k+(l>>4)],
-// B[q+(l&15)][k+(l>>4)] and holds D[p0+4(l>>4)+r][q+(l&15)].
-// No masks: the LDS layout (net_lds_floats) zero-fills and pads every
-// operand so that any k >= k1 meets a zero in A or B, and rows / columns
-// past P / Q only feed outputs the epilogue drops.  The next 16-k group's
-// operands are read before the current group's MFMAs.
-template <int NQ, bool RELU_A, bool RELU_B, class Epi>
-__device__ __forceinline__ void gemm_unit(int P, int Q, int k0, int k1, int p0, int q0,
-                                          const float* __restrict__ A, int sap, int sak,
-                                          const float* __restrict__ B, int sbq, int sbk,
-                                          Epi epi) {
-    const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
-    const float* Ap = A + (p0 + i16) * sap + k4 * sak;
-    const float* Bp = B + (q0 + i16) * sbq + k4 * sbk;
+// ---------------------------------------------------------------- MFMA tile
+// C[p][q] = sum_k A(p,k) B(q,k) for a 16-row tile and NQ 16-column tiles,
+// k in groups of 16.
+//   ACONT: A(p,k) = A[p*lda + k] (one float4 per lane and k-group), else
+//          A(p,k) = A[k*lda + p] (four floats); BCONT likewise for B(q,k).
+// Lane l = 16 k4 + i16 feeds row / column i16 and, to MFMA j of a k-group,
+// k = kb + 4 k4 + j (the same k permutation on both operands), and holds
+// D[p0 + 4 k4 + r][q0 + 16c + i16], r = 0..3 (v_mfma_f32_16x16x4_f32 layout):
+// the epilogue gets (first row, column, the four rows' values).
+template <bool ACONT, bool BCONT, int NQ>
+struct TileOps {
+    float4 a;
+    float4 b[NQ];
+    __device__ __forceinline__ static float4 ld(const float* X, int ldx, int row, int k, bool cont) {
+        if (cont) return *reinterpret_cast<const float4*>(X + row * ldx + k);
+        return make_float4(X[k * ldx + row], X[(k + 1) * ldx + row], X[(k + 2) * ldx + row],
+                           X[(k + 3) * ldx + row]);
+    }
+    __device__ __forceinline__ void load(const float* A, int lda, const float* B, int ldb, int p,
+                                         int q, int k) {
+        a = ld(A, lda, p, k, ACONT);
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) b[c] = ld(B, ldb, q + 16 * c, k, BCONT);
+    }
+    __device__ __forceinline__ void mma(floatx4 (&acc)[NQ]) const {
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[c].z, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[c].w, acc[c], 0, 0, 0);
+        }
+    }
+};
+
+// One GEMM's tiles (P x Q outputs rounded up to 16-tiles): units of one
+// 16-row tile x NQ column tiles -- a whole row of column tiles (NQ = tq <= 3:
+// one A read per NQ MFMAs) when that still gives every SIMD a unit, else
+// single tiles.  Unit u goes to wave (u + first) % nwaves, so two GEMMs of
+// one phase share the round-robin.  Each wave runs its (unit, k-group) steps
+// as one software pipeline: the next step's operands -- also across units --
+// are read before the current step's MFMAs and epilogue.
+__device__ __forceinline__ int gemm_nq(int tp, int tq) {
+    return (tq <= 3 && tp >= 4) ? tq : 1;
+}
+__device__ __forceinline__ int gemm_units(int P, int Q) {
+    const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4;
+    return tp * (tq / gemm_nq(tp, tq));
+}
+template <bool ACONT, bool BCONT, int NQ, class Epi>
+__device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, const float* A, int lda,
+                                           const float* B, int ldb, Epi epi) {
+    const int nwv = blockDim.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+    const int nk = K16 >> 4;
+    const int nmine = u0 < nu ? (nu - u0 + nwv - 1) / nwv : 0;
+    const int T = nmine * nk;
+    if (T == 0) return;
+    // step st -> unit u0 + (st / nk) * nwv, k-group st % nk (tracked
+    // incrementally).  Loads past the last step repeat it: every operand load
+    // is unconditional, so s_waitcnt can count the prefetches in flight (a
+    // load under a branch makes it wait for all of them).
+    int lu = u0, lk = 0, lst = 0;  // the step to load next
+    auto lcoords = [&](int& p, int& q, int& k) {
+        const int pt = lu / tqu, qt = (lu - pt * tqu) * NQ;
+        p = (pt << 4) + i16;
+        q = (qt << 4) + i16;
+        k = (lk << 4) + 4 * k4;
+        if (lst < T - 1) {
+            ++lst;
+            if (++lk == nk) { lk = 0; lu += nwv; }
+        }
+    };
+    int eu = u0, ek = 0;  // the step to compute
     floatx4 acc[NQ];
 #pragma unroll
     for (int c = 0; c < NQ; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float a[4], b[NQ][4];
-    auto load = [&](int kb, float (&x)[4], float (&y)[NQ][4]) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int kk = kb + 4 * u;
-            x[u] = Ap[kk * sak];
-            if (RELU_A) x[u] = fmaxf(x[u], 0.f);
+    auto finish = [&]() {
+        if (++ek == nk) {
+            const int pt = eu / tqu, qt = (eu - pt * tqu) * NQ;
 #pragma unroll
             for (int c = 0; c < NQ; ++c) {
-                y[c][u] = Bp[16 * c * sbq + kk * sbk];
-                if (RELU_B) y[c][u] = fmaxf(y[c][u], 0.f);
+                epi(pt * 16 + 4 * k4, (qt + c) * 16 + i16, acc[c]);
+                acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
+            ek = 0;
+            eu += nwv;
         }
     };
-    if (k0 < k1) load(k0, a, b);
-    for (int kb = k0; kb < k1; kb += 16) {  // wave-uniform
-        float na[4], nb[NQ][4];
-        if (kb + 16 < k1) load(kb + 16, na, nb);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int c = 0; c < NQ; ++c)
-                acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[c][u], acc[c], 0, 0, 0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            a[u] = na[u];
-#pragma unroll
-            for (int c = 0; c < NQ; ++c) b[c][u] = nb[c][u];
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int pp = p0 + 4 * k4 + r;
-        if (pp < P) {
-#pragma unroll
-            for (int c = 0; c < NQ; ++c) {
-                const int q = q0 + 16 * c + i16;
-                if (q < Q) epi(pp, q, acc[c][r]);
-            }
+    TileOps<ACONT, BCONT, NQ> x0, x1;
+    int p, q, k;
+    lcoords(p, q, k);
+    x0.load(A, lda, B, ldb, p, q, k);
+    for (int st = 0; st < T; st += 2) {  // wave-uniform
+        lcoords(p, q, k);
+        x1.load(A, lda, B, ldb, p, q, k);
+        x0.mma(acc);
+        finish();
+        lcoords(p, q, k);
+        x0.load(A, lda, B, ldb, p, q, k);
+        if (st + 1 < T) {
+            x1.mma(acc);
+            finish();
         }
     }
 }
-
-// Degenerate shapes (a side < 8, or K <= 4: the classifier layer) on VALU.
-// K >= 16: one output per 16-lane group, lanes split k, xor-shuffle reduce;
-// short K: one output per thread.
-template <bool RELU_A, bool RELU_B, class Epi>
-__device__ __forceinline__ void valu_gemm(int P, int Q, int K, const float* A, int sap, int sak,
-                                          const float* B, int sbq, int sbk, Epi epi) {
-    const int PQ = P * Q;
-    if (K >= 16) {
-        const int g = threadIdx.x >> 4, ng = blockDim.x >> 4, l16 = threadIdx.x & 15;
-        for (int base = 0; base < PQ; base += ng) {  // uniform trip count: shuffles converge
-            const int idx = min(base + g, PQ - 1);
-            const int p = idx / Q, q = idx - p * Q;
-            const float* Ap = A + p * sap;
-            const float* Bp = B + q * sbq;
-            float acc = 0.f;
-            for (int k = l16; k < K; k += 16) {
-                float x = Ap[k * sak], y = Bp[k * sbk];
-                if (RELU_A) x = fmaxf(x, 0.f);
-                if (RELU_B) y = fmaxf(y, 0.f);
-                acc = fmaf(x, y, acc);
-            }
-            acc += __shfl_xor(acc, 8, 16);
-            acc += __shfl_xor(acc, 4, 16);
-            acc += __shfl_xor(acc, 2, 16);
-            acc += __shfl_xor(acc, 1, 16);
-            if (l16 == 0 && base + g < PQ) epi(p, q, acc);
-        }
-        return;
-    }
-    for (int idx = threadIdx.x; idx < PQ; idx += blockDim.x) {
-        const int p = idx / Q, q = idx - p * Q;
-        const float* Ap = A + p * sap;
-        const float* Bp = B + q * sbq;
-        float acc = 0.f;
-        for (int k = 0; k < K; ++k) {
-            float x = Ap[k * sak], y = Bp[k * sbk];
-            if (RELU_A) x = fmaxf(x, 0.f);
-            if (RELU_B) y = fmaxf(y, 0.f);
-            acc = fmaf(x, y, acc);
-        }
-        epi(p, q, acc);
+template <bool ACONT, bool BCONT, class Epi>
+__device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const float* A, int lda,
+                                          const float* B, int ldb, Epi epi) {
+    const int wid = wave_id(), nwv = blockDim.x >> 6;
+    const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, K16 = (K + 15) & ~15;
+    const int u0 = ((wid - first) % nwv + nwv) % nwv;
+    switch (gemm_nq(tp, tq)) {
+        case 3: gemm_steps<ACONT, BCONT, 3>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
+        case 2: gemm_steps<ACONT, BCONT, 2>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
+        default: gemm_steps<ACONT, BCONT, 1>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi); break;
     }
 }
 
-// Whole GEMM: VALU for degenerate shapes, else MFMA units of 16 rows x
-// 16*NQ columns (NQ matched to Q) dealt round-robin to the waves.
-template <bool RELU_A, bool RELU_B, class Epi>
-__device__ __forceinline__ void lds_gemm(int P, int Q, int K, const float* A, int sap, int sak,
-                                         const float* B, int sbq, int sbk, Epi epi) {
-    if (P < 8 || Q < 8 || K <= 4) {
-        valu_gemm<RELU_A, RELU_B>(P, Q, K, A, sap, sak, B, sbq, sbk, epi);
-        return;
-    }
-    const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-    const int tp = (P + 15) >> 4;
-    if (Q <= 16) {
-        for (int t = wid; t < tp; t += nwv)
-            gemm_unit<1, RELU_A, RELU_B>(P, Q, 0, K, t << 4, 0, A, sap, sak, B, sbq, sbk, epi);
-    } else if (Q <= 32 || (Q > 48 && Q <= 64)) {
-        const int tq = (Q + 31) >> 5;
-        for (int t = wid; t < tp * tq; t += nwv) {
-            const int pt = t / tq;
-            gemm_unit<2, RELU_A, RELU_B>(P, Q, 0, K, pt << 4, (t - pt * tq) << 5, A, sap, sak, B,
-                                         sbq, sbk, epi);
-        }
-    } else {
-        const int tq = (Q + 47) / 48;
-        for (int t = wid; t < tp * tq; t += nwv) {
-            const int pt = t / tq;
-            gemm_unit<3, RELU_A, RELU_B>(P, Q, 0, K, pt << 4, (t - pt * tq) * 48, A, sap, sak, B,
-                                         sbq, sbk, epi);
-        }
-    }
-}
-
-// FULLCOV: address in x_recv / g_send of row r of layer l for local sample s.
-__device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int l, int r, int s) {
+// FULLCOV: address in x_recv / g_send of row r of layer l (wave-uniform) for
+// local sample s.  One source rank: one contiguous row per sample.  Several:
+// the row's source from the per-workgroup table srct in LDS ([nsrc][L]
+// source-end rows, then [nsrc][L] 64-bit offsets), built at kernel start.
+__device__ __forceinline__ int64_t fc_addr(const NetArgs& a, const int* srct, int l, int r, int s) {
+    if (a.nsrc == 1) return (int64_t)s * a.src_stride[0] + a.src_col[0][l] + r;
+    const int L = a.L;
     int p = 0;
-    while (p + 1 < a.nsrc && r >= a.src_hi[p][l]) ++p;
-    return a.src_base[p] + (int64_t)s * a.src_stride[p] + a.src_col[p][l] + (r - a.src_lo[p][l]);
+    while (p + 1 < a.nsrc && r >= srct[p * L + l]) ++p;
+    const int64_t* off = reinterpret_cast<const int64_t*>(srct + 2 * kMaxWorld * kMaxL);
+    return off[p * L + l] + r;
 }
 
-// diagnostics: one wave-0 lane of every workgroup records the shader clock at
-// phase boundaries (slot k of its row); costs nothing when stamps == nullptr
-#define NET_STAMP(k)                                                                   \
-    do {                                                                               \
-        if (a.stamps && threadIdx.x == 0)                                              \
-            a.stamps[(blockIdx.x + blockIdx.y * gridDim.x) * 16 + (k)] =               \
-                __builtin_amdgcn_s_memtime();                                          \
+// sum over each 16-lane row (DPP row rotations; every lane of the row active)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dppf<0x128>(v);  // row_ror:8
+    v += dppf<0x124>(v);  // row_ror:4
+    v += dppf<0x122>(v);  // row_ror:2
+    v += dppf<0x121>(v);  // row_ror:1
+    return v;
+}
+
+// diagnostics: one wave-0 lane of every workgroup records a clock at phase
+// boundaries into LDS (slot k), flushed to the stamp buffer at the end -- a
+// global store per stamp would make the next barrier wait for it; costs
+// nothing when stamps == nullptr
+#define NET_STAMP(k, val)                                                  \
+    do {                                                                   \
+        if (a.stamps && threadIdx.x == 0) stl[(k)] = (val);                \
     } while (0)
 
 template <int FAM>
@@ -222,87 +236,166 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
-    const int m0 = blockIdx.y * a.mc;
+    const int role = blockIdx.y;
+    const int m0 = blockIdx.z * a.mc;
     const int mcnt = min(a.mc, a.M - m0);
-    const int L = a.L;
+    const int L = a.L, Mp = a.Mp;
+    const int tid = threadIdx.x;
+    unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
+    if (a.stamps && threadIdx.x < 16) stl[threadIdx.x] = 0;
+    NET_STAMP(0, __builtin_amdgcn_s_memtime());
+    NET_STAMP(13, __builtin_amdgcn_s_memrealtime());  // chip-wide 100 MHz clock
 
-    // ---- 1. this sample's weights into LDS ------------------------------
-    // Global -> LDS copies issue kB independent loads per thread before any
-    // LDS store (a load-then-store loop would expose one memory latency per
-    // element); indices are clamped so every load is unconditional.
-    NET_STAMP(0);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-    float4* z4 = reinterpret_cast<float4*>(sm);
-    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float* dWt = sm + a.lg0 - a.ldwt;  // dW tile [dout][din + 1]
-    const int D = a.din[0], nU = mcnt * D;
-    float* U = sm + a.lu;
-    if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
-        // LDS-DMA (global_load_lds_dword): this sample's x rows (one contiguous
-        // run per source rank) and the u chunk land in the stage with no VGPR
-        // round trip; the resident regions are zeroed while they are in flight.
-        float* stage = sm + 4 * a.lstage_f4;
-        if (!(a.abl & 1)) {
-            for (int p = 0; p < a.nsrc; ++p) {
-                const int len = a.src_stride[p];
-                const float* src = a.xrecv + a.src_base[p] + (int64_t)s * len;
-                float* dst = stage + a.stage_off[p];
-                for (int c = wid; c * 64 < len; c += nwv)
-                    __builtin_amdgcn_global_load_lds(
-                        (const void*)(src + min(c * 64 + lane, len - 1)),
-                        (__attribute__((address_space(3))) void*)(dst + c * 64), 4, 0, 0);
-            }
-            const float* usrc = a.u + (int64_t)m0 * D;
-            float* udst = stage + a.stage_u;
-            for (int c = wid; c * 64 < nU; c += nwv)
-                __builtin_amdgcn_global_load_lds(
-                    (const void*)(usrc + min(c * 64 + lane, nU - 1)),
-                    (__attribute__((address_space(3))) void*)(udst + c * 64), 4, 0, 0);
+    // layers whose weight gradients this workgroup produces: [own_lo, own_hi)
+    const int own_lo = (a.nroles == 1 || role == 0) ? 0 : 1;
+    const int own_hi = (a.nroles == 1 || role == 1) ? L : 1;
+
+    // ---- 1. loads --------------------------------------------------------
+    int* srct = reinterpret_cast<int*>(sm + a.lsrc);
+    if (FAM == PSVI_FAMILY_FULLCOV && a.nsrc > 1) {
+        int64_t* off = reinterpret_cast<int64_t*>(srct + 2 * kMaxWorld * kMaxL);
+        for (int i = tid; i < a.nsrc * L; i += blockDim.x) {
+            const int p = i / L, l = i - p * L;
+            srct[i] = a.src_hi[p][l];
+            off[i] = a.src_base[p] + (int64_t)s * a.src_stride[p] + a.src_col[p][l] - a.src_lo[p][l];
         }
-        for (int i = threadIdx.x; i < a.lstage_f4; i += blockDim.x) z4[i] = zero4;
-        __syncthreads();  // drains the DMA (vmcnt(0)) and the zeroing
-        if (!(a.abl & 1)) {
-            for (int p = 0; p < a.nsrc; ++p) {
-                const float* st = stage + a.stage_off[p];
+        __syncthreads();
+    }
+    // Every global load of the phase is issued before its first LDS store:
+    // the u chunk (float4 per lane when rows are float4-sized), the labels and
+    // weights, and (full-cov) this sample's x row into a stage -- the source
+    // ranks' runs back to back -- later scattered into the padded W_l, b_l
+    // (LDS-DMA of the rows measured several times slower).  The stage
+    // overlaps the regions written from the forward pass on, whose slacks are
+    // zeroed in the first forward phase.
+    const int D = a.din[0];
+    const int r16 = tid >> 4, c16 = tid & 15, nr16 = blockDim.x >> 4;
+    float* zw = sm + a.lzw;  // the chunk's labels (as int bits) and weights
+    float* X0 = sm + a.lx[0];
+    const int ldx0 = a.ldx[0];
+    float* stage = sm + a.lstage;
+    {
+        constexpr int kU = 4, kX = 12;
+        const bool u4 = (D & 3) == 0;
+        const int nu = u4 ? mcnt * (D >> 2) : mcnt * D;  // float4s or floats of u
+        const float rdu = 1.f / (float)(u4 ? D >> 2 : D);
+        const float* usrc = a.u + (int64_t)m0 * D;
+        const int nx = FAM == PSVI_FAMILY_FULLCOV ? a.stage_off[a.nsrc] : 0;
+        const int bd = blockDim.x;
+        for (int pass = 0; pass * kU * bd < nu || pass * kX * bd < nx || pass == 0; ++pass) {  // uniform
+            const int bu = pass * kU * bd + tid, bx = pass * kX * bd + tid;
+            float4 uv[kU];
+            float xv[kX];
+            int zi = 0;
+            float wv = 0.f;
+            if (!(a.abl & 1)) {
+#pragma unroll
+                for (int k = 0; k < kU; ++k) {
+                    const int idx = max(min(bu + k * bd, nu - 1), 0);
+                    uv[k] = u4 ? *reinterpret_cast<const float4*>(usrc + 4 * idx)
+                               : make_float4(usrc[idx], 0.f, 0.f, 0.f);
+                }
+                if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
+#pragma unroll
+                    for (int k = 0; k < kX; ++k) {
+                        const int r = max(min(bx + k * bd, nx - 1), 0);
+                        int p = 0;
+#pragma unroll
+                        for (int q = 1; q < kMaxWorld; ++q)
+                            if (q < a.nsrc && r >= a.stage_off[q]) p = q;
+                        xv[k] = a.xrecv[a.src_base[p] + (int64_t)s * a.src_stride[p] + (r - a.stage_off[p])];
+                    }
+                }
+                if (pass == 0) {
+                    const int mm = min(tid, mcnt - 1);
+                    zi = a.z[m0 + mm];
+                    wv = a.w[m0 + mm];
+                }
+            }
+            if (pass == 0) {
+                // zero padding while the loads are in flight (disjoint from every
+                // loaded element): W columns >= din (16 lanes a row) and rows >=
+                // dout, u columns >= D up to the 16-multiple, u rows past the
+                // chunk, the slacks before the stage
                 for (int l = 0; l < L; ++l) {
-                    const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
-                    const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l];
-                    const float rdin = 1.f / (float)din;
-                    const float* sl = st + a.src_col[p][l] - lo;
+                    const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
+                    const int rows = (dout + 15) & ~15;
                     float* W = sm + a.lw[l];
-                    float* Bv = sm + a.lb[l];
-                    for (int r = lo + threadIdx.x; r < hi; r += blockDim.x) {
-                        const float v = sl[r];
+                    for (int j = r16; j < dout; j += nr16)
+                        for (int c = din + c16; c < ldw; c += 16) W[j * ldw + c] = 0.f;
+                    for (int i = tid; i < (rows - dout) * ldw; i += bd) W[dout * ldw + i] = 0.f;
+                }
+                const int cend = min((D + 15) & ~15, ldx0);
+                for (int m = r16; m < mcnt; m += nr16)
+                    if (D + c16 < cend) X0[m * ldx0 + D + c16] = 0.f;
+                for (int i = tid; i < (Mp - mcnt) * ldx0; i += bd) X0[mcnt * ldx0 + i] = 0.f;
+                for (int k = wave_id(); k < a.nslack_early; k += bd >> 6)  // wave-uniform slot
+                    sm[a.slack[k] + (tid & 63)] = 0.f;
+            }
+            if (a.abl & 1) continue;
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                const int idx = bu + k * bd;
+                if (idx < nu) {
+                    const int m = (int)(((float)idx + 0.5f) * rdu);  // exact for idx < 2^21
+                    if (u4) {
+                        const int c = idx - m * (D >> 2);
+                        *reinterpret_cast<float4*>(X0 + m * ldx0 + 4 * c) = uv[k];
+                    } else {
+                        X0[m * ldx0 + idx - m * D] = uv[k].x;
+                    }
+                }
+            }
+            if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
+#pragma unroll
+                for (int k = 0; k < kX; ++k)
+                    if (bx + k * bd < nx) stage[bx + k * bd] = xv[k];
+            }
+            if (pass == 0 && tid < mcnt) {
+                zw[tid] = __int_as_float(zi);
+                zw[Mp + tid] = wv;
+            }
+        }
+        for (int m = bd + tid; m < mcnt && !(a.abl & 1); m += bd) {  // chunks past one block
+            zw[m] = __int_as_float(a.z[m0 + m]);
+            zw[Mp + m] = a.w[m0 + m];
+        }
+    }
+    if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
+        __syncthreads();  // the stage is complete
+        // scatter: source p's run holds rows [lo, hi) of each layer l at
+        // src_col[p][l]; x row r of layer l is W[j][i] (r = j*din + i) or b
+        constexpr int kB = 8;
+        for (int p = 0; p < a.nsrc && !(a.abl & 1); ++p) {
+            for (int l = 0; l < L; ++l) {
+                const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
+                const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l];
+                const float rdin = 1.f / (float)din;
+                const float* sl = stage + a.stage_off[p] + a.src_col[p][l] - lo;
+                float* W = sm + a.lw[l];
+                float* Bv = sm + a.lb[l];
+                for (int base = lo + tid; base < hi; base += kB * (int)blockDim.x) {
+                    float v[kB];
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) v[k] = sl[min(base + k * (int)blockDim.x, hi - 1)];
+#pragma unroll
+                    for (int k = 0; k < kB; ++k) {
+                        const int r = base + k * (int)blockDim.x;
                         if (r < nw) {
                             // exact for r < 2^21: (r + 0.5) / din is >= 0.5/din from an integer
                             const int j = (int)(((float)r + 0.5f) * rdin), i = r - j * din;
-                            W[j * ldw + i] = v;
-                        } else {
-                            Bv[r - nw] = v;
+                            W[j * ldw + i] = v[k];
+                        } else if (r < hi) {
+                            Bv[r - nw] = v[k];
                         }
                     }
                 }
             }
-            const float* us = stage + a.stage_u;
-            const float rD = 1.f / (float)D;
-            for (int idx = threadIdx.x; idx < nU; idx += blockDim.x) {
-                const int m = (int)(((float)idx + 0.5f) * rD), i = idx - m * D;
-                U[m * a.ldu + i] = us[idx];
-            }
         }
-        for (int m = threadIdx.x; m < mcnt; m += blockDim.x) U[m * a.ldu + D] = 1.f;
-        __syncthreads();
-        for (int i = a.lstage_f4 + threadIdx.x; i < a.lds_f4; i += blockDim.x) z4[i] = zero4;
-        __syncthreads();
-        // ones column of every hidden activation (read from fwd layer 1 on,
-        // past the barrier that ends fwd layer 0)
-        for (int m = threadIdx.x; m < mcnt; m += blockDim.x)
-            for (int l = 0; l + 1 < L; ++l) sm[a.la[l] + m * a.lda[l] + a.dout[l]] = 1.f;
-    } else {
-        for (int i = threadIdx.x; i < a.lds_f4; i += blockDim.x) z4[i] = zero4;
-        __syncthreads();
+    } else if (!(a.abl & 1)) {
+        // Normal.rsample: loc + eps * softplus(rho), elementwise into place
         constexpr int kB = 16;
-        for (int l = 0; l < L && !(a.abl & 1); ++l) {
+        for (int l = 0; l < L; ++l) {
             const int din = a.din[l], dout = a.dout[l], nw = din * dout, n = nw + dout;
             float* W = sm + a.lw[l];
             float* Bv = sm + a.lb[l];
@@ -311,9 +404,8 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             const float* rho = mu + n;
             const float* eW = a.eps + a.eoff[l] + (int64_t)sg * nw;
             const float* eB = a.eps + a.eoff[l] + (int64_t)a.S_total * nw + (int64_t)sg * dout;
-            float* E = sm + a.le[l];
-            float* EB = sm + a.leb[l];
-            for (int base = threadIdx.x; base < n; base += kB * blockDim.x) {
+            const float rdin = 1.f / (float)din;
+            for (int base = tid; base < n; base += kB * blockDim.x) {
                 float vm[kB], vr[kB], ve[kB];
 #pragma unroll
                 for (int k = 0; k < kB; ++k) {
@@ -326,222 +418,253 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 for (int k = 0; k < kB; ++k) {
                     const int idx = base + k * (int)blockDim.x;
                     if (idx >= n) break;
-                    // Normal.rsample: loc + eps * scale (torch/distributions/normal.py)
                     const float val = vm[k] + ve[k] * softplus_f(vr[k]);
                     if (idx < nw) {
-                        const int j = idx / din, i = idx - j * din;
+                        // exact for idx < 2^21: (idx + 0.5) / din is >= 0.5/din from an integer
+                        const int j = (int)(((float)idx + 0.5f) * rdin), i = idx - j * din;
                         W[j * ldw + i] = val;
-                        E[j * ldw + i] = ve[k];
                     } else {
                         Bv[idx - nw] = val;
-                        EB[idx - nw] = ve[k];
                     }
                 }
             }
         }
-        if (!(a.abl & 1)) {
-            const float* src = a.u + (int64_t)m0 * D;
-            for (int base = threadIdx.x; base < nU; base += kB * blockDim.x) {
-                float v[kB];
+    }
+    __syncthreads();  // the LDS stores
+    NET_STAMP(1, __builtin_amdgcn_s_memtime());
+
+    // ---- 2. forward: X_{l+1} = relu(X_l W_l^T + b_l), then the logits
+    // X_L = X_{L-1} W_{L-1}^T + b_{L-1} into dl.  Rows past the chunk and
+    // columns past dout (up to the 16-multiple within the stride) are zero.
+    if (FAM == PSVI_FAMILY_FULLCOV)  // the slacks the stage overlapped
+        for (int k = a.nslack_early + wave_id(); k < a.nslack; k += blockDim.x >> 6)
+            sm[a.slack[k] + (tid & 63)] = 0.f;
+    for (int l = 0; l < L; ++l) {
+        const int din = a.din[l], dout = a.dout[l];
+        const bool head = l == L - 1;
+        const float* X = sm + a.lx[l];
+        float* Xn = head ? sm + a.ldl : sm + a.lx[l + 1];
+        const float* Bv = sm + a.lb[l];
+        const int ldn = head ? a.lddl : a.ldx[l + 1], jend = min((dout + 15) & ~15, ldn);
+        auto epi = [&](int m, int j, floatx4 v) {
+            if (j < jend) {
+                const bool jl = j < dout;
+                const float b = Bv[min(j, dout - 1)];
 #pragma unroll
-                for (int k = 0; k < kB; ++k) v[k] = src[min(base + k * (int)blockDim.x, nU - 1)];
-#pragma unroll
-                for (int k = 0; k < kB; ++k) {
-                    const int idx = base + k * (int)blockDim.x;
-                    if (idx >= nU) break;
-                    const int m = idx / D, i = idx - m * D;
-                    U[m * a.ldu + i] = v[k];
+                for (int r = 0; r < 4; ++r) {
+                    const float y = v[r] + b;
+                    Xn[(m + r) * ldn + j] = (jl && m + r < mcnt) ? (head ? y : fmaxf(y, 0.f)) : 0.f;
                 }
             }
-        }
-        // ones column (index dim) of u and of every hidden activation: the dW
-        // GEMM over [h | 1] then yields the bias gradient as its last column.
-        for (int m = threadIdx.x; m < mcnt; m += blockDim.x) {
-            U[m * a.ldu + D] = 1.f;
-            for (int l = 0; l + 1 < L; ++l) sm[a.la[l] + m * a.lda[l] + a.dout[l]] = 1.f;
-        }
-    }
-    __syncthreads();
-    NET_STAMP(1);
-
-    // ---- 3. forward --------------------------------------------------------
-    for (int l = 0; l < L && !(a.abl & 2); ++l) {
-        const float* H = l == 0 ? sm + a.lu : sm + a.la[l - 1];
-        const int ldh = l == 0 ? a.ldu : a.lda[l - 1];
-        float* Aout = sm + a.la[l];
-        const int ldo = a.lda[l];
-        const float* Bv = sm + a.lb[l];
-        auto epi = [&](int m, int j, float acc) { Aout[m * ldo + j] = acc + Bv[j]; };
-        if (l == 0)
-            lds_gemm<false, false>(mcnt, a.dout[l], a.din[l], H, ldh, 1, sm + a.lw[l], a.ldw[l],
-                                   1, epi);
-        else
-            lds_gemm<true, false>(mcnt, a.dout[l], a.din[l], H, ldh, 1, sm + a.lw[l], a.ldw[l],
-                                  1, epi);
+        };
+        if (l == 0) NET_STAMP(4, __builtin_amdgcn_s_memtime());
+        if (!(a.abl & 2))
+            mfma_gemm<true, true>(Mp, dout, din, 0, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
+        if (l == 0) NET_STAMP(5, __builtin_amdgcn_s_memtime());
         __syncthreads();
+        if (l < 3) NET_STAMP(9 + l, __builtin_amdgcn_s_memtime());
     }
+    NET_STAMP(2, __builtin_amdgcn_s_memtime());
 
-    NET_STAMP(2);
-    // ---- 4. weighted NLL, dlogits ------------------------------------------
+    // ---- 3. loss head: one thread per pseudopoint, logits -> weighted NLL,
+    // dlogits w_m (softmax - onehot) in place (rows past the chunk stay 0)
     {
-        const int C = a.dout[L - 1];
-        float* G = sm + a.la[L - 1];
-        const int ldg = a.lda[L - 1];
+        const int C = a.dout[L - 1], ldl = a.lddl;
         float part = 0.f;
-        for (int m = threadIdx.x; m < mcnt && !(a.abl & 4); m += blockDim.x) {
-            float* row = G + m * ldg;
-            float mx = row[0];
-            for (int k = 1; k < C; ++k) mx = fmaxf(mx, row[k]);
-            float se = 0.f;
-            for (int k = 0; k < C; ++k) se += expf(row[k] - mx);
-            const float lse = mx + logf(se);
-            const int zm = a.z[m0 + m];
-            const float wm = a.w[m0 + m];
-            part += wm * (lse - row[zm]);
-            for (int k = 0; k < C; ++k) {
-                const float pk = expf(row[k] - lse);
-                row[k] = wm * (pk - (k == zm ? 1.f : 0.f));
+        for (int m = tid; m < mcnt && !(a.abl & 4); m += blockDim.x) {
+            float* row = sm + a.ldl + m * ldl;
+            const int zm = __float_as_int(zw[m]);
+            const float wm = zw[Mp + m];
+            if (C <= kMaxC) {
+                float lg[kMaxC];
+                float mx = -INFINITY, lz = 0.f;
+#pragma unroll
+                for (int c = 0; c < kMaxC; ++c)
+                    if (c < C) {
+                        lg[c] = row[c];
+                        mx = fmaxf(mx, lg[c]);
+                        if (c == zm) lz = lg[c];
+                    }
+                float se = 0.f;
+#pragma unroll
+                for (int c = 0; c < kMaxC; ++c)
+                    if (c < C) se += expf(lg[c] - mx);
+                const float lse = mx + logf(se);
+                part += wm * (lse - lz);
+#pragma unroll
+                for (int c = 0; c < kMaxC; ++c)
+                    if (c < C) row[c] = wm * (expf(lg[c] - lse) - (c == zm ? 1.f : 0.f));
+            } else {
+                float mx = -INFINITY, lz = 0.f;
+                for (int c = 0; c < C; ++c) {
+                    mx = fmaxf(mx, row[c]);
+                    if (c == zm) lz = row[c];
+                }
+                float se = 0.f;
+                for (int c = 0; c < C; ++c) se += expf(row[c] - mx);
+                const float lse = mx + logf(se);
+                part += wm * (lse - lz);
+                for (int c = 0; c < C; ++c)
+                    row[c] = wm * (expf(row[c] - lse) - (c == zm ? 1.f : 0.f));
             }
         }
-        const float tot = block_sum(part, sm + a.lred);
-        if (threadIdx.x == 0) atomicAdd(a.nll_out, (double)tot);
+        if (role == 0) {
+            const float tot = block_sum(part, sm + a.lred);  // its barriers end the phase
+            if (tid == 0) atomicAdd(a.nll_out, (double)tot);
+        }
         __syncthreads();
     }
+    NET_STAMP(3, __builtin_amdgcn_s_memtime());
 
-    NET_STAMP(3);
-    // ---- 5. backward -------------------------------------------------------
+    // ---- 4. backward, l = L-1 .. 0: dW_l (if owned) and G_{l-1} (if a lower
+    // layer is owned), both from G_l (G_{L-1} = dlogits), their tiles in one
+    // round-robin
     float sink = 0.f;
-    for (int l = L - 1; l >= 0 && !(a.abl & 8); --l) {
-        const int din = a.din[l], dout = a.dout[l], nw = din * dout, qw = din + 1;
-        // g_l: dlogits in the last activation buffer, else a ping-pong buffer
-        const float* G = l == L - 1 ? sm + a.la[L - 1] : sm + (((L - 1 - l) & 1) ? a.lg0 : a.lg1);
-        const int ldg = l == L - 1 ? a.lda[L - 1] : a.ldgb;
-        float* Gn = sm + (((L - l) & 1) ? a.lg0 : a.lg1);  // g_{l-1}
-        const float* H = l == 0 ? sm + a.lu : sm + a.la[l - 1];
-        const int ldh = l == 0 ? a.ldu : a.lda[l - 1];
-        // dW_l = g_l^T [h_{l-1} | 1] into the LDS dW tile, and
-        // g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] into the other gradient buffer
-        {
-            auto epi = [&](int j, int i, float v) { dWt[j * qw + i] = v; };
-            if (l == 0)
-                lds_gemm<false, false>(dout, qw, mcnt, G, 1, ldg, H, 1, ldh, epi);
-            else
-                lds_gemm<false, true>(dout, qw, mcnt, G, 1, ldg, H, 1, ldh, epi);
-        }
-        if (l > 0 && !(a.abl & 128)) {
-            const float* Ap = sm + a.la[l - 1];
-            const int ldp = a.lda[l - 1];
-            auto epi = [&](int m, int i, float v) {
-                Gn[m * a.ldgb + i] = Ap[m * ldp + i] > 0.f ? v : 0.f;
-            };
-            lds_gemm<false, false>(mcnt, din, dout, G, ldg, 1, sm + a.lw[l], 1, a.ldw[l], epi);
-        }
-        __syncthreads();
-        NET_STAMP(4 + 2 * (L - 1 - l));
-        // dW tile -> global as contiguous rows; re-zero the tile
-        const int nt = dout * qw;
-        if (FAM == PSVI_FAMILY_MEANFIELD) {
-            float* accMu = a.accMu + a.woff[l];
-            float* accRho = a.accRho + a.woff[l];
-            const float* E = sm + a.le[l];
-            const float* EB = sm + a.leb[l];
-            for (int idx = threadIdx.x; idx < nt; idx += blockDim.x) {
-                const int j = idx / qw, i = idx - j * qw;
-                const float dw = dWt[idx];
-                const int o = i < din ? j * din + i : nw + j;
-                const float e = i < din ? E[j * a.ldw[l] + i] : EB[j];
-                if (a.abl & 16) { sink += dw; continue; }
-                atomicAdd(accMu + o, dw);
-                atomicAdd(accRho + o, dw * e);
-            }
+    // gradient element o of layer l: W rows j*din + i, then the biases
+    auto emit = [&](int l, int o, float v) {
+        if (a.abl & 16) { sink += v; return; }
+        if constexpr (FAM == PSVI_FAMILY_MEANFIELD) {
+            const int din = a.din[l], dout = a.dout[l], nw = din * dout;
+            const float e = o < nw ? a.eps[a.eoff[l] + (int64_t)sg * nw + o]
+                                   : a.eps[a.eoff[l] + (int64_t)a.S_total * nw +
+                                           (int64_t)sg * dout + o - nw];
+            atomicAdd(a.accMu + a.woff[l] + o, v);
+            atomicAdd(a.accRho + a.woff[l] + o, v * e);
         } else {
-            const bool at = a.atomic_g != 0;
-            for (int idx = threadIdx.x; idx < nt; idx += blockDim.x) {
-                const int j = idx / qw, i = idx - j * qw;
-                const float dw = dWt[idx];
-                if (a.abl & 16) { sink += dw; continue; }
-                // column din of [h | 1] is the bias gradient
-                float* dst = a.gsend + fc_addr(a, l, i < din ? j * din + i : nw + j, s);
-                if (at) atomicAdd(dst, dw); else *dst = dw;
+            float* dst = a.gsend + fc_addr(a, srct, l, o, s);
+            if (a.atomic_g) atomicAdd(dst, v); else *dst = v;
+        }
+    };
+    int stamp = 4, cur = 0;  // cur: gradient buffer that receives G_{l-1}
+    for (int l = L - 1; l >= 0 && !(a.abl & 8); --l) {
+        const bool own = l >= own_lo && l < own_hi;
+        const bool prop = l >= 1 && own_lo < l;
+        if (!own && !prop) break;
+        const int din = a.din[l], dout = a.dout[l];
+        const float* G = l == L - 1 ? sm + a.ldl : sm + a.lg[cur ^ 1];
+        const int ldg = l == L - 1 ? a.lddl : a.ldx[l + 1];  // G_l: the stride of X_{l+1}
+        const float* X = sm + a.lx[l];
+        const int ldx = a.ldx[l];
+        float* Gn = sm + a.lg[cur];  // G_{l-1}: row stride ldx (of X_l)
+        int first = 0;
+        if (own) {
+            // dW_l[j][i] = sum_m G_l[m][j] X_l[m][i]: both operands k(=m)-strided
+            auto epi = [&](int j, int i, floatx4 v) {
+                if (i < din) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (j + r < dout) emit(l, (j + r) * din + i, v[r]);
+                }
+            };
+            mfma_gemm<false, false>(dout, din, Mp, 0, G, ldg, X, ldx, epi);
+            first = gemm_units(dout, din);
+        }
+        if (prop) {
+            // G_{l-1}[m][i] = (sum_j G_l[m][j] W_l[j][i]) * 1[X_l[m][i] > 0]
+            const int iend = min((din + 15) & ~15, ldx);
+            auto epi = [&](int m, int i, floatx4 v) {
+                if (i < iend) {
+                    const bool il = i < din;
+                    float h[4];  // the ReLU masks, read before any store (Gn may alias X)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) h[r] = X[(m + r) * ldx + i];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) Gn[(m + r) * ldx + i] = (il && h[r] > 0.f) ? v[r] : 0.f;
+                }
+            };
+            mfma_gemm<true, false>(Mp, din, dout, first, G, ldg, sm + a.lw[l], a.ldw[l], epi);
+        }
+        if (own) {
+            // bias gradient: column sums of G_l over the chunk, 16 lanes a column
+            for (int base = 0; base < dout; base += nr16) {  // uniform: DPP rows converge
+                const int j = min(base + r16, dout - 1);
+                float acc = 0.f;
+                for (int m = c16; m < mcnt; m += 16) acc += G[m * ldg + j];
+                acc = row16_sum(acc);
+                if (c16 == 0 && base + r16 < dout) emit(l, dout * din + j, acc);
             }
         }
+        if (!prop) break;
         __syncthreads();
-        NET_STAMP(5 + 2 * (L - 1 - l));
+        NET_STAMP(min(stamp++, 8) + 2, __builtin_amdgcn_s_memtime());
+        cur ^= 1;
     }
     asm volatile("" ::"v"(sink));
+    NET_STAMP(12, __builtin_amdgcn_s_memtime());
+    NET_STAMP(14, __builtin_amdgcn_s_memrealtime());
+    if (a.stamps && threadIdx.x < 16)  // wave 0 wrote them: in order, no barrier needed
+        a.stamps[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 16 + threadIdx.x] =
+            stl[threadIdx.x];
 }
 
-static inline int odd_ld(int x) { return (x & 1) ? x : x + 1; }
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+static inline int ld4o(int x) { return x + (12 - x % 8) % 8; }  // >= x, == 4 (mod 8)
 
-// LDS floats needed for a chunk of `mc` points.  Padding contract of
-// gemm_unit (everything zero-filled at kernel start):
-//   W_l: rup(dout,32) rows (rows >= dout stay 0), odd stride >= rup(din,16)
-//        (columns din.. stay 0): k past din / dout meets zeros;
-//   h buffers (u, activations, gradients): rup(mc,16) rows (rows >= mcnt
-//        stay 0: k past the pseudopoint count meets zeros), odd stride with a
-//        ones column at index dim for u / hidden activations;
-//   every region is followed by 64 floats of zero slack for the row-wrap
-//   reads of out-of-range rows / columns (whose outputs are dropped).
-//   Resident regions (weights, u) come first; the late regions (activations,
-//   dW tile, gradient buffers) follow from lstage and double as the landing
-//   area of the full-cov LDS-DMA loads before they are zeroed.
+// LDS floats for a chunk of `mc` pseudopoints (layout and padding contract
+// in the header comment); fills the carve into `a` when given.  Row strides
+// are 4 x odd: a 16-lane float4 read along k (rows i16 = 0..15) and a 64-lane
+// float read down k (lanes 16 k4 + i16, rows 4 k4 apart) both hit distinct
+// banks.  Regions read before the forward pass come first; the full-cov x
+// stage overlaps the rest.
 static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     size_t off = 0;
+    int ns = 0;
     auto take = [&](size_t nfl) {
-        size_t o = off;
-        off += ((nfl + 3) & ~size_t(3)) + 64;
+        const size_t o = off;
+        off += (nfl + 3) & ~size_t(3);
+        if (a) a->slack[ns] = (int)off;
+        ++ns;
+        off += 64;
         return (int)o;
     };
-    const int mcr = rup(mc, 16);
-    int maxh = 1, wt = 1;
+    const int Mp = rup(mc, 16);
     for (int l = 0; l < p.L; ++l) {
         const int din = p.lay[l].din, dout = p.lay[l].dout;
-        if (l > 0) maxh = std::max(maxh, din);
-        wt = std::max(wt, dout * (din + 1));
-        const int ldw = odd_ld(rup(din, 16));
-        int lw = take((size_t)rup(dout, 32) * ldw), lb = take(dout);
-        int le = 0, leb = 0;
-        if (p.family == PSVI_FAMILY_MEANFIELD) {
-            le = take((size_t)dout * ldw);
-            leb = take(dout);
-        }
-        if (a) {
-            a->ldw[l] = ldw; a->lw[l] = lw; a->lb[l] = lb; a->le[l] = le; a->leb[l] = leb;
-        }
+        const int ldw = ld4o(rup(din, 16));
+        const int lw = take((size_t)rup(dout, 16) * ldw), lb = take(dout);
+        if (a) { a->lw[l] = lw; a->ldw[l] = ldw; a->lb[l] = lb; }
     }
-    const int ldu = odd_ld(p.lay[0].din + 1);
-    int lu = take((size_t)mcr * ldu);
-    int lred = take(16);
+    const int ldx0 = ld4o(p.lay[0].din);
+    const int lx0 = take((size_t)Mp * ldx0);
+    const int lred = take(16);
+    const int lzw = take(2 * (size_t)Mp);
+    const int lstamp = take(32);  // 16 x uint64 diagnostics stamps
+    // per-workgroup source table: [nsrc][L] ints, then [nsrc][L] int64 (8-byte aligned)
+    const int lsrc = take(2 * kMaxWorld * kMaxL + 2 * kMaxWorld * kMaxL);
+    const int ns_early = ns;
     const size_t lstage = off;
-    for (int l = 0; l < p.L; ++l) {
-        const int lda = odd_ld(p.lay[l].dout + 1);
-        int la = take((size_t)mcr * lda);
-        if (a) { a->la[l] = la; a->lda[l] = lda; }
+    int ldgmax = 4;
+    for (int l = 1; l < p.L; ++l) {
+        const int ldx = ld4o(p.lay[l].din);
+        const int lx = take((size_t)Mp * ldx);
+        ldgmax = std::max(ldgmax, ldx);
+        if (a) { a->lx[l] = lx; a->ldx[l] = ldx; }
     }
-    const int wt4 = (wt + 3) & ~3;
-    const int ldgb = odd_ld(maxh);
-    // the dW tile sits directly in front of the first gradient buffer
-    off += wt4;
-    int lg0 = take((size_t)mcr * ldgb);
-    int lg1 = take((size_t)mcr * ldgb);
+    int lg0 = 0, lg1 = 0;
+    if (p.L > 1) {
+        lg0 = take((size_t)Mp * ldgmax);
+        lg1 = take((size_t)Mp * ldgmax);
+    }
+    const int lddl = ld4o(p.lay[p.L - 1].dout);
+    const int ldl = take((size_t)Mp * lddl);
     if (p.family == PSVI_FAMILY_FULLCOV) {
-        // DMA stage: whole-wave (64-float) pieces per source, then u
-        size_t st = lstage;
+        size_t st = 0;
         for (int q = 0; q < p.world; ++q) {
-            if (a) a->stage_off[q] = (int)(st - lstage);
-            st += (size_t)rup(p.rows_tot[q], 64);
+            if (a) a->stage_off[q] = (int)st;
+            st += (size_t)p.rows_tot[q];
         }
-        if (a) a->stage_u = (int)(st - lstage);
-        st += (size_t)rup(mc * p.lay[0].din, 64);
-        off = std::max(off, st);
+        if (a) a->stage_off[p.world] = (int)st;
+        off = std::max(off, lstage + st);
     }
     off = (off + 3) & ~size_t(3);
     if (a) {
-        a->lu = lu; a->ldu = ldu; a->lred = lred;
-        a->lg0 = lg0; a->lg1 = lg1; a->ldgb = ldgb; a->ldwt = wt4;
+        a->lx[0] = lx0; a->ldx[0] = ldx0;
+        a->lg[0] = lg0; a->lg[1] = lg1; a->ldl = ldl; a->lddl = lddl;
+        a->lred = lred; a->lsrc = lsrc; a->lzw = lzw; a->lstamp = lstamp; a->lstage = (int)lstage;
+        a->Mp = Mp;
+        a->nslack = ns;
+        a->nslack_early = ns_early;
         a->lds_f4 = (int)(off / 4);
-        a->lstage_f4 = (int)(lstage / 4);
     }
     return off;
 }
@@ -550,14 +673,18 @@ int g_net_split_below = 256;  // split when a rank has fewer samples than CUs (p
 
 size_t net_plan_geometry(psvi_plan& p) {
     // One workgroup per sample and all M pseudopoints when the samples alone
-    // fill the chip (G gets plain stores: no memset, no atomics); otherwise
-    // split the pseudopoints over workgroups (partial dW summed with atomics).
-    // LDS <= 160 KiB per workgroup.
+    // fill the chip.  Otherwise two role workgroups per sample (disjoint
+    // gradient outputs), and pseudopoint chunks only if that still leaves
+    // CUs idle or the buffers exceed the LDS (partial dW summed with atomics
+    // onto a zeroed g_send).  LDS <= 160 KiB per workgroup.
     const int S_local = std::max(1, p.s_cnt[p.rank]);
     const int M = p.d.M;
+    const bool split = S_local < g_net_split_below;
+    p.net_roles = (split && p.L > 1) ? 2 : 1;
     int mchunks = 1;
-    if (S_local < g_net_split_below)
-        while (S_local * mchunks < 256 && (M + mchunks) / (mchunks + 1) >= 16) ++mchunks;
+    if (split)
+        while (S_local * p.net_roles * mchunks < 256 && (M + mchunks) / (mchunks + 1) >= 16)
+            ++mchunks;
     for (;;) {
         const int mc = (M + mchunks - 1) / mchunks;
         const size_t bytes = net_lds_floats(p, mc, nullptr) * 4;
@@ -565,7 +692,7 @@ size_t net_plan_geometry(psvi_plan& p) {
             p.mchunks = (M + mc - 1) / mc;
             p.mc = mc;
             p.net_lds = bytes;
-            p.net_threads = mc > 32 ? 512 : 256;
+            p.net_threads = rup(mc, 16) >= 48 ? 512 : 256;
             return bytes;
         }
         ++mchunks;
@@ -593,6 +720,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     a.S_total = p.d.S;
     a.s_goff = p.s_off[p.rank];
     a.atomic_g = p.mchunks > 1;
+    a.nroles = p.net_roles;
     a.abl = g_net_ablation;
     a.stamps = g_net_stamps;
     for (int l = 0; l < p.L; ++l) {
@@ -621,7 +749,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
             base += (int64_t)S_local * p.rows_tot[q];
         }
     }
-    dim3 grid(p.s_cnt[p.rank], p.mchunks), block(p.net_threads);
+    dim3 grid(p.s_cnt[p.rank], p.net_roles, p.mchunks), block(p.net_threads);
     if (p.s_cnt[p.rank] == 0) return hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL(net_kernel<PSVI_FAMILY_MEANFIELD>, grid, block, p.net_lds, st, a);

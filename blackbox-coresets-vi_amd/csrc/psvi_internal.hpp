@@ -22,6 +22,14 @@ __device__ __forceinline__ float softplus_f(float x) {
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
 
+// The wave's index in its workgroup, in an SGPR: the compiler cannot prove
+// threadIdx.x >> 6 wave-uniform, and treats loops and branches on it as
+// divergent (exec-masked, with conservative s_waitcnt that drain every
+// outstanding load at the branch).
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
@@ -31,7 +39,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 // Block-wide sum; `red` is >= blockDim/64 floats of LDS.  All threads call.
 __device__ __forceinline__ float block_sum(float v, float* red) {
     v = wave_sum(v);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = wave_id();
     __syncthreads();
     if (lane == 0) red[wid] = v;
     __syncthreads();
@@ -177,7 +185,7 @@ struct psvi_plan {
     int n_upd = 0;
     int upd_tiles = 0;  // c-blocks over all chunks (work measure)
     // net kernel geometry
-    int mchunks = 1, mc = 0, net_threads = 256;
+    int mchunks = 1, mc = 0, net_threads = 256, net_roles = 1;
     size_t net_lds = 0;
     size_t ws_bytes = 0;
     int64_t acc_count = 0;

@@ -231,21 +231,31 @@ const char* psvi_version(void);
 
 /* ---- diagnostics (profiling builds of a run; never needed for results) ---- */
 #define PSVI_DBG_NET_ABLATION 1  /* value: mask of network-kernel parts to skip
-                                    (1 loads, 2 fwd GEMMs, 4 NLL, 8 bwd GEMMs,
-                                    16 global dW writes); 0 = full kernel      */
+                                    (1 loads, 2 fwd GEMMs, 4 loss head, 8
+                                    backward, 16 global dW writes); 0 = full   */
 int psvi_debug_set(int32_t key, int32_t value);
 #define PSVI_DBG_NET_STAMPS 2    /* ptr: device uint64 buffer, 16 slots per
                                     network-kernel workgroup: s_memtime at
-                                    phase boundaries; NULL = off               */
+                                    phase boundaries (1 loads, 9..11 forward
+                                    layers, 2 forward, 3 head, 4..8 backward
+                                    phases, 12 end; 13 / 14 s_memrealtime
+                                    start / end)                               */
 #define PSVI_DBG_UPD_ABLATION 3  /* value: mask of full-cov update-kernel parts to
-                                    skip (1 G/eps loads, 2 MFMAs, 4 epilogue
-                                    loads, 8 epilogue stores)                  */
+                                    replace (1 G/eps loads by one cached
+                                    address, 2 dL MFMAs skipped, 4 corr/m/v
+                                    loads by one address, 8 stores skipped,
+                                    16 fused-sample MFMAs skipped, 32 eps_next
+                                    loads by one address, 64 Adam math by an
+                                    add)                                       */
 #define PSVI_DBG_UPD_STAMPS 4    /* ptr: device uint64 buffer, 16 slots per
                                     update-kernel workgroup (start, staged,
-                                    MFMA done, end, HW_ID, XCC_ID, tile read,
-                                    loads issued, LDS written)                 */
-#define PSVI_DBG_NET_SPLIT_BELOW 5 /* value: split each sample's pseudopoints over
-                                    several network workgroups when a rank has
+                                    loop done, end, HW_ID, XCC_ID; S <= 128:
+                                    6..11 = summed shader clocks of eps stage
+                                    1, MFMA half 1, stage 2, MFMA half 2,
+                                    epilogue, fused-sample GEMM)               */
+#define PSVI_DBG_NET_SPLIT_BELOW 5 /* value: give each sample two network
+                                    workgroups (gradient roles; pseudopoint
+                                    chunks if still short of CUs) when a rank has
                                     fewer samples than this (plans created
                                     afterwards; default 256)                   */
 #define PSVI_DBG_FWD_ABLATION 6  /* value: mask of full-cov sample-kernel parts to

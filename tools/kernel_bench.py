@@ -88,6 +88,7 @@ def main():
                             x_next=x2)
             st[0] += 1
         out["update+next sample (fused)"] = timeit(upd_smp, iters)
+    if fam == "fullcov" and plan.tiled_floats:
         ts = plan.tiled_state()
         plan.tiled_convert(params, m, v, ts, True)
 
@@ -101,6 +102,7 @@ def main():
         out["tiled convert (both ways)"] = timeit(
             lambda: (plan.tiled_convert(params, m, v, ts, True),
                      plan.tiled_convert(params, m, v, ts, False)), 20)
+    if fam == "fullcov":
         T = 20
         elb = torch.empty(T, dtype=torch.float64, device=dev)
         lws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)

@@ -14,23 +14,52 @@ import torch  # noqa: E402
 
 from psvi.runtime import InnerLoopPlan  # noqa: E402
 
-NAMES = ["loads", "fwd", "nll", "bwd2 gemm", "bwd2 out", "bwd1 gemm", "bwd1 out",
-         "bwd0 gemm", "bwd0 out"]
 CFG = {"c3": ([(64, 40), (40, 40), (40, 2)], 128, 100),
        "c4": ([(64, 40), (40, 40), (40, 2)], 1024, 200)}
 
 
-def report(name, t, abl):
-    t = t[t[:, 0] != 0]
-    d = (t[:, 1:12] - t[:, 0:1]).float()
-    prev = torch.zeros(d.shape[0])
-    print(f"{name} abl={abl}: {t.shape[0]} workgroups; s_memtime ticks, median per phase:")
-    for k, nm in enumerate(NAMES):
-        cur = d[:, k]
-        print(f"  {nm:10s} {float((cur - prev).median()):10.0f}")
-        prev = cur
-    print(f"  total      {float(d[:, len(NAMES) - 1].median()):10.0f}  "
-          f"(max {float(d[:, len(NAMES) - 1].max()):.0f})")
+def report(name, t, abl, S):
+    """Per role (workgroup rows s + S*role): median shader-clock ticks per phase."""
+    t = t[: 2 * S]
+    for role in (0, 1):
+        r = t[role * S:(role + 1) * S]
+        r = r[r[:, 0] != 0]
+        if r.shape[0] == 0:
+            continue
+        d = (r.double() - r[:, 0:1].double())
+        print(f"{name} abl={abl} role {role}: {r.shape[0]} workgroups; s_memtime ticks, median per phase:")
+        prev = torch.zeros(r.shape[0], dtype=torch.float64)
+        fw = [k for k in (9, 10, 11) if int((r[:, k] != 0).sum()) == r.shape[0]]
+        bw = [k for k in range(6, 9) if int((r[:, k] != 0).sum()) == r.shape[0]]
+        if int((r[:, 4] != 0).sum()) == r.shape[0]:
+            print(f"  (wave 0 in fwd layer 0: setup {float((d[:, 4] - d[:, 1]).median()):.0f}, "
+                  f"own GEMM {float((d[:, 5] - d[:, 4]).median()):.0f}, "
+                  f"barrier wait {float((d[:, 9] - d[:, 5]).median()):.0f})")
+        cols = [1] + fw + [2, 3] + bw + [12]
+        names = (["loads"] + [f"fwd layer {k - 9}" for k in fw] + ["fwd rest", "loss head"] +
+                 [f"bwd phase {k - 5}" for k in bw] + ["last bwd"])
+        for k, nm in zip(cols, names):
+            cur = d[:, k]
+            print(f"  {nm:12s} {float((cur - prev).median()):10.0f}")
+            prev = cur
+        print(f"  total        {float(d[:, 12].median()):10.0f}  (max {float(d[:, 12].max()):.0f})")
+        timeline(r, 13, 14)
+
+
+def timeline(t, c0, c1):
+    """Chip timeline from the 100 MHz s_memrealtime stamps in slots c0 (start), c1 (end)."""
+    st, en = t[:, c0].double(), t[:, c1].double()
+    ok = (st > 0) & (en > 0)
+    st, en = st[ok], en[ok]
+    if st.numel() == 0:
+        return
+    t0 = float(st.min())
+    q = lambda x: [float(v) for v in torch.quantile((x - 0).float(), torch.tensor([0.1, 0.5, 0.9, 1.0]))]
+    s_ = q((st - t0) * 0.01)
+    e_ = q((en - t0) * 0.01)
+    d_ = q((en - st) * 0.01)
+    print(f"  realtime (us from first start): start p10/50/90/max {s_[0]:.1f}/{s_[1]:.1f}/{s_[2]:.1f}/{s_[3]:.1f}"
+          f"  end {e_[0]:.1f}/{e_[1]:.1f}/{e_[2]:.1f}/{e_[3]:.1f}  life {d_[0]:.1f}/{d_[1]:.1f}/{d_[2]:.1f}/{d_[3]:.1f}")
 
 
 def main():
@@ -57,7 +86,7 @@ def main():
         torch.cuda.synchronize()
         plan.lib.psvi_debug_set_ptr(2, None)
         plan.lib.psvi_debug_set(1, 0)
-        report(name, st.view(nblk, 16).cpu().clone(), abl)
+        report(name, st.view(nblk, 16).cpu().clone(), abl, S)
 
 
 if __name__ == "__main__":

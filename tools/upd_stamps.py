@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Full-cov update kernel under the diagnostics API: per-workgroup shader-clock
-stamps (start / first staging / step loop done / end, HW_ID, XCC_ID) and event timing
-under ablation masks (1 G/eps loads, 2 MFMAs, 4 epilogue loads, 8 stores).
+stamps (start / first staging / step loop done / end, HW_ID, XCC_ID, summed
+loop phases) and event timing under ablation masks (psvi_hip.h
+PSVI_DBG_UPD_ABLATION: 1 G/eps loads, 2 MFMAs, 4 corr/m/v loads, 8 stores,
+16 fused-sample MFMAs, 32 eps_next loads, 64 Adam math).
 
-  python tools/upd_stamps.py [c3|c4] [abl,abl,...] [grad|adam]
+  python tools/upd_stamps.py [c3|c4] [abl,abl,...] [grad|adam|fused]
+
+fused = the bench's kernel: tiled state + next-step sample.
 """
 import ctypes
 import os
@@ -47,6 +51,30 @@ def report(t, nblk):
     xid = xcc & 0xF
     walls = [float(end[xid == x].max() - start[xid == x].min()) for x in torch.unique(xid)]
     print(f"  per-XCD wall ticks: min {min(walls):.0f} max {max(walls):.0f}")
+    timeline(t, 12, 13)
+    names = ("eps stage 1", "MFMA half 1", "eps stage 2", "MFMA half 2", "epilogue",
+             "sample GEMM")
+    ph = t[:, 6:12].double()
+    if float(ph.sum()) > 0:
+        print("  loop phases (median per workgroup, summed over its c-blocks):")
+        for k, nm in enumerate(names):
+            print(f"    {nm:12s} {float(ph[:, k].median()):8.0f}")
+
+
+def timeline(t, c0, c1):
+    """Chip timeline from the 100 MHz s_memrealtime stamps in slots c0 (start), c1 (end)."""
+    st, en = t[:, c0].double(), t[:, c1].double()
+    ok = (st > 0) & (en > 0)
+    st, en = st[ok], en[ok]
+    if st.numel() == 0:
+        return
+    t0 = float(st.min())
+    q = lambda x: [float(v) for v in torch.quantile((x - 0).float(), torch.tensor([0.1, 0.5, 0.9, 1.0]))]
+    s_ = q((st - t0) * 0.01)
+    e_ = q((en - t0) * 0.01)
+    d_ = q((en - st) * 0.01)
+    print(f"  realtime (us from first start): start p10/50/90/max {s_[0]:.1f}/{s_[1]:.1f}/{s_[2]:.1f}/{s_[3]:.1f}"
+          f"  end {e_[0]:.1f}/{e_[1]:.1f}/{e_[2]:.1f}/{e_[3]:.1f}  life {d_[0]:.1f}/{d_[1]:.1f}/{d_[2]:.1f}/{d_[3]:.1f}")
 
 
 def main():
@@ -66,9 +94,18 @@ def main():
     kl = torch.zeros(1, dtype=torch.float64, device=dev)
     lib = plan.lib
 
+    if mode == "fused":
+        tstate = plan.tiled_state()
+        plan.tiled_convert(params, m, v, tstate, True)
+        eps_n = torch.randn(plan.eps_count, generator=g).to(dev)
+        x_n = torch.empty(plan.xshard_count, device=dev)
+
     def run():
         if mode == "grad":
             plan.mvn_update(eps, gs, params, kl_out=kl, grad_out=grad)
+        elif mode == "fused":
+            plan.mvn_update_tiled(eps, gs, params, m, v, tstate, step=1, lr=0.0, kl_out=kl,
+                                  eps_next=eps_n, x_next=x_n)
         else:
             plan.mvn_update(eps, gs, params, m, v, step=1, lr=0.0, kl_out=kl)
 
