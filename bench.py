@@ -8,7 +8,10 @@ samples PER GPU (C3 on one GPU; weak scaling: S = 128 N on N GPUs, the
 N = 8 point being the C4 sample count).  One step = fresh eps draw (Philox),
 reparameterised sampling x_s = mean + L eps_s, batched forward over S x M,
 coreset-weighted NLL + KL, hand-derived backward, higher-Adam update of all
-parameters.  Inputs are synthetic (make_synthetic-shaped: X ~ N(0, I_64),
+parameters.  One GPU: the K timed steps are ONE psvi_inner_loop call (the
+product path: T chained steps, fresh Adam state, tiled corr/m/v, every
+conversion and the first sample inside the timed region); the W warm-up
+steps are a separate call.  Inputs are synthetic (make_synthetic-shaped: X ~ N(0, I_64),
 labels ~ Bernoulli(sigmoid(5 sum x))), parameters at the reference init
 (mean = 0, sd = softplus^-1(1e-6), corr = 0), N_data = 800, v = 0.
 
@@ -17,6 +20,7 @@ labels ~ Bernoulli(sigmoid(5 sum x))), parameters at the reference init
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -167,37 +171,47 @@ def main():
     m = torch.zeros_like(params)
     v = torch.zeros_like(params)
     eps = torch.empty(plan.eps_count, device=dev)
-    eps_b = [eps, torch.empty(plan.eps_count, device=dev)]  # this step / next step (world 1)
     eps_stride = (plan.eps_count + 3) // 4 * 4
-    f32 = dict(dtype=torch.float32, device=dev)
-    if world == 1:
-        xs = torch.empty(plan.xshard_count, **f32)
-        gs = torch.empty(plan.xshard_count, **f32)
     total_steps = args.warmup + args.steps
-    parts = torch.zeros(total_steps, 2, dtype=torch.float64, device=dev)
     # per-phase HIP events on every EV_EVERY-th timed step (event records between
     # kernels add dispatch latency; sampling keeps the timed region representative)
     EV_EVERY = 10
-    ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-          for k in range(args.warmup, total_steps) if (k - args.warmup) % EV_EVERY == 0}
+    if world == 1:
+        lib = plan.lib
+        ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+        elbo_w = torch.empty(max(args.warmup, 1), dtype=torch.float64, device=dev)
+        elbo_t = torch.empty(args.steps, dtype=torch.float64, device=dev)
+        if args.warmup:
+            plan.inner_loop(u, z, w, params, m, v, args.warmup, LR, seed=20251015,
+                            elbo_out=elbo_w, ws=ws)
+        # the timed loop starts over from the reference init with fresh Adam state
+        params.copy_(reference_init_params(LAYERS, dev))
+        m.zero_()
+        v.zero_()
+        torch.cuda.synchronize()
+        check_rc = lib.psvi_debug_set(8, EV_EVERY)  # PSVI_DBG_LOOP_TIMING
+        if check_rc:
+            raise RuntimeError("psvi_debug_set(PSVI_DBG_LOOP_TIMING) failed")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan.inner_loop(u, z, w, params, m, v, args.steps, LR, seed=20251015,
+                        offset=args.warmup * eps_stride, elbo_out=elbo_t, ws=ws)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        tm = (ctypes.c_double * 3)()
+        if lib.psvi_debug_loop_timing(tm):
+            raise RuntimeError("psvi_debug_loop_timing failed")
+        lib.psvi_debug_set(8, 0)
+        avg_ms = {"exchange+net": tm[0] * 1e-3, "update": tm[1] * 1e-3}
+        parts = elbo_t[:, None]
+    else:
+        parts = torch.zeros(total_steps, 2, dtype=torch.float64, device=dev)
+        ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+              for k in range(args.warmup, total_steps) if (k - args.warmup) % EV_EVERY == 0}
 
-    def one_step(k, timed):
-        t = k + 1  # Adam step of one long inner loop (never reset here)
-        e = ev.get(k) if timed else None
-        if world == 1:
-            # steady state of psvi_inner_loop: this step's x was sampled by the
-            # previous update (fused); draw the next step's eps, net, update of
-            # the tiled corr/m/v state + next sample
-            cur, nxt = eps_b[k & 1], eps_b[(k + 1) & 1]
-            if e: e[0].record()
-            randn_(nxt, seed=20251015, offset=(k + 1) * eps_stride)
-            if e: e[1].record()
-            plan.mvn_net(u, z, w, xs, gs, parts[k, 0:1])
-            if e: e[2].record()
-            plan.mvn_update_tiled(cur, gs, params, m, v, tstate, step=t, lr=LR,
-                                  kl_out=parts[k, 1:2], eps_next=nxt, x_next=xs)
-            if e: e[3].record()
-        else:
+        def one_step(k, timed):
+            t = k + 1  # Adam step of one long inner loop (never reset here)
+            e = ev.get(k) if timed else None
             randn_(eps, seed=20251015, offset=k * eps_stride)
             if e: e[0].record()
             loop.phase_sample(eps, params)
@@ -210,40 +224,28 @@ def main():
             if e: e[3].record()
             parts[k].copy_(loop.parts)
 
-    if world == 1:  # x_0 of the loop; corr / m / v into the tiled state for the loop
-        randn_(eps_b[0], seed=20251015, offset=0)
-        plan.mvn_sample(eps_b[0], params, xs)
-        tstate = plan.tiled_state(dev)
-        plan.tiled_convert(params, m, v, tstate, True)
-    for k in range(args.warmup):
-        one_step(k, False)
-    torch.cuda.synchronize()
-    if world > 1:
+        for k in range(args.warmup):
+            one_step(k, False)
+        torch.cuda.synchronize()
         dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.warmup, total_steps):
-        one_step(k, True)
-    if world == 1:  # end of the loop: packed parameters back (counted in the timed region)
-        plan.tiled_convert(params, m, v, tstate, False)
-    torch.cuda.synchronize()
-    if world > 1:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.warmup, total_steps):
+            one_step(k, True)
+        torch.cuda.synchronize()
         dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-
-    # per-phase device time (HIP events on the launch stream)
-    first = "randn(next eps)" if world == 1 else "sample"
-    ph = {first: [], "exchange+net": [], "update": []}
-    for e in ev.values():
-        ph[first].append(e[0].elapsed_time(e[1]))
-        ph["exchange+net"].append(e[1].elapsed_time(e[2]))
-        ph["update"].append(e[2].elapsed_time(e[3]))
-    avg_ms = {k: sum(x) / len(x) for k, x in ph.items()}
+        # per-phase device time (HIP events on the launch stream)
+        ph = {"sample": [], "exchange+net": [], "update": []}
+        for e in ev.values():
+            ph["sample"].append(e[0].elapsed_time(e[1]))
+            ph["exchange+net"].append(e[1].elapsed_time(e[2]))
+            ph["update"].append(e[2].elapsed_time(e[3]))
+        avg_ms = {k: sum(x) / len(x) for k, x in ph.items()}
     elbo = parts.sum(-1)
     if world > 1:
         dist.all_reduce(elbo)
@@ -260,8 +262,7 @@ def main():
         kname = "mvn_update_kernel<fused next-step sample, tiled state> + mvn_fwd_reduce_kernel"
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
-                   "net_kernel": dict(avg_us=avg_ms["exchange+net"] * 1e3),
-                   "randn_kernel": dict(avg_us=avg_ms[first] * 1e3)}
+                   "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
     else:
         work = algorithmic_work(S, rows_frac)
         wk = work["update"]

@@ -269,6 +269,27 @@ int build_plan(psvi_plan& p) {
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Diagnostics (PSVI_DBG_LOOP_TIMING): HIP events around the network and the
+// update launches of every `g_loop_every`-th full-cov inner-loop step.
+int g_loop_every = 0;
+std::vector<hipEvent_t> g_loop_ev[2];  // [net, update] x (start, end) pairs
+
+void loop_events_clear() {
+    for (auto& v : g_loop_ev) {
+        for (hipEvent_t e : v) (void)hipEventDestroy(e);
+        v.clear();
+    }
+}
+
+// records the next start or end event of phase k on the stream
+hipError_t loop_event(int k, hipStream_t st) {
+    hipEvent_t e;
+    const hipError_t rc = hipEventCreate(&e);
+    if (rc != hipSuccess) return rc;
+    g_loop_ev[k].push_back(e);
+    return hipEventRecord(e, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -278,12 +299,32 @@ const char* psvi_version(void) { return "psvi_hip 0.1.0 (gfx950)"; }
 
 int psvi_debug_set(int32_t key, int32_t value) {
     switch (key) {
+        case PSVI_DBG_LOOP_TIMING: loop_events_clear(); g_loop_every = value; return 0;
         case PSVI_DBG_NET_ABLATION: g_net_ablation = value; return 0;
         case PSVI_DBG_UPD_ABLATION: g_upd_ablation = value; return 0;
         case PSVI_DBG_NET_SPLIT_BELOW: g_net_split_below = value; return 0;
         case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }
+}
+
+int psvi_debug_loop_timing(double* out) {
+    if (!out) return fail(PSVI_EINVAL, "null out");
+    for (int k = 0; k < 2; ++k) {
+        double sum = 0.0;
+        const auto& v = g_loop_ev[k];
+        for (size_t i = 0; i + 1 < v.size(); i += 2) {
+            float ms = 0.f;
+            HIP_TRY(hipEventSynchronize(v[i + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, v[i], v[i + 1]));
+            sum += ms;
+        }
+        const size_t n = v.size() / 2;
+        out[k] = n ? 1e3 * sum / (double)n : 0.0;
+        if (k == 0) out[2] = (double)n;
+    }
+    loop_events_clear();
+    return 0;
 }
 
 int psvi_debug_set_ptr(int32_t key, void* ptr) {
@@ -612,18 +653,25 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     if (T == 0) return 0;
     const float* e = eps_t(0);
     if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
+    HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double) * (size_t)T, st));
     HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
     if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st));
     for (int t = 0; t < T; ++t) {
         h.step = hp->step + t;
-        HIP_TRY(hipMemsetAsync(elbo_out + t, 0, sizeof(double), st));
         if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
+        // Philox mode: the network kernel also draws the next step's eps
+        const bool draw = !eps && t + 1 < T;
+        float* en_buf = draw ? ebuf[(t + 1) & 1] : nullptr;
+        const bool tm = g_loop_every > 0 && t % g_loop_every == 0;
+        if (tm) HIP_TRY(loop_event(0, st));
         HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x, g, elbo_out + t,
-                           st));
-        const float* en = t + 1 < T ? eps_t(t + 1) : nullptr;
-        if (t + 1 < T && !en) return fail(PSVI_EUNSUP, "randn launch failed");
+                           st, en_buf, draw ? p->Peps : 0, seed, offset + (uint64_t)(t + 1) * es));
+        if (tm) HIP_TRY(loop_event(0, st));
+        const float* en = t + 1 < T ? (eps ? eps + (size_t)(t + 1) * p->Peps : en_buf) : nullptr;
+        if (tm) HIP_TRY(loop_event(1, st));
         HIP_TRY(launch_mvn_update(*p, e, g, params, adam_m, adam_v, &h, elbo_out + t, nullptr, 1,
                                   en, en ? x : nullptr, st, ts));
+        if (tm) HIP_TRY(loop_event(1, st));
         e = en;
     }
     if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, false, st));

@@ -146,53 +146,13 @@ hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
 }
 
 // ----------------------------------------------------- Philox4x32-10 randn
-__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
-    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-    const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
-    const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
-    c[0] = hi1 ^ c[1] ^ k0;
-    c[1] = lo1;
-    c[2] = hi0 ^ c[3] ^ k1;
-    c[3] = lo0;
-}
-
-__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        philox_round(c, k0, k1);
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
 template <bool VEC>
 __global__ __launch_bounds__(256) void randn_kernel(float* __restrict__ out, int64_t n,
                                                     uint64_t seed, uint64_t offset) {
     const int64_t nq = (n + 3) / 4;
     for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq;
-         q += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t ctr = offset / 4 + (uint64_t)q;
-        uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u};
-        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        float r[4];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            // Box-Muller on the native transcendentals: u1 in (0, 1], u2 in [0, 1);
-            // v_log_f32 is log2, v_sin/v_cos_f32 take revolutions (sin(2 pi u2))
-            const float u1 = ((float)(c[2 * j] >> 8) + 1.0f) * (1.0f / 16777216.0f);
-            const float u2 = (float)(c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
-            const float rad =
-                __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-            r[2 * j] = rad * __builtin_amdgcn_cosf(u2);
-            r[2 * j + 1] = rad * __builtin_amdgcn_sinf(u2);
-        }
-        const int64_t base = q * 4;
-        if (VEC && base + 3 < n) {
-            *reinterpret_cast<float4*>(out + base) = make_float4(r[0], r[1], r[2], r[3]);
-        } else {
-            for (int j = 0; j < 4 && base + j < n; ++j) out[base + j] = r[j];
-        }
-    }
+         q += (int64_t)gridDim.x * blockDim.x)
+        randn_quad<VEC>(out, n, seed, offset, q);
 }
 
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st) {

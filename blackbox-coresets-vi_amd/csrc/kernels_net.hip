@@ -56,7 +56,7 @@ struct NetArgs {
     int lw[kMaxL], ldw[kMaxL], lb[kMaxL], lx[kMaxL], ldx[kMaxL];
     int lg[2], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // ldl: dlogits [Mp][lddl]; lzw: z, w
     int nslack, nslack_early, slack[4 * kMaxL + 8];  // float offsets of the 64-float zero slacks
-    int lstage, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, staged by source
+    int lstage, stage_len, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, staged by source
     const float* u;
     const int32_t* z;
     const float* w;
@@ -67,6 +67,11 @@ struct NetArgs {
     int64_t poff[kMaxL], eoff[kMaxL];
     float* accMu;
     float* accRho;
+    // fused next-step draw (psvi_inner_loop): normals [0, rn_n) of the Philox
+    // stream (rn_seed, rn_off) into rn_out, split over the grid's workgroups
+    float* rn_out;
+    int64_t rn_n;
+    uint64_t rn_seed, rn_off;
     // FULLCOV (blocked by source rank)
     const float* xrecv;
     float* gsend;
@@ -253,11 +258,22 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     // ---- 1. loads --------------------------------------------------------
     int* srct = reinterpret_cast<int*>(sm + a.lsrc);
     if (FAM == PSVI_FAMILY_FULLCOV && a.nsrc > 1) {
+        // uniform loops: a per-lane index into the by-value kernel arguments
+        // would make the compiler copy the whole argument block to scratch
         int64_t* off = reinterpret_cast<int64_t*>(srct + 2 * kMaxWorld * kMaxL);
-        for (int i = tid; i < a.nsrc * L; i += blockDim.x) {
-            const int p = i / L, l = i - p * L;
-            srct[i] = a.src_hi[p][l];
-            off[i] = a.src_base[p] + (int64_t)s * a.src_stride[p] + a.src_col[p][l] - a.src_lo[p][l];
+        int64_t* xb = reinterpret_cast<int64_t*>(srct + 4 * kMaxWorld * kMaxL);
+        int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
+        for (int p = 0; p < a.nsrc; ++p) {
+            for (int l = 0; l < L; ++l)
+                if (tid == 0) {
+                    srct[p * L + l] = a.src_hi[p][l];
+                    off[p * L + l] = a.src_base[p] + (int64_t)s * a.src_stride[p] +
+                                     a.src_col[p][l] - a.src_lo[p][l];
+                }
+            if (tid == 0) {  // the stage: source p's run at stage_off[p]
+                xs0[p] = a.stage_off[p];
+                xb[p] = a.src_base[p] + (int64_t)s * a.src_stride[p] - a.stage_off[p];
+            }
         }
         __syncthreads();
     }
@@ -280,7 +296,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         const int nu = u4 ? mcnt * (D >> 2) : mcnt * D;  // float4s or floats of u
         const float rdu = 1.f / (float)(u4 ? D >> 2 : D);
         const float* usrc = a.u + (int64_t)m0 * D;
-        const int nx = FAM == PSVI_FAMILY_FULLCOV ? a.stage_off[a.nsrc] : 0;
+        const int nx = FAM == PSVI_FAMILY_FULLCOV ? a.stage_len : 0;
         const int bd = blockDim.x;
         for (int pass = 0; pass * kU * bd < nu || pass * kX * bd < nx || pass == 0; ++pass) {  // uniform
             const int bu = pass * kU * bd + tid, bx = pass * kX * bd + tid;
@@ -296,14 +312,21 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                                : make_float4(usrc[idx], 0.f, 0.f, 0.f);
                 }
                 if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
+                    // stage position r -> x_recv: one source, one run; several, the
+                    // run table in LDS (a per-lane pick among the kernel arguments
+                    // makes the compiler copy the whole argument block to scratch)
+                    const int64_t* xb = reinterpret_cast<const int64_t*>(srct + 4 * kMaxWorld * kMaxL);
+                    const int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
 #pragma unroll
                     for (int k = 0; k < kX; ++k) {
                         const int r = max(min(bx + k * bd, nx - 1), 0);
-                        int p = 0;
-#pragma unroll
-                        for (int q = 1; q < kMaxWorld; ++q)
-                            if (q < a.nsrc && r >= a.stage_off[q]) p = q;
-                        xv[k] = a.xrecv[a.src_base[p] + (int64_t)s * a.src_stride[p] + (r - a.stage_off[p])];
+                        int64_t base = (int64_t)s * a.src_stride[0];
+                        if (a.nsrc > 1) {
+                            int q = 0;
+                            while (q + 1 < a.nsrc && r >= xs0[q + 1]) ++q;
+                            base = xb[q];
+                        }
+                        xv[k] = a.xrecv[base + r];
                     }
                 }
                 if (pass == 0) {
@@ -311,6 +334,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     zi = a.z[m0 + mm];
                     wv = a.w[m0 + mm];
                 }
+            }
+            if (pass == 0 && a.rn_out) {
+                // the next step's normals while the loads are in flight (psvi_randn's stream)
+                const int64_t nq = (a.rn_n + 3) / 4;
+                const int nblk = gridDim.x * gridDim.y * gridDim.z;
+                const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+                const int64_t per = (nq + nblk - 1) / nblk, q1 = min(nq, (b + 1) * per);
+                for (int64_t q = b * per + tid; q < q1; q += bd)
+                    randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
             }
             if (pass == 0) {
                 // zero padding while the loads are in flight (disjoint from every
@@ -541,11 +573,11 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         const bool prop = l >= 1 && own_lo < l;
         if (!own && !prop) break;
         const int din = a.din[l], dout = a.dout[l];
-        const float* G = l == L - 1 ? sm + a.ldl : sm + a.lg[cur ^ 1];
+        const float* G = l == L - 1 ? sm + a.ldl : sm + (cur ? a.lg[0] : a.lg[1]);
         const int ldg = l == L - 1 ? a.lddl : a.ldx[l + 1];  // G_l: the stride of X_{l+1}
         const float* X = sm + a.lx[l];
         const int ldx = a.ldx[l];
-        float* Gn = sm + a.lg[cur];  // G_{l-1}: row stride ldx (of X_l)
+        float* Gn = sm + (cur ? a.lg[1] : a.lg[0]);  // G_{l-1}: row stride ldx (of X_l)
         int first = 0;
         if (own) {
             // dW_l[j][i] = sum_m G_l[m][j] X_l[m][i]: both operands k(=m)-strided
@@ -629,8 +661,9 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     const int lred = take(16);
     const int lzw = take(2 * (size_t)Mp);
     const int lstamp = take(32);  // 16 x uint64 diagnostics stamps
-    // per-workgroup source table: [nsrc][L] ints, then [nsrc][L] int64 (8-byte aligned)
-    const int lsrc = take(2 * kMaxWorld * kMaxL + 2 * kMaxWorld * kMaxL);
+    // per-workgroup source tables (world > 1): [nsrc][L] ints, [nsrc][L] int64
+    // (8-byte aligned), the stage's per-source int64 bases and int starts
+    const int lsrc = take(4 * kMaxWorld * kMaxL + 3 * kMaxWorld);
     const int ns_early = ns;
     const size_t lstage = off;
     int ldgmax = 4;
@@ -653,7 +686,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
             if (a) a->stage_off[q] = (int)st;
             st += (size_t)p.rows_tot[q];
         }
-        if (a) a->stage_off[p.world] = (int)st;
+        if (a) { a->stage_off[p.world] = (int)st; a->stage_len = (int)st; }
         off = std::max(off, lstage + st);
     }
     off = (off + 3) & ~size_t(3);
@@ -712,8 +745,13 @@ void net_set_lds_limit() {
 
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* accMu, float* accRho,
-                      const float* xrecv, float* gsend, double* nll_out, hipStream_t st) {
+                      const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
+                      float* rn_out, int64_t rn_n, uint64_t rn_seed, uint64_t rn_off) {
     NetArgs a{};
+    a.rn_out = rn_out;  // 16-byte aligned (workspace buffers)
+    a.rn_n = rn_n;
+    a.rn_seed = rn_seed;
+    a.rn_off = rn_off;
     a.L = p.L;
     a.M = p.d.M;
     a.mc = p.mc;

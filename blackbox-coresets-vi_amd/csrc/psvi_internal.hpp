@@ -66,6 +66,55 @@ __device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+// ------------------------------------------------- Philox4x32-10 normals
+// psvi_randn's stream: normal i of (seed, offset) is element i % 4 of
+// Philox4x32-10(counter = offset / 4 + i / 4, key = seed) through Box-Muller.
+// Shared by randn_kernel and the network kernel's fused next-step draw.
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+    const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+    c[0] = hi1 ^ c[1] ^ k0;
+    c[1] = lo1;
+    c[2] = hi0 ^ c[3] ^ k1;
+    c[3] = lo0;
+}
+
+__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        philox_round(c, k0, k1);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+// normals 4q .. 4q+3 of the stream into out[0, n)
+template <bool VEC>
+__device__ __forceinline__ void randn_quad(float* __restrict__ out, int64_t n, uint64_t seed,
+                                           uint64_t offset, int64_t q) {
+    const uint64_t ctr = offset / 4 + (uint64_t)q;
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    float r[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        // Box-Muller on the native transcendentals: u1 in (0, 1], u2 in [0, 1);
+        // v_log_f32 is log2, v_sin/v_cos_f32 take revolutions (sin(2 pi u2))
+        const float u1 = ((float)(c[2 * j] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+        const float u2 = (float)(c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
+        const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+        r[2 * j] = rad * __builtin_amdgcn_cosf(u2);
+        r[2 * j + 1] = rad * __builtin_amdgcn_sinf(u2);
+    }
+    const int64_t base = q * 4;
+    if (VEC && base + 3 < n) {
+        *reinterpret_cast<float4*>(out + base) = make_float4(r[0], r[1], r[2], r[3]);
+    } else {
+        for (int j = 0; j < 4 && base + j < n; ++j) out[base + j] = r[j];
+    }
+}
+
 // Adam, both reference variants; returns new p, updates m, v in place.
 struct AdamC {
     float lr, b1, b2, eps, omb1, omb2;
@@ -195,7 +244,9 @@ namespace psvi {
 // launchers (defined in the .hip translation units)
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* accMu, float* accRho,
-                      const float* xrecv, float* gsend, double* nll_out, hipStream_t st);
+                      const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
+                      float* rn_out = nullptr, int64_t rn_n = 0, uint64_t rn_seed = 0,
+                      uint64_t rn_off = 0);
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
                             float* m, float* v, const psvi_adam_hp* hp, double* kl_out,
                             float* grad_out, int include_kl, hipStream_t st);

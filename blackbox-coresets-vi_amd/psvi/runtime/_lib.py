@@ -85,6 +85,7 @@ SIGNATURES = {
     "psvi_adam_update": (_I32, [_I64, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P]),
     "psvi_debug_set": (_I32, [_I32, _I32]),
     "psvi_debug_set_ptr": (_I32, [_I32, _P]),
+    "psvi_debug_loop_timing": (_I32, [_P]),
     "psvi_last_error": (ctypes.c_char_p, []),
     "psvi_version": (ctypes.c_char_p, []),
 }

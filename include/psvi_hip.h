@@ -264,6 +264,14 @@ int psvi_debug_set(int32_t key, int32_t value);
                                     sample-kernel workgroup (start, first stage,
                                     MFMAs done, end, HW_ID, XCC_ID)            */
 int psvi_debug_set_ptr(int32_t key, void* ptr);
+#define PSVI_DBG_LOOP_TIMING 8   /* value: record HIP events around the network and
+                                    the update launches of every value-th step of
+                                    full-cov psvi_inner_loop calls (0 = off;
+                                    setting it drops earlier records)          */
+/* mean device microseconds of the recorded windows: out[0] network kernel,
+   out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
+   drops the records */
+int psvi_debug_loop_timing(double* out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,48 @@
+"""Every kernel compiles for gfx950 without scratch memory or VGPR spills.
+
+A per-lane index into a by-value kernel-argument struct makes the compiler
+copy the whole struct to scratch and turns every argument read into a
+dependent memory load (this happened once to the network kernel, silently:
+results stay right, the kernel gets slower).  hipcc's kernel-resource-usage
+remarks expose it at build time, so the CPU suite guards it.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "blackbox-coresets-vi_amd", "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def _resources(src, tmp_path):
+    out = tmp_path / (os.path.basename(src) + ".o")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-munsafe-fp-atomics", "-O3", "-std=c++17", "-fPIC",
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-c", src, "-o", str(out),
+           "-Rpass-analysis=kernel-resource-usage"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    kernels, cur = {}, None
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            kernels[cur] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+)", line)
+        if m and cur:
+            kernels[cur][m.group(1).strip()] = int(m.group(2))
+    return kernels
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["kernels_net.hip", "kernels_mvn.hip", "kernels_mf.hip"])
+def test_no_scratch_no_spills(src, tmp_path):
+    kernels = _resources(os.path.join(CSRC, src), tmp_path)
+    assert kernels, "no kernel resource remarks parsed"
+    bad = {k: v for k, v in kernels.items()
+           if v.get("ScratchSize", 0) or v.get("VGPRs Spill", 0)}
+    assert not bad, f"kernels using scratch or spilling VGPRs: {bad}"
