@@ -9,7 +9,7 @@ ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 R=${ROUND:-r01}
 STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
 if [[ $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 300 > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
 fi
 if [[ $STEPS == *smoke* ]]; then
