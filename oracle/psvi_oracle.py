@@ -325,3 +325,132 @@ def run_inner_loop(family, layers, params0, u, z, w, eps_steps, S, lr, adam_kind
         p, m, v = adam(adam_kind, p, g, m, v, t0 + k, lr)
         traj.append(p.copy())
     return np.array(elbos), grads, traj, m, v
+
+
+# ------------------------------------------------- outer objective (psvi_elbo)
+def _net_rows_forward(X, Ws, bs):
+    """Per-sample MLP forward over rows X (R, D): returns (nll-ready logits,
+    the layer inputs hs[l] (S, R, in_l) and pre-activations acts[l])."""
+    S = Ws[0].shape[0]
+    L = len(Ws)
+    hs = [np.broadcast_to(X[None], (S,) + X.shape)]
+    acts = []
+    for l in range(L):
+        a = np.einsum("smi,soi->smo", hs[-1], Ws[l]) + bs[l][:, None, :]
+        acts.append(a)
+        hs.append(np.maximum(a, 0.0) if l < L - 1 else a)
+    return hs, acts
+
+
+def _net_rows_backward(coef, probs_minus_onehot, hs, acts, Ws):
+    """Backward of sum_{s,r} coef[s,r] NLL_sr: per-sample dW, db and the input
+    gradient dX (S, R, D)."""
+    L = len(Ws)
+    g = probs_minus_onehot * coef[..., None]
+    dWs, dbs = [None] * L, [None] * L
+    for l in range(L - 1, -1, -1):
+        dWs[l] = np.einsum("smo,smi->soi", g, hs[l])
+        dbs[l] = g.sum(1)
+        g = np.einsum("smo,soi->smi", g, Ws[l])
+        if l > 0:
+            g = g * (acts[l - 1] > 0)
+    return dWs, dbs, g
+
+
+def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
+    """Negative PSVI-ELBO (PSVI.psvi_elbo, psvi/inference/psvi_classes.py:445-486)
+    and its first-order gradient.
+
+    X (R, D) = cat(u, xbatch) with the first n_pseudo rows the pseudopoints;
+    z (R,) class ids; w (R,) row weights: N f(v)_m for the pseudopoints
+    (``.matmul(self.N * self.f(self.v, 0))``, 478-480) and N / Nx for the data
+    rows (``self.N / Nx * all_nlls[:, Nu:].sum(-1)``, 481); eps the reference
+    draw order of ``model(all_data)``.
+      pseudo_s = sum_{m<Mu} w_m NLL_sm,  data_s = sum_{m>=Mu} w_m NLL_sm
+      nkl_s    = log p(w_s) - log q(w_s)       (sampled_nkl, neural_net.py:110-115
+                                                mean-field, 438-442 full-cov)
+               = sum_i [-x_si^2/(2 s0^2) - log s0 + eps_si^2/2 + log sigma_i]
+      (x_s = mean + L eps_s, so L^-1 (x_s - mean) = eps_s; sigma_i = softplus(sd_i),
+       the diagonal of L, or the mean-field scales)
+      lw_s = -pseudo_s + nkl_s,  W = softmax_s(lw)
+      loss = sum_s W_s (data_s - pseudo_s) - mean_s lw_s
+    Returns (loss, d loss/d params, d loss/d X[:n_pseudo], d loss/d w[:n_pseudo]).
+    The pathwise gradient of nkl_s is -x_s/s0^2 on the sampled weights; the
+    explicit one is +1/sigma_i on every scale (the eps^2/2 term is constant)."""
+    params = np.asarray(params, np.float64)
+    eps = np.asarray(eps, np.float64)
+    X = np.asarray(X, np.float64)
+    w = np.asarray(w, np.float64)
+    s0 = float(prior_sd)
+    Ws, bs, lay = [], [], []
+    po = eo = 0
+    sumlog = 0.0
+    xsq = np.zeros(S)
+    esq = np.zeros(S)
+    for din, dout in layers:
+        n = din * dout + dout
+        if family == "mf":
+            mu = params[po:po + n]
+            rho = params[po + n:po + 2 * n]
+            E = np.concatenate([eps[eo:eo + S * din * dout].reshape(S, din * dout),
+                                eps[eo + S * din * dout:eo + S * n].reshape(S, dout)], axis=1)
+            sd = softplus(rho)
+            Xs = mu[None] + sd[None] * E
+            lay.append((po, n, E, rho, sd, None))
+            po += 2 * n
+        else:
+            nc = mvn_ncorr(n)
+            mean = params[po:po + n]
+            sdr = params[po + n:po + 2 * n]
+            corr = params[po + 2 * n:po + 2 * n + nc]
+            E = eps[eo:eo + S * n].reshape(S, n)
+            Lm = mvn_dense_L(sdr, corr, n)
+            Xs = mean[None] + E @ Lm.T
+            sd = softplus(sdr)
+            lay.append((po, n, E, sdr, sd, nc))
+            po += 2 * n + nc
+        eo += S * n
+        sumlog += float(np.log(sd).sum())
+        xsq += (Xs ** 2).sum(1)
+        esq += (E ** 2).sum(1)
+        Ws.append(Xs[:, :din * dout].reshape(S, dout, din))
+        bs.append(Xs[:, din * dout:])
+    n_tot = sum(i * o + o for i, o in layers)
+    hs, acts = _net_rows_forward(X, Ws, bs)
+    logits = hs[-1]
+    R = X.shape[0]
+    mx = logits.max(-1, keepdims=True)
+    lse = (mx + np.log(np.exp(logits - mx).sum(-1, keepdims=True)))[..., 0]
+    zi = np.asarray(z).astype(np.int64)
+    nll = lse - logits[:, np.arange(R), zi]  # (S, R)
+    Mu = int(n_pseudo)
+    pseudo = nll[:, :Mu] @ w[:Mu]
+    data = nll[:, Mu:] @ w[Mu:]
+    nkl = -xsq / (2 * s0 ** 2) - n_tot * np.log(s0) + 0.5 * esq + sumlog
+    lw = -pseudo + nkl
+    W = np.exp(lw - lw.max())
+    W /= W.sum()
+    a = data - pseudo
+    abar = float((W * a).sum())
+    loss = abar - float(lw.mean())
+    ck = W * (a - abar) - 1.0 / S          # d loss / d lw_s = d loss / d nkl_s
+    cd = W                                 # d loss / d data_s
+    cp = -W - ck                           # d loss / d pseudo_s
+    coef = np.concatenate([cp[:, None] * w[None, :Mu], cd[:, None] * w[None, Mu:]], axis=1)
+    pmo = np.exp(logits - lse[..., None])
+    pmo[:, np.arange(R), zi] -= 1.0
+    dWs, dbs, dX = _net_rows_backward(coef, pmo, hs, acts, Ws)
+    grad = np.zeros_like(params)
+    sck = float(ck.sum())
+    for l, (po, n, E, sdr, sd, nc) in enumerate(lay):
+        din, dout = layers[l]
+        Xs = np.concatenate([Ws[l].reshape(S, -1), bs[l]], axis=1)
+        G = np.concatenate([dWs[l].reshape(S, -1), dbs[l]], axis=1) - ck[:, None] * Xs / s0 ** 2
+        grad[po:po + n] = G.sum(0)
+        grad[po + n:po + 2 * n] = ((G * E).sum(0) + sck / sd) * sigmoid(sdr)
+        if family != "mf":
+            r, c = tril_rows_cols(n)
+            grad[po + 2 * n:po + 2 * n + nc] = (G.T @ E)[r, c]
+    gX = dX.sum(0)[:Mu]
+    gw = (cp[:, None] * nll[:, :Mu]).sum(0)
+    return loss, grad, gX, gw

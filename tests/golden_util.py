@@ -8,8 +8,11 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def fixture_names():
-    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz")))
+def fixture_names(prefix="g"):
+    """Inner-loop fixtures (tools/gen_golden.py) start with "g", outer-objective
+    fixtures (tools/gen_golden_outer.py) with "o"."""
+    return sorted(os.path.basename(f)[:-4]
+                  for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
 
 
 def load_fixture(name):
