@@ -398,6 +398,34 @@ int psvi_plan_destroy(psvi_plan* p) {
 static size_t loop_ws_bytes(const psvi_plan* p);
 static size_t tiled_floats(const psvi_plan* p);
 
+// psvi_outer_elbo_grad workspace: the step workspace (x / g or acc), then the
+// per-row NLL [S][M], row coefficients [S][2], ck [S], sum ck, per-sample
+// stats [S][2] doubles, and the per-sample input gradients [S][M][D]
+struct OuterWs {
+    float *nll, *rowcoef, *ck, *sck, *du;
+    double* stats;
+    size_t bytes;
+};
+static OuterWs outer_ws(const psvi_plan* p, void* ws) {
+    const size_t S = p->d.S, M = p->d.M, D = p->lay[0].din;
+    char* b = (char*)ws;
+    OuterWs o{};
+    size_t off = align256(p->ws_bytes);
+    auto take = [&](size_t bytes) {
+        char* r = b ? b + off : nullptr;
+        off += align256(bytes);
+        return r;
+    };
+    o.nll = (float*)take(sizeof(float) * S * M);
+    o.rowcoef = (float*)take(sizeof(float) * 2 * S);
+    o.ck = (float*)take(sizeof(float) * S);
+    o.sck = (float*)take(sizeof(float));
+    o.stats = (double*)take(sizeof(double) * 2 * S);
+    o.du = (float*)take(sizeof(float) * S * M * D);
+    o.bytes = off;
+    return o;
+}
+
 int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
     if (!p || !value) return fail(PSVI_EINVAL, "null argument");
     const int r = p->rank;
@@ -413,6 +441,7 @@ int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
         case PSVI_Q_LOOP_WS_BYTES: *value = (int64_t)loop_ws_bytes(p); break;
         case PSVI_Q_TILED_FLOATS: *value = (int64_t)tiled_floats(p); break;
         case PSVI_Q_XRECV_COUNT: *value = (int64_t)p->s_cnt[r] * p->n_tot; break;
+        case PSVI_Q_OUTER_WS_BYTES: *value = (int64_t)outer_ws(p, nullptr).bytes; break;
         default: return fail(PSVI_EINVAL, "unknown query key");
     }
     return 0;
@@ -675,6 +704,67 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         e = en;
     }
     if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, false, st));
+    return 0;
+}
+
+int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
+                         const int32_t* z_all, const float* w_all, const float* eps,
+                         const float* params, double* loss_out, float* grad_params,
+                         float* grad_u, float* grad_w, double* sample_out, void* ws,
+                         size_t ws_bytes, void* stream) {
+    if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (p->world != 1) return fail(PSVI_ESTATE, "the outer objective needs world == 1");
+    if (p->d.S < 2) return fail(PSVI_EINVAL, "psvi_elbo needs S > 1 (psvi_classes.py:449)");
+    if (p->d.S > 2048) return fail(PSVI_EUNSUP, "the outer objective supports S <= 2048");
+    if (n_pseudo < 0 || n_pseudo > p->d.M) return fail(PSVI_EINVAL, "n_pseudo out of [0, M]");
+    if (!x_all || !z_all || !w_all || !eps || !params || !loss_out)
+        return fail(PSVI_EINVAL, "null pointer");
+    if (grad_u && !grad_params)
+        return fail(PSVI_EINVAL, "grad_u needs grad_params (one backward pass gives both)");
+    const OuterWs o = outer_ws(p, ws);
+    if (!ws || ws_bytes < o.bytes) return fail(PSVI_ENOSPC, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    char* wsb = (char*)ws;
+    float* x = nullptr;
+    float* g = nullptr;
+    float* acc = nullptr;
+    if (p->family == PSVI_FAMILY_FULLCOV) {
+        const size_t xs = sizeof(float) * (size_t)p->d.S * p->rows_tot[0];
+        x = (float*)wsb;
+        g = (float*)(wsb + align256(xs));
+        HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
+    } else {
+        acc = (float*)wsb;
+    }
+    HIP_TRY(launch_outer_stats(*p, params, eps, x, o.stats, st));
+    // 1. forward: every row's NLL
+    NetOuter fw{1, n_pseudo, o.nll, nullptr, nullptr, nullptr};
+    HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
+                       nullptr, st, nullptr, 0, 0, 0, &fw));
+    // 2. per-sample terms, softmax over samples, loss, backward coefficients
+    HIP_TRY(launch_outer_combine(*p, n_pseudo, params, w_all, o.nll, o.stats, loss_out,
+                                 o.rowcoef, o.ck, o.sck, grad_w, sample_out, st));
+    if (!grad_params) return 0;
+    // 3. backward through the network with the row coefficients (+ sampled-KL path)
+    NetOuter bw{2, n_pseudo, nullptr, o.rowcoef, o.ck, grad_u ? o.du : nullptr};
+    if (p->family == PSVI_FAMILY_FULLCOV) {
+        if (p->mchunks > 1)
+            HIP_TRY(hipMemsetAsync(g, 0, sizeof(float) * (size_t)p->d.S * p->n_tot, st));
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, nullptr, nullptr, nullptr, nullptr, x, g,
+                           nullptr, st, nullptr, 0, 0, 0, &bw));
+        // 4. reparameterised backward (no KL term: the sampled KL came in through G)
+        HIP_TRY(launch_mvn_update(*p, eps, g, const_cast<float*>(params), nullptr, nullptr,
+                                  nullptr, nullptr, grad_params, 0, nullptr, nullptr, st));
+    } else {
+        HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, acc, acc + p->n_tot, nullptr,
+                           nullptr, nullptr, st, nullptr, 0, 0, 0, &bw));
+        HIP_TRY(launch_mf_update(*p, acc, const_cast<float*>(params), nullptr, nullptr, nullptr,
+                                 nullptr, grad_params, 0, st));
+    }
+    // 5. explicit log-det term on the scales; d loss / d u
+    HIP_TRY(launch_outer_finish(*p, n_pseudo, params, o.sck, grad_params, o.du, grad_u, st));
     return 0;
 }
 

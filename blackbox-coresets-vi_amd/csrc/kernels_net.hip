@@ -75,6 +75,18 @@ struct NetArgs {
     // FULLCOV (blocked by source rank)
     const float* xrecv;
     float* gsend;
+    // outer objective (psvi_outer_elbo_grad, world 1): 0 = the inner ELBO;
+    // 1 = forward only, NLL of every row -> nll_rows [S][M] (no weighting, no
+    // backward); 2 = backward of sum_{s,m} coef_sm NLL_sm with coef_sm =
+    // w_m * rowcoef[s][m >= n_pseudo], plus the sampled-KL path term
+    // -ck_s x_s / s0^2 on every weight gradient, and (du_part) the input
+    // gradient of the pseudopoint rows [S][n_pseudo][D]
+    int outer, n_pseudo;
+    float inv_s0sq;
+    float* nll_rows;
+    const float* rowcoef;
+    const float* ck;
+    float* du_part;
     int nsrc;
     int64_t src_base[kMaxWorld];
     int src_stride[kMaxWorld];
@@ -503,10 +515,13 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     {
         const int C = a.dout[L - 1], ldl = a.lddl;
         float part = 0.f;
+        // outer backward: d loss / d pseudo_s and d loss / d data_s scale the rows
+        const float cp = a.outer == 2 ? a.rowcoef[2 * s] : 1.f;
+        const float cd = a.outer == 2 ? a.rowcoef[2 * s + 1] : 1.f;
         for (int m = tid; m < mcnt && !(a.abl & 4); m += blockDim.x) {
             float* row = sm + a.ldl + m * ldl;
             const int zm = __float_as_int(zw[m]);
-            const float wm = zw[Mp + m];
+            const float wm = zw[Mp + m] * (m0 + m < a.n_pseudo ? cp : cd);
             if (C <= kMaxC) {
                 float lg[kMaxC];
                 float mx = -INFINITY, lz = 0.f;
@@ -522,6 +537,10 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 for (int c = 0; c < kMaxC; ++c)
                     if (c < C) se += expf(lg[c] - mx);
                 const float lse = mx + logf(se);
+                if (a.outer == 1) {
+                    a.nll_rows[(size_t)s * a.M + m0 + m] = lse - lz;
+                    continue;
+                }
                 part += wm * (lse - lz);
 #pragma unroll
                 for (int c = 0; c < kMaxC; ++c)
@@ -535,12 +554,16 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 float se = 0.f;
                 for (int c = 0; c < C; ++c) se += expf(row[c] - mx);
                 const float lse = mx + logf(se);
+                if (a.outer == 1) {
+                    a.nll_rows[(size_t)s * a.M + m0 + m] = lse - lz;
+                    continue;
+                }
                 part += wm * (lse - lz);
                 for (int c = 0; c < C; ++c)
                     row[c] = wm * (expf(row[c] - lse) - (c == zm ? 1.f : 0.f));
             }
         }
-        if (role == 0) {
+        if (role == 0 && a.outer == 0) {
             const float tot = block_sum(part, sm + a.lred);  // its barriers end the phase
             if (tid == 0) atomicAdd(a.nll_out, (double)tot);
         }
@@ -567,11 +590,16 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             if (a.atomic_g) atomicAdd(dst, v); else *dst = v;
         }
     };
+    // outer backward: the sampled-KL path, d nkl_s / d x_s = -x_s / s0^2,
+    // added once per sample (pseudopoint chunk 0)
+    const float ckv = (a.outer == 2 && blockIdx.z == 0) ? a.ck[s] * a.inv_s0sq : 0.f;
     int stamp = 4, cur = 0;  // cur: gradient buffer that receives G_{l-1}
-    for (int l = L - 1; l >= 0 && !(a.abl & 8); --l) {
+    for (int l = L - 1; l >= 0 && !(a.abl & 8) && a.outer != 1; --l) {
         const bool own = l >= own_lo && l < own_hi;
         const bool prop = l >= 1 && own_lo < l;
-        if (!own && !prop) break;
+        // outer backward: input gradient of the pseudopoint rows (d loss / d u)
+        const bool dx0 = l == 0 && a.outer == 2 && a.du_part != nullptr && own_lo == 0;
+        if (!own && !prop && !dx0) break;
         const int din = a.din[l], dout = a.dout[l];
         const float* G = l == L - 1 ? sm + a.ldl : sm + (cur ? a.lg[0] : a.lg[1]);
         const int ldg = l == L - 1 ? a.lddl : a.ldx[l + 1];  // G_l: the stride of X_{l+1}
@@ -581,15 +609,35 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         int first = 0;
         if (own) {
             // dW_l[j][i] = sum_m G_l[m][j] X_l[m][i]: both operands k(=m)-strided
+            const float* Wl = sm + a.lw[l];
+            const int ldw = a.ldw[l];
             auto epi = [&](int j, int i, floatx4 v) {
                 if (i < din) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        if (j + r < dout) emit(l, (j + r) * din + i, v[r]);
+                        if (j + r < dout) {
+                            float g = v[r];
+                            if (a.outer == 2) g -= ckv * Wl[(j + r) * ldw + i];
+                            emit(l, (j + r) * din + i, g);
+                        }
                 }
             };
             mfma_gemm<false, false>(dout, din, Mp, 0, G, ldg, X, ldx, epi);
             first = gemm_units(dout, din);
+        }
+        if (dx0) {
+            // du[s][m][i] = sum_j G_0[m][j] W_0[j][i] for the chunk's pseudopoint rows
+            auto epi = [&](int m, int i, floatx4 v) {
+                if (i < din) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int mg = m0 + m + r;
+                        if (m + r < mcnt && mg < a.n_pseudo)
+                            a.du_part[((size_t)s * a.n_pseudo + mg) * din + i] = v[r];
+                    }
+                }
+            };
+            mfma_gemm<true, false>(Mp, din, dout, first, G, ldg, sm + a.lw[l], a.ldw[l], epi);
         }
         if (prop) {
             // G_{l-1}[m][i] = (sum_j G_l[m][j] W_l[j][i]) * 1[X_l[m][i] > 0]
@@ -613,6 +661,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 float acc = 0.f;
                 for (int m = c16; m < mcnt; m += 16) acc += G[m * ldg + j];
                 acc = row16_sum(acc);
+                if (a.outer == 2) acc -= ckv * sm[a.lb[l] + j];
                 if (c16 == 0 && base + r16 < dout) emit(l, dout * din + j, acc);
             }
         }
@@ -746,8 +795,18 @@ void net_set_lds_limit() {
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* accMu, float* accRho,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
-                      float* rn_out, int64_t rn_n, uint64_t rn_seed, uint64_t rn_off) {
+                      float* rn_out, int64_t rn_n, uint64_t rn_seed, uint64_t rn_off,
+                      const NetOuter* outer) {
     NetArgs a{};
+    if (outer) {
+        a.outer = outer->mode;
+        a.n_pseudo = outer->n_pseudo;
+        a.nll_rows = outer->nll_rows;
+        a.rowcoef = outer->rowcoef;
+        a.ck = outer->ck;
+        a.du_part = outer->du_part;
+    }
+    a.inv_s0sq = 1.f / (p.d.prior_sd * p.d.prior_sd);
     a.rn_out = rn_out;  // 16-byte aligned (workspace buffers)
     a.rn_n = rn_n;
     a.rn_seed = rn_seed;
@@ -787,7 +846,8 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
             base += (int64_t)S_local * p.rows_tot[q];
         }
     }
-    dim3 grid(p.s_cnt[p.rank], p.net_roles, p.mchunks), block(p.net_threads);
+    // the outer forward pass has no backward: one role
+    dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, p.mchunks), block(p.net_threads);
     if (p.s_cnt[p.rank] == 0) return hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL(net_kernel<PSVI_FAMILY_MEANFIELD>, grid, block, p.net_lds, st, a);

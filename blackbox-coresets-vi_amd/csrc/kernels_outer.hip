@@ -1,0 +1,273 @@
+// kernels_outer.hip -- the outer objective PSVI.psvi_elbo around the network
+// kernel's two outer passes (psvi_outer_elbo_grad, capi.cpp).
+//
+// Reference (/root/reference):
+//   PSVI.psvi_elbo            psvi/inference/psvi_classes.py:445-486
+//   VIMixin.sampled_nkl       psvi/models/neural_net.py:110-115
+//   MultivariateNormalVIMixin.sampled_nkl   neural_net.py:438-442
+//
+//   pseudo_s = sum_{m<Mu} w_m NLL_sm        data_s = sum_{m>=Mu} w_m NLL_sm (w = N/Nx)
+//   nkl_s    = sum_i [-x_si^2 / (2 s0^2) - log s0 + eps_si^2 / 2 + log sigma_i]
+//   lw_s = -pseudo_s + nkl_s,  W = softmax_s(lw),  a_s = data_s - pseudo_s
+//   loss = sum_s W_s a_s - mean_s lw_s
+// The reference evaluates log q(x_s) with a triangular solve of L against
+// x_s - mean; x_s = mean + L eps_s makes that solve eps_s, whose square is
+// taken directly here (the fp32 solve overflows at fn2 sizes, SURVEY.md
+// Appendix B #16).  Backward coefficients, all per sample:
+//   ck_s = d loss / d nkl_s = W_s (a_s - abar) - 1/S
+//   cd_s = d loss / d data_s = W_s,   cp_s = d loss / d pseudo_s = -W_s - ck_s
+// The network kernel's backward pass takes coef_sm = w_m c{p,d}_s per row and
+// adds the pathwise sampled-KL gradient -ck_s x_s / s0^2; the explicit
+// +sum_s ck_s / sigma_i on every scale is added here after the reparameterised
+// backward (outer_finish_kernel).
+#include "psvi_internal.hpp"
+
+namespace psvi {
+
+struct OuterArgs {
+    int L, S, M, n_pseudo, n_tot, family;
+    int n[kMaxL], woff[kMaxL];
+    int64_t poff[kMaxL], eoff[kMaxL];
+    int din[kMaxL], dout[kMaxL];
+    float s0;
+    const float* params;
+    const float* eps;
+    const float* x;        // full-cov: x_shard [S][n_tot] (world 1)
+    const float* w;        // [M] row weights
+    const float* nll;      // [S][M]
+    double* stats;         // [S][2]: sum x^2, sum eps^2
+    double* loss;          // [1]
+    float* rowcoef;        // [S][2]
+    float* ck;             // [S]
+    float* sck;            // [1] sum_s ck_s
+    float* grad_w;         // [n_pseudo] nullable
+    double* sample_out;    // [S][4] nullable: pseudo, data, nkl, weight
+    float* grad;           // [P] nullable
+    const float* du_part;  // [S][n_pseudo][D] nullable
+    float* grad_u;         // [n_pseudo][D] nullable
+};
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// block-wide double sum, result in every thread; `red` >= 16 doubles of LDS
+__device__ __forceinline__ double block_sum_all(double v, double* red) {
+    v = wave_sum_d(v);
+    const int lane = threadIdx.x & 63, wid = wave_id(), nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    return t;
+}
+__device__ __forceinline__ double block_max_all(double v, double* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+    const int lane = threadIdx.x & 63, wid = wave_id(), nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double t = -INFINITY;
+    for (int i = 0; i < nw; ++i) t = fmax(t, red[i]);
+    return t;
+}
+
+// one workgroup per sample: sum_i x_si^2 and sum_i eps_si^2 over every layer
+// (mean-field: x = mu + softplus(rho) eps, as the network kernel samples it)
+__global__ __launch_bounds__(256) void outer_stats_kernel(OuterArgs a) {
+    __shared__ double red[16];
+    const int s = blockIdx.x;
+    double sx = 0.0, se = 0.0;
+    for (int l = 0; l < a.L; ++l) {
+        const int n = a.n[l];
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            float e, x;
+            if (a.family == PSVI_FAMILY_MEANFIELD) {
+                const int dout = a.dout[l], nwl = a.din[l] * dout;
+                e = i < nwl ? a.eps[a.eoff[l] + (int64_t)s * nwl + i]
+                            : a.eps[a.eoff[l] + (int64_t)a.S * nwl + (int64_t)s * dout + i - nwl];
+                const float mu = a.params[a.poff[l] + i], rho = a.params[a.poff[l] + n + i];
+                x = mu + e * softplus_f(rho);
+            } else {
+                e = a.eps[a.eoff[l] + (int64_t)s * n + i];
+                x = a.x[(int64_t)s * a.n_tot + a.woff[l] + i];
+            }
+            sx += (double)x * x;
+            se += (double)e * e;
+        }
+    }
+    sx = block_sum_all(sx, red);
+    se = block_sum_all(se, red);
+    if (threadIdx.x == 0) {
+        a.stats[2 * s] = sx;
+        a.stats[2 * s + 1] = se;
+    }
+}
+
+// one workgroup: per-sample terms, the softmax over samples, the loss and the
+// backward coefficients
+constexpr int kOuterMaxS = 2048;  // samples the combine keeps in LDS
+__global__ __launch_bounds__(1024) void outer_combine_kernel(OuterArgs a) {
+    __shared__ double red[16];
+    __shared__ double lw[kOuterMaxS], av[kOuterMaxS];
+    __shared__ float cps[kOuterMaxS];
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int lane = tid & 63, wid = wave_id(), nwv = nthr >> 6;
+    // sum_i log sigma_i: the scales sit at poff + n .. poff + 2n in both families
+    double sl = 0.0;
+    for (int l = 0; l < a.L; ++l)
+        for (int i = tid; i < a.n[l]; i += nthr) sl += log((double)softplus_f(a.params[a.poff[l] + a.n[l] + i]));
+    sl = block_sum_all(sl, red);
+    const double s0 = a.s0, inv2 = 0.5 / (s0 * s0);
+    const double nlog = a.n_tot * log(s0);
+    // per sample (one wave each): pseudo_s, data_s
+    for (int s = wid; s < a.S; s += nwv) {
+        double ps = 0.0, ds = 0.0;
+        const float* row = a.nll + (size_t)s * a.M;
+        for (int m = lane; m < a.M; m += 64) {
+            const double t = (double)a.w[m] * row[m];
+            if (m < a.n_pseudo) ps += t; else ds += t;
+        }
+        ps = wave_sum_d(ps);
+        ds = wave_sum_d(ds);
+        if (lane == 0) {
+            const double nkl = -a.stats[2 * s] * inv2 - nlog + 0.5 * a.stats[2 * s + 1] + sl;
+            lw[s] = -ps + nkl;
+            av[s] = ds - ps;
+            if (a.sample_out) {
+                a.sample_out[4 * s] = ps;
+                a.sample_out[4 * s + 1] = ds;
+                a.sample_out[4 * s + 2] = nkl;
+            }
+        }
+    }
+    __syncthreads();
+    double mx = -INFINITY, sm = 0.0;
+    for (int s = tid; s < a.S; s += nthr) mx = fmax(mx, lw[s]);
+    mx = block_max_all(mx, red);
+    for (int s = tid; s < a.S; s += nthr) sm += exp(lw[s] - mx);
+    sm = block_sum_all(sm, red);
+    double abar = 0.0, lwsum = 0.0;
+    for (int s = tid; s < a.S; s += nthr) {
+        abar += exp(lw[s] - mx) / sm * av[s];
+        lwsum += lw[s];
+    }
+    abar = block_sum_all(abar, red);
+    lwsum = block_sum_all(lwsum, red);
+    if (tid == 0) a.loss[0] = abar - lwsum / a.S;
+    double cks = 0.0;
+    for (int s = tid; s < a.S; s += nthr) {
+        const double W = exp(lw[s] - mx) / sm;
+        const double ck = W * (av[s] - abar) - 1.0 / a.S;
+        const double cp = -W - ck;
+        a.rowcoef[2 * s] = (float)cp;
+        a.rowcoef[2 * s + 1] = (float)W;
+        a.ck[s] = (float)ck;
+        cps[s] = (float)cp;
+        cks += ck;
+        if (a.sample_out) a.sample_out[4 * s + 3] = W;
+    }
+    cks = block_sum_all(cks, red);
+    if (tid == 0) a.sck[0] = (float)cks;
+    __syncthreads();
+    // d loss / d w_m = sum_s cp_s NLL_sm for the pseudopoints
+    if (a.grad_w)
+        for (int m = tid; m < a.n_pseudo; m += nthr) {
+            double g = 0.0;
+            for (int s = 0; s < a.S; ++s) g += (double)cps[s] * a.nll[(size_t)s * a.M + m];
+            a.grad_w[m] = (float)g;
+        }
+}
+
+// after the reparameterised backward: + sum_s ck_s sigmoid(sd_i) / softplus(sd_i)
+// on every scale, and d loss / d u = sum_s du_part[s]
+__global__ __launch_bounds__(256) void outer_finish_kernel(OuterArgs a, int nu) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n_tot && a.grad) {
+        int l = 0;
+        while (l + 1 < a.L && i >= a.woff[l + 1]) ++l;
+        const int64_t ps = a.poff[l] + a.n[l] + (i - a.woff[l]);
+        const float r = a.params[ps];
+        a.grad[ps] += a.sck[0] * sigmoid_f(r) / softplus_f(r);
+    }
+    const int j = i - a.n_tot;
+    if (j >= 0 && j < nu && a.grad_u) {
+        float g = 0.f;
+        for (int s = 0; s < a.S; ++s) g += a.du_part[(size_t)s * nu + j];
+        a.grad_u[j] = g;
+    }
+}
+
+static void fill(const psvi_plan& p, OuterArgs& a) {
+    a.L = p.L;
+    a.S = p.d.S;
+    a.M = p.d.M;
+    a.n_tot = p.n_tot;
+    a.family = p.family;
+    a.s0 = p.d.prior_sd;
+    for (int l = 0; l < p.L; ++l) {
+        a.n[l] = p.lay[l].n;
+        a.woff[l] = p.lay[l].woff;
+        a.poff[l] = p.lay[l].poff;
+        a.eoff[l] = p.lay[l].eoff;
+        a.din[l] = p.lay[l].din;
+        a.dout[l] = p.lay[l].dout;
+    }
+}
+
+hipError_t launch_outer_stats(const psvi_plan& p, const float* params, const float* eps,
+                              const float* x, double* stats, hipStream_t st) {
+    OuterArgs a{};
+    fill(p, a);
+    a.params = params;
+    a.eps = eps;
+    a.x = x;
+    a.stats = stats;
+    hipLaunchKernelGGL(outer_stats_kernel, dim3(p.d.S), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_outer_combine(const psvi_plan& p, int n_pseudo, const float* params,
+                                const float* w, const float* nll, const double* stats,
+                                double* loss, float* rowcoef, float* ck, float* sck,
+                                float* grad_w, double* sample_out, hipStream_t st) {
+    if (p.d.S > kOuterMaxS) return hipErrorInvalidValue;
+    OuterArgs a{};
+    fill(p, a);
+    a.n_pseudo = n_pseudo;
+    a.params = params;
+    a.w = w;
+    a.nll = nll;
+    a.stats = const_cast<double*>(stats);
+    a.loss = loss;
+    a.rowcoef = rowcoef;
+    a.ck = ck;
+    a.sck = sck;
+    a.grad_w = grad_w;
+    a.sample_out = sample_out;
+    hipLaunchKernelGGL(outer_combine_kernel, dim3(1), dim3(1024), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* params,
+                               const float* sck, float* grad, const float* du_part,
+                               float* grad_u, hipStream_t st) {
+    OuterArgs a{};
+    fill(p, a);
+    a.n_pseudo = n_pseudo;
+    a.params = params;
+    a.sck = const_cast<float*>(sck);
+    a.grad = grad;
+    a.du_part = du_part;
+    a.grad_u = grad_u;
+    const int nu = grad_u ? n_pseudo * p.lay[0].din : 0;
+    const int n = p.n_tot + nu;
+    hipLaunchKernelGGL(outer_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, nu);
+    return hipGetLastError();
+}
+
+}  // namespace psvi

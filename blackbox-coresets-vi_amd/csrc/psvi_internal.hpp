@@ -193,6 +193,16 @@ struct UpdChunk {
 
 struct NetArgs;  // kernels_net.hip
 
+// Outer-objective passes of the network kernel (psvi_outer_elbo_grad).
+struct NetOuter {
+    int mode;             // 1 forward (per-row NLL), 2 backward (row coefficients)
+    int n_pseudo;         // rows [0, n_pseudo) are pseudopoints, the rest data
+    float* nll_rows;      // mode 1: [S][M] unweighted NLL
+    const float* rowcoef; // mode 2: [S][2] d loss / d pseudo_s, d loss / d data_s
+    const float* ck;      // mode 2: [S] d loss / d nkl_s
+    float* du_part;       // mode 2, nullable: [S][n_pseudo][D] input gradient
+};
+
 }  // namespace psvi
 
 struct psvi_plan {
@@ -246,7 +256,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
                       const float* params, const float* eps, float* accMu, float* accRho,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out = nullptr, int64_t rn_n = 0, uint64_t rn_seed = 0,
-                      uint64_t rn_off = 0);
+                      uint64_t rn_off = 0, const NetOuter* outer = nullptr);
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
                             float* m, float* v, const psvi_adam_hp* hp, double* kl_out,
                             float* grad_out, int include_kl, hipStream_t st);
@@ -263,4 +273,14 @@ hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, h
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);
 AdamC make_adam(const psvi_adam_hp* hp);
+// outer objective (kernels_outer.hip)
+hipError_t launch_outer_stats(const psvi_plan& p, const float* params, const float* eps,
+                              const float* x, double* stats, hipStream_t st);
+hipError_t launch_outer_combine(const psvi_plan& p, int n_pseudo, const float* params,
+                                const float* w, const float* nll, const double* stats,
+                                double* loss, float* rowcoef, float* ck, float* sck,
+                                float* grad_w, double* sample_out, hipStream_t st);
+hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* params,
+                               const float* sck, float* grad, const float* du_part,
+                               float* grad_u, hipStream_t st);
 }  // namespace psvi

@@ -78,6 +78,7 @@ class InnerLoopPlan:
         self.xrecv_count = q(_lib.Q_XRECV_COUNT)
         self.loop_ws_bytes = q(_lib.Q_LOOP_WS_BYTES)
         self.tiled_floats = q(_lib.Q_TILED_FLOATS)  # 0: no tiled state for this plan
+        self.outer_ws_bytes = q(_lib.Q_OUTER_WS_BYTES)
         self.eps_stride = (self.eps_count + 3) // 4 * 4   # Philox offset per loop step
         self.n_tot = sum(i * o + o for i, o in layers)
 
@@ -173,6 +174,39 @@ class InnerLoopPlan:
                                       _ptr(grad), _ptr(ws), ws.numel(), _stream()),
               "psvi_elbo_grad")
         return elbo, grad
+
+    def outer_elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad=True,
+                        grad_u=True, grad_w=True, sample_stats=False, ws=None):
+        """Outer objective (PSVI.psvi_elbo) over this plan's M rows (pseudopoints
+        first, n_pseudo of them) -- psvi_outer_elbo_grad.  Returns a dict of
+        device tensors: loss (float64, 1), and as requested grad (P), grad_u
+        (n_pseudo, D), grad_w (n_pseudo), samples (S, 4: pseudo, data, nkl,
+        weight; float64)."""
+        D = self.layers[0][0]
+        n_pseudo = int(n_pseudo)
+        _need(x_all, "x_all", self.M * D)
+        _need(z_all, "z_all", self.M, torch.int32)
+        _need(w_all, "w_all", self.M)
+        _need(eps, "eps", self.eps_count)
+        _need(params, "params", self.param_count)
+        dev = params.device
+        out = {"loss": torch.empty(1, dtype=torch.float64, device=dev)}
+        if grad:
+            out["grad"] = torch.empty(self.param_count, dtype=torch.float32, device=dev)
+        if grad and grad_u:
+            out["grad_u"] = torch.empty(n_pseudo, D, dtype=torch.float32, device=dev)
+        if grad_w:
+            out["grad_w"] = torch.empty(n_pseudo, dtype=torch.float32, device=dev)
+        if sample_stats:
+            out["samples"] = torch.empty(self.S, 4, dtype=torch.float64, device=dev)
+        if ws is None or ws.numel() < self.outer_ws_bytes:
+            ws = torch.empty(self.outer_ws_bytes, dtype=torch.uint8, device=dev)
+        check(self.lib.psvi_outer_elbo_grad(
+            self.handle, n_pseudo, _ptr(x_all), _ptr(z_all), _ptr(w_all), _ptr(eps),
+            _ptr(params), _ptr(out["loss"]), _ptr(out.get("grad")), _ptr(out.get("grad_u")),
+            _ptr(out.get("grad_w")), _ptr(out.get("samples")), _ptr(ws), ws.numel(),
+            _stream()), "psvi_outer_elbo_grad")
+        return out
 
     # ------------------------------------------------------------ phases
     def mf_accumulate(self, u, z, w, eps, params, acc, nll_out):

@@ -105,6 +105,7 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_LOOP_WS_BYTES 10 /* workspace bytes for psvi_inner_loop                 */
 #define PSVI_Q_TILED_FLOATS  11 /* floats of the tiled corr/m/v state (0: the plan has
                                    none -- it needs full-cov, world 1, S <= 128)      */
+#define PSVI_Q_OUTER_WS_BYTES 12 /* workspace bytes for psvi_outer_elbo_grad          */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
  * Samples are split in contiguous blocks; for FULLCOV the rows of every
@@ -216,6 +217,28 @@ int psvi_mvn_phase_update_tiled(const psvi_plan* plan, const float* eps,
                                 float* adam_v, float* tstate, const psvi_adam_hp* hp,
                                 double* kl_out, int32_t include_kl,
                                 const float* eps_next, float* x_next, void* stream);
+
+/* ---- outer objective ------------------------------------------------------
+ * PSVI.psvi_elbo (psvi/inference/psvi_classes.py:445-486) with the sampled KL
+ * of every layer (VIMixin.sampled_nkl, psvi/models/neural_net.py:110-115;
+ * MultivariateNormalVIMixin.sampled_nkl, neural_net.py:438-442), world == 1,
+ * 2 <= S <= 2048.  The plan's M counts ALL rows of the batch: x_all
+ * ([M][D]) = cat(u, xbatch) with the n_pseudo pseudopoints first, z_all their
+ * class ids, w_all the row weights -- N f(v)_m for the pseudopoints, N / Nx
+ * for the data rows -- and eps the draw order of model(all_data).
+ *   loss_out[0] (double, written) <- sum_s W_s (data_s - pseudo_s) - mean_s lw_s,
+ *       lw_s = -pseudo_s + nkl_s, W = softmax_s(lw)
+ *   grad_params (PARAM_COUNT, nullable) <- d loss / d params (first order)
+ *   grad_u ([n_pseudo][D], nullable; needs grad_params) <- d loss / d u
+ *   grad_w (n_pseudo, nullable) <- d loss / d w_m (chain to v / alpha on the host)
+ *   sample_out ([S][4] doubles, nullable) <- pseudo_s, data_s, nkl_s, W_s
+ * The sampled KL uses L^-1 (x_s - mean) = eps_s (the reference's fp32
+ * triangular solve overflows at fn2 sizes).  ws: PSVI_Q_OUTER_WS_BYTES. */
+int psvi_outer_elbo_grad(const psvi_plan* plan, int32_t n_pseudo, const float* x_all,
+                         const int32_t* z_all, const float* w_all, const float* eps,
+                         const float* params, double* loss_out, float* grad_params,
+                         float* grad_u, float* grad_w, double* sample_out, void* ws,
+                         size_t ws_bytes, void* stream);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] ~ N(0,1), Philox4x32-10 counter (seed, offset + i) + Box-Muller.
