@@ -19,11 +19,18 @@ What runs where
     PSVILearnV softmax(v) (v = 0), PSVIAV exp(alpha) softmax(v)
     (psvi_classes.py:111,177-183, 1350-1360, 1482-1488).
 
-Not on the HIP path: the outer objective ``psvi_elbo``
-and everything that differentiates *through* the inner loop (the nested
-unroll, CG hypergradients), evaluation and data plumbing.  Those entry points
-raise NotImplementedError instead of silently running elsewhere, and
-``inner_elbo`` treats u and v as constants (no gradient flows to them).
+  * ``PSVI.psvi_elbo(xbatch, ybatch, model, params, hyperopt)``
+    (psvi_classes.py:445-486): the outer objective with the sampled KL of every
+    layer, one ``psvi_outer_elbo_grad`` call; its ``backward()`` delivers the
+    first-order gradients to the parameters, to u and -- through the host's
+    N f(v) -- to v and alpha.  ``joint_step`` / ``alternating_step``
+    (517-539) run on it unchanged.
+
+Not on the HIP path: everything that differentiates
+*through* the inner loop (the nested unroll, CG hypergradients), evaluation
+and data plumbing.  Those entry points raise NotImplementedError instead of
+silently running elsewhere, and ``inner_elbo`` treats u and v as constants (no
+gradient flows to them).
 
 There is no CPU fallback: a missing libpsvi_hip.so or GPU raises.
 """
@@ -35,7 +42,7 @@ from ..models.neural_net import categorical_fn, model_spec
 from ..runtime import InnerLoopPlan, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
-           "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO"]
+           "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
 
 _OUTER = ("is differentiated through the inner loop (second order); that is the next "
           "row of the hot-path scope (SURVEY.md 8(f)), not part of the HIP inner loop")
@@ -56,6 +63,32 @@ class HipInnerELBO(torch.autograd.Function):
     def backward(ctx, gout):
         (grad,) = ctx.saved_tensors
         return gout * grad, None, None, None, None, None
+
+
+class HipOuterELBO(torch.autograd.Function):
+    """Negative PSVI-ELBO (outer objective) and its first-order gradients
+    w.r.t. the flat parameters, the pseudo-inputs u and the pseudopoint
+    weights N f(v) in one HIP call (psvi_outer_elbo_grad)."""
+
+    @staticmethod
+    def forward(ctx, pvec, u, wp, plan, xb, z_all, w_data, eps):
+        Mu = u.shape[0]
+        x_all = torch.cat([u.detach().reshape(Mu, -1), xb]).to(torch.float32).contiguous()
+        w_all = torch.cat([wp.detach().to(torch.float32), w_data]).contiguous()
+        out = plan.outer_elbo_grad(Mu, x_all, z_all, w_all, eps, pvec.detach().contiguous(),
+                                   grad=True, grad_u=Mu > 0, grad_w=True)
+        gu = out["grad_u"] if Mu > 0 else torch.zeros_like(x_all[:0])
+        ctx.save_for_backward(out["grad"], gu.reshape(u.shape), out["grad_w"])
+        ctx.dtypes = (pvec.dtype, u.dtype, wp.dtype)
+        return out["loss"].to(pvec.dtype).reshape(())
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        gp, gu, gw = ctx.saved_tensors
+        tp, tu, tw = ctx.dtypes
+        return ((gout * gp).to(tp), (gout * gu).to(tu), (gout * gw).to(tw),
+                None, None, None, None, None)
 
 
 class PSVI:
@@ -184,21 +217,92 @@ class PSVI:
                 self.elbos.append((1, -float(host[t])))
         return elbos
 
-    # ------------------------------------------------- outer loop (not here)
-    def psvi_elbo(self, xbatch, ybatch, model=None, params=None, hyperopt=False):
-        raise NotImplementedError("psvi_elbo (outer objective) " + _OUTER)
+    # ------------------------------------------------------ outer objective
+    def psvi_elbo(self, xbatch, ybatch, model=None, params=None, hyperopt=False, eps=None):
+        """Negative PSVI-ELBO (psvi_classes.py:445-486), a 0-dim tensor:
+        sum_s W_s (data_s - pseudo_s) - mean_s lw_s over a fresh sample of the
+        weights, W = softmax_s(lw), lw_s = -pseudo_s + sampled_nkl_s.
+        Differentiable (first order) w.r.t. the parameters (or ``params`` with
+        hyperopt=True), u, and v / alpha through N f(v).  ``eps``: the
+        library's eps layout (``eps_count`` floats) to replay a draw."""
+        assert self.mc_samples is None or self.mc_samples > 1  # psvi_classes.py:449
+        model = self.model if model is None else model
+        fam, layers, prior_sd, S = model_spec(model)
+        if S < 2:
+            raise ValueError("psvi_elbo needs mc_samples > 1 (psvi_classes.py:449)")
+        Mu = int(self.u.shape[0])
+        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
+        Nx = int(xb.shape[0])
+        key = ("outer", fam, tuple(layers), S, Mu + Nx, prior_sd)
+        if key not in self._plans:
+            self._plans[key] = InnerLoopPlan(fam, layers, S, Mu + Nx, prior_sd=prior_sd)
+        plan = self._plans[key]
+        plist = list(params) if (hyperopt and params is not None) else list(model.parameters())
+        pvec = nn.utils.parameters_to_vector(plist)
+        if pvec.numel() != plan.param_count:
+            raise ValueError(f"{pvec.numel()} parameters, plan expects {plan.param_count}")
+        z = torch.cat([self.z.detach().to(self.device).reshape(-1),
+                       ybatch.detach().to(self.device).reshape(-1)])
+        if z.is_floating_point() and not torch.equal(z, z.round()):
+            raise ValueError("labels must hold class ids (learn_z is not supported)")
+        z_all = z.to(torch.int32).contiguous()
+        C = layers[-1][1]
+        if int(z_all.min()) < 0 or int(z_all.max()) >= C:
+            raise ValueError(f"class ids must lie in [0, {C})")
+        wp = (self.N * self.f(self.v, 0)).to(torch.float32).reshape(-1)
+        w_data = torch.full((Nx,), float(self.N) / max(Nx, 1), device=self.device)
+        if eps is None:
+            eps = self._draw_eps(plan)
+        loss = HipOuterELBO.apply(pvec, self.u, wp, plan, xb, z_all, w_data, eps)
+        return loss
 
+    def setup_optimizers(self, lr0net=1e-3, lr0u=1e-3, lr0v=1e-2, lr0joint=1e-3,
+                         trainer="nested"):
+        """The optimisers run_psvi creates (psvi_classes.py:867-885): Adam on
+        the network, on u, on v (learn_v), and for trainer 'joint' one Adam
+        over all of them."""
+        self.u.requires_grad_(True)
+        self.optim_net = torch.optim.Adam(list(self.model.parameters()), lr0net)
+        self.optim_u = torch.optim.Adam([self.u], lr0u)
+        if self.learn_v:
+            self.optim_v = torch.optim.Adam([self.v], lr0v)
+        if trainer == "joint":
+            vp = list(self.model.parameters()) + [self.u] + ([self.v] if self.learn_v else [])
+            self.optim = torch.optim.Adam(vp, lr0joint)
+
+    def joint_step(self, xbatch, ybatch):
+        """psvi_classes.py:517-525: one Adam step on the outer objective over
+        the network, u (and v)."""
+        self.optim.zero_grad()
+        loss = self.psvi_elbo(xbatch, ybatch, model=self.model)
+        with torch.no_grad():
+            if self.register_elbos:
+                self.elbos.append((2, -loss.item()))
+        loss.backward()
+        self.optim.step()
+        return loss
+
+    def alternating_step(self, xbatch, ybatch):
+        """psvi_classes.py:527-539: a step of optim_net, then of optim_u, each
+        on a fresh evaluation of the outer objective."""
+        for i in range(2):
+            self.optim = self.optim_net if i == 0 else self.optim_u
+            self.optim.zero_grad()
+            loss = self.psvi_elbo(xbatch, ybatch, model=self.model)
+            with torch.no_grad():
+                if self.register_elbos:
+                    self.elbos.append((1, -loss.item())) if i == 1 else self.elbos.append(
+                        (0, -loss.item()))
+            loss.backward()
+            self.optim.step()
+        return loss
+
+    # -------------------------------------------- second order (not here)
     def nested_step(self, xbatch, ybatch, truncated=False, K=5):
         raise NotImplementedError("nested_step " + _OUTER)
 
     def hyper_step(self, xbatch, ybatch, **kwargs):
         raise NotImplementedError("hyper_step " + _OUTER)
-
-    def joint_step(self, xbatch, ybatch):
-        raise NotImplementedError("joint_step " + _OUTER)
-
-    def alternating_step(self, xbatch, ybatch):
-        raise NotImplementedError("alternating_step " + _OUTER)
 
     def run_psvi(self, *args, **kwargs):
         raise NotImplementedError("run_psvi drives the outer loop, which " + _OUTER)

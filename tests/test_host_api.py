@@ -135,10 +135,22 @@ def test_inner_loop_refuses_cpu_tensors():
         ps.inner_loop(T=1)
 
 
-def test_outer_loop_entry_points_raise():
+def test_second_order_entry_points_raise():
     f, model = fixture_model("g1_logreg_c1")
     ps = make_psvi(f, model)
-    for fn in (lambda: ps.psvi_elbo(None, None), lambda: ps.nested_step(None, None),
-               lambda: ps.hyper_step(None, None), lambda: ps.run_psvi()):
+    for fn in (lambda: ps.nested_step(None, None), lambda: ps.hyper_step(None, None),
+               lambda: ps.run_psvi()):
         with pytest.raises(NotImplementedError):
             fn()
+
+
+def test_outer_objective_has_no_cpu_fallback():
+    """psvi_elbo runs on the HIP library only: host tensors (or a missing
+    device / library) raise instead of computing anywhere else."""
+    from psvi.runtime._lib import PsviError
+
+    f, model = fixture_model("g1_logreg_c1")
+    ps = make_psvi(f, model)
+    xb, yb = torch.randn(8, 2), torch.zeros(8)
+    with pytest.raises((ValueError, PsviError)):
+        ps.psvi_elbo(xb, yb)

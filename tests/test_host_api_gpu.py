@@ -59,3 +59,78 @@ def test_inner_loop_philox_is_deterministic_and_advances():
     b = make_psvi(f, model.cuda(), "cuda")
     # same Philox stream; mean-field sums use fp32 atomics (order-nondeterministic last bits)
     assert torch.allclose(b.inner_loop(T=2).cpu(), e1, rtol=1e-7, atol=0)
+
+
+# ------------------------------------------------------------ outer objective
+def make_outer_psvi(name):
+    """PSVI object + model of an outer fixture (tools/gen_golden_outer.py), with
+    u, v (and alpha) as leaves that collect gradients."""
+    from golden_util import load_fixture
+    from psvi.inference import PSVIAV, PSVILearnV
+    from test_host_api import build_model
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    model = build_model(cfg, f["params0"]).cuda()
+    cls = PSVIAV if cfg["f"] == "exp_alpha_softmax" else PSVILearnV
+    u = torch.tensor(f["u"], dtype=torch.float32, device="cuda").requires_grad_(True)
+    z = torch.tensor(f["z"], dtype=torch.float32, device="cuda")
+    ps = cls(u=u, z=z, N=cfg["N"], model=model, mc_samples=cfg["S"], device_id=0)
+    ps.device = torch.device("cuda")
+    ps.v = torch.tensor(f["v"], dtype=torch.float32, device="cuda").requires_grad_(True)
+    if cfg["f"] == "exp_alpha_softmax":
+        ps.alpha = torch.tensor([cfg["alpha"]], dtype=torch.float32,
+                                device="cuda").requires_grad_(True)
+    xb = torch.tensor(f["xb"], device="cuda")
+    yb = torch.tensor(f["yb"], device="cuda")
+    eps = torch.tensor(f["eps"], dtype=torch.float32, device="cuda")
+    return f, cfg, model, ps, xb, yb, eps
+
+
+@pytest.mark.parametrize("name", fixture_names("o"))
+def test_psvi_elbo_backward_matches_reference(name):
+    f, cfg, model, ps, xb, yb, eps = make_outer_psvi(name)
+    loss = ps.psvi_elbo(xb, yb, eps=eps)
+    assert loss.dim() == 0
+    assert rel(loss.item(), f["loss"]) < 1e-5, (loss.item(), float(f["loss"]))
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in model.parameters()]).cpu().numpy()
+    assert_grad_close(g, f["grad_params"], what=name + " params")
+    assert_grad_close(ps.u.grad.cpu().numpy(), f["grad_u"], what=name + " u")
+    assert l2rel(ps.v.grad.cpu().numpy(), f["grad_v"]) < 1e-4
+    if cfg["f"] == "exp_alpha_softmax":
+        assert rel(ps.alpha.grad.item(), f["grad_alpha"][0]) < 1e-4
+
+
+def test_joint_step_is_adam_on_the_outer_gradient():
+    f, cfg, model, ps, xb, yb, eps = make_outer_psvi("o4_fn2_tiny")
+    ps.setup_optimizers(lr0joint=1e-3, trainer="joint")
+    p0 = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
+    u0 = ps.u.detach().cpu().numpy().copy()
+    orig = ps._draw_eps
+    ps._draw_eps = lambda plan: eps  # replay the reference's draw
+    loss = ps.joint_step(xb, yb)
+    ps._draw_eps = orig
+    assert rel(loss.item(), f["loss"]) < 1e-5
+    assert ps.elbos[-1][0] == 2
+    # first Adam step: p - lr * g / (|g| + eps) with the reference gradient
+    g = f["grad_params"]
+    want = p0 - 1e-3 * g / (np.abs(g) + 1e-8)
+    p1 = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
+    big = np.abs(g) > 1e-4 * np.abs(g).max()  # entries whose sign is not rounding noise
+    assert np.abs(p1 - want)[big].max() < 1e-6
+    gu = f["grad_u"]
+    assert np.allclose(ps.u.detach().cpu().numpy(), u0 - 1e-3 * gu / (np.abs(gu) + 1e-8),
+                       atol=1e-6)
+
+
+def test_alternating_step_moves_network_then_u():
+    f, cfg, model, ps, xb, yb, eps = make_outer_psvi("o2_fn_c2_av")
+    ps.setup_optimizers(trainer="alternating")
+    p0 = torch.nn.utils.parameters_to_vector(model.parameters()).detach().clone()
+    u0 = ps.u.detach().clone()
+    loss = ps.alternating_step(xb, yb)
+    assert torch.isfinite(loss)
+    assert [e[0] for e in ps.elbos[-2:]] == [0, 1]
+    assert not torch.equal(torch.nn.utils.parameters_to_vector(model.parameters()).detach(), p0)
+    assert not torch.equal(ps.u.detach(), u0)
