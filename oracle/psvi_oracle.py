@@ -454,3 +454,228 @@ def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=
     gX = dX.sum(0)[:Mu]
     gw = (cp[:, None] * nll[:, :Mu]).sum(0)
     return loss, grad, gX, gw
+
+
+# ------------------------------------- second order: HVP of the inner ELBO
+def _sample(family, layers, params, eps, S):
+    """Per-layer sampled weights and reparameterisation pieces."""
+    out = []
+    po = eo = 0
+    for din, dout in layers:
+        n = din * dout + dout
+        if family == "mf":
+            mu, rho = params[po:po + n], params[po + n:po + 2 * n]
+            E = np.concatenate([eps[eo:eo + S * din * dout].reshape(S, din * dout),
+                                eps[eo + S * din * dout:eo + S * n].reshape(S, dout)], axis=1)
+            X = mu[None] + softplus(rho)[None] * E
+            out.append(dict(po=po, n=n, E=E, mean=mu, sd=rho, corr=None, X=X))
+            po += 2 * n
+        else:
+            nc = mvn_ncorr(n)
+            mean, sdr, corr = params[po:po + n], params[po + n:po + 2 * n], params[po + 2 * n:po + 2 * n + nc]
+            E = eps[eo:eo + S * n].reshape(S, n)
+            X = mean[None] + E @ mvn_dense_L(sdr, corr, n).T
+            out.append(dict(po=po, n=n, E=E, mean=mean, sd=sdr, corr=corr, X=X))
+            po += 2 * n + nc
+        eo += S * n
+    return out
+
+
+def _split(layers, Xl):
+    return ([x["X"][:, :i * o].reshape(-1, o, i) for x, (i, o) in zip(Xl, layers)],
+            [x["X"][:, i * o:] for x, (i, o) in zip(Xl, layers)])
+
+
+def inner_hvp(family, layers, params, u, z, w, eps, S, vec, prior_sd=1.0):
+    """Hessian-vector product of the negative inner ELBO (psvi_classes.py:488-511)
+    at fixed eps, H vec, and the mixed products d/du (vec . grad) and
+    d/dw (vec . grad) -- what hypergrad's CG_normaleq takes from autograd
+    (torch_grad / jvp of GradientDescent's fp_map, psvi/hypergrad/
+    hypergradients.py:199-244, 308-311).  Forward-over-reverse (Pearlmutter
+    R-op): tangent sample x_dot = J vec, tangent forward, R-backward; the
+    ReLU masks are constant.  Returns (value, grad, Hv, d_u, d_w)."""
+    params = np.asarray(params, np.float64)
+    vec = np.asarray(vec, np.float64)
+    eps = np.asarray(eps, np.float64)
+    u = np.asarray(u, np.float64)
+    w = np.asarray(w, np.float64)
+    s0sq = float(prior_sd) ** 2
+    Xl = _sample(family, layers, params, eps, S)
+    Ws, bs = _split(layers, Xl)
+    # tangent sample
+    for x in Xl:
+        po, n, E = x["po"], x["n"], x["E"]
+        vm, vs_ = vec[po:po + n], vec[po + n:po + 2 * n]
+        dsd = sigmoid(x["sd"]) * vs_
+        if family == "mf":
+            x["Xd"] = vm[None] + dsd[None] * E
+        else:
+            nc = mvn_ncorr(n)
+            Lv = np.zeros((n, n))
+            Lv[np.arange(n), np.arange(n)] = dsd
+            r, c = tril_rows_cols(n)
+            Lv[r, c] = vec[po + 2 * n:po + 2 * n + nc]
+            x["Xd"] = vm[None] + E @ Lv.T
+    Wd = [x["Xd"][:, :i * o].reshape(S, o, i) for x, (i, o) in zip(Xl, layers)]
+    bd = [x["Xd"][:, i * o:] for x, (i, o) in zip(Xl, layers)]
+    L = len(layers)
+    M = u.shape[0]
+    hs, acts = _net_rows_forward(u, Ws, bs)
+    hd = [np.zeros_like(hs[0])]
+    for l in range(L):
+        ad = np.einsum("smi,soi->smo", hd[l], Ws[l]) + np.einsum("smi,soi->smo", hs[l], Wd[l]) \
+            + bd[l][:, None, :]
+        hd.append(ad * (acts[l] > 0) if l < L - 1 else ad)
+    logits, ldot = hs[-1], hd[-1]
+    mx = logits.max(-1, keepdims=True)
+    lse = (mx + np.log(np.exp(logits - mx).sum(-1, keepdims=True)))[..., 0]
+    zi = np.asarray(z).astype(np.int64)
+    nll = lse - logits[:, np.arange(M), zi]
+    p = np.exp(logits - lse[..., None])
+    pmo = p.copy()
+    pmo[:, np.arange(M), zi] -= 1.0
+    nll_dot = (pmo * ldot).sum(-1)                                   # (S, M)
+    pdot = p * (ldot - (p * ldot).sum(-1, keepdims=True))
+    g = pmo * w[None, :, None]
+    gd = pdot * w[None, :, None]
+    G, Gd = [None] * L, [None] * L
+    for l in range(L - 1, -1, -1):
+        dW = np.einsum("smo,smi->soi", g, hs[l])
+        dWd = np.einsum("smo,smi->soi", gd, hs[l]) + np.einsum("smo,smi->soi", g, hd[l])
+        G[l] = np.concatenate([dW.reshape(S, -1), g.sum(1)], axis=1)
+        Gd[l] = np.concatenate([dWd.reshape(S, -1), gd.sum(1)], axis=1)
+        g_new = np.einsum("smo,soi->smi", g, Ws[l])
+        gd_new = np.einsum("smo,soi->smi", gd, Ws[l]) + np.einsum("smo,soi->smi", g, Wd[l])
+        if l > 0:
+            g, gd = g_new * (acts[l - 1] > 0), gd_new * (acts[l - 1] > 0)
+        else:
+            d_u = gd_new.sum(0)
+    value = float((nll * w[None]).sum())
+    grad = np.zeros_like(params)
+    hv = np.zeros_like(params)
+    for l, x in enumerate(Xl):
+        po, n, E, sd = x["po"], x["n"], x["E"], x["sd"]
+        sp, sg = softplus(sd), sigmoid(sd)
+        vm, vsd = vec[po:po + n], vec[po + n:po + 2 * n]
+        mean = x["mean"]
+        ge = (G[l] * E).sum(0)
+        value += float((0.5 * ((sp ** 2 + mean ** 2) / s0sq - 1.0 - np.log(sp ** 2 / s0sq))).sum())
+        grad[po:po + n] = G[l].sum(0) + mean / s0sq
+        grad[po + n:po + 2 * n] = (ge + sp / s0sq - 1.0 / sp) * sg
+        hv[po:po + n] = Gd[l].sum(0) + vm / s0sq
+        kl2 = (1.0 / sp ** 2 + 1.0 / s0sq) * sg ** 2 + (sp / s0sq - 1.0 / sp) * sg * (1.0 - sg)
+        hv[po + n:po + 2 * n] = (Gd[l] * E).sum(0) * sg + ge * sg * (1.0 - sg) * vsd + kl2 * vsd
+        if family != "mf":
+            nc = mvn_ncorr(n)
+            corr = x["corr"]
+            r, c = tril_rows_cols(n)
+            value += float(0.5 * (corr ** 2).sum() / s0sq)
+            grad[po + 2 * n:po + 2 * n + nc] = (G[l].T @ E)[r, c] + corr / s0sq
+            hv[po + 2 * n:po + 2 * n + nc] = (Gd[l].T @ E)[r, c] + vec[po + 2 * n:po + 2 * n + nc] / s0sq
+    return value, grad, hv, d_u, nll_dot.sum(0)
+
+
+def inner_grad_uw(family, layers, params, u, z, w, eps, S, prior_sd=1.0):
+    """Negative inner ELBO, its parameter gradient and its gradients w.r.t. u
+    and w (for finite-difference checks of inner_hvp)."""
+    params = np.asarray(params, np.float64)
+    Xl = _sample(family, layers, params, np.asarray(eps, np.float64), S)
+    Ws, bs = _split(layers, Xl)
+    u = np.asarray(u, np.float64)
+    w = np.asarray(w, np.float64)
+    M = u.shape[0]
+    hs, acts = _net_rows_forward(u, Ws, bs)
+    logits = hs[-1]
+    mx = logits.max(-1, keepdims=True)
+    lse = (mx + np.log(np.exp(logits - mx).sum(-1, keepdims=True)))[..., 0]
+    zi = np.asarray(z).astype(np.int64)
+    nll = lse - logits[:, np.arange(M), zi]
+    pmo = np.exp(logits - lse[..., None])
+    pmo[:, np.arange(M), zi] -= 1.0
+    dWs, dbs, dX = _net_rows_backward(np.broadcast_to(w[None], nll.shape), pmo, hs, acts, Ws)
+    fn = mf_elbo_grad if family == "mf" else mvn_elbo_grad
+    val, grad = fn(layers, params, u, z, w, eps, S, prior_sd)
+    return val, grad, dX.sum(0), nll.sum(0)
+
+
+def torch_adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """torch.optim.Adam (the reference's optim_u / optim_v), t 1-based."""
+    m = beta1 * m + (1 - beta1) * g
+    v = beta2 * v + (1 - beta2) * g * g
+    denom = np.sqrt(v) / np.sqrt(1 - beta2 ** t) + eps
+    return p - (lr / (1 - beta1 ** t)) * m / denom, m, v
+
+
+def hyper_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer, S, T, K,
+               lr0net, lr0u, lr0v, linsys_lr=1e-4, prior_sd=1.0, cg_tol=1e-10):
+    """PSVI.hyper_step with the CG_normaleq hypergradient (psvi_classes.py:602-687,
+    psvi/hypergrad/hypergradients.py:199-244, CG_torch.py:9-45), PSVILearnV
+    weights f = softmax (v learned, not clamped).  eps_inner: the draws of the
+    inner-objective calls in order -- T inner Adam steps, fp_map, the initial
+    jvp (2: the first only sizes its dummy), then 2 per CG iteration;
+    eps_outer: the outer objective's draws (hypergradient, returned loss).
+    Returns dict(params, u, v, u_grad, v_grad, ll)."""
+    u = np.asarray(u, np.float64)
+    v = np.asarray(v, np.float64)
+    M = u.shape[0]
+    Nx = xb.shape[0]
+
+    def wts(vv):
+        return coreset_weights(vv, N, "softmax")
+
+    def softmax_T(vv, dw):  # d/dv of w = N softmax(v), applied to dw
+        e = np.exp(vv - vv.max())
+        sm = e / e.sum()
+        gs = N * dw
+        return sm * (gs - (gs * sm).sum())
+
+    w = wts(v)
+    _, _, traj, _, _ = run_inner_loop(family, layers, params0, u, z, w, eps_inner[:T], S, lr0net,
+                                      "hypergrad")
+    p = traj[-1]
+    ei = list(eps_inner[T:])
+    X = np.concatenate([u, xb])
+    zz = np.concatenate([z, yb])
+    ww = np.concatenate([w, np.full(Nx, N / Nx)])
+    o_loss, g_w, g_u, g_wts = outer_elbo_grad(family, layers, p, X, zz, ww, M, eps_outer[0], S,
+                                              prior_sd)
+    g_v = softmax_T(v, g_wts)
+    lr = linsys_lr
+    eA = ei.pop(0)                                  # w_mapped = fp_map(params, hparams)
+
+    def hv(e, x):
+        return inner_hvp(family, layers, p, u, z, w, e, S, x, prior_sd)
+
+    def jvp(x):                                     # J x = x - lr H x at a fresh draw
+        ei.pop(0)                                   # the dummy's fp_map call
+        return x - lr * hv(ei.pop(0), x)[2]
+
+    def A(x):                                       # dfp_map_dw
+        vmj = lr * hv(eA, x)[2]                     # x - J^T x
+        return vmj - jvp(vmj)
+
+    b = g_w - jvp(g_w)
+    xk = np.zeros_like(b)
+    r = b.copy()
+    pk = r.copy()
+    for _ in range(K):
+        Ap = A(pk)
+        rTr = float(r @ r)
+        alpha = rTr / float(pk @ Ap)
+        xn = xk + alpha * pk
+        rn = r - alpha * Ap
+        if float(np.linalg.norm(rn)) < cg_tol:
+            break
+        beta = float(rn @ rn) / rTr
+        pk = rn + beta * pk
+        xk, r = xn, rn
+    # grads = torch_grad(w_mapped, hparams, vs) = -lr d/dhp (vs . grad_p inner)
+    _, _, _, du, dw = hv(eA, xk)
+    u_grad = -lr * du + g_u
+    v_grad = -lr * softmax_T(v, dw) + g_v
+    u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
+    v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
+    X2 = np.concatenate([u_new, xb])
+    ww2 = np.concatenate([wts(v_new), np.full(Nx, N / Nx)])
+    ll = outer_elbo_grad(family, layers, p, X2, zz, ww2, M, eps_outer[1], S, prior_sd)[0]
+    return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, ll=ll)

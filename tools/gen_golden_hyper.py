@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Golden vectors for the second-order path of the ``hyper`` trainer.
+
+Runs ONLY in the development container (the reference is mounted read-only at
+/root/reference); the parent re-launches this script in a child interpreter
+whose sys.path holds the reference and not this repo (both are ``psvi``).
+In float64 with every Monte-Carlo draw rounded to fp32 (the HIP path's eps),
+the child records
+
+  * h*.npz -- the Hessian-vector product of the reference's inner objective
+    and its mixed products, by double backward exactly as hypergrad takes them
+    (psvi/hypergrad/hypergradients.py:199-244 torch_grad / jvp through
+    GradientDescent's fp_map, diff_optimizers.py:51-60, 157-159):
+        g = d inner_elbo / d params (create_graph);  s = g . vec
+        ds / d params (= H vec), ds / d u, ds / d v
+    with inner_elbo(model=fmodel, params=p, hyperopt=True) on a
+    monkeypatch'ed model (psvi_classes.py:602-650);
+  * y*.npz -- one full PSVI.hyper_step (psvi_classes.py:602-687): the T-step
+    first-order inner loop (hypergrad DifferentiableAdam), CG_normaleq with K
+    iterations, the u / v Adam steps, the returned outer loss -- and every
+    draw in call order, so the HIP path can replay it.
+
+Usage:  python tools/gen_golden_hyper.py
+"""
+import json
+import os
+import subprocess
+import sys
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+
+
+def _child():
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gen_golden import _install_stubs
+
+    _install_stubs()
+    import numpy as np
+    import torch
+    import torch.distributions.multivariate_normal as mvn_mod
+    import torch.distributions.normal as normal_mod
+    import torch.nn as nn
+    from torch.nn.utils import parameters_to_vector
+
+    from psvi.inference.psvi_classes import PSVILearnV
+    from psvi.models.neural_net import (VILinear, VILinearMultivariateNormal,
+                                        categorical_fn, make_fc2net, make_fcnet)
+    from psvi.robust_higher.patch import monkeypatch
+
+    torch.set_default_dtype(torch.float64)
+    draws = []
+
+    def wrap(orig):
+        def f(shape, dtype, device):
+            out = orig(shape, dtype=dtype, device=device).float().to(dtype)
+            draws.append(out.detach().clone().reshape(-1))
+            return out
+        return f
+
+    for m in (normal_mod, mvn_mod):
+        m._standard_normal = wrap(m._standard_normal)
+
+    gen = torch.Generator().manual_seed(777)
+
+    def perturb(model, mu_scale, rho_lo, rho_hi, corr_scale):
+        with torch.no_grad():
+            for name, p in model.named_parameters():
+                leaf = name.split(".")[-1]
+                if leaf in ("weight", "bias", "mean"):
+                    p.copy_(mu_scale * torch.randn(p.shape, generator=gen))
+                elif leaf in ("_weight_sd", "_bias_sd", "_sd"):
+                    p.copy_(rho_lo + (rho_hi - rho_lo) * torch.rand(p.shape, generator=gen))
+                elif leaf == "_corr":
+                    p.copy_(corr_scale * torch.randn(p.shape, generator=gen))
+                p.copy_(p.float().double())
+
+    def layer_sizes(model):
+        return [[m.in_features, m.out_features] for m in model.modules()
+                if isinstance(m, (VILinear, VILinearMultivariateNormal))]
+
+    def make_obj(model, M, D, C, S, N):
+        u = torch.randn(M, D, generator=gen).float().double().requires_grad_(True)
+        z = torch.tensor([float(i % C) for i in range(M)])
+        v = (0.2 * torch.randn(M, generator=gen)).float().double().requires_grad_(True)
+        obj = PSVILearnV.__new__(PSVILearnV)
+        obj.model = model
+        obj.u, obj.z, obj.v, obj.N = u, z, v, N
+        obj.distr_fn = categorical_fn
+        obj.learn_z, obj.learn_v, obj.parameterised = False, True, True
+        obj.mc_samples = S
+        obj.nc = C
+        obj.f = torch.softmax
+        return obj
+
+    def cfg_of(family, model, S, M, N, **kw):
+        c = dict(family=family, layers=layer_sizes(model), S=S, M=M, N=N, prior_sd=1.0,
+                 f="softmax")
+        c.update(kw)
+        return c
+
+    def run_hvp(name, family, model, M, D, C, S, N, seed, note=""):
+        torch.manual_seed(seed)
+        obj = make_obj(model, M, D, C, S, N)
+        fmodel = monkeypatch(model, copy_initial_weights=True)
+        params = [p.detach().clone().requires_grad_(True) for p in fmodel.parameters()]
+        p0 = torch.cat([p.detach().reshape(-1) for p in params])
+        vec = torch.randn(p0.numel(), generator=gen).float().double()
+        draws.clear()
+        loss = obj.inner_elbo(model=fmodel, params=params, hyperopt=True)
+        eps = torch.cat(draws).numpy()
+        g = torch.autograd.grad(loss, params, create_graph=True)
+        gvec = torch.cat([x.reshape(-1) for x in g])
+        s = (gvec * vec).sum()
+        out = torch.autograd.grad(s, params + [obj.u, obj.v])
+        hv = torch.cat([x.reshape(-1) for x in out[:len(params)]])
+        w = (obj.N * obj.f(obj.v, 0)).detach()
+        np.savez_compressed(
+            os.path.join(OUT, name + ".npz"),
+            config=np.array(json.dumps(cfg_of(family, model, S, M, N, seed=seed, note=note))),
+            params0=p0.numpy().astype(np.float32), u=obj.u.detach().numpy().astype(np.float32),
+            z=obj.z.numpy().astype(np.float32), v=obj.v.detach().numpy().astype(np.float32),
+            w=w.numpy(), eps=eps.astype(np.float32), vec=vec.numpy().astype(np.float32),
+            elbo=np.array(float(loss.detach())), grad=gvec.detach().numpy(), hv=hv.numpy(),
+            d_u=out[-2].numpy(), d_v=out[-1].numpy())
+        print(f"wrote {name}: P={p0.numel()} elbo={float(loss):.6f}")
+
+    def run_hyper_step(name, family, model, M, Nx, D, C, S, N, seed, T, K, note=""):
+        torch.manual_seed(seed)
+        obj = make_obj(model, M, D, C, S, N)
+        obj.inner_it = T
+        lr0net, lr0u, lr0v = 1e-3, 1e-3, 1e-2
+        obj.optim_net = torch.optim.Adam(list(model.parameters()), lr0net)
+        obj.optim_u = torch.optim.Adam([obj.u], lr0u)
+        obj.optim_v = torch.optim.Adam([obj.v], lr0v)
+        xb = torch.randn(Nx, D, generator=gen).float().double()
+        yb = torch.randint(0, C, (Nx,), generator=gen).double()
+        p0 = parameters_to_vector(model.parameters()).detach().clone()
+        u0, v0 = obj.u.detach().clone(), obj.v.detach().clone()
+        draws.clear()
+        sizes = []
+        n_prev = [0]
+
+        # draw counts per call (to split the recorded stream)
+        orig_inner, orig_outer = obj.inner_elbo, obj.psvi_elbo
+
+        def inner(*a, **k):
+            r = orig_inner(*a, **k)
+            sizes.append(("inner", len(draws) - n_prev[0]))
+            n_prev[0] = len(draws)
+            return r
+
+        def outer(*a, **k):
+            r = orig_outer(*a, **k)
+            sizes.append(("outer", len(draws) - n_prev[0]))
+            n_prev[0] = len(draws)
+            return r
+
+        obj.inner_elbo, obj.psvi_elbo = inner, outer
+        ll = obj.hyper_step(xb, yb, K=K)
+        calls = [k for k, _ in sizes]
+        eps = [torch.cat(draws[sum(c for _, c in sizes[:i]):sum(c for _, c in sizes[:i + 1])])
+               .numpy().astype(np.float32) for i in range(len(sizes))]
+        ne = {k: len(e) for k, e in zip(calls, eps)}
+        np.savez_compressed(
+            os.path.join(OUT, name + ".npz"),
+            config=np.array(json.dumps(cfg_of(family, model, S, M, N, Nx=Nx, T=T, K=K,
+                                              lr0net=lr0net, lr0u=lr0u, lr0v=lr0v,
+                                              linsys_lr=1e-4, calls=calls, seed=seed,
+                                              note=note))),
+            params0=p0.numpy().astype(np.float32), u0=u0.numpy().astype(np.float32),
+            v0=v0.numpy().astype(np.float32), z=obj.z.numpy().astype(np.float32),
+            xb=xb.numpy().astype(np.float32), yb=yb.numpy().astype(np.float32),
+            eps_inner=np.stack([e for k, e in zip(calls, eps) if k == "inner"]),
+            eps_outer=np.stack([e for k, e in zip(calls, eps) if k == "outer"]),
+            ll=np.array(float(ll)),
+            u=obj.u.detach().numpy(), v=obj.v.detach().numpy(),
+            u_grad=obj.u.grad.numpy(), v_grad=obj.v.grad.numpy(),
+            params=parameters_to_vector(model.parameters()).detach().numpy())
+        print(f"wrote {name}: calls={len(calls)} ll={float(ll):.6f} eps sizes={ne}")
+
+    # HVP fixtures
+    model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
+    perturb(model, 0.3, -3.5, -2.5, 0.002)
+    run_hvp("h1_fn2_tiny", "mvn", model, M=10, D=8, C=3, S=16, N=800, seed=11)
+
+    model = make_fcnet(5, 7, 3, n_layers=2, mc_samples=6, init_sd=0.05)
+    perturb(model, 0.4, -3.0, -1.0, 0.0)
+    run_hvp("h2_fn_deep", "mf", model, M=13, D=5, C=3, S=6, N=500, seed=12)
+
+    model = make_fcnet(2, 20, 4, n_layers=1, mc_samples=8, init_sd=0.1)
+    perturb(model, 0.3, -4.0, -1.0, 0.0)
+    run_hvp("h3_fn_shallow", "mf", model, M=12, D=2, C=4, S=8, N=800, seed=13)
+
+    model = nn.Sequential(VILinearMultivariateNormal(2, 2, init_sd=0.1, mc_samples=4))
+    perturb(model, 0.5, -3.0, -1.0, 0.02)
+    run_hvp("h4_logreg_fullcov", "mvn", model, M=10, D=2, C=2, S=4, N=800, seed=14)
+
+    # one whole hyper_step each
+    model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
+    perturb(model, 0.3, -3.5, -2.5, 0.002)
+    run_hyper_step("y1_fn2_tiny", "mvn", model, M=10, Nx=12, D=8, C=3, S=16, N=800, seed=21,
+                   T=3, K=4)
+
+    model = make_fcnet(5, 7, 3, n_layers=2, mc_samples=6, init_sd=0.05)
+    perturb(model, 0.4, -3.0, -1.0, 0.0)
+    run_hyper_step("y2_fn_deep", "mf", model, M=13, Nx=9, D=5, C=3, S=6, N=500, seed=22,
+                   T=3, K=4)
+
+
+def main():
+    if "--child" in sys.argv:
+        _child()
+        return
+    os.makedirs(OUT, exist_ok=True)
+    env = dict(os.environ)
+    env["PYTHONPATH"] = REF
+    env["PYTHONDONTWRITEBYTECODE"] = "1"
+    subprocess.run([sys.executable, "-B", os.path.abspath(__file__), "--child"],
+                   env=env, check=True, cwd="/tmp")
+
+
+if __name__ == "__main__":
+    main()
