@@ -406,6 +406,35 @@ struct OuterWs {
     double* stats;
     size_t bytes;
 };
+static OuterWs outer_ws(const psvi_plan* p, void* ws);
+
+// psvi_hvp workspace: the step workspace (x), x_dot [S][n_tot], the tangent
+// parameters [P] (full-cov), G and G_dot [S][n_tot], d_u parts [S][M][D],
+// NLL_dot [S][M]
+struct HvpWs {
+    float *xd, *T, *G, *Gd, *du, *nlld;
+    size_t bytes;
+};
+static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
+    const size_t S = p->d.S, M = p->d.M, D = p->lay[0].din, nt = p->n_tot;
+    char* b = (char*)ws;
+    HvpWs o{};
+    size_t off = align256(p->ws_bytes);
+    auto take = [&](size_t bytes) {
+        char* r = b ? b + off : nullptr;
+        off += align256(bytes);
+        return r;
+    };
+    o.xd = (float*)take(sizeof(float) * S * nt);
+    o.T = (float*)take(p->family == PSVI_FAMILY_FULLCOV ? sizeof(float) * (size_t)p->P : 0);
+    o.G = (float*)take(sizeof(float) * S * nt);
+    o.Gd = (float*)take(sizeof(float) * S * nt);
+    o.du = (float*)take(sizeof(float) * S * M * D);
+    o.nlld = (float*)take(sizeof(float) * S * M);
+    o.bytes = off;
+    return o;
+}
+
 static OuterWs outer_ws(const psvi_plan* p, void* ws) {
     const size_t S = p->d.S, M = p->d.M, D = p->lay[0].din;
     char* b = (char*)ws;
@@ -442,6 +471,7 @@ int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
         case PSVI_Q_TILED_FLOATS: *value = (int64_t)tiled_floats(p); break;
         case PSVI_Q_XRECV_COUNT: *value = (int64_t)p->s_cnt[r] * p->n_tot; break;
         case PSVI_Q_OUTER_WS_BYTES: *value = (int64_t)outer_ws(p, nullptr).bytes; break;
+        case PSVI_Q_HVP_WS_BYTES: *value = (int64_t)hvp_ws(p, nullptr).bytes; break;
         default: return fail(PSVI_EINVAL, "unknown query key");
     }
     return 0;
@@ -765,6 +795,37 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
     }
     // 5. explicit log-det term on the scales; d loss / d u
     HIP_TRY(launch_outer_finish(*p, n_pseudo, params, o.sck, grad_params, o.du, grad_u, st));
+    return 0;
+}
+
+int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+             const float* eps, const float* params, const float* vec, float* hv_out,
+             float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream) {
+    if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (p->world != 1) return fail(PSVI_ESTATE, "psvi_hvp needs world == 1");
+    if (!u || !z || !w || !eps || !params || !vec || !hv_out)
+        return fail(PSVI_EINVAL, "null pointer");
+    if (rop_rows(*p) == 0)
+        return fail(PSVI_EUNSUP, "model too wide for the per-sample R-op kernel's LDS");
+    const HvpWs o = hvp_ws(p, ws);
+    if (!ws || ws_bytes < o.bytes) return fail(PSVI_ENOSPC, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    float* x = nullptr;
+    if (p->family == PSVI_FAMILY_FULLCOV) {
+        x = (float*)ws;
+        // x = mean + L eps; x_dot = v_mean + (sigmoid(sd) v_sd) eps + v_corr eps
+        HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
+        HIP_TRY(launch_hvp_tangent(*p, params, vec, o.T, st));
+        HIP_TRY(launch_mvn_fwd(*p, eps, o.T, o.xd, st, true));
+    }
+    HIP_TRY(launch_net_rop(*p, u, z, w, x, o.xd, params, vec, eps, o.G, o.Gd,
+                           du_out ? o.du : nullptr, dw_out ? o.nlld : nullptr, st));
+    if (p->family == PSVI_FAMILY_FULLCOV)  // J^T G_dot (mean, sd, corr), no KL
+        HIP_TRY(launch_mvn_update(*p, eps, o.Gd, const_cast<float*>(params), nullptr, nullptr,
+                                  nullptr, nullptr, hv_out, 0, nullptr, nullptr, st));
+    HIP_TRY(launch_hvp_assemble(*p, params, vec, eps, o.G, o.Gd, o.du, o.nlld, hv_out, du_out,
+                                dw_out, st));
     return 0;
 }
 

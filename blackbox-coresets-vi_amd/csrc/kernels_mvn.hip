@@ -51,6 +51,7 @@ struct FwdArgs {
     float* part;      // split-K partial slots [n_items][S][32]
     int ldx, S;
     int64_t e_total;  // floats in eps (load guards)
+    int raw_diag;     // 1: the sd slots hold the diagonal itself (HVP tangent sample)
     int abl;                     // diagnostics ablation mask (0 in production):
                                  // 1 loads, 2 MFMAs, 4 x atomics
     unsigned long long* stamps;  // diagnostics: 16 slots per workgroup
@@ -220,7 +221,8 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
     if (s >= a.S || rr >= rb.R) return;
     const int n = a.lay[rb.layer].n, r = rb.r0 + rr;
     const float* mean = a.params + a.lay[rb.layer].poff;
-    float sum = mean[r] + softplus_f(mean[n + r]) * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
+    const float dg = a.raw_diag ? mean[n + r] : softplus_f(mean[n + r]);
+    float sum = mean[r] + dg * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
     const float* p = part + (size_t)rb.slot0 * a.S * kFwdRows + (size_t)s * kFwdRows + rr;
     const size_t st = (size_t)a.S * kFwdRows;
     // 4 independent loads in flight per thread; summation order k = 0, 1, ... kept per
@@ -881,8 +883,9 @@ hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, 
 }
 
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
-                          float* x_shard, hipStream_t st) {
+                          float* x_shard, hipStream_t st, bool raw_diag) {
     FwdArgs a{};
+    a.raw_diag = raw_diag ? 1 : 0;
     a.items = p.d_fwd;
     a.params = params;
     a.eps = eps;

@@ -261,7 +261,7 @@ hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
                             float* m, float* v, const psvi_adam_hp* hp, double* kl_out,
                             float* grad_out, int include_kl, hipStream_t st);
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
-                          float* x_shard, hipStream_t st);
+                          float* x_shard, hipStream_t st, bool raw_diag = false);
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
@@ -283,4 +283,16 @@ hipError_t launch_outer_combine(const psvi_plan& p, int n_pseudo, const float* p
 hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* params,
                                const float* sck, float* grad, const float* du_part,
                                float* grad_u, hipStream_t st);
+// Hessian-vector products (kernels_rop.hip)
+int rop_rows(const psvi_plan& p);
+hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,
+                              float* T, hipStream_t st);
+hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
+                          const float* x, const float* xd, const float* params, const float* vec,
+                          const float* eps, float* G, float* Gd, float* du, float* nlld,
+                          hipStream_t st);
+hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const float* vec,
+                               const float* eps, const float* G, const float* Gd, const float* du,
+                               const float* nlld, float* hv, float* d_u, float* d_w,
+                               hipStream_t st);
 }  // namespace psvi

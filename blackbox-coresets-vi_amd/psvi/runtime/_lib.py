@@ -29,6 +29,7 @@ Q_XRECV_COUNT = 9
 Q_LOOP_WS_BYTES = 10
 Q_TILED_FLOATS = 11
 Q_OUTER_WS_BYTES = 12
+Q_HVP_WS_BYTES = 13
 
 ERRORS = {-1: "PSVI_EINVAL", -2: "PSVI_ENOSPC", -3: "PSVI_EUNSUP", -4: "PSVI_ESTATE"}
 
@@ -84,6 +85,7 @@ SIGNATURES = {
                                ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
     "psvi_outer_elbo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _SZ, _P]),
+    "psvi_hvp": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),
     "psvi_adam_update": (_I32, [_I64, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P]),
     "psvi_debug_set": (_I32, [_I32, _I32]),

@@ -79,6 +79,7 @@ class InnerLoopPlan:
         self.loop_ws_bytes = q(_lib.Q_LOOP_WS_BYTES)
         self.tiled_floats = q(_lib.Q_TILED_FLOATS)  # 0: no tiled state for this plan
         self.outer_ws_bytes = q(_lib.Q_OUTER_WS_BYTES)
+        self.hvp_ws_bytes = q(_lib.Q_HVP_WS_BYTES)
         self.eps_stride = (self.eps_count + 3) // 4 * 4   # Philox offset per loop step
         self.n_tot = sum(i * o + o for i, o in layers)
 
@@ -207,6 +208,25 @@ class InnerLoopPlan:
             _ptr(out.get("grad_w")), _ptr(out.get("samples")), _ptr(ws), ws.numel(),
             _stream()), "psvi_outer_elbo_grad")
         return out
+
+    def hvp(self, u, z, w, eps, params, vec, mixed=True, out=None, ws=None):
+        """Hessian-vector product of the negative inner ELBO at fixed eps
+        (psvi_hvp).  Returns (hv, d_u, d_w): H vec and, with mixed=True, the
+        mixed products d/du and d/dw of vec . grad (else None, None)."""
+        self._inputs(u, z, w, eps)
+        _need(params, "params", self.param_count)
+        _need(vec, "vec", self.param_count)
+        dev = params.device
+        hv = torch.empty(self.param_count, dtype=torch.float32, device=dev) if out is None else out
+        _need(hv, "hv_out", self.param_count)
+        du = torch.empty(self.M, self.layers[0][0], dtype=torch.float32, device=dev) if mixed else None
+        dw = torch.empty(self.M, dtype=torch.float32, device=dev) if mixed else None
+        if ws is None or ws.numel() < self.hvp_ws_bytes:
+            ws = torch.empty(self.hvp_ws_bytes, dtype=torch.uint8, device=dev)
+        check(self.lib.psvi_hvp(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps), _ptr(params),
+                                _ptr(vec), _ptr(hv), _ptr(du), _ptr(dw), _ptr(ws), ws.numel(),
+                                _stream()), "psvi_hvp")
+        return hv, du, dw
 
     # ------------------------------------------------------------ phases
     def mf_accumulate(self, u, z, w, eps, params, acc, nll_out):

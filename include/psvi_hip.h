@@ -106,6 +106,7 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_TILED_FLOATS  11 /* floats of the tiled corr/m/v state (0: the plan has
                                    none -- it needs full-cov, world 1, S <= 128)      */
 #define PSVI_Q_OUTER_WS_BYTES 12 /* workspace bytes for psvi_outer_elbo_grad          */
+#define PSVI_Q_HVP_WS_BYTES  13 /* workspace bytes for psvi_hvp                       */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
  * Samples are split in contiguous blocks; for FULLCOV the rows of every
@@ -239,6 +240,24 @@ int psvi_outer_elbo_grad(const psvi_plan* plan, int32_t n_pseudo, const float* x
                          const float* params, double* loss_out, float* grad_params,
                          float* grad_u, float* grad_w, double* sample_out, void* ws,
                          size_t ws_bytes, void* stream);
+
+/* ---- second order (the `hyper` trainer's implicit hypergradient) ----------
+ * Hessian-vector product of the negative inner ELBO (psvi_inner_step's
+ * objective, KL included) at fixed eps, world == 1:
+ *   hv_out (PARAM_COUNT) <- H vec
+ *   du_out ([M][D], nullable) <- d/du (vec . d elbo / d params)
+ *   dw_out (M, nullable)      <- d/dw (vec . d elbo / d params)
+ * -- the products hypergrad's CG_normaleq takes from autograd through
+ * GradientDescent's fp_map (psvi/hypergrad/hypergradients.py:199-244, 300-311,
+ * diff_optimizers.py:51-60; PSVI.hyper_step psvi_classes.py:602-687):
+ * J^T x = x - lr H x, J x = x - lr H x (jvp), torch_grad(w_mapped, hparams, v)
+ * = -lr (du_out, dw_out chained to v).  Forward-over-reverse (R-op) through
+ * the per-sample network, one workgroup per sample (the model's per-sample
+ * weights and row chunks in LDS; PSVI_EUNSUP when they do not fit).
+ * ws: PSVI_Q_HVP_WS_BYTES. */
+int psvi_hvp(const psvi_plan* plan, const float* u, const int32_t* z, const float* w,
+             const float* eps, const float* params, const float* vec, float* hv_out,
+             float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] ~ N(0,1), Philox4x32-10 counter (seed, offset + i) + Box-Muller.

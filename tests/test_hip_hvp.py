@@ -1,0 +1,69 @@
+"""Hessian-vector products on the HIP path (psvi_hvp through the C ABI) vs the
+reference's own double backward (tests/golden/h*.npz) and vs the float64
+R-op oracle at full size.  Tolerance: 1e-4 relative (l2), as the north star's
+gradient bar; HIP fp32 vs float64."""
+import numpy as np
+import pytest
+import torch
+
+import psvi_oracle as O
+from golden_util import family_of, fixture_names, l2rel, load_fixture
+from test_oracle_hyper import softmax_T
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(x, dtype=torch.float32):
+    return torch.tensor(np.ascontiguousarray(x), dtype=dtype, device=DEV)
+
+
+def _hvp(family, layers, S, u, z, w, eps, params, vec):
+    from psvi.runtime import InnerLoopPlan
+
+    plan = InnerLoopPlan(family, layers, S, u.shape[0])
+    hv, du, dw = plan.hvp(_t(u), _t(z.astype(np.int32), torch.int32), _t(w), _t(eps),
+                          _t(params), _t(vec))
+    torch.cuda.synchronize()
+    return hv.cpu().numpy(), du.cpu().numpy(), dw.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", fixture_names("h"))
+def test_hvp_matches_reference_double_backward(name):
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    hv, du, dw = _hvp(family_of(cfg), cfg["layers"], cfg["S"], f["u"], f["z"], f["w"], f["eps"],
+                      f["params0"], f["vec"])
+    assert l2rel(hv, f["hv"]) < 1e-4, l2rel(hv, f["hv"])
+    assert l2rel(du, f["d_u"]) < 1e-4, l2rel(du, f["d_u"])
+    assert l2rel(softmax_T(f["v"].astype(np.float64), dw.astype(np.float64), cfg["N"]),
+                 f["d_v"]) < 1e-4
+
+
+@pytest.mark.parametrize("case", [
+    ("fullcov", [(64, 40), (40, 40), (40, 2)], 128, 100),   # C3
+    ("meanfield", [(2, 100), (100, 4)], 32, 50),            # C2
+    ("meanfield", [(5, 7), (7, 7), (7, 3)], 6, 70),         # row chunks
+])
+def test_hvp_fullsize_vs_oracle(case):
+    family, layers, S, M = case
+    rng = np.random.default_rng(S + M)
+    fam = "mf" if family == "meanfield" else "mvn"
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        parts += [0.15 * rng.standard_normal(n), rng.uniform(-5, -4, n)]
+        if fam == "mvn":
+            parts += [2e-4 * rng.standard_normal((n - 1) * (n - 2) // 2)]
+    params = np.concatenate(parts).astype(np.float32)
+    eps_n = sum(S * (i * o + o) for i, o in layers)
+    eps = rng.standard_normal(eps_n).astype(np.float32)
+    u = rng.standard_normal((M, layers[0][0])).astype(np.float32)
+    z = rng.integers(0, layers[-1][1], M)
+    w = O.coreset_weights(0.2 * rng.standard_normal(M), 800, "softmax").astype(np.float32)
+    vec = rng.standard_normal(params.size).astype(np.float32)
+    hv, du, dw = _hvp(family, layers, S, u, z, w, eps, params, vec)
+    _, _, hv_o, du_o, dw_o = O.inner_hvp(fam, layers, params, u, z, w, eps, S, vec)
+    assert l2rel(hv, hv_o) < 1e-4, l2rel(hv, hv_o)
+    assert l2rel(du, du_o) < 1e-4, l2rel(du, du_o)
+    assert l2rel(dw, dw_o) < 1e-4, l2rel(dw, dw_o)
