@@ -26,9 +26,17 @@ What runs where
     N f(v) -- to v and alpha.  ``joint_step`` / ``alternating_step``
     (517-539) run on it unchanged.
 
-Not on the HIP path: everything that differentiates
-*through* the inner loop (the nested unroll, CG hypergradients), evaluation
-and data plumbing.  Those entry points raise NotImplementedError instead of
+  * ``PSVI.hyper_step`` (psvi_classes.py:602-687): the T-step first-order inner
+    loop (hypergrad Adam, ``psvi_inner_loop``), then hypergrad's
+    ``CG_normaleq`` (hypergradients.py:199-244) on Hessian-vector products of
+    the inner objective (``psvi_hvp``: J^T x and the jvp J x of
+    GradientDescent's fp_map are x - lr H x), the mixed products for the
+    hypergradient of u and v, and the outer objective's direct gradients;
+    then the u / v Adam steps.  The CG vectors are float64 device tensors.
+
+Not on the HIP path: the nested trainer's unrolled
+second-order graph (reverse through T Adam steps), evaluation and data
+plumbing.  Those entry points raise NotImplementedError instead of
 silently running elsewhere, and ``inner_elbo`` treats u and v as constants (no
 gradient flows to them).
 
@@ -44,8 +52,9 @@ from ..runtime import InnerLoopPlan, randn_
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
            "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
 
-_OUTER = ("is differentiated through the inner loop (second order); that is the next "
-          "row of the hot-path scope (SURVEY.md 8(f)), not part of the HIP inner loop")
+_OUTER = ("differentiates through the unrolled inner loop (reverse through T Adam steps); "
+          "that is the next row of the hot-path scope (SURVEY.md 8(f)); trainer 'hyper' "
+          "(implicit hypergradient) runs on HIP")
 
 
 class HipInnerELBO(torch.autograd.Function):
@@ -156,7 +165,7 @@ class PSVI:
     def _draw_eps(self, plan):
         eps = torch.empty(plan.eps_count, device=self.device)
         randn_(eps, self.seed, self._eps_offset)
-        self._eps_offset += plan.eps_count
+        self._eps_offset += plan.eps_stride  # Philox offsets move in quads
         return eps
 
     # ---------------------------------------------------------- objectives
@@ -203,7 +212,7 @@ class PSVI:
         for t in range(T):
             if eps is None:
                 randn_(step_eps, self.seed, self._eps_offset)
-                self._eps_offset += plan.eps_count
+                self._eps_offset += plan.eps_stride
                 e = step_eps
             else:
                 e = eps[t]
@@ -257,7 +266,7 @@ class PSVI:
         return loss
 
     def setup_optimizers(self, lr0net=1e-3, lr0u=1e-3, lr0v=1e-2, lr0joint=1e-3,
-                         trainer="nested"):
+                         trainer="hyper"):
         """The optimisers run_psvi creates (psvi_classes.py:867-885): Adam on
         the network, on u, on v (learn_v), and for trainer 'joint' one Adam
         over all of them."""
@@ -297,12 +306,148 @@ class PSVI:
             self.optim.step()
         return loss
 
-    # -------------------------------------------- second order (not here)
+    # ------------------------------------------------------- second order
+    def _outer_plan(self, model, Nx):
+        fam, layers, prior_sd, S = model_spec(model)
+        Mu = int(self.u.shape[0])
+        key = ("outer", fam, tuple(layers), S, Mu + Nx, prior_sd)
+        if key not in self._plans:
+            self._plans[key] = InnerLoopPlan(fam, layers, S, Mu + Nx, prior_sd=prior_sd)
+        return self._plans[key]
+
+    def _chain_w(self, dw):
+        """d/dv of a linear function of w = N f(v) with coefficients dw."""
+        with torch.enable_grad():
+            wp = self.N * self.f(self.v, 0)
+            (gv,) = torch.autograd.grad(wp, self.v, grad_outputs=dw.to(wp.dtype).reshape(wp.shape))
+        return gv
+
+    def hyper_step(self, xbatch, ybatch, T=50, inner_opt_class=None, K=30, linsys_lr=1e-4,
+                   hypergrad_approx="CG_normaleq", eps_inner=None, eps_outer=None, **kwargs):
+        """psvi_classes.py:602-687 with hypergrad's CG_normaleq
+        (hypergradients.py:199-244, CG_torch.py:9-45): T = self.inner_it
+        first-order inner steps (hypergrad adam_step, step count 1..T) from the
+        model's parameters, then the implicit hypergradient of u (and v) from
+        K conjugate-gradient iterations on the normal equations of
+        fp_map(p) = p - linsys_lr * grad_p inner, the u / v Adam steps, and
+        the outer loss at the new (u, v) -- returned as a float; the final
+        parameters are written into the model.  ``eps_inner`` /
+        ``eps_outer``: optional sequences of draws (library eps layout) in the
+        reference's call order, to replay; default: this instance's Philox
+        stream."""
+        if hypergrad_approx != "CG_normaleq":
+            raise NotImplementedError(f"hypergrad_approx={hypergrad_approx!r}: only "
+                                      "CG_normaleq (the reference default) runs on HIP")
+        if self.learn_z:
+            raise NotImplementedError  # as the reference (psvi_classes.py:619-620)
+        T = self.inner_it
+        lr_net = self.optim_net.param_groups[0]["lr"]
+        model = self.model
+        self.optim_u.zero_grad()
+        if self.learn_v:
+            self.optim_v.zero_grad()
+        plan = self._plan(model)
+        u, z, w = self._data(plan)
+        it_in = iter(eps_inner) if eps_inner is not None else None
+        it_out = iter(eps_outer) if eps_outer is not None else None
+
+        def draw_inner():
+            return next(it_in) if it_in is not None else self._draw_eps(plan)
+
+        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
+        Nx = int(xb.shape[0])
+        oplan = self._outer_plan(model, Nx)
+
+        def draw_outer():
+            return next(it_out) if it_out is not None else self._draw_eps(oplan)
+
+        # 1. the inner problem: T first-order steps (trainer hyper: hypergrad adam_step)
+        plist = list(model.parameters())
+        with torch.no_grad():
+            params = nn.utils.parameters_to_vector(plist).detach().to(torch.float32).clone()
+        m = torch.zeros_like(params)
+        v2 = torch.zeros_like(params)
+        if it_in is None:  # fused loop on this instance's Philox stream
+            plan.inner_loop(u, z, w, params, m, v2, T, lr_net, kind="hypergrad", seed=self.seed,
+                            offset=self._eps_offset)
+            self._eps_offset += T * plan.eps_stride
+        else:
+            ws = plan.workspace(params.device)
+            for t in range(T):
+                plan.inner_step(u, z, w, draw_inner(), params, m, v2, step=t + 1, lr=lr_net,
+                                kind="hypergrad", ws=ws)
+        # 2. CG_normaleq
+        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1),
+                           ybatch.detach().to(self.device).reshape(-1)]).to(torch.int32)
+        w_data = torch.full((Nx,), float(self.N) / max(Nx, 1), device=self.device)
+
+        def outer(uu, ww, eps, grads=True):
+            x_all = torch.cat([uu.detach().reshape(uu.shape[0], -1), xb]).contiguous()
+            w_all = torch.cat([ww.detach().to(torch.float32), w_data]).contiguous()
+            return oplan.outer_elbo_grad(int(uu.shape[0]), x_all, z_all.contiguous(), w_all, eps,
+                                         params, grad=grads, grad_u=grads, grad_w=grads)
+
+        o = outer(u, w, draw_outer())
+        g_w = o["grad"].to(torch.float64)
+        lr = float(linsys_lr)
+        hws = torch.empty(plan.hvp_ws_bytes, dtype=torch.uint8, device=params.device)
+
+        def hvp(e, x, mixed=False):
+            hv, du, dw = plan.hvp(u, z, w, e, params, x.to(torch.float32).contiguous(),
+                                  mixed=mixed, ws=hws)
+            return hv.to(torch.float64), du, dw
+
+        eA = draw_inner()                       # w_mapped = fp_map(params, hparams)
+
+        def jvp(x):                             # J x = x - lr H x (fp_map drawn twice)
+            draw_inner()
+            return x - lr * hvp(draw_inner(), x)[0]
+
+        def A(x):                               # dfp_map_dw
+            vmj = lr * hvp(eA, x)[0]
+            return vmj - jvp(vmj)
+
+        b = g_w - jvp(g_w)
+        xk = torch.zeros_like(b)
+        r = b.clone()
+        pk = r.clone()
+        for _ in range(int(K)):                 # CG_torch.cg(Ax, b, max_iter=K, epsilon=1e-10)
+            Ap = A(pk)
+            rTr = torch.dot(r, r)
+            alpha = rTr / torch.dot(pk, Ap)
+            xn = xk + alpha * pk
+            rn = r - alpha * Ap
+            if float(torch.linalg.vector_norm(rn)) < 1e-10:
+                break
+            beta = torch.dot(rn, rn) / rTr
+            pk = rn + beta * pk
+            xk, r = xn, rn
+        _, du, dw = hvp(eA, xk, mixed=True)     # torch_grad(w_mapped, hparams, vs)
+        u_grad = (-lr * du.to(torch.float64) + o["grad_u"].to(torch.float64)).to(self.u.dtype)
+        if self.u.grad is None:
+            self.u.grad = torch.zeros_like(self.u)
+        self.u.grad += u_grad.reshape(self.u.shape)
+        if self.learn_v:
+            dwt = (-lr * dw.to(torch.float64) + o["grad_w"].to(torch.float64))
+            v_grad = self._chain_w(dwt)
+            if self.v.grad is None:
+                self.v.grad = torch.zeros_like(self.v)
+            self.v.grad += v_grad
+        self.optim_u.step()
+        if self.learn_v:
+            self.optim_v.step()
+            if not getattr(self, "parameterised", False):
+                with torch.no_grad():
+                    torch.clamp_(self.v, min=0.0)
+        # 3. the outer loss at the new (u, v), and the inner solution into the model
+        u2, _, w2 = self._data(plan)
+        ll = outer(u2, w2, draw_outer(), grads=False)["loss"]
+        with torch.no_grad():
+            nn.utils.vector_to_parameters(params.to(plist[0].dtype), plist)
+        return float(ll.item())
+
     def nested_step(self, xbatch, ybatch, truncated=False, K=5):
         raise NotImplementedError("nested_step " + _OUTER)
-
-    def hyper_step(self, xbatch, ybatch, **kwargs):
-        raise NotImplementedError("hyper_step " + _OUTER)
 
     def run_psvi(self, *args, **kwargs):
         raise NotImplementedError("run_psvi drives the outer loop, which " + _OUTER)

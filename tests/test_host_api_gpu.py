@@ -134,3 +134,58 @@ def test_alternating_step_moves_network_then_u():
     assert [e[0] for e in ps.elbos[-2:]] == [0, 1]
     assert not torch.equal(torch.nn.utils.parameters_to_vector(model.parameters()).detach(), p0)
     assert not torch.equal(ps.u.detach(), u0)
+
+
+# ----------------------------------------------------------- trainer hyper
+@pytest.mark.parametrize("name", fixture_names("y"))
+def test_hyper_step_matches_reference(name):
+    """One whole PSVI.hyper_step (inner loop, CG_normaleq on psvi_hvp, u / v
+    Adam steps, returned outer loss) replaying the reference's draws."""
+    from golden_util import load_fixture
+    from psvi.inference import PSVILearnV
+    from test_host_api import build_model
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    model = build_model(cfg, f["params0"]).cuda()
+    u = torch.tensor(f["u0"], device="cuda").requires_grad_(True)
+    z = torch.tensor(f["z"], device="cuda")
+    ps = PSVILearnV(u=u, z=z, N=cfg["N"], model=model, mc_samples=cfg["S"], device_id=0,
+                    inner_it=cfg["T"])
+    ps.device = torch.device("cuda")
+    ps.v = torch.tensor(f["v0"], device="cuda").requires_grad_(True)
+    ps.setup_optimizers(lr0net=cfg["lr0net"], lr0u=cfg["lr0u"], lr0v=cfg["lr0v"])
+    ei = [torch.tensor(e, device="cuda") for e in f["eps_inner"]]
+    eo = [torch.tensor(e, device="cuda") for e in f["eps_outer"]]
+    ll = ps.hyper_step(torch.tensor(f["xb"], device="cuda"), torch.tensor(f["yb"], device="cuda"),
+                       K=cfg["K"], linsys_lr=cfg["linsys_lr"], eps_inner=ei, eps_outer=eo)
+    p = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
+    assert l2rel(p, f["params"]) < 1e-5
+    ug, vg = ps.u.grad.cpu().numpy(), ps.v.grad.cpu().numpy()
+    print(f"{name}: u_grad l2rel {l2rel(ug, f['u_grad']):.2e}, v_grad {l2rel(vg, f['v_grad']):.2e}, "
+          f"ll rel {rel(ll, f['ll']):.2e}")
+    assert l2rel(ug, f["u_grad"]) < 1e-4
+    assert l2rel(vg, f["v_grad"]) < 1e-4
+    # first Adam step of u / v: -lr sign(grad) wherever the gradient is not rounding noise
+    for got, want, g, lr in ((ps.u, f["u"], f["u_grad"], cfg["lr0u"]),
+                             (ps.v, f["v"], f["v_grad"], cfg["lr0v"])):
+        big = np.abs(g) > 1e-3 * np.abs(g).max()
+        assert np.abs(got.detach().cpu().numpy() - want)[big].max() < 1e-3 * lr
+    assert rel(ll, f["ll"]) < 1e-5
+
+
+def test_hyper_step_philox_runs():
+    from psvi.inference import PSVILearnV
+    from psvi.models import make_fc2net
+
+    torch.manual_seed(0)
+    model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2).cuda()
+    u = torch.randn(10, 8, device="cuda").requires_grad_(True)
+    z = (torch.arange(10, device="cuda") % 3).float()
+    ps = PSVILearnV(u=u, z=z, N=800, model=model, mc_samples=16, device_id=0, inner_it=4)
+    ps.device = torch.device("cuda")
+    ps.setup_optimizers()
+    xb, yb = torch.randn(16, 8, device="cuda"), (torch.arange(16, device="cuda") % 3).float()
+    l1 = ps.hyper_step(xb, yb, K=3)
+    l2 = ps.hyper_step(xb, yb, K=3)
+    assert np.isfinite(l1) and np.isfinite(l2) and l1 != l2
