@@ -679,3 +679,69 @@ def hyper_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer
     ww2 = np.concatenate([wts(v_new), np.full(Nx, N / Nx)])
     ll = outer_elbo_grad(family, layers, p, X2, zz, ww2, M, eps_outer[1], S, prior_sd)[0]
     return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, ll=ll)
+
+
+def adam_higher_adjoint(lt, lm, lv, m, v, g, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
+    """Reverse of one robust_higher DifferentiableAdam step (optim.py:318-367)
+        m' = b1 m + (1-b1) g,  v' = b2 v + (1-b2) g^2,
+        p' = p - (lr/bc1) m' / (sqrt(v' + 1e-8)/sqrt(bc2) + eps):
+    given the adjoints (lt, lm, lv) of (p', m', v') and the step's (m', v', g),
+    returns (adjoint of g, adjoint of m, adjoint of v); p's adjoint is lt
+    plus H^T (adjoint of g)."""
+    bc1, bc2 = 1.0 - beta1 ** t, 1.0 - beta2 ** t
+    c = lr / bc1
+    sq = np.sqrt(v + 1e-8)
+    D = sq / np.sqrt(bc2) + eps
+    lm2 = lm - lt * c / D
+    lv2 = lv + lt * c * m / (D * D) / (2.0 * sq * np.sqrt(bc2))
+    lg = lm2 * (1.0 - beta1) + lv2 * 2.0 * (1.0 - beta2) * g
+    return lg, beta1 * lm2, beta2 * lv2
+
+
+def nested_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer, S, T,
+                lr0net, lr0u, lr0v, prior_sd=1.0):
+    """PSVI.nested_step (psvi_classes.py:541-600), PSVILearnV (f = softmax, v not
+    clamped): T higher-Adam steps from params0 with fresh state, the outer
+    objective at the result, its gradient w.r.t. u and v back through the
+    unrolled steps (reverse-mode through Adam, one Hessian-vector product and
+    mixed product per step), then the u / v Adam steps.
+    Returns dict(params, u, v, u_grad, v_grad, loss)."""
+    u = np.asarray(u, np.float64)
+    v = np.asarray(v, np.float64)
+    M = u.shape[0]
+    Nx = xb.shape[0]
+    w = coreset_weights(v, N, "softmax")
+
+    def softmax_T(dw):
+        e = np.exp(v - v.max())
+        sm = e / e.sum()
+        gs = N * dw
+        return sm * (gs - (gs * sm).sum())
+
+    f = mf_elbo_grad if family == "mf" else mvn_elbo_grad
+    p = np.asarray(params0, np.float64).copy()
+    m = np.zeros_like(p)
+    vv = np.zeros_like(p)
+    hist = []
+    for t in range(T):
+        _, g = f(layers, p, u, z, w, eps_inner[t], S, prior_sd)
+        pn, m, vv = adam_higher(p, g, m, vv, t + 1, lr0net)
+        hist.append((p, m.copy(), vv.copy(), g))
+        p = pn
+    X = np.concatenate([u, xb])
+    zz = np.concatenate([z, yb])
+    ww = np.concatenate([w, np.full(Nx, N / Nx)])
+    loss, lt, gu, gw = outer_elbo_grad(family, layers, p, X, zz, ww, M, eps_outer[0], S, prior_sd)
+    lm = np.zeros_like(p)
+    lv = np.zeros_like(p)
+    for t in range(T - 1, -1, -1):
+        pt, mt, vt, gt = hist[t]
+        lg, lm, lv = adam_higher_adjoint(lt, lm, lv, mt, vt, gt, t + 1, lr0net)
+        _, _, hv, du, dw = inner_hvp(family, layers, pt, u, z, w, eps_inner[t], S, lg, prior_sd)
+        lt = lt + hv
+        gu = gu + du
+        gw = gw + dw
+    u_grad, v_grad = gu, softmax_T(gw)
+    u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
+    v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
+    return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, loss=loss)

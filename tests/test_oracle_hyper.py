@@ -48,3 +48,17 @@ def test_hyper_step_oracle_matches_reference(name):
     assert l2rel(out["v_grad"], f["v_grad"]) < 1e-7
     assert l2rel(out["u"], f["u"]) < 1e-9 and l2rel(out["v"], f["v"]) < 1e-9
     assert rel(out["ll"], f["ll"]) < 1e-9
+
+
+@pytest.mark.parametrize("name", fixture_names("n"))
+def test_nested_step_oracle_matches_reference(name):
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    out = O.nested_step(cfg["family"], cfg["layers"], f["params0"], f["u0"], f["z"], f["v0"],
+                        cfg["N"], f["xb"], f["yb"], f["eps_inner"], f["eps_outer"], cfg["S"],
+                        cfg["T"], cfg["lr0net"], cfg["lr0u"], cfg["lr0v"])
+    assert rel(out["loss"], f["loss"]) < 1e-10
+    assert l2rel(out["params"], f["params"]) < 1e-10
+    assert l2rel(out["u_grad"], f["u_grad"]) < 1e-8, l2rel(out["u_grad"], f["u_grad"])
+    assert l2rel(out["v_grad"], f["v_grad"]) < 1e-8
+    assert l2rel(out["u"], f["u"]) < 1e-10 and l2rel(out["v"], f["v"]) < 1e-10

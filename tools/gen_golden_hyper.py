@@ -15,6 +15,9 @@ the child records
         ds / d params (= H vec), ds / d u, ds / d v
     with inner_elbo(model=fmodel, params=p, hyperopt=True) on a
     monkeypatch'ed model (psvi_classes.py:602-650);
+  * n*.npz -- one full PSVI.nested_step (psvi_classes.py:541-600): T higher-Adam
+    steps in innerloop_ctx, psvi_elbo.backward() through the unroll, the u / v
+    Adam steps, with every draw;
   * y*.npz -- one full PSVI.hyper_step (psvi_classes.py:602-687): the T-step
     first-order inner loop (hypergrad DifferentiableAdam), CG_normaleq with K
     iterations, the u / v Adam steps, the returned outer loss -- and every
@@ -179,6 +182,58 @@ def _child():
             params=parameters_to_vector(model.parameters()).detach().numpy())
         print(f"wrote {name}: calls={len(calls)} ll={float(ll):.6f} eps sizes={ne}")
 
+    def run_nested_step(name, family, model, M, Nx, D, C, S, N, seed, T, note=""):
+        """PSVI.nested_step (psvi_classes.py:541-600): T higher-Adam steps on
+        inner_elbo in innerloop_ctx, psvi_elbo.backward() through the unroll,
+        then the u / v Adam steps; fmodel's parameters copied into the model."""
+        torch.manual_seed(seed)
+        obj = make_obj(model, M, D, C, S, N)
+        obj.inner_it, obj.register_elbos, obj.log_every = T, False, 10
+        obj.scheduler_optim_net = None
+        lr0net, lr0u, lr0v = 1e-3, 1e-3, 1e-2
+        obj.optim_net = torch.optim.Adam(list(model.parameters()), lr0net)
+        obj.optim_u = torch.optim.Adam([obj.u], lr0u)
+        obj.optim_v = torch.optim.Adam([obj.v], lr0v)
+        xb = torch.randn(Nx, D, generator=gen).float().double()
+        yb = torch.randint(0, C, (Nx,), generator=gen).double()
+        p0 = parameters_to_vector(model.parameters()).detach().clone()
+        u0, v0 = obj.u.detach().clone(), obj.v.detach().clone()
+        draws.clear()
+        sizes, n_prev = [], [0]
+        orig_inner, orig_outer = obj.inner_elbo, obj.psvi_elbo
+
+        def inner(*a, **k):
+            r = orig_inner(*a, **k)
+            sizes.append(len(draws) - n_prev[0])
+            n_prev[0] = len(draws)
+            return r
+
+        def outer(*a, **k):
+            r = orig_outer(*a, **k)
+            sizes.append(len(draws) - n_prev[0])
+            n_prev[0] = len(draws)
+            return r
+
+        obj.inner_elbo, obj.psvi_elbo = inner, outer
+        loss = obj.nested_step(xb, yb)
+        cuts = np.cumsum([0] + sizes)
+        eps = [torch.cat(draws[cuts[i]:cuts[i + 1]]).numpy().astype(np.float32)
+               for i in range(len(sizes))]
+        np.savez_compressed(
+            os.path.join(OUT, name + ".npz"),
+            config=np.array(json.dumps(cfg_of(family, model, S, M, N, Nx=Nx, T=T,
+                                              lr0net=lr0net, lr0u=lr0u, lr0v=lr0v, seed=seed,
+                                              note=note))),
+            params0=p0.numpy().astype(np.float32), u0=u0.numpy().astype(np.float32),
+            v0=v0.numpy().astype(np.float32), z=obj.z.numpy().astype(np.float32),
+            xb=xb.numpy().astype(np.float32), yb=yb.numpy().astype(np.float32),
+            eps_inner=np.stack(eps[:T]), eps_outer=eps[T][None],
+            loss=np.array(float(loss.detach())),
+            u=obj.u.detach().numpy(), v=obj.v.detach().numpy(),
+            u_grad=obj.u.grad.numpy(), v_grad=obj.v.grad.numpy(),
+            params=parameters_to_vector(model.parameters()).detach().numpy())
+        print(f"wrote {name}: calls={len(sizes)} loss={float(loss):.6f}")
+
     # HVP fixtures
     model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
     perturb(model, 0.3, -3.5, -2.5, 0.002)
@@ -206,6 +261,20 @@ def _child():
     perturb(model, 0.4, -3.0, -1.0, 0.0)
     run_hyper_step("y2_fn_deep", "mf", model, M=13, Nx=9, D=5, C=3, S=6, N=500, seed=22,
                    T=3, K=4)
+
+    # one whole nested_step each (the reference's default trainer)
+    model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
+    perturb(model, 0.3, -3.5, -2.5, 0.002)
+    run_nested_step("n1_fn2_tiny", "mvn", model, M=10, Nx=12, D=8, C=3, S=16, N=800, seed=31,
+                    T=4)
+
+    model = make_fcnet(5, 7, 3, n_layers=2, mc_samples=6, init_sd=0.05)
+    perturb(model, 0.4, -3.0, -1.0, 0.0)
+    run_nested_step("n2_fn_deep", "mf", model, M=13, Nx=9, D=5, C=3, S=6, N=500, seed=32, T=4)
+
+    model = nn.Sequential(VILinear(2, 2, init_sd=0.1, mc_samples=4))
+    perturb(model, 0.5, -3.0, 0.5, 0.0)
+    run_nested_step("n3_logreg", "mf", model, M=10, Nx=16, D=2, C=2, S=4, N=800, seed=33, T=5)
 
 
 def main():
