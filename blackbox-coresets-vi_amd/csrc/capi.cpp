@@ -829,6 +829,17 @@ int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* 
     return 0;
 }
 
+int psvi_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const float* adam_m,
+                      const float* adam_v, const float* grad, float* lg_out,
+                      const psvi_adam_hp* hp, void* stream) {
+    if (n < 0 || !lt || !lm || !lv || !adam_m || !adam_v || !grad || !lg_out || !hp)
+        return fail(PSVI_EINVAL, "bad adam adjoint arguments");
+    if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    HIP_TRY(launch_adam_adjoint(n, lt, lm, lv, adam_m, adam_v, grad, lg_out, hp,
+                                as_stream(stream)));
+    return 0;
+}
+
 int psvi_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, void* stream) {
     if (!out || n < 0) return fail(PSVI_EINVAL, "bad randn arguments");
     if (offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");

@@ -91,6 +91,46 @@ __global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
     }
 }
 
+// Reverse of one Adam step (nested trainer: reverse-mode through the unrolled
+// inner loop, psvi_classes.py:549-560 differentiated by psvi_elbo.backward()).
+// Forward (either variant, adam_apply):  m' = b1 m + (1-b1) g,
+//   higher:    v' = b2 v + (1-b2) g^2,          p' = p - lr/bc1 m' / (sqrt(v'+1e-8)/sqrt(bc2) + eps)
+//   hypergrad: v' = b2 v + (1-b2) g^2 + 1e-12,  p' = p - lr (m'/bc1) / (sqrt(v'/bc2) + eps)
+// Given the adjoints lt, lm, lv of (p', m', v') and the step's m', v', g:
+//   lg <- adjoint of g;  lm <- adjoint of m;  lv <- adjoint of v
+// (p's adjoint is lt + H^T lg: psvi_hvp).
+__global__ __launch_bounds__(256) void adam_adjoint_kernel(int64_t n, const float* lt, float* lm,
+                                                           float* lv, const float* m,
+                                                           const float* v, const float* g,
+                                                           float* lg, AdamC a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float mm = m[i], vv = v[i], t = lt[i];
+    float dm, dv;
+    if (a.kind == PSVI_ADAM_HIGHER) {
+        const float sq = sqrtf(vv + 1e-8f), D = sq * a.inv_sqrt_bc2 + a.eps;
+        dm = -t * a.lr_bc1 / D;
+        dv = t * a.lr_bc1 * mm / (D * D) * (0.5f * a.inv_sqrt_bc2 / sq);
+    } else {
+        const float q = sqrtf(vv * a.inv_bc2), D = q + a.eps;
+        dm = -t * a.lr * a.inv_bc1 / D;
+        dv = t * a.lr * mm * a.inv_bc1 / (D * D) * (0.5f * a.inv_bc2 / fmaxf(q, 1e-30f));
+    }
+    const float lm2 = lm[i] + dm, lv2 = lv[i] + dv;
+    lg[i] = lm2 * a.omb1 + lv2 * 2.f * a.omb2 * g[i];
+    lm[i] = a.b1 * lm2;
+    lv[i] = a.b2 * lv2;
+}
+
+hipError_t launch_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const float* m,
+                               const float* v, const float* g, float* lg,
+                               const psvi_adam_hp* hp, hipStream_t st) {
+    const AdamC a = make_adam(hp);
+    hipLaunchKernelGGL(adam_adjoint_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                       lt, lm, lv, m, v, g, lg, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params, float* m,
                             float* v, const psvi_adam_hp* hp, double* kl_out,
                             float* grad_out, int include_kl, hipStream_t st) {

@@ -273,6 +273,9 @@ hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, h
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);
 AdamC make_adam(const psvi_adam_hp* hp);
+hipError_t launch_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const float* m,
+                               const float* v, const float* g, float* lg,
+                               const psvi_adam_hp* hp, hipStream_t st);
 // outer objective (kernels_outer.hip)
 hipError_t launch_outer_stats(const psvi_plan& p, const float* params, const float* eps,
                               const float* x, double* stats, hipStream_t st);

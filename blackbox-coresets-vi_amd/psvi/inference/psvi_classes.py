@@ -34,9 +34,14 @@ What runs where
     hypergradient of u and v, and the outer objective's direct gradients;
     then the u / v Adam steps.  The CG vectors are float64 device tensors.
 
-Not on the HIP path: the nested trainer's unrolled
-second-order graph (reverse through T Adam steps), evaluation and data
-plumbing.  Those entry points raise NotImplementedError instead of
+  * ``PSVI.nested_step`` (psvi_classes.py:541-600, the reference's default
+    trainer): T higher-Adam steps (``psvi_elbo_grad`` + ``psvi_adam_update``,
+    the trajectory kept on the device), the outer objective at the result,
+    and ``psvi_elbo.backward()`` through the unroll as reverse mode: per step
+    back, ``psvi_adam_adjoint`` and one ``psvi_hvp`` with its mixed products;
+    then the u / v Adam steps.
+
+Not on the HIP path: evaluation and data plumbing.  Those entry points raise NotImplementedError instead of
 silently running elsewhere, and ``inner_elbo`` treats u and v as constants (no
 gradient flows to them).
 
@@ -47,7 +52,7 @@ import torch.nn as nn
 from torch.autograd.function import once_differentiable
 
 from ..models.neural_net import categorical_fn, model_spec
-from ..runtime import InnerLoopPlan, randn_
+from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
            "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
@@ -446,8 +451,92 @@ class PSVI:
             nn.utils.vector_to_parameters(params.to(plist[0].dtype), plist)
         return float(ll.item())
 
-    def nested_step(self, xbatch, ybatch, truncated=False, K=5):
-        raise NotImplementedError("nested_step " + _OUTER)
+    def nested_step(self, xbatch, ybatch, truncated=False, K=5, eps_inner=None, eps_outer=None):
+        """psvi_classes.py:541-600: T = self.inner_it higher-Adam steps on the
+        inner objective from the model's parameters with a fresh Adam state,
+        the outer objective at the result, its gradient w.r.t. u (and v)
+        through the unrolled steps, the u / v Adam steps; the final parameters
+        are written into the model.  Returns the outer loss (0-dim tensor).
+        ``eps_inner`` (T draws) / ``eps_outer`` (1): optional replay of the
+        reference's draws; default this instance's Philox stream."""
+        if truncated:
+            raise NotImplementedError("truncated nested_step (torch.optim.Adam warm start) is "
+                                      "not on the HIP path")
+        if self.learn_z:
+            raise NotImplementedError("soft labels (learn_z) are not on the HIP path")
+        self.optim_u.zero_grad()
+        self.optim_net.zero_grad()
+        if self.learn_v:
+            self.optim_v.zero_grad()
+        model = self.model
+        T = int(self.inner_it)
+        lr_net = self.optim_net.param_groups[0]["lr"]
+        plan = self._plan(model)
+        u, z, w = self._data(plan)
+        it_in = iter(eps_inner) if eps_inner is not None else None
+        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
+        Nx = int(xb.shape[0])
+        oplan = self._outer_plan(model, Nx)
+        plist = list(model.parameters())
+        with torch.no_grad():
+            p = nn.utils.parameters_to_vector(plist).detach().to(torch.float32).clone()
+        m = torch.zeros_like(p)
+        v2 = torch.zeros_like(p)
+        ws = plan.workspace(p.device)
+        hist, elbos = [], []
+        # forward: the unrolled inner loop, trajectory kept for the reverse pass
+        for t in range(T):
+            e = next(it_in) if it_in is not None else self._draw_eps(plan)
+            elbo, g = plan.elbo_grad(u, z, w, e, p, ws=ws)
+            p_prev = p.clone()
+            adam_update_(p, g, m, v2, t + 1, lr_net, kind="higher")
+            hist.append((p_prev, m.clone(), v2.clone(), g, e))
+            elbos.append(elbo)
+        # the outer objective at the inner solution, and its direct gradients
+        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1),
+                           ybatch.detach().to(self.device).reshape(-1)]).to(torch.int32)
+        w_data = torch.full((Nx,), float(self.N) / max(Nx, 1), device=self.device)
+        eo = next(iter(eps_outer)) if eps_outer is not None else self._draw_eps(oplan)
+        x_all = torch.cat([u, xb]).contiguous()
+        w_all = torch.cat([w, w_data]).contiguous()
+        o = oplan.outer_elbo_grad(int(u.shape[0]), x_all, z_all.contiguous(), w_all, eo, p)
+        if self.register_elbos:
+            host = torch.cat(elbos).cpu()
+            for t in range(0, T, self.log_every):
+                self.elbos.append((1, -float(host[t])))
+            self.elbos.append((0, -float(o["loss"].item())))
+        # reverse mode through the T Adam steps
+        lt = o["grad"].clone()
+        lm = torch.zeros_like(p)
+        lv = torch.zeros_like(p)
+        lg = torch.empty_like(p)
+        gu = o["grad_u"].clone()
+        gw = o["grad_w"].clone()
+        hws = torch.empty(plan.hvp_ws_bytes, dtype=torch.uint8, device=p.device)
+        for t in range(T - 1, -1, -1):
+            p_prev, mt, vt, gt, e = hist[t]
+            adam_adjoint_(lt, lm, lv, mt, vt, gt, t + 1, lr_net, lg, kind="higher")
+            hv, du, dw = plan.hvp(u, z, w, e, p_prev, lg, ws=hws)
+            lt += hv
+            gu += du
+            gw += dw
+        if self.u.grad is None:
+            self.u.grad = torch.zeros_like(self.u)
+        self.u.grad += gu.reshape(self.u.shape).to(self.u.dtype)
+        self.optim_u.step()
+        if self.learn_v:
+            if self.v.grad is None:
+                self.v.grad = torch.zeros_like(self.v)
+            self.v.grad += self._chain_w(gw)
+            self.optim_v.step()
+            if not getattr(self, "parameterised", False):
+                with torch.no_grad():
+                    torch.clamp_(self.v, min=0.0)
+        if getattr(self, "scheduler_optim_net", None):
+            self.scheduler_optim_net.step()
+        with torch.no_grad():
+            nn.utils.vector_to_parameters(p.to(plist[0].dtype), plist)
+        return o["loss"].reshape(()).to(torch.float32)
 
     def run_psvi(self, *args, **kwargs):
         raise NotImplementedError("run_psvi drives the outer loop, which " + _OUTER)

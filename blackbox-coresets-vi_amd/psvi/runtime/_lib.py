@@ -86,6 +86,8 @@ SIGNATURES = {
     "psvi_outer_elbo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _SZ, _P]),
     "psvi_hvp": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "psvi_adam_adjoint": (_I32, [_I64, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP),
+                                 _P]),
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),
     "psvi_adam_update": (_I32, [_I64, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P]),
     "psvi_debug_set": (_I32, [_I32, _I32]),

@@ -341,6 +341,21 @@ def randn_(out, seed, offset=0):
     return out
 
 
+def adam_adjoint_(lt, lm, lv, adam_m, adam_v, grad, step, lr, lg_out, kind="higher"):
+    """Reverse of one Adam step (psvi_adam_adjoint): lm, lv updated in place,
+    lg_out <- adjoint of the step's gradient."""
+    n = lt.numel()
+    for t, nm in ((lt, "lt"), (lm, "lm"), (lv, "lv"), (adam_m, "adam_m"), (adam_v, "adam_v"),
+                  (grad, "grad"), (lg_out, "lg_out")):
+        _need(t, nm, n)
+    hp = make_adam(lr, step, kind)
+    lib = _lib.load()
+    check(lib.psvi_adam_adjoint(n, _ptr(lt), _ptr(lm), _ptr(lv), _ptr(adam_m), _ptr(adam_v),
+                                _ptr(grad), _ptr(lg_out), ctypes.byref(hp), _stream()),
+          "psvi_adam_adjoint")
+    return lg_out
+
+
 def adam_update_(params, grad, adam_m, adam_v, step, lr, kind="higher"):
     n = params.numel()
     for t, nm in ((params, "params"), (grad, "grad"), (adam_m, "adam_m"), (adam_v, "adam_v")):

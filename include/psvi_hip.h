@@ -259,6 +259,18 @@ int psvi_hvp(const psvi_plan* plan, const float* u, const int32_t* z, const floa
              const float* eps, const float* params, const float* vec, float* hv_out,
              float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream);
 
+/* Reverse of one Adam step (either variant) for the nested trainer's
+ * reverse-mode pass through the unrolled inner loop (PSVI.nested_step,
+ * psvi_classes.py:541-600; DifferentiableAdam._update optim.py:318-367 /
+ * adam_step diff_optimizers.py:184-213).  The step took (p, m, v, grad) to
+ * (p', adam_m, adam_v) with Adam step hp->step; given lt = adjoint of p' and
+ * lm / lv = adjoints of (adam_m, adam_v) (in/out: replaced by the adjoints of
+ * the step's incoming m, v), writes lg_out = adjoint of grad.  The adjoint of
+ * p is lt + H^T lg_out (psvi_hvp at p). */
+int psvi_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const float* adam_m,
+                      const float* adam_v, const float* grad, float* lg_out,
+                      const psvi_adam_hp* hp, void* stream);
+
 /* ---- utilities ----------------------------------------------------------- */
 /* out[i] ~ N(0,1), Philox4x32-10 counter (seed, offset + i) + Box-Muller.
  * Throughput-mode replacement for torch's normal_() draw (not bit-identical

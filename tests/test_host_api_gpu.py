@@ -189,3 +189,46 @@ def test_hyper_step_philox_runs():
     l1 = ps.hyper_step(xb, yb, K=3)
     l2 = ps.hyper_step(xb, yb, K=3)
     assert np.isfinite(l1) and np.isfinite(l2) and l1 != l2
+
+
+# ---------------------------------------------------------- trainer nested
+@pytest.mark.parametrize("name", fixture_names("n"))
+def test_nested_step_matches_reference(name):
+    """One whole PSVI.nested_step (the reference's default trainer): T higher-
+    Adam steps, the outer objective, its gradient back through the unroll
+    (psvi_adam_adjoint + psvi_hvp per step), u / v Adam steps."""
+    from golden_util import load_fixture
+    from psvi.inference import PSVILearnV
+    from test_host_api import build_model
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    model = build_model(cfg, f["params0"]).cuda()
+    u = torch.tensor(f["u0"], device="cuda").requires_grad_(True)
+    z = torch.tensor(f["z"], device="cuda")
+    ps = PSVILearnV(u=u, z=z, N=cfg["N"], model=model, mc_samples=cfg["S"], device_id=0,
+                    inner_it=cfg["T"])
+    ps.device = torch.device("cuda")
+    ps.v = torch.tensor(f["v0"], device="cuda").requires_grad_(True)
+    ps.setup_optimizers(lr0net=cfg["lr0net"], lr0u=cfg["lr0u"], lr0v=cfg["lr0v"])
+    ei = [torch.tensor(e, device="cuda") for e in f["eps_inner"]]
+    eo = [torch.tensor(e, device="cuda") for e in f["eps_outer"]]
+    loss = ps.nested_step(torch.tensor(f["xb"], device="cuda"),
+                          torch.tensor(f["yb"], device="cuda"), eps_inner=ei, eps_outer=eo)
+    assert rel(loss.item(), f["loss"]) < 1e-5
+    p = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
+    assert l2rel(p, f["params"]) < 1e-5
+    ug, vg = ps.u.grad.cpu().numpy(), ps.v.grad.cpu().numpy()
+    # Differentiating through Adam's normalisation (sqrt(v + 1e-8) smooths at
+    # |g| ~ 3e-3) amplifies the rounding of small gradient entries: the
+    # reference's own fp32 run on the same draws sits this far from its fp64
+    # run.  Bar: 1e-4, or four times the reference's own fp32 deviation.
+    for got, key in ((ug, "u_grad"), (vg, "v_grad")):
+        own = l2rel(f[key + "_fp32"], f[key])
+        print(f"{name}: {key} l2rel {l2rel(got, f[key]):.2e} (reference fp32: {own:.2e})")
+        assert l2rel(got, f[key]) < max(1e-4, 4 * own)
+    for got, want, g, lr in ((ps.u, f["u"], f["u_grad"], cfg["lr0u"]),
+                             (ps.v, f["v"], f["v_grad"], cfg["lr0v"])):
+        big = np.abs(g) > 1e-2 * np.abs(g).max()
+        assert np.abs(got.detach().cpu().numpy() - want)[big].max() < 1e-3 * lr
+    assert [e[0] for e in ps.elbos][-1] == 0

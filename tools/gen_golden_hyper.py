@@ -51,12 +51,18 @@ def _child():
                                         categorical_fn, make_fc2net, make_fcnet)
     from psvi.robust_higher.patch import monkeypatch
 
+    import copy
+
     torch.set_default_dtype(torch.float64)
     draws = []
+    replay = []  # fp32 re-runs: the recorded draws, in order
 
     def wrap(orig):
         def f(shape, dtype, device):
-            out = orig(shape, dtype=dtype, device=device).float().to(dtype)
+            if replay:
+                out = replay.pop(0).reshape(shape).to(dtype)
+            else:
+                out = orig(shape, dtype=dtype, device=device).float().to(dtype)
             draws.append(out.detach().clone().reshape(-1))
             return out
         return f
@@ -82,10 +88,13 @@ def _child():
         return [[m.in_features, m.out_features] for m in model.modules()
                 if isinstance(m, (VILinear, VILinearMultivariateNormal))]
 
-    def make_obj(model, M, D, C, S, N):
-        u = torch.randn(M, D, generator=gen).float().double().requires_grad_(True)
+    def make_obj(model, M, D, C, S, N, uv=None):
+        if uv is None:
+            u = torch.randn(M, D, generator=gen).float().double().requires_grad_(True)
+            v = (0.2 * torch.randn(M, generator=gen)).float().double().requires_grad_(True)
+        else:
+            u, v = (t.detach().clone().requires_grad_(True) for t in uv)
         z = torch.tensor([float(i % C) for i in range(M)])
-        v = (0.2 * torch.randn(M, generator=gen)).float().double().requires_grad_(True)
         obj = PSVILearnV.__new__(PSVILearnV)
         obj.model = model
         obj.u, obj.z, obj.v, obj.N = u, z, v, N
@@ -187,6 +196,7 @@ def _child():
         inner_elbo in innerloop_ctx, psvi_elbo.backward() through the unroll,
         then the u / v Adam steps; fmodel's parameters copied into the model."""
         torch.manual_seed(seed)
+        model32 = copy.deepcopy(model).float()
         obj = make_obj(model, M, D, C, S, N)
         obj.inner_it, obj.register_elbos, obj.log_every = T, False, 10
         obj.scheduler_optim_net = None
@@ -216,6 +226,22 @@ def _child():
 
         obj.inner_elbo, obj.psvi_elbo = inner, outer
         loss = obj.nested_step(xb, yb)
+        recorded = [d.clone() for d in draws]
+        # the reference's own fp32 run on the identical draws (its native dtype):
+        # how far fp32 rounding alone moves the unrolled hypergradient
+        torch.set_default_dtype(torch.float32)
+        replay[:] = [d.float() for d in recorded]
+        o32 = make_obj(model32, M, D, C, S, N, uv=(u0.float(), v0.float()))
+        o32.inner_it, o32.register_elbos, o32.log_every = T, False, 10
+        o32.scheduler_optim_net = None
+        o32.optim_net = torch.optim.Adam(list(model32.parameters()), lr0net)
+        o32.optim_u = torch.optim.Adam([o32.u], lr0u)
+        o32.optim_v = torch.optim.Adam([o32.v], lr0v)
+        o32.nested_step(xb.float(), yb.float())
+        assert not replay
+        u_grad32, v_grad32 = o32.u.grad.double().numpy(), o32.v.grad.double().numpy()
+        torch.set_default_dtype(torch.float64)
+        draws[:] = recorded
         cuts = np.cumsum([0] + sizes)
         eps = [torch.cat(draws[cuts[i]:cuts[i + 1]]).numpy().astype(np.float32)
                for i in range(len(sizes))]
@@ -231,8 +257,11 @@ def _child():
             loss=np.array(float(loss.detach())),
             u=obj.u.detach().numpy(), v=obj.v.detach().numpy(),
             u_grad=obj.u.grad.numpy(), v_grad=obj.v.grad.numpy(),
+            u_grad_fp32=u_grad32, v_grad_fp32=v_grad32,
             params=parameters_to_vector(model.parameters()).detach().numpy())
-        print(f"wrote {name}: calls={len(sizes)} loss={float(loss):.6f}")
+        e32 = np.linalg.norm(u_grad32 - obj.u.grad.numpy()) / np.linalg.norm(obj.u.grad.numpy())
+        print(f"wrote {name}: calls={len(sizes)} loss={float(loss):.6f} "
+              f"(reference fp32 u_grad l2rel vs fp64: {e32:.2e})")
 
     # HVP fixtures
     model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
