@@ -340,9 +340,9 @@ class PSVI:
         ``eps_outer``: optional sequences of draws (library eps layout) in the
         reference's call order, to replay; default: this instance's Philox
         stream."""
-        if hypergrad_approx != "CG_normaleq":
-            raise NotImplementedError(f"hypergrad_approx={hypergrad_approx!r}: only "
-                                      "CG_normaleq (the reference default) runs on HIP")
+        if hypergrad_approx not in ("CG_normaleq", "fixed_point"):
+            raise NotImplementedError(f"hypergrad_approx={hypergrad_approx!r}: the reference's "
+                                      "hyper_step offers CG_normaleq and fixed_point")
         if self.learn_z:
             raise NotImplementedError  # as the reference (psvi_classes.py:619-620)
         T = self.inner_it
@@ -402,6 +402,24 @@ class PSVI:
                                   mixed=mixed, ws=hws)
             return hv.to(torch.float64), du, dw
 
+        if hypergrad_approx == "fixed_point":
+            # hypergradients.py:83-140 with stochastic=True: a fresh fp_map per iteration
+            vs = torch.zeros_like(g_w)
+            for _ in range(int(K)):
+                prev = vs
+                vs = vs - lr * hvp(draw_inner(), vs)[0] + g_w
+                if float(torch.linalg.vector_norm(vs - prev)) < 1e-10:
+                    break
+            xk, eA = vs, draw_inner()
+        else:
+            eA = self._cg_normaleq(hvp, draw_inner, g_w, lr, K)
+            xk = self._cg_x
+        _, du, dw = hvp(eA, xk, mixed=True)     # torch_grad(w_mapped, hparams, vs)
+        return self._hyper_finish(o, du, dw, lr, plan, outer, draw_outer, params, plist)
+
+    def _cg_normaleq(self, hvp, draw_inner, g_w, lr, K):
+        """CG_normaleq's linear solve (hypergradients.py:199-244, CG_torch.py:9-45);
+        returns the draw of w_mapped, leaves the solution in self._cg_x."""
         eA = draw_inner()                       # w_mapped = fp_map(params, hparams)
 
         def jvp(x):                             # J x = x - lr H x (fp_map drawn twice)
@@ -427,7 +445,12 @@ class PSVI:
             beta = torch.dot(rn, rn) / rTr
             pk = rn + beta * pk
             xk, r = xn, rn
-        _, du, dw = hvp(eA, xk, mixed=True)     # torch_grad(w_mapped, hparams, vs)
+        self._cg_x = xk
+        return eA
+
+    def _hyper_finish(self, o, du, dw, lr, plan, outer, draw_outer, params, plist):
+        """hypergradient = -lr * mixed products + the outer objective's direct
+        gradients; u / v Adam steps; outer loss at the new (u, v)."""
         u_grad = (-lr * du.to(torch.float64) + o["grad_u"].to(torch.float64)).to(self.u.dtype)
         if self.u.grad is None:
             self.u.grad = torch.zeros_like(self.u)

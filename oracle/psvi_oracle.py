@@ -607,13 +607,17 @@ def torch_adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
 
 
 def hyper_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer, S, T, K,
-               lr0net, lr0u, lr0v, linsys_lr=1e-4, prior_sd=1.0, cg_tol=1e-10):
+               lr0net, lr0u, lr0v, linsys_lr=1e-4, prior_sd=1.0, cg_tol=1e-10,
+               approx="CG_normaleq"):
     """PSVI.hyper_step with the CG_normaleq hypergradient (psvi_classes.py:602-687,
     psvi/hypergrad/hypergradients.py:199-244, CG_torch.py:9-45), PSVILearnV
     weights f = softmax (v learned, not clamped).  eps_inner: the draws of the
     inner-objective calls in order -- T inner Adam steps, fp_map, the initial
     jvp (2: the first only sizes its dummy), then 2 per CG iteration;
     eps_outer: the outer objective's draws (hypergradient, returned loss).
+    approx="fixed_point": hypergrad's fixed_point with stochastic=True
+    (hypergradients.py:83-140): vs <- J^T vs + g_w for K draws of fp_map, then
+    one more draw for the final torch_grad.
     Returns dict(params, u, v, u_grad, v_grad, ll)."""
     u = np.asarray(u, np.float64)
     v = np.asarray(v, np.float64)
@@ -641,10 +645,26 @@ def hyper_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer
                                               prior_sd)
     g_v = softmax_T(v, g_wts)
     lr = linsys_lr
-    eA = ei.pop(0)                                  # w_mapped = fp_map(params, hparams)
-
     def hv(e, x):
         return inner_hvp(family, layers, p, u, z, w, e, S, x, prior_sd)
+
+    if approx == "fixed_point":
+        vs = np.zeros_like(g_w)
+        for _ in range(K):
+            prev = vs
+            vs = vs - lr * hv(ei.pop(0), vs)[2] + g_w   # stochastic: a fresh fp_map each time
+            if float(np.linalg.norm(vs - prev)) < cg_tol:
+                break
+        _, _, _, du, dw = hv(ei.pop(0), vs)
+        u_grad = -lr * du + g_u
+        v_grad = -lr * softmax_T(v, dw) + g_v
+        u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
+        v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
+        X2 = np.concatenate([u_new, xb])
+        ww2 = np.concatenate([wts(v_new), np.full(Nx, N / Nx)])
+        ll = outer_elbo_grad(family, layers, p, X2, zz, ww2, M, eps_outer[1], S, prior_sd)[0]
+        return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, ll=ll)
+    eA = ei.pop(0)                                  # w_mapped = fp_map(params, hparams)
 
     def jvp(x):                                     # J x = x - lr H x at a fresh draw
         ei.pop(0)                                   # the dummy's fp_map call

@@ -139,7 +139,7 @@ def test_second_order_entry_points_raise():
     f, model = fixture_model("g1_logreg_c1")
     ps = make_psvi(f, model)
     for fn in (lambda: ps.nested_step(None, None, truncated=True), lambda: ps.run_psvi(),
-               lambda: ps.hyper_step(None, None, hypergrad_approx="fixed_point")):
+               lambda: ps.hyper_step(None, None, hypergrad_approx="neumann")):
         with pytest.raises(NotImplementedError):
             fn()
 

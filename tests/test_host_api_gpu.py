@@ -158,7 +158,8 @@ def test_hyper_step_matches_reference(name):
     ei = [torch.tensor(e, device="cuda") for e in f["eps_inner"]]
     eo = [torch.tensor(e, device="cuda") for e in f["eps_outer"]]
     ll = ps.hyper_step(torch.tensor(f["xb"], device="cuda"), torch.tensor(f["yb"], device="cuda"),
-                       K=cfg["K"], linsys_lr=cfg["linsys_lr"], eps_inner=ei, eps_outer=eo)
+                       K=cfg["K"], linsys_lr=cfg["linsys_lr"], eps_inner=ei, eps_outer=eo,
+                       hypergrad_approx=cfg.get("approx", "CG_normaleq"))
     p = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
     assert l2rel(p, f["params"]) < 1e-5
     ug, vg = ps.u.grad.cpu().numpy(), ps.v.grad.cpu().numpy()

@@ -42,7 +42,7 @@ def test_hyper_step_oracle_matches_reference(name):
     out = O.hyper_step(cfg["family"], cfg["layers"], f["params0"], f["u0"], f["z"], f["v0"],
                        cfg["N"], f["xb"], f["yb"], f["eps_inner"], f["eps_outer"], cfg["S"],
                        cfg["T"], cfg["K"], cfg["lr0net"], cfg["lr0u"], cfg["lr0v"],
-                       cfg["linsys_lr"])
+                       cfg["linsys_lr"], approx=cfg.get("approx", "CG_normaleq"))
     assert l2rel(out["params"], f["params"]) < 1e-9
     assert l2rel(out["u_grad"], f["u_grad"]) < 1e-7
     assert l2rel(out["v_grad"], f["v_grad"]) < 1e-7

@@ -137,7 +137,8 @@ def _child():
             d_u=out[-2].numpy(), d_v=out[-1].numpy())
         print(f"wrote {name}: P={p0.numel()} elbo={float(loss):.6f}")
 
-    def run_hyper_step(name, family, model, M, Nx, D, C, S, N, seed, T, K, note=""):
+    def run_hyper_step(name, family, model, M, Nx, D, C, S, N, seed, T, K, note="",
+                       approx="CG_normaleq"):
         torch.manual_seed(seed)
         obj = make_obj(model, M, D, C, S, N)
         obj.inner_it = T
@@ -169,7 +170,7 @@ def _child():
             return r
 
         obj.inner_elbo, obj.psvi_elbo = inner, outer
-        ll = obj.hyper_step(xb, yb, K=K)
+        ll = obj.hyper_step(xb, yb, K=K, hypergrad_approx=approx)
         calls = [k for k, _ in sizes]
         eps = [torch.cat(draws[sum(c for _, c in sizes[:i]):sum(c for _, c in sizes[:i + 1])])
                .numpy().astype(np.float32) for i in range(len(sizes))]
@@ -179,7 +180,7 @@ def _child():
             config=np.array(json.dumps(cfg_of(family, model, S, M, N, Nx=Nx, T=T, K=K,
                                               lr0net=lr0net, lr0u=lr0u, lr0v=lr0v,
                                               linsys_lr=1e-4, calls=calls, seed=seed,
-                                              note=note))),
+                                              approx=approx, note=note))),
             params0=p0.numpy().astype(np.float32), u0=u0.numpy().astype(np.float32),
             v0=v0.numpy().astype(np.float32), z=obj.z.numpy().astype(np.float32),
             xb=xb.numpy().astype(np.float32), yb=yb.numpy().astype(np.float32),
@@ -304,6 +305,17 @@ def _child():
     model = nn.Sequential(VILinear(2, 2, init_sd=0.1, mc_samples=4))
     perturb(model, 0.5, -3.0, 0.5, 0.0)
     run_nested_step("n3_logreg", "mf", model, M=10, Nx=16, D=2, C=2, S=4, N=800, seed=33, T=5)
+
+    # hypergrad_approx="fixed_point" (hypergradients.py:83-140, stochastic)
+    model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
+    perturb(model, 0.3, -3.5, -2.5, 0.002)
+    run_hyper_step("y3_fn2_tiny_fp", "mvn", model, M=10, Nx=12, D=8, C=3, S=16, N=800,
+                   seed=23, T=3, K=4, approx="fixed_point")
+
+    model = make_fcnet(5, 7, 3, n_layers=2, mc_samples=6, init_sd=0.05)
+    perturb(model, 0.4, -3.0, -1.0, 0.0)
+    run_hyper_step("y4_fn_deep_fp", "mf", model, M=13, Nx=9, D=5, C=3, S=6, N=500, seed=24,
+                   T=3, K=4, approx="fixed_point")
 
 
 def main():
