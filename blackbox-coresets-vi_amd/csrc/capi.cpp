@@ -435,6 +435,16 @@ static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
     return o;
 }
 
+static OuterWs outer_ws(const psvi_plan* p, void* ws);
+
+// psvi_evaluate workspace: the outer workspace, then the data rows' softmax
+// [S][M][C] (bounded by M rows) and the sample weights [S]
+static size_t eval_prob_off(const psvi_plan* p);
+static size_t eval_ws_bytes(const psvi_plan* p) {
+    const size_t S = p->d.S, M = p->d.M, C = p->lay[p->L - 1].dout;
+    return eval_prob_off(p) + align256(sizeof(float) * S * M * C) + align256(sizeof(float) * S);
+}
+
 static OuterWs outer_ws(const psvi_plan* p, void* ws) {
     const size_t S = p->d.S, M = p->d.M, D = p->lay[0].din;
     char* b = (char*)ws;
@@ -472,6 +482,7 @@ int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
         case PSVI_Q_XRECV_COUNT: *value = (int64_t)p->s_cnt[r] * p->n_tot; break;
         case PSVI_Q_OUTER_WS_BYTES: *value = (int64_t)outer_ws(p, nullptr).bytes; break;
         case PSVI_Q_HVP_WS_BYTES: *value = (int64_t)hvp_ws(p, nullptr).bytes; break;
+        case PSVI_Q_EVAL_WS_BYTES: *value = (int64_t)eval_ws_bytes(p); break;
         default: return fail(PSVI_EINVAL, "unknown query key");
     }
     return 0;
@@ -795,6 +806,40 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
     }
     // 5. explicit log-det term on the scales; d loss / d u
     HIP_TRY(launch_outer_finish(*p, n_pseudo, params, o.sck, grad_params, o.du, grad_u, st));
+    return 0;
+}
+
+static size_t eval_prob_off(const psvi_plan* p) { return outer_ws(p, nullptr).bytes; }
+
+int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, const int32_t* z_all,
+                  const float* w_all, const float* eps, const float* params, int32_t correction,
+                  float* probs_out, double* stats_out, void* ws, size_t ws_bytes, void* stream) {
+    if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (p->world != 1) return fail(PSVI_ESTATE, "evaluate needs world == 1");
+    if (p->d.S < 2) return fail(PSVI_EINVAL, "evaluate needs S > 1 (psvi_classes.py:1036)");
+    if (p->d.S > 2048) return fail(PSVI_EUNSUP, "evaluate supports S <= 2048");
+    if (n_pseudo < 0 || n_pseudo > p->d.M) return fail(PSVI_EINVAL, "n_pseudo out of [0, M]");
+    if (!x_all || !z_all || !w_all || !eps || !params || !stats_out)
+        return fail(PSVI_EINVAL, "null pointer");
+    if (!ws || ws_bytes < eval_ws_bytes(p)) return fail(PSVI_ENOSPC, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    const OuterWs o = outer_ws(p, ws);
+    char* wsb = (char*)ws;
+    float* prob = (float*)(wsb + eval_prob_off(p));
+    float* W = (float*)(wsb + eval_prob_off(p) +
+                        align256(sizeof(float) * (size_t)p->d.S * p->d.M * p->lay[p->L - 1].dout));
+    float* x = nullptr;
+    if (p->family == PSVI_FAMILY_FULLCOV) {
+        x = (float*)wsb;
+        HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
+    }
+    HIP_TRY(launch_outer_stats(*p, params, eps, x, o.stats, st));
+    NetOuter fw{1, n_pseudo, o.nll, nullptr, nullptr, nullptr, prob};
+    HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
+                       nullptr, st, nullptr, 0, 0, 0, &fw));
+    HIP_TRY(launch_eval(*p, n_pseudo, params, w_all, z_all, o.nll, o.stats, prob,
+                        correction ? 1 : 0, W, probs_out, stats_out, st));
     return 0;
 }
 

@@ -87,6 +87,7 @@ struct NetArgs {
     const float* rowcoef;
     const float* ck;
     float* du_part;
+    float* prob_rows;  // outer forward (evaluate): softmax of the data rows [S][M - n_pseudo][C]
     int nsrc;
     int64_t src_base[kMaxWorld];
     int src_stride[kMaxWorld];
@@ -538,7 +539,14 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     if (c < C) se += expf(lg[c] - mx);
                 const float lse = mx + logf(se);
                 if (a.outer == 1) {
-                    a.nll_rows[(size_t)s * a.M + m0 + m] = lse - lz;
+                    const int mg = m0 + m;
+                    a.nll_rows[(size_t)s * a.M + mg] = lse - lz;
+                    if (a.prob_rows && mg >= a.n_pseudo) {
+                        float* pr = a.prob_rows + ((size_t)s * (a.M - a.n_pseudo) + mg - a.n_pseudo) * C;
+#pragma unroll
+                        for (int c = 0; c < kMaxC; ++c)
+                            if (c < C) pr[c] = expf(lg[c] - lse);
+                    }
                     continue;
                 }
                 part += wm * (lse - lz);
@@ -555,7 +563,12 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 for (int c = 0; c < C; ++c) se += expf(row[c] - mx);
                 const float lse = mx + logf(se);
                 if (a.outer == 1) {
-                    a.nll_rows[(size_t)s * a.M + m0 + m] = lse - lz;
+                    const int mg = m0 + m;
+                    a.nll_rows[(size_t)s * a.M + mg] = lse - lz;
+                    if (a.prob_rows && mg >= a.n_pseudo) {
+                        float* pr = a.prob_rows + ((size_t)s * (a.M - a.n_pseudo) + mg - a.n_pseudo) * C;
+                        for (int c = 0; c < C; ++c) pr[c] = expf(row[c] - lse);
+                    }
                     continue;
                 }
                 part += wm * (lse - lz);
@@ -805,6 +818,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         a.rowcoef = outer->rowcoef;
         a.ck = outer->ck;
         a.du_part = outer->du_part;
+        a.prob_rows = outer->prob_rows;
     }
     a.inv_s0sq = 1.f / (p.d.prior_sd * p.d.prior_sd);
     a.rn_out = rn_out;  // 16-byte aligned (workspace buffers)

@@ -183,6 +183,118 @@ __global__ __launch_bounds__(1024) void outer_combine_kernel(OuterArgs a) {
         }
 }
 
+// evaluate (psvi_classes.py:1031-1108) / pred_on_grid (1130-1175): importance
+// weights over samples, then the predictive distribution of every test row.
+// The reference's weights there use pseudo_nll = log_prob(z).matmul(N f(v)),
+// the pseudopoints' weighted LOG-LIKELIHOOD (psvi_elbo's is the negative), so
+//   lw_s = -pseudo_nll + nkl_s = +sum_m w_m NLL_sm + nkl_s;
+// that sign is reproduced.  correction == 0: uniform weights (mean over s).
+// out[4] (double): [0] entropy of the softmax weights over W > 0, [1] normalised
+// ESS (sum W)^2 / sum W^2 / S, [2] correct predictions, [3] summed test NLL
+// ([2], [3] added by eval_predict_kernel).
+__global__ __launch_bounds__(1024) void eval_weights_kernel(OuterArgs a, int correction,
+                                                            float* W, double* out) {
+    __shared__ double red[16];
+    __shared__ double lw[kOuterMaxS];
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int lane = tid & 63, wid = wave_id(), nwv = nthr >> 6;
+    double sl = 0.0;
+    for (int l = 0; l < a.L; ++l)
+        for (int i = tid; i < a.n[l]; i += nthr) sl += log((double)softplus_f(a.params[a.poff[l] + a.n[l] + i]));
+    sl = block_sum_all(sl, red);
+    const double s0 = a.s0, inv2 = 0.5 / (s0 * s0), nlog = a.n_tot * log(s0);
+    for (int s = wid; s < a.S; s += nwv) {
+        double ps = 0.0;
+        const float* row = a.nll + (size_t)s * a.M;
+        for (int m = lane; m < a.n_pseudo; m += 64) ps += (double)a.w[m] * row[m];
+        ps = wave_sum_d(ps);
+        if (lane == 0)
+            lw[s] = ps + (-a.stats[2 * s] * inv2 - nlog + 0.5 * a.stats[2 * s + 1] + sl);
+    }
+    __syncthreads();
+    double mx = -INFINITY, sm = 0.0;
+    for (int s = tid; s < a.S; s += nthr) mx = fmax(mx, lw[s]);
+    mx = block_max_all(mx, red);
+    for (int s = tid; s < a.S; s += nthr) sm += exp(lw[s] - mx);
+    sm = block_sum_all(sm, red);
+    double ent = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int s = tid; s < a.S; s += nthr) {
+        const double Wsoft = exp(lw[s] - mx) / sm;
+        if (Wsoft > 0.0) ent -= Wsoft * log(Wsoft);
+        s1 += Wsoft;
+        s2 += Wsoft * Wsoft;
+        W[s] = correction ? (float)Wsoft : 1.f / a.S;
+    }
+    ent = block_sum_all(ent, red);
+    s1 = block_sum_all(s1, red);
+    s2 = block_sum_all(s2, red);
+    if (tid == 0) {
+        out[0] = ent;
+        out[1] = s1 * s1 / s2 / a.S;
+        out[2] = 0.0;
+        out[3] = 0.0;
+    }
+}
+
+// one thread per test row: p = sum_s W_s softmax(logits_s), argmax against the
+// label, and Categorical(probs=p).log_prob(y) (normalised, clamped to
+// [eps, 1 - eps] with fp32 eps as torch's probs_to_logits)
+__global__ __launch_bounds__(256) void eval_predict_kernel(OuterArgs a, const float* W,
+                                                           const float* prob, const int32_t* z,
+                                                           float* probs_out, double* out) {
+    __shared__ double red[16];
+    const int nt = a.M - a.n_pseudo, C = a.n_tot;  // n_tot carries C here
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    double correct = 0.0, nll = 0.0;
+    if (j < nt) {
+        float best = -1.f, tot = 0.f, py = 0.f;
+        int arg = 0;
+        const int y = z[a.n_pseudo + j];
+        for (int c = 0; c < C; ++c) {
+            float p = 0.f;
+            for (int s = 0; s < a.S; ++s) p = fmaf(W[s], prob[((size_t)s * nt + j) * C + c], p);
+            if (probs_out) probs_out[(size_t)j * C + c] = p;
+            if (p > best) { best = p; arg = c; }
+            tot += p;
+            if (c == y) py = p;
+        }
+        correct = arg == y ? 1.0 : 0.0;
+        const float q = fminf(fmaxf(py / tot, 1.1920929e-07f), 1.f - 1.1920929e-07f);
+        nll = -(double)logf(q);
+    }
+    correct = block_sum_all(correct, red);
+    nll = block_sum_all(nll, red);
+    if (threadIdx.x == 0) {
+        atomicAdd(out + 2, correct);
+        atomicAdd(out + 3, nll);
+    }
+}
+
+static void fill(const psvi_plan& p, OuterArgs& a);
+
+hipError_t launch_eval(const psvi_plan& p, int n_pseudo, const float* params, const float* w,
+                       const int32_t* z, const float* nll, const double* stats,
+                       const float* prob, int correction, float* W, float* probs_out,
+                       double* out, hipStream_t st) {
+    if (p.d.S > kOuterMaxS) return hipErrorInvalidValue;
+    OuterArgs a{};
+    fill(p, a);
+    a.n_pseudo = n_pseudo;
+    a.params = params;
+    a.w = w;
+    a.nll = nll;
+    a.stats = const_cast<double*>(stats);
+    hipLaunchKernelGGL(eval_weights_kernel, dim3(1), dim3(1024), 0, st, a, correction, W, out);
+    const int nt = p.d.M - n_pseudo;
+    if (nt > 0) {
+        OuterArgs b = a;
+        b.n_tot = p.lay[p.L - 1].dout;
+        hipLaunchKernelGGL(eval_predict_kernel, dim3((nt + 255) / 256), dim3(256), 0, st, b, W,
+                           prob, z, probs_out, out);
+    }
+    return hipGetLastError();
+}
+
 // after the reparameterised backward: + sum_s ck_s sigmoid(sd_i) / softplus(sd_i)
 // on every scale, and d loss / d u = sum_s du_part[s]
 __global__ __launch_bounds__(256) void outer_finish_kernel(OuterArgs a, int nu) {

@@ -201,6 +201,7 @@ struct NetOuter {
     const float* rowcoef; // mode 2: [S][2] d loss / d pseudo_s, d loss / d data_s
     const float* ck;      // mode 2: [S] d loss / d nkl_s
     float* du_part;       // mode 2, nullable: [S][n_pseudo][D] input gradient
+    float* prob_rows;     // mode 1, nullable: [S][M - n_pseudo][C] softmax of the data rows
 };
 
 }  // namespace psvi
@@ -283,6 +284,10 @@ hipError_t launch_outer_combine(const psvi_plan& p, int n_pseudo, const float* p
                                 const float* w, const float* nll, const double* stats,
                                 double* loss, float* rowcoef, float* ck, float* sck,
                                 float* grad_w, double* sample_out, hipStream_t st);
+hipError_t launch_eval(const psvi_plan& p, int n_pseudo, const float* params, const float* w,
+                       const int32_t* z, const float* nll, const double* stats,
+                       const float* prob, int correction, float* W, float* probs_out,
+                       double* out, hipStream_t st);
 hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* params,
                                const float* sck, float* grad, const float* du_part,
                                float* grad_u, hipStream_t st);

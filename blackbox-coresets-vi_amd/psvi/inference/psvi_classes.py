@@ -113,7 +113,7 @@ class PSVI:
     def __init__(self, u=None, z=None, N=None, D=None, model=None, num_pseudo=None, seed=0,
                  mc_samples=None, learn_v=False, f=lambda *x: x[0], distr_fn=categorical_fn,
                  nc=None, register_elbos=True, inner_it=10, log_every=10, lr0net=1e-3,
-                 device_id=None, learn_z=False, **kwargs):
+                 device_id=None, learn_z=False, compute_weights_entropy=True, **kwargs):
         if learn_z:
             raise NotImplementedError("soft labels (learn_z) are not on the HIP inner loop")
         if distr_fn is not categorical_fn:
@@ -133,6 +133,8 @@ class PSVI:
         self.register_elbos, self.elbos = register_elbos, []
         self.inner_it, self.log_every, self.lr0net = inner_it, log_every, lr0net
         self.seed = seed
+        self.compute_weights_entropy = compute_weights_entropy
+        self.results = {}
         with torch.no_grad():
             self.v = torch.full((self.num_pseudo,), 1.0 / self.num_pseudo, device=self.device)
         self.v.requires_grad_(self.learn_v)
@@ -310,6 +312,57 @@ class PSVI:
             loss.backward()
             self.optim.step()
         return loss
+
+    # ------------------------------------------------------------ evaluation
+    def _predict(self, x_rows, y_rows, correction, probs, eps):
+        model = self.model
+        plan = self._outer_plan(model, int(x_rows.shape[0]))
+        Mu = int(self.u.shape[0])
+        x_all = torch.cat([self.u.detach().reshape(Mu, -1).to(torch.float32),
+                           x_rows]).contiguous()
+        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1),
+                           y_rows.to(self.device).reshape(-1)]).to(torch.int32).contiguous()
+        w_all = torch.cat([self.coreset_weights(),
+                           torch.zeros(x_rows.shape[0], device=self.device)]).contiguous()
+        with torch.no_grad():
+            pvec = nn.utils.parameters_to_vector(model.parameters()).detach().to(torch.float32)
+        e = eps if eps is not None else self._draw_eps(plan)
+        return plan.evaluate(Mu, x_all, z_all, w_all, e, pvec.contiguous(), correction, probs)
+
+    def evaluate(self, correction=True, eps=None, **kwargs):
+        """Importance-weighted predictive metrics over self.test_loader
+        (psvi_classes.py:1031-1108): (accuracy, mean test NLL, entropy of the
+        importance weights, normalised ESS, v-entropy), one psvi_evaluate per
+        test batch (fresh weights per batch; entropy / ESS from the last one,
+        as the reference).  ``eps``: optional list of draws, one per batch."""
+        assert self.mc_samples is None or self.mc_samples > 1
+        it = iter(eps) if eps is not None else None
+        correct = nll = last = None
+        total = 0
+        for xt, yt in self.test_loader:
+            xt = xt.to(self.device, torch.float32).reshape(xt.shape[0], -1)
+            st, _ = self._predict(xt, yt, correction, False, next(it) if it else None)
+            correct = st[2] if correct is None else correct + st[2]
+            nll = st[3] if nll is None else nll + st[3]
+            total += int(xt.shape[0])
+            last = st
+        iw_entropy = last[0] if self.compute_weights_entropy else None
+        ness = last[1]
+        vs = self.f(self.v, 0)
+        v_entropy = (vs.sum().square() / vs.square().sum() / self.num_pseudo
+                     if self.compute_weights_entropy else None)
+        return correct / float(total), nll / float(total), iw_entropy, ness, v_entropy
+
+    def pred_on_grid(self, n_test_per_dim=250, correction=True, eps=None, **kwargs):
+        """Predictive probabilities over a 2-d grid (psvi_classes.py:1130-1175):
+        (n_test_per_dim^2, C) with the same importance weights as evaluate."""
+        x0 = torch.linspace(-3, 4, n_test_per_dim)
+        x1 = torch.linspace(-2, 3, n_test_per_dim)
+        x_test = torch.stack(torch.meshgrid(x0, x1, indexing="ij"), dim=-1).to(self.device)
+        x_rows = x_test.reshape(-1, 2).to(torch.float32).contiguous()
+        y = torch.zeros(x_rows.shape[0], device=self.device)
+        _, probs = self._predict(x_rows, y, correction, True, eps)
+        return probs
 
     # ------------------------------------------------------- second order
     def _outer_plan(self, model, Nx):
@@ -617,6 +670,12 @@ class PSVIAV(PSVILearnV):
         self.alpha = torch.tensor([0.0], device=self.device)
         self.alpha.requires_grad_(True)
         self.f = lambda *x: torch.exp(self.alpha) * torch.softmax(x[0], x[1])
+        self.results["alpha"] = []
+
+    def evaluate(self, **kwargs):
+        """psvi_classes.py:1492-1499: records alpha, then PSVI.evaluate."""
+        self.results.setdefault("alpha", []).append(self.alpha.clone().cpu().detach().numpy())
+        return super().evaluate(**kwargs)
 
 
 class PSVIFixedU(PSVILearnV):

@@ -30,6 +30,7 @@ Q_LOOP_WS_BYTES = 10
 Q_TILED_FLOATS = 11
 Q_OUTER_WS_BYTES = 12
 Q_HVP_WS_BYTES = 13
+Q_EVAL_WS_BYTES = 14
 
 ERRORS = {-1: "PSVI_EINVAL", -2: "PSVI_ENOSPC", -3: "PSVI_EUNSUP", -4: "PSVI_ESTATE"}
 
@@ -85,6 +86,7 @@ SIGNATURES = {
                                ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
     "psvi_outer_elbo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _SZ, _P]),
+    "psvi_evaluate": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
     "psvi_hvp": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "psvi_adam_adjoint": (_I32, [_I64, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP),
                                  _P]),

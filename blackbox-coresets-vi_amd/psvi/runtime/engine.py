@@ -80,6 +80,7 @@ class InnerLoopPlan:
         self.tiled_floats = q(_lib.Q_TILED_FLOATS)  # 0: no tiled state for this plan
         self.outer_ws_bytes = q(_lib.Q_OUTER_WS_BYTES)
         self.hvp_ws_bytes = q(_lib.Q_HVP_WS_BYTES)
+        self.eval_ws_bytes = q(_lib.Q_EVAL_WS_BYTES)
         self.eps_stride = (self.eps_count + 3) // 4 * 4   # Philox offset per loop step
         self.n_tot = sum(i * o + o for i, o in layers)
 
@@ -208,6 +209,29 @@ class InnerLoopPlan:
             _ptr(out.get("grad_w")), _ptr(out.get("samples")), _ptr(ws), ws.numel(),
             _stream()), "psvi_outer_elbo_grad")
         return out
+
+    def evaluate(self, n_pseudo, x_all, z_all, w_all, eps, params, correction=True, probs=False,
+                 ws=None):
+        """Importance-weighted predictive evaluation of the data rows of this
+        plan's M rows (psvi_evaluate).  Returns (stats, probs): stats a float64
+        device tensor [entropy of W, normalised ESS, correct, summed NLL];
+        probs ([M - n_pseudo, C]) when requested."""
+        D, C = self.layers[0][0], self.layers[-1][1]
+        _need(x_all, "x_all", self.M * D)
+        _need(z_all, "z_all", self.M, torch.int32)
+        _need(w_all, "w_all", self.M)
+        _need(eps, "eps", self.eps_count)
+        _need(params, "params", self.param_count)
+        dev = params.device
+        stats = torch.empty(4, dtype=torch.float64, device=dev)
+        pr = torch.empty(self.M - int(n_pseudo), C, dtype=torch.float32, device=dev) if probs else None
+        if ws is None or ws.numel() < self.eval_ws_bytes:
+            ws = torch.empty(self.eval_ws_bytes, dtype=torch.uint8, device=dev)
+        check(self.lib.psvi_evaluate(self.handle, int(n_pseudo), _ptr(x_all), _ptr(z_all),
+                                     _ptr(w_all), _ptr(eps), _ptr(params), int(bool(correction)),
+                                     _ptr(pr), _ptr(stats), _ptr(ws), ws.numel(), _stream()),
+              "psvi_evaluate")
+        return stats, pr
 
     def hvp(self, u, z, w, eps, params, vec, mixed=True, out=None, ws=None):
         """Hessian-vector product of the negative inner ELBO at fixed eps

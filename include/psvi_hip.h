@@ -107,6 +107,7 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
                                    none -- it needs full-cov, world 1, S <= 128)      */
 #define PSVI_Q_OUTER_WS_BYTES 12 /* workspace bytes for psvi_outer_elbo_grad          */
 #define PSVI_Q_HVP_WS_BYTES  13 /* workspace bytes for psvi_hvp                       */
+#define PSVI_Q_EVAL_WS_BYTES 14 /* workspace bytes for psvi_evaluate                  */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
  * Samples are split in contiguous blocks; for FULLCOV the rows of every
@@ -240,6 +241,23 @@ int psvi_outer_elbo_grad(const psvi_plan* plan, int32_t n_pseudo, const float* x
                          const float* params, double* loss_out, float* grad_params,
                          float* grad_u, float* grad_w, double* sample_out, void* ws,
                          size_t ws_bytes, void* stream);
+
+/* Importance-weighted predictive evaluation of one test batch: PSVI.evaluate
+ * (psvi_classes.py:1031-1108) and pred_on_grid (1130-1175), world == 1,
+ * 2 <= S <= 2048.  Rows as psvi_outer_elbo_grad: x_all = cat(u, xtest), the
+ * n_pseudo pseudopoints first; z_all their labels (test labels after);
+ * w_all: N f(v) for the pseudopoints (the data rows' entries are unused).
+ * Weights W = softmax_s(+sum_m w_m NLL_sm + sampled_nkl_s) -- the reference's
+ * sign there (its pseudo_nll is the log-likelihood); correction = 0: W = 1/S.
+ *   probs_out ([M - n_pseudo][C], nullable) <- sum_s W_s softmax(logits_s)
+ *   stats_out[4] (double, written) <- entropy of W (over W > 0), normalised
+ *     ESS (sum W)^2 / sum W^2 / S, correct predictions, summed test NLL
+ *     (-log of the normalised probability of the label, clamped to fp32 eps).
+ * ws: PSVI_Q_EVAL_WS_BYTES. */
+int psvi_evaluate(const psvi_plan* plan, int32_t n_pseudo, const float* x_all,
+                  const int32_t* z_all, const float* w_all, const float* eps,
+                  const float* params, int32_t correction, float* probs_out,
+                  double* stats_out, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- second order (the `hyper` trainer's implicit hypergradient) ----------
  * Hessian-vector product of the negative inner ELBO (psvi_inner_step's

@@ -765,3 +765,44 @@ def nested_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_oute
     u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
     v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
     return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, loss=loss)
+
+
+def evaluate_batch(family, layers, params, X, z, w_pseudo, n_pseudo, eps, S, correction=True,
+                   prior_sd=1.0, clamp_eps=np.finfo(np.float64).eps):
+    """One test batch of PSVI.evaluate (psvi_classes.py:1031-1108): X = cat(u, xt),
+    z = cat(z, yt).  The weights use the reference's sign: its pseudo_nll there
+    is log_prob(z).matmul(N f(v)) (a log-likelihood), so
+    lw_s = +sum_m w_m NLL_sm + sampled_nkl_s.  Returns (correct, summed NLL,
+    entropy of W, normalised ESS, probs (Nt, C)); the NLL is
+    -Categorical(probs).log_prob(yt) with torch's clamp to [eps, 1 - eps]."""
+    params = np.asarray(params, np.float64)
+    eps = np.asarray(eps, np.float64)
+    X = np.asarray(X, np.float64)
+    s0 = float(prior_sd)
+    Xl = _sample(family, layers, params, eps, S)
+    Ws, bs = _split(layers, Xl)
+    n_tot = sum(i * o + o for i, o in layers)
+    sumlog = sum(float(np.log(softplus(x["sd"])).sum()) for x in Xl)
+    xsq = sum((x["X"] ** 2).sum(1) for x in Xl)
+    esq = sum((x["E"] ** 2).sum(1) for x in Xl)
+    nkl = -xsq / (2 * s0 ** 2) - n_tot * np.log(s0) + 0.5 * esq + sumlog
+    hs, _ = _net_rows_forward(X, Ws, bs)
+    logits = hs[-1]
+    R = X.shape[0]
+    mx = logits.max(-1, keepdims=True)
+    lse = (mx + np.log(np.exp(logits - mx).sum(-1, keepdims=True)))[..., 0]
+    zi = np.asarray(z).astype(np.int64)
+    nll = lse - logits[:, np.arange(R), zi]
+    Mu = int(n_pseudo)
+    lw = nll[:, :Mu] @ np.asarray(w_pseudo, np.float64)[:Mu] + nkl
+    W = np.exp(lw - lw.max())
+    W /= W.sum()
+    p = np.exp(logits[:, Mu:] - lse[:, Mu:, None])           # (S, Nt, C)
+    probs = np.einsum("s,snc->nc", W, p) if correction else p.mean(0)
+    yt = zi[Mu:]
+    correct = float((probs.argmax(-1) == yt).sum())
+    pn = probs / probs.sum(-1, keepdims=True)
+    q = np.clip(pn[np.arange(len(yt)), yt], clamp_eps, 1 - clamp_eps)
+    ent = float(-(W[W > 0] * np.log(W[W > 0])).sum())
+    ness = float(W.sum() ** 2 / (W ** 2).sum() / S)
+    return correct, float(-np.log(q).sum()), ent, ness, probs

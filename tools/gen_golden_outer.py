@@ -167,6 +167,67 @@ def _child():
     run("o6_logreg_fullcov", "mvn", model, PSVILearnV, M=10, Nx=16, D=2, C=2, S=4, N=800,
         seed=6, v_scale=0.3, note="logistic_regression_fullcov")
 
+    # evaluate (psvi_classes.py:1031-1108): one test batch, correction on and off
+    def run_eval(name, family, model, cls, M, Nt, D, C, S, N, seed, v_scale=0.0, alpha=None):
+        torch.manual_seed(seed)
+        u = torch.randn(M, D, generator=gen).float().double()
+        z = torch.tensor([float(i % C) for i in range(M)])
+        xt = torch.randn(Nt, D, generator=gen).float().double()
+        yt = torch.randint(0, C, (Nt,), generator=gen).double()
+        v = (v_scale * torch.randn(M, generator=gen)).float().double()
+        obj = cls.__new__(cls)
+        obj.u, obj.z, obj.v, obj.N = u, z, v, N
+        obj.distr_fn, obj.learn_z = categorical_fn, False
+        obj.mc_samples, obj.nc, obj.num_pseudo = S, C, M
+        obj.compute_weights_entropy, obj.device = True, torch.device("cpu")
+        obj.test_loader = [(xt, yt)]
+        obj.results = {"alpha": []}
+        if cls is PSVIAV:
+            obj.alpha = torch.tensor([alpha])
+            obj.f = lambda *x: torch.exp(obj.alpha) * torch.softmax(x[0], x[1])
+        else:
+            obj.f = torch.softmax
+        obj.model = model
+        p0 = parameters_to_vector(model.parameters()).detach().clone()
+        out = {}
+        for tag, corr in (("", True), ("_nc", False)):
+            draws.clear()
+            acc, nll, ent, ness, vent = obj.evaluate(correction=corr)
+            out["eps" + tag] = torch.cat(draws).numpy().astype(np.float32)
+            out["acc" + tag] = np.array(float(acc))
+            out["nll" + tag] = np.array(float(nll))
+            out["went" + tag] = np.array(float(ent))
+            out["ness" + tag] = np.array(float(ness))
+            out["vent" + tag] = np.array(float(vent))
+        w = (obj.N * obj.f(obj.v, 0)).detach()
+        cfg = dict(family=family, layers=layer_sizes(model), S=S, M=M, Nt=Nt, N=N, prior_sd=1.0,
+                   f="exp_alpha_softmax" if cls is PSVIAV else "softmax", alpha=alpha, seed=seed)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), config=np.array(json.dumps(cfg)),
+                            params0=p0.numpy().astype(np.float32),
+                            u=u.numpy().astype(np.float32), z=z.numpy().astype(np.float32),
+                            xt=xt.numpy().astype(np.float32), yt=yt.numpy().astype(np.float32),
+                            v=v.numpy().astype(np.float32), w=w.numpy(), **out)
+        print(f"wrote {name}: acc={float(out['acc']):.4f} nll={float(out['nll']):.4f} "
+              f"ness={float(out['ness']):.4f}")
+
+    with torch.no_grad():
+        model = nn.Sequential(VILinear(2, 2, init_sd=0.1, mc_samples=8))
+        perturb(model, 0.5, -3.0, 0.5, 0.0)
+        run_eval("e1_logreg", "mf", model, PSVILearnV, M=10, Nt=40, D=2, C=2, S=8, N=800,
+                 seed=41, v_scale=0.3)
+        model = make_fcnet(2, 100, 4, n_layers=1, mc_samples=16, init_sd=0.1)
+        perturb(model, 0.3, -4.0, -1.0, 0.0)
+        run_eval("e2_fn_av", "mf", model, PSVIAV, M=20, Nt=64, D=2, C=4, S=16, N=800, seed=42,
+                 v_scale=0.3, alpha=0.25)
+        model = make_fc2net(8, 6, 3, mc_samples=16, init_sd=1e-2)
+        perturb(model, 0.3, -3.5, -2.5, 0.002)
+        run_eval("e3_fn2_tiny", "mvn", model, PSVILearnV, M=10, Nt=50, D=8, C=3, S=16, N=800,
+                 seed=43, v_scale=0.2)
+        model = nn.Sequential(VILinearMultivariateNormal(2, 2, init_sd=0.1, mc_samples=4))
+        perturb(model, 0.5, -3.0, -1.0, 0.02)
+        run_eval("e4_logreg_fullcov", "mvn", model, PSVILearnV, M=10, Nt=30, D=2, C=2, S=4,
+                 N=800, seed=44, v_scale=0.3)
+
 
 def main():
     if "--child" in sys.argv:
