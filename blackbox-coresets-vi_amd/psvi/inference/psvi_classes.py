@@ -47,11 +47,14 @@ gradient flows to them).
 
 There is no CPU fallback: a missing libpsvi_hip.so or GPU raises.
 """
+import time
+
 import torch
 import torch.nn as nn
 from torch.autograd.function import once_differentiable
 
-from ..models.neural_net import categorical_fn, model_spec
+from ..models.neural_net import (VILinear, VILinearMultivariateNormal, categorical_fn,
+                                 make_fc2net, make_fcnet, model_spec)
 from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
@@ -123,6 +126,14 @@ class PSVI:
         self.device = torch.device(f"cuda:{device_id}" if device_id is not None else
                                    ("cuda" if torch.cuda.is_available() else "cpu"))
         self.u, self.z, self.N, self.D, self.nc = u, z, N, D, nc
+        self.train_dataset = kwargs.get("train_dataset")
+        self.test_dataset = kwargs.get("test_dataset")
+        self.init_dataset = kwargs.get("init_dataset")
+        for k in ("prune", "increment", "retrain_on_coreset", "reset"):
+            if kwargs.get(k):
+                raise NotImplementedError(f"{k}=True (coreset pruning / incremental learning / "
+                                          "retraining / resets) is not on the HIP path")
+        self.chosen_indices = []
         self.model = model
         self.num_pseudo = num_pseudo if num_pseudo is not None else (
             u.shape[0] if u is not None else None)
@@ -614,8 +625,144 @@ class PSVI:
             nn.utils.vector_to_parameters(p.to(plist[0].dtype), plist)
         return o["loss"].reshape(()).to(torch.float32)
 
-    def run_psvi(self, *args, **kwargs):
-        raise NotImplementedError("run_psvi drives the outer loop, which " + _OUTER)
+    # ------------------------------------------------------------ the driver
+    def set_up_model(self):
+        """psvi_classes.py:689-758 for the architectures the HIP path runs:
+        logistic_regression (VILinear), logistic_regression_fullcov, fn
+        (make_fcnet, n_layers), fn2 (make_fc2net: always 2 hidden layers, the
+        reference does not forward n_layers)."""
+        kw = dict(init_sd=self.init_sd, mc_samples=self.mc_samples)
+        if self.logistic_regression:
+            self.model = nn.Sequential(VILinear(self.D, self.nc, **kw))
+        elif self.architecture == "logistic_regression_fullcov":
+            self.model = nn.Sequential(VILinearMultivariateNormal(self.D, self.nc, **kw))
+        elif self.architecture == "fn":
+            self.model = make_fcnet(self.D, self.n_hidden, self.nc, n_layers=self.n_layers,
+                                    linear_class=VILinear, nonl_class=nn.ReLU, **kw)
+        elif self.architecture == "fn2":
+            self.model = make_fc2net(self.D, self.n_hidden, self.nc,
+                                     linear_class=VILinearMultivariateNormal, nonl_class=nn.ReLU,
+                                     **kw)
+        else:
+            raise NotImplementedError(f"architecture {self.architecture!r} is not on the HIP path "
+                                      "(lenet / alexnet / resnet / residual_fn / regressor_net)")
+        self.model = self.model.to(self.device)
+
+    @staticmethod
+    def _xy(dataset):
+        x = getattr(dataset, "data", None)
+        y = getattr(dataset, "targets", None)
+        if x is None or y is None:
+            if hasattr(dataset, "tensors"):
+                x, y = dataset.tensors[0], dataset.tensors[1]
+            else:
+                x = torch.stack([dataset[i][0] for i in range(len(dataset))])
+                y = torch.as_tensor([dataset[i][1] for i in range(len(dataset))])
+        return torch.as_tensor(x).float(), torch.as_tensor(y)
+
+    def pseudo_subsample_init(self):
+        """psvi_classes.py:229-285: the pseudodata start on a random subset with
+        an equal number of points per class (the remainder on the last class)."""
+        x, y = self._xy(self.train_dataset if self.init_dataset is None else self.init_dataset)
+        ppc = [self.num_pseudo // self.nc] * self.nc
+        ppc[-1] = self.num_pseudo - sum(ppc[:-1])
+        self.z = torch.tensor([c for c, k in enumerate(ppc) for _ in range(k)]).float().to(
+            self.device)
+        us = []
+        for c in range(self.nc):
+            idx = (y == c).nonzero().reshape(-1)
+            us.append(x[idx[torch.randperm(idx.numel())[:ppc[c]]]])
+        self.u = torch.cat(us).reshape(self.num_pseudo, -1).to(self.device).requires_grad_(True)
+
+    def pseudo_rand_init(self, variance=1.0):
+        """psvi_classes.py:287-308: noisy empirical mean, labels split over classes."""
+        x, _ = self._xy(self.train_dataset)
+        mean = x.reshape(x.shape[0], -1).mean(0)
+        self.u = (mean + variance * torch.randn(self.num_pseudo, self.D)).to(
+            self.device).requires_grad_(True)
+        per = self.num_pseudo // self.nc
+        self.z = torch.cat([c * torch.ones(per if c < self.nc - 1
+                                           else self.num_pseudo - (self.nc - 1) * per)
+                            for c in range(self.nc)]).to(self.device)
+
+    def run_psvi(self, init_args="subsample", trainer="nested", n_layers=1,
+                 logistic_regression=True, n_hidden=None, architecture=None, log_every=10,
+                 inner_it=10, data_minibatch=None, lr0net=1e-3, lr0u=1e-3, lr0joint=1e-3,
+                 lr0v=1e-2, lr0z=1e-2, init_sd=1e-3, num_epochs=1000, log_pseudodata=False,
+                 prune_idx=0, increment_idx=0, gamma=1.0, **kwargs):
+        """psvi_classes.py:761-1028 on the HIP trainers: data loaders, model set-up,
+        pseudodata initialisation, the optimisers and StepLR of the reference,
+        then num_epochs outer steps of `trainer` (nested / hyper / joint /
+        alternating), evaluating every log_every; returns the results dict
+        (accs, nlls, csizes, times, elbos, went, ness, vent, vs, avg_epoch_time,
+        gpu_memory, chosen_indices; us, zs, grid_preds with log_pseudodata)."""
+        from torch.utils.data import DataLoader
+
+        if self.learn_z:
+            raise NotImplementedError("soft labels (learn_z) are not on the HIP path")
+        if init_args not in ("subsample", "random"):
+            raise NotImplementedError(f"init_args={init_args!r}: custom / saved initialisations "
+                                      "read the reference's selection and results files")
+        self.init_args, self.trainer = init_args, trainer
+        self.logistic_regression, self.architecture = logistic_regression, architecture
+        self.n_hidden, self.n_layers, self.init_sd = n_hidden, n_layers, init_sd
+        self.log_every, self.log_pseudodata = log_every, log_pseudodata
+        self.data_minibatch, self.inner_it, self.num_epochs = data_minibatch, inner_it, num_epochs
+        self.gamma = gamma
+        epoch_quarter = (self.N // self.data_minibatch) // 4
+        self.train_loader = DataLoader(self.train_dataset, batch_size=self.data_minibatch,
+                                       shuffle=True)
+        self.test_loader = DataLoader(self.test_dataset, batch_size=self.data_minibatch,
+                                      shuffle=False)
+        self.set_up_model()
+        (self.pseudo_subsample_init if init_args == "subsample" else self.pseudo_rand_init)()
+        self.setup_optimizers(lr0net=lr0net, lr0u=lr0u, lr0v=lr0v, lr0joint=lr0joint,
+                              trainer=trainer)
+        self.scheduler_optim_net = torch.optim.lr_scheduler.StepLR(
+            self.optim_net, step_size=epoch_quarter if epoch_quarter > 0 else 10000,
+            gamma=self.gamma)
+        steps = {"nested": self.nested_step, "hyper": self.hyper_step,
+                 "alternating": self.alternating_step, "joint": self.joint_step}
+        if trainer not in steps:
+            raise ValueError(f"unknown trainer {trainer!r}")
+        psvi_step = steps[trainer]
+        accs, nlls, csizes, went, ness_l, vent, us, zs, vs, grid, times = \
+            [], [], [], [], [], [], [], [], [], [], [0]
+        t_start = time.time()
+        lpit = list(range(num_epochs))[::log_every]
+        for it in range(num_epochs):
+            xbatch, ybatch = next(iter(self.train_loader))
+            xbatch, ybatch = xbatch.to(self.device), ybatch.to(self.device)
+            if it % log_every == 0:
+                acc, nll, iw_ent, ness, v_ent = self.evaluate()
+                if log_pseudodata and it in lpit and self.D == 2:
+                    grid.append(self.pred_on_grid().detach().cpu().numpy().T)
+                with torch.no_grad():
+                    nlls.append(nll.item())
+                    accs.append(acc.item())
+                    csizes.append(self.num_pseudo)
+                    times.append(times[-1] + time.time() - t_start)
+                    vs.append(self.v.clone().cpu().detach().numpy())
+                    if iw_ent is not None:
+                        went.append(iw_ent.item())
+                    if ness is not None:
+                        ness_l.append(ness.item())
+                    if v_ent is not None:
+                        vent.append(v_ent.item())
+                    if log_pseudodata:
+                        us.append(self.u.clone().cpu().detach().numpy())
+                        zs.append(self.z.clone().cpu().detach().numpy())
+            psvi_step(xbatch, ybatch)
+        torch.cuda.synchronize()
+        self.results.update(
+            accs=accs, nlls=nlls, csizes=csizes, times=times[1:], elbos=self.elbos, went=went,
+            ness=ness_l, vent=vent, vs=vs,
+            avg_epoch_time=(time.time() - t_start) / max(num_epochs, 1),
+            gpu_memory=torch.cuda.max_memory_allocated(self.device) / 2 ** 30,
+            chosen_indices=self.chosen_indices)
+        if log_pseudodata:
+            self.results.update(us=us, zs=zs, grid_preds=grid)
+        return self.results
 
 
 class PSVILearnV(PSVI):

@@ -138,7 +138,8 @@ def test_inner_loop_refuses_cpu_tensors():
 def test_second_order_entry_points_raise():
     f, model = fixture_model("g1_logreg_c1")
     ps = make_psvi(f, model)
-    for fn in (lambda: ps.nested_step(None, None, truncated=True), lambda: ps.run_psvi(),
+    for fn in (lambda: ps.nested_step(None, None, truncated=True),
+               lambda: ps.run_psvi(init_args="custom"),
                lambda: ps.hyper_step(None, None, hypergrad_approx="neumann")):
         with pytest.raises(NotImplementedError):
             fn()
