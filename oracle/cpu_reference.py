@@ -44,6 +44,9 @@ class _MFLayer:
         pW = D.Independent(D.Normal(torch.zeros_like(muW), prior_sd), 2)
         pb = D.Independent(D.Normal(torch.zeros_like(mub), prior_sd), 1)
         kl = D.kl_divergence(qW, pW) + D.kl_divergence(qb, pb)
+        # VIMixin.sampled_nkl (neural_net.py:110-115) of this draw
+        bs = b.squeeze(1)
+        self.nkl = (pW.log_prob(W) - qW.log_prob(W)) + (pb.log_prob(bs) - qb.log_prob(bs))
         return out, kl
 
 
@@ -69,12 +72,15 @@ class _MVNLayer:
 
     def forward(self, h, p, S, prior_sd):
         mean, sd, corr = p
-        x = self._dist(mean, sd, corr).rsample((S,))
+        q = self._dist(mean, sd, corr)
+        x = q.rsample((S,))
         W = x[:, :self.din * self.dout].reshape(S, self.dout, self.din)
         b = x[:, self.din * self.dout:].reshape(S, self.dout)
         out = h.matmul(W.transpose(-1, -2)) + b.unsqueeze(-2)
         prior = D.MultivariateNormal(torch.zeros_like(mean),
                                      scale_tril=torch.full_like(mean, prior_sd).diag_embed())
+        # MultivariateNormalVIMixin.sampled_nkl (neural_net.py:438-442): triangular solves
+        self.nkl = prior.log_prob(x) - self._dist(mean, sd, corr).log_prob(x)
         return out, D.kl_divergence(self._dist(mean, sd, corr), prior)
 
 
@@ -108,6 +114,53 @@ class RefInnerStep:
         torch.nn.LogSoftmax(dim=-1)(h).permute(1, 2, 0)  # computed, unused (psvi_classes.py:495)
         nll = -D.Categorical(logits=h).log_prob(z)
         return nll.matmul(w).sum() + kl
+
+    def psvi_elbo(self, params_list, u, z, w, xb, yb, N):
+        """PSVI.psvi_elbo (psvi_classes.py:445-486) with the reference's op sequence."""
+        X = torch.cat((u, xb))
+        labels = torch.cat((z, yb))
+        h = X
+        nl = len(self.layers)
+        for i, lay in enumerate(self.layers):
+            h, _ = lay.forward(h, params_list[i], self.S, self.prior_sd)
+            if i < nl - 1:
+                h = torch.relu(h)
+        torch.nn.LogSoftmax(dim=-1)(h).permute(1, 2, 0)
+        nlls = -D.Categorical(logits=h).log_prob(labels)
+        Nu, Nx = u.shape[0], xb.shape[0]
+        pseudo = nlls[:, :Nu].matmul(w)
+        data = N / Nx * nlls[:, Nu:].sum(-1)
+        lw = -pseudo + sum(lay.nkl for lay in self.layers)
+        return lw.softmax(0).mul(data - pseudo).sum() - lw.mean()
+
+    def nested_step(self, params0, u, z, v, N, xb, yb, T, lr, seed=0, eps_inner=None,
+                    eps_outer=None):
+        """PSVI.nested_step (psvi_classes.py:541-600) for PSVILearnV: T higher-Adam
+        steps with create_graph, psvi_elbo, backward to u and v.  eps_inner /
+        eps_outer replay recorded draws (flat, reference order)."""
+        torch.manual_seed(seed)
+        u = u.detach().clone().requires_grad_(True)
+        v = v.detach().clone().requires_grad_(True)
+        p = [t.detach().clone().requires_grad_(True)
+             for ps in self.split(params0.detach().clone()) for t in ps]
+        m = [torch.zeros_like(t) for t in p]
+        s2 = [torch.zeros_like(t) for t in p]
+        for t in range(T):
+            w = N * torch.softmax(v, 0)
+            with _patched_normal(_EpsReplay(eps_inner[t]) if eps_inner is not None else None):
+                loss = self.elbo(self._group(p), u, z, w)
+            gs = torch.autograd.grad(loss, p, create_graph=True)
+            bc1, bc2 = 1 - 0.9 ** (t + 1), 1 - 0.999 ** (t + 1)
+            newp = []
+            for i, (pi, gi) in enumerate(zip(p, gs)):
+                m[i] = m[i] * 0.9 + 0.1 * gi
+                s2[i] = s2[i] * 0.999 + 0.001 * gi * gi
+                newp.append(pi - (lr / bc1) * m[i] / ((s2[i] + 1e-8).sqrt() / math.sqrt(bc2) + 1e-8))
+            p = newp
+        with _patched_normal(_EpsReplay(eps_outer) if eps_outer is not None else None):
+            out = self.psvi_elbo(self._group(p), u, z, N * torch.softmax(v, 0), xb, yb, N)
+        out.backward()
+        return float(out.detach()), u.grad, v.grad
 
     def run(self, params0, u, z, w, T, lr, eps_list=None, seed=0, adam="higher",
             create_graph=True):
