@@ -127,6 +127,67 @@ def cpu_baseline(budget_s=12.0):
                         f"in {dt:.1f} s on {torch.get_num_threads()} threads of {model}"))
 
 
+def trainer_timings(dev, cpu=True, cpu_T=2):
+    """Auxiliary evidence, not the metric: the outer step of the trainers at C3
+    (fn2 64-40-40-2, S = 128, M = 100 pseudopoints, a 128-row data batch, the
+    reference init): wall ms per call of psvi_elbo forward + backward,
+    psvi_hvp, one nested_step (inner_it = cpu_T and 100) and one hyper_step
+    (inner_it = 100, K = 30), and the op-faithful CPU nested_step
+    (oracle/cpu_reference.py, the reference's op sequence) at inner_it = cpu_T."""
+    from psvi.inference import PSVILearnV
+    from psvi.models import make_fc2net
+    from psvi.runtime import randn_
+
+    torch.manual_seed(0)
+    model = make_fc2net(64, 40, 2, mc_samples=S_PER_GPU, init_sd=1e-6).to(dev)
+    u, z, w = synthetic_inputs(dev)
+    g = torch.Generator().manual_seed(1)
+    xb = torch.randn(128, LAYERS[0][0], generator=g)
+    yb = (torch.rand(128, generator=g) < torch.sigmoid(5.0 * xb.sum(1))).float()
+    xb, yb = xb.to(dev), yb.to(dev)
+    ps = PSVILearnV(u=u.clone().requires_grad_(True), z=z.float(), N=N_DATA, model=model,
+                    mc_samples=S_PER_GPU, device_id=dev.index, inner_it=100, seed=7)
+    ps.device = dev
+    ps.register_elbos = False
+    ps.setup_optimizers()
+
+    def wall_ms(fn, n):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t0) / n * 1e3, 3)
+
+    out = {}
+    out["psvi_elbo_fwd_bwd_ms"] = wall_ms(lambda: ps.psvi_elbo(xb, yb).backward(), 10)
+    plan = ps._plan(model)
+    pv = torch.nn.utils.parameters_to_vector(model.parameters()).detach().clone()
+    vec = torch.randn(pv.numel(), device=dev)
+    e = torch.empty(plan.eps_count, device=dev)
+    randn_(e, 3)
+    zi = z.to(torch.int32)
+    out["psvi_hvp_ms"] = wall_ms(lambda: plan.hvp(u, zi, w, e, pv, vec), 10)
+    ps.inner_it = cpu_T
+    out[f"nested_step_T{cpu_T}_ms"] = wall_ms(lambda: ps.nested_step(xb, yb), 3)
+    ps.inner_it = 100
+    out["nested_step_T100_ms"] = wall_ms(lambda: ps.nested_step(xb, yb), 1)
+    out["hyper_step_T100_K30_ms"] = wall_ms(lambda: ps.hyper_step(xb, yb, K=30), 1)
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from cpu_reference import RefInnerStep, reference_init
+
+        r = RefInnerStep("mvn", LAYERS, S_PER_GPU)
+        p0 = reference_init("mvn", LAYERS)
+        t0 = time.perf_counter()
+        r.nested_step(p0, u.cpu(), z.float().cpu(), torch.zeros(M), N_DATA, xb.cpu(), yb.cpu(),
+                      cpu_T, LR)
+        out[f"cpu_nested_step_T{cpu_T}_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        out["cpu_threads"] = torch.get_num_threads()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,6 +195,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-trainers", action="store_true",
+                    help="skip the auxiliary outer-step (trainer) timings")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -291,6 +354,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_budget)
+    trainers = None
+    if rank == 0 and world == 1 and not args.no_trainers:
+        trainers = trainer_timings(dev, cpu=not args.no_cpu_baseline)
     if world > 1:
         dist.barrier()
     if rank == 0:
@@ -313,6 +379,7 @@ def main():
                        "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "trainers": trainers,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
