@@ -32,6 +32,7 @@ using namespace psvi;
 namespace {
 
 thread_local std::string g_err;
+int g_upd_chunk_tiles = 0;  // psvi_debug_set(PSVI_DBG_UPD_CHUNK, n): c-blocks per update chunk (0 = auto)
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -210,7 +211,7 @@ int build_plan(psvi_plan& p) {
             const int lo = p.row_lo[r][l], hi = p.row_hi[r][l];
             for (int b = lo / 64; 64 * b < hi; ++b) tiles += b + 1;
         }
-        const int ch = std::max(1, (tiles + 511) / 512);
+        const int ch = g_upd_chunk_tiles > 0 ? g_upd_chunk_tiles : std::max(1, (tiles + 511) / 512);
         for (int l = 0; l < p.L; ++l) {
             const int n = p.lay[l].n, lo = p.row_lo[r][l], hi = p.row_hi[r][l];
             const int xc = p.xcol_l[r][l];
@@ -304,6 +305,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_UPD_ABLATION: g_upd_ablation = value; return 0;
         case PSVI_DBG_NET_SPLIT_BELOW: g_net_split_below = value; return 0;
         case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
+        case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }
 }

@@ -340,6 +340,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     the update launches of every value-th step of
                                     full-cov psvi_inner_loop calls (0 = off;
                                     setting it drops earlier records)          */
+#define PSVI_DBG_UPD_CHUNK 9     /* value: c-blocks (64x64 tiles) per full-cov update
+                                    chunk for plans created afterwards (0 = auto:
+                                    about one chunk per resident workgroup)    */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
