@@ -210,63 +210,31 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
 }
 
 // x[s][xcol + rr] = mean[r] + softplus(sd[r]) eps[s][r] + sum over the row
-// block's slots (r = r0 + rr).  A thread owns 4 consecutive rows of one
-// sample: the slot partials ([slot][S][kFwdRows], rows from 0) move as
-// 16-byte loads, 4 slots in flight; mean / sd / eps / x are scalar (their row
-// offsets have no alignment).  16 samples x 64 rows per workgroup.  Summation
-// order per row: k = 0, 1, ... within each of 4 interleaved partials, as
-// before the vectorisation (bit-identical x).
-constexpr int kRedSamples = 256 / (kFwdRows / 4);
+// block's slots (r = r0 + rr); one workgroup per (row block, 256/kFwdRows
+// samples), coalesced along the rows.
 __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* rbs,
                                                              const float* part, FwdArgs a,
                                                              float* x) {
     const FwdRowBlock rb = rbs[blockIdx.x];
-    const int rr0 = 4 * (threadIdx.x & (kFwdRows / 4 - 1));
-    const int s = blockIdx.y * kRedSamples + threadIdx.x / (kFwdRows / 4);
-    if (s >= a.S || rr0 >= rb.R) return;
-    const int n = a.lay[rb.layer].n;
+    const int rr = threadIdx.x & (kFwdRows - 1);
+    const int s = blockIdx.y * (256 / kFwdRows) + threadIdx.x / kFwdRows;
+    if (s >= a.S || rr >= rb.R) return;
+    const int n = a.lay[rb.layer].n, r = rb.r0 + rr;
     const float* mean = a.params + a.lay[rb.layer].poff;
-    const float* E = a.eps + a.lay[rb.layer].eoff + (int64_t)s * n;
-    const float4* p = reinterpret_cast<const float4*>(part + (size_t)rb.slot0 * a.S * kFwdRows +
-                                                      (size_t)s * kFwdRows + rr0);
-    const size_t st = (size_t)a.S * kFwdRows / 4;
-    float4 s4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dg = a.raw_diag ? mean[n + r] : softplus_f(mean[n + r]);
+    float sum = mean[r] + dg * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
+    const float* p = part + (size_t)rb.slot0 * a.S * kFwdRows + (size_t)s * kFwdRows + rr;
+    const size_t st = (size_t)a.S * kFwdRows;
+    // 4 independent loads in flight per thread; summation order k = 0, 1, ... kept per
+    // partial so the result does not depend on the unroll
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
     int k = 0;
     for (; k + 4 <= rb.nk; k += 4) {
-        float4 v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = p[(k + i) * st];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            s4[i].x += v[i].x;
-            s4[i].y += v[i].y;
-            s4[i].z += v[i].z;
-            s4[i].w += v[i].w;
-        }
+        for (int i = 0; i < 4; ++i) s4[i] += p[(k + i) * st];
     }
-    for (int i = 0; k + i < rb.nk; ++i) {
-        const float4 v = p[(k + i) * st];
-        s4[i].x += v.x;
-        s4[i].y += v.y;
-        s4[i].z += v.z;
-        s4[i].w += v.w;
-    }
-    const float tot[4] = {(s4[0].x + s4[1].x) + (s4[2].x + s4[3].x),
-                          (s4[0].y + s4[1].y) + (s4[2].y + s4[3].y),
-                          (s4[0].z + s4[1].z) + (s4[2].z + s4[3].z),
-                          (s4[0].w + s4[1].w) + (s4[2].w + s4[3].w)};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int rr = rr0 + j;
-        if (rr < rb.R) {
-            const int r = rb.r0 + rr;
-            const float dg = a.raw_diag ? mean[n + r] : softplus_f(mean[n + r]);
-            const float sum = mean[r] + dg * E[r];
-            x[(int64_t)s * a.ldx + rb.xcol + rr] = sum + tot[j];
-        }
-    }
+    for (int i = 0; k + i < rb.nk; ++i) s4[i] += p[(k + i) * st];
+    x[(int64_t)s * a.ldx + rb.xcol + rr] = sum + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
 }
 
 int g_fwd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_FWD_ABLATION, mask)
@@ -931,7 +899,7 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     if (p.n_fwd == 0) return hipSuccess;
     // every x element is written by exactly one reduce thread: no memset
     hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd), dim3(256), 0, st, a);
-    constexpr int spb = kRedSamples;  // samples per reduce workgroup
+    constexpr int spb = 256 / kFwdRows;  // samples per reduce workgroup
     hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb), dim3(256), 0,
                        st, p.d_frb, p.d_fwd_part, a, x_shard);
     return hipGetLastError();
@@ -984,7 +952,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             f.ldx = p.rows_tot[p.rank];
             f.S = p.d.S;
             fill_layers(p, f.lay);
-            constexpr int spb = kRedSamples;
+            constexpr int spb = 256 / kFwdRows;
             hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb),
                                dim3(256), 0, st, p.d_ufrb, p.d_upd_part, f, x_next);
         } else {
@@ -1011,7 +979,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         f.ldx = p.rows_tot[p.rank];
         f.S = p.d.S;
         fill_layers(p, f.lay);
-        constexpr int spb = kRedSamples;
+        constexpr int spb = 256 / kFwdRows;
         hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb), dim3(256),
                            0, st, p.d_ufrb, p.d_upd_part, f, x_next);
         return hipGetLastError();
