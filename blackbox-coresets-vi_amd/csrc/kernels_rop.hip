@@ -29,9 +29,14 @@ namespace psvi {
 
 struct RopArgs {
     int L, M, S, n_tot, family, rc, maxd;
+    int nsplit;  // workgroups per sample (row halves); 2: G / G_dot added onto zeroed buffers,
+                 // two addends, so the sum is exact-order independent
     int din[kMaxL], dout[kMaxL], woff[kMaxL];
     int64_t poff[kMaxL], eoff[kMaxL];
     int lx, lxd, lg, lgd, lh[kMaxL + 1], lhd[kMaxL + 1], ld0, ld1, ldd0, ldd1;  // LDS carve
+    // W_l / W_dot_l in LDS: rows of an odd stride ldw[l] (a lane per output row
+    // then hits its own bank), layer l at xo[l] of the X / XD regions, b after W
+    int ldw[kMaxL], xo[kMaxL];
     const float* u;
     const int32_t* z;
     const float* w;
@@ -46,7 +51,7 @@ struct RopArgs {
     float* nlld;       // [S][M]
 };
 
-__global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
+__global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     const int L = a.L, D = a.din[0], C = a.dout[L - 1];
@@ -72,15 +77,19 @@ __global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
                 xv = a.params[pm] + softplus_f(rho) * e;
                 xdv = a.vec[pm] + sigmoid_f(rho) * a.vec[pr] * e;
             }
-            X[o] = xv;
-            XD[o] = xdv;
+            const int dst = a.xo[l] + (i < nw ? (i / din) * a.ldw[l] + i % din
+                                              : dout * a.ldw[l] + (i - nw));
+            X[dst] = xv;
+            XD[dst] = xdv;
             GA[o] = 0.f;
             GDA[o] = 0.f;
         }
     }
     __syncthreads();
-    for (int m0 = 0; m0 < a.M; m0 += a.rc) {
-        const int rc = min(a.rc, a.M - m0);
+    const int rows_per = (a.M + a.nsplit - 1) / a.nsplit;
+    const int m_lo = blockIdx.y * rows_per, m_hi = min(a.M, m_lo + rows_per);
+    for (int m0 = m_lo; m0 < m_hi; m0 += a.rc) {
+        const int rc = min(a.rc, m_hi - m0);
         // inputs: h_0 = u rows, h_dot_0 = 0
         for (int i = tid; i < rc * D; i += nt) {
             sm[a.lh[0] + i] = a.u[(int64_t)m0 * D + i];
@@ -89,11 +98,11 @@ __global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
         __syncthreads();
         // forward + tangent forward
         for (int l = 0; l < L; ++l) {
-            const int din = a.din[l], dout = a.dout[l];
-            const float* W = X + a.woff[l];
-            const float* Wd = XD + a.woff[l];
-            const float* b = W + din * dout;
-            const float* bd = Wd + din * dout;
+            const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
+            const float* W = X + a.xo[l];
+            const float* Wd = XD + a.xo[l];
+            const float* b = W + dout * ldw;
+            const float* bd = Wd + dout * ldw;
             const float* H = sm + a.lh[l];
             const float* HD = sm + a.lhd[l];
             float* Hn = sm + a.lh[l + 1];
@@ -103,9 +112,9 @@ __global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
                 float acc = b[o], accd = bd[o];
                 for (int i = 0; i < din; ++i) {
                     const float h = H[m * din + i], hd = HD[m * din + i];
-                    const float wv = W[o * din + i];
+                    const float wv = W[o * ldw + i];
                     acc = fmaf(h, wv, acc);
-                    accd = fmaf(hd, wv, fmaf(h, Wd[o * din + i], accd));
+                    accd = fmaf(hd, wv, fmaf(h, Wd[o * ldw + i], accd));
                 }
                 if (l < L - 1) {
                     Hn[q] = acc > 0.f ? acc : 0.f;
@@ -146,9 +155,9 @@ __global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
         __syncthreads();
         // R-backward
         for (int l = L - 1; l >= 0; --l) {
-            const int din = a.din[l], dout = a.dout[l], nw = din * dout;
-            const float* W = X + a.woff[l];
-            const float* Wd = XD + a.woff[l];
+            const int din = a.din[l], dout = a.dout[l], nw = din * dout, ldw = a.ldw[l];
+            const float* W = X + a.xo[l];
+            const float* Wd = XD + a.xo[l];
             const float* H = sm + a.lh[l];
             const float* HD = sm + a.lhd[l];
             float* GW = GA + a.woff[l];
@@ -183,9 +192,9 @@ __global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
                     float t = 0.f, td = 0.f;
                     for (int o = 0; o < dout; ++o) {
                         const float dl = Dl[m * a.maxd + o], ddl = DDl[m * a.maxd + o];
-                        const float wv = W[o * din + i];
+                        const float wv = W[o * ldw + i];
                         t = fmaf(dl, wv, t);
-                        td = fmaf(ddl, wv, fmaf(dl, Wd[o * din + i], td));
+                        td = fmaf(ddl, wv, fmaf(dl, Wd[o * ldw + i], td));
                     }
                     if (l > 0) {
                         const bool on = H[q] > 0.f;
@@ -202,8 +211,13 @@ __global__ __launch_bounds__(256) void net_rop_kernel(RopArgs a) {
         }
     }
     for (int o = tid; o < a.n_tot; o += nt) {
-        a.G[(int64_t)s * a.n_tot + o] = GA[o];
-        a.Gd[(int64_t)s * a.n_tot + o] = GDA[o];
+        if (a.nsplit == 1) {
+            a.G[(int64_t)s * a.n_tot + o] = GA[o];
+            a.Gd[(int64_t)s * a.n_tot + o] = GDA[o];
+        } else {
+            atomicAdd(a.G + (int64_t)s * a.n_tot + o, GA[o]);
+            atomicAdd(a.Gd + (int64_t)s * a.n_tot + o, GDA[o]);
+        }
     }
 }
 
@@ -304,8 +318,14 @@ static size_t rop_carve(const psvi_plan& p, int rc, RopArgs* a) {
     };
     int maxd = 0;
     for (int l = 0; l < p.L; ++l) maxd = std::max(maxd, std::max(p.lay[l].din, p.lay[l].dout));
-    maxd = rup4(maxd);
-    const int lx = take(p.n_tot), lxd = take(p.n_tot), lg = take(p.n_tot), lgd = take(p.n_tot);
+    maxd = rup4(maxd) | 1;  // odd row stride of the delta buffers
+    int xo[kMaxL], ldw[kMaxL], xtot = 0;
+    for (int l = 0; l < p.L; ++l) {
+        ldw[l] = p.lay[l].din | 1;
+        xo[l] = xtot;
+        xtot += p.lay[l].dout * ldw[l] + p.lay[l].dout;
+    }
+    const int lx = take(xtot), lxd = take(xtot), lg = take(p.n_tot), lgd = take(p.n_tot);
     int lh[kMaxL + 1], lhd[kMaxL + 1];
     for (int l = 0; l <= p.L; ++l) {
         const int d = l < p.L ? p.lay[l].din : p.lay[p.L - 1].dout;
@@ -316,6 +336,7 @@ static size_t rop_carve(const psvi_plan& p, int rc, RopArgs* a) {
     const int ldd0 = take((size_t)rc * maxd), ldd1 = take((size_t)rc * maxd);
     if (a) {
         a->lx = lx; a->lxd = lxd; a->lg = lg; a->lgd = lgd;
+        for (int l = 0; l < p.L; ++l) { a->xo[l] = xo[l]; a->ldw[l] = ldw[l]; }
         for (int l = 0; l <= p.L; ++l) { a->lh[l] = lh[l]; a->lhd[l] = lhd[l]; }
         a->ld0 = ld0; a->ld1 = ld1; a->ldd0 = ldd0; a->ldd1 = ldd1;
         a->maxd = maxd;
@@ -378,7 +399,15 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     a.u = u; a.z = z; a.w = w; a.x = x; a.xd = xd;
     a.params = params; a.vec = vec; a.eps = eps;
     a.G = G; a.Gd = Gd; a.du = du; a.nlld = nlld;
-    hipLaunchKernelGGL(net_rop_kernel, dim3(p.d.S), dim3(256), lds, st, a);
+    // two workgroups per sample while the samples alone leave CUs idle
+    a.nsplit = (p.d.S < 256 && p.d.M > 1) ? 2 : 1;
+    if (a.nsplit > 1) {
+        const size_t bytes = sizeof(float) * (size_t)p.d.S * p.n_tot;
+        hipError_t e = hipMemsetAsync(G, 0, bytes, st);
+        if (e == hipSuccess) e = hipMemsetAsync(Gd, 0, bytes, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(net_rop_kernel, dim3(p.d.S, a.nsplit), dim3(512), lds, st, a);
     return hipGetLastError();
 }
 
