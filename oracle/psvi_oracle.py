@@ -806,3 +806,176 @@ def evaluate_batch(family, layers, params, X, z, w_pseudo, n_pseudo, eps, S, cor
     ent = float(-(W[W > 0] * np.log(W[W > 0])).sum())
     ness = float(W.sum() ** 2 / (W ** 2).sum() / S)
     return correct, float(-np.log(q).sum()), ent, ness, probs
+
+
+# ------------------------------------------------------------------ LeNet
+# make_lenet (psvi/models/neural_net.py:334-359) with the default VI classes:
+#   VIConv2d(1,6,5,pad 2) ReLU BatchMaxPool2d(2)  VIConv2d(6,16,5) ReLU BatchMaxPool2d(2)
+#   Flatten  VILinear(400,120) ReLU  VILinear(120,84) ReLU  VILinear(84,10)
+# The convs and the first two linears carry the model's mc_samples (S weight
+# sets); the last linear keeps the default mc_samples=1: ONE shared sample
+# (weight batch shape (), neural_net.py:164-170).  inner_elbo's KL sums over
+# VILinear modules only (psvi_classes.py:506-510): the conv layers have none.
+LENET_LAYERS = [  # (n_weight, n_bias, batched over S, has KL)
+    (150, 6, True, False), (2400, 16, True, False),
+    (48000, 120, True, True), (10080, 84, True, True), (840, 10, False, True)]
+
+
+def lenet_param_count():
+    return 2 * sum(nw + nb for nw, nb, _, _ in LENET_LAYERS)
+
+
+def lenet_eps_count(S):
+    return sum((S if bat else 1) * (nw + nb) for nw, nb, bat, _ in LENET_LAYERS)
+
+
+def _windows(x, k):
+    """(..., H, W) -> (..., H-k+1, W-k+1, k, k) sliding views."""
+    return np.lib.stride_tricks.sliding_window_view(x, (k, k), axis=(-2, -1))
+
+
+def _conv(x, W, b, pad):
+    """Per-sample conv: x (S,M,Ci,H,W), W (S,Co,Ci,k,k), b (S,Co).  Equal to
+    VIConv2d.forward's grouped conv over the S-repeated input (neural_net.py:202-246)."""
+    k = W.shape[-1]
+    xp = np.pad(x, [(0, 0)] * 3 + [(pad, pad)] * 2)
+    return (np.einsum("smchwij,socij->smohw", _windows(xp, k), W, optimize=True)
+            + b[:, None, :, None, None])
+
+
+def _relu_pool(a):
+    """relu then 2x2/2 max-pool (BatchMaxPool2d, neural_net.py:249-255); returns
+    the pooled map and the gradient route: flat window index (row-major, the
+    first maximum, as torch's max_pool2d) or -1 where relu kills it."""
+    S, M, C, H, W = a.shape
+    win = a.reshape(S, M, C, H // 2, 2, W // 2, 2).transpose(0, 1, 2, 3, 5, 4, 6)
+    win = win.reshape(S, M, C, H // 2, W // 2, 4)
+    r = np.maximum(win, 0.0)
+    arg = r.argmax(-1)
+    out = np.take_along_axis(r, arg[..., None], -1)[..., 0]
+    arg = np.where(out > 0, arg, -1)
+    return out, arg
+
+
+def _unpool(g, arg, H, W):
+    S, M, C, h, w = g.shape
+    full = np.zeros((S, M, C, h, w, 4))
+    ok = arg >= 0
+    np.put_along_axis(full, np.where(ok, arg, 0)[..., None], np.where(ok, g, 0.0)[..., None], -1)
+    full = full.reshape(S, M, C, h, w, 2, 2).transpose(0, 1, 2, 3, 5, 4, 6)
+    return full.reshape(S, M, C, H, W)
+
+
+def lenet_sample(params, eps, S):
+    """W_s = mu + softplus(rho) eps_s per layer (VIMixin.rsample, neural_net.py:155-162)."""
+    params = np.asarray(params, np.float64)
+    eps = np.asarray(eps, np.float64)
+    out, po, eo = [], 0, 0
+    for nw, nb, bat, _ in LENET_LAYERS:
+        n = nw + nb
+        mu, rho = params[po:po + n], params[po + n:po + 2 * n]
+        ns = S if bat else 1
+        e_w = eps[eo:eo + ns * nw].reshape(ns, nw)
+        e_b = eps[eo + ns * nw:eo + ns * n].reshape(ns, nb)
+        E = np.concatenate([e_w, e_b], 1)
+        out.append(dict(po=po, n=n, nw=nw, mu=mu, rho=rho, E=E, bat=bat,
+                        X=mu[None] + softplus(rho)[None] * E))
+        po += 2 * n
+        eo += ns * n
+    return out
+
+
+def lenet_forward(Xl, u, S):
+    """LeNet forward over (S, M) images u (M,1,28,28); returns (logits, cache)."""
+    u = np.asarray(u, np.float64).reshape(-1, 1, 28, 28)
+    M = u.shape[0]
+    c1, c2, f1, f2, f3 = Xl
+    W1, b1 = c1["X"][:, :150].reshape(S, 6, 1, 5, 5), c1["X"][:, 150:]
+    W2, b2 = c2["X"][:, :2400].reshape(S, 16, 6, 5, 5), c2["X"][:, 2400:]
+    x0 = np.broadcast_to(u[None], (S, M, 1, 28, 28))
+    a1 = _conv(x0, W1, b1, 2)
+    p1, g1 = _relu_pool(a1)
+    a2 = _conv(p1, W2, b2, 0)
+    p2, g2 = _relu_pool(a2)
+    x = p2.reshape(S, M, 400)
+    Wf = [f1["X"][:, :48000].reshape(S, 120, 400), f2["X"][:, :10080].reshape(S, 84, 120),
+          np.broadcast_to(f3["X"][:, :840].reshape(1, 10, 84), (S, 10, 84))]
+    bf = [f1["X"][:, 48000:], f2["X"][:, 10080:], np.broadcast_to(f3["X"][:, 840:], (S, 10))]
+    hs = [x]
+    for l in range(3):
+        a = np.einsum("smi,soi->smo", hs[-1], Wf[l]) + bf[l][:, None, :]
+        hs.append(np.maximum(a, 0.0) if l < 2 else a)
+    cache = dict(x0=x0, W1=W1, W2=W2, p1=p1, g1=g1, g2=g2, Wf=Wf, hs=hs)
+    return hs[-1], cache
+
+
+def lenet_elbo_grad(params, u, z, w, eps, S, prior_sd=1.0):
+    """Negative inner ELBO (psvi_classes.py:488-511) of a make_lenet model and
+    its gradient w.r.t. the flat parameter vector (parameters_to_vector order:
+    per layer weight, bias, _weight_sd, _bias_sd)."""
+    params = np.asarray(params, np.float64)
+    s0 = float(prior_sd)
+    Xl = lenet_sample(params, eps, S)
+    logits, c = lenet_forward(Xl, u, S)
+    M = logits.shape[1]
+    w = np.asarray(w, np.float64)
+    zi = np.asarray(z).astype(np.int64)
+    mx = logits.max(-1, keepdims=True)
+    e = np.exp(logits - mx)
+    lse = mx[..., 0] + np.log(e.sum(-1))
+    nll = lse - logits[:, np.arange(M), zi]
+    data = float((nll @ w).sum())
+    P = e / e.sum(-1, keepdims=True)
+    P[:, np.arange(M), zi] -= 1.0
+    d = P * w[None, :, None]                                      # d logits
+    hs, Wf = c["hs"], c["Wf"]
+    G = [None] * 5
+    for l in (2, 1, 0):
+        dW = np.einsum("smo,smi->soi", d, hs[l])
+        db = d.sum(1)
+        G[2 + l] = np.concatenate([dW.reshape(S, -1), db], 1)
+        d = np.einsum("smo,soi->smi", d, Wf[l])
+        if l > 0:
+            d = d * (hs[l] > 0)
+    dp2 = d.reshape(S, M, 16, 5, 5)
+    da2 = _unpool(dp2, c["g2"], 10, 10)
+    dW2 = np.einsum("smohw,smchwij->socij", da2, _windows(c["p1"], 5), optimize=True)
+    G[1] = np.concatenate([dW2.reshape(S, -1), da2.sum((1, 3, 4))], 1)
+    da2p = np.pad(da2, [(0, 0)] * 3 + [(4, 4)] * 2)
+    dp1 = np.einsum("smohwij,socij->smchw", _windows(da2p, 5), c["W2"][..., ::-1, ::-1],
+                    optimize=True)
+    da1 = _unpool(dp1, c["g1"], 28, 28)
+    x0p = np.pad(c["x0"], [(0, 0)] * 3 + [(2, 2)] * 2)
+    dW1 = np.einsum("smohw,smchwij->socij", da1, _windows(x0p, 5), optimize=True)
+    G[0] = np.concatenate([dW1.reshape(S, -1), da1.sum((1, 3, 4))], 1)
+    G[4] = G[4].sum(0, keepdims=True)                             # shared sample
+    grad = np.zeros_like(params)
+    kl = 0.0
+    for (nw, nb, bat, has_kl), x, g in zip(LENET_LAYERS, Xl, G):
+        po, n, mu, rho = x["po"], x["n"], x["mu"], x["rho"]
+        sp = softplus(rho)
+        gmu = g.sum(0)
+        grho = (g * x["E"]).sum(0)
+        if has_kl:
+            vr = (sp / s0) ** 2
+            kl += float((0.5 * (vr + (mu / s0) ** 2 - 1.0 - np.log(vr))).sum())
+            gmu = gmu + mu / s0 ** 2
+            grho = grho + sp / s0 ** 2 - 1.0 / sp
+        grad[po:po + n] = gmu
+        grad[po + n:po + 2 * n] = grho * sigmoid(rho)
+    return data + kl, grad
+
+
+def lenet_inner_loop(params0, u, z, w, eps_steps, S, lr, adam_kind, prior_sd=1.0, t0=1):
+    """T lenet inner steps (run_inner_loop's contract)."""
+    p = np.asarray(params0, dtype=np.float64).copy()
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    elbos, grads, traj = [], [], []
+    for k, e in enumerate(eps_steps):
+        val, g = lenet_elbo_grad(p, u, z, w, e, S, prior_sd)
+        elbos.append(val)
+        grads.append(g)
+        p, m, v = adam(adam_kind, p, g, m, v, t0 + k, lr)
+        traj.append(p.copy())
+    return np.array(elbos), grads, traj, m, v

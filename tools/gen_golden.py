@@ -321,6 +321,29 @@ def _child():
     run_nested("g5_logreg_fullcov", "mvn", model, PSVILearnV, u, z, torch.zeros(10), 800,
                1e-3, 3, 110, dict(S=4, note="logistic_regression_fullcov"))
 
+    # L1/L2: lenet (make_lenet, neural_net.py:334-359): VIConv2d + BatchMaxPool2d +
+    # VILinear, the last layer one shared sample (its default mc_samples=1,
+    # init_sd=0.01); MNIST-shaped u.  cfg["layers"] lists the VILinear layers only.
+    from psvi.models.neural_net import make_lenet
+
+    torch.manual_seed(0)
+    u6 = torch.randn(4, 1, 28, 28, generator=gen)
+    z6 = torch.tensor([1.0, 7.0, 3.0, 9.0])
+    model = make_lenet(mc_samples=3, init_sd=0.05)
+    perturb(model, gen, 0.15, -4.0, -2.0, 0.0)
+    run_nested("l1_lenet_tiny", "lenet", model, PSVILearnV, u6, z6, torch.zeros(4), 60000,
+               1e-3, 2, 120, dict(S=3, note="lenet (C5 architecture), M=4, S=3"))
+
+    torch.manual_seed(0)
+    u7 = torch.randn(6, 1, 28, 28, generator=gen)
+    z7 = torch.tensor([0.0, 2.0, 4.0, 6.0, 8.0, 5.0])
+    model = make_lenet(mc_samples=2, init_sd=0.05)
+    perturb(model, gen, 0.2, -3.5, -2.0, 0.0)
+    v7 = 0.3 * torch.randn(6, generator=gen)
+    run_hyper("l2_lenet_hyper", "lenet", model, PSVIAV, u7, z7, v7, 60000, 1e-3, 2, 130,
+              dict(S=2, f="exp_alpha_softmax", alpha=0.1, note="lenet hyper, PSVIAV"),
+              alpha=0.1)
+
 
 def main():
     if "--child" in sys.argv:
