@@ -51,6 +51,7 @@ int hip_fail(hipError_t e, const char* where) {
     } while (0)
 
 constexpr int kFwdKChunk = 256;  // columns of L per forward work item
+constexpr int64_t kLenetRowFloats = 1176 + 400 * 2 + 120 * 2 + 84 * 2 + 10;  // per (s, m)
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -137,7 +138,50 @@ static std::vector<UpdChunk> xcd_order(const std::vector<UpdChunk>& in) {
     return out;
 }
 
+// make_lenet (neural_net.py:334-359): five mean-field-style layers, the first
+// two convolutions ("din" = in_channels * 25), the last one a single shared
+// sample.  Samples are sharded like the mean-field family.
+int build_lenet_plan(psvi_plan& p) {
+    static const int din[5] = {25, 150, 400, 120, 84}, dout[5] = {6, 16, 120, 84, 10};
+    const int S = p.d.S;
+    p.d.n_layers = 5;
+    p.d.dims[0] = 784;
+    for (int l = 0; l < 5; ++l) p.d.dims[l + 1] = dout[l];
+    p.L = 5;
+    int64_t po = 0, eo = 0;
+    int wo = 0;
+    for (int l = 0; l < 5; ++l) {
+        LayerInfo& li = p.lay[l];
+        li.din = din[l];
+        li.dout = dout[l];
+        li.n = din[l] * dout[l] + dout[l];
+        li.nc = 0;
+        li.poff = po;
+        li.eoff = eo;
+        li.woff = wo;
+        po += 2 * (int64_t)li.n;
+        eo += (l < 4 ? (int64_t)S : 1) * li.n;
+        wo += li.n;
+    }
+    p.P = po;
+    p.Peps = eo;
+    p.n_tot = wo;
+    for (int q = 0; q < p.world; ++q) {
+        const int base = S / p.world, rem = S % p.world;
+        p.s_cnt[q] = base + (q < rem ? 1 : 0);
+        p.s_off[q] = q * base + std::min(q, rem);
+        p.rows_tot[q] = 0;
+    }
+    p.acc_count = 2 * (int64_t)p.n_tot;
+    p.ws_bytes = align256(sizeof(float) * (size_t)p.acc_count);
+    const int64_t kMaxOff = (int64_t(1) << 31) - 4096;
+    if (p.Peps > kMaxOff || (int64_t)p.s_cnt[p.rank] * p.d.M * kLenetRowFloats > kMaxOff * 4)
+        return fail(PSVI_EUNSUP, "LeNet scratch beyond the supported size");
+    return 0;
+}
+
 int build_plan(psvi_plan& p) {
+    if (p.family == PSVI_FAMILY_LENET) return build_lenet_plan(p);
     const psvi_net_desc& d = p.d;
     p.L = d.n_layers;
     int64_t po = 0, eo = 0;
@@ -342,9 +386,18 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                      psvi_plan** out) {
     if (!out) return fail(PSVI_EINVAL, "null out");
     *out = nullptr;
-    if (int rc = check_desc(d)) return rc;
-    if (family != PSVI_FAMILY_MEANFIELD && family != PSVI_FAMILY_FULLCOV)
+    if (family != PSVI_FAMILY_MEANFIELD && family != PSVI_FAMILY_FULLCOV &&
+        family != PSVI_FAMILY_LENET)
         return fail(PSVI_EINVAL, "unknown family");
+    psvi_net_desc dl;
+    if (family == PSVI_FAMILY_LENET && d) {  // fixed architecture: dims ignored
+        dl = *d;
+        dl.n_layers = 5;
+        const int dims[6] = {784, 6, 16, 120, 84, 10};
+        for (int l = 0; l < 6; ++l) dl.dims[l] = dims[l];
+        d = &dl;
+    }
+    if (int rc = check_desc(d)) return rc;
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world)
         return fail(PSVI_EINVAL, "world/rank out of range (world <= 8)");
     int ndev = 0;
@@ -375,6 +428,11 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                 hipMalloc((void**)&p->d_upd_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the fused-sample scratch");
         }
+        if (!rc && family == PSVI_FAMILY_LENET) {
+            const size_t bytes = lenet_ws(*p, nullptr).bytes;
+            if (hipMalloc(&p->d_lenet_ws, bytes) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the LeNet activation scratch");
+        }
         p->on_device = rc == 0;
     }
     if (rc) {
@@ -393,6 +451,7 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_ufrb) (void)hipFree(p->d_ufrb);
     if (p->d_upd_part) (void)hipFree(p->d_upd_part);
     if (p->d_upd) (void)hipFree(p->d_upd);
+    if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);
     delete p;
     return 0;
 }
@@ -519,7 +578,11 @@ static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const
                      int include_kl, void* ws, hipStream_t st) {
     HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double), st));
     char* wsb = (char*)ws;
-    if (p->family == PSVI_FAMILY_MEANFIELD) {
+    if (p->family == PSVI_FAMILY_LENET) {
+        float* acc = (float*)wsb;
+        HIP_TRY(launch_lenet(*p, u, z, w, params, eps, acc, elbo_out, p->d_lenet_ws, st));
+        HIP_TRY(launch_mf_update(*p, acc, params, m, v, hp, elbo_out, grad_out, include_kl, st));
+    } else if (p->family == PSVI_FAMILY_MEANFIELD) {
         float* acc = (float*)wsb;
         HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
         HIP_TRY(launch_net(*p, u, z, w, params, eps, acc, acc + p->n_tot, nullptr, nullptr,
@@ -562,11 +625,15 @@ int psvi_elbo_grad(const psvi_plan* p, const float* u, const int32_t* z, const f
 int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* z,
                              const float* w, const float* eps, const float* params, float* acc,
                              double* nll_out, void* stream) {
-    if (!p || p->family != PSVI_FAMILY_MEANFIELD) return fail(PSVI_ESTATE, "not a mean-field plan");
+    if (!p || p->family == PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a mean-field plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!u || !z || !w || !eps || !params || !acc || !nll_out)
         return fail(PSVI_EINVAL, "null pointer");
     hipStream_t st = as_stream(stream);
+    if (p->family == PSVI_FAMILY_LENET) {
+        HIP_TRY(launch_lenet(*p, u, z, w, params, eps, acc, nll_out, p->d_lenet_ws, st));
+        return 0;
+    }
     HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
     HIP_TRY(launch_net(*p, u, z, w, params, eps, acc, acc + p->n_tot, nullptr, nullptr, nll_out,
                        st));
@@ -576,7 +643,7 @@ int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* 
 int psvi_mf_phase_update(const psvi_plan* p, const float* acc, float* params, float* adam_m,
                          float* adam_v, const psvi_adam_hp* hp, double* kl_out,
                          float* grad_out, int32_t include_kl, void* stream) {
-    if (!p || p->family != PSVI_FAMILY_MEANFIELD) return fail(PSVI_ESTATE, "not a mean-field plan");
+    if (!p || p->family == PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a mean-field plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!acc || !params) return fail(PSVI_EINVAL, "null pointer");
     if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
@@ -702,7 +769,7 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
                                                                                          : nullptr;
     };
     psvi_adam_hp h = *hp;
-    if (p->family == PSVI_FAMILY_MEANFIELD) {
+    if (p->family != PSVI_FAMILY_FULLCOV) {
         for (int t = 0; t < T; ++t) {
             const float* e = eps_t(t);
             if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
@@ -756,6 +823,8 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
                          float* grad_u, float* grad_w, double* sample_out, void* ws,
                          size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (p->family == PSVI_FAMILY_LENET)
+        return fail(PSVI_EUNSUP, "LeNet plans run the inner loop only (outer objective: not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "the outer objective needs world == 1");
     if (p->d.S < 2) return fail(PSVI_EINVAL, "psvi_elbo needs S > 1 (psvi_classes.py:449)");
@@ -817,6 +886,8 @@ int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, cons
                   const float* w_all, const float* eps, const float* params, int32_t correction,
                   float* probs_out, double* stats_out, void* ws, size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (p->family == PSVI_FAMILY_LENET)
+        return fail(PSVI_EUNSUP, "LeNet plans run the inner loop only (outer objective: not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "evaluate needs world == 1");
     if (p->d.S < 2) return fail(PSVI_EINVAL, "evaluate needs S > 1 (psvi_classes.py:1036)");
@@ -849,6 +920,8 @@ int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* 
              const float* eps, const float* params, const float* vec, float* hv_out,
              float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (p->family == PSVI_FAMILY_LENET)
+        return fail(PSVI_EUNSUP, "LeNet plans run the inner loop only (outer objective: not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "psvi_hvp needs world == 1");
     if (!u || !z || !w || !eps || !params || !vec || !hv_out)

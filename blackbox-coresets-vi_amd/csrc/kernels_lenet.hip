@@ -1,0 +1,595 @@
+// kernels_lenet.hip -- the coreset-ELBO inner step of make_lenet (config C5):
+// per-sample VIConv2d + BatchMaxPool2d towers, the VILinear head as batched
+// GEMMs, weighted NLL, and the hand-derived backward down to the per-sample
+// weight gradients.  The parameter update (KL on the VILinear layers only,
+// Adam) is the mean-field mf_update_kernel with a layer mask.
+//
+// Reference (/root/reference):
+//   make_lenet            psvi/models/neural_net.py:334-359
+//   VIConv2d.forward      neural_net.py:202-246 (grouped conv over the S-repeated
+//                         input == one conv per sample with its own weights)
+//   BatchMaxPool2d        neural_net.py:249-255 (2x2/2 max-pool per (s, m) map)
+//   VILinear.forward      neural_net.py:176-179; the last layer's mc_samples=1
+//                         gives ONE shared weight sample (neural_net.py:164-170)
+//   inner_elbo            psvi/inference/psvi_classes.py:488-511
+//
+// Layout (per sample s, floats, the plan's woff order = parameter order):
+//   conv1 W [6][1][5][5] b[6] | conv2 W [16][6][5][5] b[16] | fc1 W [120][400]
+//   b[120] | fc2 W [84][120] b[84] | fc3 W [10][84] b[10]        (n_tot = 61706)
+// Activations, row (s, m) major: P1 [S][M][6][14][14] (pooled conv1, kept for
+// conv2's weight gradient), route1/route2 int8 (pool window index of the first
+// maximum, -1 where relu zeroes it), X2 [S][M][400], H1 [S][M][120],
+// H2 [S][M][84], D [S][M][10] (logits, then d logits).
+#include "psvi_internal.hpp"
+
+namespace psvi {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kNConv = 2572;  // conv1 W+b, conv2 W+b: the per-sample conv block
+constexpr int kP1 = 1176;     // 6 x 14 x 14
+constexpr int kX2 = 400;      // 16 x 5 x 5
+
+// ------------------------------------------------------------ weight draw
+struct SampleArgs {
+    int L, n_tot, S_loc, s_off, S_tot;
+    int woff[kMaxL + 1], nw[kMaxL], n[kMaxL], batched[kMaxL];
+    int64_t poff[kMaxL], eoff[kMaxL];
+};
+
+__device__ __forceinline__ int64_t lenet_eps_index(const SampleArgs& a, int l, int idx, int sg) {
+    if (!a.batched[l]) return a.eoff[l] + idx;
+    const int nw = a.nw[l];
+    return idx < nw ? a.eoff[l] + (int64_t)sg * nw + idx
+                    : a.eoff[l] + (int64_t)a.S_tot * nw + (int64_t)sg * (a.n[l] - nw) + (idx - nw);
+}
+
+__device__ __forceinline__ int lenet_layer(const SampleArgs& a, int j) {
+    int l = 0;
+    while (l + 1 < a.L && j >= a.woff[l + 1]) ++l;
+    return l;
+}
+
+// Wsamp[s][j] = mu_j + softplus(rho_j) eps_(s, j)   (VIMixin.rsample, neural_net.py:155-162)
+__global__ __launch_bounds__(kThreads) void lenet_sample_kernel(SampleArgs a,
+                                                                const float* __restrict__ params,
+                                                                const float* __restrict__ eps,
+                                                                float* __restrict__ wsamp) {
+    const int64_t total = (int64_t)a.S_loc * a.n_tot;
+    for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * kThreads) {
+        const int s = (int)(i / a.n_tot), j = (int)(i - (int64_t)s * a.n_tot);
+        const int l = lenet_layer(a, j);
+        const int idx = j - a.woff[l];
+        const float mu = params[a.poff[l] + idx], rho = params[a.poff[l] + a.n[l] + idx];
+        wsamp[i] = mu + softplus_f(rho) * eps[lenet_eps_index(a, l, idx, a.s_off + s)];
+    }
+}
+
+// acc[j] = sum_s dW[s][j],  acc[n_tot + j] = sum_s dW[s][j] eps_(s, j)
+__global__ __launch_bounds__(kThreads) void lenet_acc_kernel(SampleArgs a,
+                                                             const float* __restrict__ eps,
+                                                             const float* __restrict__ dws,
+                                                             float* __restrict__ acc) {
+    const int j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.n_tot) return;
+    const int l = lenet_layer(a, j);
+    const int idx = j - a.woff[l];
+    float g = 0.f, ge = 0.f;
+    for (int s = 0; s < a.S_loc; ++s) {
+        const float d = dws[(int64_t)s * a.n_tot + j];
+        g += d;
+        ge += d * eps[lenet_eps_index(a, l, idx, a.s_off + s)];
+    }
+    acc[j] = g;
+    acc[a.n_tot + j] = ge;
+}
+
+// ------------------------------------------------------- conv towers, fwd
+struct ConvArgs {
+    int M, n_tot, nchunk, chunk;
+    const float* u;       // [M][28][28]
+    const float* wsamp;   // [S][n_tot]
+    float* p1;            // [S][M][1176]
+    int8_t* r1;           // [S][M][1176]
+    float* x2;            // [S][M][400]
+    int8_t* r2;           // [S][M][400]
+    const float* dx2;     // bwd: [S][M][400]
+    float* part;          // bwd: [S][nchunk][2572]
+};
+
+// relu + first-max 2x2 pool of four conv values in window order (0,0) (0,1)
+// (1,0) (1,1): torch's max_pool2d keeps the first maximum; the gradient of a
+// window whose maximum is <= 0 dies in relu's backward (route -1).
+__device__ __forceinline__ float relu_pool4(float a0, float a1, float a2, float a3, int8_t& r) {
+    float m = a0;
+    int k = 0;
+    if (a1 > m) { m = a1; k = 1; }
+    if (a2 > m) { m = a2; k = 2; }
+    if (a3 > m) { m = a3; k = 3; }
+    r = m > 0.f ? (int8_t)k : (int8_t)-1;
+    return m > 0.f ? m : 0.f;
+}
+
+__global__ __launch_bounds__(kThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
+    __shared__ float w1[150], b1[6], w2[2400], b2[16];
+    __shared__ float in[32 * 32];       // 28x28 image, zero padding 2
+    __shared__ float p1[kP1];
+    __shared__ float a2[1600];          // conv2 pre-activation [16][10][10]
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    for (int i = tid; i < kNConv; i += kThreads) {
+        const float v = ws[i];
+        if (i < 150) w1[i] = v;
+        else if (i < 156) b1[i - 150] = v;
+        else if (i < 2556) w2[i - 156] = v;
+        else b2[i - 2556] = v;
+    }
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 1024; i += kThreads) {
+            const int y = (i >> 5) - 2, x = (i & 31) - 2;
+            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+        }
+        __syncthreads();
+        const int64_t row = (int64_t)s * a.M + m;
+        // conv1 (1 -> 6, 5x5, pad 2) + relu + pool: one pooled output per item
+        for (int o = tid; o < kP1; o += kThreads) {
+            const int c = o / 196, py = (o % 196) / 14, px = o % 14;
+            float patch[6][6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) patch[i][j] = in[(2 * py + i) * 32 + 2 * px + j];
+            float acc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = b1[c];
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const float wv = w1[c * 25 + i * 5 + j];
+                    acc[0] += wv * patch[i][j];
+                    acc[1] += wv * patch[i][j + 1];
+                    acc[2] += wv * patch[i + 1][j];
+                    acc[3] += wv * patch[i + 1][j + 1];
+                }
+            int8_t r;
+            const float v = relu_pool4(acc[0], acc[1], acc[2], acc[3], r);
+            p1[o] = v;
+            a.p1[row * kP1 + o] = v;
+            a.r1[row * kP1 + o] = r;
+        }
+        __syncthreads();
+        // conv2 (6 -> 16, 5x5): one pre-activation per item
+        for (int o = tid; o < 1600; o += kThreads) {
+            const int k = o / 100, y = (o % 100) / 10, x = o % 10;
+            float acc = b2[k];
+            for (int c = 0; c < 6; ++c) {
+                const float* pc = p1 + c * 196 + y * 14 + x;
+                const float* wk = w2 + k * 150 + c * 25;
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) acc += wk[i * 5 + j] * pc[i * 14 + j];
+            }
+            a2[o] = acc;
+        }
+        __syncthreads();
+        for (int o = tid; o < kX2; o += kThreads) {
+            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
+            const float* ak = a2 + k * 100 + 2 * py * 10 + 2 * px;
+            int8_t r;
+            const float v = relu_pool4(ak[0], ak[1], ak[10], ak[11], r);
+            a.x2[row * kX2 + o] = v;
+            a.r2[row * kX2 + o] = r;
+        }
+    }
+}
+
+// ------------------------------------------------------- conv towers, bwd
+// Given d X2 (the head's input gradient) per (s, m): route through pool2/relu,
+// accumulate conv2's weight gradient against P1, form d P1 (the transposed conv
+// restricted to the routed positions), route through pool1/relu, accumulate
+// conv1's weight gradient against the padded image.  Per-(s, chunk) partial
+// sums, reduced over chunks in fixed order by lenet_conv_reduce_kernel.
+__global__ __launch_bounds__(kThreads) void lenet_conv_bwd_kernel(ConvArgs a) {
+    __shared__ float w2[2400];
+    __shared__ float in[32 * 32];
+    __shared__ float p1[kP1];
+    __shared__ float g2[kX2];     // routed gradient of each pooled conv2 output
+    __shared__ int pos2[kX2];     // its conv2 position y * 10 + x
+    __shared__ float dp1[kP1];
+    __shared__ float g1[kP1];
+    __shared__ int pos1[kP1];     // routed conv1 position y * 28 + x
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    for (int i = tid; i < 2400; i += kThreads) w2[i] = ws[156 + i];
+    float accw2[10];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) accw2[r] = 0.f;
+    float acc1 = 0.f;  // tid < 150: conv1 weight; 150..155: conv1 bias; 156..171: conv2 bias
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        const int64_t row = (int64_t)s * a.M + m;
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 1024; i += kThreads) {
+            const int y = (i >> 5) - 2, x = (i & 31) - 2;
+            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+        }
+        for (int i = tid; i < kP1; i += kThreads) p1[i] = a.p1[row * kP1 + i];
+        for (int o = tid; o < kX2; o += kThreads) {
+            const int r = a.r2[row * kX2 + o];
+            const int py = (o % 25) / 5, px = o % 5;
+            g2[o] = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
+            const int rr = r >= 0 ? r : 0;
+            pos2[o] = (2 * py + (rr >> 1)) * 10 + 2 * px + (rr & 1);
+        }
+        __syncthreads();
+        // conv2 weight gradient: dW2[k][c][i][j] += sum_p g2[k][p] P1[c][y_p + i][x_p + j]
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            const int e = tid + r * kThreads;
+            if (e < 2400) {
+                const int k = e / 150, c = (e % 150) / 25, i = (e % 25) / 5, j = e % 5;
+                const float* pc = p1 + c * 196 + i * 14 + j;
+                float acc = 0.f;
+                for (int p = 0; p < 25; ++p) {
+                    const int q = pos2[k * 25 + p];
+                    acc += g2[k * 25 + p] * pc[(q / 10) * 14 + q % 10];
+                }
+                accw2[r] += acc;
+            }
+        }
+        if (tid >= 156 && tid < 172) {
+            const int k = tid - 156;
+            float acc = 0.f;
+            for (int p = 0; p < 25; ++p) acc += g2[k * 25 + p];
+            acc1 += acc;
+        }
+        // d P1[c][yy][xx] = sum_k sum_(routed (y, x) within the 5x5 window)
+        //                   g2 W2[k][c][yy - y][xx - x]
+        for (int o = tid; o < kP1; o += kThreads) {
+            const int c = o / 196, yy = (o % 196) / 14, xx = o % 14;
+            const int pylo = max(0, yy - 4) >> 1, pyhi = min(9, yy) >> 1;
+            const int pxlo = max(0, xx - 4) >> 1, pxhi = min(9, xx) >> 1;
+            float acc = 0.f;
+            for (int k = 0; k < 16; ++k) {
+                const float* wk = w2 + k * 150 + c * 25;
+                for (int py = pylo; py <= pyhi; ++py)
+                    for (int px = pxlo; px <= pxhi; ++px) {
+                        const int p = k * 25 + py * 5 + px;
+                        const int q = pos2[p];
+                        const int dy = yy - q / 10, dx = xx - q % 10;
+                        if (dy >= 0 && dy < 5 && dx >= 0 && dx < 5) acc += g2[p] * wk[dy * 5 + dx];
+                    }
+            }
+            dp1[o] = acc;
+        }
+        __syncthreads();
+        for (int o = tid; o < kP1; o += kThreads) {
+            const int r = a.r1[row * kP1 + o];
+            const int py = (o % 196) / 14, px = o % 14;
+            g1[o] = r >= 0 ? dp1[o] : 0.f;
+            const int rr = r >= 0 ? r : 0;
+            pos1[o] = (2 * py + (rr >> 1)) * 28 + 2 * px + (rr & 1);
+        }
+        __syncthreads();
+        // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
+        if (tid < 150) {
+            const int c = tid / 25, i = (tid % 25) / 5, j = tid % 5;
+            float acc = 0.f;
+            for (int p = 0; p < 196; ++p) {
+                const int q = pos1[c * 196 + p];
+                acc += g1[c * 196 + p] * in[(q / 28 + i) * 32 + q % 28 + j];
+            }
+            acc1 += acc;
+        } else if (tid < 156) {
+            const int c = tid - 150;
+            float acc = 0.f;
+            for (int p = 0; p < 196; ++p) acc += g1[c * 196 + p];
+            acc1 += acc;
+        }
+    }
+    float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
+    if (tid < 156) out[tid] = acc1;
+    else if (tid < 172) out[2556 + tid - 156] = acc1;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const int e = tid + r * kThreads;
+        if (e < 2400) out[156 + e] = accw2[r];
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void lenet_conv_reduce_kernel(int S_loc, int nchunk,
+                                                                     int n_tot,
+                                                                     const float* __restrict__ part,
+                                                                     float* __restrict__ dws) {
+    const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    if (i >= (int64_t)S_loc * kNConv) return;
+    const int s = (int)(i / kNConv), e = (int)(i % kNConv);
+    const float* p = part + (int64_t)s * nchunk * kNConv + e;
+    float g = 0.f;
+    for (int c = 0; c < nchunk; ++c) g += p[(int64_t)c * kNConv];
+    dws[(int64_t)s * n_tot + e] = g;
+}
+
+// ---------------------------------------------------------- head GEMMs
+// C[b](m, n) = sum_k A[b](m, k) B[b](k, n) with arbitrary element strides,
+// 64x64 tiles, k-steps of 16 through LDS, 4x4 outputs per thread (fp32 VALU:
+// the head is 1/7 of the step's flops).  Epilogue flags: 1 add bias[b][n],
+// 2 relu, 4 multiply by (mask[b](m, n) > 0) (relu's backward).
+struct GemmArgs {
+    int M, N, K;
+    const float* A; int64_t sAb; int sAm, sAk;
+    const float* B; int64_t sBb; int sBk, sBn;
+    float* C; int64_t sCb; int sCm;
+    int epi;
+    const float* bias; int64_t sbias;
+    const float* mask; int64_t sMb; int sMm;
+};
+
+__global__ __launch_bounds__(kThreads) void lenet_gemm_kernel(GemmArgs g) {
+    __shared__ float As[16][64 + 4];
+    __shared__ float Bs[16][64 + 4];
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64, b = blockIdx.z;
+    const float* A = g.A + b * g.sAb;
+    const float* B = g.B + b * g.sBb;
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    const bool a_kfast = g.sAk == 1, b_nfast = g.sBn == 1;
+    for (int k0 = 0; k0 < g.K; k0 += 16) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = tid + r * kThreads;
+            int mm, kk;
+            if (a_kfast) { kk = e & 15; mm = e >> 4; } else { mm = e & 63; kk = e >> 6; }
+            const int gm = m0 + mm, gk = k0 + kk;
+            As[kk][mm] = (gm < g.M && gk < g.K) ? A[(int64_t)gm * g.sAm + (int64_t)gk * g.sAk] : 0.f;
+            int nn, kb;
+            if (b_nfast) { nn = e & 63; kb = e >> 6; } else { kb = e & 15; nn = e >> 4; }
+            const int gn = n0 + nn, gkb = k0 + kb;
+            Bs[kb][nn] = (gn < g.N && gkb < g.K) ? B[(int64_t)gkb * g.sBk + (int64_t)gn * g.sBn] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            float av[4], bv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) av[i] = As[kk][ty * 4 + i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
+        }
+        __syncthreads();
+    }
+    float* C = g.C + b * g.sCb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + ty * 4 + i;
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + tx * 4 + j;
+            if (n >= g.N) continue;
+            float v = acc[i][j];
+            if (g.epi & 1) v += g.bias[b * g.sbias + n];
+            if (g.epi & 2) v = fmaxf(v, 0.f);
+            if (g.epi & 4) v = g.mask[b * g.sMb + (int64_t)m * g.sMm + n] > 0.f ? v : 0.f;
+            C[(int64_t)m * g.sCm + n] = v;
+        }
+    }
+}
+
+// out[b * sOb + n] = sum_m X[b][m][n]  (bias gradients; fixed order over m)
+__global__ __launch_bounds__(kThreads) void lenet_colsum_kernel(const float* __restrict__ X,
+                                                                int M, int N,
+                                                                float* __restrict__ out,
+                                                                int64_t sOb) {
+    const int b = blockIdx.x;
+    const float* x = X + (int64_t)b * M * N;
+    for (int n = threadIdx.x; n < N; n += kThreads) {
+        float acc = 0.f;
+        for (int m = 0; m < M; ++m) acc += x[(int64_t)m * N + n];
+        out[b * sOb + n] = acc;
+    }
+}
+
+// weighted NLL of each (s, m) row and d logits in place: w_m (softmax - onehot)
+__global__ __launch_bounds__(kThreads) void lenet_loss_kernel(int rows, int M,
+                                                              const int32_t* __restrict__ z,
+                                                              const float* __restrict__ w,
+                                                              float* __restrict__ D,
+                                                              double* __restrict__ nll_out) {
+    __shared__ float red[kThreads / kWave];
+    const int r = blockIdx.x * kThreads + threadIdx.x;
+    float contrib = 0.f;
+    if (r < rows) {
+        const int m = r % M;
+        float* d = D + (int64_t)r * 10;
+        float l[10];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) { l[c] = d[c]; mx = fmaxf(mx, l[c]); }
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) { l[c] = expf(l[c] - mx); se += l[c]; }
+        const int zc = min(max(z[m], 0), 9);  // ids are validated by the host
+        const float wm = w[m];
+        const float lse = mx + logf(se);
+        contrib = wm * (lse - d[zc]);
+        const float inv = 1.f / se;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) d[c] = wm * (l[c] * inv - (c == zc ? 1.f : 0.f));
+    }
+    const float tot = block_sum(contrib, red);
+    if (threadIdx.x == 0) atomicAdd(nll_out, (double)tot);
+}
+
+hipError_t gemm(const GemmArgs& g, int batch, hipStream_t st) {
+    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, batch);
+    hipLaunchKernelGGL(lenet_gemm_kernel, grid, dim3(kThreads), 0, st, g);
+    return hipGetLastError();
+}
+
+GemmArgs gemm_args(int M, int N, int K, const float* A, int64_t sAb, int sAm, int sAk,
+                   const float* B, int64_t sBb, int sBk, int sBn, float* C, int64_t sCb,
+                   int sCm) {
+    GemmArgs g{};
+    g.M = M; g.N = N; g.K = K;
+    g.A = A; g.sAb = sAb; g.sAm = sAm; g.sAk = sAk;
+    g.B = B; g.sBb = sBb; g.sBk = sBk; g.sBn = sBn;
+    g.C = C; g.sCb = sCb; g.sCm = sCm;
+    return g;
+}
+
+}  // namespace
+
+LenetWs lenet_ws(const psvi_plan& p, void* base) {
+    const int64_t S = p.s_cnt[p.rank], M = p.d.M;
+    LenetWs w{};
+    w.nchunk = lenet_nchunk(p);
+    size_t off = 0;
+    char* b = (char*)base;
+    auto take = [&](size_t bytes) -> void* {
+        void* r = b ? (void*)(b + off) : nullptr;
+        off += (bytes + 255) & ~size_t(255);
+        return r;
+    };
+    w.wsamp = (float*)take(sizeof(float) * S * p.n_tot);
+    w.dws = (float*)take(sizeof(float) * S * p.n_tot);
+    w.p1 = (float*)take(sizeof(float) * S * M * kP1);
+    w.r1 = (int8_t*)take(S * M * kP1);
+    w.x2 = (float*)take(sizeof(float) * S * M * kX2);
+    w.r2 = (int8_t*)take(S * M * kX2);
+    w.h1 = (float*)take(sizeof(float) * S * M * 120);
+    w.h2 = (float*)take(sizeof(float) * S * M * 84);
+    w.d = (float*)take(sizeof(float) * S * M * 10);
+    w.dh2 = (float*)take(sizeof(float) * S * M * 84);
+    w.dh1 = (float*)take(sizeof(float) * S * M * 120);
+    w.dx2 = (float*)take(sizeof(float) * S * M * kX2);
+    w.part = (float*)take(sizeof(float) * S * w.nchunk * kNConv);
+    w.bytes = off;
+    return w;
+}
+
+int lenet_nchunk(const psvi_plan& p) {
+    // >= ~2048 workgroups over the chip (256 CUs), at most one image per chunk
+    const int S = p.s_cnt[p.rank], M = p.d.M;
+    const int want = (2048 + S - 1) / S;
+    return std::max(1, std::min(M, want));
+}
+
+static SampleArgs sample_args(const psvi_plan& p) {
+    SampleArgs a{};
+    a.L = p.L;
+    a.n_tot = p.n_tot;
+    a.S_loc = p.s_cnt[p.rank];
+    a.s_off = p.s_off[p.rank];
+    a.S_tot = p.d.S;
+    for (int l = 0; l < p.L; ++l) {
+        a.woff[l] = p.lay[l].woff;
+        a.n[l] = p.lay[l].n;
+        a.nw[l] = p.lay[l].din * p.lay[l].dout;
+        a.batched[l] = l < p.L - 1;
+        a.poff[l] = p.lay[l].poff;
+        a.eoff[l] = p.lay[l].eoff;
+    }
+    a.woff[p.L] = p.n_tot;
+    return a;
+}
+
+hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
+                        const float* params, const float* eps, float* acc, double* nll_out,
+                        void* ws, hipStream_t st) {
+    const LenetWs W = lenet_ws(p, ws);
+    const SampleArgs sa = sample_args(p);
+    const int S = sa.S_loc, M = p.d.M, nt = p.n_tot;
+    if (S == 0) return hipMemsetAsync(acc, 0, sizeof(float) * 2 * nt, st);
+    const int64_t rows = (int64_t)S * M;
+    {
+        const int64_t nb = std::min<int64_t>(((int64_t)S * nt + kThreads - 1) / kThreads, 8192);
+        hipLaunchKernelGGL(lenet_sample_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, sa,
+                           params, eps, W.wsamp);
+    }
+    ConvArgs ca{};
+    ca.M = M;
+    ca.n_tot = nt;
+    ca.nchunk = W.nchunk;
+    ca.chunk = (M + W.nchunk - 1) / W.nchunk;
+    ca.u = u;
+    ca.wsamp = W.wsamp;
+    ca.p1 = W.p1;
+    ca.r1 = W.r1;
+    ca.x2 = W.x2;
+    ca.r2 = W.r2;
+    ca.dx2 = W.dx2;
+    ca.part = W.part;
+    hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kThreads), 0, st, ca);
+    const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
+    const float* Ws = W.wsamp;
+    // head forward: H1 = relu(X2 W1^T + b1), H2 = relu(H1 W2^T + b2), D = H2 W3^T + b3
+    GemmArgs g = gemm_args(M, 120, 400, W.x2, (int64_t)M * 400, 400, 1, Ws + w3, nt, 1, 400,
+                           W.h1, (int64_t)M * 120, 120);
+    g.epi = 3; g.bias = Ws + w3 + 48000; g.sbias = nt;
+    if (hipError_t e = gemm(g, S, st)) return e;
+    g = gemm_args(M, 84, 120, W.h1, (int64_t)M * 120, 120, 1, Ws + w4, nt, 1, 120, W.h2,
+                  (int64_t)M * 84, 84);
+    g.epi = 3; g.bias = Ws + w4 + 10080; g.sbias = nt;
+    if (hipError_t e = gemm(g, S, st)) return e;
+    g = gemm_args(M, 10, 84, W.h2, (int64_t)M * 84, 84, 1, Ws + w5, nt, 1, 84, W.d,
+                  (int64_t)M * 10, 10);
+    g.epi = 1; g.bias = Ws + w5 + 840; g.sbias = nt;
+    if (hipError_t e = gemm(g, S, st)) return e;
+    hipLaunchKernelGGL(lenet_loss_kernel, dim3((unsigned)((rows + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, (int)rows, M, z, w, W.d, nll_out);
+    // head backward
+    float* dW = W.dws;
+    g = gemm_args(10, 84, M, W.d, (int64_t)M * 10, 1, 10, W.h2, (int64_t)M * 84, 84, 1,
+                  dW + w5, nt, 84);
+    if (hipError_t e = gemm(g, S, st)) return e;
+    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, W.d, M, 10,
+                       dW + w5 + 840, (int64_t)nt);
+    g = gemm_args(M, 84, 10, W.d, (int64_t)M * 10, 10, 1, Ws + w5, nt, 84, 1, W.dh2,
+                  (int64_t)M * 84, 84);
+    g.epi = 4; g.mask = W.h2; g.sMb = (int64_t)M * 84; g.sMm = 84;
+    if (hipError_t e = gemm(g, S, st)) return e;
+    g = gemm_args(84, 120, M, W.dh2, (int64_t)M * 84, 1, 84, W.h1, (int64_t)M * 120, 120, 1,
+                  dW + w4, nt, 120);
+    if (hipError_t e = gemm(g, S, st)) return e;
+    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, W.dh2, M, 84,
+                       dW + w4 + 10080, (int64_t)nt);
+    g = gemm_args(M, 120, 84, W.dh2, (int64_t)M * 84, 84, 1, Ws + w4, nt, 120, 1, W.dh1,
+                  (int64_t)M * 120, 120);
+    g.epi = 4; g.mask = W.h1; g.sMb = (int64_t)M * 120; g.sMm = 120;
+    if (hipError_t e = gemm(g, S, st)) return e;
+    g = gemm_args(120, 400, M, W.dh1, (int64_t)M * 120, 1, 120, W.x2, (int64_t)M * 400, 400, 1,
+                  dW + w3, nt, 400);
+    if (hipError_t e = gemm(g, S, st)) return e;
+    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, W.dh1, M, 120,
+                       dW + w3 + 48000, (int64_t)nt);
+    g = gemm_args(M, 400, 120, W.dh1, (int64_t)M * 120, 120, 1, Ws + w3, nt, 400, 1, W.dx2,
+                  (int64_t)M * 400, 400);
+    if (hipError_t e = gemm(g, S, st)) return e;
+    // conv towers backward, then the per-sample sums with eps
+    hipLaunchKernelGGL(lenet_conv_bwd_kernel, dim3(W.nchunk, S), dim3(kThreads), 0, st, ca);
+    hipLaunchKernelGGL(lenet_conv_reduce_kernel,
+                       dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, S, W.nchunk, nt, W.part, dW);
+    hipLaunchKernelGGL(lenet_acc_kernel, dim3((nt + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       st, sa, eps, dW, acc);
+    return hipGetLastError();
+}
+
+}  // namespace psvi

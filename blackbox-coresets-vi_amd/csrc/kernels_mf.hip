@@ -44,6 +44,7 @@ struct MfUpdArgs {
     float* grad_out;
     double* kl_out;
     int include_kl;
+    unsigned kl_mask;  // layers carrying a KL term (LeNet: the VILinear layers only)
     float inv_s0sq, log_s0;
     AdamC adam;
 };
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
         const float* accMu = a.acc;
         const float* accRho = accMu + a.n_tot;
         float gmu = accMu[e], grho = accRho[e] * sg;
-        if (a.include_kl) {
+        if (a.include_kl && ((a.kl_mask >> l) & 1u)) {
             gmu += mu * a.inv_s0sq;
             grho += (sp * a.inv_s0sq - 1.f / sp) * sg;
             // _kl_normal_normal with q = N(0, s0): 0.5(vr + mu^2/s0^2 - 1 - log vr)
@@ -150,6 +151,7 @@ hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
     a.grad_out = grad_out;
     a.kl_out = kl_out;
     a.include_kl = include_kl;
+    a.kl_mask = p.family == PSVI_FAMILY_LENET ? 0x1Cu : 0xFFu;
     const float s0 = p.d.prior_sd;
     a.inv_s0sq = 1.f / (s0 * s0);
     a.log_s0 = logf(s0);

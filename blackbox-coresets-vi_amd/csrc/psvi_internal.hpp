@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -249,6 +250,8 @@ struct psvi_plan {
     size_t net_lds = 0;
     size_t ws_bytes = 0;
     int64_t acc_count = 0;
+    // LeNet: plan-owned activation / gradient scratch (kernels_lenet.hip)
+    void* d_lenet_ws = nullptr;
 };
 
 namespace psvi {
@@ -291,6 +294,20 @@ hipError_t launch_eval(const psvi_plan& p, int n_pseudo, const float* params, co
 hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* params,
                                const float* sck, float* grad, const float* du_part,
                                float* grad_u, hipStream_t st);
+// LeNet (kernels_lenet.hip): scratch carve of the plan-owned buffer
+struct LenetWs {
+    float *wsamp, *dws, *p1, *x2, *h1, *h2, *d, *dh2, *dh1, *dx2, *part;
+    int8_t *r1, *r2;
+    int nchunk;
+    size_t bytes;
+};
+int lenet_nchunk(const psvi_plan& p);
+LenetWs lenet_ws(const psvi_plan& p, void* base);  // base nullptr: sizes only
+// per-sample weight draw, forward, weighted NLL (+= nll_out), backward, and
+// acc = [sum_s dW | sum_s dW eps] over the rank's samples (acc fully written)
+hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
+                        const float* params, const float* eps, float* acc, double* nll_out,
+                        void* ws, hipStream_t st);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
 hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,

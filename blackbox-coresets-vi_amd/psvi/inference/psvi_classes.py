@@ -169,7 +169,7 @@ class PSVI:
         return self._plans[key]
 
     def _data(self, plan):
-        M, D = plan.M, plan.layers[0][0]
+        M, D = plan.M, plan.in_features
         u = self.u.detach().to(self.device, torch.float32).reshape(M, D).contiguous()
         z = self.z.detach().to(self.device)
         if z.is_floating_point() and not torch.equal(z, z.round()):

@@ -31,6 +31,7 @@ __all__ = [
     "VIMixin", "VILinear", "MultivariateNormalVIMixin", "VILinearMultivariateNormal",
     "make_fcnet", "make_fc2net", "make_logreg", "set_mc_samples", "inverse_softplus",
     "categorical_fn", "gaussian_fn", "vi_layers", "model_spec",
+    "VIConv2d", "BatchMaxPool2d", "make_lenet", "LENET_LAYERS",
 ]
 
 
@@ -236,6 +237,64 @@ class VILinearMultivariateNormal(MultivariateNormalVIMixin, nn.Linear):
         return out
 
 
+class VIConv2d(VIMixin, nn.Conv2d):
+    """Mean-field Bayesian conv layer (neural_net.py:194-246): S weight samples,
+    each convolving its own copy of the input (one grouped conv with
+    groups=S).  Input (M, C, H, W) or (S, M, C, H, W); output (S, M, K, H', W')
+    when mc_samples > 1."""
+
+    def __init__(self, *args, **kwargs):
+        if "groups" in kwargs:
+            raise ValueError("groups is reserved: it parallelises the conv over samples")
+        super().__init__(*args, **kwargs)
+
+    def forward(self, x):
+        S = self.mc_samples
+        if S > 1:
+            x = x.repeat(1, S, 1, 1) if x.ndim == 4 else x.transpose(0, 1).flatten(1, 2)
+        self._cached_weight, self._cached_bias = self.rsample()
+        wt = self._cached_weight.flatten(0, 1) if S > 1 else self._cached_weight
+        b = self._cached_bias.flatten() if self.bias is not None else None
+        a = F.conv2d(x, wt, b, stride=self.stride, padding=self.padding,
+                     dilation=self.dilation, groups=S)
+        if S > 1:
+            return a.view(-1, S, self.out_channels, *a.shape[-2:]).transpose(0, 1)
+        return a
+
+
+class BatchMaxPool2d(nn.MaxPool2d):
+    """Max-pool over the trailing (C, H, W) of an (S, M, C, H, W) map
+    (neural_net.py:249-255; its ``x.shape == 4`` guard is never true, so 5-d
+    input always takes the flattening path -- kept)."""
+
+    def forward(self, x):
+        d0, d1 = x.shape[:2]
+        x = super().forward(x.flatten(0, 1))
+        return x.view(d0, d1, *x.shape[1:])
+
+
+def make_lenet(conv_class=None, linear_class=None, pool_class=None, nonl_class=None, **kwargs):
+    """LeNet-5 BNN (neural_net.py:334-359).  kwargs (mc_samples, init_sd,
+    prior_sd) go to every layer but the last, which keeps the VILinear defaults:
+    mc_samples=1 (one weight sample shared by all S) and init_sd=0.01."""
+    conv_class = conv_class or VIConv2d
+    linear_class = linear_class or VILinear
+    pool_class = pool_class or BatchMaxPool2d
+    nonl_class = nonl_class or nn.ReLU
+    return nn.Sequential(
+        conv_class(1, 6, 5, padding=2, **kwargs), nonl_class(), pool_class(2, 2),
+        conv_class(6, 16, 5, padding=0, **kwargs), nonl_class(), pool_class(2, 2),
+        nn.Flatten(-3, -1),
+        linear_class(400, 120, **kwargs), nonl_class(),
+        linear_class(120, 84, **kwargs), nonl_class(),
+        linear_class(84, 10))
+
+
+# (weight elements / out channels, out) of make_lenet's variational layers as
+# the HIP library lays them out (n = in*out + out per layer)
+LENET_LAYERS = [(25, 6), (150, 16), (400, 120), (120, 84), (84, 10)]
+
+
 # ------------------------------------------------------------ builders
 def _stack(in_dim, h_dim, out_dim, n_layers, linear_class, nonl_class, mc_samples, kwargs):
     net = nn.Sequential()
@@ -279,14 +338,48 @@ def vi_layers(model):
     return [m for m in model.modules() if isinstance(m, (VIMixin, MultivariateNormalVIMixin))]
 
 
+def _lenet_spec(mods):
+    """("lenet", LENET_LAYERS, prior_sd, S) for make_lenet's exact stack."""
+    kinds = [VIConv2d, nn.ReLU, BatchMaxPool2d, VIConv2d, nn.ReLU, BatchMaxPool2d, nn.Flatten,
+             VILinear, nn.ReLU, VILinear, nn.ReLU, VILinear]
+    if len(mods) != len(kinds) or not all(isinstance(m, k) for m, k in zip(mods, kinds)):
+        raise ValueError("only make_lenet's exact stack runs on the HIP LeNet path")
+    c1, c2, f1, f2, f3 = mods[0], mods[3], mods[7], mods[9], mods[11]
+    for c, (ci, co, pad) in ((c1, (1, 6, 2)), (c2, (6, 16, 0))):
+        if (c.in_channels, c.out_channels, c.kernel_size, c.padding, c.stride, c.dilation) != \
+                (ci, co, (5, 5), (pad, pad), (1, 1), (1, 1)) or c.bias is None:
+            raise ValueError("LeNet conv layers must be make_lenet's (5x5, stride 1, bias)")
+    for p in (mods[2], mods[5]):
+        if p.kernel_size not in (2, (2, 2)) or p.stride not in (2, (2, 2)) or \
+                p.padding not in (0, (0, 0)) or p.dilation not in (1, (1, 1)) or p.ceil_mode:
+            raise ValueError("LeNet pools must be 2x2 / stride 2")
+    if (mods[6].start_dim, mods[6].end_dim) != (-3, -1):
+        raise ValueError("LeNet flatten must be Flatten(-3, -1)")
+    for f, (i, o) in ((f1, (400, 120)), (f2, (120, 84)), (f3, (84, 10))):
+        if (f.in_features, f.out_features) != (i, o) or f.bias is None:
+            raise ValueError("LeNet linear layers must be 400-120-84-10 with bias")
+    S = int(c1.mc_samples)
+    if any(int(m.mc_samples) != S for m in (c2, f1, f2)) or S < 2:
+        raise ValueError("LeNet: the convs and the first two linears share mc_samples > 1")
+    if int(f3.mc_samples) != 1:
+        raise ValueError("LeNet: the last layer keeps one shared sample (mc_samples=1)")
+    prior = float(c1.prior_sd)
+    if any(float(m.prior_sd) != prior for m in (c2, f1, f2, f3)):
+        raise ValueError("all layers must share prior_sd")
+    return "lenet", list(LENET_LAYERS), prior, S
+
+
 def model_spec(model):
     """(family, [(in, out), ...], prior_sd, mc_samples) of a model the HIP inner
     loop can run: an nn.Sequential of variational linear layers of one family
-    with ReLU between them.  Raises ValueError otherwise."""
+    with ReLU between them, or make_lenet's stack (family "lenet").  Raises
+    ValueError otherwise."""
     if not isinstance(model, nn.Sequential):
         raise ValueError("the HIP inner loop runs nn.Sequential VI stacks (make_fcnet / "
-                         "make_fc2net / make_logreg)")
+                         "make_fc2net / make_logreg / make_lenet)")
     mods = list(model.children())
+    if mods and isinstance(mods[0], VIConv2d):
+        return _lenet_spec(mods)
     layers, fam, prior, S = [], None, None, None
     for i, m in enumerate(mods):
         if i % 2 == 1:

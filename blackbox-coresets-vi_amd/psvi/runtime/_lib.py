@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libpsvi_hip.so")
 MAX_LAYERS = 8
 FAMILY_MEANFIELD = 0
 FAMILY_FULLCOV = 1
+FAMILY_LENET = 2
 ADAM_HIGHER = 0
 ADAM_HYPERGRAD = 1
 

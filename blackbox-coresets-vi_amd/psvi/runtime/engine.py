@@ -46,11 +46,19 @@ class InnerLoopPlan:
     def __init__(self, family, layers, S, M, prior_sd=1.0, world=1, rank=0):
         self.lib = _lib.load()
         self.family = family
-        fam = {"meanfield": _lib.FAMILY_MEANFIELD, "fullcov": _lib.FAMILY_FULLCOV}[family]
+        fam = {"meanfield": _lib.FAMILY_MEANFIELD, "fullcov": _lib.FAMILY_FULLCOV,
+               "lenet": _lib.FAMILY_LENET}[family]
         layers = [tuple(int(x) for x in l) for l in layers]
-        for a, b in zip(layers[:-1], layers[1:]):
-            if a[1] != b[0]:
-                raise ValueError(f"layer sizes do not chain: {layers}")
+        if family == "lenet":
+            # fixed make_lenet stack (conv "in" = in_channels * 25); input 1x28x28
+            if layers != [(25, 6), (150, 16), (400, 120), (120, 84), (84, 10)]:
+                raise ValueError(f"not make_lenet's layer table: {layers}")
+            self.in_features = 784
+        else:
+            for a, b in zip(layers[:-1], layers[1:]):
+                if a[1] != b[0]:
+                    raise ValueError(f"layer sizes do not chain: {layers}")
+            self.in_features = layers[0][0]
         if not 1 <= len(layers) <= _lib.MAX_LAYERS:
             raise ValueError("1..8 layers supported")
         self.layers = layers
@@ -111,7 +119,7 @@ class InnerLoopPlan:
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=device)
 
     def _inputs(self, u, z, w, eps):
-        _need(u, "u", self.M * self.layers[0][0])
+        _need(u, "u", self.M * self.in_features)
         _need(z, "z", self.M, torch.int32)
         _need(w, "w", self.M)
         _need(eps, "eps", self.eps_count)
@@ -141,7 +149,7 @@ class InnerLoopPlan:
         """T chained inner steps (psvi_inner_loop).  eps: (T, eps_count) device
         tensor, or None for in-library Philox draws (seed, offset + t * eps_stride).
         Returns the (T,) float64 device tensor of negative ELBOs before each step."""
-        _need(u, "u", self.M * self.layers[0][0])
+        _need(u, "u", self.M * self.in_features)
         _need(z, "z", self.M, torch.int32)
         _need(w, "w", self.M)
         for t, n in ((params, "params"), (adam_m, "adam_m"), (adam_v, "adam_v")):
@@ -318,7 +326,7 @@ class InnerLoopPlan:
             _ptr(x_next), _stream()), "psvi_mvn_phase_update_tiled")
 
     def mvn_net(self, u, z, w, x_recv, g_send, nll_out):
-        _need(u, "u", self.M * self.layers[0][0])
+        _need(u, "u", self.M * self.in_features)
         _need(z, "z", self.M, torch.int32)
         _need(w, "w", self.M)
         _need(x_recv, "x_recv", self.xrecv_count)

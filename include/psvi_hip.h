@@ -19,7 +19,8 @@
  *   - Every pointer argument is a DEVICE pointer (fp32 unless stated) owned by
  *     the caller; the library never allocates device memory inside a step
  *     (psvi_plan_create allocates its immutable work lists and the plan-owned
- *     split-K scratch of the full-cov sample phase; a plan's calls must not
+ *     split-K scratch of the full-cov sample phase and the LeNet activation
+ *     scratch; a plan's calls must not
  *     run concurrently on different streams).
  *   - Steps are stream-ordered and asynchronous on `stream` (a hipStream_t
  *     passed as void*; NULL = default stream); no host synchronisation inside.
@@ -65,6 +66,20 @@ extern "C" {
 #define PSVI_FAMILY_MEANFIELD 0   /* VILinear stack: logistic_regression, fn   */
 #define PSVI_FAMILY_FULLCOV   1   /* VILinearMultivariateNormal stack: fn2,
                                      logistic_regression_fullcov              */
+#define PSVI_FAMILY_LENET     2   /* make_lenet (neural_net.py:334-359): VIConv2d(1,6,5,p2)
+                                     ReLU BatchMaxPool2d(2) VIConv2d(6,16,5) ReLU pool
+                                     VILinear 400-120-84-10 (the last one ONE shared
+                                     sample, mc_samples=1); u is (M,1,28,28).  The
+                                     architecture is fixed: n_layers / dims of the
+                                     descriptor are ignored.  Parameters: the
+                                     mean-field layout per layer (conv weights in
+                                     (out,in,5,5) order); eps per layer in draw order,
+                                     W (S,n_w) then b (S,n_b), the last layer (n_w)
+                                     then (n_b) without S.  KL on the VILinear layers
+                                     only (psvi_classes.py:506-510).  Entry points:
+                                     inner_step, elbo_grad, inner_loop and the
+                                     mean-field phases; the plan owns the activation
+                                     scratch (about S*M*7.9 KB).                  */
 
 /* Adam variants */
 #define PSVI_ADAM_HIGHER    0   /* robust_higher DifferentiableAdam (optim.py:318-367):

@@ -102,6 +102,23 @@ def test_plan_geometry_meanfield():
         InnerLoopPlan("meanfield", [(2, 100), (99, 4)], 32, 50)  # does not chain
 
 
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_plan_geometry_lenet_c5(world):
+    """make_lenet at C5 (S=256, M=500): 123,412 parameters, one shared sample
+    in the last layer (850 eps), samples sharded like the mean-field family."""
+    from psvi.runtime import InnerLoopPlan
+
+    LEN = [(25, 6), (150, 16), (400, 120), (120, 84), (84, 10)]
+    ps = [InnerLoopPlan("lenet", LEN, 256, 500, world=world, rank=r) for r in range(world)]
+    for r, p in enumerate(ps):
+        assert p.param_count == 123_412 and p.eps_count == 256 * 60_856 + 850
+        assert p.acc_count == 2 * 61_706 and p.in_features == 784
+        assert p.s_offset == sum(q.s_local for q in ps[:r])
+    assert sum(p.s_local for p in ps) == 256
+    with pytest.raises(ValueError):
+        InnerLoopPlan("lenet", LEN[:-1], 256, 500)
+
+
 def test_plan_rejects_oversized_layer():
     from psvi.runtime import InnerLoopPlan, PsviError
 

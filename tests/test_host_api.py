@@ -155,3 +155,60 @@ def test_outer_objective_has_no_cpu_fallback():
     xb, yb = torch.randn(8, 2), torch.zeros(8)
     with pytest.raises((ValueError, PsviError)):
         ps.psvi_elbo(xb, yb)
+
+
+def test_make_lenet_layout_and_spec():
+    """make_lenet (neural_net.py:334-359): parameter order = the library's
+    layout, model_spec -> family "lenet"; the last layer keeps mc_samples=1."""
+    from psvi.models import LENET_LAYERS, make_lenet, model_spec, set_mc_samples
+
+    net = make_lenet(mc_samples=4, init_sd=0.05)
+    names = [n for n, _ in net.named_parameters()]
+    assert names[:4] == ["0.weight", "0.bias", "0._weight_sd", "0._bias_sd"]
+    assert sum(p.numel() for p in net.parameters()) == O.lenet_param_count()
+    assert model_spec(net) == ("lenet", LENET_LAYERS, 1.0, 4)
+    assert net[11].mc_samples == 1
+    f = load_fixture("l1_lenet_tiny")
+    with torch.no_grad():
+        nn.utils.vector_to_parameters(torch.tensor(f["params0"]), net.parameters())
+    assert np.array_equal(nn.utils.parameters_to_vector(net.parameters()).detach().numpy(),
+                          f["params0"])
+    set_mc_samples(net, 4)  # also sets the last layer: no longer make_lenet's model
+    with pytest.raises(ValueError, match="shared sample"):
+        model_spec(net)
+
+
+def test_lenet_torch_forward_matches_oracle():
+    """The host VIConv2d / BatchMaxPool2d modules (prediction path) compute the
+    oracle's forward on the same weight draws."""
+    from psvi.models import make_lenet
+
+    f = load_fixture("l1_lenet_tiny")
+    S = f["cfg"]["S"]
+    net = make_lenet(mc_samples=S).double()
+    with torch.no_grad():
+        nn.utils.vector_to_parameters(torch.tensor(f["params0"], dtype=torch.float64),
+                                      net.parameters())
+    Xl = O.lenet_sample(f["params0"], f["eps"][0], S)
+    logits_o, _ = O.lenet_forward(Xl, f["u"], S)
+    draws = []
+    for x, (nw, nb, bat, _) in zip(Xl, O.LENET_LAYERS):
+        E = x["E"]
+        draws += [E[:, :nw], E[:, nw:]]
+    it = iter(draws)
+    import psvi.models.neural_net as nnmod
+
+    def fake_rsample(self):
+        ew, eb = next(it), next(it)
+        ew = torch.tensor(ew).reshape((self.mc_samples,) * (self.mc_samples > 1) + self.weight.shape)
+        eb = torch.tensor(eb).reshape(((self.mc_samples, 1) if self.mc_samples > 1 else ())
+                                      + self.bias.shape)
+        return self.weight + self.weight_sd * ew, self.bias + self.bias_sd * eb
+
+    orig = nnmod.VIMixin.rsample
+    nnmod.VIMixin.rsample = fake_rsample
+    try:
+        logits = net(torch.tensor(f["u"], dtype=torch.float64)).detach().numpy()
+    finally:
+        nnmod.VIMixin.rsample = orig
+    assert np.allclose(logits, logits_o, rtol=1e-10, atol=1e-10)
