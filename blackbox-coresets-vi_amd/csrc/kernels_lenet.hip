@@ -112,14 +112,18 @@ __device__ __forceinline__ float relu_pool4(float a0, float a1, float a2, float 
     return m > 0.f ? m : 0.f;
 }
 
-__global__ __launch_bounds__(kThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
+// One workgroup per (image chunk, sample): the sample's conv weights stay in
+// LDS while the chunk's images stream through.  320 threads (5 waves): the
+// bwd kernel's 294 transposed-conv blocks fit in one pass.
+constexpr int kConvThreads = 320;
+
+__global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
     __shared__ float w1[150], b1[6], w2[2400], b2[16];
     __shared__ float in[32 * 32];       // 28x28 image, zero padding 2
     __shared__ float p1[kP1];
-    __shared__ float a2[1600];          // conv2 pre-activation [16][10][10]
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    for (int i = tid; i < kNConv; i += kThreads) {
+    for (int i = tid; i < kNConv; i += kConvThreads) {
         const float v = ws[i];
         if (i < 150) w1[i] = v;
         else if (i < 156) b1[i - 150] = v;
@@ -130,14 +134,15 @@ __global__ __launch_bounds__(kThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
     for (int m = m0; m < m1; ++m) {
         __syncthreads();
         const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kThreads) {
+        for (int i = tid; i < 1024; i += kConvThreads) {
             const int y = (i >> 5) - 2, x = (i & 31) - 2;
             in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
         }
         __syncthreads();
         const int64_t row = (int64_t)s * a.M + m;
-        // conv1 (1 -> 6, 5x5, pad 2) + relu + pool: one pooled output per item
-        for (int o = tid; o < kP1; o += kThreads) {
+        // conv1 (1 -> 6, 5x5, pad 2) + relu + pool: one pooled output (its 2x2
+        // conv window from a 6x6 patch in registers) per item
+        for (int o = tid; o < kP1; o += kConvThreads) {
             const int c = o / 196, py = (o % 196) / 14, px = o % 14;
             float patch[6][6];
 #pragma unroll
@@ -164,26 +169,33 @@ __global__ __launch_bounds__(kThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
             a.r1[row * kP1 + o] = r;
         }
         __syncthreads();
-        // conv2 (6 -> 16, 5x5): one pre-activation per item
-        for (int o = tid; o < 1600; o += kThreads) {
-            const int k = o / 100, y = (o % 100) / 10, x = o % 10;
-            float acc = b2[k];
+        // conv2 (6 -> 16, 5x5) + relu + pool, same blocking per input channel
+        for (int o = tid; o < kX2; o += kConvThreads) {
+            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
+            float acc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = b2[k];
             for (int c = 0; c < 6; ++c) {
-                const float* pc = p1 + c * 196 + y * 14 + x;
+                const float* pc = p1 + c * 196 + 2 * py * 14 + 2 * px;
                 const float* wk = w2 + k * 150 + c * 25;
+                float patch[6][6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) patch[i][j] = pc[i * 14 + j];
 #pragma unroll
                 for (int i = 0; i < 5; ++i)
 #pragma unroll
-                    for (int j = 0; j < 5; ++j) acc += wk[i * 5 + j] * pc[i * 14 + j];
+                    for (int j = 0; j < 5; ++j) {
+                        const float wv = wk[i * 5 + j];
+                        acc[0] += wv * patch[i][j];
+                        acc[1] += wv * patch[i][j + 1];
+                        acc[2] += wv * patch[i + 1][j];
+                        acc[3] += wv * patch[i + 1][j + 1];
+                    }
             }
-            a2[o] = acc;
-        }
-        __syncthreads();
-        for (int o = tid; o < kX2; o += kThreads) {
-            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
-            const float* ak = a2 + k * 100 + 2 * py * 10 + 2 * px;
             int8_t r;
-            const float v = relu_pool4(ak[0], ak[1], ak[10], ak[11], r);
+            const float v = relu_pool4(acc[0], acc[1], acc[2], acc[3], r);
             a.x2[row * kX2 + o] = v;
             a.r2[row * kX2 + o] = r;
         }
@@ -191,116 +203,145 @@ __global__ __launch_bounds__(kThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------- conv towers, bwd
-// Given d X2 (the head's input gradient) per (s, m): route through pool2/relu,
-// accumulate conv2's weight gradient against P1, form d P1 (the transposed conv
-// restricted to the routed positions), route through pool1/relu, accumulate
-// conv1's weight gradient against the padded image.  Per-(s, chunk) partial
-// sums, reduced over chunks in fixed order by lenet_conv_reduce_kernel.
-__global__ __launch_bounds__(kThreads) void lenet_conv_bwd_kernel(ConvArgs a) {
+// Given d X2 (the head's input gradient) per (s, m): route through pool2/relu
+// (one conv2 position per pooled output), accumulate conv2's weight gradient
+// against P1 (25 routed terms per weight), form d P1 as the transposed conv
+// of the routed map (dense, zero-padded in LDS, 2x2 output blocks per thread),
+// route through pool1/relu, accumulate conv1's weight gradient against the
+// padded image.  Per-(s, chunk) partial sums, reduced over chunks in fixed
+// order by lenet_conv_reduce_kernel: bitwise run-to-run reproducible.
+constexpr int kDA = 18;  // routed conv2 gradient plane, 10x10 plus a 4-wide zero border
+
+__global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a) {
     __shared__ float w2[2400];
     __shared__ float in[32 * 32];
     __shared__ float p1[kP1];
-    __shared__ float g2[kX2];     // routed gradient of each pooled conv2 output
-    __shared__ int pos2[kX2];     // its conv2 position y * 10 + x
-    __shared__ float dp1[kP1];
-    __shared__ float g1[kP1];
-    __shared__ int pos1[kP1];     // routed conv1 position y * 28 + x
+    __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
+    __shared__ int off2[kX2];        // its conv2 position y * 14 + x (P1 plane offset)
+    __shared__ float da2[16 * kDA * kDA];
+    __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
+    __shared__ int off1[kP1];        // its conv1 position y * 32 + x (padded image)
+    __shared__ float red[160];
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    for (int i = tid; i < 2400; i += kThreads) w2[i] = ws[156 + i];
-    float accw2[10];
+    for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
+    for (int i = tid; i < 16 * kDA * kDA; i += kConvThreads) da2[i] = 0.f;
+    // conv2 weight entries owned by this thread: e = tid + r * 320
+    constexpr int kR2 = (2400 + kConvThreads - 1) / kConvThreads;
+    int kb[kR2], pb[kR2];
 #pragma unroll
-    for (int r = 0; r < 10; ++r) accw2[r] = 0.f;
-    float acc1 = 0.f;  // tid < 150: conv1 weight; 150..155: conv1 bias; 156..171: conv2 bias
+    for (int r = 0; r < kR2; ++r) {
+        const int e = min(tid + r * kConvThreads, 2399);
+        kb[r] = (e / 150) * 25;
+        pb[r] = ((e % 150) / 25) * 196 + ((e % 25) / 5) * 14 + e % 5;
+    }
+    float accw2[kR2];
+#pragma unroll
+    for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
+    // conv1: threads [0, 160) and [160, 320) split the 196 routed positions;
+    // e < 150 weight (c, i, j), 150..155 bias
+    const int half = tid / 160, e1 = tid % 160;
+    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * 32 + e1 % 5;
+    const int cb1 = (e1 >= 150 && e1 < 156) ? e1 - 150 : c1;
+    float acc1 = 0.f, accb2 = 0.f;
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
     for (int m = m0; m < m1; ++m) {
         __syncthreads();
         const int64_t row = (int64_t)s * a.M + m;
         const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kThreads) {
+        for (int i = tid; i < 1024; i += kConvThreads) {
             const int y = (i >> 5) - 2, x = (i & 31) - 2;
             in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
         }
-        for (int i = tid; i < kP1; i += kThreads) p1[i] = a.p1[row * kP1 + i];
-        for (int o = tid; o < kX2; o += kThreads) {
+        for (int i = tid; i < kP1; i += kConvThreads) p1[i] = a.p1[row * kP1 + i];
+        for (int o = tid; o < kX2; o += kConvThreads) {
             const int r = a.r2[row * kX2 + o];
-            const int py = (o % 25) / 5, px = o % 5;
-            g2[o] = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
+            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
             const int rr = r >= 0 ? r : 0;
-            pos2[o] = (2 * py + (rr >> 1)) * 10 + 2 * px + (rr & 1);
+            const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
+            const float g = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
+            g2[o] = g;
+            off2[o] = y * 14 + x;
+            if (r >= 0) da2[k * kDA * kDA + (y + 4) * kDA + x + 4] = g;
         }
         __syncthreads();
         // conv2 weight gradient: dW2[k][c][i][j] += sum_p g2[k][p] P1[c][y_p + i][x_p + j]
 #pragma unroll
-        for (int r = 0; r < 10; ++r) {
-            const int e = tid + r * kThreads;
-            if (e < 2400) {
-                const int k = e / 150, c = (e % 150) / 25, i = (e % 25) / 5, j = e % 5;
-                const float* pc = p1 + c * 196 + i * 14 + j;
+        for (int r = 0; r < kR2; ++r) {
+            if (tid + r * kConvThreads < 2400) {
                 float acc = 0.f;
-                for (int p = 0; p < 25; ++p) {
-                    const int q = pos2[k * 25 + p];
-                    acc += g2[k * 25 + p] * pc[(q / 10) * 14 + q % 10];
-                }
+#pragma unroll
+                for (int p = 0; p < 25; ++p) acc += g2[kb[r] + p] * p1[pb[r] + off2[kb[r] + p]];
                 accw2[r] += acc;
             }
         }
-        if (tid >= 156 && tid < 172) {
-            const int k = tid - 156;
+        if (tid < 16) {
             float acc = 0.f;
-            for (int p = 0; p < 25; ++p) acc += g2[k * 25 + p];
-            acc1 += acc;
+            for (int p = 0; p < 25; ++p) acc += g2[tid * 25 + p];
+            accb2 += acc;
         }
-        // d P1[c][yy][xx] = sum_k sum_(routed (y, x) within the 5x5 window)
-        //                   g2 W2[k][c][yy - y][xx - x]
-        for (int o = tid; o < kP1; o += kThreads) {
-            const int c = o / 196, yy = (o % 196) / 14, xx = o % 14;
-            const int pylo = max(0, yy - 4) >> 1, pyhi = min(9, yy) >> 1;
-            const int pxlo = max(0, xx - 4) >> 1, pxhi = min(9, xx) >> 1;
-            float acc = 0.f;
+        // d P1 (transposed conv, 2x2 output blocks), routed through pool1 / relu
+        if (tid < 294) {
+            const int c = tid / 49, yy = 2 * ((tid % 49) / 7), xx = 2 * (tid % 7);
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
             for (int k = 0; k < 16; ++k) {
+                const float* q = da2 + k * kDA * kDA + yy * kDA + xx;
+                float Q[6][6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) Q[i][j] = q[i * kDA + j];
                 const float* wk = w2 + k * 150 + c * 25;
-                for (int py = pylo; py <= pyhi; ++py)
-                    for (int px = pxlo; px <= pxhi; ++px) {
-                        const int p = k * 25 + py * 5 + px;
-                        const int q = pos2[p];
-                        const int dy = yy - q / 10, dx = xx - q % 10;
-                        if (dy >= 0 && dy < 5 && dx >= 0 && dx < 5) acc += g2[p] * wk[dy * 5 + dx];
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        const float wv = wk[i * 5 + j];
+                        acc[0] += wv * Q[4 - i][4 - j];
+                        acc[1] += wv * Q[4 - i][5 - j];
+                        acc[2] += wv * Q[5 - i][4 - j];
+                        acc[3] += wv * Q[5 - i][5 - j];
                     }
             }
-            dp1[o] = acc;
-        }
-        __syncthreads();
-        for (int o = tid; o < kP1; o += kThreads) {
-            const int r = a.r1[row * kP1 + o];
-            const int py = (o % 196) / 14, px = o % 14;
-            g1[o] = r >= 0 ? dp1[o] : 0.f;
-            const int rr = r >= 0 ? r : 0;
-            pos1[o] = (2 * py + (rr >> 1)) * 28 + 2 * px + (rr & 1);
-        }
-        __syncthreads();
-        // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
-        if (tid < 150) {
-            const int c = tid / 25, i = (tid % 25) / 5, j = tid % 5;
-            float acc = 0.f;
-            for (int p = 0; p < 196; ++p) {
-                const int q = pos1[c * 196 + p];
-                acc += g1[c * 196 + p] * in[(q / 28 + i) * 32 + q % 28 + j];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int yq = yy + (q >> 1), xq = xx + (q & 1);
+                const int o = c * 196 + yq * 14 + xq;
+                const int r = a.r1[row * kP1 + o];
+                const int rr = r >= 0 ? r : 0;
+                g1[o] = r >= 0 ? acc[q] : 0.f;
+                off1[o] = (2 * yq + (rr >> 1)) * 32 + 2 * xq + (rr & 1);
             }
-            acc1 += acc;
-        } else if (tid < 156) {
-            const int c = tid - 150;
+        }
+        __syncthreads();
+        // clear the routed entries of the dense plane for the next image
+        for (int o = tid; o < kX2; o += kConvThreads) {
+            const int k = o / 25, q = off2[o];
+            da2[k * kDA * kDA + (q / 14 + 4) * kDA + q % 14 + 4] = 0.f;
+        }
+        // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
+        if (e1 < 156) {
+            const int p0 = half * 98;
             float acc = 0.f;
-            for (int p = 0; p < 196; ++p) acc += g1[c * 196 + p];
+            if (e1 < 150) {
+#pragma unroll 7
+                for (int p = p0; p < p0 + 98; ++p) acc += g1[c1 * 196 + p] * in[off1[c1 * 196 + p] + o1];
+            } else {
+#pragma unroll 7
+                for (int p = p0; p < p0 + 98; ++p) acc += g1[cb1 * 196 + p];
+            }
             acc1 += acc;
         }
     }
+    __syncthreads();
+    if (half == 1) red[e1] = acc1;
+    __syncthreads();
     float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
-    if (tid < 156) out[tid] = acc1;
-    else if (tid < 172) out[2556 + tid - 156] = acc1;
+    if (half == 0 && e1 < 156) out[e1] = acc1 + red[e1];
+    if (tid < 16) out[2556 + tid] = accb2;
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const int e = tid + r * kThreads;
+    for (int r = 0; r < kR2; ++r) {
+        const int e = tid + r * kConvThreads;
         if (e < 2400) out[156 + e] = accw2[r];
     }
 }
@@ -536,7 +577,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     ca.r2 = W.r2;
     ca.dx2 = W.dx2;
     ca.part = W.part;
-    hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kThreads), 0, st, ca);
+    hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
     const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
     const float* Ws = W.wsamp;
     // head forward: H1 = relu(X2 W1^T + b1), H2 = relu(H1 W2^T + b2), D = H2 W3^T + b3
@@ -583,7 +624,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
                   (int64_t)M * 400, 400);
     if (hipError_t e = gemm(g, S, st)) return e;
     // conv towers backward, then the per-sample sums with eps
-    hipLaunchKernelGGL(lenet_conv_bwd_kernel, dim3(W.nchunk, S), dim3(kThreads), 0, st, ca);
+    hipLaunchKernelGGL(lenet_conv_bwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
     hipLaunchKernelGGL(lenet_conv_reduce_kernel,
                        dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
                        dim3(kThreads), 0, st, S, W.nchunk, nt, W.part, dW);
