@@ -127,6 +127,47 @@ def cpu_baseline(budget_s=12.0):
                         f"in {dt:.1f} s on {torch.get_num_threads()} threads of {model}"))
 
 
+def lenet_timings(dev, cpu=True, T=10):
+    """Auxiliary evidence, not the metric: config C5's inner step (make_lenet,
+    S = 256, M = 500 MNIST-shaped synthetic pseudopoints, N = 60000) through
+    psvi_inner_loop with in-library draws, and one op-faithful CPU step of the
+    same model (oracle/cpu_reference.py RefLenetStep: the reference's grouped
+    conv / max-pool / batched matmul sequence with create_graph autograd)."""
+    from psvi.models import LENET_LAYERS, make_lenet
+    from psvi.runtime import InnerLoopPlan
+
+    S, M = 256, 500
+    torch.manual_seed(0)
+    net = make_lenet(mc_samples=S, init_sd=0.05)
+    p0 = torch.nn.utils.parameters_to_vector(net.parameters()).detach()
+    plan = InnerLoopPlan("lenet", LENET_LAYERS, S, M)
+    g = torch.Generator().manual_seed(2)
+    u = torch.randn(M, 1, 28, 28, generator=g)
+    z = torch.randint(0, 10, (M,), generator=g)
+    w = torch.full((M,), 60000.0 / M)
+    params = p0.to(dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    ud, zd, wd = u.to(dev), z.to(dev, torch.int32), w.to(dev)
+    ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+    plan.inner_loop(ud, zd, wd, params, m, v, 2, LR, seed=1, ws=ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan.inner_loop(ud, zd, wd, params, m, v, T, LR, seed=2, ws=ws)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / T * 1e3
+    out = {"config": "C5 lenet S=256 M=500", "gpu_ms_per_inner_step": round(ms, 3),
+           "gpu_inner_steps_per_s": round(1e3 / ms, 2)}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from cpu_reference import RefLenetStep
+
+        t0 = time.perf_counter()
+        RefLenetStep(S).run(p0, u, z.float(), w, 1, LR)
+        out["cpu_ms_per_inner_step"] = round((time.perf_counter() - t0) * 1e3, 1)
+        out["cpu_threads"] = torch.get_num_threads()
+    return out
+
+
 def trainer_timings(dev, cpu=True, cpu_T=2):
     """Auxiliary evidence, not the metric: the outer step of the trainers at C3
     (fn2 64-40-40-2, S = 128, M = 100 pseudopoints, a 128-row data batch, the
@@ -195,6 +236,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-lenet", action="store_true",
+                    help="skip the auxiliary C5 (lenet) inner-step timing")
     ap.add_argument("--no-trainers", action="store_true",
                     help="skip the auxiliary outer-step (trainer) timings")
     args = ap.parse_args()
@@ -357,6 +400,9 @@ def main():
     trainers = None
     if rank == 0 and world == 1 and not args.no_trainers:
         trainers = trainer_timings(dev, cpu=not args.no_cpu_baseline)
+    lenet = None
+    if rank == 0 and world == 1 and not args.no_lenet:
+        lenet = lenet_timings(dev, cpu=not args.no_cpu_baseline)
     if world > 1:
         dist.barrier()
     if rank == 0:
@@ -380,6 +426,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "trainers": trainers,
+            "lenet_c5": lenet,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

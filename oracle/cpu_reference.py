@@ -206,6 +206,71 @@ class RefInnerStep:
         return out
 
 
+class _LenetLayer:
+    """One make_lenet variational layer: [weight, bias, _weight_sd, _bias_sd]."""
+
+    def __init__(self, wshape, batched):
+        nw = 1
+        for d in wshape:
+            nw *= d
+        nb = wshape[0]
+        self.shapes = [wshape, (nb,), wshape, (nb,)]
+        self.sizes = [nw, nb, nw, nb]
+        self.batched = batched
+
+
+class RefLenetStep(RefInnerStep):
+    """make_lenet (neural_net.py:334-359) with the reference's op sequence:
+    VIConv2d's grouped conv over the S-repeated input (202-246), BatchMaxPool2d
+    on the flattened (S*M) maps (249-255), batched VILinear matmuls, the last
+    layer one shared sample (mc_samples=1), KL over the VILinear layers only
+    (psvi_classes.py:506-510).  run() / nested-step machinery inherited."""
+
+    def __init__(self, S, prior_sd=1.0):
+        self.family, self.S, self.prior_sd = "lenet", S, prior_sd
+        self.layers = [_LenetLayer((6, 1, 5, 5), True), _LenetLayer((16, 6, 5, 5), True),
+                       _LenetLayer((120, 400), True), _LenetLayer((84, 120), True),
+                       _LenetLayer((10, 84), False)]
+
+    def _q(self, p):
+        W, b, rW, rb = p
+        return (D.Independent(D.Normal(W, F.softplus(rW)), W.ndim),
+                D.Independent(D.Normal(b, F.softplus(rb)), 1))
+
+    def elbo(self, params_list, u, z, w):
+        S = self.S
+        x = u.reshape(-1, 1, 28, 28)
+        for li, pad in ((0, 2), (1, 0)):
+            qW, qb = self._q(params_list[li])
+            Ws = qW.rsample((S,))
+            bs = qb.rsample((S, 1))
+            x = x.repeat(1, S, 1, 1) if x.ndim == 4 else x.transpose(0, 1).flatten(1, 2)
+            a = F.conv2d(x, Ws.flatten(0, 1), bs.flatten(), padding=pad, groups=S)
+            a = a.view(-1, S, Ws.shape[1], *a.shape[-2:]).transpose(0, 1)
+            a = torch.relu(a)
+            d0, d1 = a.shape[:2]
+            pooled = F.max_pool2d(a.flatten(0, 1), 2, 2)
+            x = pooled.view(d0, d1, *pooled.shape[1:])
+        h = x.flatten(-3, -1)
+        kl = 0.0
+        for li in (2, 3, 4):
+            W, b, _, _ = params_list[li]
+            qW, qb = self._q(params_list[li])
+            if li < 4:
+                Ws, bs = qW.rsample((S,)), qb.rsample((S, 1))
+            else:
+                Ws, bs = qW.rsample(), qb.rsample()
+            h = h.matmul(Ws.transpose(-2, -1)) + bs
+            if li < 4:
+                h = torch.relu(h)
+            pW = D.Independent(D.Normal(torch.zeros_like(W), self.prior_sd), 2)
+            pb = D.Independent(D.Normal(torch.zeros_like(b), self.prior_sd), 1)
+            kl = kl + D.kl_divergence(qW, pW) + D.kl_divergence(qb, pb)
+        torch.nn.LogSoftmax(dim=-1)(h).permute(1, 2, 0)  # computed, unused (psvi_classes.py:495)
+        nll = -D.Categorical(logits=h).log_prob(z)
+        return nll.matmul(w).sum() + kl
+
+
 class _EpsReplay:
     def __init__(self, flat):
         self.flat = torch.as_tensor(flat)

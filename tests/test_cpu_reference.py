@@ -41,3 +41,18 @@ def test_cpu_nested_step_matches_reference(name):
     assert rel(loss, f["loss"]) < 1e-10
     assert l2rel(gu.numpy(), f["u_grad"]) < 1e-8
     assert l2rel(gv.numpy(), f["v_grad"]) < 1e-8
+
+
+def test_lenet_op_faithful_step_matches_reference_fixture():
+    """RefLenetStep (the bench's C5 CPU baseline) replays make_lenet's inner
+    loop: the reference's ELBOs and Adam trajectory on its own draws."""
+    from cpu_reference import RefLenetStep
+
+    f = load_fixture("l1_lenet_tiny")
+    cfg = f["cfg"]
+    r = RefLenetStep(cfg["S"])
+    elbos, p = r.run(torch.tensor(f["params0"]), torch.tensor(f["u"]),
+                     torch.tensor(f["z"]), torch.tensor(f["w"]), cfg["T"], cfg["lr"],
+                     eps_list=[torch.tensor(e) for e in f["eps"]])
+    assert np.allclose(elbos, f["elbo"], rtol=1e-5)
+    assert np.linalg.norm(p.numpy() - f["params"][-1]) <= 1e-5 * np.linalg.norm(f["params"][-1])
