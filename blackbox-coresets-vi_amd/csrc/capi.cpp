@@ -609,6 +609,7 @@ int psvi_inner_step(const psvi_plan* p, const float* u, const int32_t* z, const 
     if (!params || !adam_m || !adam_v || !hp || !elbo_out)
         return fail(PSVI_EINVAL, "null state pointer");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
     return step_impl(p, u, z, w, eps, params, adam_m, adam_v, hp, elbo_out, nullptr, 1, ws,
                      as_stream(stream));
 }
@@ -648,6 +649,7 @@ int psvi_mf_phase_update(const psvi_plan* p, const float* acc, float* params, fl
     if (!acc || !params) return fail(PSVI_EINVAL, "null pointer");
     if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
     if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (!grad_out && (hp->kind < 0 || hp->kind > 2)) return fail(PSVI_EINVAL, "unknown adam kind");
     HIP_TRY(launch_mf_update(*p, acc, params, adam_m, adam_v, hp, kl_out, grad_out,
                              include_kl ? 1 : 0, as_stream(stream)));
     return 0;
@@ -684,6 +686,7 @@ int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_s
     if (!eps || !g_shard || !params) return fail(PSVI_EINVAL, "null pointer");
     if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
     if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (!grad_out && (hp->kind < 0 || hp->kind > 2)) return fail(PSVI_EINVAL, "unknown adam kind");
     HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, grad_out,
                               include_kl ? 1 : 0, nullptr, nullptr, as_stream(stream)));
     return 0;
@@ -698,6 +701,7 @@ int psvi_mvn_phase_update_sample(const psvi_plan* p, const float* eps, const flo
     if (!eps || !g_shard || !params || !eps_next || !x_next) return fail(PSVI_EINVAL, "null pointer");
     if (!adam_m || !adam_v || !hp) return fail(PSVI_EINVAL, "null adam state");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
     HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, nullptr,
                               include_kl ? 1 : 0, eps_next, x_next, as_stream(stream)));
     return 0;
@@ -738,6 +742,7 @@ int psvi_mvn_phase_update_tiled(const psvi_plan* p, const float* eps, const floa
         return fail(PSVI_EINVAL, "null pointer");
     if (!eps_next != !x_next) return fail(PSVI_EINVAL, "eps_next and x_next go together");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
     HIP_TRY(launch_mvn_update(*p, eps, g_shard, params, adam_m, adam_v, hp, kl_out, nullptr,
                               include_kl ? 1 : 0, eps_next, x_next, as_stream(stream), tstate));
     return 0;
@@ -754,6 +759,7 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         return fail(PSVI_EINVAL, "null pointer");
     if (T < 0) return fail(PSVI_EINVAL, "T must be >= 0");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
     if (!eps && offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");
     if (!ws || ws_bytes < loop_ws_bytes(p)) return fail(PSVI_ENOSPC, "workspace too small");
     hipStream_t st = as_stream(stream);
@@ -955,6 +961,8 @@ int psvi_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const fl
     if (n < 0 || !lt || !lm || !lv || !adam_m || !adam_v || !grad || !lg_out || !hp)
         return fail(PSVI_EINVAL, "bad adam adjoint arguments");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (hp->kind != PSVI_ADAM_HIGHER && hp->kind != PSVI_ADAM_HYPERGRAD)
+        return fail(PSVI_EUNSUP, "adam adjoint: higher / hypergrad variants only");
     HIP_TRY(launch_adam_adjoint(n, lt, lm, lv, adam_m, adam_v, grad, lg_out, hp,
                                 as_stream(stream)));
     return 0;
@@ -972,6 +980,7 @@ int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m,
     if (n < 0 || !params || !grad || !adam_m || !adam_v || !hp)
         return fail(PSVI_EINVAL, "bad adam arguments");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
+    if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
     HIP_TRY(launch_adam(n, params, grad, adam_m, adam_v, hp, as_stream(stream)));
     return 0;
 }

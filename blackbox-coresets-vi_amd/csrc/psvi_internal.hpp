@@ -133,6 +133,11 @@ __device__ __forceinline__ float adam_apply(const AdamC& a, float p, float g, fl
         v = a.b2 * v + a.omb2 * g * g;
         const float denom = sqrtf(v + 1e-8f) * a.inv_sqrt_bc2 + a.eps;
         return p - a.lr_bc1 * (m / denom);
+    } else if (a.kind == PSVI_ADAM_TORCH) {
+        // torch.optim.Adam (single-tensor path): denom = sqrt(v)/sqrt(bc2) + eps
+        v = a.b2 * v + a.omb2 * g * g;
+        const float denom = sqrtf(v) * a.inv_sqrt_bc2 + a.eps;
+        return p - a.lr_bc1 * (m / denom);
     } else {
         // diff_optimizers.py:197-213: v += 1e-12 stored; denom = sqrt(v/bc2)+eps
         v = a.b2 * v + a.omb2 * g * g + 1e-12f;
@@ -149,6 +154,10 @@ __device__ __forceinline__ float adam_apply_fast(const AdamC& a, float p, float 
     if (a.kind == PSVI_ADAM_HIGHER) {
         v = a.b2 * v + a.omb2 * g * g;
         const float denom = __builtin_amdgcn_sqrtf(v + 1e-8f) * a.inv_sqrt_bc2 + a.eps;
+        return p - a.lr_bc1 * m * __builtin_amdgcn_rcpf(denom);
+    } else if (a.kind == PSVI_ADAM_TORCH) {
+        v = a.b2 * v + a.omb2 * g * g;
+        const float denom = __builtin_amdgcn_sqrtf(v) * a.inv_sqrt_bc2 + a.eps;
         return p - a.lr_bc1 * m * __builtin_amdgcn_rcpf(denom);
     } else {
         v = a.b2 * v + a.omb2 * g * g + 1e-12f;

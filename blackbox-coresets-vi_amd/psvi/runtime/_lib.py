@@ -17,6 +17,7 @@ FAMILY_FULLCOV = 1
 FAMILY_LENET = 2
 ADAM_HIGHER = 0
 ADAM_HYPERGRAD = 1
+ADAM_TORCH = 2
 
 Q_PARAM_COUNT = 1
 Q_EPS_COUNT = 2

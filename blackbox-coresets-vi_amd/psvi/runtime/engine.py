@@ -35,7 +35,8 @@ def _need(t, name, numel, dtype=torch.float32):
 
 
 def make_adam(lr, step, kind="higher", betas=(0.9, 0.999), eps=1e-8):
-    k = {"higher": _lib.ADAM_HIGHER, "hypergrad": _lib.ADAM_HYPERGRAD}[kind]
+    k = {"higher": _lib.ADAM_HIGHER, "hypergrad": _lib.ADAM_HYPERGRAD,
+         "torch": _lib.ADAM_TORCH}[kind]
     return AdamHP(float(lr), float(betas[0]), float(betas[1]), float(eps), int(step), k)
 
 

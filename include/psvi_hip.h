@@ -86,6 +86,9 @@ extern "C" {
                                    denom = sqrt(v + 1e-8)/sqrt(bc2) + eps            */
 #define PSVI_ADAM_HYPERGRAD 1   /* hypergrad adam_step (diff_optimizers.py:197-213):
                                    v += 1e-12 stored; denom = sqrt(v/bc2) + eps      */
+#define PSVI_ADAM_TORCH     2   /* torch.optim.Adam (the MFVI baselines' optim_vi,
+                                   baselines.py:870, 1020): denom = sqrt(v)/sqrt(bc2) + eps;
+                                   not differentiable here (psvi_adam_adjoint refuses) */
 
 typedef struct psvi_net_desc {
     int32_t n_layers;                     /* affine VI layers                     */

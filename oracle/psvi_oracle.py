@@ -979,3 +979,45 @@ def lenet_inner_loop(params0, u, z, w, eps_steps, S, lr, adam_kind, prior_sd=1.0
         p, m, v = adam(adam_kind, p, g, m, v, t0 + k, lr)
         traj.append(p.copy())
     return np.array(elbos), grads, traj, m, v
+
+
+# ------------------------------------------------------- MFVI baselines
+def mfvi_run(family, layers, params0, x, y, xt, yt, draws, S, iters, log_every, lr, scale,
+             eval_last=True, prior_sd=1.0):
+    """run_mfvi / run_mfvi_subset (psvi/inference/baselines.py:824-914, 917-1062):
+    per iteration loss = scale * sum_{s,b} NLL + KL(VILinear modules only: none
+    for a full-covariance stack, baselines.py:889), torch.optim.Adam; every
+    log_every iterations (and the last one for run_mfvi: eval_last) the
+    predictive of the MEAN LOGITS over S: accuracy and mean NLL.  ``draws`` is
+    the flat noise stream in consumption order (training and evaluation
+    forwards interleaved).  Returns (elbos, accs, nlls, params)."""
+    f = mf_elbo_grad if family == "mf" else mvn_elbo_grad
+    n_eps = (mf_eps_count if family == "mf" else mvn_eps_count)(layers, S)
+    p = np.asarray(params0, np.float64).copy()
+    m, v = np.zeros_like(p), np.zeros_like(p)
+    x = np.asarray(x, np.float64)
+    w = np.full(x.shape[0], float(scale))
+    o = 0
+    elbos, accs, nlls = [], [], []
+    for i in range(iters):
+        e = np.asarray(draws[o:o + n_eps], np.float64)
+        o += n_eps
+        val, g = f(layers, p, x, y, w, e, S, prior_sd)
+        if family != "mf":
+            k, gk = f(layers, p, x, y, 0 * w, e, S, prior_sd)
+            val, g = val - k, g - gk
+        elbos.append(-val)
+        p, m, v = torch_adam_step(p, g, m, v, i + 1, lr)
+        if i % log_every == 0 or (eval_last and i == iters - 1):
+            e = np.asarray(draws[o:o + n_eps], np.float64)
+            o += n_eps
+            Ws, bs = _split(layers, _sample(family, layers, p, e, S))
+            hs, _ = _net_rows_forward(np.asarray(xt, np.float64), Ws, bs)
+            lg = hs[-1].mean(0)
+            yi = np.asarray(yt).astype(np.int64)
+            mx = lg.max(-1, keepdims=True)
+            ls = lg - mx - np.log(np.exp(lg - mx).sum(-1, keepdims=True))
+            accs.append(float((lg.argmax(-1) == yi).mean()))
+            nlls.append(float(-ls[np.arange(len(yi)), yi].mean()))
+    assert o == len(draws), (o, len(draws))
+    return np.array(elbos), np.array(accs), np.array(nlls), p

@@ -18,7 +18,8 @@ def fixture_names(prefix="g"):
 def load_fixture(name):
     d = np.load(os.path.join(GOLDEN, name + ".npz"))
     cfg = json.loads(str(d["config"]))
-    cfg["layers"] = [tuple(x) for x in cfg["layers"]]
+    if "layers" in cfg:
+        cfg["layers"] = [tuple(x) for x in cfg["layers"]]
     out = {k: d[k] for k in d.files if k != "config"}
     out["cfg"] = cfg
     return out
