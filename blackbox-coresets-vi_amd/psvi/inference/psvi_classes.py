@@ -54,7 +54,7 @@ import torch.nn as nn
 from torch.autograd.function import once_differentiable
 
 from ..models.neural_net import (VILinear, VILinearMultivariateNormal, categorical_fn,
-                                 make_fc2net, make_fcnet, model_spec)
+                                 make_fc2net, make_fcnet, make_lenet, model_spec)
 from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
@@ -153,6 +153,13 @@ class PSVI:
         self._eps_offset = 0
 
     # ------------------------------------------------------------ helpers
+    def _outer_supported(self, what):
+        """The outer objective, its second order and evaluate run for the
+        MLP families; make_lenet runs the inner loop only."""
+        if model_spec(self.model)[0] == "lenet":
+            raise NotImplementedError(f"{what} for make_lenet is not built on the HIP path "
+                                      "(its inner loop is)")
+
     def coreset_weights(self):
         """N f(v): the per-pseudopoint NLL weights (detached, fp32)."""
         with torch.no_grad():
@@ -255,6 +262,9 @@ class PSVI:
         assert self.mc_samples is None or self.mc_samples > 1  # psvi_classes.py:449
         model = self.model if model is None else model
         fam, layers, prior_sd, S = model_spec(model)
+        if fam == "lenet":
+            raise NotImplementedError("psvi_elbo for make_lenet is not built on the HIP path "
+                                      "(its inner loop is)")
         if S < 2:
             raise ValueError("psvi_elbo needs mc_samples > 1 (psvi_classes.py:449)")
         Mu = int(self.u.shape[0])
@@ -346,6 +356,7 @@ class PSVI:
         importance weights, normalised ESS, v-entropy), one psvi_evaluate per
         test batch (fresh weights per batch; entropy / ESS from the last one,
         as the reference).  ``eps``: optional list of draws, one per batch."""
+        self._outer_supported("evaluate")
         assert self.mc_samples is None or self.mc_samples > 1
         it = iter(eps) if eps is not None else None
         correct = nll = last = None
@@ -404,6 +415,7 @@ class PSVI:
         ``eps_outer``: optional sequences of draws (library eps layout) in the
         reference's call order, to replay; default: this instance's Philox
         stream."""
+        self._outer_supported("hyper_step")
         if hypergrad_approx not in ("CG_normaleq", "fixed_point"):
             raise NotImplementedError(f"hypergrad_approx={hypergrad_approx!r}: the reference's "
                                       "hyper_step offers CG_normaleq and fixed_point")
@@ -546,6 +558,7 @@ class PSVI:
         are written into the model.  Returns the outer loss (0-dim tensor).
         ``eps_inner`` (T draws) / ``eps_outer`` (1): optional replay of the
         reference's draws; default this instance's Philox stream."""
+        self._outer_supported("nested_step")
         if truncated:
             raise NotImplementedError("truncated nested_step (torch.optim.Adam warm start) is "
                                       "not on the HIP path")
@@ -643,9 +656,12 @@ class PSVI:
             self.model = make_fc2net(self.D, self.n_hidden, self.nc,
                                      linear_class=VILinearMultivariateNormal, nonl_class=nn.ReLU,
                                      **kw)
+        elif self.architecture == "lenet":
+            # inner loop only on the HIP path (psvi_elbo / HVP for LeNet: not built)
+            self.model = make_lenet(linear_class=VILinear, nonl_class=nn.ReLU, **kw)
         else:
             raise NotImplementedError(f"architecture {self.architecture!r} is not on the HIP path "
-                                      "(lenet / alexnet / resnet / residual_fn / regressor_net)")
+                                      "(alexnet / resnet / residual_fn / regressor_net)")
         self.model = self.model.to(self.device)
 
     @staticmethod
