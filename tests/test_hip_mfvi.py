@@ -75,3 +75,19 @@ def test_mfvi_lenet_step_runs_on_hip():
                    train_dataset=TensorDataset(x, y), test_dataset=TensorDataset(x[:16], y[:16]))
     assert len(res["elbos"]) == 3 and np.isfinite(res["elbos"]).all()
     assert len(res["accs"]) == 2
+
+
+def test_experiment_driver_end_to_end(tmp_path):
+    """flow_psvi-style driver on halfmoon: a PSVI method and the MFVI baseline,
+    results dict in the reference's layout, written as .pk / .json."""
+    from psvi.experiments import experiment_driver
+
+    args = dict(mc_samples=4, num_epochs=2, data_minibatch=100, inner_it=2, trainer="nested",
+                log_every=1, lr0u=1e-3, lr0net=1e-3, lr0v=1e-2, init_sd=1e-3,
+                coreset_sizes=[10], num_trials=1, test_ratio=0.2, architecture="fn",
+                logistic_regression=False, n_hidden=10, fnm="drv",
+                results_folder=str(tmp_path))
+    res = experiment_driver(["halfmoon"], ["psvi_learn_v", "mfvi"], args)
+    assert len(res["halfmoon"]["psvi_learn_v"]["10"]["0"]["accs"]) >= 1
+    assert len(res["halfmoon"]["mfvi"]["-1"]["0"]["elbos"]) == 4
+    assert (tmp_path / "drv.pk").exists() and (tmp_path / "drv.json").exists()
