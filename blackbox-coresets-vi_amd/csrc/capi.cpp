@@ -507,7 +507,7 @@ static size_t eval_ws_bytes(const psvi_plan* p) {
 }
 
 static OuterWs outer_ws(const psvi_plan* p, void* ws) {
-    const size_t S = p->d.S, M = p->d.M, D = p->lay[0].din;
+    const size_t S = p->d.S, M = p->d.M, D = plan_in_dim(*p);
     char* b = (char*)ws;
     OuterWs o{};
     size_t off = align256(p->ws_bytes);
@@ -829,8 +829,6 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
                          float* grad_u, float* grad_w, double* sample_out, void* ws,
                          size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
-    if (p->family == PSVI_FAMILY_LENET)
-        return fail(PSVI_EUNSUP, "LeNet plans run the inner loop only (outer objective: not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "the outer objective needs world == 1");
     if (p->d.S < 2) return fail(PSVI_EINVAL, "psvi_elbo needs S > 1 (psvi_classes.py:449)");
@@ -858,8 +856,12 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
     HIP_TRY(launch_outer_stats(*p, params, eps, x, o.stats, st));
     // 1. forward: every row's NLL
     NetOuter fw{1, n_pseudo, o.nll, nullptr, nullptr, nullptr};
-    HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
-                       nullptr, st, nullptr, 0, 0, 0, &fw));
+    if (p->family == PSVI_FAMILY_LENET)
+        HIP_TRY(launch_lenet(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr,
+                             p->d_lenet_ws, st, &fw));
+    else
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
+                           nullptr, st, nullptr, 0, 0, 0, &fw));
     // 2. per-sample terms, softmax over samples, loss, backward coefficients
     HIP_TRY(launch_outer_combine(*p, n_pseudo, params, w_all, o.nll, o.stats, loss_out,
                                  o.rowcoef, o.ck, o.sck, grad_w, sample_out, st));
@@ -874,6 +876,11 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
         // 4. reparameterised backward (no KL term: the sampled KL came in through G)
         HIP_TRY(launch_mvn_update(*p, eps, g, const_cast<float*>(params), nullptr, nullptr,
                                   nullptr, nullptr, grad_params, 0, nullptr, nullptr, st));
+    } else if (p->family == PSVI_FAMILY_LENET) {
+        HIP_TRY(launch_lenet(*p, x_all, z_all, w_all, params, eps, acc, nullptr, p->d_lenet_ws,
+                             st, &bw));
+        HIP_TRY(launch_mf_update(*p, acc, const_cast<float*>(params), nullptr, nullptr, nullptr,
+                                 nullptr, grad_params, 0, st));
     } else {
         HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
         HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, acc, acc + p->n_tot, nullptr,
@@ -892,8 +899,6 @@ int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, cons
                   const float* w_all, const float* eps, const float* params, int32_t correction,
                   float* probs_out, double* stats_out, void* ws, size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
-    if (p->family == PSVI_FAMILY_LENET)
-        return fail(PSVI_EUNSUP, "LeNet plans run the inner loop only (outer objective: not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "evaluate needs world == 1");
     if (p->d.S < 2) return fail(PSVI_EINVAL, "evaluate needs S > 1 (psvi_classes.py:1036)");
@@ -915,8 +920,12 @@ int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, cons
     }
     HIP_TRY(launch_outer_stats(*p, params, eps, x, o.stats, st));
     NetOuter fw{1, n_pseudo, o.nll, nullptr, nullptr, nullptr, prob};
-    HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
-                       nullptr, st, nullptr, 0, 0, 0, &fw));
+    if (p->family == PSVI_FAMILY_LENET)
+        HIP_TRY(launch_lenet(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr,
+                             p->d_lenet_ws, st, &fw));
+    else
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
+                           nullptr, st, nullptr, 0, 0, 0, &fw));
     HIP_TRY(launch_eval(*p, n_pseudo, params, w_all, z_all, o.nll, o.stats, prob,
                         correction ? 1 : 0, W, probs_out, stats_out, st));
     return 0;
@@ -927,7 +936,7 @@ int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* 
              float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (p->family == PSVI_FAMILY_LENET)
-        return fail(PSVI_EUNSUP, "LeNet plans run the inner loop only (outer objective: not built)");
+        return fail(PSVI_EUNSUP, "LeNet plans have no HVP (its R-op through the conv towers is not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "psvi_hvp needs world == 1");
     if (!u || !z || !w || !eps || !params || !vec || !hv_out)

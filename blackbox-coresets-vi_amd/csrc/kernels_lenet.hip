@@ -68,17 +68,24 @@ __global__ __launch_bounds__(kThreads) void lenet_sample_kernel(SampleArgs a,
 }
 
 // acc[j] = sum_s dW[s][j],  acc[n_tot + j] = sum_s dW[s][j] eps_(s, j)
+// ck (outer backward, nullable): the pathwise sampled-KL gradient
+// -ck_s W_s / s0^2 joins every VILinear-layer weight gradient
 __global__ __launch_bounds__(kThreads) void lenet_acc_kernel(SampleArgs a,
                                                              const float* __restrict__ eps,
                                                              const float* __restrict__ dws,
-                                                             float* __restrict__ acc) {
+                                                             float* __restrict__ acc,
+                                                             const float* __restrict__ ck,
+                                                             const float* __restrict__ wsamp,
+                                                             float inv_s0sq) {
     const int j = blockIdx.x * kThreads + threadIdx.x;
     if (j >= a.n_tot) return;
     const int l = lenet_layer(a, j);
     const int idx = j - a.woff[l];
+    const bool path = ck != nullptr && l >= 2;
     float g = 0.f, ge = 0.f;
     for (int s = 0; s < a.S_loc; ++s) {
-        const float d = dws[(int64_t)s * a.n_tot + j];
+        float d = dws[(int64_t)s * a.n_tot + j];
+        if (path) d -= ck[s] * wsamp[(int64_t)s * a.n_tot + j] * inv_s0sq;
         g += d;
         ge += d * eps[lenet_eps_index(a, l, idx, a.s_off + s)];
     }
@@ -97,6 +104,8 @@ struct ConvArgs {
     int8_t* r2;           // [S][M][400]
     const float* dx2;     // bwd: [S][M][400]
     float* part;          // bwd: [S][nchunk][2572]
+    float* du;            // bwd <DU>: [S][n_pseudo][784] input gradient of the pseudo rows
+    int n_pseudo;
 };
 
 // relu + first-max 2x2 pool of four conv values in window order (0,0) (0,1)
@@ -212,7 +221,13 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
 // order by lenet_conv_reduce_kernel: bitwise run-to-run reproducible.
 constexpr int kDA = 18;  // routed conv2 gradient plane, 10x10 plus a 4-wide zero border
 
+// DU (outer backward): also d u = the transposed conv1 of the routed conv1
+// gradient (dense, zero-bordered LDS plane, 2x2 pixel blocks per thread) for
+// the pseudopoint rows m < n_pseudo.
+template <bool DU>
 __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a) {
+    __shared__ float w1[DU ? 150 : 1];
+    __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
     __shared__ float w2[2400];
     __shared__ float in[32 * 32];
     __shared__ float p1[kP1];
@@ -226,6 +241,10 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
     for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
     for (int i = tid; i < 16 * kDA * kDA; i += kConvThreads) da2[i] = 0.f;
+    if (DU) {
+        for (int i = tid; i < 150; i += kConvThreads) w1[i] = ws[i];
+        for (int i = tid; i < 6 * 1024; i += kConvThreads) da1[i] = 0.f;
+    }
     // conv2 weight entries owned by this thread: e = tid + r * 320
     constexpr int kR2 = (2400 + kConvThreads - 1) / kConvThreads;
     int kb[kR2], pb[kR2];
@@ -331,6 +350,42 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
                 for (int p = p0; p < p0 + 98; ++p) acc += g1[cb1 * 196 + p];
             }
             acc1 += acc;
+        }
+        if (DU && m < a.n_pseudo) {
+            for (int o = tid; o < kP1; o += kConvThreads)
+                da1[(o / 196) * 1024 + off1[o] + 2 * 32 + 2] = g1[o];
+            __syncthreads();
+            if (tid < 196) {
+                const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
+                float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+                for (int c = 0; c < 6; ++c) {
+                    const float* q = da1 + c * 1024 + yy * 32 + xx;
+                    float Q[6][6];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i)
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * 32 + j];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) {
+                            const float wv = w1[c * 25 + i * 5 + j];
+                            acc[0] += wv * Q[4 - i][4 - j];
+                            acc[1] += wv * Q[4 - i][5 - j];
+                            acc[2] += wv * Q[5 - i][4 - j];
+                            acc[3] += wv * Q[5 - i][5 - j];
+                        }
+                }
+                float* out = a.du + ((int64_t)s * a.n_pseudo + m) * 784 + yy * 28 + xx;
+                out[0] = acc[0];
+                out[1] = acc[1];
+                out[28] = acc[2];
+                out[29] = acc[3];
+            }
+            __syncthreads();
+            for (int o = tid; o < kP1; o += kConvThreads)
+                da1[(o / 196) * 1024 + off1[o] + 2 * 32 + 2] = 0.f;
         }
     }
     __syncthreads();
@@ -448,14 +503,53 @@ __global__ __launch_bounds__(kThreads) void lenet_colsum_kernel(const float* __r
 }
 
 // weighted NLL of each (s, m) row and d logits in place: w_m (softmax - onehot)
+// mode 0 (inner step): nll_out += sum w_m NLL, D <- w_m (softmax - onehot);
+// mode 1 (outer forward): nll_rows[s][m] <- NLL, prob_rows <- softmax of the
+// data rows (m >= n_pseudo), D untouched; mode 2 (outer backward): D <-
+// coef_sm (softmax - onehot), coef_sm = w_m rowcoef[s][m >= n_pseudo]
+struct LossOuter {
+    int mode, n_pseudo;
+    float* nll_rows;
+    float* prob_rows;
+    const float* rowcoef;
+};
+
 __global__ __launch_bounds__(kThreads) void lenet_loss_kernel(int rows, int M,
                                                               const int32_t* __restrict__ z,
                                                               const float* __restrict__ w,
                                                               float* __restrict__ D,
-                                                              double* __restrict__ nll_out) {
+                                                              double* __restrict__ nll_out,
+                                                              LossOuter o) {
     __shared__ float red[kThreads / kWave];
     const int r = blockIdx.x * kThreads + threadIdx.x;
     float contrib = 0.f;
+    if (o.mode != 0) {
+        if (r >= rows) return;
+        const int m = r % M, s = r / M;
+        float* d = D + (int64_t)r * 10;
+        float l[10];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) { l[c] = d[c]; mx = fmaxf(mx, l[c]); }
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) { l[c] = expf(l[c] - mx); se += l[c]; }
+        const int zc = min(max(z[m], 0), 9);
+        const float inv = 1.f / se;
+        if (o.mode == 1) {
+            o.nll_rows[r] = mx + logf(se) - d[zc];
+            if (o.prob_rows && m >= o.n_pseudo) {
+                float* pr = o.prob_rows + ((int64_t)s * (M - o.n_pseudo) + (m - o.n_pseudo)) * 10;
+#pragma unroll
+                for (int c = 0; c < 10; ++c) pr[c] = l[c] * inv;
+            }
+        } else {
+            const float cf = w[m] * o.rowcoef[2 * s + (m >= o.n_pseudo ? 1 : 0)];
+#pragma unroll
+            for (int c = 0; c < 10; ++c) d[c] = cf * (l[c] * inv - (c == zc ? 1.f : 0.f));
+        }
+        return;
+    }
     if (r < rows) {
         const int m = r % M;
         float* d = D + (int64_t)r * 10;
@@ -553,8 +647,16 @@ static SampleArgs sample_args(const psvi_plan& p) {
 
 hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                         const float* params, const float* eps, float* acc, double* nll_out,
-                        void* ws, hipStream_t st) {
+                        void* ws, hipStream_t st, const NetOuter* outer) {
     const LenetWs W = lenet_ws(p, ws);
+    LossOuter lo{};
+    if (outer) {
+        lo.mode = outer->mode;
+        lo.n_pseudo = outer->n_pseudo;
+        lo.nll_rows = outer->nll_rows;
+        lo.prob_rows = outer->prob_rows;
+        lo.rowcoef = outer->rowcoef;
+    }
     const SampleArgs sa = sample_args(p);
     const int S = sa.S_loc, M = p.d.M, nt = p.n_tot;
     if (S == 0) return hipMemsetAsync(acc, 0, sizeof(float) * 2 * nt, st);
@@ -594,7 +696,8 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     g.epi = 1; g.bias = Ws + w5 + 840; g.sbias = nt;
     if (hipError_t e = gemm(g, S, st)) return e;
     hipLaunchKernelGGL(lenet_loss_kernel, dim3((unsigned)((rows + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, st, (int)rows, M, z, w, W.d, nll_out);
+                       dim3(kThreads), 0, st, (int)rows, M, z, w, W.d, nll_out, lo);
+    if (lo.mode == 1) return hipGetLastError();
     // head backward
     float* dW = W.dws;
     g = gemm_args(10, 84, M, W.d, (int64_t)M * 10, 1, 10, W.h2, (int64_t)M * 84, 84, 1,
@@ -624,12 +727,22 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
                   (int64_t)M * 400, 400);
     if (hipError_t e = gemm(g, S, st)) return e;
     // conv towers backward, then the per-sample sums with eps
-    hipLaunchKernelGGL(lenet_conv_bwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
+    const bool du = outer && outer->du_part;
+    if (du) {
+        ca.du = outer->du_part;
+        ca.n_pseudo = outer->n_pseudo;
+        hipLaunchKernelGGL(lenet_conv_bwd_kernel<true>, dim3(W.nchunk, S), dim3(kConvThreads), 0,
+                           st, ca);
+    } else {
+        hipLaunchKernelGGL(lenet_conv_bwd_kernel<false>, dim3(W.nchunk, S), dim3(kConvThreads), 0,
+                           st, ca);
+    }
     hipLaunchKernelGGL(lenet_conv_reduce_kernel,
                        dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
                        dim3(kThreads), 0, st, S, W.nchunk, nt, W.part, dW);
     hipLaunchKernelGGL(lenet_acc_kernel, dim3((nt + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                       st, sa, eps, dW, acc);
+                       st, sa, eps, dW, acc, outer ? outer->ck : nullptr, W.wsamp,
+                       1.f / (p.d.prior_sd * p.d.prior_sd));
     return hipGetLastError();
 }
 

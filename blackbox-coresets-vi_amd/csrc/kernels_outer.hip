@@ -26,6 +26,10 @@ namespace psvi {
 
 struct OuterArgs {
     int L, S, M, n_pseudo, n_tot, family;
+    unsigned nkl_mask;     // layers in the sampled KL (plan_nkl_mask)
+    int nkl_n;             // their sampled elements per sample
+    int in_dim;            // input features per row (plan_in_dim)
+    int batched[kMaxL];    // LeNet: the last layer is one shared sample
     int n[kMaxL], woff[kMaxL];
     int64_t poff[kMaxL], eoff[kMaxL];
     int din[kMaxL], dout[kMaxL];
@@ -83,13 +87,15 @@ __global__ __launch_bounds__(256) void outer_stats_kernel(OuterArgs a) {
     const int s = blockIdx.x;
     double sx = 0.0, se = 0.0;
     for (int l = 0; l < a.L; ++l) {
+        if (!((a.nkl_mask >> l) & 1u)) continue;
         const int n = a.n[l];
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             float e, x;
-            if (a.family == PSVI_FAMILY_MEANFIELD) {
+            if (a.family != PSVI_FAMILY_FULLCOV) {
                 const int dout = a.dout[l], nwl = a.din[l] * dout;
-                e = i < nwl ? a.eps[a.eoff[l] + (int64_t)s * nwl + i]
-                            : a.eps[a.eoff[l] + (int64_t)a.S * nwl + (int64_t)s * dout + i - nwl];
+                e = !a.batched[l] ? a.eps[a.eoff[l] + i]
+                    : i < nwl ? a.eps[a.eoff[l] + (int64_t)s * nwl + i]
+                              : a.eps[a.eoff[l] + (int64_t)a.S * nwl + (int64_t)s * dout + i - nwl];
                 const float mu = a.params[a.poff[l] + i], rho = a.params[a.poff[l] + n + i];
                 x = mu + e * softplus_f(rho);
             } else {
@@ -120,10 +126,12 @@ __global__ __launch_bounds__(1024) void outer_combine_kernel(OuterArgs a) {
     // sum_i log sigma_i: the scales sit at poff + n .. poff + 2n in both families
     double sl = 0.0;
     for (int l = 0; l < a.L; ++l)
-        for (int i = tid; i < a.n[l]; i += nthr) sl += log((double)softplus_f(a.params[a.poff[l] + a.n[l] + i]));
+        if ((a.nkl_mask >> l) & 1u)
+            for (int i = tid; i < a.n[l]; i += nthr)
+                sl += log((double)softplus_f(a.params[a.poff[l] + a.n[l] + i]));
     sl = block_sum_all(sl, red);
     const double s0 = a.s0, inv2 = 0.5 / (s0 * s0);
-    const double nlog = a.n_tot * log(s0);
+    const double nlog = a.nkl_n * log(s0);
     // per sample (one wave each): pseudo_s, data_s
     for (int s = wid; s < a.S; s += nwv) {
         double ps = 0.0, ds = 0.0;
@@ -200,9 +208,11 @@ __global__ __launch_bounds__(1024) void eval_weights_kernel(OuterArgs a, int cor
     const int lane = tid & 63, wid = wave_id(), nwv = nthr >> 6;
     double sl = 0.0;
     for (int l = 0; l < a.L; ++l)
-        for (int i = tid; i < a.n[l]; i += nthr) sl += log((double)softplus_f(a.params[a.poff[l] + a.n[l] + i]));
+        if ((a.nkl_mask >> l) & 1u)
+            for (int i = tid; i < a.n[l]; i += nthr)
+                sl += log((double)softplus_f(a.params[a.poff[l] + a.n[l] + i]));
     sl = block_sum_all(sl, red);
-    const double s0 = a.s0, inv2 = 0.5 / (s0 * s0), nlog = a.n_tot * log(s0);
+    const double s0 = a.s0, inv2 = 0.5 / (s0 * s0), nlog = a.nkl_n * log(s0);
     for (int s = wid; s < a.S; s += nwv) {
         double ps = 0.0;
         const float* row = a.nll + (size_t)s * a.M;
@@ -302,9 +312,11 @@ __global__ __launch_bounds__(256) void outer_finish_kernel(OuterArgs a, int nu) 
     if (i < a.n_tot && a.grad) {
         int l = 0;
         while (l + 1 < a.L && i >= a.woff[l + 1]) ++l;
-        const int64_t ps = a.poff[l] + a.n[l] + (i - a.woff[l]);
-        const float r = a.params[ps];
-        a.grad[ps] += a.sck[0] * sigmoid_f(r) / softplus_f(r);
+        if ((a.nkl_mask >> l) & 1u) {
+            const int64_t ps = a.poff[l] + a.n[l] + (i - a.woff[l]);
+            const float r = a.params[ps];
+            a.grad[ps] += a.sck[0] * sigmoid_f(r) / softplus_f(r);
+        }
     }
     const int j = i - a.n_tot;
     if (j >= 0 && j < nu && a.grad_u) {
@@ -321,6 +333,13 @@ static void fill(const psvi_plan& p, OuterArgs& a) {
     a.n_tot = p.n_tot;
     a.family = p.family;
     a.s0 = p.d.prior_sd;
+    a.nkl_mask = plan_nkl_mask(p);
+    a.in_dim = plan_in_dim(p);
+    a.nkl_n = 0;
+    for (int l = 0; l < p.L; ++l) {
+        a.batched[l] = !(p.family == PSVI_FAMILY_LENET && l == p.L - 1);
+        if ((a.nkl_mask >> l) & 1u) a.nkl_n += p.lay[l].n;
+    }
     for (int l = 0; l < p.L; ++l) {
         a.n[l] = p.lay[l].n;
         a.woff[l] = p.lay[l].woff;
@@ -376,7 +395,7 @@ hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* pa
     a.grad = grad;
     a.du_part = du_part;
     a.grad_u = grad_u;
-    const int nu = grad_u ? n_pseudo * p.lay[0].din : 0;
+    const int nu = grad_u ? n_pseudo * plan_in_dim(p) : 0;
     const int n = p.n_tot + nu;
     hipLaunchKernelGGL(outer_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, nu);
     return hipGetLastError();

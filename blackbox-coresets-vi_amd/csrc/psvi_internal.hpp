@@ -264,6 +264,15 @@ struct psvi_plan {
 };
 
 namespace psvi {
+// input features per row: D, or 1x28x28 for LeNet
+inline int plan_in_dim(const psvi_plan& p) {
+    return p.family == PSVI_FAMILY_LENET ? 784 : p.lay[0].din;
+}
+// layers whose sampled KL enters psvi_elbo (LeNet: the VILinear layers only,
+// psvi_classes.py:455-459 sums sampled_nkl over VILinear modules)
+inline unsigned plan_nkl_mask(const psvi_plan& p) {
+    return p.family == PSVI_FAMILY_LENET ? 0x1Cu : 0xFFu;
+}
 // launchers (defined in the .hip translation units)
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* accMu, float* accRho,
@@ -314,9 +323,12 @@ int lenet_nchunk(const psvi_plan& p);
 LenetWs lenet_ws(const psvi_plan& p, void* base);  // base nullptr: sizes only
 // per-sample weight draw, forward, weighted NLL (+= nll_out), backward, and
 // acc = [sum_s dW | sum_s dW eps] over the rank's samples (acc fully written)
+// outer (psvi_outer_elbo_grad / psvi_evaluate): mode 1 forward only (per-row
+// NLL, softmax of the data rows), mode 2 backward of the row coefficients with
+// the pathwise sampled-KL term on the VILinear layers and d u of the pseudo rows
 hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                         const float* params, const float* eps, float* acc, double* nll_out,
-                        void* ws, hipStream_t st);
+                        void* ws, hipStream_t st, const NetOuter* outer = nullptr);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
 hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,

@@ -154,11 +154,11 @@ class PSVI:
 
     # ------------------------------------------------------------ helpers
     def _outer_supported(self, what):
-        """The outer objective, its second order and evaluate run for the
-        MLP families; make_lenet runs the inner loop only."""
+        """The second-order trainers need psvi_hvp, which the MLP families have;
+        make_lenet runs the inner loop, psvi_elbo and evaluate only."""
         if model_spec(self.model)[0] == "lenet":
-            raise NotImplementedError(f"{what} for make_lenet is not built on the HIP path "
-                                      "(its inner loop is)")
+            raise NotImplementedError(f"{what} for make_lenet needs the HVP through the conv "
+                                      "towers, which is not built on the HIP path")
 
     def coreset_weights(self):
         """N f(v): the per-pseudopoint NLL weights (detached, fp32)."""
@@ -262,9 +262,6 @@ class PSVI:
         assert self.mc_samples is None or self.mc_samples > 1  # psvi_classes.py:449
         model = self.model if model is None else model
         fam, layers, prior_sd, S = model_spec(model)
-        if fam == "lenet":
-            raise NotImplementedError("psvi_elbo for make_lenet is not built on the HIP path "
-                                      "(its inner loop is)")
         if S < 2:
             raise ValueError("psvi_elbo needs mc_samples > 1 (psvi_classes.py:449)")
         Mu = int(self.u.shape[0])
@@ -356,7 +353,6 @@ class PSVI:
         importance weights, normalised ESS, v-entropy), one psvi_evaluate per
         test batch (fresh weights per batch; entropy / ESS from the last one,
         as the reference).  ``eps``: optional list of draws, one per batch."""
-        self._outer_supported("evaluate")
         assert self.mc_samples is None or self.mc_samples > 1
         it = iter(eps) if eps is not None else None
         correct = nll = last = None

@@ -193,7 +193,7 @@ class InnerLoopPlan:
         device tensors: loss (float64, 1), and as requested grad (P), grad_u
         (n_pseudo, D), grad_w (n_pseudo), samples (S, 4: pseudo, data, nkl,
         weight; float64)."""
-        D = self.layers[0][0]
+        D = self.in_features
         n_pseudo = int(n_pseudo)
         _need(x_all, "x_all", self.M * D)
         _need(z_all, "z_all", self.M, torch.int32)
@@ -225,7 +225,7 @@ class InnerLoopPlan:
         plan's M rows (psvi_evaluate).  Returns (stats, probs): stats a float64
         device tensor [entropy of W, normalised ESS, correct, summed NLL];
         probs ([M - n_pseudo, C]) when requested."""
-        D, C = self.layers[0][0], self.layers[-1][1]
+        D, C = self.in_features, self.layers[-1][1]
         _need(x_all, "x_all", self.M * D)
         _need(z_all, "z_all", self.M, torch.int32)
         _need(w_all, "w_all", self.M)

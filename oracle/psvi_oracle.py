@@ -358,6 +358,9 @@ def _net_rows_backward(coef, probs_minus_onehot, hs, acts, Ws):
 
 
 def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
+    if family == "lenet":
+        return lenet_outer_elbo_grad(params, np.asarray(X).reshape(-1, 1, 28, 28), z, w,
+                                     n_pseudo, eps, S, prior_sd)
     """Negative PSVI-ELBO (PSVI.psvi_elbo, psvi/inference/psvi_classes.py:445-486)
     and its first-order gradient.
 
@@ -775,6 +778,9 @@ def evaluate_batch(family, layers, params, X, z, w_pseudo, n_pseudo, eps, S, cor
     lw_s = +sum_m w_m NLL_sm + sampled_nkl_s.  Returns (correct, summed NLL,
     entropy of W, normalised ESS, probs (Nt, C)); the NLL is
     -Categorical(probs).log_prob(yt) with torch's clamp to [eps, 1 - eps]."""
+    if family == "lenet":
+        return lenet_evaluate_batch(params, np.asarray(X).reshape(-1, 1, 28, 28), z, w_pseudo,
+                                    n_pseudo, eps, S, correction, prior_sd, clamp_eps)
     params = np.asarray(params, np.float64)
     eps = np.asarray(eps, np.float64)
     X = np.asarray(X, np.float64)
@@ -909,25 +915,11 @@ def lenet_forward(Xl, u, S):
     return hs[-1], cache
 
 
-def lenet_elbo_grad(params, u, z, w, eps, S, prior_sd=1.0):
-    """Negative inner ELBO (psvi_classes.py:488-511) of a make_lenet model and
-    its gradient w.r.t. the flat parameter vector (parameters_to_vector order:
-    per layer weight, bias, _weight_sd, _bias_sd)."""
-    params = np.asarray(params, np.float64)
-    s0 = float(prior_sd)
-    Xl = lenet_sample(params, eps, S)
-    logits, c = lenet_forward(Xl, u, S)
-    M = logits.shape[1]
-    w = np.asarray(w, np.float64)
-    zi = np.asarray(z).astype(np.int64)
-    mx = logits.max(-1, keepdims=True)
-    e = np.exp(logits - mx)
-    lse = mx[..., 0] + np.log(e.sum(-1))
-    nll = lse - logits[:, np.arange(M), zi]
-    data = float((nll @ w).sum())
-    P = e / e.sum(-1, keepdims=True)
-    P[:, np.arange(M), zi] -= 1.0
-    d = P * w[None, :, None]                                      # d logits
+def _lenet_backward(c, d, S, M, want_dx=False):
+    """Backward of the LeNet forward (cache c) from d logits (S, M, 10): per-layer
+    per-sample weight gradients G[l] (S, n_l) in parameter order (the last
+    layer's too), and, with want_dx, d input (S, M, 784) through the conv1
+    transpose."""
     hs, Wf = c["hs"], c["Wf"]
     G = [None] * 5
     for l in (2, 1, 0):
@@ -948,22 +940,107 @@ def lenet_elbo_grad(params, u, z, w, eps, S, prior_sd=1.0):
     x0p = np.pad(c["x0"], [(0, 0)] * 3 + [(2, 2)] * 2)
     dW1 = np.einsum("smohw,smchwij->socij", da1, _windows(x0p, 5), optimize=True)
     G[0] = np.concatenate([dW1.reshape(S, -1), da1.sum((1, 3, 4))], 1)
-    G[4] = G[4].sum(0, keepdims=True)                             # shared sample
-    grad = np.zeros_like(params)
+    dx = None
+    if want_dx:
+        da1p = np.pad(da1, [(0, 0)] * 3 + [(2, 2)] * 2)
+        dx = np.einsum("smchwij,scij->smhw", _windows(da1p, 5), c["W1"][:, :, 0, ::-1, ::-1],
+                       optimize=True).reshape(S, M, 784)
+    return G, dx
+
+
+def _lenet_param_grad(Xl, G, s0, kl_layers=True, sck=0.0):
+    """d / d (mu, rho) from per-sample weight gradients; the VILinear layers
+    add the analytic KL gradient (kl_layers) and/or the explicit sum_s ck_s /
+    sigma of the sampled KL (sck).  Returns (grad, kl)."""
+    P = sum(2 * (nw + nb) for nw, nb, _, _ in LENET_LAYERS)
+    grad = np.zeros(P)
     kl = 0.0
     for (nw, nb, bat, has_kl), x, g in zip(LENET_LAYERS, Xl, G):
         po, n, mu, rho = x["po"], x["n"], x["mu"], x["rho"]
+        if not bat:
+            g = g.sum(0, keepdims=True)                           # shared sample
         sp = softplus(rho)
         gmu = g.sum(0)
         grho = (g * x["E"]).sum(0)
-        if has_kl:
+        if has_kl and kl_layers:
             vr = (sp / s0) ** 2
             kl += float((0.5 * (vr + (mu / s0) ** 2 - 1.0 - np.log(vr))).sum())
             gmu = gmu + mu / s0 ** 2
             grho = grho + sp / s0 ** 2 - 1.0 / sp
+        if has_kl and sck:
+            grho = grho + sck / sp
         grad[po:po + n] = gmu
         grad[po + n:po + 2 * n] = grho * sigmoid(rho)
+    return grad, kl
+
+
+def lenet_elbo_grad(params, u, z, w, eps, S, prior_sd=1.0):
+    """Negative inner ELBO (psvi_classes.py:488-511) of a make_lenet model and
+    its gradient w.r.t. the flat parameter vector (parameters_to_vector order:
+    per layer weight, bias, _weight_sd, _bias_sd)."""
+    params = np.asarray(params, np.float64)
+    s0 = float(prior_sd)
+    Xl = lenet_sample(params, eps, S)
+    logits, c = lenet_forward(Xl, u, S)
+    M = logits.shape[1]
+    w = np.asarray(w, np.float64)
+    zi = np.asarray(z).astype(np.int64)
+    mx = logits.max(-1, keepdims=True)
+    e = np.exp(logits - mx)
+    lse = mx[..., 0] + np.log(e.sum(-1))
+    nll = lse - logits[:, np.arange(M), zi]
+    data = float((nll @ w).sum())
+    P = e / e.sum(-1, keepdims=True)
+    P[:, np.arange(M), zi] -= 1.0
+    G, _ = _lenet_backward(c, P * w[None, :, None], S, M)
+    grad, kl = _lenet_param_grad(Xl, G, s0)
     return data + kl, grad
+
+
+def lenet_outer_elbo_grad(params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
+    """PSVI.psvi_elbo (psvi_classes.py:445-486) of a make_lenet model on rows
+    X = cat(u, xbatch) (R, 1, 28, 28): sampled_nkl over the VILinear layers
+    only (the last one's single shared sample enters every s), W = softmax_s(lw),
+    loss = sum_s W_s (data_s - pseudo_s) - mean_s lw_s.  w: per-row weights
+    (N f(v) for the pseudo rows, N / Nx for the data rows).  Returns
+    (loss, d params, d u (n_pseudo, 784), d w (n_pseudo))."""
+    params = np.asarray(params, np.float64)
+    s0 = float(prior_sd)
+    Xl = lenet_sample(params, eps, S)
+    logits, c = lenet_forward(Xl, X, S)
+    R = logits.shape[1]
+    w = np.asarray(w, np.float64)
+    zi = np.asarray(z).astype(np.int64)
+    mx = logits.max(-1, keepdims=True)
+    e = np.exp(logits - mx)
+    lse = mx[..., 0] + np.log(e.sum(-1))
+    nll = lse - logits[:, np.arange(R), zi]
+    Mu = int(n_pseudo)
+    pseudo = nll[:, :Mu] @ w[:Mu]
+    data = nll[:, Mu:] @ w[Mu:]
+    nkl = np.zeros(S)
+    for x in Xl[2:]:
+        n = x["n"]
+        nkl = nkl + ((-(x["X"] ** 2).sum(1) / (2 * s0 ** 2) - n * np.log(s0)
+                      + 0.5 * (x["E"] ** 2).sum(1) + np.log(softplus(x["rho"])).sum()))
+    lw = -pseudo + nkl
+    Wt = np.exp(lw - lw.max())
+    Wt /= Wt.sum()
+    a = data - pseudo
+    abar = float((Wt * a).sum())
+    loss = abar - lw.mean()
+    ck = Wt * (a - abar) - 1.0 / S
+    cp = -Wt - ck
+    coef = np.where(np.arange(R)[None, :] < Mu, cp[:, None], Wt[:, None]) * w[None, :]
+    Pm = e / e.sum(-1, keepdims=True)
+    Pm[:, np.arange(R), zi] -= 1.0
+    G, dx = _lenet_backward(c, Pm * coef[..., None], S, R, want_dx=True)
+    for l in (2, 3, 4):                   # pathwise sampled-KL: -ck_s x_s / s0^2
+        G[l] = G[l] - ck[:, None] * np.broadcast_to(Xl[l]["X"], (S, Xl[l]["n"])) / s0 ** 2
+    grad, _ = _lenet_param_grad(Xl, G, s0, kl_layers=False, sck=float(ck.sum()))
+    gu = dx[:, :Mu].sum(0)
+    gw = cp @ nll[:, :Mu]
+    return float(loss), grad, gu, gw
 
 
 def lenet_inner_loop(params0, u, z, w, eps_steps, S, lr, adam_kind, prior_sd=1.0, t0=1):
@@ -1021,3 +1098,34 @@ def mfvi_run(family, layers, params0, x, y, xt, yt, draws, S, iters, log_every, 
             nlls.append(float(-ls[np.arange(len(yi)), yi].mean()))
     assert o == len(draws), (o, len(draws))
     return np.array(elbos), np.array(accs), np.array(nlls), p
+
+
+def lenet_evaluate_batch(params, X, z, w_pseudo, n_pseudo, eps, S, correction=True,
+                         prior_sd=1.0, clamp_eps=np.finfo(np.float64).eps):
+    """evaluate_batch for make_lenet: sampled_nkl over the VILinear layers only."""
+    params = np.asarray(params, np.float64)
+    s0 = float(prior_sd)
+    Xl = lenet_sample(params, eps, S)
+    logits, _ = lenet_forward(Xl, X, S)
+    nkl = np.zeros(S)
+    for x in Xl[2:]:
+        nkl = nkl + ((-(x["X"] ** 2).sum(1) / (2 * s0 ** 2) - x["n"] * np.log(s0)
+                      + 0.5 * (x["E"] ** 2).sum(1) + np.log(softplus(x["rho"])).sum()))
+    R = logits.shape[1]
+    mx = logits.max(-1, keepdims=True)
+    lse = (mx + np.log(np.exp(logits - mx).sum(-1, keepdims=True)))[..., 0]
+    zi = np.asarray(z).astype(np.int64)
+    nll = lse - logits[:, np.arange(R), zi]
+    Mu = int(n_pseudo)
+    lw = nll[:, :Mu] @ np.asarray(w_pseudo, np.float64)[:Mu] + nkl
+    W = np.exp(lw - lw.max())
+    W /= W.sum()
+    p = np.exp(logits[:, Mu:] - lse[:, Mu:, None])
+    probs = np.einsum("s,snc->nc", W, p) if correction else p.mean(0)
+    yt = zi[Mu:]
+    correct = float((probs.argmax(-1) == yt).sum())
+    pn = probs / probs.sum(-1, keepdims=True)
+    q = np.clip(pn[np.arange(len(yt)), yt], clamp_eps, 1 - clamp_eps)
+    ent = float(-(W[W > 0] * np.log(W[W > 0])).sum())
+    ness = float(W.sum() ** 2 / (W ** 2).sum() / S)
+    return correct, float(-np.log(q).sum()), ent, ness, probs

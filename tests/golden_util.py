@@ -26,7 +26,16 @@ def load_fixture(name):
 
 
 def family_of(cfg):
-    return "meanfield" if cfg["family"] == "mf" else "fullcov"
+    return {"mf": "meanfield", "mvn": "fullcov", "lenet": "lenet"}[cfg["family"]]
+
+
+LENET_PLAN_LAYERS = [(25, 6), (150, 16), (400, 120), (120, 84), (84, 10)]
+
+
+def plan_layers(cfg):
+    """The InnerLoopPlan layer table of a fixture (LeNet fixtures list only
+    their VILinear layers in cfg["layers"])."""
+    return LENET_PLAN_LAYERS if cfg["family"] == "lenet" else cfg["layers"]
 
 
 def adam_kind(cfg):

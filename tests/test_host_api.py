@@ -13,8 +13,14 @@ from golden_util import family_of, fixture_names, load_fixture
 
 def build_model(cfg, params0):
     """The reference module stack a fixture was generated from, at params0."""
-    from psvi.models import VILinear, VILinearMultivariateNormal
+    from psvi.models import VILinear, VILinearMultivariateNormal, make_lenet
 
+    if cfg["family"] == "lenet":
+        net = make_lenet(mc_samples=cfg["S"])
+        with torch.no_grad():
+            nn.utils.vector_to_parameters(torch.tensor(params0, dtype=torch.float32),
+                                          net.parameters())
+        return net
     cls = VILinear if family_of(cfg) == "meanfield" else VILinearMultivariateNormal
     mods = []
     for i, (a, b) in enumerate(cfg["layers"]):

@@ -72,3 +72,25 @@ def test_run_psvi_like_flow_psvi(trainer, arch, cls):
     assert res["csizes"] == [10] * n_log
     assert res["grid_preds"][0].shape == (2, 250 * 250)
     assert np.asarray(res["us"][0]).shape == (10, 2)
+
+
+@pytest.mark.parametrize("trainer", ["joint", "alternating"])
+def test_run_psvi_lenet_first_order_trainers(trainer):
+    """make_lenet through run_psvi on an MNIST-shaped synthetic set with the
+    first-order trainers (psvi_elbo + evaluate on the LeNet kernels); the
+    second-order ones refuse LeNet (no HVP through the conv towers)."""
+    import psvi.inference as I
+    from psvi.experiments import make_mnist_shaped
+
+    x, y, xt, yt = make_mnist_shaped(n_train=256, n_test=64, seed=1)
+    tr, te = _DS(x, y), _DS(xt, yt)
+    kw = flow_kwargs(trainer=trainer, architecture="lenet", logistic_regression=False,
+                     D=28, N=256, x=None, y=None, xt=None, yt=None, train_dataset=tr,
+                     test_dataset=te, nc=10, num_pseudo=10, mc_samples=3, data_minibatch=32,
+                     log_pseudodata=False, init_sd=0.05, dnm="mnist_shaped")
+    torch.manual_seed(0)
+    res = I.PSVILearnV(**kw).run_psvi(**kw)
+    assert len(res["accs"]) == 2 and all(math.isfinite(x) for x in res["nlls"])
+    with pytest.raises(NotImplementedError, match="HVP"):
+        kw2 = dict(kw, trainer="hyper")
+        I.PSVILearnV(**kw2).run_psvi(**kw2)

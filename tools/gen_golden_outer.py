@@ -76,11 +76,12 @@ def _child():
                 if isinstance(m, (VILinear, VILinearMultivariateNormal))]
 
     def run(name, family, model, cls, M, Nx, D, C, S, N, seed, v_scale=0.0, alpha=None,
-            note=""):
+            note="", shape=None):
         torch.manual_seed(seed)
-        u = torch.randn(M, D, generator=gen).float().double().requires_grad_(True)
+        dims = shape or (D,)
+        u = torch.randn(M, *dims, generator=gen).float().double().requires_grad_(True)
         z = torch.tensor([float(i % C) for i in range(M)])
-        xb = torch.randn(Nx, D, generator=gen).float().double()
+        xb = torch.randn(Nx, *dims, generator=gen).float().double()
         yb = torch.randint(0, C, (Nx,), generator=gen).double()
         v = (v_scale * torch.randn(M, generator=gen)).float().double().requires_grad_(True)
         obj = cls.__new__(cls)
@@ -168,11 +169,13 @@ def _child():
         seed=6, v_scale=0.3, note="logistic_regression_fullcov")
 
     # evaluate (psvi_classes.py:1031-1108): one test batch, correction on and off
-    def run_eval(name, family, model, cls, M, Nt, D, C, S, N, seed, v_scale=0.0, alpha=None):
+    def run_eval(name, family, model, cls, M, Nt, D, C, S, N, seed, v_scale=0.0, alpha=None,
+                 shape=None):
         torch.manual_seed(seed)
-        u = torch.randn(M, D, generator=gen).float().double()
+        dims = shape or (D,)
+        u = torch.randn(M, *dims, generator=gen).float().double()
         z = torch.tensor([float(i % C) for i in range(M)])
-        xt = torch.randn(Nt, D, generator=gen).float().double()
+        xt = torch.randn(Nt, *dims, generator=gen).float().double()
         yt = torch.randint(0, C, (Nt,), generator=gen).double()
         v = (v_scale * torch.randn(M, generator=gen)).float().double()
         obj = cls.__new__(cls)
@@ -227,6 +230,26 @@ def _child():
         perturb(model, 0.5, -3.0, -1.0, 0.02)
         run_eval("e4_logreg_fullcov", "mvn", model, PSVILearnV, M=10, Nt=30, D=2, C=2, S=4,
                  N=800, seed=44, v_scale=0.3)
+
+    # LeNet (make_lenet, neural_net.py:334-359): sampled_nkl over VILinear only,
+    # the last layer one shared sample; MNIST-shaped rows
+    from psvi.models.neural_net import make_lenet
+
+    model = make_lenet(mc_samples=3, init_sd=0.05)
+    perturb(model, 0.15, -4.0, -2.0, 0.0)
+    run("o7_lenet", "lenet", model, PSVILearnV, M=4, Nx=5, D=784, C=10, S=3, N=60000, seed=7,
+        v_scale=0.3, note="lenet, PSVILearnV", shape=(1, 28, 28))
+    model = make_lenet(mc_samples=4, init_sd=0.05)
+    perturb(model, 0.2, -3.5, -2.0, 0.0)
+    run("o8_lenet_av", "lenet", model, PSVIAV, M=3, Nx=4, D=784, C=10, S=4, N=60000, seed=8,
+        v_scale=0.3, alpha=0.2, note="lenet, PSVIAV", shape=(1, 28, 28))
+    with torch.no_grad():
+        # mild weights: test probabilities stay above fp32's clamp (1.2e-7), which
+        # the float64 reference run would not apply
+        model = make_lenet(mc_samples=4, init_sd=0.05)
+        perturb(model, 0.03, -4.0, -2.0, 0.0)
+        run_eval("e5_lenet", "lenet", model, PSVILearnV, M=4, Nt=12, D=784, C=10, S=4,
+                 N=60000, seed=45, v_scale=0.3, shape=(1, 28, 28))
 
 
 def main():
