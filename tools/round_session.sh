@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 R=${ROUND:-r01}
-STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
+STEPS=${STEPS:-tests,smoke,bench,prof,lprof,pmc}
 if [[ $STEPS == *tests* ]]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; ok $rc || exit $rc
@@ -24,6 +24,10 @@ BCMD="python3 bench.py --no-cpu-baseline --no-trainers --no-lenet --steps 200 --
 if [[ $STEPS == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${R} -o bench -- $BCMD > gpurun_out/prof_${R}.log 2>&1; rc=$?
   echo "prof rc=$rc"; ok $rc || exit $rc
+fi
+if [[ $STEPS == *lprof* ]]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lprof_${R} -o lenet -- python3 tools/lenet_probe.py --T 5 --reps 1 > gpurun_out/lprof_${R}.log 2>&1; rc=$?
+  echo "lenet prof rc=$rc"; ok $rc || exit $rc
 fi
 if [[ $STEPS == *pmc* ]]; then
   CMD="python3 bench.py --no-cpu-baseline --no-trainers --no-lenet --steps 50 --warmup 5" \
