@@ -313,7 +313,8 @@ def run_inner_loop(family, layers, params0, u, z, w, eps_steps, S, lr, adam_kind
     """T inner steps (one per eps_steps row): returns (elbos, grads, params, m, v).
     nested trainer: fresh higher-Adam state at t=1 (psvi_classes.py:549-555);
     hyper trainer: hypergrad step_cnt from 1 (psvi_classes.py:622-647)."""
-    f = mf_elbo_grad if family == "mf" else mvn_elbo_grad
+    f = {"mf": mf_elbo_grad, "mvn": mvn_elbo_grad,
+         "lenet": lambda _l, p, u, z, w, e, S, sd: lenet_elbo_grad(p, u, z, w, e, S, sd)}[family]
     p = np.asarray(params0, dtype=np.float64).copy()
     m = np.zeros_like(p)
     v = np.zeros_like(p)
@@ -359,8 +360,10 @@ def _net_rows_backward(coef, probs_minus_onehot, hs, acts, Ws):
 
 def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
     if family == "lenet":
-        return lenet_outer_elbo_grad(params, np.asarray(X).reshape(-1, 1, 28, 28), z, w,
-                                     n_pseudo, eps, S, prior_sd)
+        X = np.asarray(X)
+        loss, g, gu, gw = lenet_outer_elbo_grad(params, X.reshape(-1, 1, 28, 28), z, w,
+                                                n_pseudo, eps, S, prior_sd)
+        return loss, g, gu.reshape((int(n_pseudo),) + X.shape[1:]), gw
     """Negative PSVI-ELBO (PSVI.psvi_elbo, psvi/inference/psvi_classes.py:445-486)
     and its first-order gradient.
 
@@ -490,6 +493,11 @@ def _split(layers, Xl):
 
 
 def inner_hvp(family, layers, params, u, z, w, eps, S, vec, prior_sd=1.0):
+    if family == "lenet":
+        u = np.asarray(u)
+        val, g, hv, du, dw = lenet_inner_hvp(params, u.reshape(-1, 1, 28, 28), z, w, eps, S, vec,
+                                             prior_sd)
+        return val, g, hv, du.reshape(u.shape), dw
     """Hessian-vector product of the negative inner ELBO (psvi_classes.py:488-511)
     at fixed eps, H vec, and the mixed products d/du (vec . grad) and
     d/dw (vec . grad) -- what hypergrad's CG_normaleq takes from autograd
@@ -1129,3 +1137,111 @@ def lenet_evaluate_batch(params, X, z, w_pseudo, n_pseudo, eps, S, correction=Tr
     ent = float(-(W[W > 0] * np.log(W[W > 0])).sum())
     ness = float(W.sum() ** 2 / (W ** 2).sum() / S)
     return correct, float(-np.log(q).sum()), ent, ness, probs
+
+
+def _route(a, arg):
+    """Gather a (S,M,C,H,W) at the pool routes (0 where relu zeroes the window)."""
+    S, M, C, H, W = a.shape
+    win = a.reshape(S, M, C, H // 2, 2, W // 2, 2).transpose(0, 1, 2, 3, 5, 4, 6)
+    win = win.reshape(S, M, C, H // 2, W // 2, 4)
+    out = np.take_along_axis(win, np.maximum(arg, 0)[..., None], -1)[..., 0]
+    return np.where(arg >= 0, out, 0.0)
+
+
+def lenet_inner_hvp(params, u, z, w, eps, S, vec, prior_sd=1.0):
+    """Hessian-vector product of the LeNet negative inner ELBO at fixed eps and
+    the mixed products d/du, d/dw of vec . grad (inner_hvp's contract):
+    forward-over-reverse with the relu masks and pool routes held constant.
+    Returns (value, grad, Hv, d_u (M, 784), d_w (M,))."""
+    params = np.asarray(params, np.float64)
+    vec = np.asarray(vec, np.float64)
+    s0 = float(prior_sd)
+    val, grad = lenet_elbo_grad(params, u, z, w, eps, S, prior_sd)
+    Xl = lenet_sample(params, eps, S)
+    logits, c = lenet_forward(Xl, u, S)
+    M = logits.shape[1]
+    w = np.asarray(w, np.float64)
+    zi = np.asarray(z).astype(np.int64)
+    # tangent weights W_dot = v_mu + sigmoid(rho) v_rho eps
+    Td = []
+    for x in Xl:
+        po, n = x["po"], x["n"]
+        Td.append(vec[po:po + n][None] + (sigmoid(x["rho"]) * vec[po + n:po + 2 * n])[None] * x["E"])
+    W1d, b1d = Td[0][:, :150].reshape(-1, 6, 1, 5, 5), Td[0][:, 150:]
+    W2d, b2d = Td[1][:, :2400].reshape(-1, 16, 6, 5, 5), Td[1][:, 2400:]
+    # primal activations (recomputed with pre-activations) and tangent forward
+    W1, W2 = c["W1"], c["W2"]
+    b1, b2 = Xl[0]["X"][:, 150:], Xl[1]["X"][:, 2400:]
+    x0 = c["x0"]
+    a1d = _conv(x0, W1d, b1d, 2)
+    p1d = _route(a1d, c["g1"])
+    a2d = _conv(p1d, W2, np.zeros_like(b2), 0) + _conv(c["p1"], W2d, b2d, 0)
+    xd = _route(a2d, c["g2"]).reshape(S, M, 400)
+    hs, Wf = c["hs"], c["Wf"]
+    Wfd = [Td[2][:, :48000].reshape(S, 120, 400), Td[3][:, :10080].reshape(S, 84, 120),
+           np.broadcast_to(Td[4][:, :840].reshape(1, 10, 84), (S, 10, 84))]
+    bfd = [Td[2][:, 48000:], Td[3][:, 10080:], np.broadcast_to(Td[4][:, 840:], (S, 10))]
+    hds = [xd]
+    for l in range(3):
+        ad = (np.einsum("smi,soi->smo", hds[-1], Wf[l]) + np.einsum("smi,soi->smo", hs[l], Wfd[l])
+              + bfd[l][:, None, :])
+        hds.append(ad * (hs[l + 1] > 0) if l < 2 else ad)
+    ld = hds[-1]
+    mx = logits.max(-1, keepdims=True)
+    e = np.exp(logits - mx)
+    P = e / e.sum(-1, keepdims=True)
+    Pm = P.copy()
+    Pm[:, np.arange(M), zi] -= 1.0
+    nlld = (Pm * ld).sum(-1)                                     # tangent of NLL_sm
+    d = Pm * w[None, :, None]
+    dd = w[None, :, None] * (P * ld - P * (P * ld).sum(-1, keepdims=True))
+    Gd = [None] * 5
+    for l in (2, 1, 0):
+        dW = np.einsum("smo,smi->soi", dd, hs[l]) + np.einsum("smo,smi->soi", d, hds[l])
+        Gd[2 + l] = np.concatenate([dW.reshape(S, -1), dd.sum(1)], 1)
+        dd_new = np.einsum("smo,soi->smi", dd, Wf[l]) + np.einsum("smo,soi->smi", d, Wfd[l])
+        d = np.einsum("smo,soi->smi", d, Wf[l])
+        if l > 0:
+            dd_new = dd_new * (hs[l] > 0)
+            d = d * (hs[l] > 0)
+        dd = dd_new
+    da2 = _unpool(d.reshape(S, M, 16, 5, 5), c["g2"], 10, 10)
+    da2d = _unpool(dd.reshape(S, M, 16, 5, 5), c["g2"], 10, 10)
+    dW2d = (np.einsum("smohw,smchwij->socij", da2d, _windows(c["p1"], 5), optimize=True)
+            + np.einsum("smohw,smchwij->socij", da2, _windows(p1d, 5), optimize=True))
+    Gd[1] = np.concatenate([dW2d.reshape(S, -1), da2d.sum((1, 3, 4))], 1)
+    pad4 = [(0, 0)] * 3 + [(4, 4)] * 2
+    dp1 = np.einsum("smohwij,socij->smchw", _windows(np.pad(da2, pad4), 5), W2[..., ::-1, ::-1],
+                    optimize=True)
+    dp1d = (np.einsum("smohwij,socij->smchw", _windows(np.pad(da2d, pad4), 5),
+                      W2[..., ::-1, ::-1], optimize=True)
+            + np.einsum("smohwij,socij->smchw", _windows(np.pad(da2, pad4), 5),
+                        W2d[..., ::-1, ::-1], optimize=True))
+    da1 = _unpool(dp1, c["g1"], 28, 28)
+    da1d = _unpool(dp1d, c["g1"], 28, 28)
+    pad2 = [(0, 0)] * 3 + [(2, 2)] * 2
+    dW1d = np.einsum("smohw,smchwij->socij", da1d, _windows(np.pad(x0, pad2), 5), optimize=True)
+    Gd[0] = np.concatenate([dW1d.reshape(S, -1), da1d.sum((1, 3, 4))], 1)
+    dud = (np.einsum("smchwij,scij->smhw", _windows(np.pad(da1d, pad2), 5),
+                     W1[:, :, 0, ::-1, ::-1], optimize=True)
+           + np.einsum("smchwij,scij->smhw", _windows(np.pad(da1, pad2), 5),
+                       W1d[:, :, 0, ::-1, ::-1], optimize=True))
+    # primal per-sample G (for the softplus curvature) from the backward helper
+    Pw = Pm * w[None, :, None]
+    G, _ = _lenet_backward(c, Pw, S, M)
+    hv = np.zeros_like(params)
+    for (nw, nb, bat, has_kl), x, g, gd in zip(LENET_LAYERS, Xl, G, Gd):
+        po, n, mu, rho = x["po"], x["n"], x["mu"], x["rho"]
+        if not bat:
+            g, gd = g.sum(0, keepdims=True), gd.sum(0, keepdims=True)
+        sp, sg = softplus(rho), sigmoid(rho)
+        vm, vr = vec[po:po + n], vec[po + n:po + 2 * n]
+        E = x["E"]
+        hm = gd.sum(0)
+        hr = (gd * E).sum(0) * sg + (g * E).sum(0) * sg * (1 - sg) * vr
+        if has_kl:
+            hm = hm + vm / s0 ** 2
+            hr = hr + ((1 / sp ** 2 + 1 / s0 ** 2) * sg * sg + (sp / s0 ** 2 - 1 / sp) * sg * (1 - sg)) * vr
+        hv[po:po + n] = hm
+        hv[po + n:po + 2 * n] = hr
+    return val, grad, hv, dud.sum(0).reshape(M, 784), nlld.sum(0)

@@ -88,9 +88,9 @@ def _child():
         return [[m.in_features, m.out_features] for m in model.modules()
                 if isinstance(m, (VILinear, VILinearMultivariateNormal))]
 
-    def make_obj(model, M, D, C, S, N, uv=None):
+    def make_obj(model, M, D, C, S, N, uv=None, shape=None):
         if uv is None:
-            u = torch.randn(M, D, generator=gen).float().double().requires_grad_(True)
+            u = torch.randn(M, *(shape or (D,)), generator=gen).float().double().requires_grad_(True)
             v = (0.2 * torch.randn(M, generator=gen)).float().double().requires_grad_(True)
         else:
             u, v = (t.detach().clone().requires_grad_(True) for t in uv)
@@ -111,9 +111,9 @@ def _child():
         c.update(kw)
         return c
 
-    def run_hvp(name, family, model, M, D, C, S, N, seed, note=""):
+    def run_hvp(name, family, model, M, D, C, S, N, seed, note="", shape=None):
         torch.manual_seed(seed)
-        obj = make_obj(model, M, D, C, S, N)
+        obj = make_obj(model, M, D, C, S, N, shape=shape)
         fmodel = monkeypatch(model, copy_initial_weights=True)
         params = [p.detach().clone().requires_grad_(True) for p in fmodel.parameters()]
         p0 = torch.cat([p.detach().reshape(-1) for p in params])
@@ -138,15 +138,15 @@ def _child():
         print(f"wrote {name}: P={p0.numel()} elbo={float(loss):.6f}")
 
     def run_hyper_step(name, family, model, M, Nx, D, C, S, N, seed, T, K, note="",
-                       approx="CG_normaleq"):
+                       approx="CG_normaleq", shape=None):
         torch.manual_seed(seed)
-        obj = make_obj(model, M, D, C, S, N)
+        obj = make_obj(model, M, D, C, S, N, shape=shape)
         obj.inner_it = T
         lr0net, lr0u, lr0v = 1e-3, 1e-3, 1e-2
         obj.optim_net = torch.optim.Adam(list(model.parameters()), lr0net)
         obj.optim_u = torch.optim.Adam([obj.u], lr0u)
         obj.optim_v = torch.optim.Adam([obj.v], lr0v)
-        xb = torch.randn(Nx, D, generator=gen).float().double()
+        xb = torch.randn(Nx, *(shape or (D,)), generator=gen).float().double()
         yb = torch.randint(0, C, (Nx,), generator=gen).double()
         p0 = parameters_to_vector(model.parameters()).detach().clone()
         u0, v0 = obj.u.detach().clone(), obj.v.detach().clone()
@@ -316,6 +316,19 @@ def _child():
     perturb(model, 0.4, -3.0, -1.0, 0.0)
     run_hyper_step("y4_fn_deep_fp", "mf", model, M=13, Nx=9, D=5, C=3, S=6, N=500, seed=24,
                    T=3, K=4, approx="fixed_point")
+
+    # LeNet (make_lenet, C5's architecture): double backward through the conv
+    # towers, and one whole hyper_step (C5's trainer) with CG_normaleq
+    from psvi.models.neural_net import make_lenet
+
+    model = make_lenet(mc_samples=3, init_sd=0.05)
+    perturb(model, 0.15, -4.0, -2.0, 0.0)
+    run_hvp("h5_lenet", "lenet", model, M=4, D=784, C=10, S=3, N=60000, seed=15,
+            shape=(1, 28, 28))
+    model = make_lenet(mc_samples=2, init_sd=0.05)
+    perturb(model, 0.1, -4.0, -2.0, 0.0)
+    run_hyper_step("y5_lenet", "lenet", model, M=4, Nx=6, D=784, C=10, S=2, N=60000,
+                   seed=25, T=2, K=3, shape=(1, 28, 28))
 
 
 def main():
