@@ -480,6 +480,10 @@ static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
     const size_t S = p->d.S, M = p->d.M, D = p->lay[0].din, nt = p->n_tot;
     char* b = (char*)ws;
     HvpWs o{};
+    if (p->family == PSVI_FAMILY_LENET) {  // tangent scratch of launch_lenet_hvp
+        o.bytes = lenet_tan_ws(*p, nullptr).bytes;
+        return o;
+    }
     size_t off = align256(p->ws_bytes);
     auto take = [&](size_t bytes) {
         char* r = b ? b + off : nullptr;
@@ -935,12 +939,17 @@ int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* 
              const float* eps, const float* params, const float* vec, float* hv_out,
              float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
-    if (p->family == PSVI_FAMILY_LENET)
-        return fail(PSVI_EUNSUP, "LeNet plans have no HVP (its R-op through the conv towers is not built)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "psvi_hvp needs world == 1");
     if (!u || !z || !w || !eps || !params || !vec || !hv_out)
         return fail(PSVI_EINVAL, "null pointer");
+    if (p->family == PSVI_FAMILY_LENET) {
+        if (!ws || ws_bytes < lenet_tan_ws(*p, nullptr).bytes)
+            return fail(PSVI_ENOSPC, "workspace too small");
+        HIP_TRY(launch_lenet_hvp(*p, u, z, w, eps, params, vec, hv_out, du_out, dw_out, ws,
+                                 as_stream(stream)));
+        return 0;
+    }
     if (rop_rows(*p) == 0)
         return fail(PSVI_EUNSUP, "model too wide for the per-sample R-op kernel's LDS");
     const HvpWs o = hvp_ws(p, ws);

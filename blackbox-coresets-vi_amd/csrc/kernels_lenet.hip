@@ -417,8 +417,9 @@ __global__ __launch_bounds__(kThreads) void lenet_conv_reduce_kernel(int S_loc, 
 // ---------------------------------------------------------- head GEMMs
 // C[b](m, n) = sum_k A[b](m, k) B[b](k, n) with arbitrary element strides,
 // 64x64 tiles, k-steps of 16 through LDS, 4x4 outputs per thread (fp32 VALU:
-// the head is 1/7 of the step's flops).  Epilogue flags: 1 add bias[b][n],
-// 2 relu, 4 multiply by (mask[b](m, n) > 0) (relu's backward).
+// the head is 1/7 of the step's flops).  Epilogue flags, in order: 8 add the
+// existing C (a second product of a tangent), 1 add bias[b][n], 2 relu, 4
+// multiply by (mask[b](m, n) > 0) (relu's backward).
 struct GemmArgs {
     int M, N, K;
     const float* A; int64_t sAb; int sAm, sAk;
@@ -480,6 +481,7 @@ __global__ __launch_bounds__(kThreads) void lenet_gemm_kernel(GemmArgs g) {
             const int n = n0 + tx * 4 + j;
             if (n >= g.N) continue;
             float v = acc[i][j];
+            if (g.epi & 8) v += C[(int64_t)m * g.sCm + n];  // accumulate onto C
             if (g.epi & 1) v += g.bias[b * g.sbias + n];
             if (g.epi & 2) v = fmaxf(v, 0.f);
             if (g.epi & 4) v = g.mask[b * g.sMb + (int64_t)m * g.sMm + n] > 0.f ? v : 0.f;
@@ -512,6 +514,7 @@ struct LossOuter {
     float* nll_rows;
     float* prob_rows;
     const float* rowcoef;
+    float* prob_all;  // mode 0, nullable: softmax of every row [S][M][10] (HVP)
 };
 
 __global__ __launch_bounds__(kThreads) void lenet_loss_kernel(int rows, int M,
@@ -565,11 +568,369 @@ __global__ __launch_bounds__(kThreads) void lenet_loss_kernel(int rows, int M,
         const float lse = mx + logf(se);
         contrib = wm * (lse - d[zc]);
         const float inv = 1.f / se;
+        if (o.prob_all)
+#pragma unroll
+            for (int c = 0; c < 10; ++c) o.prob_all[(int64_t)r * 10 + c] = l[c] * inv;
 #pragma unroll
         for (int c = 0; c < 10; ++c) d[c] = wm * (l[c] * inv - (c == zc ? 1.f : 0.f));
     }
     const float tot = block_sum(contrib, red);
     if (threadIdx.x == 0) atomicAdd(nll_out, (double)tot);
+}
+
+// ------------------------------------------------------ HVP (R-op) kernels
+// psvi_hvp for LeNet: forward-over-reverse at fixed eps with the relu masks
+// and pool routes of the primal pass held constant (oracle lenet_inner_hvp).
+
+// W_dot[s][j] = v_mu + sigmoid(rho) v_rho eps_(s, j)
+__global__ __launch_bounds__(kThreads) void lenet_tangent_kernel(SampleArgs a,
+                                                                 const float* __restrict__ params,
+                                                                 const float* __restrict__ vec,
+                                                                 const float* __restrict__ eps,
+                                                                 float* __restrict__ wdot) {
+    const int64_t total = (int64_t)a.S_loc * a.n_tot;
+    for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * kThreads) {
+        const int s = (int)(i / a.n_tot), j = (int)(i - (int64_t)s * a.n_tot);
+        const int l = lenet_layer(a, j);
+        const int idx = j - a.woff[l];
+        const int64_t pm = a.poff[l] + idx, pr = pm + a.n[l];
+        wdot[i] = vec[pm] + sigmoid_f(params[pr]) * vec[pr] *
+                                eps[lenet_eps_index(a, l, idx, a.s_off + s)];
+    }
+}
+
+struct TanArgs {
+    int M, n_tot, nchunk, chunk;
+    const float* u;
+    const float* wsamp;
+    const float* wdot;
+    const float* p1;
+    const int8_t* r1;
+    const int8_t* r2;
+    const float* dx2;    // primal d X2
+    const float* dx2d;   // tangent d X2
+    float* p1d;          // fwd out: tangent pooled conv1 [S][M][1176]
+    float* x2d;          // fwd out: tangent X2 [S][M][400]
+    float* part;         // bwd out: tangent conv weight gradients [S][nchunk][2572]
+    float* du;           // bwd out, nullable: [S][M][784] tangent of d u
+};
+
+// tangent forward of the conv towers: only the routed conv positions matter
+__global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_tan_kernel(TanArgs a) {
+    __shared__ float w2[2400], wd[kNConv];
+    __shared__ float in[32 * 32];
+    __shared__ float p1[kP1], p1d[kP1];
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    const float* wds = a.wdot + (int64_t)s * a.n_tot;
+    for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
+    for (int i = tid; i < kNConv; i += kConvThreads) wd[i] = wds[i];
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        const int64_t row = (int64_t)s * a.M + m;
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 1024; i += kConvThreads) {
+            const int y = (i >> 5) - 2, x = (i & 31) - 2;
+            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+        }
+        for (int i = tid; i < kP1; i += kConvThreads) p1[i] = a.p1[row * kP1 + i];
+        __syncthreads();
+        for (int o = tid; o < kP1; o += kConvThreads) {
+            const int r = a.r1[row * kP1 + o];
+            float v = 0.f;
+            if (r >= 0) {
+                const int c = o / 196, py = (o % 196) / 14, px = o % 14;
+                const int y = 2 * py + (r >> 1), x = 2 * px + (r & 1);
+                v = wd[150 + c];
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) v += wd[c * 25 + i * 5 + j] * in[(y + i) * 32 + x + j];
+            }
+            p1d[o] = v;
+            a.p1d[row * kP1 + o] = v;
+        }
+        __syncthreads();
+        for (int o = tid; o < kX2; o += kConvThreads) {
+            const int r = a.r2[row * kX2 + o];
+            float v = 0.f;
+            if (r >= 0) {
+                const int k = o / 25, py = (o % 25) / 5, px = o % 5;
+                const int y = 2 * py + (r >> 1), x = 2 * px + (r & 1);
+                v = wd[2556 + k];
+                for (int c = 0; c < 6; ++c) {
+                    const float* wk = w2 + k * 150 + c * 25;
+                    const float* wdk = wd + 156 + k * 150 + c * 25;
+                    const int base = c * 196 + y * 14 + x;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+#pragma unroll
+                        for (int j = 0; j < 5; ++j)
+                            v += wk[i * 5 + j] * p1d[base + i * 14 + j] +
+                                 wdk[i * 5 + j] * p1[base + i * 14 + j];
+                }
+            }
+            a.x2d[row * kX2 + o] = v;
+        }
+    }
+}
+
+// tangent of d logits and of each row's NLL:
+//   dd = w (P . l_dot - P (P . l_dot)),  nll_dot = (P - onehot) . l_dot
+__global__ __launch_bounds__(kThreads) void lenet_loss_tan_kernel(int rows, int M,
+                                                                  const int32_t* __restrict__ z,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ P,
+                                                                  float* __restrict__ LD,
+                                                                  float* __restrict__ nlld) {
+    const int r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= rows) return;
+    const int m = r % M;
+    const int zc = min(max(z[m], 0), 9);
+    const float* p = P + (int64_t)r * 10;
+    float* ld = LD + (int64_t)r * 10;
+    float pl = 0.f;
+#pragma unroll
+    for (int c = 0; c < 10; ++c) pl += p[c] * ld[c];
+    nlld[r] = pl - ld[zc];
+    const float wm = w[m];
+    float out[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) out[c] = wm * p[c] * (ld[c] - pl);
+#pragma unroll
+    for (int c = 0; c < 10; ++c) ld[c] = out[c];
+}
+
+// 2x2 block of a transposed 5x5 conv: acc[q] += sum_ij w[i][j] Q[4 - i + dy][4 - j + dx]
+// over a 6x6 patch at q (row stride ld) of a zero-bordered plane
+__device__ __forceinline__ void convT_block(const float* q, int ld, const float* wk,
+                                            float (&acc)[4]) {
+    float Q[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * ld + j];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const float wv = wk[i * 5 + j];
+            acc[0] += wv * Q[4 - i][4 - j];
+            acc[1] += wv * Q[4 - i][5 - j];
+            acc[2] += wv * Q[5 - i][4 - j];
+            acc[3] += wv * Q[5 - i][5 - j];
+        }
+}
+
+// tangent backward of the conv towers: G_dot for conv2 and conv1, and the
+// tangent of d u (the mixed product d/du) for every row.  One LDS plane
+// region serves the routed conv2 gradients (primal and tangent, 18x18 with a
+// 4-wide border) and then the routed conv1 gradients (32x32 with a 2-wide
+// border); it is re-zeroed per image.
+constexpr int kPlane = 2 * 6 * 1024;  // >= 2 * 16 * kDA * kDA
+__global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArgs a) {
+    __shared__ float w1[150], wd1[150], w2[2400], wd2[2400];
+    __shared__ float in[32 * 32];
+    __shared__ float p1[kP1], p1d[kP1];
+    __shared__ float g2[kX2], g2d[kX2];
+    __shared__ int off2[kX2];
+    __shared__ float g1[kP1], g1d[kP1];
+    __shared__ int off1[kP1];
+    __shared__ float plane[kPlane];
+    __shared__ float red[160];
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    const float* wds = a.wdot + (int64_t)s * a.n_tot;
+    for (int i = tid; i < 150; i += kConvThreads) { w1[i] = ws[i]; wd1[i] = wds[i]; }
+    for (int i = tid; i < 2400; i += kConvThreads) { w2[i] = ws[156 + i]; wd2[i] = wds[156 + i]; }
+    constexpr int kR2 = (2400 + kConvThreads - 1) / kConvThreads;
+    int kb[kR2], pb[kR2];
+#pragma unroll
+    for (int r = 0; r < kR2; ++r) {
+        const int e = min(tid + r * kConvThreads, 2399);
+        kb[r] = (e / 150) * 25;
+        pb[r] = ((e % 150) / 25) * 196 + ((e % 25) / 5) * 14 + e % 5;
+    }
+    float accw2[kR2];
+#pragma unroll
+    for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
+    const int half = tid / 160, e1 = tid % 160;
+    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * 32 + e1 % 5;
+    const int cb1 = (e1 >= 150 && e1 < 156) ? e1 - 150 : c1;
+    float acc1 = 0.f, accb2 = 0.f;
+    float* da2 = plane;
+    float* da2d = plane + 16 * kDA * kDA;
+    float* da1 = plane;
+    float* da1d = plane + 6 * 1024;
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        const int64_t row = (int64_t)s * a.M + m;
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 1024; i += kConvThreads) {
+            const int y = (i >> 5) - 2, x = (i & 31) - 2;
+            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+        }
+        for (int i = tid; i < kP1; i += kConvThreads) {
+            p1[i] = a.p1[row * kP1 + i];
+            p1d[i] = a.p1d[row * kP1 + i];
+        }
+        for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
+        __syncthreads();
+        for (int o = tid; o < kX2; o += kConvThreads) {
+            const int r = a.r2[row * kX2 + o];
+            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
+            const int rr = r >= 0 ? r : 0;
+            const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
+            const float g = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
+            const float gd = r >= 0 ? a.dx2d[row * kX2 + o] : 0.f;
+            g2[o] = g;
+            g2d[o] = gd;
+            off2[o] = y * 14 + x;
+            da2[k * kDA * kDA + (y + 4) * kDA + x + 4] = g;
+            da2d[k * kDA * kDA + (y + 4) * kDA + x + 4] = gd;
+        }
+        __syncthreads();
+        // G_dot conv2: sum_p g2_dot P1 + g2 P1_dot at the routed windows
+#pragma unroll
+        for (int r = 0; r < kR2; ++r) {
+            if (tid + r * kConvThreads < 2400) {
+                float acc = 0.f;
+#pragma unroll
+                for (int p = 0; p < 25; ++p) {
+                    const int q = pb[r] + off2[kb[r] + p];
+                    acc += g2d[kb[r] + p] * p1[q] + g2[kb[r] + p] * p1d[q];
+                }
+                accw2[r] += acc;
+            }
+        }
+        if (tid < 16) {
+            float acc = 0.f;
+            for (int p = 0; p < 25; ++p) acc += g2d[tid * 25 + p];
+            accb2 += acc;
+        }
+        // d P1 and its tangent (transposed conv2), routed through pool1 / relu
+        if (tid < 294) {
+            const int c = tid / 49, yy = 2 * ((tid % 49) / 7), xx = 2 * (tid % 7);
+            float acc[4] = {0.f, 0.f, 0.f, 0.f}, accd[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < 16; ++k) {
+                const int po = k * kDA * kDA + yy * kDA + xx;
+                convT_block(da2 + po, kDA, w2 + k * 150 + c * 25, acc);
+                convT_block(da2d + po, kDA, w2 + k * 150 + c * 25, accd);
+                convT_block(da2 + po, kDA, wd2 + k * 150 + c * 25, accd);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int yq = yy + (q >> 1), xq = xx + (q & 1);
+                const int o = c * 196 + yq * 14 + xq;
+                const int r = a.r1[row * kP1 + o];
+                const int rr = r >= 0 ? r : 0;
+                g1[o] = r >= 0 ? acc[q] : 0.f;
+                g1d[o] = r >= 0 ? accd[q] : 0.f;
+                off1[o] = (2 * yq + (rr >> 1)) * 32 + 2 * xq + (rr & 1);
+            }
+        }
+        __syncthreads();
+        // G_dot conv1 (the image is constant): sum_p g1_dot in[...]
+        if (e1 < 156) {
+            const int p0 = half * 98;
+            float acc = 0.f;
+            if (e1 < 150) {
+#pragma unroll 7
+                for (int p = p0; p < p0 + 98; ++p)
+                    acc += g1d[c1 * 196 + p] * in[off1[c1 * 196 + p] + o1];
+            } else {
+#pragma unroll 7
+                for (int p = p0; p < p0 + 98; ++p) acc += g1d[cb1 * 196 + p];
+            }
+            acc1 += acc;
+        }
+        if (a.du) {
+            for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
+            __syncthreads();
+            for (int o = tid; o < kP1; o += kConvThreads) {
+                const int q = (o / 196) * 1024 + off1[o] + 2 * 32 + 2;
+                da1[q] = g1[o];
+                da1d[q] = g1d[o];
+            }
+            __syncthreads();
+            if (tid < 196) {
+                const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
+                float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+                for (int c = 0; c < 6; ++c) {
+                    convT_block(da1d + c * 1024 + yy * 32 + xx, 32, w1 + c * 25, acc);
+                    convT_block(da1 + c * 1024 + yy * 32 + xx, 32, wd1 + c * 25, acc);
+                }
+                float* out = a.du + row * 784 + yy * 28 + xx;
+                out[0] = acc[0];
+                out[1] = acc[1];
+                out[28] = acc[2];
+                out[29] = acc[3];
+            }
+        }
+    }
+    __syncthreads();
+    if (half == 1) red[e1] = acc1;
+    __syncthreads();
+    float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
+    if (half == 0 && e1 < 156) out[e1] = acc1 + red[e1];
+    if (tid < 16) out[2556 + tid] = accb2;
+#pragma unroll
+    for (int r = 0; r < kR2; ++r) {
+        const int e = tid + r * kConvThreads;
+        if (e < 2400) out[156 + e] = accw2[r];
+    }
+}
+
+// H vec: sum_s G_dot (+ eps) through the reparameterisation, the softplus
+// curvature sum_s (G_s eps_s) sigmoid'(rho) v_rho, the KL Hessian on the
+// VILinear layers; then d_u = sum_s du_dot, d_w = sum_s nll_dot.
+__global__ __launch_bounds__(kThreads) void lenet_hvp_assemble_kernel(
+    SampleArgs a, const float* __restrict__ params, const float* __restrict__ vec,
+    const float* __restrict__ eps, const float* __restrict__ G, const float* __restrict__ Gd,
+    const float* __restrict__ dud, const float* __restrict__ nlld, float* __restrict__ hv,
+    float* __restrict__ d_u, float* __restrict__ d_w, int M, float inv_s0sq) {
+    const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    if (i < a.n_tot) {
+        const int j = (int)i;
+        const int l = lenet_layer(a, j);
+        const int idx = j - a.woff[l];
+        float gd = 0.f, gde = 0.f, ge = 0.f;
+        for (int s = 0; s < a.S_loc; ++s) {
+            const float e = eps[lenet_eps_index(a, l, idx, a.s_off + s)];
+            const float g = G[(int64_t)s * a.n_tot + j], gdv = Gd[(int64_t)s * a.n_tot + j];
+            ge = fmaf(g, e, ge);
+            gd += gdv;
+            gde = fmaf(gdv, e, gde);
+        }
+        const int64_t pm = a.poff[l] + idx, pr = pm + a.n[l];
+        const float r = params[pr], sp = softplus_f(r), sg = sigmoid_f(r);
+        const float vr = vec[pr];
+        float hm = gd, hr = gde * sg + ge * sg * (1.f - sg) * vr;
+        if (l >= 2) {  // KL on the VILinear layers
+            hm += vec[pm] * inv_s0sq;
+            hr += ((1.f / (sp * sp) + inv_s0sq) * sg * sg + (sp * inv_s0sq - 1.f / sp) * sg * (1.f - sg)) * vr;
+        }
+        hv[pm] = hm;
+        hv[pr] = hr;
+        return;
+    }
+    const int64_t j = i - a.n_tot;
+    if (d_u && j < (int64_t)M * 784) {
+        float g = 0.f;
+        for (int s = 0; s < a.S_loc; ++s) g += dud[(int64_t)s * M * 784 + j];
+        d_u[j] = g;
+        return;
+    }
+    const int64_t k = j - (d_u ? (int64_t)M * 784 : 0);
+    if (d_w && k >= 0 && k < M) {
+        float g = 0.f;
+        for (int s = 0; s < a.S_loc; ++s) g += nlld[(int64_t)s * M + k];
+        d_w[k] = g;
+    }
 }
 
 hipError_t gemm(const GemmArgs& g, int batch, hipStream_t st) {
@@ -654,8 +1015,9 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
         lo.mode = outer->mode;
         lo.n_pseudo = outer->n_pseudo;
         lo.nll_rows = outer->nll_rows;
-        lo.prob_rows = outer->prob_rows;
+        lo.prob_rows = outer->mode == 0 ? nullptr : outer->prob_rows;
         lo.rowcoef = outer->rowcoef;
+        lo.prob_all = outer->mode == 0 ? outer->prob_rows : nullptr;
     }
     const SampleArgs sa = sample_args(p);
     const int S = sa.S_loc, M = p.d.M, nt = p.n_tot;
@@ -743,6 +1105,138 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     hipLaunchKernelGGL(lenet_acc_kernel, dim3((nt + kThreads - 1) / kThreads), dim3(kThreads), 0,
                        st, sa, eps, dW, acc, outer ? outer->ck : nullptr, W.wsamp,
                        1.f / (p.d.prior_sd * p.d.prior_sd));
+    return hipGetLastError();
+}
+
+LenetTanWs lenet_tan_ws(const psvi_plan& p, void* base) {
+    const int64_t S = p.s_cnt[p.rank], M = p.d.M;
+    LenetTanWs w{};
+    size_t off = 0;
+    char* b = (char*)base;
+    auto take = [&](size_t bytes) -> void* {
+        void* r = b ? (void*)(b + off) : nullptr;
+        off += (bytes + 255) & ~size_t(255);
+        return r;
+    };
+    w.nll = (double*)take(sizeof(double));
+    w.acc = (float*)take(sizeof(float) * 2 * p.n_tot);
+    w.wdot = (float*)take(sizeof(float) * S * p.n_tot);
+    w.gd = (float*)take(sizeof(float) * S * p.n_tot);
+    w.p1d = (float*)take(sizeof(float) * S * M * kP1);
+    w.x2d = (float*)take(sizeof(float) * S * M * kX2);
+    w.h1d = (float*)take(sizeof(float) * S * M * 120);
+    w.h2d = (float*)take(sizeof(float) * S * M * 84);
+    w.ld = (float*)take(sizeof(float) * S * M * 10);
+    w.prob = (float*)take(sizeof(float) * S * M * 10);
+    w.dh2d = (float*)take(sizeof(float) * S * M * 84);
+    w.dh1d = (float*)take(sizeof(float) * S * M * 120);
+    w.dx2d = (float*)take(sizeof(float) * S * M * kX2);
+    w.part = (float*)take(sizeof(float) * S * lenet_nchunk(p) * kNConv);
+    w.du = (float*)take(sizeof(float) * S * M * 784);
+    w.nlld = (float*)take(sizeof(float) * S * M);
+    w.bytes = off;
+    return w;
+}
+
+hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
+                            const float* eps, const float* params, const float* vec, float* hv,
+                            float* d_u, float* d_w, void* tws, hipStream_t st) {
+    const LenetWs W = lenet_ws(p, p.d_lenet_ws);
+    const LenetTanWs T = lenet_tan_ws(p, tws);
+    const SampleArgs sa = sample_args(p);
+    const int S = sa.S_loc, M = p.d.M, nt = p.n_tot;
+    const int64_t rows = (int64_t)S * M;
+    // primal pass: activations, routes, per-sample G, row probabilities
+    if (hipError_t e = hipMemsetAsync(T.nll, 0, sizeof(double), st)) return e;
+    NetOuter keep{0, 0, nullptr, nullptr, nullptr, nullptr, T.prob};
+    if (hipError_t e = launch_lenet(p, u, z, w, params, eps, T.acc, T.nll, p.d_lenet_ws, st, &keep))
+        return e;
+    {
+        const int64_t nb = std::min<int64_t>(((int64_t)S * nt + kThreads - 1) / kThreads, 8192);
+        hipLaunchKernelGGL(lenet_tangent_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, sa,
+                           params, vec, eps, T.wdot);
+    }
+    TanArgs ta{};
+    ta.M = M;
+    ta.n_tot = nt;
+    ta.nchunk = W.nchunk;
+    ta.chunk = (M + W.nchunk - 1) / W.nchunk;
+    ta.u = u;
+    ta.wsamp = W.wsamp;
+    ta.wdot = T.wdot;
+    ta.p1 = W.p1;
+    ta.r1 = W.r1;
+    ta.r2 = W.r2;
+    ta.dx2 = W.dx2;
+    ta.dx2d = T.dx2d;
+    ta.p1d = T.p1d;
+    ta.x2d = T.x2d;
+    ta.part = T.part;
+    ta.du = d_u ? T.du : nullptr;
+    hipLaunchKernelGGL(lenet_conv_fwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
+    const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
+    const float* Ws = W.wsamp;
+    const float* Wd = T.wdot;
+    // head tangent forward: h1_dot = 1[h1>0] (x2_dot W1^T + x2 W1_dot^T + b1_dot), ...
+    auto fwd2 = [&](int K, int N, const float* Ad, const float* A, int lw, int lb, float* C,
+                    const float* mask) -> hipError_t {
+        GemmArgs g = gemm_args(M, N, K, Ad, (int64_t)M * K, K, 1, Ws + lw, nt, 1, K, C,
+                               (int64_t)M * N, N);
+        if (hipError_t e = gemm(g, S, st)) return e;
+        g = gemm_args(M, N, K, A, (int64_t)M * K, K, 1, Wd + lw, nt, 1, K, C, (int64_t)M * N, N);
+        g.epi = 8 | 1 | (mask ? 4 : 0);
+        g.bias = Wd + lb;
+        g.sbias = nt;
+        g.mask = mask;
+        g.sMb = (int64_t)M * N;
+        g.sMm = N;
+        return gemm(g, S, st);
+    };
+    if (hipError_t e = fwd2(400, 120, T.x2d, W.x2, w3, w3 + 48000, T.h1d, W.h1)) return e;
+    if (hipError_t e = fwd2(120, 84, T.h1d, W.h1, w4, w4 + 10080, T.h2d, W.h2)) return e;
+    if (hipError_t e = fwd2(84, 10, T.h2d, W.h2, w5, w5 + 840, T.ld, nullptr)) return e;
+    hipLaunchKernelGGL(lenet_loss_tan_kernel, dim3((unsigned)((rows + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, (int)rows, M, z, w, T.prob, T.ld, T.nlld);
+    // head tangent backward (T.ld now holds d logits_dot)
+    auto dW2 = [&](int O, int I, const float* Dd, const float* Hp, const float* Dp,
+                   const float* Hd, int lw) -> hipError_t {
+        GemmArgs g = gemm_args(O, I, M, Dd, (int64_t)M * O, 1, O, Hp, (int64_t)M * I, I, 1,
+                               T.gd + lw, nt, I);
+        if (hipError_t e = gemm(g, S, st)) return e;
+        g = gemm_args(O, I, M, Dp, (int64_t)M * O, 1, O, Hd, (int64_t)M * I, I, 1, T.gd + lw, nt,
+                      I);
+        g.epi = 8;
+        if (hipError_t e = gemm(g, S, st)) return e;
+        hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, Dd, M, O,
+                           T.gd + lw + O * I, (int64_t)nt);
+        return hipGetLastError();
+    };
+    auto dX2 = [&](int O, int I, const float* Dd, const float* Dp, int lw, float* C,
+                   const float* mask) -> hipError_t {
+        GemmArgs g = gemm_args(M, I, O, Dd, (int64_t)M * O, O, 1, Ws + lw, nt, I, 1, C,
+                               (int64_t)M * I, I);
+        if (hipError_t e = gemm(g, S, st)) return e;
+        g = gemm_args(M, I, O, Dp, (int64_t)M * O, O, 1, Wd + lw, nt, I, 1, C, (int64_t)M * I, I);
+        g.epi = 8 | (mask ? 4 : 0);
+        g.mask = mask;
+        g.sMb = (int64_t)M * I;
+        g.sMm = I;
+        return gemm(g, S, st);
+    };
+    if (hipError_t e = dW2(10, 84, T.ld, W.h2, W.d, T.h2d, w5)) return e;
+    if (hipError_t e = dX2(10, 84, T.ld, W.d, w5, T.dh2d, W.h2)) return e;
+    if (hipError_t e = dW2(84, 120, T.dh2d, W.h1, W.dh2, T.h1d, w4)) return e;
+    if (hipError_t e = dX2(84, 120, T.dh2d, W.dh2, w4, T.dh1d, W.h1)) return e;
+    if (hipError_t e = dW2(120, 400, T.dh1d, W.x2, W.dh1, T.x2d, w3)) return e;
+    if (hipError_t e = dX2(120, 400, T.dh1d, W.dh1, w3, T.dx2d, nullptr)) return e;
+    hipLaunchKernelGGL(lenet_conv_bwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
+    hipLaunchKernelGGL(lenet_conv_reduce_kernel,
+                       dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, S, W.nchunk, nt, T.part, T.gd);
+    const int64_t n = nt + (d_u ? (int64_t)M * 784 : 0) + (d_w ? M : 0);
+    hipLaunchKernelGGL(lenet_hvp_assemble_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, sa, params, vec, eps, W.dws, T.gd, T.du, T.nlld, hv,
+                       d_u, d_w, M, 1.f / (p.d.prior_sd * p.d.prior_sd));
     return hipGetLastError();
 }
 

@@ -329,6 +329,18 @@ LenetWs lenet_ws(const psvi_plan& p, void* base);  // base nullptr: sizes only
 hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                         const float* params, const float* eps, float* acc, double* nll_out,
                         void* ws, hipStream_t st, const NetOuter* outer = nullptr);
+// LeNet HVP (kernels_lenet.hip): tangent scratch in the caller's workspace;
+// the primal pass uses the plan-owned scratch
+struct LenetTanWs {
+    double* nll;
+    float *acc, *wdot, *gd, *p1d, *x2d, *h1d, *h2d, *ld, *prob, *dh2d, *dh1d, *dx2d, *part, *du,
+        *nlld;
+    size_t bytes;
+};
+LenetTanWs lenet_tan_ws(const psvi_plan& p, void* base);
+hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
+                            const float* eps, const float* params, const float* vec, float* hv,
+                            float* d_u, float* d_w, void* tws, hipStream_t st);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
 hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,

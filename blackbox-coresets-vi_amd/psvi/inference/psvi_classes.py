@@ -153,13 +153,6 @@ class PSVI:
         self._eps_offset = 0
 
     # ------------------------------------------------------------ helpers
-    def _outer_supported(self, what):
-        """The second-order trainers need psvi_hvp, which the MLP families have;
-        make_lenet runs the inner loop, psvi_elbo and evaluate only."""
-        if model_spec(self.model)[0] == "lenet":
-            raise NotImplementedError(f"{what} for make_lenet needs the HVP through the conv "
-                                      "towers, which is not built on the HIP path")
-
     def coreset_weights(self):
         """N f(v): the per-pseudopoint NLL weights (detached, fp32)."""
         with torch.no_grad():
@@ -411,7 +404,6 @@ class PSVI:
         ``eps_outer``: optional sequences of draws (library eps layout) in the
         reference's call order, to replay; default: this instance's Philox
         stream."""
-        self._outer_supported("hyper_step")
         if hypergrad_approx not in ("CG_normaleq", "fixed_point"):
             raise NotImplementedError(f"hypergrad_approx={hypergrad_approx!r}: the reference's "
                                       "hyper_step offers CG_normaleq and fixed_point")
@@ -554,7 +546,6 @@ class PSVI:
         are written into the model.  Returns the outer loss (0-dim tensor).
         ``eps_inner`` (T draws) / ``eps_outer`` (1): optional replay of the
         reference's draws; default this instance's Philox stream."""
-        self._outer_supported("nested_step")
         if truncated:
             raise NotImplementedError("truncated nested_step (torch.optim.Adam warm start) is "
                                       "not on the HIP path")

@@ -252,7 +252,7 @@ class InnerLoopPlan:
         dev = params.device
         hv = torch.empty(self.param_count, dtype=torch.float32, device=dev) if out is None else out
         _need(hv, "hv_out", self.param_count)
-        du = torch.empty(self.M, self.layers[0][0], dtype=torch.float32, device=dev) if mixed else None
+        du = torch.empty(self.M, self.in_features, dtype=torch.float32, device=dev) if mixed else None
         dw = torch.empty(self.M, dtype=torch.float32, device=dev) if mixed else None
         if ws is None or ws.numel() < self.hvp_ws_bytes:
             ws = torch.empty(self.hvp_ws_bytes, dtype=torch.uint8, device=dev)

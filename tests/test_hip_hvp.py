@@ -7,7 +7,7 @@ import pytest
 import torch
 
 import psvi_oracle as O
-from golden_util import family_of, fixture_names, l2rel, load_fixture
+from golden_util import family_of, fixture_names, l2rel, load_fixture, plan_layers
 from test_oracle_hyper import softmax_T
 
 pytestmark = pytest.mark.gpu
@@ -32,7 +32,7 @@ def _hvp(family, layers, S, u, z, w, eps, params, vec):
 def test_hvp_matches_reference_double_backward(name):
     f = load_fixture(name)
     cfg = f["cfg"]
-    hv, du, dw = _hvp(family_of(cfg), cfg["layers"], cfg["S"], f["u"], f["z"], f["w"], f["eps"],
+    hv, du, dw = _hvp(family_of(cfg), plan_layers(cfg), cfg["S"], f["u"], f["z"], f["w"], f["eps"],
                       f["params0"], f["vec"])
     assert l2rel(hv, f["hv"]) < 1e-4, l2rel(hv, f["hv"])
     assert l2rel(du, f["d_u"]) < 1e-4, l2rel(du, f["d_u"])

@@ -74,11 +74,11 @@ def test_run_psvi_like_flow_psvi(trainer, arch, cls):
     assert np.asarray(res["us"][0]).shape == (10, 2)
 
 
-@pytest.mark.parametrize("trainer", ["joint", "alternating"])
-def test_run_psvi_lenet_first_order_trainers(trainer):
-    """make_lenet through run_psvi on an MNIST-shaped synthetic set with the
-    first-order trainers (psvi_elbo + evaluate on the LeNet kernels); the
-    second-order ones refuse LeNet (no HVP through the conv towers)."""
+@pytest.mark.parametrize("trainer", ["joint", "alternating", "hyper", "nested"])
+def test_run_psvi_lenet_trainers(trainer):
+    """make_lenet through run_psvi on an MNIST-shaped synthetic set with every
+    trainer: psvi_elbo, evaluate, and for hyper / nested the LeNet HVP (C5's
+    bilevel outer) on the LeNet kernels."""
     import psvi.inference as I
     from psvi.experiments import make_mnist_shaped
 
@@ -91,6 +91,3 @@ def test_run_psvi_lenet_first_order_trainers(trainer):
     torch.manual_seed(0)
     res = I.PSVILearnV(**kw).run_psvi(**kw)
     assert len(res["accs"]) == 2 and all(math.isfinite(x) for x in res["nlls"])
-    with pytest.raises(NotImplementedError, match="HVP"):
-        kw2 = dict(kw, trainer="hyper")
-        I.PSVILearnV(**kw2).run_psvi(**kw2)
