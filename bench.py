@@ -157,6 +157,35 @@ def lenet_timings(dev, cpu=True, T=10):
     ms = (time.perf_counter() - t0) / T * 1e3
     out = {"config": "C5 lenet S=256 M=500", "gpu_ms_per_inner_step": round(ms, 3),
            "gpu_inner_steps_per_s": round(1e3 / ms, 2)}
+    # C5's bilevel outer: one psvi_hvp, and one hyper_step (inner_it = 10, K = 30,
+    # a 128-image data batch) through the reference-shaped PSVILearnV
+    from psvi.inference import PSVILearnV
+    from psvi.runtime import randn_
+
+    e = torch.empty(plan.eps_count, device=dev)
+    randn_(e, 5)
+    vec = torch.randn(plan.param_count, generator=g).to(dev)
+    plan.hvp(ud, zd, wd, e, params, vec)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        plan.hvp(ud, zd, wd, e, params, vec)
+    torch.cuda.synchronize()
+    out["gpu_hvp_ms"] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
+    net_d = make_lenet(mc_samples=S, init_sd=0.05).to(dev)
+    ps = PSVILearnV(u=ud.clone().requires_grad_(True), z=zd.float(), N=60000, model=net_d,
+                    mc_samples=S, device_id=dev.index, inner_it=10, seed=7)
+    ps.device = dev
+    ps.register_elbos = False
+    ps.setup_optimizers()
+    xb = torch.randn(128, 1, 28, 28, generator=g).to(dev)
+    yb = torch.randint(0, 10, (128,), generator=g).float().to(dev)
+    ps.hyper_step(xb, yb, K=30)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ps.hyper_step(xb, yb, K=30)
+    torch.cuda.synchronize()
+    out["gpu_hyper_step_T10_K30_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from cpu_reference import RefLenetStep
