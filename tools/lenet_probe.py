@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--M", type=int, default=500)
     ap.add_argument("--T", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--hvp", type=int, default=0, help="also time N psvi_hvp calls")
     a = ap.parse_args()
     from psvi.models import make_lenet
     from psvi.runtime import InnerLoopPlan
@@ -43,6 +44,19 @@ def main():
         print(f"S={a.S} M={a.M} T={a.T}: {dt * 1e3:.3f} ms/step  "
               f"({1.0 / dt:.1f} inner-steps/s)  elbo[0]={el[0].item():.6g} "
               f"elbo[-1]={el[-1].item():.6g}", flush=True)
+    if a.hvp:
+        from psvi.runtime import randn_
+
+        e = torch.empty(plan.eps_count, device="cuda")
+        randn_(e, 9)
+        vec = torch.randn(plan.param_count, device="cuda")
+        plan.hvp(u, z, w, e, params, vec)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.hvp):
+            plan.hvp(u, z, w, e, params, vec)
+        torch.cuda.synchronize()
+        print(f"psvi_hvp: {(time.perf_counter() - t0) / a.hvp * 1e3:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
