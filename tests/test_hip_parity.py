@@ -11,7 +11,7 @@ import pytest
 import torch
 
 import psvi_oracle as O
-from golden_util import (adam_kind, assert_grad_close, family_of, fixture_names, l2rel,
+from golden_util import (adam_kind, assert_grad_close, family_of, fixture_names, l2rel, plan_layers,
                          load_fixture, rel)
 
 pytestmark = pytest.mark.gpu
@@ -343,3 +343,37 @@ def test_tiled_update_equals_packed(name, fused):
     if fused:
         assert torch.isfinite(x2).all()
         assert l2rel(x2.cpu().numpy(), x1.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["g2r_fn_c2_rand_av", "g3r_fn2_tiny_rand", "l1_lenet_tiny"])
+def test_inner_loop_checkpoint_resume(name):
+    """Checkpoint / resume: the inner-loop state is caller-owned,
+    so saving params and the Adam m, v with torch.save after k steps and
+    resuming with step0 = k + 1 continues the same trajectory."""
+    import io
+
+    from psvi.runtime import InnerLoopPlan
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    plan = InnerLoopPlan(family_of(cfg), plan_layers(cfg), cfg["S"], cfg["M"])
+    u, z, w = _t(f["u"]), _t(f["z"].astype(np.int32), torch.int32), _t(f["w"])
+    T, kind, eps = cfg["T"], adam_kind(cfg), _t(f["eps"])
+    p1 = _t(f["params0"])
+    m1, v1 = torch.zeros_like(p1), torch.zeros_like(p1)
+    e1 = plan.inner_loop(u, z, w, p1, m1, v1, T, cfg["lr"], kind=kind, eps=eps)
+    p2 = _t(f["params0"])
+    m2, v2 = torch.zeros_like(p2), torch.zeros_like(p2)
+    k = 1
+    ea = plan.inner_loop(u, z, w, p2, m2, v2, k, cfg["lr"], kind=kind,
+                         eps=eps[:k].contiguous()).clone()
+    buf = io.BytesIO()
+    torch.save({"params": p2, "m": m2, "v": v2, "step": k}, buf)
+    buf.seek(0)
+    st = torch.load(buf, weights_only=True)  # a file this test wrote
+    eb = plan.inner_loop(u, z, w, st["params"], st["m"], st["v"], T - k, cfg["lr"], kind=kind,
+                         step0=st["step"] + 1, eps=eps[k:].contiguous())
+    e2 = torch.cat([ea, eb]).cpu().numpy()
+    assert rel(e2, e1.cpu().numpy()) < 1e-6
+    for a, b in ((st["params"], p1), (st["m"], m1), (st["v"], v1)):
+        assert l2rel(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
