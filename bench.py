@@ -86,7 +86,7 @@ def algorithmic_work(S, rows_frac=1.0):
                 sample=dict(bytes=fwd_bytes, flops=fwd_flops))
 
 
-def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r01e_pmc_traffic.json")):
+def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r01f_pmc_traffic.json")):
     """HBM bytes per launch of the listed kernels (summed: the phase the
     roofline times) from the committed rocprofv3 PMC summary
     (tools/pmc_session.sh -> tools/pmc_report.py --json: separate FETCH_SIZE /
