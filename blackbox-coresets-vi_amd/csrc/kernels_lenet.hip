@@ -490,18 +490,22 @@ __global__ __launch_bounds__(kThreads) void lenet_gemm_kernel(GemmArgs g) {
     }
 }
 
-// out[b * sOb + n] = sum_m X[b][m][n]  (bias gradients; fixed order over m)
+// out[b * sOb + n] = sum_m X[b][m][n]  (bias gradients): one workgroup per
+// (b, 64 columns), four row groups (m = g mod 4) summed in a fixed order
 __global__ __launch_bounds__(kThreads) void lenet_colsum_kernel(const float* __restrict__ X,
                                                                 int M, int N,
                                                                 float* __restrict__ out,
                                                                 int64_t sOb) {
-    const int b = blockIdx.x;
+    __shared__ float red[4][64];
+    const int b = blockIdx.x, c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int n = blockIdx.y * 64 + c;
     const float* x = X + (int64_t)b * M * N;
-    for (int n = threadIdx.x; n < N; n += kThreads) {
-        float acc = 0.f;
-        for (int m = 0; m < M; ++m) acc += x[(int64_t)m * N + n];
-        out[b * sOb + n] = acc;
-    }
+    float acc = 0.f;
+    if (n < N)
+        for (int m = g; m < M; m += 4) acc += x[(int64_t)m * N + n];
+    red[g][c] = acc;
+    __syncthreads();
+    if (g == 0 && n < N) out[b * sOb + n] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
 }
 
 // weighted NLL of each (s, m) row and d logits in place: w_m (softmax - onehot)
@@ -724,6 +728,31 @@ __device__ __forceinline__ void convT_block(const float* q, int ld, const float*
         }
 }
 
+// convT_block for two weight sets over one patch: acc_a += wa * Q, acc_b += wb * Q
+__device__ __forceinline__ void convT_block2(const float* q, int ld, const float* wa,
+                                             const float* wb, float (&acc_a)[4],
+                                             float (&acc_b)[4]) {
+    float Q[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * ld + j];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const float va = wa[i * 5 + j], vb = wb[i * 5 + j];
+            acc_a[0] += va * Q[4 - i][4 - j];
+            acc_a[1] += va * Q[4 - i][5 - j];
+            acc_a[2] += va * Q[5 - i][4 - j];
+            acc_a[3] += va * Q[5 - i][5 - j];
+            acc_b[0] += vb * Q[4 - i][4 - j];
+            acc_b[1] += vb * Q[4 - i][5 - j];
+            acc_b[2] += vb * Q[5 - i][4 - j];
+            acc_b[3] += vb * Q[5 - i][5 - j];
+        }
+}
+
 // tangent backward of the conv towers: G_dot for conv2 and conv1, and the
 // tangent of d u (the mixed product d/du) for every row.  One LDS plane
 // region serves the routed conv2 gradients (primal and tangent, 18x18 with a
@@ -817,9 +846,9 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
             float acc[4] = {0.f, 0.f, 0.f, 0.f}, accd[4] = {0.f, 0.f, 0.f, 0.f};
             for (int k = 0; k < 16; ++k) {
                 const int po = k * kDA * kDA + yy * kDA + xx;
-                convT_block(da2 + po, kDA, w2 + k * 150 + c * 25, acc);
+                convT_block2(da2 + po, kDA, w2 + k * 150 + c * 25, wd2 + k * 150 + c * 25, acc,
+                             accd);
                 convT_block(da2d + po, kDA, w2 + k * 150 + c * 25, accd);
-                convT_block(da2 + po, kDA, wd2 + k * 150 + c * 25, accd);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1065,7 +1094,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     g = gemm_args(10, 84, M, W.d, (int64_t)M * 10, 1, 10, W.h2, (int64_t)M * 84, 84, 1,
                   dW + w5, nt, 84);
     if (hipError_t e = gemm(g, S, st)) return e;
-    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, W.d, M, 10,
+    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S, (10 + 63) / 64), dim3(kThreads), 0, st, W.d, M, 10,
                        dW + w5 + 840, (int64_t)nt);
     g = gemm_args(M, 84, 10, W.d, (int64_t)M * 10, 10, 1, Ws + w5, nt, 84, 1, W.dh2,
                   (int64_t)M * 84, 84);
@@ -1074,7 +1103,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     g = gemm_args(84, 120, M, W.dh2, (int64_t)M * 84, 1, 84, W.h1, (int64_t)M * 120, 120, 1,
                   dW + w4, nt, 120);
     if (hipError_t e = gemm(g, S, st)) return e;
-    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, W.dh2, M, 84,
+    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S, (84 + 63) / 64), dim3(kThreads), 0, st, W.dh2, M, 84,
                        dW + w4 + 10080, (int64_t)nt);
     g = gemm_args(M, 120, 84, W.dh2, (int64_t)M * 84, 84, 1, Ws + w4, nt, 120, 1, W.dh1,
                   (int64_t)M * 120, 120);
@@ -1083,7 +1112,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     g = gemm_args(120, 400, M, W.dh1, (int64_t)M * 120, 1, 120, W.x2, (int64_t)M * 400, 400, 1,
                   dW + w3, nt, 400);
     if (hipError_t e = gemm(g, S, st)) return e;
-    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, W.dh1, M, 120,
+    hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S, (120 + 63) / 64), dim3(kThreads), 0, st, W.dh1, M, 120,
                        dW + w3 + 48000, (int64_t)nt);
     g = gemm_args(M, 400, 120, W.dh1, (int64_t)M * 120, 120, 1, Ws + w3, nt, 400, 1, W.dx2,
                   (int64_t)M * 400, 400);
@@ -1207,7 +1236,7 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
                       I);
         g.epi = 8;
         if (hipError_t e = gemm(g, S, st)) return e;
-        hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S), dim3(kThreads), 0, st, Dd, M, O,
+        hipLaunchKernelGGL(lenet_colsum_kernel, dim3(S, (O + 63) / 64), dim3(kThreads), 0, st, Dd, M, O,
                            T.gd + lw + O * I, (int64_t)nt);
         return hipGetLastError();
     };
