@@ -155,8 +155,14 @@ def lenet_timings(dev, cpu=True, T=10):
     plan.inner_loop(ud, zd, wd, params, m, v, T, LR, seed=2, ws=ws)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / T * 1e3
+    # 289.8 GFLOP of algorithmic work per C5 inner step
+    # (106.6 forward + 183.2 backward); fp32 peak 157.3 TFLOP/s (VALU and MFMA alike)
+    tfl = 289.8e9 / (ms * 1e-3) / 1e12
     out = {"config": "C5 lenet S=256 M=500", "gpu_ms_per_inner_step": round(ms, 3),
-           "gpu_inner_steps_per_s": round(1e3 / ms, 2)}
+           "gpu_inner_steps_per_s": round(1e3 / ms, 2),
+           "roofline": {"bound": "fp32 (VALU = MFMA peak)", "achieved": round(tfl, 2),
+                        "peak": 157.3, "unit": "TFLOP/s", "frac": round(tfl / 157.3, 4),
+                        "algorithmic_gflop_per_step": 289.8}}
     # C5's bilevel outer: one psvi_hvp, and one hyper_step (inner_it = 10, K = 30,
     # a 128-image data batch) through the reference-shaped PSVILearnV
     from psvi.inference import PSVILearnV
