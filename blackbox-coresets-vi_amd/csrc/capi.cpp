@@ -827,18 +827,21 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     return 0;
 }
 
-int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
-                         const int32_t* z_all, const float* w_all, const float* eps,
-                         const float* params, double* loss_out, float* grad_params,
-                         float* grad_u, float* grad_w, double* sample_out, void* ws,
-                         size_t ws_bytes, void* stream) {
+// ext_coef == nullptr: the whole objective (stats, forward, combine, backward).
+// Otherwise [rowcoef (S x 2) | ck (S) | sck (1)] replace the combine: the
+// backward of a caller-formed softmax over samples (sample-sharded outer).
+static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
+                      const int32_t* z_all, const float* w_all, const float* eps,
+                      const float* params, double* loss_out, float* grad_params,
+                      float* grad_u, float* grad_w, double* sample_out,
+                      const float* ext_coef, void* ws, size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "the outer objective needs world == 1");
-    if (p->d.S < 2) return fail(PSVI_EINVAL, "psvi_elbo needs S > 1 (psvi_classes.py:449)");
+    if (p->d.S < 1) return fail(PSVI_EINVAL, "S must be >= 1");
     if (p->d.S > 2048) return fail(PSVI_EUNSUP, "the outer objective supports S <= 2048");
     if (n_pseudo < 0 || n_pseudo > p->d.M) return fail(PSVI_EINVAL, "n_pseudo out of [0, M]");
-    if (!x_all || !z_all || !w_all || !eps || !params || !loss_out)
+    if (!x_all || !z_all || !w_all || !eps || !params || (!loss_out && !ext_coef))
         return fail(PSVI_EINVAL, "null pointer");
     if (grad_u && !grad_params)
         return fail(PSVI_EINVAL, "grad_u needs grad_params (one backward pass gives both)");
@@ -857,7 +860,7 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
     } else {
         acc = (float*)wsb;
     }
-    HIP_TRY(launch_outer_stats(*p, params, eps, x, o.stats, st));
+    if (!ext_coef) HIP_TRY(launch_outer_stats(*p, params, eps, x, o.stats, st));
     // 1. forward: every row's NLL
     NetOuter fw{1, n_pseudo, o.nll, nullptr, nullptr, nullptr};
     if (p->family == PSVI_FAMILY_LENET)
@@ -866,9 +869,20 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
     else
         HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
                            nullptr, st, nullptr, 0, 0, 0, &fw));
-    // 2. per-sample terms, softmax over samples, loss, backward coefficients
-    HIP_TRY(launch_outer_combine(*p, n_pseudo, params, w_all, o.nll, o.stats, loss_out,
-                                 o.rowcoef, o.ck, o.sck, grad_w, sample_out, st));
+    if (!ext_coef) {
+        // 2. per-sample terms, softmax over samples, loss, backward coefficients
+        HIP_TRY(launch_outer_combine(*p, n_pseudo, params, w_all, o.nll, o.stats, loss_out,
+                                     o.rowcoef, o.ck, o.sck, grad_w, sample_out, st));
+    } else {
+        const size_t S = p->d.S;
+        HIP_TRY(hipMemcpyAsync(o.rowcoef, ext_coef, sizeof(float) * 2 * S,
+                               hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(o.ck, ext_coef + 2 * S, sizeof(float) * S,
+                               hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(o.sck, ext_coef + 3 * S, sizeof(float), hipMemcpyDeviceToDevice,
+                               st));
+        if (grad_w) HIP_TRY(launch_outer_gradw(*p, n_pseudo, o.nll, o.rowcoef, grad_w, st));
+    }
     if (!grad_params) return 0;
     // 3. backward through the network with the row coefficients (+ sampled-KL path)
     NetOuter bw{2, n_pseudo, nullptr, o.rowcoef, o.ck, grad_u ? o.du : nullptr};
@@ -898,6 +912,25 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
 }
 
 static size_t eval_prob_off(const psvi_plan* p) { return outer_ws(p, nullptr).bytes; }
+
+int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
+                         const int32_t* z_all, const float* w_all, const float* eps,
+                         const float* params, double* loss_out, float* grad_params,
+                         float* grad_u, float* grad_w, double* sample_out, void* ws,
+                         size_t ws_bytes, void* stream) {
+    return outer_impl(p, n_pseudo, x_all, z_all, w_all, eps, params, loss_out, grad_params,
+                      grad_u, grad_w, sample_out, nullptr, ws, ws_bytes, stream);
+}
+
+int psvi_outer_elbo_grad_coef(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
+                              const int32_t* z_all, const float* w_all, const float* eps,
+                              const float* params, const float* coef, float* grad_params,
+                              float* grad_u, float* grad_w, void* ws, size_t ws_bytes,
+                              void* stream) {
+    if (!coef) return fail(PSVI_EINVAL, "null coefficients");
+    return outer_impl(p, n_pseudo, x_all, z_all, w_all, eps, params, nullptr, grad_params,
+                      grad_u, grad_w, nullptr, coef, ws, ws_bytes, stream);
+}
 
 int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, const int32_t* z_all,
                   const float* w_all, const float* eps, const float* params, int32_t correction,

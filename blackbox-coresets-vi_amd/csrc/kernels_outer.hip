@@ -401,4 +401,25 @@ hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* pa
     return hipGetLastError();
 }
 
+// d loss / d w_m = sum_s cp_s NLL_sm (the combine kernel's last loop) for
+// caller-given coefficients (psvi_outer_elbo_grad_coef)
+__global__ __launch_bounds__(256) void outer_gradw_kernel(int S, int M, int n_pseudo,
+                                                          const float* __restrict__ nll,
+                                                          const float* __restrict__ rowcoef,
+                                                          float* __restrict__ grad_w) {
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= n_pseudo) return;
+    double g = 0.0;
+    for (int s = 0; s < S; ++s) g += (double)rowcoef[2 * s] * nll[(size_t)s * M + m];
+    grad_w[m] = (float)g;
+}
+
+hipError_t launch_outer_gradw(const psvi_plan& p, int n_pseudo, const float* nll,
+                              const float* rowcoef, float* grad_w, hipStream_t st) {
+    if (n_pseudo <= 0) return hipSuccess;
+    hipLaunchKernelGGL(outer_gradw_kernel, dim3((n_pseudo + 255) / 256), dim3(256), 0, st,
+                       p.d.S, p.d.M, n_pseudo, nll, rowcoef, grad_w);
+    return hipGetLastError();
+}
+
 }  // namespace psvi

@@ -309,6 +309,8 @@ hipError_t launch_eval(const psvi_plan& p, int n_pseudo, const float* params, co
                        const int32_t* z, const float* nll, const double* stats,
                        const float* prob, int correction, float* W, float* probs_out,
                        double* out, hipStream_t st);
+hipError_t launch_outer_gradw(const psvi_plan& p, int n_pseudo, const float* nll,
+                              const float* rowcoef, float* grad_w, hipStream_t st);
 hipError_t launch_outer_finish(const psvi_plan& p, int n_pseudo, const float* params,
                                const float* sck, float* grad, const float* du_part,
                                float* grad_u, hipStream_t st);

@@ -88,6 +88,8 @@ SIGNATURES = {
                                ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
     "psvi_outer_elbo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _SZ, _P]),
+    "psvi_outer_elbo_grad_coef": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                         _SZ, _P]),
     "psvi_evaluate": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
     "psvi_hvp": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "psvi_adam_adjoint": (_I32, [_I64, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP),

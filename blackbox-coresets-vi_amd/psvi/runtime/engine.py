@@ -219,6 +219,36 @@ class InnerLoopPlan:
             _stream()), "psvi_outer_elbo_grad")
         return out
 
+    def outer_grad_coef(self, n_pseudo, x_all, z_all, w_all, eps, params, coef, grad_u=True,
+                        grad_w=True, ws=None):
+        """Backward of the outer objective with caller-given per-sample
+        coefficients coef = [rowcoef (S, 2) | ck (S) | sck] (float32, 3S + 1)
+        -- psvi_outer_elbo_grad_coef, the second pass of the sample-sharded
+        outer objective (sharded.ShardedOuter).  Returns grad (P), grad_u
+        (n_pseudo, D) and grad_w (n_pseudo) as requested."""
+        D = self.in_features
+        n_pseudo = int(n_pseudo)
+        _need(x_all, "x_all", self.M * D)
+        _need(z_all, "z_all", self.M, torch.int32)
+        _need(w_all, "w_all", self.M)
+        _need(eps, "eps", self.eps_count)
+        _need(params, "params", self.param_count)
+        _need(coef, "coef", 3 * self.S + 1)
+        dev = params.device
+        out = {"grad": torch.empty(self.param_count, dtype=torch.float32, device=dev)}
+        if grad_u:
+            out["grad_u"] = torch.empty(n_pseudo, D, dtype=torch.float32, device=dev)
+        if grad_w:
+            out["grad_w"] = torch.empty(n_pseudo, dtype=torch.float32, device=dev)
+        if ws is None or ws.numel() < self.outer_ws_bytes:
+            ws = torch.empty(self.outer_ws_bytes, dtype=torch.uint8, device=dev)
+        check(self.lib.psvi_outer_elbo_grad_coef(
+            self.handle, n_pseudo, _ptr(x_all), _ptr(z_all), _ptr(w_all), _ptr(eps),
+            _ptr(params), _ptr(coef), _ptr(out["grad"]), _ptr(out.get("grad_u")),
+            _ptr(out.get("grad_w")), _ptr(ws), ws.numel(), _stream()),
+            "psvi_outer_elbo_grad_coef")
+        return out
+
     def evaluate(self, n_pseudo, x_all, z_all, w_all, eps, params, correction=True, probs=False,
                  ws=None):
         """Importance-weighted predictive evaluation of the data rows of this

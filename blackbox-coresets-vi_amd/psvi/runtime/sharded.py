@@ -137,3 +137,115 @@ class ShardedInnerLoop:
         for t in tensors:
             t.mul_(mask)
             self.comm.all_reduce(t)
+
+
+# ---------------------------------------------------------------------------
+# Sample-sharded outer objective (PSVI.psvi_elbo, psvi_classes.py:447-486)
+# ---------------------------------------------------------------------------
+def sample_split(S, world):
+    """Contiguous sample blocks [(offset, count)] per rank (first S % world
+    ranks one larger), the split of the inner-loop plans."""
+    base, rem = divmod(S, world)
+    out, o = [], 0
+    for r in range(world):
+        c = base + (r < rem)
+        out.append((o, c))
+        o += c
+    return out
+
+
+def local_eps(family, layers, S, s_off, s_cnt, eps):
+    """The noise of samples [s_off, s_off + s_cnt) out of the global eps (the
+    reference draw order, include/psvi_hip.h) laid out for a world-1 plan of
+    s_cnt samples.  LeNet's last layer is one shared draw (unbatched VILinear)."""
+    parts, o = [], 0
+    for l, (din, dout) in enumerate(layers):
+        nw = din * dout
+        if family == "fullcov":
+            n = nw + dout
+            parts.append(eps[o:o + S * n].view(S, n)[s_off:s_off + s_cnt].reshape(-1))
+            o += S * n
+        elif family == "lenet" and l == len(layers) - 1:
+            parts.append(eps[o:o + nw + dout])
+            o += nw + dout
+        else:
+            parts.append(eps[o:o + S * nw].view(S, nw)[s_off:s_off + s_cnt].reshape(-1))
+            o += S * nw
+            parts.append(eps[o:o + S * dout].view(S, dout)[s_off:s_off + s_cnt].reshape(-1))
+            o += S * dout
+    assert o == eps.numel(), (o, eps.numel())
+    return torch.cat(parts).contiguous()
+
+
+def outer_coefficients(terms):
+    """Per-sample terms (S, 3) float64 [pseudo NLL sum, data NLL sum, KL-ish
+    nkl] of ALL samples -> (loss, cp, cd, ck): the psvi_elbo value and the
+    derivatives of the loss w.r.t. each sample's pseudo, data and nkl terms.
+    loss = sum_s W_s (data_s - pseudo_s) - mean_s lw_s with lw = nkl - pseudo,
+    W = softmax(lw) over samples (psvi_classes.py:463-481)."""
+    pseudo, data, nkl = terms[:, 0], terms[:, 1], terms[:, 2]
+    S = terms.shape[0]
+    lw = nkl - pseudo
+    W = torch.softmax(lw, 0)
+    a = data - pseudo
+    abar = (W * a).sum()
+    loss = abar - lw.mean()
+    ck = W * (a - abar) - 1.0 / S
+    cp = -W - ck
+    return loss, cp, W, ck
+
+
+def pack_coef(cp, cd, ck, s_off, s_cnt):
+    """[rowcoef (s_cnt, 2) | ck (s_cnt) | sck] for psvi_outer_elbo_grad_coef."""
+    sl = slice(s_off, s_off + s_cnt)
+    rc = torch.stack([cp[sl], cd[sl]], 1).reshape(-1)
+    return torch.cat([rc, ck[sl], ck[sl].sum().reshape(1)]).float().contiguous()
+
+
+class ShardedOuter:
+    """The outer objective with the S samples split over ranks.  Pass 1: each
+    rank's world-1 plan of its own samples gives the per-sample terms
+    (psvi_outer_elbo_grad, sample_out only); one all-reduce assembles all S;
+    the softmax over samples is formed on every rank identically (float64);
+    pass 2 (psvi_outer_elbo_grad_coef) gives this rank's partial gradients,
+    summed by one all-reduce.  Parameters, pseudo/data rows and the global eps
+    are replicated; the per-sample towers are not."""
+
+    def __init__(self, family, layers, S, M, world, rank, prior_sd=1.0, device="cuda",
+                 comm=None):
+        self.family, self.layers, self.S, self.M = family, list(layers), S, M
+        self.world, self.rank, self.comm, self.device = world, rank, comm, device
+        self.split = sample_split(S, world)
+        self.s_off, self.s_cnt = self.split[rank]
+        if self.s_cnt < 1:
+            raise ValueError(f"rank {rank} has no samples (S={S}, world={world})")
+        self.plan = InnerLoopPlan(family, layers, self.s_cnt, M, prior_sd=prior_sd)
+
+    def local_terms(self, n_pseudo, x_all, z_all, w_all, eps, params):
+        """Pass 1 -> (eps_local, terms (s_cnt, 3) float64)."""
+        e = local_eps(self.family, self.layers, self.S, self.s_off, self.s_cnt, eps)
+        o = self.plan.outer_elbo_grad(n_pseudo, x_all, z_all, w_all, e, params, grad=False,
+                                      grad_w=False, sample_stats=True)
+        return e, o["samples"][:, :3].contiguous()
+
+    def local_grads(self, n_pseudo, x_all, z_all, w_all, eps_local, params, cp, cd, ck,
+                    grad_u=True, grad_w=True):
+        """Pass 2: this rank's partial gradients for global coefficients."""
+        coef = pack_coef(cp, cd, ck, self.s_off, self.s_cnt).to(params.device)
+        return self.plan.outer_grad_coef(n_pseudo, x_all, z_all, w_all, eps_local, params, coef,
+                                         grad_u=grad_u, grad_w=grad_w)
+
+    def elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad_u=True, grad_w=True):
+        """Loss (float64 tensor) and the full gradients on every rank."""
+        e, t = self.local_terms(n_pseudo, x_all, z_all, w_all, eps, params)
+        terms = torch.zeros(self.S, 3, dtype=torch.float64, device=t.device)
+        terms[self.s_off:self.s_off + self.s_cnt] = t
+        self.comm.all_reduce(terms)
+        loss, cp, cd, ck = outer_coefficients(terms)
+        g = self.local_grads(n_pseudo, x_all, z_all, w_all, e, params, cp, cd, ck,
+                             grad_u=grad_u, grad_w=grad_w)
+        for k in ("grad", "grad_u", "grad_w"):
+            if k in g:
+                self.comm.all_reduce(g[k])
+        g["loss"] = loss.reshape(1)
+        return g

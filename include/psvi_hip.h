@@ -260,6 +260,22 @@ int psvi_outer_elbo_grad(const psvi_plan* plan, int32_t n_pseudo, const float* x
                          float* grad_u, float* grad_w, double* sample_out, void* ws,
                          size_t ws_bytes, void* stream);
 
+/* The backward half of psvi_outer_elbo_grad with caller-given per-sample
+ * coefficients instead of the plan's own softmax over its S samples:
+ *   coef = [rowcoef (S x 2): d loss / d pseudo_s, d loss / d data_s |
+ *           ck (S): d loss / d nkl_s | sck (1): the sum of ck over these samples]
+ * (floats, device).  For the sample-sharded outer objective:
+ * each rank runs psvi_outer_elbo_grad on a plan of its own samples for the
+ * per-sample terms (sample_out), the host forms the softmax over ALL samples
+ * (psvi.runtime.sharded.ShardedOuter), and each rank's grad_params / grad_u /
+ * grad_w from this call are partial sums over its samples (sum over ranks).
+ * S may be 1 here.  ws: PSVI_Q_OUTER_WS_BYTES. */
+int psvi_outer_elbo_grad_coef(const psvi_plan* plan, int32_t n_pseudo, const float* x_all,
+                              const int32_t* z_all, const float* w_all, const float* eps,
+                              const float* params, const float* coef, float* grad_params,
+                              float* grad_u, float* grad_w, void* ws, size_t ws_bytes,
+                              void* stream);
+
 /* Importance-weighted predictive evaluation of one test batch: PSVI.evaluate
  * (psvi_classes.py:1031-1108) and pred_on_grid (1130-1175), world == 1,
  * 2 <= S <= 2048.  Rows as psvi_outer_elbo_grad: x_all = cat(u, xtest), the
