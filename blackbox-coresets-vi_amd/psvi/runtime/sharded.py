@@ -212,14 +212,16 @@ class ShardedOuter:
     are replicated; the per-sample towers are not."""
 
     def __init__(self, family, layers, S, M, world, rank, prior_sd=1.0, device="cuda",
-                 comm=None):
+                 comm=None, plan=None):
+        """plan: a world-1 plan of this rank's samples (built when None)."""
         self.family, self.layers, self.S, self.M = family, list(layers), S, M
         self.world, self.rank, self.comm, self.device = world, rank, comm, device
         self.split = sample_split(S, world)
         self.s_off, self.s_cnt = self.split[rank]
         if self.s_cnt < 1:
             raise ValueError(f"rank {rank} has no samples (S={S}, world={world})")
-        self.plan = InnerLoopPlan(family, layers, self.s_cnt, M, prior_sd=prior_sd)
+        self.plan = plan if plan is not None else InnerLoopPlan(family, layers, self.s_cnt, M,
+                                                                prior_sd=prior_sd)
 
     def local_terms(self, n_pseudo, x_all, z_all, w_all, eps, params):
         """Pass 1 -> (eps_local, terms (s_cnt, 3) float64)."""
