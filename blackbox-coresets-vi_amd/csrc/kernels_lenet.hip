@@ -126,10 +126,20 @@ __device__ __forceinline__ float relu_pool4(float a0, float a1, float a2, float 
 // bwd kernel's 294 transposed-conv blocks fit in one pass.
 constexpr int kConvThreads = 320;
 
+// LDS planes of the forward split by column parity: a 2x2-pool window's
+// patch starts at an even column, so adjacent lanes read 2 columns apart --
+// 2-3-way ds_read_b32 bank conflicts in one 32-bank group.  With the even and
+// odd columns in separate planes, lanes read consecutive words; the row
+// strides put a wave's 3 (conv1) or 5 (conv2) patch rows on disjoint banks.
+constexpr int kInH = 23;   // padded image: 32 rows x 16 half-columns, stride 23
+constexpr int kInP = 32 * kInH;
+constexpr int kP1H = 13;   // pooled conv1 map: 6 x 14 rows x 7 half-columns, stride 13
+constexpr int kP1P = 6 * 14 * kP1H;
+
 __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
     __shared__ float w1[150], b1[6], w2[2400], b2[16];
-    __shared__ float in[32 * 32];       // 28x28 image, zero padding 2
-    __shared__ float p1[kP1];
+    __shared__ float in[2 * kInP];      // 28x28 image, zero padding 2, [parity][y][x / 2]
+    __shared__ float p1[2 * kP1P];      // [parity][c][y][x / 2]
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
     for (int i = tid; i < kNConv; i += kConvThreads) {
@@ -145,7 +155,8 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
         const float* um = a.u + (int64_t)m * 784;
         for (int i = tid; i < 1024; i += kConvThreads) {
             const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+            in[(i & 1) * kInP + (i >> 5) * kInH + ((i & 31) >> 1)] =
+                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
         }
         __syncthreads();
         const int64_t row = (int64_t)s * a.M + m;
@@ -157,7 +168,8 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
 #pragma unroll
             for (int i = 0; i < 6; ++i)
 #pragma unroll
-                for (int j = 0; j < 6; ++j) patch[i][j] = in[(2 * py + i) * 32 + 2 * px + j];
+                for (int j = 0; j < 6; ++j)
+                    patch[i][j] = in[(j & 1) * kInP + (2 * py + i) * kInH + px + (j >> 1)];
             float acc[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] = b1[c];
@@ -173,7 +185,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
                 }
             int8_t r;
             const float v = relu_pool4(acc[0], acc[1], acc[2], acc[3], r);
-            p1[o] = v;
+            p1[(px & 1) * kP1P + (c * 14 + py) * kP1H + (px >> 1)] = v;
             a.p1[row * kP1 + o] = v;
             a.r1[row * kP1 + o] = r;
         }
@@ -185,13 +197,13 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[q] = b2[k];
             for (int c = 0; c < 6; ++c) {
-                const float* pc = p1 + c * 196 + 2 * py * 14 + 2 * px;
+                const float* pc = p1 + (c * 14 + 2 * py) * kP1H + px;
                 const float* wk = w2 + k * 150 + c * 25;
                 float patch[6][6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i)
 #pragma unroll
-                    for (int j = 0; j < 6; ++j) patch[i][j] = pc[i * 14 + j];
+                    for (int j = 0; j < 6; ++j) patch[i][j] = pc[(j & 1) * kP1P + i * kP1H + (j >> 1)];
 #pragma unroll
                 for (int i = 0; i < 5; ++i)
 #pragma unroll
