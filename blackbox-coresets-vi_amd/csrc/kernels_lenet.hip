@@ -232,6 +232,18 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
 // padded image.  Per-(s, chunk) partial sums, reduced over chunks in fixed
 // order by lenet_conv_reduce_kernel: bitwise run-to-run reproducible.
 constexpr int kDA = 18;  // routed conv2 gradient plane, 10x10 plus a 4-wide zero border
+// The backward's LDS planes, laid out against ds_read_b32 bank conflicts (32
+// banks per 32-lane group): the routed conv2 plane split by column parity
+// (lanes read 2 columns apart) with 10-word rows, so the 5 patch rows of a
+// half-wave land on (nearly) disjoint banks; the padded image with 37-word
+// rows, so the 25 taps (i, j) of one conv1 weight row block sit on 25 banks.
+constexpr int kDAH = 10;              // half-columns per row of a parity plane
+constexpr int kDAK = kDA * kDAH;      // one output channel's parity plane
+constexpr int kDAP = 16 * kDAK;       // one parity plane (16 channels)
+constexpr int kBS = 37;               // padded-image row stride in the backward
+__device__ __forceinline__ int da2_at(int k, int y, int x) {  // bordered (y, x)
+    return (x & 1) * kDAP + k * kDAK + y * kDAH + (x >> 1);
+}
 
 // DU (outer backward): also d u = the transposed conv1 of the routed conv1
 // gradient (dense, zero-bordered LDS plane, 2x2 pixel blocks per thread) for
@@ -241,18 +253,18 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     __shared__ float w1[DU ? 150 : 1];
     __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
     __shared__ float w2[2400];
-    __shared__ float in[32 * 32];
+    __shared__ float in[32 * kBS];
     __shared__ float p1[kP1];
     __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
     __shared__ int off2[kX2];        // its conv2 position y * 14 + x (P1 plane offset)
-    __shared__ float da2[16 * kDA * kDA];
+    __shared__ float da2[2 * kDAP];  // [parity][k][y][x / 2]
     __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
-    __shared__ int off1[kP1];        // its conv1 position y * 32 + x (padded image)
+    __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
     __shared__ float red[160];
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
     for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
-    for (int i = tid; i < 16 * kDA * kDA; i += kConvThreads) da2[i] = 0.f;
+    for (int i = tid; i < 2 * kDAP; i += kConvThreads) da2[i] = 0.f;
     if (DU) {
         for (int i = tid; i < 150; i += kConvThreads) w1[i] = ws[i];
         for (int i = tid; i < 6 * 1024; i += kConvThreads) da1[i] = 0.f;
@@ -272,7 +284,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     // conv1: threads [0, 160) and [160, 320) split the 196 routed positions;
     // e < 150 weight (c, i, j), 150..155 bias
     const int half = tid / 160, e1 = tid % 160;
-    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * 32 + e1 % 5;
+    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * kBS + e1 % 5;
     const int cb1 = (e1 >= 150 && e1 < 156) ? e1 - 150 : c1;
     float acc1 = 0.f, accb2 = 0.f;
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
@@ -282,7 +294,8 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
         const float* um = a.u + (int64_t)m * 784;
         for (int i = tid; i < 1024; i += kConvThreads) {
             const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+            in[(i >> 5) * kBS + (i & 31)] =
+                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
         }
         for (int i = tid; i < kP1; i += kConvThreads) p1[i] = a.p1[row * kP1 + i];
         for (int o = tid; o < kX2; o += kConvThreads) {
@@ -293,7 +306,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
             const float g = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
             g2[o] = g;
             off2[o] = y * 14 + x;
-            if (r >= 0) da2[k * kDA * kDA + (y + 4) * kDA + x + 4] = g;
+            if (r >= 0) da2[da2_at(k, y + 4, x + 4)] = g;
         }
         __syncthreads();
         // conv2 weight gradient: dW2[k][c][i][j] += sum_p g2[k][p] P1[c][y_p + i][x_p + j]
@@ -316,12 +329,12 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
             const int c = tid / 49, yy = 2 * ((tid % 49) / 7), xx = 2 * (tid % 7);
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             for (int k = 0; k < 16; ++k) {
-                const float* q = da2 + k * kDA * kDA + yy * kDA + xx;
+                const float* q = da2 + k * kDAK + yy * kDAH + (xx >> 1);
                 float Q[6][6];
 #pragma unroll
                 for (int i = 0; i < 6; ++i)
 #pragma unroll
-                    for (int j = 0; j < 6; ++j) Q[i][j] = q[i * kDA + j];
+                    for (int j = 0; j < 6; ++j) Q[i][j] = q[(j & 1) * kDAP + i * kDAH + (j >> 1)];
                 const float* wk = w2 + k * 150 + c * 25;
 #pragma unroll
                 for (int i = 0; i < 5; ++i)
@@ -341,14 +354,14 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
                 const int r = a.r1[row * kP1 + o];
                 const int rr = r >= 0 ? r : 0;
                 g1[o] = r >= 0 ? acc[q] : 0.f;
-                off1[o] = (2 * yq + (rr >> 1)) * 32 + 2 * xq + (rr & 1);
+                off1[o] = (2 * yq + (rr >> 1)) * kBS + 2 * xq + (rr & 1);
             }
         }
         __syncthreads();
         // clear the routed entries of the dense plane for the next image
         for (int o = tid; o < kX2; o += kConvThreads) {
             const int k = o / 25, q = off2[o];
-            da2[k * kDA * kDA + (q / 14 + 4) * kDA + q % 14 + 4] = 0.f;
+            da2[da2_at(k, q / 14 + 4, q % 14 + 4)] = 0.f;
         }
         // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
         if (e1 < 156) {
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
         }
         if (DU && m < a.n_pseudo) {
             for (int o = tid; o < kP1; o += kConvThreads)
-                da1[(o / 196) * 1024 + off1[o] + 2 * 32 + 2] = g1[o];
+                da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = g1[o];
             __syncthreads();
             if (tid < 196) {
                 const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
@@ -397,7 +410,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
             }
             __syncthreads();
             for (int o = tid; o < kP1; o += kConvThreads)
-                da1[(o / 196) * 1024 + off1[o] + 2 * 32 + 2] = 0.f;
+                da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = 0.f;
         }
     }
     __syncthreads();
