@@ -241,6 +241,10 @@ constexpr int kDAH = 10;              // half-columns per row of a parity plane
 constexpr int kDAK = kDA * kDAH;      // one output channel's parity plane
 constexpr int kDAP = 16 * kDAK;       // one parity plane (16 channels)
 constexpr int kBS = 37;               // padded-image row stride in the backward
+// the pooled conv1 map P1 likewise: 37-word rows, channel planes 537 words
+// apart, so the 25 taps of a conv2 weight block and the next channel's first
+// taps fall on distinct banks
+constexpr int kP1S = 37, kP1C = 14 * kP1S + 19;
 __device__ __forceinline__ int da2_at(int k, int y, int x) {  // bordered (y, x)
     return (x & 1) * kDAP + k * kDAK + y * kDAH + (x >> 1);
 }
@@ -254,9 +258,9 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
     __shared__ float w2[2400];
     __shared__ float in[32 * kBS];
-    __shared__ float p1[kP1];
+    __shared__ float p1[6 * kP1C];   // [c][y * kP1S + x]
     __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
-    __shared__ int off2[kX2];        // its conv2 position y * 14 + x (P1 plane offset)
+    __shared__ int off2[kX2];        // its conv2 position y * kP1S + x (P1 plane offset)
     __shared__ float da2[2 * kDAP];  // [parity][k][y][x / 2]
     __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
     __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     for (int r = 0; r < kR2; ++r) {
         const int e = min(tid + r * kConvThreads, 2399);
         kb[r] = (e / 150) * 25;
-        pb[r] = ((e % 150) / 25) * 196 + ((e % 25) / 5) * 14 + e % 5;
+        pb[r] = ((e % 150) / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
     }
     float accw2[kR2];
 #pragma unroll
@@ -297,7 +301,8 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
             in[(i >> 5) * kBS + (i & 31)] =
                 (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
         }
-        for (int i = tid; i < kP1; i += kConvThreads) p1[i] = a.p1[row * kP1 + i];
+        for (int i = tid; i < kP1; i += kConvThreads)
+            p1[(i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14] = a.p1[row * kP1 + i];
         for (int o = tid; o < kX2; o += kConvThreads) {
             const int r = a.r2[row * kX2 + o];
             const int k = o / 25, py = (o % 25) / 5, px = o % 5;
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
             const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
             const float g = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
             g2[o] = g;
-            off2[o] = y * 14 + x;
+            off2[o] = y * kP1S + x;
             if (r >= 0) da2[da2_at(k, y + 4, x + 4)] = g;
         }
         __syncthreads();
@@ -361,7 +366,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
         // clear the routed entries of the dense plane for the next image
         for (int o = tid; o < kX2; o += kConvThreads) {
             const int k = o / 25, q = off2[o];
-            da2[da2_at(k, q / 14 + 4, q % 14 + 4)] = 0.f;
+            da2[da2_at(k, q / kP1S + 4, q % kP1S + 4)] = 0.f;
         }
         // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
         if (e1 < 156) {
