@@ -739,13 +739,15 @@ __global__ __launch_bounds__(kThreads) void lenet_loss_tan_kernel(int rows, int 
 
 // 2x2 block of a transposed 5x5 conv: acc[q] += sum_ij w[i][j] Q[4 - i + dy][4 - j + dx]
 // over a 6x6 patch at q (row stride ld) of a zero-bordered plane
+// PAR > 0: q is a parity-split plane (da2_at layout, odd columns PAR words on)
+template <int PAR = 0>
 __device__ __forceinline__ void convT_block(const float* q, int ld, const float* wk,
                                             float (&acc)[4]) {
     float Q[6][6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * ld + j];
+        for (int j = 0; j < 6; ++j) Q[i][j] = PAR ? q[(j & 1) * PAR + i * ld + (j >> 1)] : q[i * ld + j];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -759,6 +761,7 @@ __device__ __forceinline__ void convT_block(const float* q, int ld, const float*
 }
 
 // convT_block for two weight sets over one patch: acc_a += wa * Q, acc_b += wb * Q
+template <int PAR = 0>
 __device__ __forceinline__ void convT_block2(const float* q, int ld, const float* wa,
                                              const float* wb, float (&acc_a)[4],
                                              float (&acc_b)[4]) {
@@ -766,7 +769,7 @@ __device__ __forceinline__ void convT_block2(const float* q, int ld, const float
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * ld + j];
+        for (int j = 0; j < 6; ++j) Q[i][j] = PAR ? q[(j & 1) * PAR + i * ld + (j >> 1)] : q[i * ld + j];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -788,11 +791,11 @@ __device__ __forceinline__ void convT_block2(const float* q, int ld, const float
 // region serves the routed conv2 gradients (primal and tangent, 18x18 with a
 // 4-wide border) and then the routed conv1 gradients (32x32 with a 2-wide
 // border); it is re-zeroed per image.
-constexpr int kPlane = 2 * 6 * 1024;  // >= 2 * 16 * kDA * kDA
+constexpr int kPlane = 2 * 6 * 1024;  // >= 2 * 2 * kDAP (primal + tangent conv2 planes)
 __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArgs a) {
     __shared__ float w1[150], wd1[150], w2[2400], wd2[2400];
-    __shared__ float in[32 * 32];
-    __shared__ float p1[kP1], p1d[kP1];
+    __shared__ float in[32 * kBS];                  // the backward's layouts (see kDAH)
+    __shared__ float p1[6 * kP1C], p1d[6 * kP1C];
     __shared__ float g2[kX2], g2d[kX2];
     __shared__ int off2[kX2];
     __shared__ float g1[kP1], g1d[kP1];
@@ -810,17 +813,17 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     for (int r = 0; r < kR2; ++r) {
         const int e = min(tid + r * kConvThreads, 2399);
         kb[r] = (e / 150) * 25;
-        pb[r] = ((e % 150) / 25) * 196 + ((e % 25) / 5) * 14 + e % 5;
+        pb[r] = ((e % 150) / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
     }
     float accw2[kR2];
 #pragma unroll
     for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
     const int half = tid / 160, e1 = tid % 160;
-    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * 32 + e1 % 5;
+    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * kBS + e1 % 5;
     const int cb1 = (e1 >= 150 && e1 < 156) ? e1 - 150 : c1;
     float acc1 = 0.f, accb2 = 0.f;
     float* da2 = plane;
-    float* da2d = plane + 16 * kDA * kDA;
+    float* da2d = plane + 2 * kDAP;
     float* da1 = plane;
     float* da1d = plane + 6 * 1024;
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
@@ -830,11 +833,13 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
         const float* um = a.u + (int64_t)m * 784;
         for (int i = tid; i < 1024; i += kConvThreads) {
             const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+            in[(i >> 5) * kBS + (i & 31)] =
+                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
         }
         for (int i = tid; i < kP1; i += kConvThreads) {
-            p1[i] = a.p1[row * kP1 + i];
-            p1d[i] = a.p1d[row * kP1 + i];
+            const int q = (i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14;
+            p1[q] = a.p1[row * kP1 + i];
+            p1d[q] = a.p1d[row * kP1 + i];
         }
         for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
         __syncthreads();
@@ -847,9 +852,9 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
             const float gd = r >= 0 ? a.dx2d[row * kX2 + o] : 0.f;
             g2[o] = g;
             g2d[o] = gd;
-            off2[o] = y * 14 + x;
-            da2[k * kDA * kDA + (y + 4) * kDA + x + 4] = g;
-            da2d[k * kDA * kDA + (y + 4) * kDA + x + 4] = gd;
+            off2[o] = y * kP1S + x;
+            da2[da2_at(k, y + 4, x + 4)] = g;
+            da2d[da2_at(k, y + 4, x + 4)] = gd;
         }
         __syncthreads();
         // G_dot conv2: sum_p g2_dot P1 + g2 P1_dot at the routed windows
@@ -875,10 +880,10 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
             const int c = tid / 49, yy = 2 * ((tid % 49) / 7), xx = 2 * (tid % 7);
             float acc[4] = {0.f, 0.f, 0.f, 0.f}, accd[4] = {0.f, 0.f, 0.f, 0.f};
             for (int k = 0; k < 16; ++k) {
-                const int po = k * kDA * kDA + yy * kDA + xx;
-                convT_block2(da2 + po, kDA, w2 + k * 150 + c * 25, wd2 + k * 150 + c * 25, acc,
-                             accd);
-                convT_block(da2d + po, kDA, w2 + k * 150 + c * 25, accd);
+                const int po = k * kDAK + yy * kDAH + (xx >> 1);
+                convT_block2<kDAP>(da2 + po, kDAH, w2 + k * 150 + c * 25,
+                                   wd2 + k * 150 + c * 25, acc, accd);
+                convT_block<kDAP>(da2d + po, kDAH, w2 + k * 150 + c * 25, accd);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -888,7 +893,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
                 const int rr = r >= 0 ? r : 0;
                 g1[o] = r >= 0 ? acc[q] : 0.f;
                 g1d[o] = r >= 0 ? accd[q] : 0.f;
-                off1[o] = (2 * yq + (rr >> 1)) * 32 + 2 * xq + (rr & 1);
+                off1[o] = (2 * yq + (rr >> 1)) * kBS + 2 * xq + (rr & 1);
             }
         }
         __syncthreads();
@@ -910,7 +915,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
             for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
             __syncthreads();
             for (int o = tid; o < kP1; o += kConvThreads) {
-                const int q = (o / 196) * 1024 + off1[o] + 2 * 32 + 2;
+                const int q = (o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2;
                 da1[q] = g1[o];
                 da1d[q] = g1d[o];
             }
