@@ -261,7 +261,9 @@ int psvi_outer_elbo_grad(const psvi_plan* plan, int32_t n_pseudo, const float* x
                          size_t ws_bytes, void* stream);
 
 /* The backward half of psvi_outer_elbo_grad with caller-given per-sample
- * coefficients instead of the plan's own softmax over its S samples:
+ * coefficients instead of the plan's own softmax over its S samples
+ * (replaces the autograd backward of PSVI.psvi_elbo, psvi_classes.py:463-486,
+ * when the samples are split over ranks):
  *   coef = [rowcoef (S x 2): d loss / d pseudo_s, d loss / d data_s |
  *           ck (S): d loss / d nkl_s | sck (1): the sum of ck over these samples]
  * (floats, device).  For the sample-sharded outer objective:
