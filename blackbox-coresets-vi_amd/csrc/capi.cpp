@@ -834,7 +834,8 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
                       const int32_t* z_all, const float* w_all, const float* eps,
                       const float* params, double* loss_out, float* grad_params,
                       float* grad_u, float* grad_w, double* sample_out,
-                      const float* ext_coef, void* ws, size_t ws_bytes, void* stream) {
+                      const float* ext_coef, void* ws, size_t ws_bytes, void* stream,
+                      int ablated = 0) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "the outer objective needs world == 1");
@@ -872,7 +873,7 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
     if (!ext_coef) {
         // 2. per-sample terms, softmax over samples, loss, backward coefficients
         HIP_TRY(launch_outer_combine(*p, n_pseudo, params, w_all, o.nll, o.stats, loss_out,
-                                     o.rowcoef, o.ck, o.sck, grad_w, sample_out, st));
+                                     o.rowcoef, o.ck, o.sck, grad_w, sample_out, ablated, st));
     } else {
         const size_t S = p->d.S;
         HIP_TRY(hipMemcpyAsync(o.rowcoef, ext_coef, sizeof(float) * 2 * S,
@@ -920,6 +921,17 @@ int psvi_outer_elbo_grad(const psvi_plan* p, int32_t n_pseudo, const float* x_al
                          size_t ws_bytes, void* stream) {
     return outer_impl(p, n_pseudo, x_all, z_all, w_all, eps, params, loss_out, grad_params,
                       grad_u, grad_w, sample_out, nullptr, ws, ws_bytes, stream);
+}
+
+int psvi_outer_ablated_elbo_grad(const psvi_plan* p, const float* x_all,
+                                 const int32_t* z_all, const float* w_all, const float* eps,
+                                 const float* params, double* loss_out, float* grad_params,
+                                 double* sample_out, void* ws, size_t ws_bytes, void* stream) {
+    if (p && p->family == PSVI_FAMILY_FULLCOV)
+        return fail(PSVI_EUNSUP, "PSVI_Ablated's sampled KL sums VILinear layers only; a "
+                                 "full-covariance model has none (the reference fails there)");
+    return outer_impl(p, 0, x_all, z_all, w_all, eps, params, loss_out, grad_params, nullptr,
+                      nullptr, sample_out, nullptr, ws, ws_bytes, stream, 1);
 }
 
 int psvi_outer_elbo_grad_coef(const psvi_plan* p, int32_t n_pseudo, const float* x_all,

@@ -34,6 +34,7 @@ struct OuterArgs {
     int64_t poff[kMaxL], eoff[kMaxL];
     int din[kMaxL], dout[kMaxL];
     float s0;
+    int ablated;           // PSVI_Ablated.psvi_elbo: mean data - mean nkl (no softmax)
     const float* params;
     const float* eps;
     const float* x;        // full-cov: x_shard [S][n_tot] (world 1)
@@ -144,8 +145,8 @@ __global__ __launch_bounds__(1024) void outer_combine_kernel(OuterArgs a) {
         ds = wave_sum_d(ds);
         if (lane == 0) {
             const double nkl = -a.stats[2 * s] * inv2 - nlog + 0.5 * a.stats[2 * s + 1] + sl;
-            lw[s] = -ps + nkl;
-            av[s] = ds - ps;
+            lw[s] = a.ablated ? nkl : -ps + nkl;
+            av[s] = a.ablated ? ds : ds - ps;
             if (a.sample_out) {
                 a.sample_out[4 * s] = ps;
                 a.sample_out[4 * s + 1] = ds;
@@ -154,6 +155,26 @@ __global__ __launch_bounds__(1024) void outer_combine_kernel(OuterArgs a) {
         }
     }
     __syncthreads();
+    if (a.ablated) {
+        // PSVI_Ablated.psvi_elbo (psvi_classes.py:1397-1408): data rows only,
+        // loss = mean_s data_s - mean_s nkl_s; constant coefficients
+        double dsum = 0.0, ksum = 0.0;
+        for (int s = tid; s < a.S; s += nthr) {
+            dsum += av[s];
+            ksum += lw[s];
+            a.rowcoef[2 * s] = 0.f;
+            a.rowcoef[2 * s + 1] = 1.f / a.S;
+            a.ck[s] = -1.f / a.S;
+            if (a.sample_out) a.sample_out[4 * s + 3] = 1.0 / a.S;
+        }
+        dsum = block_sum_all(dsum, red);
+        ksum = block_sum_all(ksum, red);
+        if (tid == 0) {
+            a.loss[0] = (dsum - ksum) / a.S;
+            a.sck[0] = -1.f;
+        }
+        return;
+    }
     double mx = -INFINITY, sm = 0.0;
     for (int s = tid; s < a.S; s += nthr) mx = fmax(mx, lw[s]);
     mx = block_max_all(mx, red);
@@ -365,10 +386,12 @@ hipError_t launch_outer_stats(const psvi_plan& p, const float* params, const flo
 hipError_t launch_outer_combine(const psvi_plan& p, int n_pseudo, const float* params,
                                 const float* w, const float* nll, const double* stats,
                                 double* loss, float* rowcoef, float* ck, float* sck,
-                                float* grad_w, double* sample_out, hipStream_t st) {
+                                float* grad_w, double* sample_out, int ablated,
+                                hipStream_t st) {
     if (p.d.S > kOuterMaxS) return hipErrorInvalidValue;
     OuterArgs a{};
     fill(p, a);
+    a.ablated = ablated;
     a.n_pseudo = n_pseudo;
     a.params = params;
     a.w = w;

@@ -304,7 +304,8 @@ hipError_t launch_outer_stats(const psvi_plan& p, const float* params, const flo
 hipError_t launch_outer_combine(const psvi_plan& p, int n_pseudo, const float* params,
                                 const float* w, const float* nll, const double* stats,
                                 double* loss, float* rowcoef, float* ck, float* sck,
-                                float* grad_w, double* sample_out, hipStream_t st);
+                                float* grad_w, double* sample_out, int ablated,
+                                hipStream_t st);
 hipError_t launch_eval(const psvi_plan& p, int n_pseudo, const float* params, const float* w,
                        const int32_t* z, const float* nll, const double* stats,
                        const float* prob, int correction, float* W, float* probs_out,

@@ -41,9 +41,23 @@ What runs where
     back, ``psvi_adam_adjoint`` and one ``psvi_hvp`` with its mixed products;
     then the u / v Adam steps.
 
-Not on the HIP path: evaluation and data plumbing.  Those entry points raise NotImplementedError instead of
-silently running elsewhere, and ``inner_elbo`` treats u and v as constants (no
-gradient flows to them).
+  * ``PSVI.evaluate`` / ``pred_on_grid`` (psvi_classes.py:1031-1175): the
+    importance-weighted predictive, one ``psvi_evaluate`` per test batch.
+
+  * The plugin variants (psvi_classes.py:1344-1884) differ only in what the
+    outer step learns and which outer objective it differentiates:
+    ``PSVIAV`` / ``PSVIAFixedU`` add alpha (w = N exp(alpha) softmax(v)) with
+    its own Adam ``optim_alpha``; ``PSVIFixedU`` / ``PSVIAFixedU`` freeze u;
+    ``PSVI_Ablated`` / ``PSVI_No_IW`` use the ablated outer objective
+    (``psvi_outer_ablated_elbo_grad``: mean data NLL minus mean sampled KL, no
+    importance weights); ``PSVI_No_IW`` trains single-sample, where the
+    reference's inner objective scores every pseudo row against every pseudo
+    label (its 2-d logits broadcast in Categorical.log_prob) -- reproduced as
+    the standard objective over M*C expanded rows.
+
+``inner_elbo`` treats u and v as constants (no gradient flows to them); the
+trainers carry the hypergradients of u, v and alpha themselves.  Soft labels
+(``learn_z``) and the truncated nested step raise NotImplementedError.
 
 There is no CPU fallback: a missing libpsvi_hip.so or GPU raises.
 """
@@ -59,11 +73,6 @@ from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
            "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
-
-_OUTER = ("differentiates through the unrolled inner loop (reverse through T Adam steps); "
-          "that is the next row of the hot-path scope (SURVEY.md 8(f)); trainer 'hyper' "
-          "(implicit hypergradient) runs on HIP")
-
 
 class HipInnerELBO(torch.autograd.Function):
     """Negative inner ELBO and its parameter gradient in one HIP call.
@@ -108,10 +117,38 @@ class HipOuterELBO(torch.autograd.Function):
                 None, None, None, None, None)
 
 
+class HipAblatedELBO(torch.autograd.Function):
+    """PSVI_Ablated's outer objective (mean data NLL minus mean sampled KL over
+    the data batch) and its parameter gradient in one HIP call
+    (psvi_outer_ablated_elbo_grad).  No pseudopoint enters it."""
+
+    @staticmethod
+    def forward(ctx, pvec, plan, xb, yb, w_data, eps):
+        out = plan.outer_ablated_elbo_grad(xb, yb, w_data, eps, pvec.detach().contiguous())
+        ctx.save_for_backward(out["grad"])
+        ctx.ptype = pvec.dtype
+        return out["loss"].to(pvec.dtype).reshape(())
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        (gp,) = ctx.saved_tensors
+        return (gout * gp).to(ctx.ptype), None, None, None, None, None
+
+
 class PSVI:
     """Pseudodata (coreset) VI with fixed rescaled coefficients v = 1/M
     (psvi_classes.py:83).  Keyword names follow the reference; arguments that
-    only concern the outer loop / data plumbing are accepted and ignored."""
+    only concern the outer loop / data plumbing are accepted and ignored.
+
+    Variant switches (set by the subclasses): ``_learn_u`` (False: u frozen,
+    PSVIFixedU / PSVIAFixedU), ``_outer_mode`` ("iw" PSVI.psvi_elbo, "ablated"
+    PSVI_Ablated.psvi_elbo), ``_noiw`` (PSVI_No_IW's single-sample inner
+    objective)."""
+
+    _learn_u = True
+    _outer_mode = "iw"
+    _noiw = False
 
     def __init__(self, u=None, z=None, N=None, D=None, model=None, num_pseudo=None, seed=0,
                  mc_samples=None, learn_v=False, f=lambda *x: x[0], distr_fn=categorical_fn,
@@ -144,6 +181,7 @@ class PSVI:
         self.register_elbos, self.elbos = register_elbos, []
         self.inner_it, self.log_every, self.lr0net = inner_it, log_every, lr0net
         self.seed = seed
+        self.lr0alpha = kwargs.get("lr0alpha", 1e-3)
         self.compute_weights_entropy = compute_weights_entropy
         self.results = {}
         with torch.no_grad():
@@ -151,6 +189,7 @@ class PSVI:
         self.v.requires_grad_(self.learn_v)
         self._plans = {}
         self._eps_offset = 0
+        self._labels_ok = None
 
     # ------------------------------------------------------------ helpers
     def coreset_weights(self):
@@ -158,27 +197,79 @@ class PSVI:
         with torch.no_grad():
             return (self.N * self.f(self.v, 0)).to(torch.float32).contiguous()
 
+    def _noiw_rows(self, model):
+        """PSVI_No_IW trains with one sample; a single-sample mean-field model
+        gives 2-d logits, which inner_elbo unsqueezes to (M, 1, C)
+        (psvi_classes.py:492-493), so Categorical.log_prob(z) broadcasts to
+        (M, M): every pseudo row is scored against every pseudo label."""
+        if not self._noiw:
+            return False
+        fam, _, _, S = model_spec(model)
+        if S != 1:
+            return False
+        if fam != "meanfield":
+            raise NotImplementedError("PSVI_No_IW runs mean-field models on the HIP path "
+                                      "(the reference's ablated outer objective fails on "
+                                      "full-covariance ones)")
+        return True
+
     def _plan(self, model):
         fam, layers, prior_sd, S = model_spec(model)
         if self.mc_samples is not None and S != self.mc_samples:
             raise ValueError(f"model mc_samples {S} != PSVI mc_samples {self.mc_samples}")
         M = int(self.u.shape[0])
+        if self._noiw_rows(model):
+            M *= layers[-1][1]
         key = (fam, tuple(layers), S, M, prior_sd)
         if key not in self._plans:
             self._plans[key] = InnerLoopPlan(fam, layers, S, M, prior_sd=prior_sd)
         return self._plans[key]
 
-    def _data(self, plan):
-        M, D = plan.M, plan.in_features
-        u = self.u.detach().to(self.device, torch.float32).reshape(M, D).contiguous()
-        z = self.z.detach().to(self.device)
+    def _check_labels(self, z, C):
+        """Class ids in [0, C) -- validated once per label tensor version (a
+        device-to-host read; not on every objective call)."""
+        key = (id(z), getattr(z, "_version", 0), C)
+        if self._labels_ok == key:
+            return
         if z.is_floating_point() and not torch.equal(z, z.round()):
             raise ValueError("z must hold class ids (learn_z is not supported)")
-        z = z.to(torch.int32).contiguous()
-        C = plan.layers[-1][1]
-        if int(z.min()) < 0 or int(z.max()) >= C:
+        if z.numel() and (int(z.min()) < 0 or int(z.max()) >= C):
             raise ValueError(f"class ids must lie in [0, {C})")
-        return u, z, self.coreset_weights()
+        self._labels_ok = key
+
+    @staticmethod
+    def _batch_labels(y, C):
+        """Minibatch labels as int32 on the device, without a host read: out-of-
+        range ids are clamped for memory safety (the loaders hand out class ids)."""
+        return y.reshape(-1).to(torch.int32).clamp_(0, C - 1).contiguous()
+
+    def _data(self, plan):
+        """(u, z, w) of the inner objective's rows: the pseudopoints, or for
+        PSVI_No_IW's single-sample objective the M*C expanded rows (u_i, class
+        c, W_c = sum of w_j over the pseudopoints labelled c)."""
+        C = plan.layers[-1][1]
+        M0 = int(self.u.shape[0])
+        D = plan.in_features
+        self._check_labels(self.z, C)
+        u = self.u.detach().to(self.device, torch.float32).reshape(M0, D).contiguous()
+        z = self.z.detach().to(self.device).to(torch.int32).contiguous()
+        w = self.coreset_weights()
+        if plan.M == M0:
+            return u, z, w
+        Wc = torch.zeros(C, dtype=torch.float32, device=self.device).index_add_(0, z.long(), w)
+        return (u.repeat_interleave(C, 0).contiguous(),
+                torch.arange(C, dtype=torch.int32, device=self.device).repeat(M0).contiguous(),
+                Wc.repeat(M0).contiguous())
+
+    def _fold(self, plan, du, dw):
+        """Row gradients of _data's rows back onto the pseudopoints."""
+        M0 = int(self.u.shape[0])
+        if plan.M == M0:
+            return du, dw
+        C = plan.layers[-1][1]
+        z = self.z.detach().to(self.device).long()
+        return (du.reshape(M0, C, -1).sum(1),
+                dw.reshape(M0, C).sum(0)[z])
 
     def _draw_eps(self, plan):
         eps = torch.empty(plan.eps_count, device=self.device)
@@ -252,36 +343,38 @@ class PSVI:
         Differentiable (first order) w.r.t. the parameters (or ``params`` with
         hyperopt=True), u, and v / alpha through N f(v).  ``eps``: the
         library's eps layout (``eps_count`` floats) to replay a draw."""
-        assert self.mc_samples is None or self.mc_samples > 1  # psvi_classes.py:449
         model = self.model if model is None else model
         fam, layers, prior_sd, S = model_spec(model)
-        if S < 2:
-            raise ValueError("psvi_elbo needs mc_samples > 1 (psvi_classes.py:449)")
-        Mu = int(self.u.shape[0])
-        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
-        Nx = int(xb.shape[0])
-        key = ("outer", fam, tuple(layers), S, Mu + Nx, prior_sd)
-        if key not in self._plans:
-            self._plans[key] = InnerLoopPlan(fam, layers, S, Mu + Nx, prior_sd=prior_sd)
-        plan = self._plans[key]
+        C = layers[-1][1]
         plist = list(params) if (hyperopt and params is not None) else list(model.parameters())
         pvec = nn.utils.parameters_to_vector(plist)
+        xb, yb, w_data = self._outer_rows(xbatch, ybatch, C)
+        Nx = int(xb.shape[0])
+        if self._outer_mode == "ablated":
+            # PSVI_Ablated.psvi_elbo (psvi_classes.py:1397-1408): model(xbatch) only
+            if fam == "fullcov":
+                raise AttributeError("'int' object has no attribute 'mean': PSVI_Ablated's "
+                                     "sampled KL sums VILinear modules only, a full-covariance "
+                                     "model has none (psvi_classes.py:1403-1408)")
+            plan = self._outer_plan(model, Nx, n_pseudo=0)
+            if pvec.numel() != plan.param_count:
+                raise ValueError(f"{pvec.numel()} parameters, plan expects {plan.param_count}")
+            if eps is None:
+                eps = self._draw_eps(plan)
+            return HipAblatedELBO.apply(pvec, plan, xb, yb, w_data, eps)
+        assert self.mc_samples is None or self.mc_samples > 1  # psvi_classes.py:449
+        if S < 2:
+            raise ValueError("psvi_elbo needs mc_samples > 1 (psvi_classes.py:449)")
+        plan = self._outer_plan(model, Nx)
         if pvec.numel() != plan.param_count:
             raise ValueError(f"{pvec.numel()} parameters, plan expects {plan.param_count}")
-        z = torch.cat([self.z.detach().to(self.device).reshape(-1),
-                       ybatch.detach().to(self.device).reshape(-1)])
-        if z.is_floating_point() and not torch.equal(z, z.round()):
-            raise ValueError("labels must hold class ids (learn_z is not supported)")
-        z_all = z.to(torch.int32).contiguous()
-        C = layers[-1][1]
-        if int(z_all.min()) < 0 or int(z_all.max()) >= C:
-            raise ValueError(f"class ids must lie in [0, {C})")
+        self._check_labels(self.z, C)
+        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1).to(torch.int32),
+                           yb]).contiguous()
         wp = (self.N * self.f(self.v, 0)).to(torch.float32).reshape(-1)
-        w_data = torch.full((Nx,), float(self.N) / max(Nx, 1), device=self.device)
         if eps is None:
             eps = self._draw_eps(plan)
-        loss = HipOuterELBO.apply(pvec, self.u, wp, plan, xb, z_all, w_data, eps)
-        return loss
+        return HipOuterELBO.apply(pvec, self.u, wp, plan, xb, z_all, w_data, eps)
 
     def setup_optimizers(self, lr0net=1e-3, lr0u=1e-3, lr0v=1e-2, lr0joint=1e-3,
                          trainer="hyper"):
@@ -293,6 +386,8 @@ class PSVI:
         self.optim_u = torch.optim.Adam([self.u], lr0u)
         if self.learn_v:
             self.optim_v = torch.optim.Adam([self.v], lr0v)
+        if self._alpha() is not None:   # PSVIAV / PSVIAFixedU (psvi_classes.py:1489, 1761)
+            self.optim_alpha = torch.optim.Adam([self.alpha], self.lr0alpha)
         if trainer == "joint":
             vp = list(self.model.parameters()) + [self.u] + ([self.v] if self.learn_v else [])
             self.optim = torch.optim.Adam(vp, lr0joint)
@@ -376,34 +471,122 @@ class PSVI:
         return probs
 
     # ------------------------------------------------------- second order
-    def _outer_plan(self, model, Nx):
+    def _outer_plan(self, model, Nx, n_pseudo=None):
         fam, layers, prior_sd, S = model_spec(model)
-        Mu = int(self.u.shape[0])
+        Mu = int(self.u.shape[0]) if n_pseudo is None else int(n_pseudo)
         key = ("outer", fam, tuple(layers), S, Mu + Nx, prior_sd)
         if key not in self._plans:
             self._plans[key] = InnerLoopPlan(fam, layers, S, Mu + Nx, prior_sd=prior_sd)
         return self._plans[key]
 
+    def _alpha(self):
+        return getattr(self, "alpha", None)
+
     def _chain_w(self, dw):
-        """d/dv of a linear function of w = N f(v) with coefficients dw."""
+        """(d/dv, d/dalpha) of a linear function of w = N f(v) with coefficients
+        dw; d/dalpha is None without alpha (PSVIAV / PSVIAFixedU have it)."""
+        alpha = self._alpha()
         with torch.enable_grad():
-            wp = self.N * self.f(self.v, 0)
-            (gv,) = torch.autograd.grad(wp, self.v, grad_outputs=dw.to(wp.dtype).reshape(wp.shape))
-        return gv
+            v = self.v.detach().requires_grad_(True)
+            hp = [v]
+            if alpha is not None:
+                a = alpha.detach().requires_grad_(True)
+                hp.append(a)
+                wp = self.N * torch.exp(a) * torch.softmax(v, 0)
+            else:
+                wp = self.N * self.f(v, 0)
+            gs = torch.autograd.grad(wp, hp, grad_outputs=dw.to(wp.dtype).reshape(wp.shape))
+        return gs[0], (gs[1] if alpha is not None else None)
+
+    @staticmethod
+    def _add_grad(t, g):
+        g = g.reshape(t.shape).to(t.dtype)
+        if t.grad is None:
+            t.grad = g.clone()
+        else:
+            t.grad += g
+
+    def _hparam_steps(self, u_grad, w_grad):
+        """Accumulate the hypergradients and step the outer optimisers: optim_u
+        (unless u is frozen), optim_v (learn_v; clamped at 0 unless
+        parameterised) and optim_alpha (psvi_classes.py:585-591, 676-681,
+        1576-1579, 1610-1612, 1650-1651, 1843-1845, 1873-1875)."""
+        if self._learn_u:
+            self._add_grad(self.u, u_grad)
+            self.optim_u.step()
+        if self.learn_v:
+            gv, ga = self._chain_w(w_grad)
+            self._add_grad(self.v, gv)
+            if ga is not None:
+                self._add_grad(self.alpha, ga)
+            self.optim_v.step()
+            if ga is not None:
+                self.optim_alpha.step()
+            if not getattr(self, "parameterised", False):
+                with torch.no_grad():
+                    torch.clamp_(self.v, min=0.0)
+
+    def _zero_hparam_grads(self):
+        if self._learn_u:
+            self.optim_u.zero_grad()
+        else:
+            self.u.requires_grad_(False)        # psvi_classes.py:1632, 1664, 1821, 1863
+        if self.learn_v:
+            self.optim_v.zero_grad()
+        if self._alpha() is not None and hasattr(self, "optim_alpha"):
+            self.optim_alpha.zero_grad()
+
+    def _outer_rows(self, xbatch, ybatch, C):
+        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
+        yb = self._batch_labels(ybatch.detach().to(self.device), C)
+        Nx = int(xb.shape[0])
+        return xb.contiguous(), yb, torch.full((Nx,), float(self.N) / max(Nx, 1),
+                                               device=self.device)
+
+    def _outer_fn(self, model, xbatch, ybatch, u, z, params):
+        """(plan, f(u, w, eps, grads) -> dict(loss, grad, grad_u, grad_w)) of this
+        class's outer objective at fixed parameters (float32 device tensors)."""
+        fam, layers, _, _ = model_spec(model)
+        xb, yb, w_data = self._outer_rows(xbatch, ybatch, layers[-1][1])
+        Nx = int(xb.shape[0])
+        if self._outer_mode == "ablated":
+            if fam == "fullcov":
+                raise AttributeError("'int' object has no attribute 'mean': PSVI_Ablated's "
+                                     "sampled KL sums VILinear modules only, a full-covariance "
+                                     "model has none (psvi_classes.py:1403-1408)")
+            oplan = self._outer_plan(model, Nx, n_pseudo=0)
+
+            def f(uu, ww, eps, grads=True):
+                o = oplan.outer_ablated_elbo_grad(xb, yb, w_data, eps, params, grad=grads)
+                if grads:
+                    o["grad_u"] = torch.zeros_like(uu)
+                    o["grad_w"] = torch.zeros(uu.shape[0], device=uu.device)
+                return o
+            return oplan, f
+        oplan = self._outer_plan(model, Nx)
+        z_all = torch.cat([z, yb]).contiguous()
+
+        def f(uu, ww, eps, grads=True):
+            x_all = torch.cat([uu.detach().reshape(uu.shape[0], -1), xb]).contiguous()
+            w_all = torch.cat([ww.detach().to(torch.float32), w_data]).contiguous()
+            return oplan.outer_elbo_grad(int(uu.shape[0]), x_all, z_all, w_all, eps, params,
+                                         grad=grads, grad_u=grads, grad_w=grads)
+        return oplan, f
 
     def hyper_step(self, xbatch, ybatch, T=50, inner_opt_class=None, K=30, linsys_lr=1e-4,
                    hypergrad_approx="CG_normaleq", eps_inner=None, eps_outer=None, **kwargs):
         """psvi_classes.py:602-687 with hypergrad's CG_normaleq
         (hypergradients.py:199-244, CG_torch.py:9-45): T = self.inner_it
         first-order inner steps (hypergrad adam_step, step count 1..T) from the
-        model's parameters, then the implicit hypergradient of u (and v) from
-        K conjugate-gradient iterations on the normal equations of
-        fp_map(p) = p - linsys_lr * grad_p inner, the u / v Adam steps, and
-        the outer loss at the new (u, v) -- returned as a float; the final
-        parameters are written into the model.  ``eps_inner`` /
-        ``eps_outer``: optional sequences of draws (library eps layout) in the
-        reference's call order, to replay; default: this instance's Philox
-        stream."""
+        model's parameters, then the implicit hypergradient of the hparams --
+        u (unless frozen), v (learn_v) and alpha (PSVIAV / PSVIAFixedU,
+        1504-1581, 1774-1850) -- from K conjugate-gradient iterations on the
+        normal equations of fp_map(p) = p - linsys_lr * grad_p inner, their
+        Adam steps, and the outer loss at the new hparams -- returned as a
+        float; the final parameters are written into the model.
+        ``eps_inner`` / ``eps_outer``: optional sequences of draws (library eps
+        layout) in the reference's call order, to replay; default: this
+        instance's Philox stream."""
         if hypergrad_approx not in ("CG_normaleq", "fixed_point"):
             raise NotImplementedError(f"hypergrad_approx={hypergrad_approx!r}: the reference's "
                                       "hyper_step offers CG_normaleq and fixed_point")
@@ -412,9 +595,7 @@ class PSVI:
         T = self.inner_it
         lr_net = self.optim_net.param_groups[0]["lr"]
         model = self.model
-        self.optim_u.zero_grad()
-        if self.learn_v:
-            self.optim_v.zero_grad()
+        self._zero_hparam_grads()
         plan = self._plan(model)
         u, z, w = self._data(plan)
         it_in = iter(eps_inner) if eps_inner is not None else None
@@ -422,13 +603,6 @@ class PSVI:
 
         def draw_inner():
             return next(it_in) if it_in is not None else self._draw_eps(plan)
-
-        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
-        Nx = int(xb.shape[0])
-        oplan = self._outer_plan(model, Nx)
-
-        def draw_outer():
-            return next(it_out) if it_out is not None else self._draw_eps(oplan)
 
         # 1. the inner problem: T first-order steps (trainer hyper: hypergrad adam_step)
         plist = list(model.parameters())
@@ -445,18 +619,15 @@ class PSVI:
             for t in range(T):
                 plan.inner_step(u, z, w, draw_inner(), params, m, v2, step=t + 1, lr=lr_net,
                                 kind="hypergrad", ws=ws)
-        # 2. CG_normaleq
-        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1),
-                           ybatch.detach().to(self.device).reshape(-1)]).to(torch.int32)
-        w_data = torch.full((Nx,), float(self.N) / max(Nx, 1), device=self.device)
+        # 2. the outer objective's direct gradients, then CG_normaleq / fixed_point
+        u0 = self.u.detach().to(self.device, torch.float32).reshape(self.u.shape[0], -1)
+        z0 = self.z.detach().to(self.device).reshape(-1).to(torch.int32)
+        oplan, outer = self._outer_fn(model, xbatch, ybatch, u0, z0, params)
 
-        def outer(uu, ww, eps, grads=True):
-            x_all = torch.cat([uu.detach().reshape(uu.shape[0], -1), xb]).contiguous()
-            w_all = torch.cat([ww.detach().to(torch.float32), w_data]).contiguous()
-            return oplan.outer_elbo_grad(int(uu.shape[0]), x_all, z_all.contiguous(), w_all, eps,
-                                         params, grad=grads, grad_u=grads, grad_w=grads)
+        def draw_outer():
+            return next(it_out) if it_out is not None else self._draw_eps(oplan)
 
-        o = outer(u, w, draw_outer())
+        o = outer(u0, self.coreset_weights(), draw_outer())
         g_w = o["grad"].to(torch.float64)
         lr = float(linsys_lr)
         hws = torch.empty(plan.hvp_ws_bytes, dtype=torch.uint8, device=params.device)
@@ -464,6 +635,8 @@ class PSVI:
         def hvp(e, x, mixed=False):
             hv, du, dw = plan.hvp(u, z, w, e, params, x.to(torch.float32).contiguous(),
                                   mixed=mixed, ws=hws)
+            if mixed:
+                du, dw = self._fold(plan, du, dw)
             return hv.to(torch.float64), du, dw
 
         if hypergrad_approx == "fixed_point":
@@ -479,7 +652,16 @@ class PSVI:
             eA = self._cg_normaleq(hvp, draw_inner, g_w, lr, K)
             xk = self._cg_x
         _, du, dw = hvp(eA, xk, mixed=True)     # torch_grad(w_mapped, hparams, vs)
-        return self._hyper_finish(o, du, dw, lr, plan, outer, draw_outer, params, plist)
+        # 3. hypergradient = -lr * mixed products + the outer objective's direct gradients
+        u_grad = (-lr * du.to(torch.float64) + o["grad_u"].to(torch.float64)).to(self.u.dtype)
+        w_grad = -lr * dw.to(torch.float64) + o["grad_w"].to(torch.float64)
+        self._hparam_steps(u_grad, w_grad)
+        # 4. the outer loss at the new hparams, and the inner solution into the model
+        u1 = self.u.detach().to(self.device, torch.float32).reshape(self.u.shape[0], -1)
+        ll = outer(u1, self.coreset_weights(), draw_outer(), grads=False)["loss"]
+        with torch.no_grad():
+            nn.utils.vector_to_parameters(params.to(plist[0].dtype), plist)
+        return float(ll.item())
 
     def _cg_normaleq(self, hvp, draw_inner, g_w, lr, K):
         """CG_normaleq's linear solve (hypergradients.py:199-244, CG_torch.py:9-45);
@@ -512,58 +694,29 @@ class PSVI:
         self._cg_x = xk
         return eA
 
-    def _hyper_finish(self, o, du, dw, lr, plan, outer, draw_outer, params, plist):
-        """hypergradient = -lr * mixed products + the outer objective's direct
-        gradients; u / v Adam steps; outer loss at the new (u, v)."""
-        u_grad = (-lr * du.to(torch.float64) + o["grad_u"].to(torch.float64)).to(self.u.dtype)
-        if self.u.grad is None:
-            self.u.grad = torch.zeros_like(self.u)
-        self.u.grad += u_grad.reshape(self.u.shape)
-        if self.learn_v:
-            dwt = (-lr * dw.to(torch.float64) + o["grad_w"].to(torch.float64))
-            v_grad = self._chain_w(dwt)
-            if self.v.grad is None:
-                self.v.grad = torch.zeros_like(self.v)
-            self.v.grad += v_grad
-        self.optim_u.step()
-        if self.learn_v:
-            self.optim_v.step()
-            if not getattr(self, "parameterised", False):
-                with torch.no_grad():
-                    torch.clamp_(self.v, min=0.0)
-        # 3. the outer loss at the new (u, v), and the inner solution into the model
-        u2, _, w2 = self._data(plan)
-        ll = outer(u2, w2, draw_outer(), grads=False)["loss"]
-        with torch.no_grad():
-            nn.utils.vector_to_parameters(params.to(plist[0].dtype), plist)
-        return float(ll.item())
-
     def nested_step(self, xbatch, ybatch, truncated=False, K=5, eps_inner=None, eps_outer=None):
-        """psvi_classes.py:541-600: T = self.inner_it higher-Adam steps on the
-        inner objective from the model's parameters with a fresh Adam state,
-        the outer objective at the result, its gradient w.r.t. u (and v)
-        through the unrolled steps, the u / v Adam steps; the final parameters
-        are written into the model.  Returns the outer loss (0-dim tensor).
-        ``eps_inner`` (T draws) / ``eps_outer`` (1): optional replay of the
-        reference's draws; default this instance's Philox stream."""
+        """psvi_classes.py:541-600 (and the variants' overrides, 1583-1620,
+        1631-1657, 1852-1884): T = self.inner_it higher-Adam steps on the inner
+        objective from the model's parameters with a fresh Adam state, the
+        outer objective at the result, its gradient w.r.t. the hparams (u
+        unless frozen, v, alpha) through the unrolled steps, their Adam steps;
+        the final parameters are written into the model.  Returns the outer
+        loss (0-dim tensor).  ``eps_inner`` (T draws) / ``eps_outer`` (1):
+        optional replay of the reference's draws; default this instance's
+        Philox stream."""
         if truncated:
             raise NotImplementedError("truncated nested_step (torch.optim.Adam warm start) is "
                                       "not on the HIP path")
         if self.learn_z:
             raise NotImplementedError("soft labels (learn_z) are not on the HIP path")
-        self.optim_u.zero_grad()
+        self._zero_hparam_grads()
         self.optim_net.zero_grad()
-        if self.learn_v:
-            self.optim_v.zero_grad()
         model = self.model
         T = int(self.inner_it)
         lr_net = self.optim_net.param_groups[0]["lr"]
         plan = self._plan(model)
         u, z, w = self._data(plan)
         it_in = iter(eps_inner) if eps_inner is not None else None
-        xb = xbatch.detach().to(self.device, torch.float32).reshape(xbatch.shape[0], -1)
-        Nx = int(xb.shape[0])
-        oplan = self._outer_plan(model, Nx)
         plist = list(model.parameters())
         with torch.no_grad():
             p = nn.utils.parameters_to_vector(plist).detach().to(torch.float32).clone()
@@ -580,13 +733,11 @@ class PSVI:
             hist.append((p_prev, m.clone(), v2.clone(), g, e))
             elbos.append(elbo)
         # the outer objective at the inner solution, and its direct gradients
-        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1),
-                           ybatch.detach().to(self.device).reshape(-1)]).to(torch.int32)
-        w_data = torch.full((Nx,), float(self.N) / max(Nx, 1), device=self.device)
+        u0 = self.u.detach().to(self.device, torch.float32).reshape(self.u.shape[0], -1)
+        z0 = self.z.detach().to(self.device).reshape(-1).to(torch.int32)
+        oplan, outer = self._outer_fn(model, xbatch, ybatch, u0, z0, p)
         eo = next(iter(eps_outer)) if eps_outer is not None else self._draw_eps(oplan)
-        x_all = torch.cat([u, xb]).contiguous()
-        w_all = torch.cat([w, w_data]).contiguous()
-        o = oplan.outer_elbo_grad(int(u.shape[0]), x_all, z_all.contiguous(), w_all, eo, p)
+        o = outer(u0, self.coreset_weights(), eo)
         if self.register_elbos:
             host = torch.cat(elbos).cpu()
             for t in range(0, T, self.log_every):
@@ -604,21 +755,11 @@ class PSVI:
             p_prev, mt, vt, gt, e = hist[t]
             adam_adjoint_(lt, lm, lv, mt, vt, gt, t + 1, lr_net, lg, kind="higher")
             hv, du, dw = plan.hvp(u, z, w, e, p_prev, lg, ws=hws)
+            du, dw = self._fold(plan, du, dw)
             lt += hv
-            gu += du
+            gu += du.reshape(gu.shape)
             gw += dw
-        if self.u.grad is None:
-            self.u.grad = torch.zeros_like(self.u)
-        self.u.grad += gu.reshape(self.u.shape).to(self.u.dtype)
-        self.optim_u.step()
-        if self.learn_v:
-            if self.v.grad is None:
-                self.v.grad = torch.zeros_like(self.v)
-            self.v.grad += self._chain_w(gw)
-            self.optim_v.step()
-            if not getattr(self, "parameterised", False):
-                with torch.no_grad():
-                    torch.clamp_(self.v, min=0.0)
+        self._hparam_steps(gu, gw)
         if getattr(self, "scheduler_optim_net", None):
             self.scheduler_optim_net.step()
         with torch.no_grad():
@@ -800,27 +941,64 @@ class PSVIFreeV(PSVI):
 
 
 class PSVI_Ablated(PSVILearnV):
-    """Differs from PSVILearnV only in the outer objective (psvi_classes.py:1388-1408)."""
+    """PSVILearnV with the ablated outer objective (psvi_classes.py:1388-1408):
+    psvi_elbo = mean_s (N/Nx) sum_x NLL_s(x) - mean_s sampled_nkl_s over the data
+    batch only, no importance weights over samples; u and v reach it only
+    through the inner loop.  On a full-covariance model the reference's sum over
+    VILinear modules is the int 0 and raises AttributeError; so does this."""
+
+    _outer_mode = "ablated"
 
 
 class PSVI_No_IW(PSVI_Ablated):
-    """Single-sample training (psvi_classes.py:1411-1420)."""
+    """Single-sample training, multi-sample testing (psvi_classes.py:1411-1472):
+    mc_samples = 1 for the inner loop and the ablated outer objective;
+    evaluate / pred_on_grid switch the mean-field layers to mc_samples_eval
+    samples and back.  With one sample the reference's inner objective scores
+    every pseudo row against every pseudo label (2-d logits unsqueezed to
+    (M, 1, C), psvi_classes.py:492-493); the HIP path runs it as M*C expanded
+    rows.  Mean-field models only (full-covariance ones fail in the reference's
+    ablated objective)."""
+
+    _noiw = True
 
     def __init__(self, **kwargs):
         super().__init__(**kwargs)
         self.mc_samples = 1
 
+    def _multi(self, mc_samples_eval, mc_samples_train, fn):
+        from ..models.neural_net import set_mc_samples
+
+        self.mc_samples = mc_samples_eval
+        set_mc_samples(self.model, mc_samples_eval)
+        try:
+            return fn()
+        finally:
+            self.mc_samples = 1
+            set_mc_samples(self.model, mc_samples_train)
+
+    def evaluate(self, correction=True, mc_samples_eval=5, mc_samples_train=1, **kwargs):
+        """psvi_classes.py:1423-1447: PSVI.evaluate with mc_samples_eval samples."""
+        return self._multi(mc_samples_eval, mc_samples_train,
+                           lambda: PSVI.evaluate(self, correction=True, **kwargs))
+
+    def pred_on_grid(self, correction=True, n_test_per_dim=250, mc_samples_eval=5,
+                     mc_samples_train=1, **kwargs):
+        """psvi_classes.py:1449-1472."""
+        return self._multi(mc_samples_eval, mc_samples_train,
+                           lambda: PSVI.pred_on_grid(self, n_test_per_dim=n_test_per_dim,
+                                                     correction=correction, **kwargs))
+
 
 class PSVIAV(PSVILearnV):
     """Learnable simplex weights times a learnable total evidence exp(alpha)
-    (psvi_classes.py:1475-1490)."""
+    (psvi_classes.py:1475-1620): hparams [u, v, alpha]; optim_alpha (Adam,
+    lr0alpha) steps with optim_v in nested_step / hyper_step.  Like the
+    reference, trainer 'joint' leaves alpha out of its optimiser (867-881)."""
 
     def __init__(self, learn_v=True, **kwargs):
         super().__init__(**kwargs)
-        self.alpha = torch.tensor([0.0], device=self.device)
-        self.alpha.requires_grad_(True)
-        self.f = lambda *x: torch.exp(self.alpha) * torch.softmax(x[0], x[1])
-        self.results["alpha"] = []
+        _init_alpha(self)
 
     def evaluate(self, **kwargs):
         """psvi_classes.py:1492-1499: records alpha, then PSVI.evaluate."""
@@ -829,8 +1007,44 @@ class PSVIAV(PSVILearnV):
 
 
 class PSVIFixedU(PSVILearnV):
-    """u held fixed; same inner loop (psvi_classes.py:1622)."""
+    """Fixed pseudopoint locations (psvi_classes.py:1622-1740): u is frozen
+    (requires_grad False, optim_u never stepped), only v is learned."""
+
+    _learn_u = False
+
+    def hyper_step(self, xbatch, ybatch, *args, **kwargs):
+        """The reference hands hypergrad a DifferentiableAdam as fp_map
+        (psvi_classes.py:1710-1712): its 3-way split of the plain parameter list
+        makes the functional model call fail with IndexError before anything
+        moves (SURVEY.md Appendix B #24).  Reproduced: the same error."""
+        self.u.requires_grad_(False)
+        if self.learn_v:
+            self.optim_v.zero_grad()
+        raise IndexError("list index out of range: PSVIFixedU.hyper_step's fp_map is a "
+                         "DifferentiableAdam over the plain parameter list "
+                         "(psvi_classes.py:1710-1712), as in the reference")
 
 
-class PSVIAFixedU(PSVIAV):
-    """u held fixed, learnable evidence scale; same inner loop (psvi_classes.py:1743)."""
+class PSVIAFixedU(PSVILearnV):
+    """Fixed pseudopoint locations, learnable simplex weights and evidence scale
+    exp(alpha) (psvi_classes.py:1743-1884): hparams [v, alpha]."""
+
+    _learn_u = False
+
+    def __init__(self, learn_v=True, **kwargs):
+        super().__init__(**kwargs)
+        _init_alpha(self)
+
+    def evaluate(self, **kwargs):
+        """psvi_classes.py:1761-1768: records alpha, then PSVI.evaluate."""
+        self.results.setdefault("alpha", []).append(self.alpha.clone().cpu().detach().numpy())
+        return super().evaluate(**kwargs)
+
+
+def _init_alpha(obj):
+    """alpha = 0, f = exp(alpha) softmax(v) and its Adam (psvi_classes.py:1482-1490)."""
+    obj.alpha = torch.tensor([0.0], device=obj.device)
+    obj.alpha.requires_grad_(True)
+    obj.f = lambda *x: torch.exp(obj.alpha) * torch.softmax(x[0], x[1])
+    obj.optim_alpha = torch.optim.Adam([obj.alpha], obj.lr0alpha)
+    obj.results["alpha"] = []

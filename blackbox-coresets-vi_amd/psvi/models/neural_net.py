@@ -51,9 +51,10 @@ def inverse_softplus(x):
 
 
 def set_mc_samples(net, mc_samples):
-    """Set the number of MC samples of every variational layer (neural_net.py:26-29)."""
+    """Set the number of MC samples of every mean-field layer (neural_net.py:26-29:
+    VIMixin modules only -- full-covariance layers keep theirs)."""
     for m in net.modules():
-        if isinstance(m, (VIMixin, MultivariateNormalVIMixin)):
+        if isinstance(m, VIMixin):
             m.mc_samples = mc_samples
 
 

@@ -88,6 +88,7 @@ SIGNATURES = {
                                ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
     "psvi_outer_elbo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _SZ, _P]),
+    "psvi_outer_ablated_elbo_grad": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "psvi_outer_elbo_grad_coef": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                          _SZ, _P]),
     "psvi_evaluate": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _SZ, _P]),

@@ -219,6 +219,31 @@ class InnerLoopPlan:
             _stream()), "psvi_outer_elbo_grad")
         return out
 
+    def outer_ablated_elbo_grad(self, x_all, z_all, w_all, eps, params, grad=True,
+                                sample_stats=False, ws=None):
+        """PSVI_Ablated.psvi_elbo over this plan's M data rows (no pseudopoints):
+        mean_s data_s - mean_s nkl_s -- psvi_outer_ablated_elbo_grad.  Returns
+        a dict: loss (float64, 1), grad (P) when requested, samples (S, 4)."""
+        D = self.in_features
+        _need(x_all, "x_all", self.M * D)
+        _need(z_all, "z_all", self.M, torch.int32)
+        _need(w_all, "w_all", self.M)
+        _need(eps, "eps", self.eps_count)
+        _need(params, "params", self.param_count)
+        dev = params.device
+        out = {"loss": torch.empty(1, dtype=torch.float64, device=dev)}
+        if grad:
+            out["grad"] = torch.empty(self.param_count, dtype=torch.float32, device=dev)
+        if sample_stats:
+            out["samples"] = torch.empty(self.S, 4, dtype=torch.float64, device=dev)
+        if ws is None or ws.numel() < self.outer_ws_bytes:
+            ws = torch.empty(self.outer_ws_bytes, dtype=torch.uint8, device=dev)
+        check(self.lib.psvi_outer_ablated_elbo_grad(
+            self.handle, _ptr(x_all), _ptr(z_all), _ptr(w_all), _ptr(eps), _ptr(params),
+            _ptr(out["loss"]), _ptr(out.get("grad")), _ptr(out.get("samples")), _ptr(ws),
+            ws.numel(), _stream()), "psvi_outer_ablated_elbo_grad")
+        return out
+
     def outer_grad_coef(self, n_pseudo, x_all, z_all, w_all, eps, params, coef, grad_u=True,
                         grad_w=True, ws=None):
         """Backward of the outer objective with caller-given per-sample

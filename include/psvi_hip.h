@@ -260,6 +260,23 @@ int psvi_outer_elbo_grad(const psvi_plan* plan, int32_t n_pseudo, const float* x
                          float* grad_u, float* grad_w, double* sample_out, void* ws,
                          size_t ws_bytes, void* stream);
 
+/* PSVI_Ablated.psvi_elbo (psvi/inference/psvi_classes.py:1397-1408; also
+ * PSVI_No_IW's, 1411): the outer objective without importance weighting,
+ * over the data batch only (x_all = xbatch, the plan's M = Nx rows, w_all =
+ * N / Nx each; no pseudopoints), 1 <= S <= 2048:
+ *   loss_out[0] (double, written) <- mean_s data_s - mean_s nkl_s,
+ *       data_s = sum_m w_m NLL_sm, nkl_s the sampled KL of the VILinear
+ *       layers (every mean-field layer; LeNet's three linear layers)
+ *   grad_params (PARAM_COUNT, nullable) <- d loss / d params (first order)
+ *   sample_out ([S][4] doubles, nullable) <- 0, data_s, nkl_s, 1/S
+ * A full-covariance plan returns PSVI_EUNSUP: the reference's sum over
+ * VILinear modules is then the int 0 and 0.mean() raises.
+ * ws: PSVI_Q_OUTER_WS_BYTES. */
+int psvi_outer_ablated_elbo_grad(const psvi_plan* plan, const float* x_all,
+                                 const int32_t* z_all, const float* w_all, const float* eps,
+                                 const float* params, double* loss_out, float* grad_params,
+                                 double* sample_out, void* ws, size_t ws_bytes, void* stream);
+
 /* The backward half of psvi_outer_elbo_grad with caller-given per-sample
  * coefficients instead of the plan's own softmax over its S samples
  * (replaces the autograd backward of PSVI.psvi_elbo, psvi_classes.py:463-486,

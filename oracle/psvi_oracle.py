@@ -358,11 +358,12 @@ def _net_rows_backward(coef, probs_minus_onehot, hs, acts, Ws):
     return dWs, dbs, g
 
 
-def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
+def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=1.0,
+                    mode="iw"):
     if family == "lenet":
         X = np.asarray(X)
         loss, g, gu, gw = lenet_outer_elbo_grad(params, X.reshape(-1, 1, 28, 28), z, w,
-                                                n_pseudo, eps, S, prior_sd)
+                                                n_pseudo, eps, S, prior_sd, mode)
         return loss, g, gu.reshape((int(n_pseudo),) + X.shape[1:]), gw
     """Negative PSVI-ELBO (PSVI.psvi_elbo, psvi/inference/psvi_classes.py:445-486)
     and its first-order gradient.
@@ -382,7 +383,14 @@ def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=
       loss = sum_s W_s (data_s - pseudo_s) - mean_s lw_s
     Returns (loss, d loss/d params, d loss/d X[:n_pseudo], d loss/d w[:n_pseudo]).
     The pathwise gradient of nkl_s is -x_s/s0^2 on the sampled weights; the
-    explicit one is +1/sigma_i on every scale (the eps^2/2 term is constant)."""
+    explicit one is +1/sigma_i on every scale (the eps^2/2 term is constant).
+    mode="ablated": PSVI_Ablated.psvi_elbo (psvi_classes.py:1397-1408),
+      loss = mean_s data_s - mean_s nkl_s  (no pseudo rows: n_pseudo = 0), with
+      nkl over the VILinear layers only -- a full-covariance model has none, and
+      the reference fails there (sum() of nothing is the int 0, 0.mean())."""
+    if mode == "ablated" and family != "mf":
+        raise AttributeError("'int' object has no attribute 'mean' (PSVI_Ablated.psvi_elbo "
+                             "on a model without VILinear layers)")
     params = np.asarray(params, np.float64)
     eps = np.asarray(eps, np.float64)
     X = np.asarray(X, np.float64)
@@ -433,15 +441,7 @@ def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=
     pseudo = nll[:, :Mu] @ w[:Mu]
     data = nll[:, Mu:] @ w[Mu:]
     nkl = -xsq / (2 * s0 ** 2) - n_tot * np.log(s0) + 0.5 * esq + sumlog
-    lw = -pseudo + nkl
-    W = np.exp(lw - lw.max())
-    W /= W.sum()
-    a = data - pseudo
-    abar = float((W * a).sum())
-    loss = abar - float(lw.mean())
-    ck = W * (a - abar) - 1.0 / S          # d loss / d lw_s = d loss / d nkl_s
-    cd = W                                 # d loss / d data_s
-    cp = -W - ck                           # d loss / d pseudo_s
+    loss, cp, cd, ck = _outer_coef(pseudo, data, nkl, S, mode)
     coef = np.concatenate([cp[:, None] * w[None, :Mu], cd[:, None] * w[None, Mu:]], axis=1)
     pmo = np.exp(logits - lse[..., None])
     pmo[:, np.arange(R), zi] -= 1.0
@@ -460,6 +460,26 @@ def outer_elbo_grad(family, layers, params, X, z, w, n_pseudo, eps, S, prior_sd=
     gX = dX.sum(0)[:Mu]
     gw = (cp[:, None] * nll[:, :Mu]).sum(0)
     return loss, grad, gX, gw
+
+
+def _outer_coef(pseudo, data, nkl, S, mode):
+    """loss and its derivatives w.r.t. each sample's pseudo, data and nkl terms.
+    iw (PSVI.psvi_elbo, psvi_classes.py:476-486): lw = -pseudo + nkl,
+    W = softmax_s(lw), loss = sum_s W_s (data_s - pseudo_s) - mean_s lw_s.
+    ablated (PSVI_Ablated.psvi_elbo, 1397-1408): loss = mean data - mean nkl."""
+    if mode == "ablated":
+        loss = float(data.mean() - nkl.mean())
+        return loss, np.zeros(S), np.full(S, 1.0 / S), np.full(S, -1.0 / S)
+    if mode != "iw":
+        raise ValueError(mode)
+    lw = -pseudo + nkl
+    W = np.exp(lw - lw.max())
+    W /= W.sum()
+    a = data - pseudo
+    abar = float((W * a).sum())
+    loss = abar - float(lw.mean())
+    ck = W * (a - abar) - 1.0 / S          # d loss / d lw_s = d loss / d nkl_s
+    return loss, -W - ck, W, ck            # cp = d loss / d pseudo_s, cd = d / d data_s
 
 
 # ------------------------------------- second order: HVP of the inner ELBO
@@ -617,47 +637,140 @@ def torch_adam_step(p, g, m, v, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
     return p - (lr / (1 - beta1 ** t)) * m / denom, m, v
 
 
+class Variant:
+    """What a PSVI plugin class changes in the outer step (hyper_step /
+    nested_step), psvi_classes.py:1344-1884:
+      f        "softmax" (PSVILearnV and subclasses) or "exp_alpha_softmax"
+               (PSVIAV / PSVIAFixedU: w = N exp(alpha) softmax(v), 1486-1488);
+      alpha    the starting alpha (exp_alpha_softmax), stepped by its own
+               torch Adam with lr0alpha (1489, 1578, 1610);
+      fixed_u  PSVIFixedU / PSVIAFixedU: u.requires_grad_(False), optim_u never
+               stepped (1631-1742, 1790-1884);
+      outer    "iw" (PSVI.psvi_elbo) or "ablated" (PSVI_Ablated / PSVI_No_IW);
+      noiw     PSVI_No_IW's single-sample inner objective: 2-d logits are
+               unsqueezed to (M, 1, C) (psvi_classes.py:492-493), so
+               Categorical.log_prob(z) broadcasts to (M, M) and the objective is
+               sum_i sum_j w_j NLL(logits_i, z_j) = sum_i sum_c W_c NLL(logits_i, c),
+               W_c = sum_{j: z_j = c} w_j: the standard objective over M*C
+               expanded rows (u_i, class c, weight W_c)."""
+
+    def __init__(self, f="softmax", alpha=None, fixed_u=False, outer="iw", noiw=False,
+                 lr0alpha=1e-3):
+        self.f, self.alpha, self.fixed_u = f, alpha, fixed_u
+        self.outer, self.noiw, self.lr0alpha = outer, noiw, lr0alpha
+
+
+def weights_vjp(v, alpha, dw, N, f="softmax"):
+    """(d/dv, d/dalpha) of dw . w with w = N f(v) (coreset_weights)."""
+    v = np.asarray(v, np.float64)
+    e = np.exp(v - v.max())
+    sm = e / e.sum()
+    scale = N * (np.exp(alpha) if f == "exp_alpha_softmax" else 1.0)
+    gs = scale * np.asarray(dw, np.float64)
+    dv = sm * (gs - (gs * sm).sum())
+    dalpha = float((gs * sm).sum()) if f == "exp_alpha_softmax" else None
+    return dv, dalpha
+
+
+def inner_rows(u, z, w, C, noiw):
+    """The rows the inner objective scores: (u, z, w) itself, or PSVI_No_IW's
+    M*C expanded rows (Variant.noiw); fold(du, dw) maps row gradients back."""
+    u = np.asarray(u, np.float64)
+    if not noiw:
+        return u, z, w, lambda du, dw: (du, dw)
+    M = u.shape[0]
+    zi = np.asarray(z).astype(np.int64)
+    Wc = np.bincount(zi, weights=np.asarray(w, np.float64), minlength=C)
+    ue = np.repeat(u, C, axis=0)                      # row i*C + c
+    ze = np.tile(np.arange(C), M).astype(np.float64)
+    we = np.tile(Wc, M)
+
+    def fold(du, dw):
+        return (np.asarray(du).reshape((M, C) + u.shape[1:]).sum(1),
+                np.asarray(dw).reshape(M, C).sum(0)[zi])
+    return ue, ze, we, fold
+
+
+def _outer_rows(var, u, z, w, xb, yb, N):
+    """Rows, labels, weights and pseudo count of the outer objective."""
+    Nx = xb.shape[0]
+    if var.outer == "ablated":   # model(xbatch) only (psvi_classes.py:1402)
+        return np.asarray(xb, np.float64), np.asarray(yb), np.full(Nx, N / Nx), 0
+    return (np.concatenate([u, xb]), np.concatenate([z, yb]),
+            np.concatenate([w, np.full(Nx, N / Nx)]), u.shape[0])
+
+
+def _outer(var, family, layers, p, u, z, w, xb, yb, N, eps, S, prior_sd):
+    X, zz, ww, Mu = _outer_rows(var, u, z, w, xb, yb, N)
+    loss, g, gu, gw = outer_elbo_grad(family, layers, p, X, zz, ww, Mu, eps, S, prior_sd,
+                                      mode=var.outer)
+    if Mu == 0:
+        gu, gw = np.zeros_like(u), np.zeros(u.shape[0])
+    return loss, g, gu.reshape(u.shape), gw
+
+
+def _hparam_steps(var, u, v, u_grad, v_grad, a_grad, lr0u, lr0v):
+    """The optim_u / optim_v / optim_alpha steps (first torch Adam step each)."""
+    u_new = u if var.fixed_u else torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)[0]
+    v_new = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)[0]
+    a_new = None
+    if var.f == "exp_alpha_softmax":
+        a = np.array([var.alpha], np.float64)
+        a_new = float(torch_adam_step(a, np.array([a_grad]), 0 * a, 0 * a, 1, var.lr0alpha)[0][0])
+    return u_new, v_new, a_new
+
+
+def _n_classes(layers, family):
+    return 10 if family == "lenet" else layers[-1][1]
+
+
 def hyper_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer, S, T, K,
                lr0net, lr0u, lr0v, linsys_lr=1e-4, prior_sd=1.0, cg_tol=1e-10,
-               approx="CG_normaleq"):
+               approx="CG_normaleq", variant=None):
     """PSVI.hyper_step with the CG_normaleq hypergradient (psvi_classes.py:602-687,
     psvi/hypergrad/hypergradients.py:199-244, CG_torch.py:9-45), PSVILearnV
-    weights f = softmax (v learned, not clamped).  eps_inner: the draws of the
+    weights f = softmax (v learned, not clamped) unless ``variant`` (Variant:
+    PSVIAV 1504-1581, PSVIAFixedU 1774-1850, PSVI_Ablated / PSVI_No_IW through
+    the base method) says otherwise.  eps_inner: the draws of the
     inner-objective calls in order -- T inner Adam steps, fp_map, the initial
     jvp (2: the first only sizes its dummy), then 2 per CG iteration;
     eps_outer: the outer objective's draws (hypergradient, returned loss).
     approx="fixed_point": hypergrad's fixed_point with stochastic=True
     (hypergradients.py:83-140): vs <- J^T vs + g_w for K draws of fp_map, then
     one more draw for the final torch_grad.
-    Returns dict(params, u, v, u_grad, v_grad, ll)."""
+    Returns dict(params, u, v, u_grad, v_grad, ll) (+ alpha, alpha_grad)."""
+    var = variant or Variant()
+    if var.fixed_u and var.f != "exp_alpha_softmax":
+        # PSVIFixedU.hyper_step hands hypergrad a DifferentiableAdam as fp_map
+        # (psvi_classes.py:1710): it splits the plain parameter list in three
+        # and the model call fails (Appendix B #24 of SURVEY.md)
+        raise IndexError("list index out of range (PSVIFixedU.hyper_step: 3-way "
+                         "DifferentiableAdam fp_map)")
     u = np.asarray(u, np.float64)
     v = np.asarray(v, np.float64)
-    M = u.shape[0]
-    Nx = xb.shape[0]
+    C = _n_classes(layers, family)
 
-    def wts(vv):
-        return coreset_weights(vv, N, "softmax")
-
-    def softmax_T(vv, dw):  # d/dv of w = N softmax(v), applied to dw
-        e = np.exp(vv - vv.max())
-        sm = e / e.sum()
-        gs = N * dw
-        return sm * (gs - (gs * sm).sum())
+    def wts(vv, aa=var.alpha):
+        return coreset_weights(vv, N, var.f, aa)
 
     w = wts(v)
-    _, _, traj, _, _ = run_inner_loop(family, layers, params0, u, z, w, eps_inner[:T], S, lr0net,
-                                      "hypergrad")
+    ui, zi, wi, fold = inner_rows(u, z, w, C, var.noiw)
+    if family == "lenet":
+        _, _, traj, _, _ = lenet_inner_loop(params0, ui, zi, wi, eps_inner[:T], S, lr0net,
+                                            "hypergrad", prior_sd)
+    else:
+        _, _, traj, _, _ = run_inner_loop(family, layers, params0, ui, zi, wi, eps_inner[:T], S,
+                                          lr0net, "hypergrad")
     p = traj[-1]
     ei = list(eps_inner[T:])
-    X = np.concatenate([u, xb])
-    zz = np.concatenate([z, yb])
-    ww = np.concatenate([w, np.full(Nx, N / Nx)])
-    o_loss, g_w, g_u, g_wts = outer_elbo_grad(family, layers, p, X, zz, ww, M, eps_outer[0], S,
-                                              prior_sd)
-    g_v = softmax_T(v, g_wts)
+    o_loss, g_w, g_u, g_wts = _outer(var, family, layers, p, u, z, w, xb, yb, N, eps_outer[0],
+                                     S, prior_sd)
     lr = linsys_lr
+
     def hv(e, x):
-        return inner_hvp(family, layers, p, u, z, w, e, S, x, prior_sd)
+        val, g, h, du, dw = inner_hvp(family, layers, p, ui, zi, wi, e, S, x, prior_sd)
+        du, dw = fold(du, dw)
+        return val, g, h, du, dw
 
     if approx == "fixed_point":
         vs = np.zeros_like(g_w)
@@ -666,50 +779,46 @@ def hyper_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer
             vs = vs - lr * hv(ei.pop(0), vs)[2] + g_w   # stochastic: a fresh fp_map each time
             if float(np.linalg.norm(vs - prev)) < cg_tol:
                 break
-        _, _, _, du, dw = hv(ei.pop(0), vs)
-        u_grad = -lr * du + g_u
-        v_grad = -lr * softmax_T(v, dw) + g_v
-        u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
-        v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
-        X2 = np.concatenate([u_new, xb])
-        ww2 = np.concatenate([wts(v_new), np.full(Nx, N / Nx)])
-        ll = outer_elbo_grad(family, layers, p, X2, zz, ww2, M, eps_outer[1], S, prior_sd)[0]
-        return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, ll=ll)
-    eA = ei.pop(0)                                  # w_mapped = fp_map(params, hparams)
+        xk, eA = vs, ei.pop(0)
+    else:
+        eA = ei.pop(0)                              # w_mapped = fp_map(params, hparams)
 
-    def jvp(x):                                     # J x = x - lr H x at a fresh draw
-        ei.pop(0)                                   # the dummy's fp_map call
-        return x - lr * hv(ei.pop(0), x)[2]
+        def jvp(x):                                 # J x = x - lr H x at a fresh draw
+            ei.pop(0)                               # the dummy's fp_map call
+            return x - lr * hv(ei.pop(0), x)[2]
 
-    def A(x):                                       # dfp_map_dw
-        vmj = lr * hv(eA, x)[2]                     # x - J^T x
-        return vmj - jvp(vmj)
+        def A(x):                                   # dfp_map_dw
+            vmj = lr * hv(eA, x)[2]                 # x - J^T x
+            return vmj - jvp(vmj)
 
-    b = g_w - jvp(g_w)
-    xk = np.zeros_like(b)
-    r = b.copy()
-    pk = r.copy()
-    for _ in range(K):
-        Ap = A(pk)
-        rTr = float(r @ r)
-        alpha = rTr / float(pk @ Ap)
-        xn = xk + alpha * pk
-        rn = r - alpha * Ap
-        if float(np.linalg.norm(rn)) < cg_tol:
-            break
-        beta = float(rn @ rn) / rTr
-        pk = rn + beta * pk
-        xk, r = xn, rn
+        b = g_w - jvp(g_w)
+        xk = np.zeros_like(b)
+        r = b.copy()
+        pk = r.copy()
+        for _ in range(K):
+            Ap = A(pk)
+            rTr = float(r @ r)
+            alpha = rTr / float(pk @ Ap)
+            xn = xk + alpha * pk
+            rn = r - alpha * Ap
+            if float(np.linalg.norm(rn)) < cg_tol:
+                break
+            beta = float(rn @ rn) / rTr
+            pk = rn + beta * pk
+            xk, r = xn, rn
     # grads = torch_grad(w_mapped, hparams, vs) = -lr d/dhp (vs . grad_p inner)
     _, _, _, du, dw = hv(eA, xk)
     u_grad = -lr * du + g_u
-    v_grad = -lr * softmax_T(v, dw) + g_v
-    u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
-    v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
-    X2 = np.concatenate([u_new, xb])
-    ww2 = np.concatenate([wts(v_new), np.full(Nx, N / Nx)])
-    ll = outer_elbo_grad(family, layers, p, X2, zz, ww2, M, eps_outer[1], S, prior_sd)[0]
-    return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, ll=ll)
+    dw_tot = -lr * dw + g_wts
+    v_grad, a_grad = weights_vjp(v, var.alpha, dw_tot, N, var.f)
+    u_new, v_new, a_new = _hparam_steps(var, u, v, u_grad, v_grad, a_grad, lr0u, lr0v)
+    ll = _outer(var, family, layers, p, u_new, z, wts(v_new, a_new), xb, yb, N, eps_outer[1], S,
+                prior_sd)[0]
+    out = dict(params=p, u=u_new, v=v_new, u_grad=None if var.fixed_u else u_grad,
+               v_grad=v_grad, ll=ll)
+    if a_new is not None:
+        out.update(alpha=a_new, alpha_grad=a_grad)
+    return out
 
 
 def adam_higher_adjoint(lt, lm, lv, m, v, g, t, lr, beta1=0.9, beta2=0.999, eps=1e-8):
@@ -729,53 +838,56 @@ def adam_higher_adjoint(lt, lm, lv, m, v, g, t, lr, beta1=0.9, beta2=0.999, eps=
     return lg, beta1 * lm2, beta2 * lv2
 
 
+
 def nested_step(family, layers, params0, u, z, v, N, xb, yb, eps_inner, eps_outer, S, T,
-                lr0net, lr0u, lr0v, prior_sd=1.0):
+                lr0net, lr0u, lr0v, prior_sd=1.0, variant=None):
     """PSVI.nested_step (psvi_classes.py:541-600), PSVILearnV (f = softmax, v not
-    clamped): T higher-Adam steps from params0 with fresh state, the outer
-    objective at the result, its gradient w.r.t. u and v back through the
-    unrolled steps (reverse-mode through Adam, one Hessian-vector product and
-    mixed product per step), then the u / v Adam steps.
-    Returns dict(params, u, v, u_grad, v_grad, loss)."""
+    clamped) unless ``variant`` (Variant: PSVIAV 1583-1620, PSVIFixedU
+    1631-1657, PSVIAFixedU 1852-1884, PSVI_Ablated / PSVI_No_IW through the
+    base method): T higher-Adam steps from params0 with fresh state, the outer
+    objective at the result, its gradient w.r.t. u and v (and alpha) back
+    through the unrolled steps (reverse-mode through Adam, one Hessian-vector
+    product and mixed product per step), then the hparam Adam steps.
+    Returns dict(params, u, v, u_grad, v_grad, loss) (+ alpha, alpha_grad)."""
+    var = variant or Variant()
     u = np.asarray(u, np.float64)
     v = np.asarray(v, np.float64)
-    M = u.shape[0]
-    Nx = xb.shape[0]
-    w = coreset_weights(v, N, "softmax")
-
-    def softmax_T(dw):
-        e = np.exp(v - v.max())
-        sm = e / e.sum()
-        gs = N * dw
-        return sm * (gs - (gs * sm).sum())
-
-    f = mf_elbo_grad if family == "mf" else mvn_elbo_grad
+    C = _n_classes(layers, family)
+    w = coreset_weights(v, N, var.f, var.alpha)
+    ui, zi, wi, fold = inner_rows(u, z, w, C, var.noiw)
+    if family == "lenet":
+        f = lambda _l, p, uu, zz, ww, e, S, sd: lenet_elbo_grad(p, uu, zz, ww, e, S, sd)
+    else:
+        f = mf_elbo_grad if family == "mf" else mvn_elbo_grad
     p = np.asarray(params0, np.float64).copy()
     m = np.zeros_like(p)
     vv = np.zeros_like(p)
     hist = []
     for t in range(T):
-        _, g = f(layers, p, u, z, w, eps_inner[t], S, prior_sd)
+        _, g = f(layers, p, ui, zi, wi, eps_inner[t], S, prior_sd)
         pn, m, vv = adam_higher(p, g, m, vv, t + 1, lr0net)
         hist.append((p, m.copy(), vv.copy(), g))
         p = pn
-    X = np.concatenate([u, xb])
-    zz = np.concatenate([z, yb])
-    ww = np.concatenate([w, np.full(Nx, N / Nx)])
-    loss, lt, gu, gw = outer_elbo_grad(family, layers, p, X, zz, ww, M, eps_outer[0], S, prior_sd)
+    loss, lt, gu, gw = _outer(var, family, layers, p, u, z, w, xb, yb, N, eps_outer[0], S,
+                              prior_sd)
     lm = np.zeros_like(p)
     lv = np.zeros_like(p)
     for t in range(T - 1, -1, -1):
         pt, mt, vt, gt = hist[t]
         lg, lm, lv = adam_higher_adjoint(lt, lm, lv, mt, vt, gt, t + 1, lr0net)
-        _, _, hv, du, dw = inner_hvp(family, layers, pt, u, z, w, eps_inner[t], S, lg, prior_sd)
+        _, _, hv, du, dw = inner_hvp(family, layers, pt, ui, zi, wi, eps_inner[t], S, lg,
+                                     prior_sd)
+        du, dw = fold(du, dw)
         lt = lt + hv
         gu = gu + du
         gw = gw + dw
-    u_grad, v_grad = gu, softmax_T(gw)
-    u_new, _, _ = torch_adam_step(u, u_grad, 0 * u, 0 * u, 1, lr0u)
-    v_new, _, _ = torch_adam_step(v, v_grad, 0 * v, 0 * v, 1, lr0v)
-    return dict(params=p, u=u_new, v=v_new, u_grad=u_grad, v_grad=v_grad, loss=loss)
+    v_grad, a_grad = weights_vjp(v, var.alpha, gw, N, var.f)
+    u_new, v_new, a_new = _hparam_steps(var, u, v, gu, v_grad, a_grad, lr0u, lr0v)
+    out = dict(params=p, u=u_new, v=v_new, u_grad=None if var.fixed_u else gu, v_grad=v_grad,
+               loss=loss)
+    if a_new is not None:
+        out.update(alpha=a_new, alpha_grad=a_grad)
+    return out
 
 
 def evaluate_batch(family, layers, params, X, z, w_pseudo, n_pseudo, eps, S, correction=True,
@@ -1005,7 +1117,7 @@ def lenet_elbo_grad(params, u, z, w, eps, S, prior_sd=1.0):
     return data + kl, grad
 
 
-def lenet_outer_elbo_grad(params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
+def lenet_outer_elbo_grad(params, X, z, w, n_pseudo, eps, S, prior_sd=1.0, mode="iw"):
     """PSVI.psvi_elbo (psvi_classes.py:445-486) of a make_lenet model on rows
     X = cat(u, xbatch) (R, 1, 28, 28): sampled_nkl over the VILinear layers
     only (the last one's single shared sample enters every s), W = softmax_s(lw),
@@ -1031,14 +1143,7 @@ def lenet_outer_elbo_grad(params, X, z, w, n_pseudo, eps, S, prior_sd=1.0):
         n = x["n"]
         nkl = nkl + ((-(x["X"] ** 2).sum(1) / (2 * s0 ** 2) - n * np.log(s0)
                       + 0.5 * (x["E"] ** 2).sum(1) + np.log(softplus(x["rho"])).sum()))
-    lw = -pseudo + nkl
-    Wt = np.exp(lw - lw.max())
-    Wt /= Wt.sum()
-    a = data - pseudo
-    abar = float((Wt * a).sum())
-    loss = abar - lw.mean()
-    ck = Wt * (a - abar) - 1.0 / S
-    cp = -Wt - ck
+    loss, cp, Wt, ck = _outer_coef(pseudo, data, nkl, S, mode)
     coef = np.where(np.arange(R)[None, :] < Mu, cp[:, None], Wt[:, None]) * w[None, :]
     Pm = e / e.sum(-1, keepdims=True)
     Pm[:, np.arange(R), zi] -= 1.0

@@ -218,3 +218,81 @@ def test_lenet_torch_forward_matches_oracle():
     finally:
         nnmod.VIMixin.rsample = orig
     assert np.allclose(logits, logits_o, rtol=1e-10, atol=1e-10)
+
+
+# ------------------------------------------------------------ plugin variants
+def _variant(cls_name, S=4, M=6, C=3, D=2):
+    import psvi.inference as PI
+    from psvi.models import make_fcnet
+
+    torch.manual_seed(0)
+    model = make_fcnet(D, 5, C, n_layers=1, mc_samples=S)
+    u = torch.randn(M, D).requires_grad_(True)
+    z = torch.tensor([float(i % C) for i in range(M)])
+    ps = getattr(PI, cls_name)(u=u, z=z, N=100, model=model, mc_samples=S, lr0alpha=0.05)
+    ps.device = torch.device("cpu")
+    return ps
+
+
+def test_variant_switches_follow_the_reference_classes():
+    import psvi.inference as PI
+
+    assert PI.PSVIFixedU._learn_u is False and PI.PSVIAFixedU._learn_u is False
+    assert PI.PSVI_Ablated._outer_mode == "ablated" and PI.PSVI_No_IW._outer_mode == "ablated"
+    assert PI.PSVI_No_IW._noiw and not PI.PSVI_Ablated._noiw
+    assert issubclass(PI.PSVIAFixedU, PI.PSVILearnV) and not issubclass(PI.PSVIAFixedU, PI.PSVIAV)
+    ps = _variant("PSVI_No_IW", S=1)
+    assert ps.mc_samples == 1
+    for name in ("PSVIAV", "PSVIAFixedU"):
+        ps = _variant(name)
+        assert float(ps.alpha) == 0.0 and ps.alpha.requires_grad
+        assert ps.optim_alpha.param_groups[0]["lr"] == 0.05
+        ps.setup_optimizers()
+        assert ps.optim_alpha.param_groups[0]["params"][0] is ps.alpha
+
+
+def test_chain_w_gives_v_and_alpha_gradients():
+    ps = _variant("PSVIAV")
+    with torch.no_grad():
+        ps.alpha.fill_(0.3)
+        ps.v.copy_(torch.linspace(-1, 1, 6))
+    dw = torch.randn(6, dtype=torch.float64)
+    gv, ga = ps._chain_w(dw)
+    v = ps.v.detach().double().requires_grad_(True)
+    a = ps.alpha.detach().double().requires_grad_(True)
+    (100 * torch.exp(a) * torch.softmax(v, 0) * dw).sum().backward()
+    assert torch.allclose(gv.double(), v.grad, rtol=1e-5)
+    assert torch.allclose(ga.double(), a.grad, rtol=1e-5)
+    ps2 = _variant("PSVILearnV")
+    gv2, ga2 = ps2._chain_w(dw)
+    assert ga2 is None and gv2.shape == (6,)
+
+
+def test_noiw_rows_reproduce_the_broadcast_objective():
+    """PSVI_No_IW's single-sample inner objective (the reference's (M, M)
+    broadcast of Categorical.log_prob) equals the standard objective over
+    the M*C expanded rows _data builds."""
+    from psvi.models import model_spec
+
+    ps = _variant("PSVI_No_IW", S=1, M=7, C=3)
+    with torch.no_grad():
+        ps.v.copy_(torch.rand(7))
+    fam, layers, _, _ = model_spec(ps.model)
+
+    class P:
+        M, in_features = 7 * 3, 2
+    P.layers = layers
+    u, z, w = ps._data(P)
+    assert u.shape == (21, 2) and z.tolist() == [0, 1, 2] * 7
+    logits = torch.randn(7, 3, dtype=torch.float64)
+    wp = ps.coreset_weights().double()
+    # reference: logits (M, 1, C) against z (M,) -> (M, M), matmul w, sum
+    ref = -torch.distributions.Categorical(logits=logits.unsqueeze(1)).log_prob(ps.z.double())
+    ref = ref.matmul(wp).sum()
+    le = logits.repeat_interleave(3, 0)
+    got = (-torch.distributions.Categorical(logits=le).log_prob(z.double()) * w.double()).sum()
+    assert torch.allclose(got, ref, rtol=1e-6)
+    du, dw = ps._fold(P, torch.ones(21, 2), torch.arange(21.0))
+    assert du.shape == (7, 2) and torch.all(du == 3)
+    byclass = torch.arange(21.0).reshape(7, 3).sum(0)
+    assert torch.equal(dw, byclass[ps.z.long()])
