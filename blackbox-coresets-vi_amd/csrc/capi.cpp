@@ -21,6 +21,7 @@ void net_set_lds_limit();                // kernels_net.hip
 extern int g_net_ablation;               // kernels_net.hip
 extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
+extern int g_stream_off;                 // kernels_mvn.hip
 extern int g_net_split_below;            // kernels_net.hip
 extern int g_fwd_ablation;               // kernels_mvn.hip
 extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
@@ -32,6 +33,7 @@ using namespace psvi;
 namespace {
 
 thread_local std::string g_err;
+int g_stream_wgs = 0;       // psvi_debug_set(PSVI_DBG_STREAM_WGS, n): streaming-update workgroups (0 = 256)
 int g_upd_chunk_tiles = 0;  // psvi_debug_set(PSVI_DBG_UPD_CHUNK, n): c-blocks per update chunk (0 = auto)
 
 int fail(int code, const std::string& msg) {
@@ -301,6 +303,56 @@ int build_plan(psvi_plan& p) {
         p.h_ufrb = ufrb;
         p.n_ufrb = (int)ufrb.size();
         p.n_uslots = nslots;
+        // streaming fused update: the tile list (layer-major, band-major, the
+        // diagonal tile last in its band) cut into equal contiguous runs, one
+        // per workgroup (one workgroup per CU)
+        if (p.fuse_sample && S % 32 == 0 && p.world == 1) {
+            std::vector<uint32_t> tmap;
+            std::vector<int> tband;  // band id per tile
+            int nband = 0;
+            for (int l = 0; l < p.L; ++l)
+                for (int b = 0; b < p.lay[l].nb; ++b, ++nband)
+                    for (int k = 0; k <= b; ++k) {
+                        tmap.push_back((uint32_t)l << 28 | (uint32_t)b << 14 | (uint32_t)k);
+                        tband.push_back(nband);
+                    }
+            const int T = (int)tmap.size();
+            const int nwg = std::max(1, std::min(g_stream_wgs > 0 ? g_stream_wgs : 256, T));
+            // equal-cost runs: a diagonal tile also updates its band's mean / sd,
+            // a band's first tile follows a slot flush and a G reload (measured
+            // shader clocks: about 0.35 and 0.4 of a plain tile)
+            std::vector<double> cum(T + 1, 0.0);
+            for (int t = 0; t < T; ++t) {
+                const uint32_t k = tmap[t] & 0x3fff, b = (tmap[t] >> 14) & 0x3fff;
+                cum[t + 1] = cum[t] + 1.0 + (k == b ? 0.35 : 0.0) + (k == 0 ? 0.4 : 0.0);
+            }
+            std::vector<int> cut(nwg + 1, 0);
+            cut[nwg] = T;
+            for (int w = 1; w < nwg; ++w) {
+                const double target = cum[T] * w / nwg;
+                int t = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+                cut[w] = std::max(cut[w - 1] + 1, std::min(t, T - (nwg - w)));
+            }
+            std::vector<std::vector<int>> band_slots(nband);
+            int ns = 0;
+            for (int w = 0; w < nwg; ++w) {
+                const int t0 = cut[w], t1 = cut[w + 1];
+                p.h_str.push_back(StreamRange{t0, t1, ns, t0 < T ? tmap[t0] : 0u});
+                for (int t = t0; t < t1; ++t)
+                    if (t == t0 || tband[t] != tband[t - 1]) band_slots[tband[t]].push_back(ns++);
+            }
+            int bid = 0;
+            for (int l = 0; l < p.L; ++l)
+                for (int b = 0; b < p.lay[l].nb; ++b, ++bid) {
+                    const int r0 = 64 * b, R = std::min(64, p.lay[l].n - r0);
+                    const auto& sl = band_slots[bid];
+                    p.h_sfrb.push_back(FwdRowBlock{sl.front(), (int)sl.size(), R,
+                                                   p.xcol_l[r][l] + r0, l, r0});
+                }
+            p.n_str = (int)p.h_str.size();
+            p.n_sfrb = (int)p.h_sfrb.size();
+            p.n_sslots = ns;
+        }
         p.upd_tiles = tiles;
         p.n_fwd = (int)fwd.size();
         p.n_upd = (int)p.h_upd.size();
@@ -350,6 +402,8 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_NET_SPLIT_BELOW: g_net_split_below = value; return 0;
         case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
+        case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
+        case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }
 }
@@ -428,6 +482,12 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                 hipMalloc((void**)&p->d_upd_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the fused-sample scratch");
         }
+        if (!rc && p->n_str > 0) {
+            const size_t bytes = sizeof(float) * (size_t)p->n_sslots * p->d.S * 64;
+            if (!(rc = upload(p->h_str, &p->d_str)) && !(rc = upload(p->h_sfrb, &p->d_sfrb)) &&
+                hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the streaming-update scratch");
+        }
         if (!rc && family == PSVI_FAMILY_LENET) {
             const size_t bytes = lenet_ws(*p, nullptr).bytes;
             if (hipMalloc(&p->d_lenet_ws, bytes) != hipSuccess)
@@ -449,6 +509,9 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_frb) (void)hipFree(p->d_frb);
     if (p->d_fwd_part) (void)hipFree(p->d_fwd_part);
     if (p->d_ufrb) (void)hipFree(p->d_ufrb);
+    if (p->d_str) (void)hipFree(p->d_str);
+    if (p->d_sfrb) (void)hipFree(p->d_sfrb);
+    if (p->d_str_part) (void)hipFree(p->d_str_part);
     if (p->d_upd_part) (void)hipFree(p->d_upd_part);
     if (p->d_upd) (void)hipFree(p->d_upd);
     if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);

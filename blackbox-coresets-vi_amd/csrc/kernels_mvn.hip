@@ -17,6 +17,8 @@
 // (row r starts at r(r-1)/2) and run on v_mfma_f32_32x32x2_f32 (exact fp32,
 // gfx950 has no xf32).  The backward never writes dL to HBM: the Adam update
 // of corr (p, m, v read + written once) is the GEMM epilogue.
+#include <type_traits>
+
 #include "psvi_internal.hpp"
 
 namespace psvi {
@@ -802,6 +804,451 @@ __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_ker
     UPD_STAMP(13, __builtin_amdgcn_s_memrealtime());
 }
 
+// ------------------------------------------------- streaming fused update
+// The inner loop's steady-state update (Adam, tiled corr/m/v state, world 1,
+// S a multiple of 32 up to 128) fused with the next step's sample, as one
+// persistent workgroup per CU walking a contiguous run of the layer-major,
+// band-major tile list (band b: tiles k = 0 .. b, the diagonal last).
+// Per 64x64 tile (l, b, k), wave (wr, wc) owns rows 64b + 32wr + [0, 32) x
+// columns 64k + 32wc + [0, 32):
+//   dL^T[c][r] = sum_s eps[s][c] G[s][r]      v_mfma_f32_32x32x2_f32, K = S;
+//       A = eps (the tile's column block), B = G (the band's slice), both
+//       from LDS with ds_read_b32 (the band's slice is staged once per band);
+//   corr/m/v <- Adam on the accumulators (tiled state: the fragment order, 1 KB
+//       per wave instruction); the new L entries stay in registers;
+//   x'[s][r] += sum_c eps'[s][c] L'[r][c]     K = the wave's 32 columns:
+//       B = L' straight from the registers (K permuted to the fragment
+//       order), A = eps' from LDS, one ds_read_b128 per 4 MFMAs.
+// x' accumulates in registers over the run's tiles of one band; at the band's
+// end the two column-half waves add their partials through LDS and write the
+// segment's slot ([S][64]); mvn_fwd_reduce_kernel adds a band's slots.
+// Prefetch: tile i+1's corr/m/v and eps / eps' blocks are loaded behind tile
+// i's x' GEMM (eps blocks into the other LDS buffer after it), the next
+// band's G slice too.  LDS rows of the eps blocks are 16 float4 slots, slot
+// c4 stored at c4 ^ (s & 15): the dL reads (one row, 32 columns) and the x'
+// reads (16 rows, one float4 column) are both bank-conflict free.
+// One barrier per tile (three at a band's end).
+struct StrArgs {
+    const StreamRange* ranges;
+    int nb[kMaxL];         // bands per layer
+    const float* eps;
+    const float* eps_next;
+    const float* g;
+    int ldg, S;
+    int64_t g_total, e_total;
+    float* params;
+    float* m;
+    float* v;
+    float* tp;
+    float* tm;
+    float* tv;
+    float* part;
+    double* kl_out;
+    int include_kl;
+    int abl;                       // diagnostics ablation mask (0 in production)
+    unsigned long long* stamps;    // diagnostics: 16 slots per workgroup (nullptr in production)
+    float inv_s0sq, log_s0;
+    AdamC adam;
+    int xcol[kMaxL];
+    MvnLayerArgs lay[kMaxL];
+};
+
+struct StrTile {
+    int l, b, k, n, eoff, xc;
+    int64_t tb, poff;
+};
+
+__device__ __forceinline__ StrTile str_tile(const StrArgs& a, int l, int b, int k) {
+    StrTile T;
+    T.l = l;
+    T.b = b;
+    T.k = k;
+    T.n = a.lay[l].n;
+    T.eoff = (int)a.lay[l].eoff;
+    T.xc = a.xcol[l];
+    T.poff = a.lay[l].poff;
+    T.tb = tile_index(a.lay[l], b, k) * 4096;
+    return T;
+}
+
+// Adam with the variant fixed at compile time (adam_apply_fast's arithmetic)
+template <int KIND>
+__device__ __forceinline__ float adam_fast_k(const AdamC& a, float p, float g, float& m, float& v) {
+    m = a.b1 * m + a.omb1 * g;
+    if (KIND == PSVI_ADAM_HIGHER) {
+        v = a.b2 * v + a.omb2 * g * g;
+        const float denom = __builtin_amdgcn_sqrtf(v + 1e-8f) * a.inv_sqrt_bc2 + a.eps;
+        return p - a.lr_bc1 * m * __builtin_amdgcn_rcpf(denom);
+    } else if (KIND == PSVI_ADAM_TORCH) {
+        v = a.b2 * v + a.omb2 * g * g;
+        const float denom = __builtin_amdgcn_sqrtf(v) * a.inv_sqrt_bc2 + a.eps;
+        return p - a.lr_bc1 * m * __builtin_amdgcn_rcpf(denom);
+    } else {
+        v = a.b2 * v + a.omb2 * g * g + 1e-12f;
+        const float denom = __builtin_amdgcn_sqrtf(v * a.inv_bc2) + a.eps;
+        return p - a.lr * (m * a.inv_bc1) * __builtin_amdgcn_rcpf(denom);
+    }
+}
+
+constexpr int kStrBuf = 128 * 16;  // float4 per eps block buffer ([128 samples][16 slots])
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // plain vector loads / stores (no memcpy)
+
+template <int NS, int KIND>  // NS = S / 32; KIND: Adam variant
+__global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
+    constexpr int KT = 16 * NS;  // K steps of the dL GEMM (2 samples each)
+    // [0, 4 kStrBuf): eps / eps' blocks, two buffers; then the band's G slice [128][64]
+    __shared__ __attribute__((aligned(16))) f32x4 sm[4 * kStrBuf + 2048];
+    f32x4* const Gl4 = sm + 4 * kStrBuf;
+    const float* const Gl = reinterpret_cast<const float*>(Gl4);
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    const int wr = wv >> 1, wc = wv & 1, h = lane >> 5, l32 = lane & 31;
+    const StreamRange R = a.ranges[blockIdx.x];
+    const int t0 = __builtin_amdgcn_readfirstlane(R.t0);
+    const int t1 = __builtin_amdgcn_readfirstlane(R.t1);
+    int slot = __builtin_amdgcn_readfirstlane(R.slot0);
+    const int S = a.S;
+    // diagnostics: shader clocks per phase summed over the run's tiles (thread 0)
+    unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+    auto ph = [&](int q) __attribute__((always_inline)) {
+        if (a.stamps && tid == 0) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            if (q >= 0) tph[q] += tt - tlast;
+            tlast = tt;
+        }
+    };
+    const int ab = a.abl;
+    const int e_hi = (int)a.e_total - 4, g_hi = (int)a.g_total - 4;
+
+    // eps / eps' block of a tile: 8 + 8 float4 per thread, registers then LDS
+    f32x4 ereg[8], enreg[8];
+    auto load_E = [&](const StrTile& T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int off = (ab & 1) ? 4 * c4 : min(T.eoff + s * T.n + 64 * T.k + 4 * c4, e_hi);
+            ereg[j] = *reinterpret_cast<const f32x4*>(a.eps + off);
+            enreg[j] = *reinterpret_cast<const f32x4*>(a.eps_next + off);
+        }
+    };
+    // the float4 clamped at the buffer's end holds columns shifted by d: move
+    // them back (applied where the registers are consumed, after the loads land)
+    auto fix_E = [&](const StrTile& T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int o = T.eoff + s * T.n + 64 * T.k + 4 * c4, d = o - min(o, e_hi);
+            if (d > 0) {  // VALU-only: the loads are already unconditional
+                ereg[j] = f32x4{d < 4 ? ereg[j][min(d, 3)] : 0.f, d < 3 ? ereg[j][min(d + 1, 3)] : 0.f,
+                                d < 2 ? ereg[j][min(d + 2, 3)] : 0.f, d < 1 ? ereg[j][3] : 0.f};
+                enreg[j] = f32x4{d < 4 ? enreg[j][min(d, 3)] : 0.f, d < 3 ? enreg[j][min(d + 1, 3)] : 0.f,
+                                 d < 2 ? enreg[j][min(d + 2, 3)] : 0.f, d < 1 ? enreg[j][3] : 0.f};
+            }
+        }
+    };
+    auto store_E = [&](int bi, const StrTile& T) __attribute__((always_inline)) {
+        fix_E(T);
+        f32x4* E = sm + 2 * bi * kStrBuf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = tid + 256 * j, s = f >> 4, c4 = f & 15;
+            const int o = s * 16 + (c4 ^ (s & 15));
+            E[o] = ereg[j];
+            E[kStrBuf + o] = enreg[j];
+        }
+    };
+    // the band's G slice [s][64 rows]: 8 float4 per thread
+    f32x4 greg[8];
+    auto load_G = [&](const StrTile& T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            greg[j] = *reinterpret_cast<const f32x4*>(
+                a.g + min(s * a.ldg + T.xc + 64 * T.b + 4 * c4, g_hi));
+        }
+    };
+    auto store_G = [&](const StrTile& T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int o = s * a.ldg + T.xc + 64 * T.b + 4 * c4, d = o - min(o, g_hi);
+            f32x4 gv = greg[j];
+            if (d > 0)  // clamped at the buffer's end (see fix_E)
+                gv = f32x4{d < 4 ? gv[min(d, 3)] : 0.f, d < 3 ? gv[min(d + 1, 3)] : 0.f,
+                           d < 2 ? gv[min(d + 2, 3)] : 0.f, 0.f};
+            Gl4[tid + 256 * j] = gv;
+        }
+    };
+    f32x4 P[4], M4[4], V4[4];
+    auto frag_off = [&](const StrTile& T, int g) __attribute__((always_inline)) {
+        return T.tb + (int64_t)((wv * 4 + g) * 64 + lane) * 4;
+    };
+    auto load_pmv = [&](const StrTile& T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int64_t o = (ab & 1) ? (int64_t)((wv * 4 + g) * 64 + lane) * 4 : frag_off(T, g);
+            P[g] = *reinterpret_cast<const f32x4*>(a.tp + o);
+            M4[g] = *reinterpret_cast<const f32x4*>(a.tm + o);
+            V4[g] = *reinterpret_cast<const f32x4*>(a.tv + o);
+        }
+    };
+
+    floatx16 xacc[NS];
+#pragma unroll
+    for (int sb = 0; sb < NS; ++sb)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) xacc[sb][q] = 0.f;
+    float klp = 0.f, kld = 0.f;  // sum corr^2 (scaled at the end), diagonal KL terms
+
+    // per-lane LDS offsets of the XOR-swizzled reads
+    int okd[8];  // dL A operand (floats): row s = 2t + h, column 32wc + l32; index t & 7
+    {
+        const int c = 32 * wc + l32, c4 = c >> 2;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) okd[k] = h * 64 + 4 * ((c4 ^ h) ^ (2 * k)) + (c & 3);
+    }
+    int okx[4];  // x' A operand (float4): row l32 (+ 32 sb), slot 8wc + 2g + h
+#pragma unroll
+    for (int g = 0; g < 4; ++g) okx[g] = l32 * 16 + ((8 * wc + 2 * g + h) ^ (l32 & 15));
+    const int ogb = h * 64 + 32 * wr + l32;  // G[2t + h][32wr + l32] at ogb + 128 t
+
+    if (a.stamps && tid == 0) {
+        a.stamps[(size_t)blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
+        a.stamps[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    }
+    // prologue: tile t0
+    // tile (l, b, k) of t0, then walked in list order with scalar arithmetic
+    int tl = __builtin_amdgcn_readfirstlane(R.lbk0 >> 28);
+    int tb_ = __builtin_amdgcn_readfirstlane((R.lbk0 >> 14) & 0x3fff);
+    int tk = __builtin_amdgcn_readfirstlane(R.lbk0 & 0x3fff);
+    StrTile cur = str_tile(a, tl, tb_, tk);
+    load_E(cur);
+    load_G(cur);
+    store_E(0, cur);
+    store_G(cur);
+    __syncthreads();
+
+    // one tile; HAS_NEXT / NEWBAND compile-time so that every load is unconditional
+    auto tile = [&](int i, const StrTile& nxt, auto has_next_c, auto newband_c) __attribute__((always_inline)) {
+        constexpr bool has_next = decltype(has_next_c)::value;
+        constexpr bool newband = decltype(newband_c)::value;
+        const int bi = (i - t0) & 1;
+        ph(-1);
+        const float* Ef = reinterpret_cast<const float*>(sm + 2 * bi * kStrBuf);
+        const f32x4* En = sm + (2 * bi + 1) * kStrBuf;
+        // ---- this tile's corr/m/v: in flight behind the dL GEMM
+        load_pmv(cur);
+        // ---- dL^T = eps^T G over the samples
+        floatx16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        if (!(ab & 2)) {
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ef[okd[t & 7] + 128 * t],
+                                                           Gl[ogb + 128 * t], acc, 0, 0, 0);
+        }
+        ph(0);
+        const int n = cur.n, r = 64 * cur.b + 32 * wr + l32;
+        // ---- diagonal tile: sum_s G and sum_s G eps of the band's rows -> mean / sd
+        if (cur.k == cur.b && wc == 0) {
+            // row c of the band per lane pair; the sums run in the chunked
+            // kernel's order (four partials over sample groups 16w + [0, 16)
+            // (+ 64), added left to right), so both kernels agree bit for bit
+            const int c = 32 * wr + l32;
+            float pm2[2], ps2[2];
+#pragma unroll
+            for (int ww = 0; ww < 2; ++ww) {
+                const int w = 2 * h + ww;
+                float gm = 0.f, gsum = 0.f;
+#pragma unroll
+                for (int hh = 0; hh < (NS > 2 ? 2 : 1); ++hh)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const int sm_ = hh * 64 + 16 * w + j;
+                        if (sm_ < 32 * NS) {
+                            const float gv = Gl[sm_ * 64 + c];
+                            gm += gv;
+                            gsum = fmaf(gv, Ef[sm_ * 64 + 4 * ((c >> 2) ^ (sm_ & 15)) + (c & 3)],
+                                        gsum);
+                        }
+                    }
+                pm2[ww] = gm;
+                ps2[ww] = gsum;
+            }
+            const float m2 = __shfl_xor(pm2[0], 32, kWave), m3 = __shfl_xor(pm2[1], 32, kWave);
+            const float s2 = __shfl_xor(ps2[0], 32, kWave), s3 = __shfl_xor(ps2[1], 32, kWave);
+            const float dgm = ((pm2[0] + pm2[1]) + m2) + m3;
+            const float dgs = ((ps2[0] + ps2[1]) + s2) + s3;
+            if (h == 0 && r < n) {
+                const int pm = (int)cur.poff + r, ps = pm + n;
+                const float mu = a.params[pm], sdr = a.params[ps];
+                const float sp = softplus_f(sdr), sg = sigmoid_f(sdr);
+                float gmean = dgm, gsd = dgs * sg;
+                if (a.include_kl) {
+                    gmean += mu * a.inv_s0sq;
+                    gsd += (sp * a.inv_s0sq - 1.f / sp) * sg;
+                    kld += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
+                }
+                float mm = a.m[pm], vv = a.v[pm];
+                a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
+                a.m[pm] = mm;
+                a.v[pm] = vv;
+                mm = a.m[ps];
+                vv = a.v[ps];
+                a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
+                a.m[ps] = mm;
+                a.v[ps] = vv;
+            }
+        }
+        ph(1);
+        // ---- per column group g: Adam on the accumulators (fragment order =
+        // tiled order), the stores, then g's share of the x' GEMM with the next
+        // tile's loads spread between its MFMAs (a burst of them stalls the
+        // in-order wave on the memory queue)
+        const bool rv = r >= 1 && r <= n - 2;
+        const float kls = a.include_kl ? a.inv_s0sq : 0.f;
+        float Lf[16];
+        auto issue_load = [&](int q) __attribute__((always_inline)) {
+            // q < 16: the next tile's eps blocks (8 + 8); then (NEWBAND) the
+            // next band's G slice (8)
+            if constexpr (has_next) {
+                if (q < 16) {
+                    const int j = q >> 1;
+                    const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+                    const int off = (ab & 1) ? 4 * c4
+                                             : min(nxt.eoff + s * nxt.n + 64 * nxt.k + 4 * c4, e_hi);
+                    if ((q & 1) == 0) ereg[j] = *reinterpret_cast<const f32x4*>(a.eps + off);
+                    else enreg[j] = *reinterpret_cast<const f32x4*>(a.eps_next + off);
+                } else if constexpr (newband) {
+                    const int j = q - 16;
+                    const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+                    greg[j] = *reinterpret_cast<const f32x4*>(
+                        a.g + min(s * a.ldg + nxt.xc + 64 * nxt.b + 4 * c4, g_hi));
+                }
+            }
+        };
+        constexpr int NLOAD = has_next ? (newband ? 24 : 16) : 0;
+        f32x4 avn = En[okx[0]];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int cb = 64 * cur.k + 32 * wc + 8 * g + 4 * h;
+            float pn[4], mn[4], vn[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float p = P[g][e];
+                klp += p * p;
+                const bool ok = rv && cb + e < r;
+                const float gv = acc[4 * g + e] + p * kls;
+                float mm = M4[g][e], vv = V4[g][e];
+                pn[e] = adam_fast_k<KIND>(a.adam, p, ok ? gv : 0.f, mm, vv);
+                mn[e] = mm;
+                vn[e] = vv;
+                Lf[4 * g + e] = pn[e];
+            }
+            const int64_t o = frag_off(cur, g);
+            if (!(ab & 4)) {
+                *reinterpret_cast<f32x4*>(a.tp + o) = f32x4{pn[0], pn[1], pn[2], pn[3]};
+                *reinterpret_cast<f32x4*>(a.tm + o) = f32x4{mn[0], mn[1], mn[2], mn[3]};
+                *reinterpret_cast<f32x4*>(a.tv + o) = f32x4{vn[0], vn[1], vn[2], vn[3]};
+            }
+            // x' += eps' L'^T over this group's 8 columns, all sample blocks; the
+            // A fragments are read one slot ahead, and each slot is pinned
+            // (sched_barrier) so the loads stay spread between the MFMAs
+#pragma unroll
+            for (int sb = 0; sb < NS; ++sb) {
+                const int k = g * NS + sb;
+                const f32x4 av = avn;
+                if (k + 1 < 4 * NS) avn = En[okx[(k + 1) / NS] + 512 * ((k + 1) % NS)];
+                if (!(ab & 2)) {
+                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], Lf[4 * g + 0], xacc[sb], 0, 0, 0);
+                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1], Lf[4 * g + 1], xacc[sb], 0, 0, 0);
+                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[2], Lf[4 * g + 2], xacc[sb], 0, 0, 0);
+                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[3], Lf[4 * g + 3], xacc[sb], 0, 0, 0);
+                }
+                // this slot's share of the next tile's loads (slot k of 4 NS)
+                constexpr int NSLOT = 4 * NS;
+#pragma unroll
+                for (int q = 0; q < NLOAD; ++q)
+                    if ((q * NSLOT) / (NLOAD > 0 ? NLOAD : 1) == k) issue_load(q);
+                __builtin_amdgcn_sched_barrier(0x6);  // VALU / SALU may cross, memory and MFMA may not
+            }
+        }
+        ph(2);
+        ph(3);
+        ph(4);
+        if constexpr (has_next) store_E(bi ^ 1, nxt);
+        ph(5);
+        // ---- band end (or run end): the two column halves' x' partials -> the slot
+        if constexpr (!has_next || newband) {
+            __syncthreads();  // every wave done reading buffer bi and the G slice
+            float* X = reinterpret_cast<float*>(sm + 2 * bi * kStrBuf);
+            if (wc == 1) {
+#pragma unroll
+                for (int sb = 0; sb < NS; ++sb)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) X[((wr * NS + sb) * 16 + q) * 64 + lane] = xacc[sb][q];
+            }
+            if constexpr (newband) store_G(nxt);
+            __syncthreads();
+            if (wc == 0) {
+                float* dst = a.part + (size_t)slot * S * 64 + 32 * wr + l32;
+#pragma unroll
+                for (int sb = 0; sb < NS; ++sb)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int s = 32 * sb + (q & 3) + 8 * (q >> 2) + 4 * h;
+                        dst[(size_t)s * 64] = xacc[sb][q] + X[((wr * NS + sb) * 16 + q) * 64 + lane];
+                    }
+            }
+#pragma unroll
+            for (int sb = 0; sb < NS; ++sb)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) xacc[sb][q] = 0.f;
+            ++slot;
+        }
+        ph(6);
+        __syncthreads();  // buffer bi ^ 1 complete; buffer bi free
+        ph(7);
+        if (tid == 0) ++tph[9];
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    for (int i = t0; i + 1 < t1; ++i) {
+        if (++tk > tb_) {
+            tk = 0;
+            int nbl = a.nb[0];  // select: a dynamic index into the argument copies it to scratch
+#pragma unroll
+            for (int l = 1; l < kMaxL; ++l)
+                if (tl == l) nbl = a.nb[l];
+            if (++tb_ == nbl) {
+                tb_ = 0;
+                ++tl;
+            }
+        }
+        const StrTile nxt = str_tile(a, tl, tb_, tk);
+        if (nxt.l != cur.l || nxt.b != cur.b)
+            tile(i, nxt, T_{}, T_{});
+        else
+            tile(i, nxt, T_{}, F_{});
+        cur = nxt;
+    }
+    tile(t1 - 1, cur, F_{}, F_{});
+    if (a.stamps && tid == 0) {
+        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
+#pragma unroll
+        for (int q = 0; q < 10; ++q) o[q] = tph[q];
+        o[10] = __builtin_amdgcn_s_memtime();
+        o[11] = __builtin_amdgcn_s_memrealtime();
+    }
+    klp = klp * (0.5f * a.inv_s0sq) + kld;
+    if (a.kl_out && a.include_kl) {
+        const float tot = block_sum(klp, reinterpret_cast<float*>(sm));
+        if (tid == 0) atomicAdd(a.kl_out, (double)tot);
+    }
+}
+
+int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1)
+
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
 
@@ -905,6 +1352,24 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     return hipGetLastError();
 }
 
+template <int NS>
+static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
+    if (kind == PSVI_ADAM_HIGHER)
+        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER>), g, bl, 0, st, b);
+    else if (kind == PSVI_ADAM_TORCH)
+        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_TORCH>), g, bl, 0, st, b);
+    else
+        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HYPERGRAD>), g, bl, 0, st, b);
+}
+static void launch_stream(int ns, int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
+    switch (ns) {
+        case 1: launch_stream_ns<1>(kind, g, bl, st, b); break;
+        case 2: launch_stream_ns<2>(kind, g, bl, st, b); break;
+        case 3: launch_stream_ns<3>(kind, g, bl, st, b); break;
+        default: launch_stream_ns<4>(kind, g, bl, st, b); break;
+    }
+}
+
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
@@ -941,6 +1406,48 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         a.tp = tstate;
         a.tm = tstate + tf;
         a.tv = tstate + 2 * tf;
+        if (eps_next && p.n_str > 0 && !g_stream_off) {
+            StrArgs b{};
+            b.ranges = p.d_str;
+            b.eps = eps;
+            b.eps_next = eps_next;
+            b.g = g_shard;
+            b.ldg = a.ldg;
+            b.S = a.S;
+            b.g_total = a.g_total;
+            b.e_total = a.e_total;
+            b.params = params;
+            b.m = m;
+            b.v = v;
+            b.tp = a.tp;
+            b.tm = a.tm;
+            b.tv = a.tv;
+            b.part = p.d_str_part;
+            b.kl_out = kl_out;
+            b.include_kl = include_kl;
+            b.abl = g_upd_ablation;
+            b.stamps = g_upd_stamps;
+            b.inv_s0sq = a.inv_s0sq;
+            b.log_s0 = a.log_s0;
+            b.adam = a.adam;
+            for (int l = 0; l < p.L; ++l) {
+                b.xcol[l] = p.xcol_l[p.rank][l];
+                b.nb[l] = p.lay[l].nb;
+            }
+            fill_layers(p, b.lay);
+            const dim3 sg(p.n_str);
+            launch_stream(a.S / 32, b.adam.kind, sg, block, st, b);
+            FwdArgs f{};
+            f.params = params;
+            f.eps = eps_next;
+            f.ldx = p.rows_tot[p.rank];
+            f.S = p.d.S;
+            fill_layers(p, f.lay);
+            constexpr int spb = 256 / kFwdRows;
+            hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_sfrb, (f.S + spb - 1) / spb),
+                               dim3(256), 0, st, p.d_sfrb, p.d_str_part, f, x_next);
+            return hipGetLastError();
+        }
         if (eps_next) {
             a.eps_next = eps_next;
             a.part = p.d_upd_part;

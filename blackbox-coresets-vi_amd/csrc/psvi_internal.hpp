@@ -201,6 +201,15 @@ struct UpdChunk {
     int slot;  // fused next-step sample: partial-sum slot ([S][64] floats), -1 if none
 };
 
+// Streaming fused update (mvn_stream_kernel): workgroup w walks tiles
+// [t0, t1) of the layer-major, band-major tile list; its x' partial of each
+// band it touches goes to slots slot0, slot0 + 1, ... (a band's slots are
+// consecutive over the workgroups).
+struct StreamRange {
+    int t0, t1, slot0;
+    uint32_t lbk0;  // tile t0 as layer << 28 | b << 14 | k
+};
+
 struct NetArgs;  // kernels_net.hip
 
 // Outer-objective passes of the network kernel (psvi_outer_elbo_grad).
@@ -252,6 +261,14 @@ struct psvi_plan {
     psvi::FwdRowBlock* d_ufrb = nullptr;
     int n_ufrb = 0, n_uslots = 0;
     float* d_upd_part = nullptr;
+    // streaming fused update (fuse_sample plans with S % 32 == 0): one
+    // workgroup per range, tile map, band row blocks over its slots
+    std::vector<psvi::StreamRange> h_str;
+    std::vector<psvi::FwdRowBlock> h_sfrb;
+    psvi::StreamRange* d_str = nullptr;
+    psvi::FwdRowBlock* d_sfrb = nullptr;
+    float* d_str_part = nullptr;
+    int n_str = 0, n_sfrb = 0, n_sslots = 0;
     int n_upd = 0;
     int upd_tiles = 0;  // c-blocks over all chunks (work measure)
     // net kernel geometry

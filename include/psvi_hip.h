@@ -396,6 +396,11 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_UPD_CHUNK 9     /* value: c-blocks (64x64 tiles) per full-cov update
                                     chunk for plans created afterwards (0 = auto:
                                     about one chunk per resident workgroup)    */
+#define PSVI_DBG_UPD_STREAM_OFF 10 /* value: 1 = the tiled fused update runs the
+                                    chunked kernel instead of the streaming one
+                                    (A/B diagnostics; 0 = streaming)           */
+#define PSVI_DBG_STREAM_WGS 11   /* value: workgroups of the streaming update for
+                                    plans created afterwards (0 = 256)         */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

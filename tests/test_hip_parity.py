@@ -212,7 +212,11 @@ def test_fused_update_sample_equals_separate(name):
     x2 = torch.full_like(xs, float("nan"))
     plan.mvn_update(eps0, gs, p2, m2, v2, step=1, lr=cfg["lr"], kl_out=k2, eps_next=eps1,
                     x_next=x2)
-    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    # the streaming kernel (S a multiple of 32) contracts the Adam arithmetic
+    # differently from the packed one: equal to within a few ulp
+    for a, b in ((p1, p2), (m1, m2), (v1, v2)):
+        a, b = a.cpu().numpy().astype(np.float64), b.cpu().numpy()
+        assert np.abs(a - b).max() <= 1e-7 * np.abs(b).max()
     assert rel(k1.item(), k2.item()) < 1e-12
     assert torch.isfinite(x2).all()
     assert l2rel(x2.cpu().numpy(), x1.cpu().numpy()) < 1e-6
@@ -338,7 +342,11 @@ def test_tiled_update_equals_packed(name, fused):
     plan.mvn_update_tiled(eps0, gs, p2, m2, v2, ts, step=1, lr=cfg["lr"], kind=adam_kind(cfg),
                           kl_out=k2, **kw)
     plan.tiled_convert(p2, m2, v2, ts, False)
-    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    # the streaming kernel (S a multiple of 32) contracts the Adam arithmetic
+    # differently from the packed one: equal to within a few ulp
+    for a, b in ((p1, p2), (m1, m2), (v1, v2)):
+        a, b = a.cpu().numpy().astype(np.float64), b.cpu().numpy()
+        assert np.abs(a - b).max() <= 1e-7 * np.abs(b).max()
     assert rel(k1.item(), k2.item()) < 1e-6  # fp32 per-thread partial sums, other order
     if fused:
         assert torch.isfinite(x2).all()

@@ -1,0 +1,128 @@
+"""The streaming fused full-cov update (mvn_stream_kernel: persistent workgroup
+per CU, G / eps blocks in LDS, Adam on the accumulators, the next step's
+sample from the registers) against the chunked packed-state update on the
+same inputs, and the whole inner loop at C3's shape against the oracle.
+
+Same inputs, same arithmetic per corr entry (dL sums the samples in the same
+pairs and order; mean / sd sums too), so corr / m / v agree to a few ulp (fma
+contraction of the Adam epilogue); x' sums in another order (fp32, 1e-6)."""
+import numpy as np
+import pytest
+import torch
+
+import psvi_oracle as O
+from golden_util import l2rel, rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DBG_STREAM_OFF = 10
+
+
+def _lib():
+    from psvi.runtime import _lib as L
+
+    return L.load()
+
+
+def _case(layers, S, seed):
+    rng = np.random.default_rng(seed)
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        parts += [0.1 * rng.standard_normal(n), rng.uniform(-5, -3, n),
+                  (0.15 / np.sqrt(n)) * rng.standard_normal((n - 1) * (n - 2) // 2)]
+    p = np.concatenate(parts).astype(np.float32)
+    m = (1e-3 * rng.standard_normal(p.size)).astype(np.float32)
+    v = (1e-6 * rng.random(p.size)).astype(np.float32)
+    return rng, p, m, v
+
+
+SHAPES = [([(64, 40), (40, 40), (40, 2)], 128),   # C3
+          ([(7, 5), (5, 3)], 32),                  # n = 40, 18: one partial band each
+          ([(30, 33), (33, 2)], 96),               # n = 1023, 68
+          ([(12, 20), (20, 4)], 64)]
+
+
+@pytest.mark.parametrize("layers,S", SHAPES)
+@pytest.mark.parametrize("kind", ["higher", "hypergrad"])
+def test_stream_update_equals_chunked(layers, S, kind):
+    from psvi.runtime import InnerLoopPlan
+
+    plan = InnerLoopPlan("fullcov", layers, S, 10)
+    assert plan.tiled_floats > 0
+    rng, p0, m0, v0 = _case(layers, S, 11)
+    t = lambda a: torch.tensor(a, device=DEV)
+    eps0 = t(rng.standard_normal(plan.eps_count).astype(np.float32))
+    eps1 = t(rng.standard_normal(plan.eps_count).astype(np.float32))
+    gs = t((0.05 * rng.standard_normal(plan.xshard_count)).astype(np.float32))
+    out = {}
+    for mode in ("packed", "stream", "chunked"):
+        p, m, v = t(p0), t(m0), t(v0)
+        kl = torch.zeros(1, dtype=torch.float64, device=DEV)
+        x = torch.full((plan.xshard_count,), float("nan"), device=DEV)
+        if mode == "packed":
+            plan.mvn_update(eps0, gs, p, m, v, step=3, lr=1e-3, kind=kind, kl_out=kl,
+                            eps_next=eps1, x_next=x)
+        else:
+            _lib().psvi_debug_set(DBG_STREAM_OFF, 1 if mode == "chunked" else 0)
+            try:
+                ts = plan.tiled_state()
+                plan.tiled_convert(p, m, v, ts, True)
+                plan.mvn_update_tiled(eps0, gs, p, m, v, ts, step=3, lr=1e-3, kind=kind,
+                                      kl_out=kl, eps_next=eps1, x_next=x)
+                plan.tiled_convert(p, m, v, ts, False)
+            finally:
+                _lib().psvi_debug_set(DBG_STREAM_OFF, 0)
+        torch.cuda.synchronize()
+        out[mode] = [a.cpu().numpy() for a in (p, m, v, x)] + [kl.item()]
+    ref = out["packed"]
+    for mode in ("stream", "chunked"):
+        p, m, v, x, kl = out[mode]
+        assert np.isfinite(x).all(), mode
+        assert l2rel(x, ref[3]) < 1e-6, (mode, l2rel(x, ref[3]))
+        assert rel(kl, ref[4]) < 1e-6, mode
+        for a, b, what in ((p, ref[0], "p"), (m, ref[1], "m"), (v, ref[2], "v")):
+            d = np.abs(a.astype(np.float64) - b)
+            assert d.max() <= 1e-6 * max(np.abs(b).max(), 1e-30), (mode, what, d.max())
+    # corr / m / v: the same arithmetic in both kernels (the sample sums in the
+    # same pairs and order), up to the compiler's fma contraction of Adam
+    for k in range(3):
+        a, b = out["stream"][k].astype(np.float64), out["chunked"][k]
+        assert np.abs(a - b).max() <= 1e-7 * np.abs(b).max(), k
+
+
+def test_c3_inner_loop_stream_matches_oracle():
+    """Three chained C3 steps through psvi_inner_loop (fused, tiled, streaming)
+    against the chunked kernel's loop (tight) and the float64 oracle's
+    trajectory (Adam turns sub-rounding gradient entries into +-lr steps, so
+    both fp32 paths sit the same distance from it)."""
+    from psvi.runtime import InnerLoopPlan
+
+    layers, S, M, T = [(64, 40), (40, 40), (40, 2)], 128, 100, 3
+    rng = np.random.default_rng(5)
+    _, p0, _, _ = _case(layers, S, 5)
+    u = rng.standard_normal((M, 64)).astype(np.float32)
+    z = rng.integers(0, 2, M).astype(np.int32)
+    w = O.coreset_weights(0.3 * rng.standard_normal(M), 800).astype(np.float32)
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    eps = rng.standard_normal((T, plan.eps_count)).astype(np.float32)
+    t = lambda a, d=torch.float32: torch.tensor(a, dtype=d, device=DEV)
+    res = {}
+    for off in (0, 1):
+        _lib().psvi_debug_set(DBG_STREAM_OFF, off)
+        try:
+            p = t(p0)
+            m, v = torch.zeros_like(p), torch.zeros_like(p)
+            e = plan.inner_loop(t(u), t(z, torch.int32), t(w), p, m, v, T, 1e-3, eps=t(eps))
+            res[off] = (e.cpu().numpy(), p.cpu().numpy())
+        finally:
+            _lib().psvi_debug_set(DBG_STREAM_OFF, 0)
+    o_elbo, _, o_traj, _, _ = O.run_inner_loop("mvn", layers, p0, u, z, w, eps, S, 1e-3, "higher")
+    (es, ps), (ec, pc) = res[0], res[1]
+    assert np.all(np.abs(es - o_elbo) <= 1e-5 * np.abs(o_elbo)), (es, o_elbo)
+    assert np.all(np.abs(es - ec) <= 1e-6 * np.abs(ec))
+    assert l2rel(ps, pc) < 1e-6
+    e_s, e_c = l2rel(ps, o_traj[-1]), l2rel(pc, o_traj[-1])
+    print(f"C3 T={T}: params l2rel vs oracle stream {e_s:.2e} chunked {e_c:.2e}")
+    assert e_s < 2 * e_c + 1e-6 and e_s < 1e-3
+    assert np.abs(ps - o_traj[-1]).max() <= 2 * T * 1e-3
