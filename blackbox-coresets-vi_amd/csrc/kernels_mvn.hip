@@ -845,8 +845,7 @@ struct StrArgs {
     float* part;
     double* kl_out;
     int include_kl;
-    int abl;                       // diagnostics ablation mask (0 in production)
-    unsigned long long* stamps;    // diagnostics: 16 slots per workgroup (nullptr in production)
+    unsigned long long* stamps;    // diagnostics: 16 slots per workgroup (DIAG build only)
     float inv_s0sq, log_s0;
     AdamC adam;
     int xcol[kMaxL];
@@ -893,7 +892,8 @@ __device__ __forceinline__ float adam_fast_k(const AdamC& a, float p, float g, f
 constexpr int kStrBuf = 128 * 16;  // float4 per eps block buffer ([128 samples][16 slots])
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // plain vector loads / stores (no memcpy)
 
-template <int NS, int KIND>  // NS = S / 32; KIND: Adam variant
+// NS = S / 32; KIND: Adam variant; DIAG: the diagnostics build (phase stamps)
+template <int NS, int KIND, bool DIAG = false>
 __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     constexpr int KT = 16 * NS;  // K steps of the dL GEMM (2 samples each)
     // [0, 4 kStrBuf): eps / eps' blocks, two buffers; then the band's G slice [128][64]
@@ -910,13 +910,12 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     // diagnostics: shader clocks per phase summed over the run's tiles (thread 0)
     unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
     auto ph = [&](int q) __attribute__((always_inline)) {
-        if (a.stamps && tid == 0) {
+        if (DIAG && tid == 0) {
             const unsigned long long tt = __builtin_amdgcn_s_memtime();
             if (q >= 0) tph[q] += tt - tlast;
             tlast = tt;
         }
     };
-    const int ab = a.abl;
     const int e_hi = (int)a.e_total - 4, g_hi = (int)a.g_total - 4;
 
     // eps / eps' block of a tile: 8 + 8 float4 per thread, registers then LDS
@@ -925,7 +924,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
-            const int off = (ab & 1) ? 4 * c4 : min(T.eoff + s * T.n + 64 * T.k + 4 * c4, e_hi);
+            const int off = min(T.eoff + s * T.n + 64 * T.k + 4 * c4, e_hi);
             ereg[j] = *reinterpret_cast<const f32x4*>(a.eps + off);
             enreg[j] = *reinterpret_cast<const f32x4*>(a.eps_next + off);
         }
@@ -985,7 +984,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     auto load_pmv = [&](const StrTile& T) __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const int64_t o = (ab & 1) ? (int64_t)((wv * 4 + g) * 64 + lane) * 4 : frag_off(T, g);
+            const int64_t o = frag_off(T, g);
             P[g] = *reinterpret_cast<const f32x4*>(a.tp + o);
             M4[g] = *reinterpret_cast<const f32x4*>(a.tm + o);
             V4[g] = *reinterpret_cast<const f32x4*>(a.tv + o);
@@ -1011,7 +1010,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     for (int g = 0; g < 4; ++g) okx[g] = l32 * 16 + ((8 * wc + 2 * g + h) ^ (l32 & 15));
     const int ogb = h * 64 + 32 * wr + l32;  // G[2t + h][32wr + l32] at ogb + 128 t
 
-    if (a.stamps && tid == 0) {
+    if (DIAG && tid == 0) {
         a.stamps[(size_t)blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
         a.stamps[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1041,12 +1040,10 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
         floatx16 acc;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-        if (!(ab & 2)) {
 #pragma unroll
-            for (int t = 0; t < KT; ++t)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ef[okd[t & 7] + 128 * t],
-                                                           Gl[ogb + 128 * t], acc, 0, 0, 0);
-        }
+        for (int t = 0; t < KT; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ef[okd[t & 7] + 128 * t], Gl[ogb + 128 * t],
+                                                       acc, 0, 0, 0);
         ph(0);
         const int n = cur.n, r = 64 * cur.b + 32 * wr + l32;
         // ---- diagonal tile: sum_s G and sum_s G eps of the band's rows -> mean / sd
@@ -1115,8 +1112,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
                 if (q < 16) {
                     const int j = q >> 1;
                     const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
-                    const int off = (ab & 1) ? 4 * c4
-                                             : min(nxt.eoff + s * nxt.n + 64 * nxt.k + 4 * c4, e_hi);
+                    const int off = min(nxt.eoff + s * nxt.n + 64 * nxt.k + 4 * c4, e_hi);
                     if ((q & 1) == 0) ereg[j] = *reinterpret_cast<const f32x4*>(a.eps + off);
                     else enreg[j] = *reinterpret_cast<const f32x4*>(a.eps_next + off);
                 } else if constexpr (newband) {
@@ -1146,11 +1142,9 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
                 Lf[4 * g + e] = pn[e];
             }
             const int64_t o = frag_off(cur, g);
-            if (!(ab & 4)) {
-                *reinterpret_cast<f32x4*>(a.tp + o) = f32x4{pn[0], pn[1], pn[2], pn[3]};
-                *reinterpret_cast<f32x4*>(a.tm + o) = f32x4{mn[0], mn[1], mn[2], mn[3]};
-                *reinterpret_cast<f32x4*>(a.tv + o) = f32x4{vn[0], vn[1], vn[2], vn[3]};
-            }
+            *reinterpret_cast<f32x4*>(a.tp + o) = f32x4{pn[0], pn[1], pn[2], pn[3]};
+            *reinterpret_cast<f32x4*>(a.tm + o) = f32x4{mn[0], mn[1], mn[2], mn[3]};
+            *reinterpret_cast<f32x4*>(a.tv + o) = f32x4{vn[0], vn[1], vn[2], vn[3]};
             // x' += eps' L'^T over this group's 8 columns, all sample blocks; the
             // A fragments are read one slot ahead, and each slot is pinned
             // (sched_barrier) so the loads stay spread between the MFMAs
@@ -1159,12 +1153,10 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
                 const int k = g * NS + sb;
                 const f32x4 av = avn;
                 if (k + 1 < 4 * NS) avn = En[okx[(k + 1) / NS] + 512 * ((k + 1) % NS)];
-                if (!(ab & 2)) {
-                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], Lf[4 * g + 0], xacc[sb], 0, 0, 0);
-                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1], Lf[4 * g + 1], xacc[sb], 0, 0, 0);
-                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[2], Lf[4 * g + 2], xacc[sb], 0, 0, 0);
-                    xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[3], Lf[4 * g + 3], xacc[sb], 0, 0, 0);
-                }
+                xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], Lf[4 * g + 0], xacc[sb], 0, 0, 0);
+                xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1], Lf[4 * g + 1], xacc[sb], 0, 0, 0);
+                xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[2], Lf[4 * g + 2], xacc[sb], 0, 0, 0);
+                xacc[sb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[3], Lf[4 * g + 3], xacc[sb], 0, 0, 0);
                 // this slot's share of the next tile's loads (slot k of 4 NS)
                 constexpr int NSLOT = 4 * NS;
 #pragma unroll
@@ -1209,7 +1201,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
         ph(6);
         __syncthreads();  // buffer bi ^ 1 complete; buffer bi free
         ph(7);
-        if (tid == 0) ++tph[9];
+        if (DIAG && tid == 0) ++tph[9];
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
@@ -1233,7 +1225,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
         cur = nxt;
     }
     tile(t1 - 1, cur, F_{}, F_{});
-    if (a.stamps && tid == 0) {
+    if (DIAG && tid == 0) {
         unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
 #pragma unroll
         for (int q = 0; q < 10; ++q) o[q] = tph[q];
@@ -1425,7 +1417,6 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             b.part = p.d_str_part;
             b.kl_out = kl_out;
             b.include_kl = include_kl;
-            b.abl = g_upd_ablation;
             b.stamps = g_upd_stamps;
             b.inv_s0sq = a.inv_s0sq;
             b.log_s0 = a.log_s0;
@@ -1436,7 +1427,10 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             }
             fill_layers(p, b.lay);
             const dim3 sg(p.n_str);
-            launch_stream(a.S / 32, b.adam.kind, sg, block, st, b);
+            if (b.stamps && a.S == 128 && b.adam.kind == PSVI_ADAM_HIGHER)
+                hipLaunchKernelGGL((mvn_stream_kernel<4, PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
+            else
+                launch_stream(a.S / 32, b.adam.kind, sg, block, st, b);
             FwdArgs f{};
             f.params = params;
             f.eps = eps_next;
