@@ -1043,9 +1043,10 @@ int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, cons
     return 0;
 }
 
-int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
-             const float* eps, const float* params, const float* vec, float* hv_out,
-             float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream) {
+int psvi_hvp_partial(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                     const float* eps, const float* params, const float* vec,
+                     int32_t include_kl, float* hv_out, float* du_out, float* dw_out, void* ws,
+                     size_t ws_bytes, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "psvi_hvp needs world == 1");
@@ -1055,7 +1056,7 @@ int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* 
         if (!ws || ws_bytes < lenet_tan_ws(*p, nullptr).bytes)
             return fail(PSVI_ENOSPC, "workspace too small");
         HIP_TRY(launch_lenet_hvp(*p, u, z, w, eps, params, vec, hv_out, du_out, dw_out, ws,
-                                 as_stream(stream)));
+                                 as_stream(stream), include_kl != 0));
         return 0;
     }
     if (rop_rows(*p) == 0)
@@ -1077,8 +1078,15 @@ int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* 
         HIP_TRY(launch_mvn_update(*p, eps, o.Gd, const_cast<float*>(params), nullptr, nullptr,
                                   nullptr, nullptr, hv_out, 0, nullptr, nullptr, st));
     HIP_TRY(launch_hvp_assemble(*p, params, vec, eps, o.G, o.Gd, o.du, o.nlld, hv_out, du_out,
-                                dw_out, st));
+                                dw_out, st, include_kl != 0));
     return 0;
+}
+
+int psvi_hvp(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+             const float* eps, const float* params, const float* vec, float* hv_out,
+             float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream) {
+    return psvi_hvp_partial(p, u, z, w, eps, params, vec, 1, hv_out, du_out, dw_out, ws,
+                            ws_bytes, stream);
 }
 
 int psvi_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const float* adam_m,

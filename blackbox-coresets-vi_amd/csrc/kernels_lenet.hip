@@ -808,13 +808,16 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     for (int i = tid; i < 150; i += kConvThreads) { w1[i] = ws[i]; wd1[i] = wds[i]; }
     for (int i = tid; i < 2400; i += kConvThreads) { w2[i] = ws[156 + i]; wd2[i] = wds[156 + i]; }
     constexpr int kR2 = (2400 + kConvThreads - 1) / kConvThreads;
-    int kb[kR2], pb[kR2];
-#pragma unroll
-    for (int r = 0; r < kR2; ++r) {
+    // the conv2 weight e's routed-gradient base (kb) and P1 tap base (pb) are
+    // formed where they are read: kept in 16 registers across the image loop
+    // they pushed the kernel into scratch spills
+    auto kb = [&](int r) __attribute__((always_inline)) {
+        return (min(tid + r * kConvThreads, 2399) / 150) * 25;
+    };
+    auto pb = [&](int r) __attribute__((always_inline)) {
         const int e = min(tid + r * kConvThreads, 2399);
-        kb[r] = (e / 150) * 25;
-        pb[r] = ((e % 150) / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
-    }
+        return ((e % 150) / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
+    };
     float accw2[kR2];
 #pragma unroll
     for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
@@ -862,10 +865,11 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
         for (int r = 0; r < kR2; ++r) {
             if (tid + r * kConvThreads < 2400) {
                 float acc = 0.f;
+                const int kbr = kb(r), pbr = pb(r);
 #pragma unroll
                 for (int p = 0; p < 25; ++p) {
-                    const int q = pb[r] + off2[kb[r] + p];
-                    acc += g2d[kb[r] + p] * p1[q] + g2[kb[r] + p] * p1d[q];
+                    const int q = pbr + off2[kbr + p];
+                    acc += g2d[kbr + p] * p1[q] + g2[kbr + p] * p1d[q];
                 }
                 accw2[r] += acc;
             }
@@ -956,7 +960,7 @@ __global__ __launch_bounds__(kThreads) void lenet_hvp_assemble_kernel(
     SampleArgs a, const float* __restrict__ params, const float* __restrict__ vec,
     const float* __restrict__ eps, const float* __restrict__ G, const float* __restrict__ Gd,
     const float* __restrict__ dud, const float* __restrict__ nlld, float* __restrict__ hv,
-    float* __restrict__ d_u, float* __restrict__ d_w, int M, float inv_s0sq) {
+    float* __restrict__ d_u, float* __restrict__ d_w, int M, float inv_s0sq, int include_kl) {
     const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
     if (i < a.n_tot) {
         const int j = (int)i;
@@ -974,7 +978,7 @@ __global__ __launch_bounds__(kThreads) void lenet_hvp_assemble_kernel(
         const float r = params[pr], sp = softplus_f(r), sg = sigmoid_f(r);
         const float vr = vec[pr];
         float hm = gd, hr = gde * sg + ge * sg * (1.f - sg) * vr;
-        if (l >= 2) {  // KL on the VILinear layers
+        if (l >= 2 && include_kl) {  // KL on the VILinear layers (not in a shard's partial)
             hm += vec[pm] * inv_s0sq;
             hr += ((1.f / (sp * sp) + inv_s0sq) * sg * sg + (sp * inv_s0sq - 1.f / sp) * sg * (1.f - sg)) * vr;
         }
@@ -1204,7 +1208,7 @@ LenetTanWs lenet_tan_ws(const psvi_plan& p, void* base) {
 
 hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                             const float* eps, const float* params, const float* vec, float* hv,
-                            float* d_u, float* d_w, void* tws, hipStream_t st) {
+                            float* d_u, float* d_w, void* tws, hipStream_t st, bool include_kl) {
     const LenetWs W = lenet_ws(p, p.d_lenet_ws);
     const LenetTanWs T = lenet_tan_ws(p, tws);
     const SampleArgs sa = sample_args(p);
@@ -1300,7 +1304,8 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
     const int64_t n = nt + (d_u ? (int64_t)M * 784 : 0) + (d_w ? M : 0);
     hipLaunchKernelGGL(lenet_hvp_assemble_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
                        dim3(kThreads), 0, st, sa, params, vec, eps, W.dws, T.gd, T.du, T.nlld, hv,
-                       d_u, d_w, M, 1.f / (p.d.prior_sd * p.d.prior_sd));
+                       d_u, d_w, M, 1.f / (p.d.prior_sd * p.d.prior_sd),
+                       include_kl ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -1348,18 +1348,18 @@ template <int NS>
 static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
     if (kind == PSVI_ADAM_HIGHER)
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER>), g, bl, 0, st, b);
-    else if (kind == PSVI_ADAM_TORCH)
-        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_TORCH>), g, bl, 0, st, b);
     else
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HYPERGRAD>), g, bl, 0, st, b);
 }
+// the trainers' variants (higher / hypergrad Adam) at S = 128 (C3 and the
+// sharded C4 per-GPU count); other S take the chunked kernel (the stream
+// kernel's narrower instantiations spilled their scalar registers to scratch)
+static bool stream_ok(int S, int kind) {
+    return S == 128 && (kind == PSVI_ADAM_HIGHER || kind == PSVI_ADAM_HYPERGRAD);
+}
 static void launch_stream(int ns, int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
-    switch (ns) {
-        case 1: launch_stream_ns<1>(kind, g, bl, st, b); break;
-        case 2: launch_stream_ns<2>(kind, g, bl, st, b); break;
-        case 3: launch_stream_ns<3>(kind, g, bl, st, b); break;
-        default: launch_stream_ns<4>(kind, g, bl, st, b); break;
-    }
+    (void)ns;
+    launch_stream_ns<4>(kind, g, bl, st, b);
 }
 
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
@@ -1398,7 +1398,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         a.tp = tstate;
         a.tm = tstate + tf;
         a.tv = tstate + 2 * tf;
-        if (eps_next && p.n_str > 0 && !g_stream_off) {
+        if (eps_next && p.n_str > 0 && !g_stream_off && stream_ok(a.S, a.adam.kind)) {
             StrArgs b{};
             b.ranges = p.d_str;
             b.eps = eps;

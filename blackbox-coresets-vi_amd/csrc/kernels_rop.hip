@@ -237,9 +237,11 @@ __global__ __launch_bounds__(256) void hvp_tangent_kernel(RopArgs a, float* T) {
 // corr prior terms, then d_u (M x D), then d_w (M).
 __global__ __launch_bounds__(256) void hvp_assemble_kernel(RopArgs a, float* hv, float* d_u,
                                                            float* d_w, int64_t ncorr_tot,
-                                                           float inv_s0sq) {
+                                                           float inv_s0sq, float klw) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int D = a.din[0];
+    // klw = 0: a sample shard's partial product without the KL Hessian
+    const float kls = klw * inv_s0sq;
     if (i < a.n_tot) {
         const int e = (int)i;
         int l = 0;
@@ -261,14 +263,14 @@ __global__ __launch_bounds__(256) void hvp_assemble_kernel(RopArgs a, float* hv,
         }
         const float r = a.params[ps], sp = softplus_f(r), sg = sigmoid_f(r);
         const float vsd = a.vec[ps];
-        const float kl2 = (1.f / (sp * sp) + inv_s0sq) * sg * sg + (sp * inv_s0sq - 1.f / sp) * sg * (1.f - sg);
+        const float kl2 = klw * ((1.f / (sp * sp) + inv_s0sq) * sg * sg + (sp * inv_s0sq - 1.f / sp) * sg * (1.f - sg));
         const float curv = ge * sg * (1.f - sg) * vsd + kl2 * vsd;
         if (a.family == PSVI_FAMILY_FULLCOV) {
             // the update kernel's gradient mode already wrote sum G_dot, diag(G_dot^T E) sg
-            hv[pm] += a.vec[pm] * inv_s0sq;
+            hv[pm] += a.vec[pm] * kls;
             hv[ps] += curv;
         } else {
-            hv[pm] = gd + a.vec[pm] * inv_s0sq;
+            hv[pm] = gd + a.vec[pm] * kls;
             hv[ps] = gde * sg + curv;
         }
         return;
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(256) void hvp_assemble_kernel(RopArgs a, float* hv,
             const int64_t nc = (int64_t)(n - 1) * (n - 2) / 2;
             if (j < base + nc) {
                 const int64_t pc = a.poff[l] + 2 * n + (j - base);
-                hv[pc] += a.vec[pc] * inv_s0sq;
+                hv[pc] += a.vec[pc] * kls;
                 return;
             }
             base += nc;
@@ -414,7 +416,7 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
 hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const float* vec,
                                const float* eps, const float* G, const float* Gd, const float* du,
                                const float* nlld, float* hv, float* d_u, float* d_w,
-                               hipStream_t st) {
+                               hipStream_t st, bool include_kl) {
     RopArgs a{};
     rop_fill(p, a);
     a.params = params; a.vec = vec; a.eps = eps;
@@ -428,7 +430,7 @@ hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const fl
     const int64_t total = p.n_tot + nct + (int64_t)p.d.M * p.lay[0].din + p.d.M;
     const float s0 = p.d.prior_sd;
     hipLaunchKernelGGL(hvp_assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       st, a, hv, d_u, d_w, nct, 1.f / (s0 * s0));
+                       st, a, hv, d_u, d_w, nct, 1.f / (s0 * s0), include_kl ? 1.f : 0.f);
     return hipGetLastError();
 }
 

@@ -360,7 +360,8 @@ struct LenetTanWs {
 LenetTanWs lenet_tan_ws(const psvi_plan& p, void* base);
 hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                             const float* eps, const float* params, const float* vec, float* hv,
-                            float* d_u, float* d_w, void* tws, hipStream_t st);
+                            float* d_u, float* d_w, void* tws, hipStream_t st,
+                            bool include_kl = true);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
 hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,
@@ -372,5 +373,5 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
 hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const float* vec,
                                const float* eps, const float* G, const float* Gd, const float* du,
                                const float* nlld, float* hv, float* d_u, float* d_w,
-                               hipStream_t st);
+                               hipStream_t st, bool include_kl = true);
 }  // namespace psvi

@@ -75,20 +75,33 @@ __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PS
            "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
 
 class HipInnerELBO(torch.autograd.Function):
-    """Negative inner ELBO and its parameter gradient in one HIP call.
-    Inputs other than the flat parameter vector are constants."""
+    """Negative inner ELBO as an autograd node over one psvi_elbo_grad call
+    (value and parameter gradient computed by the caller, PSVI.inner_elbo).
+    u_g / w_g are the rows' inputs and weights carrying their graphs to u, v
+    and alpha: when the backward is asked for them it forms d/du and d/dw of
+    the weighted NLL with ``rows_fn`` (the outer-objective kernel in
+    coefficient mode, every sample's pseudo term with coefficient 1) -- what
+    the reference's autograd delivers through inner_elbo
+    (psvi_classes.py:488-511)."""
 
     @staticmethod
-    def forward(ctx, pvec, plan, u, z, w, eps):
-        elbo, grad = plan.elbo_grad(u, z, w, eps, pvec.detach().contiguous())
+    def forward(ctx, pvec, u_g, w_g, elbo, grad, rows_fn):
         ctx.save_for_backward(grad)
-        return elbo.to(pvec.dtype).reshape(())
+        ctx.rows_fn = rows_fn
+        ctx.shapes = (u_g.shape, u_g.dtype, w_g.shape, w_g.dtype)
+        return elbo.to(pvec.dtype).reshape(()).clone()
 
     @staticmethod
     @once_differentiable
     def backward(ctx, gout):
         (grad,) = ctx.saved_tensors
-        return gout * grad, None, None, None, None, None
+        gu = gw = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            us, ut, ws, wt = ctx.shapes
+            du, dw = ctx.rows_fn()
+            gu = (gout * du).reshape(us).to(ut) if ctx.needs_input_grad[1] else None
+            gw = (gout * dw).reshape(ws).to(wt) if ctx.needs_input_grad[2] else None
+        return gout * grad, gu, gw, None, None, None
 
 
 class HipOuterELBO(torch.autograd.Function):
@@ -153,7 +166,8 @@ class PSVI:
     def __init__(self, u=None, z=None, N=None, D=None, model=None, num_pseudo=None, seed=0,
                  mc_samples=None, learn_v=False, f=lambda *x: x[0], distr_fn=categorical_fn,
                  nc=None, register_elbos=True, inner_it=10, log_every=10, lr0net=1e-3,
-                 device_id=None, learn_z=False, compute_weights_entropy=True, **kwargs):
+                 device_id=None, learn_z=False, compute_weights_entropy=True, world=1, rank=0,
+                 comm=None, **kwargs):
         if learn_z:
             raise NotImplementedError("soft labels (learn_z) are not on the HIP inner loop")
         if distr_fn is not categorical_fn:
@@ -190,6 +204,14 @@ class PSVI:
         self._plans = {}
         self._eps_offset = 0
         self._labels_ok = None
+        # samples split over `world` ranks (one process per GPU):
+        # every objective / HVP sums the ranks' shares with one all-reduce
+        self.world, self.rank = int(world), int(rank)
+        if self.world > 1 and comm is None:
+            from ..runtime.sharded import TorchDistComm
+            comm = TorchDistComm()
+        self.comm = comm
+        self._make_plan = InnerLoopPlan
 
     # ------------------------------------------------------------ helpers
     def coreset_weights(self):
@@ -222,8 +244,22 @@ class PSVI:
             M *= layers[-1][1]
         key = (fam, tuple(layers), S, M, prior_sd)
         if key not in self._plans:
-            self._plans[key] = InnerLoopPlan(fam, layers, S, M, prior_sd=prior_sd)
+            self._plans[key] = self._new_plan(fam, layers, S, M, prior_sd, outer=False)
         return self._plans[key]
+
+    def _new_plan(self, fam, layers, S, M, prior_sd, outer):
+        """A world-1 plan, or with world > 1 the sample-sharded form of one
+        (this rank's samples; results all-reduced): SampleShardedPlan for the
+        inner objective and its HVP, ShardedOuter for the outer objective."""
+        if self.world == 1:
+            return self._make_plan(fam, layers, S, M, prior_sd=prior_sd)
+        from ..runtime.sharded import SampleShardedPlan, ShardedOuter, sample_split
+
+        s_cnt = sample_split(S, self.world)[self.rank][1]
+        local = self._make_plan(fam, layers, s_cnt, M, prior_sd=prior_sd)
+        cls = ShardedOuter if outer else SampleShardedPlan
+        return cls(fam, layers, S, M, self.world, self.rank, prior_sd=prior_sd, comm=self.comm,
+                   plan=local)
 
     def _check_labels(self, z, C):
         """Class ids in [0, C) -- validated once per label tensor version (a
@@ -261,6 +297,44 @@ class PSVI:
                 torch.arange(C, dtype=torch.int32, device=self.device).repeat(M0).contiguous(),
                 Wc.repeat(M0).contiguous())
 
+    def _rows_graph(self, plan):
+        """_data's rows as functions of the hyperparameters: the row inputs
+        (from u) and weights (N f(v), through v / alpha) with their autograd
+        graphs, for the functional inner loop (psvi.robust_higher) and for
+        inner_elbo's gradients w.r.t. u and v."""
+        M0 = int(self.u.shape[0])
+        u_g = self.u.reshape(M0, plan.in_features)
+        w_g = (self.N * self.f(self.v, 0)).reshape(-1)
+        if plan.M == M0:
+            return u_g, w_g
+        C = plan.layers[-1][1]
+        z = self.z.detach().to(w_g.device).long()
+        Wc = torch.zeros(C, dtype=w_g.dtype, device=w_g.device).index_add(0, z, w_g)
+        return u_g.repeat_interleave(C, 0), Wc.repeat(M0)
+
+    def _row_grad_fn(self, model, plan, u, z, w, eps, pvec):
+        """() -> (d/du, d/dw) of sum_s sum_m w_m NLL_sm over the plan's rows:
+        psvi_outer_elbo_grad_coef with pseudo coefficient 1 for every sample
+        (the KL term does not depend on the rows)."""
+        from ..runtime.sharded import ShardedOuter, pack_coef
+
+        fam, layers, prior_sd, S = model_spec(model)
+        key = ("rows", fam, tuple(layers), S, plan.M, prior_sd)
+        if key not in self._plans:
+            self._plans[key] = self._new_plan(fam, layers, S, plan.M, prior_sd, outer=True)
+        op = self._plans[key]
+
+        def fn():
+            one = torch.ones(S, dtype=torch.float64)
+            zero = torch.zeros(S, dtype=torch.float64)
+            if isinstance(op, ShardedOuter):
+                g = op.coef_grads(plan.M, u, z, w, eps, pvec, one, zero, zero)
+            else:
+                g = op.outer_grad_coef(plan.M, u, z, w, eps, pvec,
+                                       pack_coef(one, zero, zero, 0, S).to(pvec.device))
+            return g["grad_u"], g["grad_w"]
+        return fn
+
     def _fold(self, plan, du, dw):
         """Row gradients of _data's rows back onto the pseudopoints."""
         M0 = int(self.u.shape[0])
@@ -271,7 +345,20 @@ class PSVI:
         return (du.reshape(M0, C, -1).sum(1),
                 dw.reshape(M0, C).sum(0)[z])
 
+    def replay_eps(self, draws):
+        """Serve the next objective evaluations' noise from ``draws`` (the
+        library's eps layout, in call order) instead of the Philox stream --
+        to replay the reference's own draws through code that calls
+        inner_elbo / psvi_elbo itself (the functional inner loop)."""
+        self._eps_feed = iter(list(draws))
+
     def _draw_eps(self, plan):
+        feed = getattr(self, "_eps_feed", None)
+        if feed is not None:
+            e = next(feed, None)
+            if e is not None:
+                return e.to(self.device, torch.float32).reshape(-1).contiguous()
+            self._eps_feed = None
         eps = torch.empty(plan.eps_count, device=self.device)
         randn_(eps, self.seed, self._eps_offset)
         self._eps_offset += plan.eps_stride  # Philox offsets move in quads
@@ -285,7 +372,10 @@ class PSVI:
         otherwise the model's own parameters are used.  Fresh eps per call
         (Philox stream of this instance) unless ``eps`` (the library's eps
         layout, ``InnerLoopPlan.eps_count`` floats) is given.  Differentiable
-        w.r.t. those parameters (first order); u and v are constants here."""
+        (first order) w.r.t. those parameters and -- as the reference's
+        autograd -- w.r.t. u and v / alpha where they require grad.  The result
+        carries ``_psvi_inner`` (plan, rows, draw, gradient) for
+        psvi.robust_higher's differentiable optimiser."""
         model = self.model if model is None else model
         plan = self._plan(model)
         plist = list(params) if (hyperopt and params is not None) else list(model.parameters())
@@ -294,7 +384,14 @@ class PSVI:
             raise ValueError(f"{pvec.numel()} parameters, plan expects {plan.param_count}")
         u, z, w = self._data(plan)
         eps = self._draw_eps(plan) if eps is None else eps
-        return HipInnerELBO.apply(pvec, plan, u, z, w, eps)
+        p = pvec.detach().to(torch.float32).contiguous()
+        elbo, grad = plan.elbo_grad(u, z, w, eps, p)
+        u_g, w_g = self._rows_graph(plan)
+        out = HipInnerELBO.apply(pvec, u_g, w_g, elbo, grad,
+                                 self._row_grad_fn(model, plan, u, z, w, eps, p))
+        out._psvi_inner = dict(plan=plan, u=u, z=z, w=w, eps=eps, u_g=u_g, w_g=w_g, grad=grad,
+                               params=p)
+        return out
 
     def inner_loop(self, T=None, model=None, lr=None, kind="higher", eps=None):
         """T fused HIP inner steps from the model's current parameters with a
@@ -476,7 +573,7 @@ class PSVI:
         Mu = int(self.u.shape[0]) if n_pseudo is None else int(n_pseudo)
         key = ("outer", fam, tuple(layers), S, Mu + Nx, prior_sd)
         if key not in self._plans:
-            self._plans[key] = InnerLoopPlan(fam, layers, S, Mu + Nx, prior_sd=prior_sd)
+            self._plans[key] = self._new_plan(fam, layers, S, Mu + Nx, prior_sd, outer=True)
         return self._plans[key]
 
     def _alpha(self):

@@ -374,7 +374,9 @@ def model_spec(model):
     """(family, [(in, out), ...], prior_sd, mc_samples) of a model the HIP inner
     loop can run: an nn.Sequential of variational linear layers of one family
     with ReLU between them, or make_lenet's stack (family "lenet").  Raises
-    ValueError otherwise."""
+    ValueError otherwise.  A functional view (psvi.robust_higher's fmodel)
+    reports the spec of the module it wraps."""
+    model = getattr(model, "_psvi_module", model)
     if not isinstance(model, nn.Sequential):
         raise ValueError("the HIP inner loop runs nn.Sequential VI stacks (make_fcnet / "
                          "make_fc2net / make_logreg / make_lenet)")

@@ -93,6 +93,7 @@ SIGNATURES = {
                                          _SZ, _P]),
     "psvi_evaluate": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _SZ, _P]),
     "psvi_hvp": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "psvi_hvp_partial": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _SZ, _P]),
     "psvi_adam_adjoint": (_I32, [_I64, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP),
                                  _P]),
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),

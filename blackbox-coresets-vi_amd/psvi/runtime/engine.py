@@ -297,10 +297,12 @@ class InnerLoopPlan:
               "psvi_evaluate")
         return stats, pr
 
-    def hvp(self, u, z, w, eps, params, vec, mixed=True, out=None, ws=None):
+    def hvp(self, u, z, w, eps, params, vec, mixed=True, out=None, ws=None, include_kl=True):
         """Hessian-vector product of the negative inner ELBO at fixed eps
         (psvi_hvp).  Returns (hv, d_u, d_w): H vec and, with mixed=True, the
-        mixed products d/du and d/dw of vec . grad (else None, None)."""
+        mixed products d/du and d/dw of vec . grad (else None, None).
+        include_kl=False: this plan's samples' share without the KL Hessian
+        (psvi_hvp_partial, one rank of a sample-sharded product)."""
         self._inputs(u, z, w, eps)
         _need(params, "params", self.param_count)
         _need(vec, "vec", self.param_count)
@@ -311,9 +313,10 @@ class InnerLoopPlan:
         dw = torch.empty(self.M, dtype=torch.float32, device=dev) if mixed else None
         if ws is None or ws.numel() < self.hvp_ws_bytes:
             ws = torch.empty(self.hvp_ws_bytes, dtype=torch.uint8, device=dev)
-        check(self.lib.psvi_hvp(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps), _ptr(params),
-                                _ptr(vec), _ptr(hv), _ptr(du), _ptr(dw), _ptr(ws), ws.numel(),
-                                _stream()), "psvi_hvp")
+        check(self.lib.psvi_hvp_partial(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps),
+                                        _ptr(params), _ptr(vec), int(bool(include_kl)), _ptr(hv),
+                                        _ptr(du), _ptr(dw), _ptr(ws), ws.numel(), _stream()),
+              "psvi_hvp_partial")
         return hv, du, dw
 
     # ------------------------------------------------------------ phases
@@ -429,14 +432,15 @@ def randn_(out, seed, offset=0):
     return out
 
 
-def adam_adjoint_(lt, lm, lv, adam_m, adam_v, grad, step, lr, lg_out, kind="higher"):
+def adam_adjoint_(lt, lm, lv, adam_m, adam_v, grad, step, lr, lg_out, kind="higher",
+                  betas=(0.9, 0.999), eps=1e-8):
     """Reverse of one Adam step (psvi_adam_adjoint): lm, lv updated in place,
     lg_out <- adjoint of the step's gradient."""
     n = lt.numel()
     for t, nm in ((lt, "lt"), (lm, "lm"), (lv, "lv"), (adam_m, "adam_m"), (adam_v, "adam_v"),
                   (grad, "grad"), (lg_out, "lg_out")):
         _need(t, nm, n)
-    hp = make_adam(lr, step, kind)
+    hp = make_adam(lr, step, kind, betas, eps)
     lib = _lib.load()
     check(lib.psvi_adam_adjoint(n, _ptr(lt), _ptr(lm), _ptr(lv), _ptr(adam_m), _ptr(adam_v),
                                 _ptr(grad), _ptr(lg_out), ctypes.byref(hp), _stream()),
@@ -444,11 +448,12 @@ def adam_adjoint_(lt, lm, lv, adam_m, adam_v, grad, step, lr, lg_out, kind="high
     return lg_out
 
 
-def adam_update_(params, grad, adam_m, adam_v, step, lr, kind="higher"):
+def adam_update_(params, grad, adam_m, adam_v, step, lr, kind="higher", betas=(0.9, 0.999),
+                 eps=1e-8):
     n = params.numel()
     for t, nm in ((params, "params"), (grad, "grad"), (adam_m, "adam_m"), (adam_v, "adam_v")):
         _need(t, nm, n)
-    hp = make_adam(lr, step, kind)
+    hp = make_adam(lr, step, kind, betas, eps)
     lib = _lib.load()
     check(lib.psvi_adam_update(n, _ptr(params), _ptr(grad), _ptr(adam_m), _ptr(adam_v),
                                ctypes.byref(hp), _stream()), "psvi_adam_update")

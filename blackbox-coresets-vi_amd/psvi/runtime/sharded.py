@@ -23,7 +23,7 @@ rank draws it from the same Philox stream, so it never crosses the wire.
 """
 import torch
 
-from .engine import InnerLoopPlan
+from .engine import InnerLoopPlan, adam_update_, randn_
 
 
 class TorchDistComm:
@@ -222,6 +222,8 @@ class ShardedOuter:
             raise ValueError(f"rank {rank} has no samples (S={S}, world={world})")
         self.plan = plan if plan is not None else InnerLoopPlan(family, layers, self.s_cnt, M,
                                                                 prior_sd=prior_sd)
+        self.prior_sd = prior_sd
+        self._full = None
 
     def local_terms(self, n_pseudo, x_all, z_all, w_all, eps, params):
         """Pass 1 -> (eps_local, terms (s_cnt, 3) float64)."""
@@ -237,13 +239,17 @@ class ShardedOuter:
         return self.plan.outer_grad_coef(n_pseudo, x_all, z_all, w_all, eps_local, params, coef,
                                          grad_u=grad_u, grad_w=grad_w)
 
-    def elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad_u=True, grad_w=True):
-        """Loss (float64 tensor) and the full gradients on every rank."""
+    def elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad_u=True, grad_w=True,
+                  grads=True):
+        """Loss (float64 tensor) and the full gradients on every rank
+        (grads=False: the loss only, pass 1 and one all-reduce)."""
         e, t = self.local_terms(n_pseudo, x_all, z_all, w_all, eps, params)
         terms = torch.zeros(self.S, 3, dtype=torch.float64, device=t.device)
         terms[self.s_off:self.s_off + self.s_cnt] = t
         self.comm.all_reduce(terms)
         loss, cp, cd, ck = outer_coefficients(terms)
+        if not grads:
+            return {"loss": loss.reshape(1)}
         g = self.local_grads(n_pseudo, x_all, z_all, w_all, e, params, cp, cd, ck,
                              grad_u=grad_u, grad_w=grad_w)
         for k in ("grad", "grad_u", "grad_w"):
@@ -251,3 +257,169 @@ class ShardedOuter:
                 self.comm.all_reduce(g[k])
         g["loss"] = loss.reshape(1)
         return g
+
+    def coef_grads(self, n_pseudo, x_all, z_all, w_all, eps, params, cp, cd, ck, grad_u=True,
+                   grad_w=True):
+        """Pass 2 alone for given global coefficients (global eps), summed
+        over ranks."""
+        e = local_eps(self.family, self.layers, self.S, self.s_off, self.s_cnt, eps)
+        g = self.local_grads(n_pseudo, x_all, z_all, w_all, e, params, cp, cd, ck,
+                             grad_u=grad_u, grad_w=grad_w)
+        for k in ("grad", "grad_u", "grad_w"):
+            if k in g:
+                self.comm.all_reduce(g[k])
+        return g
+
+    # ---- InnerLoopPlan's outer-objective methods (global eps), for PSVI ----
+    @property
+    def eps_count(self):
+        return eps_count(self.family, self.layers, self.S)
+
+    @property
+    def eps_stride(self):
+        return (self.eps_count + 3) // 4 * 4
+
+    @property
+    def param_count(self):
+        return self.plan.param_count
+
+    @property
+    def in_features(self):
+        return self.plan.in_features
+
+    def outer_elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad=True,
+                        grad_u=True, grad_w=True, sample_stats=False, ws=None):
+        """psvi_outer_elbo_grad's contract over all S samples (loss, grad,
+        grad_u, grad_w as requested; per-sample stats are not assembled)."""
+        if sample_stats:
+            raise NotImplementedError("per-sample stats of a sharded outer objective: use "
+                                      "local_terms")
+        g = self.elbo_grad(n_pseudo, x_all, z_all, w_all, eps, params, grad_u=grad and grad_u,
+                           grad_w=grad_w, grads=grad or grad_w)
+        if not grad:
+            g.pop("grad", None)
+            g.pop("grad_u", None)
+        return g
+
+    def outer_ablated_elbo_grad(self, x_all, z_all, w_all, eps, params, grad=True,
+                                sample_stats=False, ws=None):
+        """PSVI_Ablated's objective mean_s data_s - mean_s nkl_s over all S
+        samples: each rank's mean over its own samples, weighted s_cnt / S, one
+        all-reduce of the loss and the gradient."""
+        if sample_stats:
+            raise NotImplementedError("per-sample stats of a sharded outer objective")
+        e = local_eps(self.family, self.layers, self.S, self.s_off, self.s_cnt, eps)
+        o = self.plan.outer_ablated_elbo_grad(x_all, z_all, w_all, e, params, grad=grad)
+        f = self.s_cnt / self.S
+        for k in ("loss", "grad"):
+            if k in o:
+                o[k] = (o[k] * f).contiguous()
+                self.comm.all_reduce(o[k])
+        return o
+
+    def evaluate(self, n_pseudo, x_all, z_all, w_all, eps, params, correction=True,
+                 probs=False, ws=None):
+        """The importance-weighted predictive (once per log_every outer steps):
+        replicated on every rank on a world-1 plan of all S samples."""
+        if self._full is None:
+            self._full = InnerLoopPlan(self.family, self.layers, self.S, self.M,
+                                       prior_sd=self.prior_sd)
+        return self._full.evaluate(n_pseudo, x_all, z_all, w_all, eps, params,
+                                   correction=correction, probs=probs)
+
+
+# ---------------------------------------------------------------------------
+# Sample-sharded inner objective and second order (PSVI.inner_elbo / inner
+# loop, hyper_step's CG_normaleq products, nested_step's reverse pass)
+# ---------------------------------------------------------------------------
+def eps_count(family, layers, S):
+    """Floats of one draw of all S samples (include/psvi_hip.h eps layout;
+    LeNet's last layer is one shared draw)."""
+    n = 0
+    for l, (din, dout) in enumerate(layers):
+        k = din * dout + dout
+        n += k if (family == "lenet" and l == len(layers) - 1) else S * k
+    return n
+
+
+class SampleShardedPlan:
+    """InnerLoopPlan's inner-objective methods for S samples split over ranks
+    (sample_split): this rank runs a world-1 plan of its own s_cnt samples on
+    its slice of the global eps (local_eps), the sample-independent KL terms on
+    rank 0 only (psvi_elbo_grad include_kl, psvi_hvp_partial), and one
+    all-reduce sums each result.  The contract is a world-1 plan of all S
+    samples -- same eps layout, same Philox draw sequence -- with values equal
+    up to fp32 summation order, so PSVI's trainers run unchanged on it
+    (C4 / C5 at 8 GPUs; hypergradients.py:199-244 and
+    psvi_classes.py:541-687 split over samples).  Parameters and Adam state
+    stay replicated: every rank applies the same all-reduced gradient."""
+
+    def __init__(self, family, layers, S, M, world, rank, comm, prior_sd=1.0, plan=None,
+                 adam=None):
+        self.family, self.layers = family, [tuple(l) for l in layers]
+        self.S, self.M, self.world, self.rank, self.comm = int(S), int(M), world, rank, comm
+        self.split = sample_split(self.S, world)
+        self.s_off, self.s_cnt = self.split[rank]
+        if self.s_cnt < 1:
+            raise ValueError(f"rank {rank} has no samples (S={S}, world={world})")
+        self.plan = plan if plan is not None else InnerLoopPlan(family, layers, self.s_cnt, M,
+                                                                prior_sd=prior_sd)
+        self._adam = adam if adam is not None else adam_update_
+        self.param_count = self.plan.param_count
+        self.in_features = self.plan.in_features
+        self.eps_count = eps_count(family, self.layers, self.S)
+        self.eps_stride = (self.eps_count + 3) // 4 * 4
+        self.ws_bytes = self.plan.ws_bytes
+        self.hvp_ws_bytes = self.plan.hvp_ws_bytes
+        self.n_tot = sum(i * o + o for i, o in self.layers)
+
+    def local(self, eps):
+        return local_eps(self.family, self.layers, self.S, self.s_off, self.s_cnt, eps)
+
+    def workspace(self, device="cuda"):
+        return self.plan.workspace(device)
+
+    def _reduce(self, *ts):
+        for t in ts:
+            if t is not None:
+                self.comm.all_reduce(t)
+
+    def elbo_grad(self, u, z, w, eps, params, include_kl=True, ws=None):
+        e, g = self.plan.elbo_grad(u, z, w, self.local(eps), params,
+                                   include_kl=include_kl and self.rank == 0, ws=ws)
+        self._reduce(e, g)
+        return e, g
+
+    def hvp(self, u, z, w, eps, params, vec, mixed=True, out=None, ws=None, include_kl=True):
+        hv, du, dw = self.plan.hvp(u, z, w, self.local(eps), params, vec, mixed=mixed, out=out,
+                                   ws=ws, include_kl=include_kl and self.rank == 0)
+        self._reduce(hv, du, dw)
+        return hv, du, dw
+
+    def inner_step(self, u, z, w, eps, params, adam_m, adam_v, step, lr, kind="higher",
+                   elbo_out=None, ws=None):
+        """psvi_inner_step's contract: the all-reduced gradient, then the same
+        Adam step on every rank's replica."""
+        e, g = self.elbo_grad(u, z, w, eps, params, ws=ws)
+        self._adam(params, g, adam_m, adam_v, step, lr, kind=kind)
+        if elbo_out is None:
+            return e
+        elbo_out.copy_(e.reshape(elbo_out.shape))
+        return elbo_out
+
+    def inner_loop(self, u, z, w, params, adam_m, adam_v, T, lr, kind="higher", step0=1,
+                   eps=None, seed=0, offset=0, elbo_out=None, ws=None):
+        """psvi_inner_loop's contract (the same Philox draws: step t at
+        offset + t * eps_stride of the global layout)."""
+        T = int(T)
+        dev = params.device
+        out = elbo_out if elbo_out is not None else torch.empty(max(T, 1), dtype=torch.float64,
+                                                                 device=dev)
+        ev = eps.reshape(T, -1) if eps is not None else None
+        buf = torch.empty(self.eps_count, device=dev) if eps is None else None
+        for t in range(T):
+            if ev is None:
+                randn_(buf, seed, offset + t * self.eps_stride)
+            self.inner_step(u, z, w, ev[t] if ev is not None else buf, params, adam_m, adam_v,
+                            step0 + t, lr, kind=kind, elbo_out=out[t:t + 1], ws=ws)
+        return out[:T]

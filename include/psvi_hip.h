@@ -330,6 +330,19 @@ int psvi_hvp(const psvi_plan* plan, const float* u, const int32_t* z, const floa
              const float* eps, const float* params, const float* vec, float* hv_out,
              float* du_out, float* dw_out, void* ws, size_t ws_bytes, void* stream);
 
+/* psvi_hvp over this plan's samples only, for the sample-sharded second-order
+ * trainers (PSVI.hyper_step's CG_normaleq products and PSVI.nested_step's
+ * reverse pass, psvi/hypergrad/hypergradients.py:199-244, 300-311;
+ * psvi_classes.py:541-687, split over ranks): each rank runs it on a world-1
+ * plan of its own samples with its slice of the global eps; include_kl = 1 on
+ * exactly one rank adds the KL Hessian (sample-independent), 0 leaves it out,
+ * so hv_out / du_out / dw_out summed over ranks (one all-reduce) equal
+ * psvi_hvp over all S samples.  psvi_hvp == psvi_hvp_partial(include_kl = 1). */
+int psvi_hvp_partial(const psvi_plan* plan, const float* u, const int32_t* z, const float* w,
+                     const float* eps, const float* params, const float* vec,
+                     int32_t include_kl, float* hv_out, float* du_out, float* dw_out, void* ws,
+                     size_t ws_bytes, void* stream);
+
 /* Reverse of one Adam step (either variant) for the nested trainer's
  * reverse-mode pass through the unrolled inner loop (PSVI.nested_step,
  * psvi_classes.py:541-600; DifferentiableAdam._update optim.py:318-367 /

@@ -1144,6 +1144,41 @@ def lenet_outer_elbo_grad(params, X, z, w, n_pseudo, eps, S, prior_sd=1.0, mode=
         nkl = nkl + ((-(x["X"] ** 2).sum(1) / (2 * s0 ** 2) - n * np.log(s0)
                       + 0.5 * (x["E"] ** 2).sum(1) + np.log(softplus(x["rho"])).sum()))
     loss, cp, Wt, ck = _outer_coef(pseudo, data, nkl, S, mode)
+    grad, gu, gw = _lenet_outer_backward(Xl, c, e, zi, w, Mu, nll, cp, Wt, ck, S, s0)
+    return float(loss), grad, gu, gw
+
+
+def lenet_outer_coef_grad(params, X, z, w, n_pseudo, eps, S, cp, cd, ck, prior_sd=1.0):
+    """The sample-sharded outer objective's two passes on these S samples
+    (psvi_outer_elbo_grad sample_out, psvi_outer_elbo_grad_coef): the
+    per-sample terms (S, 3) [pseudo_s, data_s, nkl_s] and the gradients of
+    sum_s (cp_s pseudo_s + cd_s data_s + ck_s nkl_s) w.r.t. params, u and w
+    for caller-given coefficients (psvi_classes.py:463-486 split over ranks)."""
+    params = np.asarray(params, np.float64)
+    s0 = float(prior_sd)
+    Xl = lenet_sample(params, eps, S)
+    logits, c = lenet_forward(Xl, X, S)
+    R = logits.shape[1]
+    w = np.asarray(w, np.float64)
+    zi = np.asarray(z).astype(np.int64)
+    mx = logits.max(-1, keepdims=True)
+    e = np.exp(logits - mx)
+    lse = mx[..., 0] + np.log(e.sum(-1))
+    nll = lse - logits[:, np.arange(R), zi]
+    Mu = int(n_pseudo)
+    nkl = np.zeros(S)
+    for x in Xl[2:]:
+        nkl = nkl + ((-(x["X"] ** 2).sum(1) / (2 * s0 ** 2) - x["n"] * np.log(s0)
+                      + 0.5 * (x["E"] ** 2).sum(1) + np.log(softplus(x["rho"])).sum()))
+    terms = np.stack([nll[:, :Mu] @ w[:Mu], nll[:, Mu:] @ w[Mu:], nkl], 1)
+    cp, cd, ck = (np.asarray(a, np.float64) for a in (cp, cd, ck))
+    grad, gu, gw = _lenet_outer_backward(Xl, c, e, zi, w, Mu, nll, cp, cd, ck, S, s0)
+    return terms, grad, gu, gw
+
+
+def _lenet_outer_backward(Xl, c, e, zi, w, Mu, nll, cp, Wt, ck, S, s0):
+    """d/d(params, u, w) of sum_s (cp_s pseudo_s + Wt_s data_s + ck_s nkl_s)."""
+    R = nll.shape[1]
     coef = np.where(np.arange(R)[None, :] < Mu, cp[:, None], Wt[:, None]) * w[None, :]
     Pm = e / e.sum(-1, keepdims=True)
     Pm[:, np.arange(R), zi] -= 1.0
@@ -1153,7 +1188,7 @@ def lenet_outer_elbo_grad(params, X, z, w, n_pseudo, eps, S, prior_sd=1.0, mode=
     grad, _ = _lenet_param_grad(Xl, G, s0, kl_layers=False, sck=float(ck.sum()))
     gu = dx[:, :Mu].sum(0)
     gw = cp @ nll[:, :Mu]
-    return float(loss), grad, gu, gw
+    return grad, gu, gw
 
 
 def lenet_inner_loop(params0, u, z, w, eps_steps, S, lr, adam_kind, prior_sd=1.0, t0=1):

@@ -70,3 +70,74 @@ def assert_grad_close(g, gref, l2tol=1e-4, rtol=1e-3, atol_frac=1e-4, what="grad
     bad = np.abs(g - gref) > tol
     assert not bad.any(), (f"{what}: {int(bad.sum())} elements out of tolerance, "
                            f"worst idx {int(np.argmax(np.abs(g - gref)))}")
+
+
+# ---------------------------------------------------------------------------
+# C5 (make_lenet, S = 256, M = 500) parity case: one rank's share of a world-8
+# sample split, regenerated from a seed (the oracle's outputs are the fixture
+# tests/golden/c5_lenet_rank.npz, tools/gen_oracle_c5.py)
+C5 = dict(S=256, M=500, world=8, rank=3, Nx=64, N=60000, seed=2026)
+
+
+def c5_lenet_case(seed=C5["seed"]):
+    """Seeded C5 inputs: params at a trained-like scale, M MNIST-shaped
+    pseudo-images with coreset weights N f(v), a data batch of Nx rows, the
+    rank's noise (its S / world samples per batched layer, plus the shared
+    last-layer draw), outer coefficients and an HVP direction."""
+    import psvi_oracle as O
+
+    rng = np.random.default_rng(seed)
+    S, M, Nx = C5["S"], C5["M"], C5["Nx"]
+    s_cnt = S // C5["world"]
+    P = O.lenet_param_count()
+    params = np.empty(P)
+    po = 0
+    for nw, nb, _, _ in O.LENET_LAYERS:
+        n = nw + nb
+        params[po:po + n] = 0.15 * rng.normal(size=n)
+        params[po + n:po + 2 * n] = rng.uniform(-4.0, -2.0, size=n)
+        po += 2 * n
+    u = rng.normal(size=(M, 1, 28, 28))
+    z = rng.integers(0, 10, size=M)
+    v = rng.normal(size=M)
+    w = C5["N"] * np.exp(v) / np.exp(v).sum()
+    xb = rng.normal(size=(Nx, 1, 28, 28))
+    yb = rng.integers(0, 10, size=Nx)
+    eps_loc = rng.normal(size=O.lenet_eps_count(s_cnt))
+    # coefficients of the form outer_coefficients produces: W_s the softmax
+    # weight (this rank holds 32 of 256 samples: sum ~ 1/8), ck_s = W_s (a_s -
+    # abar) - 1/S, cp_s = -W_s - ck_s, cd_s = W_s
+    r = rng.normal(size=(3, s_cnt))
+    W = np.exp(0.3 * r[0])
+    W /= 8.0 * W.sum()
+    ck = W * r[1] - 1.0 / S
+    coef = np.stack([-W - ck, W, ck])
+    vec = rng.normal(size=P) * 1e-2
+    f32 = lambda a: np.asarray(a, np.float32)
+    return dict(params=f32(params), u=f32(u), z=z.astype(np.int32), w=f32(w), xb=f32(xb),
+                yb=yb.astype(np.int32), eps_loc=f32(eps_loc), cp=coef[0], cd=coef[1],
+                ck=coef[2], vec=f32(vec), s_cnt=s_cnt, s_off=C5["rank"] * s_cnt)
+
+
+def c5_global_eps(case, fill=np.nan):
+    """The global (S = 256) eps in the reference draw order with the rank's
+    samples (and the shared last-layer draw) from the case and every other
+    sample's noise = fill: a plan that reads outside its shard sees NaN."""
+    import psvi_oracle as O
+
+    S, s_off, s_cnt = C5["S"], case["s_off"], case["s_cnt"]
+    out = np.full(O.lenet_eps_count(S), fill, np.float32)
+    go = lo = 0
+    for nw, nb, bat, _ in O.LENET_LAYERS:
+        if not bat:
+            out[go:go + nw + nb] = case["eps_loc"][lo:lo + nw + nb]
+            go += nw + nb
+            lo += nw + nb
+            continue
+        for k in (nw, nb):
+            g = out[go:go + S * k].reshape(S, k)
+            g[s_off:s_off + s_cnt] = case["eps_loc"][lo:lo + s_cnt * k].reshape(s_cnt, k)
+            go += S * k
+            lo += s_cnt * k
+    assert go == out.size and lo == case["eps_loc"].size
+    return out

@@ -1,0 +1,162 @@
+"""LeNet (make_lenet) parity at config C5's full size: S = 256, M = 500.
+
+The fp64 oracle takes minutes per call at this size, so its outputs for one
+rank's share of a world-8 sample split (samples 96..127 of 256, all 500
+pseudo-images, a 64-row data batch) are committed
+(tests/golden/c5_lenet_rank.npz, tools/gen_oracle_c5.py; the inputs are
+regenerated from the seed by golden_util.c5_lenet_case).  Checked against it:
+
+* the inner objective through the S = 256 plan's world-8 rank (the noise of
+  every other sample is NaN, so any read outside the shard shows);
+* the outer objective's two sample-sharded passes (per-sample terms, then the
+  gradients for given coefficients) through sharded.ShardedOuter;
+* psvi_hvp with its mixed products on the rank's samples.
+
+Size-independent properties at the full size: the 8 ranks' inner accumulators
+sum to the single-plan one, and the 8 ranks' partial HVPs (KL Hessian on rank
+0 only, psvi_hvp_partial) sum to the single-plan S = 256 product.
+
+Tolerance (north star): values and gradients within 1e-4 relative (l2 for
+vectors, plus the per-element bound of golden_util.assert_grad_close)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import (C5, assert_grad_close, c5_global_eps, c5_lenet_case, l2rel,
+                         load_fixture, rel)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LENET = [(25, 6), (150, 16), (400, 120), (120, 84), (84, 10)]
+
+
+def _t(x, dtype=torch.float32):
+    return torch.tensor(np.ascontiguousarray(x), dtype=dtype, device=DEV)
+
+
+@pytest.fixture(scope="module")
+def case():
+    return c5_lenet_case(), load_fixture("c5_lenet_rank")
+
+
+def _plan(S, M, world=1, rank=0):
+    from psvi.runtime import InnerLoopPlan
+
+    return InnerLoopPlan("lenet", LENET, S, M, world=world, rank=rank)
+
+
+def _rows_close(got, want, what, tol=1e-4, max_frac=0.01):
+    """Per-row (per pseudo-image) comparison of d/du: at C5's size a few
+    (sample, image) pairs sit on a max-pool tie or a ReLU kink where fp32 and
+    fp64 route the gradient differently (tests/test_hip_fullsize.py has the
+    same boundary at C4); those rows are reported and bounded in number, every
+    other row must match to tol."""
+    got = np.asarray(got, np.float64).reshape(want.shape[0], -1)
+    want = np.asarray(want, np.float64).reshape(want.shape[0], -1)
+    scale = np.linalg.norm(want) / np.sqrt(want.shape[0])
+    err = np.linalg.norm(got - want, axis=1) / np.maximum(np.linalg.norm(want, axis=1), 1e-3 * scale)
+    bad = err > tol
+    print(f"{what}: rows over {tol:g}: {int(bad.sum())}/{len(err)}, worst {err.max():.2e} "
+          f"(row {int(err.argmax())}), median {np.median(err):.2e}, total l2rel "
+          f"{np.linalg.norm(got - want) / np.linalg.norm(want):.2e}")
+    assert bad.mean() <= max_frac, what
+
+
+def test_c5_inner_rank_shard_matches_oracle(case):
+    c, f = case
+    S, M = C5["S"], C5["M"]
+    plan = _plan(S, M, world=C5["world"], rank=C5["rank"])
+    assert plan.s_local == c["s_cnt"] and plan.s_offset == c["s_off"]
+    params = _t(c["params"])
+    u, z, w = _t(c["u"]), _t(c["z"], torch.int32), _t(c["w"])
+    eps = _t(c5_global_eps(c))          # NaN outside the rank's samples
+    acc = torch.empty(plan.acc_count, device=DEV)
+    nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.mf_accumulate(u, z, w, eps, params, acc, nll)
+    kl = torch.zeros(1, dtype=torch.float64, device=DEV)
+    grad = torch.empty_like(params)
+    plan.mf_update(acc, params, kl_out=kl, grad_out=grad, include_kl=True)
+    assert torch.isfinite(grad).all()
+    assert rel(nll.item() + kl.item(), f["inner_value"]) < 1e-5
+    assert_grad_close(grad.cpu().numpy(), f["inner_grad"], what="C5 inner grad")
+
+
+def test_c5_outer_sharded_passes_match_oracle(case):
+    from psvi.runtime.sharded import ShardedOuter
+
+    c, f = case
+    S, M, Nx = C5["S"], C5["M"], C5["Nx"]
+    so = ShardedOuter("lenet", LENET, S, M + Nx, C5["world"], C5["rank"], device=DEV)
+    assert (so.s_off, so.s_cnt) == (c["s_off"], c["s_cnt"])
+    x_all = _t(np.concatenate([c["u"], c["xb"]]).reshape(M + Nx, -1))
+    z_all = _t(np.concatenate([c["z"], c["yb"]]), torch.int32)
+    w_all = _t(np.concatenate([c["w"], np.full(Nx, C5["N"] / Nx, np.float32)]))
+    params = _t(c["params"])
+    e, terms = so.local_terms(M, x_all, z_all, w_all, _t(c5_global_eps(c)), params)
+    assert rel(terms.cpu().numpy(), f["outer_terms"]) < 1e-5
+    # global coefficient vectors: NaN outside this rank's samples
+    full = {k: torch.full((S,), float("nan"), dtype=torch.float64) for k in ("cp", "cd", "ck")}
+    for k in full:
+        full[k][c["s_off"]:c["s_off"] + c["s_cnt"]] = torch.from_numpy(c[k])
+    g = so.local_grads(M, x_all, z_all, w_all, e, params, full["cp"], full["cd"], full["ck"])
+    assert_grad_close(g["grad"].cpu().numpy(), f["outer_grad"], what="C5 outer grad")
+    _rows_close(g["grad_u"].cpu().numpy(), f["outer_grad_u"], "C5 outer d/du")
+    assert l2rel(g["grad_w"].cpu().numpy(), f["outer_grad_w"]) < 1e-4
+
+
+def test_c5_hvp_rank_samples_match_oracle(case):
+    c, f = case
+    plan = _plan(c["s_cnt"], C5["M"])
+    u, z, w = _t(c["u"]), _t(c["z"], torch.int32), _t(c["w"])
+    hv, du, dw = plan.hvp(u, z, w, _t(c["eps_loc"]), _t(c["params"]), _t(c["vec"]))
+    assert_grad_close(hv.cpu().numpy(), f["hvp"], what="C5 H v")
+    _rows_close(du.cpu().numpy(), f["hvp_du"].reshape(du.shape), "C5 hvp d/du")
+    assert l2rel(dw.cpu().numpy(), f["hvp_dw"]) < 1e-4
+
+
+def test_c5_accumulators_of_8_ranks_sum_to_single():
+    c = c5_lenet_case(seed=11)
+    S, M = C5["S"], C5["M"]
+    from psvi.runtime import randn_
+
+    params, u, z, w = _t(c["params"]), _t(c["u"]), _t(c["z"], torch.int32), _t(c["w"])
+    eps = torch.empty(_plan(S, M).eps_count, device=DEV)
+    randn_(eps, seed=3)
+    single = _plan(S, M)
+    acc1 = torch.empty(single.acc_count, device=DEV)
+    nll1 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    single.mf_accumulate(u, z, w, eps, params, acc1, nll1)
+    acc8 = torch.zeros_like(acc1)
+    nll8 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    for r in range(8):
+        pr = _plan(S, M, world=8, rank=r)
+        a = torch.empty(pr.acc_count, device=DEV)
+        pr.mf_accumulate(u, z, w, eps, params, a, nll8)
+        acc8 += a
+    assert rel(nll8.item(), nll1.item()) < 1e-6
+    assert l2rel(acc8.cpu().numpy(), acc1.cpu().numpy()) < 1e-5
+
+
+def test_c5_partial_hvps_of_8_ranks_sum_to_single():
+    from psvi.runtime import randn_
+    from psvi.runtime.sharded import local_eps, sample_split
+
+    c = c5_lenet_case(seed=12)
+    S, M = C5["S"], C5["M"]
+    params, u, z, w = _t(c["params"]), _t(c["u"]), _t(c["z"], torch.int32), _t(c["w"])
+    vec = _t(c["vec"])
+    single = _plan(S, M)
+    eps = torch.empty(single.eps_count, device=DEV)
+    randn_(eps, seed=4)
+    hv1, du1, dw1 = single.hvp(u, z, w, eps, params, vec)
+    hv8, du8, dw8 = torch.zeros_like(hv1), torch.zeros_like(du1), torch.zeros_like(dw1)
+    for r, (off, cnt) in enumerate(sample_split(S, 8)):
+        pr = _plan(cnt, M)
+        h, a, b = pr.hvp(u, z, w, local_eps("lenet", LENET, S, off, cnt, eps), params, vec,
+                         include_kl=(r == 0))
+        hv8 += h
+        du8 += a
+        dw8 += b
+    assert l2rel(hv8.cpu().numpy(), hv1.cpu().numpy()) < 1e-5
+    assert l2rel(du8.cpu().numpy(), du1.cpu().numpy()) < 1e-5
+    assert l2rel(dw8.cpu().numpy(), dw1.cpu().numpy()) < 1e-5

@@ -1,0 +1,142 @@
+"""Sample-sharded second-order trainers on the GPU: PSVI.hyper_step /
+nested_step with world > 1, the ranks emulated as threads of one process (one
+PSVI instance per rank, all_reduce through a thread barrier).  Each rank's
+inner objective, psvi_hvp_partial and outer passes run on a world-1 plan of its
+own samples (SampleShardedPlan, ShardedOuter); every rank must reproduce the
+reference's whole hyper_step / nested_step (y*, n*, v14 fixtures), and at
+C5's size (make_lenet, S = 256, M = 500) the world-8 hyper_step must agree with
+the world-1 one on the same Philox draws."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import l2rel, load_fixture, rel
+
+pytestmark = pytest.mark.gpu
+
+
+class _ThreadComm:
+    def __init__(self, world):
+        self.slots = [None] * world
+        self.bar = threading.Barrier(world)
+
+    def bind(self, rank):
+        outer = self
+
+        class _Rank:
+            def all_reduce(self, t):
+                outer.slots[rank] = t.clone()
+                outer.bar.wait()
+                total = sum(outer.slots[r] for r in range(len(outer.slots)))
+                outer.bar.wait()
+                t.copy_(total)
+
+        return _Rank()
+
+
+def _run_ranks(world, fn):
+    comm = _ThreadComm(world)
+    res, errs = [None] * world, []
+
+    def run(r):
+        try:
+            res[r] = fn(r, comm.bind(r))
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- surfaced below
+            errs.append(e)
+            comm.bar.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    assert not errs, errs
+    return res
+
+
+def _fixture_rank(name, cls, world, rank, comm):
+    from test_host_api import build_model
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    model = build_model(cfg, f["params0"]).cuda()
+    u = torch.tensor(f["u0"], device="cuda").requires_grad_(True)
+    ps = cls(u=u, z=torch.tensor(f["z"], device="cuda"), N=cfg["N"], model=model,
+             mc_samples=cfg["S"], device_id=0, inner_it=cfg["T"], world=world, rank=rank,
+             comm=comm)
+    ps.device = torch.device("cuda")
+    ps.v = torch.tensor(f["v0"], device="cuda").requires_grad_(True)
+    if getattr(ps, "alpha", None) is not None and "alpha0" in f:
+        ps.alpha = torch.tensor(f["alpha0"], device="cuda").reshape(1).requires_grad_(True)
+        ps.f = lambda *x: torch.exp(ps.alpha) * torch.softmax(x[0], x[1])
+    ps.setup_optimizers(lr0net=cfg["lr0net"], lr0u=cfg["lr0u"], lr0v=cfg["lr0v"])
+    ei = [torch.tensor(e, device="cuda") for e in f["eps_inner"]]
+    eo = [torch.tensor(e, device="cuda") for e in f["eps_outer"]]
+    xb, yb = torch.tensor(f["xb"], device="cuda"), torch.tensor(f["yb"], device="cuda")
+    if "K" in cfg:
+        ll = ps.hyper_step(xb, yb, K=cfg["K"], linsys_lr=cfg["linsys_lr"], eps_inner=ei,
+                           eps_outer=eo, hypergrad_approx=cfg.get("approx", "CG_normaleq"))
+    else:
+        ll = ps.nested_step(xb, yb, eps_inner=ei, eps_outer=eo).item()
+    p = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
+    return dict(ll=ll, params=p, u_grad=ps.u.grad.cpu().numpy(), v_grad=ps.v.grad.cpu().numpy())
+
+
+@pytest.mark.parametrize("name,world", [("y1_fn2_tiny", 8), ("y2_fn_deep", 3), ("y5_lenet", 2),
+                                        ("n1_fn2_tiny", 4), ("n2_fn_deep", 2)])
+def test_sharded_trainer_matches_reference(name, world):
+    from psvi.inference import PSVILearnV
+
+    f = load_fixture(name)
+    res = _run_ranks(world, lambda r, c: _fixture_rank(name, PSVILearnV, world, r, c))
+    for g in res:
+        assert l2rel(g["params"], f["params"]) < 1e-5
+        for k in ("u_grad", "v_grad"):
+            own = l2rel(f[k + "_fp32"], f[k]) if k + "_fp32" in f else 0.0
+            assert l2rel(g[k], f[k]) < max(1e-4, 4 * own), (name, k, l2rel(g[k], f[k]))
+        assert rel(g["ll"], f["ll"] if "ll" in f else f["loss"]) < 1e-5
+        assert np.array_equal(g["params"], res[0]["params"])
+
+
+def test_c5_lenet_hyper_step_world8_matches_world1():
+    """C5's bilevel outer (make_lenet, S = 256, M = 500, a 128-image data
+    batch) split over 8 ranks against one rank, same Philox draws."""
+    from psvi.inference import PSVILearnV
+    from psvi.models import make_lenet
+
+    S, M = 256, 500
+    g = torch.Generator().manual_seed(3)
+    u0 = torch.randn(M, 1, 28, 28, generator=g)
+    z = torch.randint(0, 10, (M,), generator=g).float()
+    xb = torch.randn(128, 1, 28, 28, generator=g).cuda()
+    yb = torch.randint(0, 10, (128,), generator=g).float().cuda()
+    torch.manual_seed(0)
+    p0 = torch.nn.utils.parameters_to_vector(make_lenet(mc_samples=S, init_sd=0.05).parameters())
+
+    def rank_fn(world):
+        def fn(r, comm):
+            net = make_lenet(mc_samples=S, init_sd=0.05).cuda()
+            with torch.no_grad():
+                torch.nn.utils.vector_to_parameters(p0.detach().cuda(), net.parameters())
+            ps = PSVILearnV(u=u0.clone().cuda().requires_grad_(True), z=z.cuda(), N=60000,
+                            model=net, mc_samples=S, device_id=0, inner_it=2, seed=7,
+                            world=world, rank=r, comm=comm)
+            ps.device = torch.device("cuda")
+            ps.register_elbos = False
+            ps.setup_optimizers()
+            ll = ps.hyper_step(xb, yb, K=3)
+            pv = torch.nn.utils.parameters_to_vector(net.parameters()).detach().cpu().numpy()
+            return dict(ll=ll, params=pv, u_grad=ps.u.grad.cpu().numpy(),
+                        v_grad=ps.v.grad.cpu().numpy())
+        return fn
+
+    one = _run_ranks(1, rank_fn(1))[0]
+    eight = _run_ranks(8, rank_fn(8))
+    for g in eight:
+        assert l2rel(g["params"], one["params"]) < 1e-5
+        assert l2rel(g["u_grad"], one["u_grad"]) < 1e-3
+        assert l2rel(g["v_grad"], one["v_grad"]) < 1e-3
+        assert rel(g["ll"], one["ll"]) < 1e-5

@@ -37,10 +37,11 @@ def _case(layers, S, seed):
     return rng, p, m, v
 
 
+# the stream kernel runs at S = 128 (stream_ok in kernels_mvn.hip)
 SHAPES = [([(64, 40), (40, 40), (40, 2)], 128),   # C3
-          ([(7, 5), (5, 3)], 32),                  # n = 40, 18: one partial band each
-          ([(30, 33), (33, 2)], 96),               # n = 1023, 68
-          ([(12, 20), (20, 4)], 64)]
+          ([(7, 5), (5, 3)], 128),                 # n = 40, 18: one partial band each
+          ([(30, 33), (33, 2)], 128),              # n = 1023, 68
+          ([(12, 20), (20, 4)], 128)]
 
 
 @pytest.mark.parametrize("layers,S", SHAPES)
