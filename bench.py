@@ -86,7 +86,7 @@ def algorithmic_work(S, rows_frac=1.0):
                 sample=dict(bytes=fwd_bytes, flops=fwd_flops))
 
 
-def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r01f_pmc_traffic.json")):
+def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")):
     """HBM bytes per launch of the listed kernels (summed: the phase the
     roofline times) from the committed rocprofv3 PMC summary
     (tools/pmc_session.sh -> tools/pmc_report.py --json: separate FETCH_SIZE /
@@ -98,12 +98,40 @@ def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r01f_pmc_traffic.j
         return None
 
 
+def _cpu_model():
+    try:
+        return open("/proc/cpuinfo").read().split("model name")[1].split(":")[1].split("\n")[0].strip()
+    except Exception:
+        return "unknown"
+
+
+def pin_cpu_threads():
+    """the reference on all the cores this process may
+    use -- the CPU affinity, capped by OMP_NUM_THREADS where the host sets it
+    (the GPU box's CPU share; its affinity and os.cpu_count() report the whole
+    machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    torch.set_num_threads(max(1, n))
+    return torch.get_num_threads()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line stays alone on stdout)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(budget_s=12.0):
     """Op-faithful torch CPU restatement of the reference inner step
-    (oracle/cpu_reference.py) on a bounded number of C3 steps."""
+    (oracle/cpu_reference.py) on a bounded number of C3 steps, with the
+    anomaly-detection setting of the reference's driver
+    (psvi/experiments/flow_psvi.py:50 turns it on) timed beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from cpu_reference import RefInnerStep, reference_init
 
+    threads = pin_cpu_threads()
     torch.manual_seed(0)
     r = RefInnerStep("mvn", LAYERS, S_PER_GPU)
     p0 = reference_init("mvn", LAYERS)
@@ -117,14 +145,125 @@ def cpu_baseline(budget_s=12.0):
     t0 = time.perf_counter()
     r.run(p0, u, z, w, n, LR)
     dt = time.perf_counter() - t0
-    try:
-        model = open("/proc/cpuinfo").read().split("model name")[1].split(":")[1].split("\n")[0].strip()
-    except Exception:
-        model = "unknown"
-    return dict(value=n / dt, unit="inner-steps/s", cores=torch.get_num_threads(), kind="port",
+    # anomaly detection on (the reference driver's setting), a short sample
+    na = max(2, min(10, n // 4))
+    with torch.autograd.set_detect_anomaly(True, check_nan=True):
+        t0 = time.perf_counter()
+        r.run(p0, u, z, w, na, LR)
+        dta = time.perf_counter() - t0
+    model = _cpu_model()
+    return dict(value=n / dt, unit="inner-steps/s", cores=threads, kind="port",
+                anomaly_on_value=round(na / dta, 3),
                 sample=(f"C3 fn2 S=128 M=100: one nested inner loop of {n} steps "
                         f"(autograd.grad create_graph=True + higher-Adam, anomaly off) "
-                        f"in {dt:.1f} s on {torch.get_num_threads()} threads of {model}"))
+                        f"in {dt:.1f} s on {threads} threads (torch.set_num_threads: the "
+                        f"process's CPU affinity capped by OMP_NUM_THREADS) of {model}; "
+                        f"anomaly_on_value: {na} steps "
+                        f"with torch.autograd.set_detect_anomaly(True) as flow_psvi.py:50"))
+
+
+def c2_timings(dev, steps=300, cpu=True):
+    """Auxiliary line for BASELINE.json configs[1] (C2): fn = make_fcnet 2 -> 100
+    -> 4 (one hidden layer, diagonal covariance) on a four_blobs-shaped
+    problem, M = 50 pseudopoints, S = 32, psvi_inner_loop with in-library draws;
+    and the op-faithful CPU step of the same model."""
+    from psvi.runtime import InnerLoopPlan
+
+    layers, S, M = [(2, 100), (100, 4)], 32, 50
+    plan = InnerLoopPlan("meanfield", layers, S, M)
+    g = torch.Generator().manual_seed(3)
+    u = torch.randn(M, 2, generator=g)
+    z = torch.randint(0, 4, (M,), generator=g)
+    w = torch.full((M,), 1000.0 / M)
+    params = _mf_init(layers).to(dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    ud, zd, wd = u.to(dev), z.to(dev, torch.int32), w.to(dev)
+    ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+    plan.inner_loop(ud, zd, wd, params, m, v, 20, LR, seed=1, ws=ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan.inner_loop(ud, zd, wd, params, m, v, steps, LR, seed=2, ws=ws)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"config": "C2 fn 2-100-4 meanfield, S=32, M=50 (four_blobs-shaped)",
+           "gpu_inner_steps_per_s": round(steps / dt, 1)}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from cpu_reference import RefInnerStep, reference_init
+
+        r = RefInnerStep("mf", layers, S)
+        p0 = reference_init("mf", layers)
+        r.run(p0, u, z.float(), w, 3, LR)
+        t0 = time.perf_counter()
+        r.run(p0, u, z.float(), w, 30, LR)
+        out["cpu_inner_steps_per_s"] = round(30 / (time.perf_counter() - t0), 2)
+        out["cpu_threads"] = torch.get_num_threads()
+    return out
+
+
+def _mf_init(layers, init_sd=1e-3):
+    parts = []
+    isp = math.log(math.expm1(init_sd))
+    g = torch.Generator().manual_seed(4)
+    for din, dout in layers:
+        bound = 1.0 / math.sqrt(din)
+        parts += [(torch.rand(din * dout + dout, generator=g) * 2 - 1) * bound,
+                  torch.full((din * dout + dout,), isp)]
+    return torch.cat(parts)
+
+
+C4 = dict(S=1024, M=200)
+
+
+def c4_timings(dev, world, rank, steps=100, warmup=10):
+    """Auxiliary line for BASELINE.json configs[3] (C4): fn2 64-40-40-2 full-cov,
+    S = 1024, M = 200 -- the same total work at every N (strong scaling):
+    N = 1 runs psvi_inner_loop; N > 1 the rows-of-L x samples sharded step
+    (ShardedInnerLoop, two all_to_alls per step).  inner-steps/s of the whole
+    job; BASELINE's ">= 6x at 8 GPUs over 1" is this line at N = 8 over N = 1."""
+    from psvi.runtime import InnerLoopPlan, randn_
+    from psvi.runtime.sharded import ShardedInnerLoop, TorchDistComm
+
+    S, Mc = C4["S"], C4["M"]
+    g = torch.Generator().manual_seed(5)
+    u = torch.randn(Mc, 64, generator=g).to(dev)
+    z = (torch.rand(Mc, generator=g) < torch.sigmoid(5.0 * u.cpu().sum(1))).to(torch.int32).to(dev)
+    w = torch.full((Mc,), N_DATA / Mc, device=dev)
+    params = reference_init_params(LAYERS, dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    if world == 1:
+        plan = InnerLoopPlan("fullcov", LAYERS, S, Mc)
+        ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+        plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=11, ws=ws)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan.inner_loop(u, z, w, params, m, v, steps, LR, seed=12, ws=ws)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    else:
+        import torch.distributed as dist
+
+        loop = ShardedInnerLoop("fullcov", LAYERS, S, Mc, world, rank, device=dev,
+                                comm=TorchDistComm())
+        eps = torch.empty(loop.plan.eps_count, device=dev)
+        stride = (loop.plan.eps_count + 3) // 4 * 4
+        for k in range(warmup):
+            randn_(eps, 11, k * stride)
+            loop.step(u, z, w, eps, params, m, v, k + 1, LR)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            randn_(eps, 12, k * stride)
+            loop.step(u, z, w, eps, params, m, v, warmup + k + 1, LR)
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return {"config": f"C4 fn2 full-cov S={S} M={Mc}, {world} GPU(s) (strong scaling)",
+            "inner_steps_per_s": round(steps / dt, 2), "ms_per_step": round(dt / steps * 1e3, 4)}
 
 
 def lenet_timings(dev, cpu=True, T=10):
@@ -275,6 +414,10 @@ def main():
                     help="skip the auxiliary C5 (lenet) inner-step timing")
     ap.add_argument("--no-trainers", action="store_true",
                     help="skip the auxiliary outer-step (trainer) timings")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the auxiliary C4 (S=1024, M=200) strong-scaling line")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="skip the auxiliary C2 (fn, S=32, M=50) line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -400,7 +543,8 @@ def main():
         # small slot-reduce kernel, inside the same event pair)
         wk = algorithmic_work_fused(S)
         hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
-        kname = "mvn_update_kernel<fused next-step sample, tiled state> + mvn_fwd_reduce_kernel"
+        kname = ("mvn_stream_kernel (fused update + next-step sample, tiled state) + "
+                 "mvn_fwd_reduce_kernel")
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
@@ -422,21 +566,40 @@ def main():
         roofline = dict(bound="mfma", achieved=round(wk["flops"] / upd_s / 1e12, 2),
                         peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s")
     roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
-                    traffic=pmc_traffic(["mvn_update_kernel", "mvn_fwd_reduce_kernel"]
+                    traffic=pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"]
                                         if world == 1 else ["mvn_update_kernel"]),
                     kernel=kname, algorithmic_bytes_per_launch=int(wk["bytes"]),
                     algorithmic_flops_per_launch=int(wk["flops"]),
                     floors_us=dict(hbm=round(hbm_s * 1e6, 2), mfma=round(mfma_s * 1e6, 2)),
                     kernels={k: {kk: round(vv, 2) for kk, vv in d.items()}
                              for k, d in kernels.items()})
+    # the whole inner step's algorithmic work at C3 (2.682 GFLOP,
+    # 134.7 MB per S = 128 shard) against the fp32 MFMA peak -- the step's roofline
+    # fraction, beside the dominant kernel's own above
+    step_floor_us = 2.682e9 * (S / S_PER_GPU) / world / (FP32_MFMA_PEAK_TFLOPS * 1e12) * 1e6
+    step_roofline = dict(bound="mfma (ridge: HBM 16.8 us / MFMA 17.05 us per C3 shard)",
+                         algorithmic_gflop_per_gpu=round(2.682 * S / S_PER_GPU / world, 3),
+                         floor_us=round(step_floor_us, 2),
+                         frac=round(step_floor_us / (elapsed / args.steps * 1e6), 4))
+    log(f"headline: {args.steps / elapsed:.1f} steps/s; C4 line")
+    c4 = None
+    if not args.no_c4:
+        c4 = c4_timings(dev, world, rank)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("CPU baseline")
         cpu = cpu_baseline(args.cpu_budget)
+    c2 = None
+    if rank == 0 and world == 1 and not args.no_c2:
+        log("C2 line")
+        c2 = c2_timings(dev, cpu=not args.no_cpu_baseline)
     trainers = None
     if rank == 0 and world == 1 and not args.no_trainers:
+        log("trainers")
         trainers = trainer_timings(dev, cpu=not args.no_cpu_baseline)
     lenet = None
     if rank == 0 and world == 1 and not args.no_lenet:
+        log("C5 lenet")
         lenet = lenet_timings(dev, cpu=not args.no_cpu_baseline)
     if world > 1:
         dist.barrier()
@@ -459,7 +622,10 @@ def main():
                        "params": plan.param_count, "parallelism": f"rows-of-L x samples sharded over {world}",
                        "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite},
             "roofline": roofline,
+            "step_roofline": step_roofline,
             "cpu_baseline": cpu,
+            ("c4_1gpu" if world == 1 else "c4"): c4,
+            "c2": c2,
             "trainers": trainers,
             "lenet_c5": lenet,
         }

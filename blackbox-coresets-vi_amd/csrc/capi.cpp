@@ -1102,6 +1102,13 @@ int psvi_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const fl
     return 0;
 }
 
+int psvi_nonfinite(const void* data, int64_t n, int32_t dtype, int32_t* flag, void* stream) {
+    if (!data || !flag || n < 0 || (dtype != 0 && dtype != 1))
+        return fail(PSVI_EINVAL, "bad nonfinite arguments");
+    HIP_TRY(launch_nonfinite(data, n, dtype, flag, as_stream(stream)));
+    return 0;
+}
+
 int psvi_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, void* stream) {
     if (!out || n < 0) return fail(PSVI_EINVAL, "bad randn arguments");
     if (offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");

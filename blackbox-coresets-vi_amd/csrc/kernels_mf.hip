@@ -209,4 +209,30 @@ hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, h
     return hipGetLastError();
 }
 
+// ------------------------------------------------- non-finite values flag
+// flag[0] |= 1 when any of the n values is NaN or +-inf: the device-side check
+// that stands in for torch.autograd.set_detect_anomaly (flow_psvi.py:50) on the
+// HIP path; one int32 for the host to read once per outer step.
+template <typename T>
+__global__ __launch_bounds__(256) void nonfinite_kernel(const T* __restrict__ x, int64_t n,
+                                                        int32_t* __restrict__ flag) {
+    bool bad = false;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        bad |= !isfinite(x[i]);
+    if (__any(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1);
+}
+
+hipError_t launch_nonfinite(const void* x, int64_t n, int dtype, int32_t* flag, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t nb = std::min<int64_t>((n + 255) / 256, 1024);
+    if (dtype == 1)
+        hipLaunchKernelGGL(nonfinite_kernel<double>, dim3((unsigned)nb), dim3(256), 0, st,
+                           (const double*)x, n, flag);
+    else
+        hipLaunchKernelGGL(nonfinite_kernel<float>, dim3((unsigned)nb), dim3(256), 0, st,
+                           (const float*)x, n, flag);
+    return hipGetLastError();
+}
+
 }  // namespace psvi

@@ -362,6 +362,7 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
                             const float* eps, const float* params, const float* vec, float* hv,
                             float* d_u, float* d_w, void* tws, hipStream_t st,
                             bool include_kl = true);
+hipError_t launch_nonfinite(const void* x, int64_t n, int dtype, int32_t* flag, hipStream_t st);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
 hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,

@@ -69,7 +69,7 @@ from torch.autograd.function import once_differentiable
 
 from ..models.neural_net import (VILinear, VILinearMultivariateNormal, categorical_fn,
                                  make_fc2net, make_fcnet, make_lenet, model_spec)
-from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, randn_
+from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, nonfinite_, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
            "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
@@ -149,6 +149,43 @@ class HipAblatedELBO(torch.autograd.Function):
         return (gout * gp).to(ctx.ptype), None, None, None, None, None
 
 
+class HipOuterRowsELBO(torch.autograd.Function):
+    """PSVI.psvi_elbo over caller-formed rows whose weights -- pseudo AND data
+    rows -- carry autograd graphs: learn_z's soft labels as expanded rows
+    (psvi_classes.py:450-486), where every row's target depends on z through
+    the softmax over all rows.  One psvi_outer_elbo_grad (loss, parameter,
+    pseudo-row input and weight gradients, the sample weights W_s), then one
+    psvi_outer_elbo_grad_coef with every row as a pseudo row and coefficient
+    W_s for the data rows' weight gradients sum_s W_s NLL_s,row."""
+
+    @staticmethod
+    def forward(ctx, pvec, u_rows, w_rows, plan, x_all, z_all, eps, n_pseudo):
+        from ..runtime.sharded import pack_coef
+
+        p = pvec.detach().to(torch.float32).contiguous()
+        w = w_rows.detach().to(torch.float32).contiguous()
+        out = plan.outer_elbo_grad(n_pseudo, x_all, z_all, w, eps, p, grad=True,
+                                   grad_u=n_pseudo > 0, grad_w=True, sample_stats=True)
+        R, S = x_all.shape[0], out["samples"].shape[0]
+        W = out["samples"][:, 3].cpu()
+        zero = torch.zeros(S, dtype=torch.float64)
+        gd = plan.outer_grad_coef(R, x_all, z_all, w, eps, p,
+                                  pack_coef(W, zero, zero, 0, S).to(p.device),
+                                  grad_u=False, grad_w=True)["grad_w"][n_pseudo:]
+        gu = out["grad_u"] if n_pseudo > 0 else torch.zeros_like(x_all[:0])
+        ctx.save_for_backward(out["grad"], gu, torch.cat([out["grad_w"], gd]))
+        ctx.meta = (pvec.dtype, u_rows.shape, u_rows.dtype, w_rows.dtype)
+        return out["loss"].to(pvec.dtype).reshape(())
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        gp, gu, gw = ctx.saved_tensors
+        tp, us, ut, wt = ctx.meta
+        return ((gout * gp).to(tp), (gout * gu).reshape(us).to(ut), (gout * gw).to(wt),
+                None, None, None, None, None)
+
+
 class PSVI:
     """Pseudodata (coreset) VI with fixed rescaled coefficients v = 1/M
     (psvi_classes.py:83).  Keyword names follow the reference; arguments that
@@ -168,8 +205,6 @@ class PSVI:
                  nc=None, register_elbos=True, inner_it=10, log_every=10, lr0net=1e-3,
                  device_id=None, learn_z=False, compute_weights_entropy=True, world=1, rank=0,
                  comm=None, **kwargs):
-        if learn_z:
-            raise NotImplementedError("soft labels (learn_z) are not on the HIP inner loop")
         if distr_fn is not categorical_fn:
             raise NotImplementedError("the HIP inner loop implements the categorical likelihood")
         torch.manual_seed(seed)
@@ -189,7 +224,7 @@ class PSVI:
         self.num_pseudo = num_pseudo if num_pseudo is not None else (
             u.shape[0] if u is not None else None)
         self.mc_samples = mc_samples
-        self.learn_v, self.learn_z = learn_v, False
+        self.learn_v, self.learn_z = learn_v, bool(learn_z)
         self.f = f
         self.distr_fn = distr_fn
         self.register_elbos, self.elbos = register_elbos, []
@@ -240,7 +275,9 @@ class PSVI:
         if self.mc_samples is not None and S != self.mc_samples:
             raise ValueError(f"model mc_samples {S} != PSVI mc_samples {self.mc_samples}")
         M = int(self.u.shape[0])
-        if self._noiw_rows(model):
+        if self._noiw_rows(model) or self.learn_z:
+            if self._noiw and self.learn_z:
+                raise NotImplementedError("PSVI_No_IW with soft labels (learn_z)")
             M *= layers[-1][1]
         key = (fam, tuple(layers), S, M, prior_sd)
         if key not in self._plans:
@@ -264,6 +301,10 @@ class PSVI:
     def _check_labels(self, z, C):
         """Class ids in [0, C) -- validated once per label tensor version (a
         device-to-host read; not on every objective call)."""
+        if self.learn_z:
+            if tuple(z.shape[-1:]) != (C,):
+                raise ValueError(f"learn_z: z must be (M, {C}) label logits")
+            return
         key = (id(z), getattr(z, "_version", 0), C)
         if self._labels_ok == key:
             return
@@ -288,8 +329,16 @@ class PSVI:
         D = plan.in_features
         self._check_labels(self.z, C)
         u = self.u.detach().to(self.device, torch.float32).reshape(M0, D).contiguous()
-        z = self.z.detach().to(self.device).to(torch.int32).contiguous()
         w = self.coreset_weights()
+        if self.learn_z:
+            # soft labels as M*C rows (u_i, class c, w_i q_ic), q = softmax(z, 0):
+            # sum_c q (log q - log p) = sum_c q NLL(c) + sum_c q log q
+            # (psvi_classes.py:496-505; the constant is added by inner_elbo)
+            q = torch.softmax(self.z.detach().to(self.device, torch.float32), 0)
+            return (u.repeat_interleave(C, 0).contiguous(),
+                    torch.arange(C, dtype=torch.int32, device=self.device).repeat(M0).contiguous(),
+                    (w[:, None] * q).reshape(-1).contiguous())
+        z = self.z.detach().to(self.device).to(torch.int32).contiguous()
         if plan.M == M0:
             return u, z, w
         Wc = torch.zeros(C, dtype=torch.float32, device=self.device).index_add_(0, z.long(), w)
@@ -305,6 +354,9 @@ class PSVI:
         M0 = int(self.u.shape[0])
         u_g = self.u.reshape(M0, plan.in_features)
         w_g = (self.N * self.f(self.v, 0)).reshape(-1)
+        if self.learn_z:
+            q = torch.softmax(self.z, 0)
+            return u_g.repeat_interleave(q.shape[1], 0), (w_g[:, None] * q).reshape(-1)
         if plan.M == M0:
             return u_g, w_g
         C = plan.layers[-1][1]
@@ -344,6 +396,23 @@ class PSVI:
         z = self.z.detach().to(self.device).long()
         return (du.reshape(M0, C, -1).sum(1),
                 dw.reshape(M0, C).sum(0)[z])
+
+    def _anomaly_check(self, what, *tensors):
+        """With torch.autograd.set_detect_anomaly on (the reference driver's
+        setting, flow_psvi.py:50), a device-side non-finite scan of the step's
+        objective values and gradients (psvi_nonfinite) and ONE flag read per
+        outer step; raises RuntimeError as anomaly mode does.  Off: nothing."""
+        if not torch.is_anomaly_enabled():
+            return
+        ts = [t.detach().contiguous() for t in tensors if t is not None and t.is_cuda]
+        if not ts:
+            return
+        flag = torch.zeros(1, dtype=torch.int32, device=ts[0].device)
+        nonfinite_(flag, *[t if t.dtype in (torch.float32, torch.float64) else t.float()
+                           for t in ts])
+        if int(flag.item()):
+            raise RuntimeError(f"{type(self).__name__}.{what}: non-finite value in the objective "
+                               "or its gradients (anomaly detection)")
 
     def replay_eps(self, draws):
         """Serve the next objective evaluations' noise from ``draws`` (the
@@ -389,6 +458,10 @@ class PSVI:
         u_g, w_g = self._rows_graph(plan)
         out = HipInnerELBO.apply(pvec, u_g, w_g, elbo, grad,
                                  self._row_grad_fn(model, plan, u, z, w, eps, p))
+        if self.learn_z:   # + S sum_m w_m sum_c q log q (KLDivLoss's target entropy term)
+            q = torch.softmax(self.z, 0)
+            wq = (self.N * self.f(self.v, 0)).reshape(-1, 1) * torch.special.xlogy(q, q)
+            out = out + (model_spec(model)[3] * wq.sum()).to(out.dtype)
         out._psvi_inner = dict(plan=plan, u=u, z=z, w=w, eps=eps, u_g=u_g, w_g=w_g, grad=grad,
                                params=p)
         return out
@@ -424,6 +497,7 @@ class PSVI:
                 e = eps[t]
             plan.inner_step(u, z, w, e, params, m, v, step=t + 1, lr=lr, kind=kind,
                             elbo_out=elbos[t:t + 1], ws=ws)
+        self._anomaly_check("inner_loop", elbos, params)
         with torch.no_grad():
             nn.utils.vector_to_parameters(params.to(plist[0].dtype), plist)
         if self.register_elbos:
@@ -462,6 +536,8 @@ class PSVI:
         assert self.mc_samples is None or self.mc_samples > 1  # psvi_classes.py:449
         if S < 2:
             raise ValueError("psvi_elbo needs mc_samples > 1 (psvi_classes.py:449)")
+        if self.learn_z:
+            return self._soft_psvi_elbo(model, fam, layers, S, pvec, xb, yb, Nx, eps)
         plan = self._outer_plan(model, Nx)
         if pvec.numel() != plan.param_count:
             raise ValueError(f"{pvec.numel()} parameters, plan expects {plan.param_count}")
@@ -473,8 +549,45 @@ class PSVI:
             eps = self._draw_eps(plan)
         return HipOuterELBO.apply(pvec, self.u, wp, plan, xb, z_all, w_data, eps)
 
+    def _soft_psvi_elbo(self, model, fam, layers, S, pvec, xb, yb, Nx, eps):
+        """psvi_elbo with soft labels (psvi_classes.py:450-486, learn_z): the
+        targets of all rows are softmax over rows of cat(z, nc onehot(y)),
+        each row r scored sum_c Q_rc (log Q_rc - log p_src).  Rows expand to
+        (r, c) with weight w_r Q_rc; the entropy terms shift every sample's
+        pseudo term by one constant (no effect on the loss) and its data term
+        by cd = N / Nx sum_x sum_c Q_xc log Q_xc, added here."""
+        if self.world > 1:
+            raise NotImplementedError("learn_z with samples split over ranks")
+        C = layers[-1][1]
+        Mu = int(self.u.shape[0])
+        R0 = Mu + Nx
+        key = ("soft-outer", fam, tuple(layers), S, R0 * C)
+        if key not in self._plans:
+            self._plans[key] = self._new_plan(fam, layers, S, R0 * C, model_spec(model)[2],
+                                              outer=True)
+        plan = self._plans[key]
+        if pvec.numel() != plan.param_count:
+            raise ValueError(f"{pvec.numel()} parameters, plan expects {plan.param_count}")
+        onehot = torch.nn.functional.one_hot(yb.long(), C).to(self.z.dtype) * self.nc_or(C)
+        Q = torch.softmax(torch.cat([self.z, onehot]), 0)
+        wp = (self.N * self.f(self.v, 0)).reshape(-1)
+        w_rows = torch.cat([(wp[:, None] * Q[:Mu]).reshape(-1),
+                            (float(self.N) / max(Nx, 1) * Q[Mu:]).reshape(-1)])
+        u_rows = self.u.reshape(Mu, -1).repeat_interleave(C, 0)
+        x_all = torch.cat([u_rows.detach(), xb.repeat_interleave(C, 0)]).to(torch.float32)
+        z_all = torch.arange(C, dtype=torch.int32, device=self.device).repeat(R0).contiguous()
+        if eps is None:
+            eps = self._draw_eps(plan)
+        loss = HipOuterRowsELBO.apply(pvec, u_rows, w_rows, plan, x_all.contiguous(), z_all,
+                                      eps, Mu * C)
+        cd = float(self.N) / max(Nx, 1) * torch.special.xlogy(Q[Mu:], Q[Mu:]).sum()
+        return loss + cd.to(loss.dtype)
+
+    def nc_or(self, C):
+        return self.nc if self.nc is not None else C
+
     def setup_optimizers(self, lr0net=1e-3, lr0u=1e-3, lr0v=1e-2, lr0joint=1e-3,
-                         trainer="hyper"):
+                         trainer="hyper", lr0z=1e-2):
         """The optimisers run_psvi creates (psvi_classes.py:867-885): Adam on
         the network, on u, on v (learn_v), and for trainer 'joint' one Adam
         over all of them."""
@@ -485,6 +598,9 @@ class PSVI:
             self.optim_v = torch.optim.Adam([self.v], lr0v)
         if self._alpha() is not None:   # PSVIAV / PSVIAFixedU (psvi_classes.py:1489, 1761)
             self.optim_alpha = torch.optim.Adam([self.alpha], self.lr0alpha)
+        if self.learn_z:                 # psvi_classes.py:869-870
+            self.z.requires_grad_(True)
+            self.optim_z = torch.optim.Adam([self.z], lr0z)
         if trainer == "joint":
             vp = list(self.model.parameters()) + [self.u] + ([self.v] if self.learn_v else [])
             self.optim = torch.optim.Adam(vp, lr0joint)
@@ -523,10 +639,16 @@ class PSVI:
         Mu = int(self.u.shape[0])
         x_all = torch.cat([self.u.detach().reshape(Mu, -1).to(torch.float32),
                            x_rows]).contiguous()
-        z_all = torch.cat([self.z.detach().to(self.device).reshape(-1),
-                           y_rows.to(self.device).reshape(-1)]).to(torch.int32).contiguous()
-        w_all = torch.cat([self.coreset_weights(),
-                           torch.zeros(x_rows.shape[0], device=self.device)]).contiguous()
+        if self.learn_z:
+            # psvi_classes.py:1049-1056: with soft labels the pseudo term is one
+            # scalar summed over the samples, so W = softmax_s(sampled_nkl_s)
+            zp = torch.zeros(Mu, dtype=torch.int32, device=self.device)
+            wp = torch.zeros(Mu, device=self.device)
+        else:
+            zp = self.z.detach().to(self.device).reshape(-1)
+            wp = self.coreset_weights()
+        z_all = torch.cat([zp, y_rows.to(self.device).reshape(-1)]).to(torch.int32).contiguous()
+        w_all = torch.cat([wp, torch.zeros(x_rows.shape[0], device=self.device)]).contiguous()
         with torch.no_grad():
             pvec = nn.utils.parameters_to_vector(model.parameters()).detach().to(torch.float32)
         e = eps if eps is not None else self._draw_eps(plan)
@@ -752,6 +874,7 @@ class PSVI:
         # 3. hypergradient = -lr * mixed products + the outer objective's direct gradients
         u_grad = (-lr * du.to(torch.float64) + o["grad_u"].to(torch.float64)).to(self.u.dtype)
         w_grad = -lr * dw.to(torch.float64) + o["grad_w"].to(torch.float64)
+        self._anomaly_check("hyper_step", o["loss"], params, u_grad, w_grad)
         self._hparam_steps(u_grad, w_grad)
         # 4. the outer loss at the new hparams, and the inner solution into the model
         u1 = self.u.detach().to(self.device, torch.float32).reshape(self.u.shape[0], -1)
@@ -801,11 +924,10 @@ class PSVI:
         loss (0-dim tensor).  ``eps_inner`` (T draws) / ``eps_outer`` (1):
         optional replay of the reference's draws; default this instance's
         Philox stream."""
-        if truncated:
-            raise NotImplementedError("truncated nested_step (torch.optim.Adam warm start) is "
-                                      "not on the HIP path")
-        if self.learn_z:
-            raise NotImplementedError("soft labels (learn_z) are not on the HIP path")
+        if truncated or self.learn_z:
+            if eps_inner is not None or eps_outer is not None:
+                self.replay_eps(list(eps_inner or []) + list(eps_outer or []))
+            return self._nested_step_unrolled(xbatch, ybatch, truncated, K)
         self._zero_hparam_grads()
         self.optim_net.zero_grad()
         model = self.model
@@ -856,12 +978,83 @@ class PSVI:
             lt += hv
             gu += du.reshape(gu.shape)
             gw += dw
+        self._anomaly_check("nested_step", torch.cat(elbos), o["loss"], p, gu, gw)
         self._hparam_steps(gu, gw)
         if getattr(self, "scheduler_optim_net", None):
             self.scheduler_optim_net.step()
         with torch.no_grad():
             nn.utils.vector_to_parameters(p.to(plist[0].dtype), plist)
         return o["loss"].reshape(()).to(torch.float32)
+
+    def _nested_step_unrolled(self, xbatch, ybatch, truncated=False, K=5):
+        """nested_step on psvi.robust_higher's differentiable inner loop, in the
+        reference's own order (psvi_classes.py:541-600, PSVIAV 1587-1620,
+        PSVIAFixedU 1852-1884): the hypergradients of u, v, alpha and the soft
+        labels z reach them through autograd.  truncated (561-583): first
+        inner_it - K non-differentiable steps of torch.optim.Adam (lr 1e-4) on
+        the inner objective, whose backward accumulates into the network's,
+        u's, v's and z's gradients without zeroing between steps (as the
+        reference's loop: the psvi_elbo hypergradient is added on top); then K
+        differentiable steps."""
+        from ..robust_higher import innerloop_ctx
+
+        self._zero_hparam_grads()
+        self.optim_net.zero_grad()
+        if self.learn_z:
+            self.optim_z.zero_grad()
+        n_diff = self.inner_it
+        if truncated:
+            plist = list(self.model.parameters())
+            p = nn.utils.parameters_to_vector(plist).detach().to(torch.float32).clone()
+            m, v = torch.zeros_like(p), torch.zeros_like(p)
+            for in_it in range(self.inner_it - K):
+                mfvi_loss = self.inner_elbo(model=self.model)
+                with torch.no_grad():
+                    if self.register_elbos and in_it % self.log_every == 0:
+                        self.elbos.append((1, -mfvi_loss.item()))
+                mfvi_loss.backward()
+                # inner_opt.step(): torch.optim.Adam on the accumulated gradients
+                g = torch.cat([(q.grad if q.grad is not None else torch.zeros_like(q)).reshape(-1)
+                               for q in plist]).to(torch.float32).contiguous()
+                adam_update_(p, g, m, v, in_it + 1, 1e-4, kind="torch")
+                with torch.no_grad():
+                    nn.utils.vector_to_parameters(p.to(plist[0].dtype), plist)
+            for q in plist:           # inner_opt.zero_grad()
+                q.grad = None
+            n_diff = K
+        with innerloop_ctx(self.model, self.optim_net) as (fmodel, diffopt):
+            for in_it in range(n_diff):
+                mfvi_loss = self.inner_elbo(model=fmodel)
+                with torch.no_grad():
+                    if self.register_elbos and in_it % self.log_every == 0:
+                        self.elbos.append((1, -mfvi_loss.item()))
+                diffopt.step(mfvi_loss)
+            psvi_loss = self.psvi_elbo(xbatch, ybatch, model=fmodel)
+            with torch.no_grad():
+                if self.register_elbos:
+                    self.elbos.append((0, -psvi_loss.item()))
+            psvi_loss.backward()
+        self._anomaly_check("nested_step", psvi_loss.reshape(1), fmodel.flat,
+                            *[t.grad for t in (self.u, self.v, self.z) if t is not None
+                              and getattr(t, "grad", None) is not None])
+        if self._learn_u:
+            self.optim_u.step()
+        if self.learn_v:
+            self.optim_v.step()
+            if self._alpha() is not None:
+                self.optim_alpha.step()
+            if not getattr(self, "parameterised", False):
+                with torch.no_grad():
+                    torch.clamp_(self.v, min=0.0)
+        if self.learn_z:
+            self.optim_z.step()
+        if getattr(self, "scheduler_optim_net", None):
+            self.scheduler_optim_net.step()
+        with torch.no_grad():
+            nn.utils.vector_to_parameters(
+                nn.utils.parameters_to_vector(list(fmodel.parameters())).to(
+                    next(self.model.parameters()).dtype), self.model.parameters())
+        return psvi_loss
 
     # ------------------------------------------------------------ the driver
     def set_up_model(self):
@@ -914,6 +1107,7 @@ class PSVI:
             idx = (y == c).nonzero().reshape(-1)
             us.append(x[idx[torch.randperm(idx.numel())[:ppc[c]]]])
         self.u = torch.cat(us).reshape(self.num_pseudo, -1).to(self.device).requires_grad_(True)
+        self._soft_label_init()
 
     def pseudo_rand_init(self, variance=1.0):
         """psvi_classes.py:287-308: noisy empirical mean, labels split over classes."""
@@ -925,6 +1119,13 @@ class PSVI:
         self.z = torch.cat([c * torch.ones(per if c < self.nc - 1
                                            else self.num_pseudo - (self.nc - 1) * per)
                             for c in range(self.nc)]).to(self.device)
+        self._soft_label_init()
+
+    def _soft_label_init(self):
+        """learn_z: labels as logits close to one-hot (psvi_classes.py:259-264)."""
+        if self.learn_z:
+            self.z = torch.nn.functional.one_hot(self.z.long(), num_classes=self.nc).float()
+            self.z.requires_grad_(True)
 
     def run_psvi(self, init_args="subsample", trainer="nested", n_layers=1,
                  logistic_regression=True, n_hidden=None, architecture=None, log_every=10,
@@ -939,8 +1140,6 @@ class PSVI:
         gpu_memory, chosen_indices; us, zs, grid_preds with log_pseudodata)."""
         from torch.utils.data import DataLoader
 
-        if self.learn_z:
-            raise NotImplementedError("soft labels (learn_z) are not on the HIP path")
         if init_args not in ("subsample", "random"):
             raise NotImplementedError(f"init_args={init_args!r}: custom / saved initialisations "
                                       "read the reference's selection and results files")
@@ -958,7 +1157,7 @@ class PSVI:
         self.set_up_model()
         (self.pseudo_subsample_init if init_args == "subsample" else self.pseudo_rand_init)()
         self.setup_optimizers(lr0net=lr0net, lr0u=lr0u, lr0v=lr0v, lr0joint=lr0joint,
-                              trainer=trainer)
+                              trainer=trainer, lr0z=lr0z)
         self.scheduler_optim_net = torch.optim.lr_scheduler.StepLR(
             self.optim_net, step_size=epoch_quarter if epoch_quarter > 0 else 10000,
             gamma=self.gamma)

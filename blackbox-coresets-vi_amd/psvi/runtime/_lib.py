@@ -97,6 +97,7 @@ SIGNATURES = {
     "psvi_adam_adjoint": (_I32, [_I64, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP),
                                  _P]),
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),
+    "psvi_nonfinite": (_I32, [_P, _I64, _I32, _P, _P]),
     "psvi_adam_update": (_I32, [_I64, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P]),
     "psvi_debug_set": (_I32, [_I32, _I32]),
     "psvi_debug_set_ptr": (_I32, [_I32, _P]),

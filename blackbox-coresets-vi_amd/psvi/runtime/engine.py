@@ -432,6 +432,21 @@ def randn_(out, seed, offset=0):
     return out
 
 
+def nonfinite_(flag, *tensors):
+    """flag (device int32, 1 element) |= 1 if any value of the float32 /
+    float64 device tensors is NaN or +-inf (psvi_nonfinite; no host sync)."""
+    _need(flag, "flag", 1, torch.int32)
+    lib = _lib.load()
+    for t in tensors:
+        if t is None:
+            continue
+        if t.dtype not in (torch.float32, torch.float64) or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("nonfinite_: contiguous float32 / float64 device tensors")
+        check(lib.psvi_nonfinite(_ptr(t), t.numel(), int(t.dtype == torch.float64), _ptr(flag),
+                                 _stream()), "psvi_nonfinite")
+    return flag
+
+
 def adam_adjoint_(lt, lm, lv, adam_m, adam_v, grad, step, lr, lg_out, kind="higher",
                   betas=(0.9, 0.999), eps=1e-8):
     """Reverse of one Adam step (psvi_adam_adjoint): lm, lv updated in place,

@@ -360,6 +360,13 @@ int psvi_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv, const fl
  * Throughput-mode replacement for torch's normal_() draw (not bit-identical
  * to torch's generator; parity mode passes torch-drawn eps instead). */
 int psvi_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, void* stream);
+/* flag[0] |= 1 when any of the n values at data (dtype 0: float, 1: double;
+ * device) is NaN or +-inf; flag is a caller-zeroed device int32.  The HIP
+ * path's stand-in for torch.autograd.set_detect_anomaly, which the reference
+ * driver turns on (psvi/experiments/flow_psvi.py:50): PSVI's trainers check
+ * their ELBO / loss / gradient buffers with it and read the flag once per
+ * outer step when anomaly detection is enabled. */
+int psvi_nonfinite(const void* data, int64_t n, int32_t dtype, int32_t* flag, void* stream);
 /* Generic fused Adam over n floats (either variant). */
 int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m,
                      float* adam_v, const psvi_adam_hp* hp, void* stream);

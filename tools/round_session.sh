@@ -20,7 +20,7 @@ if [[ $STEPS == *bench* ]]; then
   timeout -k 10 600 python bench.py > gpurun_out/bench_${R}.log 2>&1; rc=$?
   echo "bench rc=$rc"; tail -1 gpurun_out/bench_${R}.log; ok $rc || exit $rc
 fi
-BCMD="python3 bench.py --no-cpu-baseline --no-trainers --no-lenet --steps 200 --warmup 20"
+BCMD="python3 bench.py --no-cpu-baseline --no-trainers --no-lenet --no-c4 --no-c2 --steps 200 --warmup 20"
 if [[ $STEPS == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${R} -o bench -- $BCMD > gpurun_out/prof_${R}.log 2>&1; rc=$?
   echo "prof rc=$rc"; ok $rc || exit $rc
@@ -30,7 +30,7 @@ if [[ $STEPS == *lprof* ]]; then
   echo "lenet prof rc=$rc"; ok $rc || exit $rc
 fi
 if [[ $STEPS == *pmc* ]]; then
-  CMD="python3 bench.py --no-cpu-baseline --no-trainers --no-lenet --steps 50 --warmup 5" \
+  CMD="python3 bench.py --no-cpu-baseline --no-trainers --no-lenet --no-c4 --no-c2 --steps 50 --warmup 5" \
   PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS|SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY|SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
     bash tools/pmc_session.sh; rc=$?
   echo "pmc rc=$rc"; ok $rc || exit $rc
