@@ -144,7 +144,14 @@ def test_inner_loop_refuses_cpu_tensors():
 def test_second_order_entry_points_raise():
     f, model = fixture_model("g1_logreg_c1")
     ps = make_psvi(f, model)
-    for fn in (lambda: ps.nested_step(None, None, truncated=True),
+    def soft_hyper():
+        ps.learn_z = True       # the reference's hyper_step raises for learn_z (619-620)
+        try:
+            ps.hyper_step(None, None)
+        finally:
+            ps.learn_z = False
+
+    for fn in (soft_hyper,
                lambda: ps.run_psvi(init_args="custom"),
                lambda: ps.hyper_step(None, None, hypergrad_approx="neumann")):
         with pytest.raises(NotImplementedError):
