@@ -34,6 +34,7 @@ namespace {
 
 thread_local std::string g_err;
 int g_stream_wgs = 0;       // psvi_debug_set(PSVI_DBG_STREAM_WGS, n): streaming-update workgroups (0 = 256)
+int g_stream_rr = 0;        // psvi_debug_set(PSVI_DBG_STREAM_RR, 1): runs dealt round-robin over XCDs (A/B)
 int g_upd_chunk_tiles = 0;  // psvi_debug_set(PSVI_DBG_UPD_CHUNK, n): c-blocks per update chunk (0 = auto)
 
 int fail(int code, const std::string& msg) {
@@ -349,6 +350,17 @@ int build_plan(psvi_plan& p) {
                     p.h_sfrb.push_back(FwdRowBlock{sl.front(), (int)sl.size(), R,
                                                    p.xcol_l[r][l] + r0, l, r0});
                 }
+            // XCD-aware placement: workgroup w runs on XCD w % 8 (round-robin
+            // dispatch), so XCD x takes the contiguous eighth [x per, (x + 1) per)
+            // of the run list -- its bands' G slices and the eps / eps' columns
+            // up to its last band stay in that XCD's L2 instead of every XCD
+            // touching every band of both layers
+            if (nwg % 8 == 0 && !g_stream_rr) {
+                const int per = nwg / 8;
+                std::vector<StreamRange> xr(nwg);
+                for (int w = 0; w < nwg; ++w) xr[w] = p.h_str[(w % 8) * per + w / 8];
+                p.h_str.swap(xr);
+            }
             p.n_str = (int)p.h_str.size();
             p.n_sfrb = (int)p.h_sfrb.size();
             p.n_sslots = ns;
@@ -404,6 +416,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
+        case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }
 }

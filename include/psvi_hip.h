@@ -421,6 +421,10 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     (A/B diagnostics; 0 = streaming)           */
 #define PSVI_DBG_STREAM_WGS 11   /* value: workgroups of the streaming update for
                                     plans created afterwards (0 = 256)         */
+#define PSVI_DBG_STREAM_RR 12    /* value: 1 = the streaming update's runs dealt
+                                    round-robin over the XCDs instead of one
+                                    contiguous eighth per XCD (plans created
+                                    afterwards; A/B diagnostics)               */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
