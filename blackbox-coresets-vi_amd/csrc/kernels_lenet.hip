@@ -24,6 +24,8 @@
 
 namespace psvi {
 
+int g_lenet_gemm_valu = 0;  // psvi_debug_set(PSVI_DBG_LENET_GEMM_VALU, 1): the VALU head GEMM (A/B)
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -520,6 +522,86 @@ __global__ __launch_bounds__(kThreads) void lenet_gemm_kernel(GemmArgs g) {
     }
 }
 
+// The same batched GEMM on the matrix cores: 64x64 tiles, four waves of one
+// 32x32 v_mfma_f32_32x32x2_f32 accumulator each, k-steps of 16 staged through
+// two LDS buffers (the next step's operands are loaded into registers before
+// this step's MFMAs and written to the other buffer after them: one barrier
+// per step).  Operand reads: lane l takes A(m0 + 32 wr + l % 32, k + l / 32)
+// and B(k + l / 32, n0 + 32 wc + l % 32) -- 68-word LDS rows, conflict free.
+// Accumulator element q of lane l is C(32 wr + 8 (q / 4) + 4 (l / 32) + q % 4,
+// 32 wc + l % 32).  Same epilogue flags as lenet_gemm_kernel.
+typedef float gemm_f32x16 __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(kThreads) void lenet_gemm_mfma_kernel(GemmArgs g) {
+    __shared__ float As[2][16][68];
+    __shared__ float Bs[2][16][68];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1, h = lane >> 5, l32 = lane & 31;
+    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64, b = blockIdx.z;
+    const float* A = g.A + b * g.sAb;
+    const float* B = g.B + b * g.sBb;
+    const bool a_kfast = g.sAk == 1, b_nfast = g.sBn == 1;
+    float ra[4], rb[4];
+    auto gload = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = tid + r * kThreads;
+            int mm, kk;
+            if (a_kfast) { kk = e & 15; mm = e >> 4; } else { mm = e & 63; kk = e >> 6; }
+            const int gm = m0 + mm, gk = k0 + kk;
+            ra[r] = (gm < g.M && gk < g.K) ? A[(int64_t)gm * g.sAm + (int64_t)gk * g.sAk] : 0.f;
+            int nn, kb;
+            if (b_nfast) { nn = e & 63; kb = e >> 6; } else { kb = e & 15; nn = e >> 4; }
+            const int gn = n0 + nn, gkb = k0 + kb;
+            rb[r] = (gn < g.N && gkb < g.K) ? B[(int64_t)gkb * g.sBk + (int64_t)gn * g.sBn] : 0.f;
+        }
+    };
+    auto sstore = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = tid + r * kThreads;
+            int mm, kk;
+            if (a_kfast) { kk = e & 15; mm = e >> 4; } else { mm = e & 63; kk = e >> 6; }
+            As[buf][kk][mm] = ra[r];
+            int nn, kb;
+            if (b_nfast) { nn = e & 63; kb = e >> 6; } else { kb = e & 15; nn = e >> 4; }
+            Bs[buf][kb][nn] = rb[r];
+        }
+    };
+    gemm_f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < g.K; k0 += 16) {
+        const bool more = k0 + 16 < g.K;
+        if (more) gload(k0 + 16);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][2 * kk + h][32 * wr + l32],
+                                                       Bs[buf][2 * kk + h][32 * wc + l32], acc,
+                                                       0, 0, 0);
+        if (more) sstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* C = g.C + b * g.sCb;
+    const int n = n0 + 32 * wc + l32;
+    if (n >= g.N) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int m = m0 + 32 * wr + 8 * (q >> 2) + 4 * h + (q & 3);
+        if (m >= g.M) continue;
+        float v = acc[q];
+        if (g.epi & 8) v += C[(int64_t)m * g.sCm + n];  // accumulate onto C
+        if (g.epi & 1) v += g.bias[b * g.sbias + n];
+        if (g.epi & 2) v = fmaxf(v, 0.f);
+        if (g.epi & 4) v = g.mask[b * g.sMb + (int64_t)m * g.sMm + n] > 0.f ? v : 0.f;
+        C[(int64_t)m * g.sCm + n] = v;
+    }
+}
+
 // out[b * sOb + n] = sum_m X[b][m][n]  (bias gradients): one workgroup per
 // (b, 64 columns), four row groups (m = g mod 4) summed in a fixed order
 __global__ __launch_bounds__(kThreads) void lenet_colsum_kernel(const float* __restrict__ X,
@@ -1003,7 +1085,10 @@ __global__ __launch_bounds__(kThreads) void lenet_hvp_assemble_kernel(
 
 hipError_t gemm(const GemmArgs& g, int batch, hipStream_t st) {
     dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, batch);
-    hipLaunchKernelGGL(lenet_gemm_kernel, grid, dim3(kThreads), 0, st, g);
+    if (g_lenet_gemm_valu)
+        hipLaunchKernelGGL(lenet_gemm_kernel, grid, dim3(kThreads), 0, st, g);
+    else
+        hipLaunchKernelGGL(lenet_gemm_mfma_kernel, grid, dim3(kThreads), 0, st, g);
     return hipGetLastError();
 }
 
