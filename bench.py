@@ -366,8 +366,9 @@ def trainer_timings(dev, cpu=True, cpu_T=2):
     ps.register_elbos = False
     ps.setup_optimizers()
 
-    def wall_ms(fn, n):
-        fn()
+    def wall_ms(fn, n, warm=1):
+        for _ in range(warm):  # plan creation, workspace and allocator growth
+            fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(n):
@@ -376,14 +377,14 @@ def trainer_timings(dev, cpu=True, cpu_T=2):
         return round((time.perf_counter() - t0) / n * 1e3, 3)
 
     out = {}
-    out["psvi_elbo_fwd_bwd_ms"] = wall_ms(lambda: ps.psvi_elbo(xb, yb).backward(), 10)
+    out["psvi_elbo_fwd_bwd_ms"] = wall_ms(lambda: ps.psvi_elbo(xb, yb).backward(), 20, warm=3)
     plan = ps._plan(model)
     pv = torch.nn.utils.parameters_to_vector(model.parameters()).detach().clone()
     vec = torch.randn(pv.numel(), device=dev)
     e = torch.empty(plan.eps_count, device=dev)
     randn_(e, 3)
     zi = z.to(torch.int32)
-    out["psvi_hvp_ms"] = wall_ms(lambda: plan.hvp(u, zi, w, e, pv, vec), 10)
+    out["psvi_hvp_ms"] = wall_ms(lambda: plan.hvp(u, zi, w, e, pv, vec), 20, warm=3)
     ps.inner_it = cpu_T
     out[f"nested_step_T{cpu_T}_ms"] = wall_ms(lambda: ps.nested_step(xb, yb), 3)
     ps.inner_it = 100

@@ -109,16 +109,17 @@ template <bool ACONT, bool BCONT, int NQ>
 struct TileOps {
     float4 a;
     float4 b[NQ];
-    __device__ __forceinline__ static float4 ld(const float* X, int ldx, int row, int k, bool cont) {
-        if (cont) return *reinterpret_cast<const float4*>(X + row * ldx + k);
-        return make_float4(X[k * ldx + row], X[(k + 1) * ldx + row], X[(k + 2) * ldx + row],
-                           X[(k + 3) * ldx + row]);
+    // k-contiguous: one float4 at p; k-strided: p[0], p[ld], p[2 ld], p[3 ld]
+    __device__ __forceinline__ static float4 ld(const float* p, int ldx, bool cont) {
+        if (cont) return *reinterpret_cast<const float4*>(p);
+        return make_float4(p[0], p[ldx], p[2 * ldx], p[3 * ldx]);
     }
-    __device__ __forceinline__ void load(const float* A, int lda, const float* B, int ldb, int p,
-                                         int q, int k) {
-        a = ld(A, lda, p, k, ACONT);
+    // pa / pb: this lane's first operand element of the k-group; column tile c
+    // of B sits 16 c rows (BCONT) or 16 c columns further
+    __device__ __forceinline__ void load(const float* pa, int lda, const float* pb, int ldb) {
+        a = ld(pa, lda, ACONT);
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) b[c] = ld(B, ldb, q + 16 * c, k, BCONT);
+        for (int c = 0; c < NQ; ++c) b[c] = ld(pb + 16 * c * (BCONT ? ldb : 1), ldb, BCONT);
     }
     __device__ __forceinline__ void mma(floatx4 (&acc)[NQ]) const {
 #pragma unroll
@@ -135,11 +136,13 @@ struct TileOps {
 // 16-row tile x NQ column tiles -- a whole row of column tiles (NQ = tq <= 3:
 // one A read per NQ MFMAs) when that still gives every SIMD a unit, else
 // single tiles.  Unit u goes to wave (u + first) % nwaves, so two GEMMs of
-// one phase share the round-robin.  Each wave runs its (unit, k-group) steps
-// as one software pipeline: the next step's operands -- also across units --
-// are read before the current step's MFMAs and epilogue.
+// one phase share the round-robin.  Per unit: the operand pointers are
+// formed once, the k-groups run as a two-deep register pipeline (the next
+// group's LDS reads issued before the current group's MFMAs) with constant
+// pointer steps, and the next unit's first group is read before this unit's
+// epilogue.
 __device__ __forceinline__ int gemm_nq(int tp, int tq) {
-    return (tq <= 3 && tp >= 4) ? tq : 1;
+    return (tq <= 3 && 2 * tp >= (int)(blockDim.x >> 6)) ? tq : 1;
 }
 __device__ __forceinline__ int gemm_units(int P, int Q) {
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4;
@@ -150,55 +153,54 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
                                            const float* B, int ldb, Epi epi) {
     const int nwv = blockDim.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
     const int nk = K16 >> 4;
-    const int nmine = u0 < nu ? (nu - u0 + nwv - 1) / nwv : 0;
-    const int T = nmine * nk;
-    if (T == 0) return;
-    // step st -> unit u0 + (st / nk) * nwv, k-group st % nk (tracked
-    // incrementally).  Loads past the last step repeat it: every operand load
-    // is unconditional, so s_waitcnt can count the prefetches in flight (a
-    // load under a branch makes it wait for all of them).
-    int lu = u0, lk = 0, lst = 0;  // the step to load next
-    auto lcoords = [&](int& p, int& q, int& k) {
-        const int pt = lu / tqu, qt = (lu - pt * tqu) * NQ;
-        p = (pt << 4) + i16;
-        q = (qt << 4) + i16;
-        k = (lk << 4) + 4 * k4;
-        if (lst < T - 1) {
-            ++lst;
-            if (++lk == nk) { lk = 0; lu += nwv; }
-        }
+    if (u0 >= nu) return;  // wave-uniform
+    const int da = ACONT ? 16 : 16 * lda, db = BCONT ? 16 : 16 * ldb;  // one k-group
+    auto ptrs = [&](int u, const float*& pa, const float*& pb, int& p0, int& q0) {
+        const int pt = u / tqu, qt = (u - pt * tqu) * NQ;
+        p0 = pt << 4;
+        q0 = qt << 4;
+        pa = ACONT ? A + (p0 + i16) * lda + 4 * k4 : A + 4 * k4 * lda + p0 + i16;
+        pb = BCONT ? B + (q0 + i16) * ldb + 4 * k4 : B + 4 * k4 * ldb + q0 + i16;
     };
-    int eu = u0, ek = 0;  // the step to compute
-    floatx4 acc[NQ];
-#pragma unroll
-    for (int c = 0; c < NQ; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    auto finish = [&]() {
-        if (++ek == nk) {
-            const int pt = eu / tqu, qt = (eu - pt * tqu) * NQ;
-#pragma unroll
-            for (int c = 0; c < NQ; ++c) {
-                epi(pt * 16 + 4 * k4, (qt + c) * 16 + i16, acc[c]);
-                acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-            }
-            ek = 0;
-            eu += nwv;
-        }
-    };
+    const float *pa, *pb;
+    int p0, q0;
+    ptrs(u0, pa, pb, p0, q0);
     TileOps<ACONT, BCONT, NQ> x0, x1;
-    int p, q, k;
-    lcoords(p, q, k);
-    x0.load(A, lda, B, ldb, p, q, k);
-    for (int st = 0; st < T; st += 2) {  // wave-uniform
-        lcoords(p, q, k);
-        x1.load(A, lda, B, ldb, p, q, k);
-        x0.mma(acc);
-        finish();
-        lcoords(p, q, k);
-        x0.load(A, lda, B, ldb, p, q, k);
-        if (st + 1 < T) {
+    x0.load(pa, lda, pb, ldb);
+    for (int u = u0; u < nu; u += nwv) {  // wave-uniform
+        floatx4 acc[NQ];
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // x0 holds group 0; two groups per trip with fixed registers (no
+        // copies at the back edge, so the reads of the group after next stay
+        // in flight across the current group's MFMAs), then a 1- or 2-group tail
+        int kg = 0;
+        for (; kg + 2 < nk; kg += 2) {
+            pa += da;
+            pb += db;
+            x1.load(pa, lda, pb, ldb);
+            x0.mma(acc);
+            pa += da;
+            pb += db;
+            x0.load(pa, lda, pb, ldb);
             x1.mma(acc);
-            finish();
         }
+        if (kg + 1 < nk) {
+            pa += da;
+            pb += db;
+            x1.load(pa, lda, pb, ldb);
+            x0.mma(acc);
+            x1.mma(acc);
+        } else {
+            x0.mma(acc);
+        }
+        const int pe = p0, qe = q0;
+        if (u + nwv < nu) {
+            ptrs(u + nwv, pa, pb, p0, q0);
+            x0.load(pa, lda, pb, ldb);
+        }
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) epi(pe + 4 * k4, qe + 16 * c + i16, acc[c]);
     }
 }
 template <bool ACONT, bool BCONT, class Epi>
@@ -218,11 +220,12 @@ __device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const 
 // local sample s.  One source rank: one contiguous row per sample.  Several:
 // the row's source from the per-workgroup table srct in LDS ([nsrc][L]
 // source-end rows, then [nsrc][L] 64-bit offsets), built at kernel start.
-__device__ __forceinline__ int64_t fc_addr(const NetArgs& a, const int* srct, int l, int r, int s) {
-    if (a.nsrc == 1) return (int64_t)s * a.src_stride[0] + a.src_col[0][l] + r;
+__device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int nsrc, const int* srct, int l, int r,
+                                           int s) {
+    if (nsrc == 1) return (int64_t)s * a.src_stride[0] + a.src_col[0][l] + r;
     const int L = a.L;
     int p = 0;
-    while (p + 1 < a.nsrc && r >= srct[p * L + l]) ++p;
+    while (p + 1 < nsrc && r >= srct[p * L + l]) ++p;
     const int64_t* off = reinterpret_cast<const int64_t*>(srct + 2 * kMaxWorld * kMaxL);
     return off[p * L + l] + r;
 }
@@ -231,6 +234,13 @@ __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, const int* srct, in
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dppf<0x128>(v));
+    v = fmaxf(v, dppf<0x124>(v));
+    v = fmaxf(v, dppf<0x122>(v));
+    v = fmaxf(v, dppf<0x121>(v));
+    return v;
 }
 __device__ __forceinline__ float row16_sum(float v) {
     v += dppf<0x128>(v);  // row_ror:8
@@ -249,7 +259,11 @@ __device__ __forceinline__ float row16_sum(float v) {
         if (a.stamps && threadIdx.x == 0) stl[(k)] = (val);                \
     } while (0)
 
-template <int FAM>
+// MSRC: full-cov rows from several source ranks (world > 1).  The single-source
+// instantiation has straight-line x loads: with the run-table path in the
+// same kernel the register allocator shares registers across the two paths
+// and the waitcnt pass then serialises the u and x loads (seen in the ISA).
+template <int FAM, bool MSRC>
 __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
@@ -262,6 +276,8 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
     if (a.stamps && threadIdx.x < 16) stl[threadIdx.x] = 0;
     NET_STAMP(0, __builtin_amdgcn_s_memtime());
+    // diagnostics: each wave's start, for the launch skew in slot 15
+    const unsigned long long wstart = a.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
     NET_STAMP(13, __builtin_amdgcn_s_memrealtime());  // chip-wide 100 MHz clock
 
     // layers whose weight gradients this workgroup produces: [own_lo, own_hi)
@@ -270,13 +286,14 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
 
     // ---- 1. loads --------------------------------------------------------
     int* srct = reinterpret_cast<int*>(sm + a.lsrc);
-    if (FAM == PSVI_FAMILY_FULLCOV && a.nsrc > 1) {
+    const int nsrc = MSRC ? a.nsrc : 1;
+    if (FAM == PSVI_FAMILY_FULLCOV && MSRC) {
         // uniform loops: a per-lane index into the by-value kernel arguments
         // would make the compiler copy the whole argument block to scratch
         int64_t* off = reinterpret_cast<int64_t*>(srct + 2 * kMaxWorld * kMaxL);
         int64_t* xb = reinterpret_cast<int64_t*>(srct + 4 * kMaxWorld * kMaxL);
         int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
-        for (int p = 0; p < a.nsrc; ++p) {
+        for (int p = 0; p < nsrc; ++p) {
             for (int l = 0; l < L; ++l)
                 if (tid == 0) {
                     srct[p * L + l] = a.src_hi[p][l];
@@ -304,42 +321,42 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int ldx0 = a.ldx[0];
     float* stage = sm + a.lstage;
     {
-        constexpr int kU = 4, kX = 12;
-        const bool u4 = (D & 3) == 0;
-        const int nu = u4 ? mcnt * (D >> 2) : mcnt * D;  // float4s or floats of u
-        const float rdu = 1.f / (float)(u4 ? D >> 2 : D);
+        // u chunk as a flat run of nu floats (one load path for every D: two
+        // paths -- float4 rows and scalars -- are tail-merged by the compiler
+        // into split loads serialised on s_waitcnt vmcnt, seen in the ISA)
+        constexpr int kU = 16, kX = 12;
+        const int nu = mcnt * D;
+        const float rdu = 1.f / (float)D;
         const float* usrc = a.u + (int64_t)m0 * D;
         const int nx = FAM == PSVI_FAMILY_FULLCOV ? a.stage_len : 0;
         const int bd = blockDim.x;
         for (int pass = 0; pass * kU * bd < nu || pass * kX * bd < nx || pass == 0; ++pass) {  // uniform
             const int bu = pass * kU * bd + tid, bx = pass * kX * bd + tid;
-            float4 uv[kU];
+            float uv[kU];
             float xv[kX];
             int zi = 0;
             float wv = 0.f;
             if (!(a.abl & 1)) {
 #pragma unroll
-                for (int k = 0; k < kU; ++k) {
-                    const int idx = max(min(bu + k * bd, nu - 1), 0);
-                    uv[k] = u4 ? *reinterpret_cast<const float4*>(usrc + 4 * idx)
-                               : make_float4(usrc[idx], 0.f, 0.f, 0.f);
-                }
+                for (int k = 0; k < kU; ++k) uv[k] = usrc[max(min(bu + k * bd, nu - 1), 0)];
                 if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
-                    // stage position r -> x_recv: one source, one run; several, the
-                    // run table in LDS (a per-lane pick among the kernel arguments
-                    // makes the compiler copy the whole argument block to scratch)
-                    const int64_t* xb = reinterpret_cast<const int64_t*>(srct + 4 * kMaxWorld * kMaxL);
-                    const int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
+                    if constexpr (!MSRC) {
+                        const float* xr = a.xrecv + (int64_t)s * a.src_stride[0];
 #pragma unroll
-                    for (int k = 0; k < kX; ++k) {
-                        const int r = max(min(bx + k * bd, nx - 1), 0);
-                        int64_t base = (int64_t)s * a.src_stride[0];
-                        if (a.nsrc > 1) {
+                        for (int k = 0; k < kX; ++k) xv[k] = xr[max(min(bx + k * bd, nx - 1), 0)];
+                    } else {
+                        // stage position r -> x_recv through the run table in LDS (a
+                        // per-lane pick among the kernel arguments makes the compiler
+                        // copy the whole argument block to scratch)
+                        const int64_t* xb = reinterpret_cast<const int64_t*>(srct + 4 * kMaxWorld * kMaxL);
+                        const int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
+#pragma unroll
+                        for (int k = 0; k < kX; ++k) {
+                            const int r = max(min(bx + k * bd, nx - 1), 0);
                             int q = 0;
-                            while (q + 1 < a.nsrc && r >= xs0[q + 1]) ++q;
-                            base = xb[q];
+                            while (q + 1 < nsrc && r >= xs0[q + 1]) ++q;
+                            xv[k] = a.xrecv[xb[q] + r];
                         }
-                        xv[k] = a.xrecv[base + r];
                     }
                 }
                 if (pass == 0) {
@@ -347,15 +364,6 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     zi = a.z[m0 + mm];
                     wv = a.w[m0 + mm];
                 }
-            }
-            if (pass == 0 && a.rn_out) {
-                // the next step's normals while the loads are in flight (psvi_randn's stream)
-                const int64_t nq = (a.rn_n + 3) / 4;
-                const int nblk = gridDim.x * gridDim.y * gridDim.z;
-                const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-                const int64_t per = (nq + nblk - 1) / nblk, q1 = min(nq, (b + 1) * per);
-                for (int64_t q = b * per + tid; q < q1; q += bd)
-                    randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
             }
             if (pass == 0) {
                 // zero padding while the loads are in flight (disjoint from every
@@ -383,12 +391,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 const int idx = bu + k * bd;
                 if (idx < nu) {
                     const int m = (int)(((float)idx + 0.5f) * rdu);  // exact for idx < 2^21
-                    if (u4) {
-                        const int c = idx - m * (D >> 2);
-                        *reinterpret_cast<float4*>(X0 + m * ldx0 + 4 * c) = uv[k];
-                    } else {
-                        X0[m * ldx0 + idx - m * D] = uv[k].x;
-                    }
+                    X0[m * ldx0 + idx - m * D] = uv[k];
                 }
             }
             if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         // scatter: source p's run holds rows [lo, hi) of each layer l at
         // src_col[p][l]; x row r of layer l is W[j][i] (r = j*din + i) or b
         constexpr int kB = 8;
-        for (int p = 0; p < a.nsrc && !(a.abl & 1); ++p) {
+        for (int p = 0; p < nsrc && !(a.abl & 1); ++p) {
             for (int l = 0; l < L; ++l) {
                 const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
                 const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l];
@@ -475,8 +478,14 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             }
         }
     }
+    if (a.stamps && (tid & 63) == 0) stl[16 + wave_id()] = wstart;
     __syncthreads();  // the LDS stores
     NET_STAMP(1, __builtin_amdgcn_s_memtime());
+    if (a.stamps && tid == 0) {
+        unsigned long long mx = 0;
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) mx = max(mx, stl[16 + q]);
+        stl[15] = mx;
+    }
 
     // ---- 2. forward: X_{l+1} = relu(X_l W_l^T + b_l), then the logits
     // X_L = X_{L-1} W_{L-1}^T + b_{L-1} into dl.  Rows past the chunk and
@@ -484,6 +493,13 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     if (FAM == PSVI_FAMILY_FULLCOV)  // the slacks the stage overlapped
         for (int k = a.nslack_early + wave_id(); k < a.nslack; k += blockDim.x >> 6)
             sm[a.slack[k] + (tid & 63)] = 0.f;
+    // The inner objective's loss head (C <= 16: one column tile, a row's
+    // logits on the 16 lanes of a DPP row) runs in the head GEMM's epilogue:
+    // log-softmax over the lanes, weighted NLL, dlogits w_m (softmax - onehot)
+    // stored in place of the logits -- no separate phase and barrier.
+    const int C = a.dout[L - 1];
+    const bool fuse_head = a.outer == 0 && C <= 16 && !(a.abl & 4);
+    float part = 0.f;  // this thread's share of the chunk's weighted NLL
     for (int l = 0; l < L; ++l) {
         const int din = a.din[l], dout = a.dout[l];
         const bool head = l == L - 1;
@@ -491,6 +507,30 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         float* Xn = head ? sm + a.ldl : sm + a.lx[l + 1];
         const float* Bv = sm + a.lb[l];
         const int ldn = head ? a.lddl : a.ldx[l + 1], jend = min((dout + 15) & ~15, ldn);
+        if (head && fuse_head) {
+            auto epi = [&](int m, int j, floatx4 v) {  // j = i16: every lane of the row takes part
+                const bool jl = j < C;
+                const float b = Bv[min(j, C - 1)];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m + r;
+                    const float y = v[r] + b;
+                    const float mx = row16_max(jl ? y : -INFINITY);
+                    const float lse = mx + logf(row16_sum(jl ? expf(y - mx) : 0.f));
+                    const int zr = __float_as_int(zw[row]);
+                    const float wr = zw[Mp + row];
+                    const bool ok = row < mcnt;
+                    const float dl = (ok && jl) ? wr * (expf(y - lse) - (j == zr ? 1.f : 0.f)) : 0.f;
+                    if (j < jend) Xn[row * ldn + j] = dl;
+                    if (ok && j == zr) part += wr * (lse - y);
+                }
+            };
+            if (!(a.abl & 2))
+                mfma_gemm<true, true>(Mp, dout, din, 0, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
+            __syncthreads();
+            if (l < 3) NET_STAMP(9 + l, __builtin_amdgcn_s_memtime());
+            continue;
+        }
         auto epi = [&](int m, int j, floatx4 v) {
             if (j < jend) {
                 const bool jl = j < dout;
@@ -513,9 +553,8 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
 
     // ---- 3. loss head: one thread per pseudopoint, logits -> weighted NLL,
     // dlogits w_m (softmax - onehot) in place (rows past the chunk stay 0)
-    {
-        const int C = a.dout[L - 1], ldl = a.lddl;
-        float part = 0.f;
+    if (!fuse_head) {
+        const int ldl = a.lddl;
         // outer backward: d loss / d pseudo_s and d loss / d data_s scale the rows
         const float cp = a.outer == 2 ? a.rowcoef[2 * s] : 1.f;
         const float cd = a.outer == 2 ? a.rowcoef[2 * s + 1] : 1.f;
@@ -576,10 +615,6 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     row[c] = wm * (expf(row[c] - lse) - (c == zm ? 1.f : 0.f));
             }
         }
-        if (role == 0 && a.outer == 0) {
-            const float tot = block_sum(part, sm + a.lred);  // its barriers end the phase
-            if (tid == 0) atomicAdd(a.nll_out, (double)tot);
-        }
         __syncthreads();
     }
     NET_STAMP(3, __builtin_amdgcn_s_memtime());
@@ -599,7 +634,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             atomicAdd(a.accMu + a.woff[l] + o, v);
             atomicAdd(a.accRho + a.woff[l] + o, v * e);
         } else {
-            float* dst = a.gsend + fc_addr(a, srct, l, o, s);
+            float* dst = a.gsend + fc_addr(a, nsrc, srct, l, o, s);
             if (a.atomic_g) atomicAdd(dst, v); else *dst = v;
         }
     };
@@ -684,6 +719,21 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         cur ^= 1;
     }
     asm volatile("" ::"v"(sink));
+    if (role == 0 && a.outer == 0) {  // the chunk's weighted NLL (role 1 computed the same)
+        const float tot = block_sum(part, sm + a.lred);
+        if (tid == 0) atomicAdd(a.nll_out, (double)tot);
+    }
+    if (a.rn_out) {
+        // the next step's normals (psvi_randn's stream), split over the grid's
+        // workgroups.  Last, so that no s_waitcnt of the phases above waits for
+        // these stores to retire.
+        const int64_t nq = (a.rn_n + 3) / 4;
+        const int nblk = gridDim.x * gridDim.y * gridDim.z;
+        const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int64_t per = (nq + nblk - 1) / nblk, q1 = min(nq, (b + 1) * per);
+        for (int64_t q = b * per + tid; q < q1; q += blockDim.x)
+            randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
+    }
     NET_STAMP(12, __builtin_amdgcn_s_memtime());
     NET_STAMP(14, __builtin_amdgcn_s_memrealtime());
     if (a.stamps && threadIdx.x < 16)  // wave 0 wrote them: in order, no barrier needed
@@ -722,7 +772,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     const int lx0 = take((size_t)Mp * ldx0);
     const int lred = take(16);
     const int lzw = take(2 * (size_t)Mp);
-    const int lstamp = take(32);  // 16 x uint64 diagnostics stamps
+    const int lstamp = take(48);  // 16 x uint64 diagnostics stamps + 8 wave starts
     // per-workgroup source tables (world > 1): [nsrc][L] ints, [nsrc][L] int64
     // (8-byte aligned), the stage's per-source int64 bases and int starts
     const int lsrc = take(4 * kMaxWorld * kMaxL + 3 * kMaxWorld);
@@ -764,6 +814,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     return off;
 }
 
+int g_net_threads = 0;        // psvi_debug_set(PSVI_DBG_NET_THREADS, n): 0 = by chunk size
 int g_net_split_below = 256;  // split when a rank has fewer samples than CUs (psvi_debug_set(PSVI_DBG_NET_SPLIT_BELOW, n))
 
 size_t net_plan_geometry(psvi_plan& p) {
@@ -787,7 +838,7 @@ size_t net_plan_geometry(psvi_plan& p) {
             p.mchunks = (M + mc - 1) / mc;
             p.mc = mc;
             p.net_lds = bytes;
-            p.net_threads = rup(mc, 16) >= 48 ? 512 : 256;
+            p.net_threads = g_net_threads ? g_net_threads : (rup(mc, 16) >= 48 ? 512 : 256);
             return bytes;
         }
         ++mchunks;
@@ -799,9 +850,11 @@ unsigned long long* g_net_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_NET_
 
 void net_set_lds_limit() {
     // gfx950: up to 160 KiB of LDS per workgroup
-    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_MEANFIELD>,
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_MEANFIELD, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV>,
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
@@ -864,9 +917,11 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, p.mchunks), block(p.net_threads);
     if (p.s_cnt[p.rank] == 0) return hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
-        hipLaunchKernelGGL(net_kernel<PSVI_FAMILY_MEANFIELD>, grid, block, p.net_lds, st, a);
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
+    else if (p.world > 1)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true>), grid, block, p.net_lds, st, a);
     else
-        hipLaunchKernelGGL(net_kernel<PSVI_FAMILY_FULLCOV>, grid, block, p.net_lds, st, a);
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false>), grid, block, p.net_lds, st, a);
     return hipGetLastError();
 }
 

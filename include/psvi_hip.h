@@ -427,6 +427,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     afterwards; A/B diagnostics)               */
 #define PSVI_DBG_LENET_GEMM_VALU 13 /* value: 1 = LeNet's head GEMMs on the fp32
                                     VALU kernel instead of the MFMA one (A/B)  */
+#define PSVI_DBG_NET_THREADS 14  /* value: threads per network workgroup (256 or
+                                    512; 0 = by chunk size) for plans created
+                                    afterwards (A/B diagnostics)               */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
