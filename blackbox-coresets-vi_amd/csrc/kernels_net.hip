@@ -20,14 +20,16 @@
 // whose buffers exceed the LDS, and for ranks with very few samples.)
 //
 // LDS holds everything a workgroup touches.  Every matrix is row-major with
-// a row stride of 4 x odd floats: the MFMA operand reads -- float4 along k for
-// k-contiguous operands, single floats down k for k-strided ones -- are then
-// free of bank conflicts in both orientations (every buffer is read both
-// ways: activations by the forward GEMM and by the dW GEMM, gradients by the
-// propagation GEMM and by the dW GEMM, weights by the forward and the
-// propagation GEMM).  Contractions run on v_mfma_f32_16x16x4_f32 tiles (exact
-// fp32) with double-buffered operand reads, tiles dealt round-robin to the
-// waves (wave w sits on SIMD w % 4).
+// a row stride == 8 (mod 16) floats, and every GEMM operand is read without
+// bank conflicts: a k-contiguous operand as one ds_read_b128 per lane (the
+// 16-lane groups of ds_read_b128 then cover 16 distinct 16-byte slots), a
+// k-strided one as ds_read_b32 with the k order of kbase/kstep (the two
+// lane-groups of a 32-lane half two rows apart).  The forward GEMM reads X_l
+// and W_l along k; the propagation GEMM reads G_l along k and a transposed
+// copy W_l^T (written with W_l); the weight-gradient GEMM reads G_l and X_l
+// down k.  Contractions run on v_mfma_f32_16x16x4_f32 tiles (exact fp32)
+// with double-buffered operand reads, tiles dealt round-robin to the waves
+// (wave w sits on SIMD w % 4).
 // Padding contract: W rows / columns past dout / din are zero; activation and
 // gradient rows past the chunk's pseudopoints are zero and their columns up
 // to the next multiple of 16 (within the row stride) too (epilogues write
@@ -54,6 +56,7 @@ struct NetArgs {
     // LDS carve (float offsets) and row strides: W_l, b_l, X_l (input of layer l:
     // X_0 = u chunk, X_l = relu(a_{l-1})), two gradient buffers, dlogits
     int lw[kMaxL], ldw[kMaxL], lb[kMaxL], lx[kMaxL], ldx[kMaxL];
+    int lwt[kMaxL], ldwt[kMaxL];  // W_l^T (l >= 1: the propagation GEMM's k-contiguous operand)
     int lg[2], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // ldl: dlogits [Mp][lddl]; lzw: z, w
     int nslack, nslack_early, slack[4 * kMaxL + 8];  // float offsets of the 64-float zero slacks
     int lstage, stage_len, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, staged by source
@@ -105,14 +108,28 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // k = kb + 4 k4 + j (the same k permutation on both operands), and holds
 // D[p0 + 4 k4 + r][q0 + 16c + i16], r = 0..3 (v_mfma_f32_16x16x4_f32 layout):
 // the epilogue gets (first row, column, the four rows' values).
+// k order of a 16-wide k-group.  Lane-group k4 feeds MFMA j of the group
+// with k = kperm(k4, j).  A k-contiguous operand reads one float4 per lane,
+// so k = 4 k4 + j.  When both operands are k-strided the order is free, and
+// k = (j & 1) + 4 (j >> 1) + 2 (k4 & 1) + 8 (k4 >> 1) puts the two
+// lane-groups of a 32-lane half two rows apart: with row strides == 8 (mod 16)
+// floats that is 16 banks, so their ds_read_b32 are conflict-free (4 k4 rows
+// apart would be 0 banks mod 32: 2-way).
+template <bool PERM>
+__device__ __forceinline__ int kbase(int k4) { return PERM ? 2 * (k4 & 1) + 8 * (k4 >> 1) : 4 * k4; }
+template <bool PERM>
+__device__ __forceinline__ int kstep(int j) { return PERM ? (j & 1) + 4 * (j >> 1) : j; }
+
 template <bool ACONT, bool BCONT, int NQ>
 struct TileOps {
+    static constexpr bool PERM = !ACONT && !BCONT;
     float4 a;
     float4 b[NQ];
-    // k-contiguous: one float4 at p; k-strided: p[0], p[ld], p[2 ld], p[3 ld]
+    // k-contiguous: one float4 at p; k-strided: the rows kstep(0..3) below p
     __device__ __forceinline__ static float4 ld(const float* p, int ldx, bool cont) {
         if (cont) return *reinterpret_cast<const float4*>(p);
-        return make_float4(p[0], p[ldx], p[2 * ldx], p[3 * ldx]);
+        return make_float4(p[kstep<PERM>(0) * ldx], p[kstep<PERM>(1) * ldx], p[kstep<PERM>(2) * ldx],
+                           p[kstep<PERM>(3) * ldx]);
     }
     // pa / pb: this lane's first operand element of the k-group; column tile c
     // of B sits 16 c rows (BCONT) or 16 c columns further
@@ -155,12 +172,14 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
     const int nk = K16 >> 4;
     if (u0 >= nu) return;  // wave-uniform
     const int da = ACONT ? 16 : 16 * lda, db = BCONT ? 16 : 16 * ldb;  // one k-group
+    const int rot = (k4 & 1) << 1;  // epilogue row rotation: v[r] is row 4 k4 + ((r + rot) & 3)
     auto ptrs = [&](int u, const float*& pa, const float*& pb, int& p0, int& q0) {
         const int pt = u / tqu, qt = (u - pt * tqu) * NQ;
         p0 = pt << 4;
         q0 = qt << 4;
-        pa = ACONT ? A + (p0 + i16) * lda + 4 * k4 : A + 4 * k4 * lda + p0 + i16;
-        pb = BCONT ? B + (q0 + i16) * ldb + 4 * k4 : B + 4 * k4 * ldb + q0 + i16;
+        constexpr bool PERM = !ACONT && !BCONT;
+        pa = ACONT ? A + (p0 + i16) * lda + 4 * k4 : A + kbase<PERM>(k4) * lda + p0 + i16;
+        pb = BCONT ? B + (q0 + i16) * ldb + 4 * k4 : B + kbase<PERM>(k4) * ldb + q0 + i16;
     };
     const float *pa, *pb;
     int p0, q0;
@@ -199,8 +218,14 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
             ptrs(u + nwv, pa, pb, p0, q0);
             x0.load(pa, lda, pb, ldb);
         }
+        // odd lane-groups hand over their four rows rotated by two: the
+        // epilogue's row-wise LDS accesses of the two groups of a 32-lane half
+        // are then 2 or 6 rows apart (16 banks at strides == 8 mod 16), not 4
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) epi(pe + 4 * k4, qe + 16 * c + i16, acc[c]);
+        for (int c = 0; c < NQ; ++c) {
+            const floatx4 v = acc[c];
+            epi(pe + 4 * k4, qe + 16 * c + i16, rot ? floatx4{v[2], v[3], v[0], v[1]} : v, rot);
+        }
     }
 }
 template <bool ACONT, bool BCONT, class Epi>
@@ -282,6 +307,9 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
 
     // layers whose weight gradients this workgroup produces: [own_lo, own_hi)
     const int own_lo = (a.nroles == 1 || role == 0) ? 0 : 1;
+    // W_l^T (the propagation GEMM's k-contiguous operand) is written with W_l
+    // for the layers this workgroup propagates through: l > own_lo
+    const int wt_lo = a.outer == 1 ? L : max(1, own_lo + 1);
     const int own_hi = (a.nroles == 1 || role == 1) ? L : 1;
 
     // ---- 1. loads --------------------------------------------------------
@@ -373,6 +401,11 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 for (int l = 0; l < L; ++l) {
                     const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
                     const int rows = (dout + 15) & ~15;
+                    if (l > 0) {  // W^T columns dout .. the 16-multiple (K padding of the propagation)
+                        float* WT = sm + a.lwt[l];
+                        for (int i = r16; i < din; i += nr16)
+                            if (dout + c16 < rows) WT[i * a.ldwt[l] + dout + c16] = 0.f;
+                    }
                     float* W = sm + a.lw[l];
                     for (int j = r16; j < dout; j += nr16)
                         for (int c = din + c16; c < ldw; c += 16) W[j * ldw + c] = 0.f;
@@ -417,10 +450,12 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         for (int p = 0; p < nsrc && !(a.abl & 1); ++p) {
             for (int l = 0; l < L; ++l) {
                 const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
-                const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l];
+                const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l], ldwt = a.ldwt[l];
+                const bool wt = l >= wt_lo;
                 const float rdin = 1.f / (float)din;
                 const float* sl = stage + a.stage_off[p] + a.src_col[p][l] - lo;
                 float* W = sm + a.lw[l];
+                float* WT = sm + a.lwt[l];
                 float* Bv = sm + a.lb[l];
                 for (int base = lo + tid; base < hi; base += kB * (int)blockDim.x) {
                     float v[kB];
@@ -433,6 +468,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                             // exact for r < 2^21: (r + 0.5) / din is >= 0.5/din from an integer
                             const int j = (int)(((float)r + 0.5f) * rdin), i = r - j * din;
                             W[j * ldw + i] = v[k];
+                            if (wt) WT[i * ldwt + j] = v[k];
                         } else if (r < hi) {
                             Bv[r - nw] = v[k];
                         }
@@ -446,8 +482,10 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         for (int l = 0; l < L; ++l) {
             const int din = a.din[l], dout = a.dout[l], nw = din * dout, n = nw + dout;
             float* W = sm + a.lw[l];
+            float* WT = sm + a.lwt[l];
             float* Bv = sm + a.lb[l];
-            const int ldw = a.ldw[l];
+            const int ldw = a.ldw[l], ldwt = a.ldwt[l];
+            const bool wt = l >= wt_lo;
             const float* mu = a.params + a.poff[l];
             const float* rho = mu + n;
             const float* eW = a.eps + a.eoff[l] + (int64_t)sg * nw;
@@ -471,6 +509,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                         // exact for idx < 2^21: (idx + 0.5) / din is >= 0.5/din from an integer
                         const int j = (int)(((float)idx + 0.5f) * rdin), i = idx - j * din;
                         W[j * ldw + i] = val;
+                        if (wt) WT[i * ldwt + j] = val;
                     } else {
                         Bv[idx - nw] = val;
                     }
@@ -508,12 +547,12 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         const float* Bv = sm + a.lb[l];
         const int ldn = head ? a.lddl : a.ldx[l + 1], jend = min((dout + 15) & ~15, ldn);
         if (head && fuse_head) {
-            auto epi = [&](int m, int j, floatx4 v) {  // j = i16: every lane of the row takes part
+            auto epi = [&](int m, int j, floatx4 v, int rot) {  // j = i16: every lane of the row takes part
                 const bool jl = j < C;
                 const float b = Bv[min(j, C - 1)];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = m + r;
+                    const int row = m + ((r + rot) & 3);
                     const float y = v[r] + b;
                     const float mx = row16_max(jl ? y : -INFINITY);
                     const float lse = mx + logf(row16_sum(jl ? expf(y - mx) : 0.f));
@@ -531,14 +570,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             if (l < 3) NET_STAMP(9 + l, __builtin_amdgcn_s_memtime());
             continue;
         }
-        auto epi = [&](int m, int j, floatx4 v) {
+        auto epi = [&](int m, int j, floatx4 v, int rot) {
             if (j < jend) {
                 const bool jl = j < dout;
                 const float b = Bv[min(j, dout - 1)];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float y = v[r] + b;
-                    Xn[(m + r) * ldn + j] = (jl && m + r < mcnt) ? (head ? y : fmaxf(y, 0.f)) : 0.f;
+                    const int row = m + ((r + rot) & 3);
+                    Xn[row * ldn + j] = (jl && row < mcnt) ? (head ? y : fmaxf(y, 0.f)) : 0.f;
                 }
             }
         };
@@ -659,15 +699,17 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             // dW_l[j][i] = sum_m G_l[m][j] X_l[m][i]: both operands k(=m)-strided
             const float* Wl = sm + a.lw[l];
             const int ldw = a.ldw[l];
-            auto epi = [&](int j, int i, floatx4 v) {
+            auto epi = [&](int j0, int i, floatx4 v, int rot) {
                 if (i < din) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (j + r < dout) {
+                    for (int r = 0; r < 4; ++r) {
+                        const int j = j0 + ((r + rot) & 3);
+                        if (j < dout) {
                             float g = v[r];
-                            if (a.outer == 2) g -= ckv * Wl[(j + r) * ldw + i];
-                            emit(l, (j + r) * din + i, g);
+                            if (a.outer == 2) g -= ckv * Wl[j * ldw + i];
+                            emit(l, j * din + i, g);
                         }
+                    }
                 }
             };
             mfma_gemm<false, false>(dout, din, Mp, 0, G, ldg, X, ldx, epi);
@@ -675,12 +717,12 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         }
         if (dx0) {
             // du[s][m][i] = sum_j G_0[m][j] W_0[j][i] for the chunk's pseudopoint rows
-            auto epi = [&](int m, int i, floatx4 v) {
+            auto epi = [&](int m0r, int i, floatx4 v, int rot) {
                 if (i < din) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int mg = m0 + m + r;
-                        if (m + r < mcnt && mg < a.n_pseudo)
+                        const int m = m0r + ((r + rot) & 3), mg = m0 + m;
+                        if (m < mcnt && mg < a.n_pseudo)
                             a.du_part[((size_t)s * a.n_pseudo + mg) * din + i] = v[r];
                     }
                 }
@@ -690,27 +732,45 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         if (prop) {
             // G_{l-1}[m][i] = (sum_j G_l[m][j] W_l[j][i]) * 1[X_l[m][i] > 0]
             const int iend = min((din + 15) & ~15, ldx);
-            auto epi = [&](int m, int i, floatx4 v) {
+            auto epi = [&](int m, int i, floatx4 v, int rot) {
                 if (i < iend) {
                     const bool il = i < din;
                     float h[4];  // the ReLU masks, read before any store (Gn may alias X)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) h[r] = X[(m + r) * ldx + i];
+                    for (int r = 0; r < 4; ++r) h[r] = X[(m + ((r + rot) & 3)) * ldx + i];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) Gn[(m + r) * ldx + i] = (il && h[r] > 0.f) ? v[r] : 0.f;
+                    for (int r = 0; r < 4; ++r)
+                        Gn[(m + ((r + rot) & 3)) * ldx + i] = (il && h[r] > 0.f) ? v[r] : 0.f;
                 }
             };
-            mfma_gemm<true, false>(Mp, din, dout, first, G, ldg, sm + a.lw[l], a.ldw[l], epi);
+            mfma_gemm<true, true>(Mp, din, dout, first, G, ldg, sm + a.lwt[l], a.ldwt[l], epi);
         }
         if (own) {
-            // bias gradient: column sums of G_l over the chunk, 16 lanes a column
-            for (int base = 0; base < dout; base += nr16) {  // uniform: DPP rows converge
-                const int j = min(base + r16, dout - 1);
-                float acc = 0.f;
-                for (int m = c16; m < mcnt; m += 16) acc += G[m * ldg + j];
-                acc = row16_sum(acc);
-                if (a.outer == 2) acc -= ckv * sm[a.lb[l] + j];
-                if (c16 == 0 && base + r16 < dout) emit(l, dout * din + j, acc);
+            // bias gradient: column sums of G_l over the chunk.  Wave q takes
+            // columns 16 q .. 16 q + 15: lane (k4, i16) reads the float4 of
+            // columns 16 q + 4 k4 .. + 3 in rows i16, i16 + 16, ... (the GEMM's
+            // conflict-free ds_read_b128 pattern), then DPP row sums over i16.
+            const int lane = tid & 63, i16 = lane & 15, k4 = lane >> 4;
+            for (int q = wave_id(); 16 * q < dout; q += blockDim.x >> 6) {  // wave-uniform
+                const int j0 = 16 * q + 4 * k4;
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int m = i16; m < mcnt; m += 16) {
+                    const float4 g4 = *reinterpret_cast<const float4*>(G + m * ldg + j0);
+                    acc.x += g4.x; acc.y += g4.y; acc.z += g4.z; acc.w += g4.w;
+                }
+                const float sums[4] = {row16_sum(acc.x), row16_sum(acc.y), row16_sum(acc.z),
+                                       row16_sum(acc.w)};
+                if (i16 == 0) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = j0 + e;
+                        if (j < dout) {
+                            float b = sums[e];
+                            if (a.outer == 2) b -= ckv * sm[a.lb[l] + j];
+                            emit(l, dout * din + j, b);
+                        }
+                    }
+                }
             }
         }
         if (!prop) break;
@@ -742,7 +802,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
 }
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
-static inline int ld4o(int x) { return x + (12 - x % 8) % 8; }  // >= x, == 4 (mod 8)
+static inline int ld8o(int x) { return x + (24 - x % 16) % 16; }  // >= x, == 8 (mod 16)
 
 // LDS floats for a chunk of `mc` pseudopoints (layout and padding contract
 // in the header comment); fills the carve into `a` when given.  Row strides
@@ -764,11 +824,19 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     const int Mp = rup(mc, 16);
     for (int l = 0; l < p.L; ++l) {
         const int din = p.lay[l].din, dout = p.lay[l].dout;
-        const int ldw = ld4o(rup(din, 16));
+        const int ldw = ld8o(rup(din, 16));
         const int lw = take((size_t)rup(dout, 16) * ldw), lb = take(dout);
         if (a) { a->lw[l] = lw; a->ldw[l] = ldw; a->lb[l] = lb; }
+        if (l > 0) {  // W^T: rows i < din (16-multiple), columns j < dout (16-multiple)
+            const int ldwt = ld8o(rup(dout, 16));
+            const int lwt = take((size_t)rup(din, 16) * ldwt);
+            if (a) { a->lwt[l] = lwt; a->ldwt[l] = ldwt; }
+        } else if (a) {
+            a->lwt[0] = lw;  // unused (no propagation below layer 0)
+            a->ldwt[0] = ldw;
+        }
     }
-    const int ldx0 = ld4o(p.lay[0].din);
+    const int ldx0 = ld8o(p.lay[0].din);
     const int lx0 = take((size_t)Mp * ldx0);
     const int lred = take(16);
     const int lzw = take(2 * (size_t)Mp);
@@ -780,7 +848,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     const size_t lstage = off;
     int ldgmax = 4;
     for (int l = 1; l < p.L; ++l) {
-        const int ldx = ld4o(p.lay[l].din);
+        const int ldx = ld8o(p.lay[l].din);
         const int lx = take((size_t)Mp * ldx);
         ldgmax = std::max(ldgmax, ldx);
         if (a) { a->lx[l] = lx; a->ldx[l] = ldx; }
@@ -790,7 +858,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
         lg0 = take((size_t)Mp * ldgmax);
         lg1 = take((size_t)Mp * ldgmax);
     }
-    const int lddl = ld4o(p.lay[p.L - 1].dout);
+    const int lddl = ld8o(p.lay[p.L - 1].dout);
     const int ldl = take((size_t)Mp * lddl);
     if (p.family == PSVI_FAMILY_FULLCOV) {
         size_t st = 0;
