@@ -159,7 +159,7 @@ struct TileOps {
 // pointer steps, and the next unit's first group is read before this unit's
 // epilogue.
 __device__ __forceinline__ int gemm_nq(int tp, int tq) {
-    return (tq <= 3 && 2 * tp >= (int)(blockDim.x >> 6)) ? tq : 1;
+    return (tq <= 3 && tp >= 4) ? tq : 1;
 }
 __device__ __forceinline__ int gemm_units(int P, int Q) {
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int own_lo = (a.nroles == 1 || role == 0) ? 0 : 1;
     // W_l^T (the propagation GEMM's k-contiguous operand) is written with W_l
     // for the layers this workgroup propagates through: l > own_lo
-    const int wt_lo = a.outer == 1 ? L : max(1, own_lo + 1);
+    const int wt_lo = (a.outer == 1 || FAM != PSVI_FAMILY_FULLCOV) ? L : max(1, own_lo + 1);
     const int own_hi = (a.nroles == 1 || role == 1) ? L : 1;
 
     // ---- 1. loads --------------------------------------------------------
@@ -743,7 +743,10 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                         Gn[(m + ((r + rot) & 3)) * ldx + i] = (il && h[r] > 0.f) ? v[r] : 0.f;
                 }
             };
-            mfma_gemm<true, true>(Mp, din, dout, first, G, ldg, sm + a.lwt[l], a.ldwt[l], epi);
+            if constexpr (FAM == PSVI_FAMILY_FULLCOV)
+                mfma_gemm<true, true>(Mp, din, dout, first, G, ldg, sm + a.lwt[l], a.ldwt[l], epi);
+            else  // mean-field: K = dout is small (the classifier), W read down k
+                mfma_gemm<true, false>(Mp, din, dout, first, G, ldg, sm + a.lw[l], a.ldw[l], epi);
         }
         if (own) {
             // bias gradient: column sums of G_l over the chunk.  Wave q takes
@@ -758,18 +761,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     const float4 g4 = *reinterpret_cast<const float4*>(G + m * ldg + j0);
                     acc.x += g4.x; acc.y += g4.y; acc.z += g4.z; acc.w += g4.w;
                 }
-                const float sums[4] = {row16_sum(acc.x), row16_sum(acc.y), row16_sum(acc.z),
-                                       row16_sum(acc.w)};
-                if (i16 == 0) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int j = j0 + e;
-                        if (j < dout) {
-                            float b = sums[e];
-                            if (a.outer == 2) b -= ckv * sm[a.lb[l] + j];
-                            emit(l, dout * din + j, b);
-                        }
-                    }
+                const float s0 = row16_sum(acc.x), s1 = row16_sum(acc.y), s2 = row16_sum(acc.z),
+                            s3 = row16_sum(acc.w);
+                // lanes i16 = 0..3 of the row emit one column each (in parallel:
+                // the mean-field emit reads eps and adds atomically)
+                if (i16 < 4 && j0 + i16 < dout) {
+                    const int j = j0 + i16;
+                    float b = i16 == 0 ? s0 : i16 == 1 ? s1 : i16 == 2 ? s2 : s3;
+                    if (a.outer == 2) b -= ckv * sm[a.lb[l] + j];
+                    emit(l, dout * din + j, b);
                 }
             }
         }
