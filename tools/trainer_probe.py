@@ -5,6 +5,8 @@ backward, bench.py's trainer line) goes: wall ms per call, device ms per call
 only).
 
   python tools/trainer_probe.py [calls]
+  python tools/trainer_probe.py --trainers   (one nested_step and one hyper_step at
+                                              inner_it 100, K 30: for a rocprofv3 trace)
 """
 import os
 import sys
@@ -19,7 +21,9 @@ from bench import LAYERS, N_DATA, S_PER_GPU, synthetic_inputs  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    trainers = "--trainers" in sys.argv
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n = int(args[0]) if args else 20
     from psvi.inference import PSVILearnV
     from psvi.models import make_fc2net
 
@@ -36,6 +40,16 @@ def main():
     ps.device = dev
     ps.register_elbos = False
     ps.setup_optimizers()
+    if trainers:
+        for name, f in (("nested_step", lambda: ps.nested_step(xb, yb)),
+                        ("hyper_step", lambda: ps.hyper_step(xb, yb, K=30))):
+            f()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            print(f"{name} (inner_it 100): {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+        return
     fn = lambda: ps.psvi_elbo(xb, yb).backward()  # noqa: E731
     for _ in range(3):
         fn()
