@@ -227,10 +227,19 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
     float sum = mean[r] + dg * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
     const float* p = part + (size_t)rb.slot0 * a.S * kFwdRows + (size_t)s * kFwdRows + rr;
     const size_t st = (size_t)a.S * kFwdRows;
-    // 4 independent loads in flight per thread; summation order k = 0, 1, ... kept per
-    // partial so the result does not depend on the unroll
+    // The first 8 slots as unconditional loads at clamped indices (all in
+    // flight at once; a row block of C3's streaming update has 1-10 slots),
+    // any further ones 4 at a time.  Partial sums s4[k % 4] in slot order k =
+    // 0, 1, ..., so the result does not depend on the unroll.
     float s4[4] = {0.f, 0.f, 0.f, 0.f};
-    int k = 0;
+    {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = p[max(min(i, rb.nk - 1), 0) * st];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s4[i & 3] += i < rb.nk ? v[i] : 0.f;
+    }
+    int k = 8;
     for (; k + 4 <= rb.nk; k += 4) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) s4[i] += p[(k + i) * st];
