@@ -214,38 +214,60 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
 // x[s][xcol + rr] = mean[r] + softplus(sd[r]) eps[s][r] + sum over the row
 // block's slots (r = r0 + rr); one workgroup per (row block, 256/kFwdRows
 // samples), coalesced along the rows.
+// Two samples per thread (s and s + 4 of the block's 8): the row block's
+// descriptor, mean and softplus(sd) serve both, and twice the loads are in
+// flight.
+constexpr int kRedSpb = 2 * 256 / kFwdRows;  // samples per reduce block
 __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* rbs,
                                                              const float* part, FwdArgs a,
                                                              float* x) {
     const FwdRowBlock rb = rbs[blockIdx.x];
     const int rr = threadIdx.x & (kFwdRows - 1);
-    const int s = blockIdx.y * (256 / kFwdRows) + threadIdx.x / kFwdRows;
-    if (s >= a.S || rr >= rb.R) return;
+    const int s0 = blockIdx.y * kRedSpb + threadIdx.x / kFwdRows, s1 = s0 + kRedSpb / 2;
+    if (s0 >= a.S || rr >= rb.R) return;
+    const bool two = s1 < a.S;
     const int n = a.lay[rb.layer].n, r = rb.r0 + rr;
     const float* mean = a.params + a.lay[rb.layer].poff;
-    const float dg = a.raw_diag ? mean[n + r] : softplus_f(mean[n + r]);
-    float sum = mean[r] + dg * a.eps[a.lay[rb.layer].eoff + (int64_t)s * n + r];
-    const float* p = part + (size_t)rb.slot0 * a.S * kFwdRows + (size_t)s * kFwdRows + rr;
+    const float* eps = a.eps + a.lay[rb.layer].eoff + r;
+    const float e0 = eps[(int64_t)s0 * n], e1 = eps[(int64_t)(two ? s1 : s0) * n];
+    const float mu = mean[r], sdr = mean[n + r];
     const size_t st = (size_t)a.S * kFwdRows;
+    const float* p0 = part + (size_t)rb.slot0 * st + (size_t)s0 * kFwdRows + rr;
+    const float* p1 = part + (size_t)rb.slot0 * st + (size_t)(two ? s1 : s0) * kFwdRows + rr;
     // The first 8 slots as unconditional loads at clamped indices (all in
     // flight at once; a row block of C3's streaming update has 1-10 slots),
     // any further ones 4 at a time.  Partial sums s4[k % 4] in slot order k =
     // 0, 1, ..., so the result does not depend on the unroll.
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
     {
-        float v[8];
+        float va[8], vb[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = p[max(min(i, rb.nk - 1), 0) * st];
+        for (int i = 0; i < 8; ++i) {
+            const size_t o = (size_t)max(min(i, rb.nk - 1), 0) * st;
+            va[i] = p0[o];
+            vb[i] = p1[o];
+        }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s4[i & 3] += i < rb.nk ? v[i] : 0.f;
+        for (int i = 0; i < 8; ++i) {
+            a4[i & 3] += i < rb.nk ? va[i] : 0.f;
+            b4[i & 3] += i < rb.nk ? vb[i] : 0.f;
+        }
     }
     int k = 8;
     for (; k + 4 <= rb.nk; k += 4) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s4[i] += p[(k + i) * st];
+        for (int i = 0; i < 4; ++i) {
+            a4[i] += p0[(k + i) * st];
+            b4[i] += p1[(k + i) * st];
+        }
     }
-    for (int i = 0; k + i < rb.nk; ++i) s4[i] += p[(k + i) * st];
-    x[(int64_t)s * a.ldx + rb.xcol + rr] = sum + ((s4[0] + s4[1]) + (s4[2] + s4[3]));
+    for (int i = 0; k + i < rb.nk; ++i) {
+        a4[i] += p0[(k + i) * st];
+        b4[i] += p1[(k + i) * st];
+    }
+    const float dg = a.raw_diag ? sdr : softplus_f(sdr);
+    x[(int64_t)s0 * a.ldx + rb.xcol + rr] = (mu + dg * e0) + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
+    if (two) x[(int64_t)s1 * a.ldx + rb.xcol + rr] = (mu + dg * e1) + ((b4[0] + b4[1]) + (b4[2] + b4[3]));
 }
 
 int g_fwd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_FWD_ABLATION, mask)
@@ -1347,7 +1369,7 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     if (p.n_fwd == 0) return hipSuccess;
     // every x element is written by exactly one reduce thread: no memset
     hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd), dim3(256), 0, st, a);
-    constexpr int spb = 256 / kFwdRows;  // samples per reduce workgroup
+    constexpr int spb = kRedSpb;  // samples per reduce workgroup
     hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb), dim3(256), 0,
                        st, p.d_frb, p.d_fwd_part, a, x_shard);
     return hipGetLastError();
@@ -1446,7 +1468,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             f.ldx = p.rows_tot[p.rank];
             f.S = p.d.S;
             fill_layers(p, f.lay);
-            constexpr int spb = 256 / kFwdRows;
+            constexpr int spb = kRedSpb;
             hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_sfrb, (f.S + spb - 1) / spb),
                                dim3(256), 0, st, p.d_sfrb, p.d_str_part, f, x_next);
             return hipGetLastError();
@@ -1462,7 +1484,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             f.ldx = p.rows_tot[p.rank];
             f.S = p.d.S;
             fill_layers(p, f.lay);
-            constexpr int spb = 256 / kFwdRows;
+            constexpr int spb = kRedSpb;
             hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb),
                                dim3(256), 0, st, p.d_ufrb, p.d_upd_part, f, x_next);
         } else {
@@ -1489,7 +1511,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         f.ldx = p.rows_tot[p.rank];
         f.S = p.d.S;
         fill_layers(p, f.lay);
-        constexpr int spb = 256 / kFwdRows;
+        constexpr int spb = kRedSpb;
         hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb), dim3(256),
                            0, st, p.d_ufrb, p.d_upd_part, f, x_next);
         return hipGetLastError();
