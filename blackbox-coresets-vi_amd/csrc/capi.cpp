@@ -508,6 +508,12 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                 hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the streaming-update scratch");
         }
+        if (!rc && family == PSVI_FAMILY_MEANFIELD) {
+            const size_t bytes = sizeof(float) * (size_t)std::max(1, p->s_cnt[p->rank]) *
+                                 p->mchunks * p->n_tot;
+            if (hipMalloc((void**)&p->d_mf_slots, bytes) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the mean-field gradient slots");
+        }
         if (!rc && family == PSVI_FAMILY_LENET) {
             const size_t bytes = lenet_ws(*p, nullptr).bytes;
             if (hipMalloc(&p->d_lenet_ws, bytes) != hipSuccess)
@@ -535,6 +541,7 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_upd_part) (void)hipFree(p->d_upd_part);
     if (p->d_upd) (void)hipFree(p->d_upd);
     if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);
+    if (p->d_mf_slots) (void)hipFree(p->d_mf_slots);
     delete p;
     return 0;
 }
@@ -670,18 +677,18 @@ static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const
         HIP_TRY(launch_lenet(*p, u, z, w, params, eps, acc, elbo_out, p->d_lenet_ws, st));
         HIP_TRY(launch_mf_update(*p, acc, params, m, v, hp, elbo_out, grad_out, include_kl, st));
     } else if (p->family == PSVI_FAMILY_MEANFIELD) {
-        float* acc = (float*)wsb;
-        HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
-        HIP_TRY(launch_net(*p, u, z, w, params, eps, acc, acc + p->n_tot, nullptr, nullptr,
-                           elbo_out, st));
-        HIP_TRY(launch_mf_update(*p, acc, params, m, v, hp, elbo_out, grad_out, include_kl, st));
+        // per-(sample, chunk) gradient slots, summed in a fixed order by the update
+        HIP_TRY(launch_net(*p, u, z, w, params, eps, p->d_mf_slots, nullptr, nullptr, elbo_out,
+                           st));
+        HIP_TRY(launch_mf_update(*p, nullptr, params, m, v, hp, elbo_out, grad_out, include_kl,
+                                 st, eps));
     } else {
         const size_t xs = sizeof(float) * (size_t)p->d.S * p->rows_tot[0];
         float* x = (float*)wsb;
         float* g = (float*)(wsb + align256(xs));
         HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
         if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
-        HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x, g, elbo_out, st));
+        HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x, g, elbo_out, st));
         HIP_TRY(launch_mvn_update(*p, eps, g, params, m, v, hp, elbo_out, grad_out, include_kl,
                                   nullptr, nullptr, st));
     }
@@ -722,9 +729,8 @@ int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* 
         HIP_TRY(launch_lenet(*p, u, z, w, params, eps, acc, nll_out, p->d_lenet_ws, st));
         return 0;
     }
-    HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
-    HIP_TRY(launch_net(*p, u, z, w, params, eps, acc, acc + p->n_tot, nullptr, nullptr, nll_out,
-                       st));
+    HIP_TRY(launch_net(*p, u, z, w, params, eps, p->d_mf_slots, nullptr, nullptr, nll_out, st));
+    HIP_TRY(launch_mf_slot_acc(*p, eps, acc, st));
     return 0;
 }
 
@@ -760,8 +766,7 @@ int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, con
     if (p->mchunks > 1)
         HIP_TRY(hipMemsetAsync(g_send, 0,
                                sizeof(float) * (size_t)p->s_cnt[p->rank] * p->n_tot, st));
-    HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x_recv, g_send, nll_out,
-                       st));
+    HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x_recv, g_send, nll_out, st));
     return 0;
 }
 
@@ -862,6 +867,27 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
                                                                                          : nullptr;
     };
     psvi_adam_hp h = *hp;
+    if (p->family == PSVI_FAMILY_MEANFIELD) {
+        // two launches per step: the network kernel (which also draws the next
+        // step's eps in Philox mode) and the slot-reducing update; the ELBO
+        // accumulators are cleared once for the whole loop
+        if (T == 0) return 0;
+        const float* e = eps_t(0);
+        if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
+        HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double) * (size_t)T, st));
+        for (int t = 0; t < T; ++t) {
+            h.step = hp->step + t;
+            const bool draw = !eps && t + 1 < T;
+            float* en_buf = draw ? ebuf[(t + 1) & 1] : nullptr;
+            HIP_TRY(launch_net(*p, u, z, w, params, e, p->d_mf_slots, nullptr, nullptr,
+                               elbo_out + t, st, en_buf, draw ? p->Peps : 0, seed,
+                               offset + (uint64_t)(t + 1) * es));
+            HIP_TRY(launch_mf_update(*p, nullptr, params, adam_m, adam_v, &h, elbo_out + t,
+                                     nullptr, 1, st, e));
+            e = t + 1 < T ? (eps ? eps + (size_t)(t + 1) * p->Peps : en_buf) : nullptr;
+        }
+        return 0;
+    }
     if (p->family != PSVI_FAMILY_FULLCOV) {
         for (int t = 0; t < T; ++t) {
             const float* e = eps_t(t);
@@ -896,7 +922,7 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         float* en_buf = draw ? ebuf[(t + 1) & 1] : nullptr;
         const bool tm = g_loop_every > 0 && t % g_loop_every == 0;
         if (tm) HIP_TRY(loop_event(0, st));
-        HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, nullptr, x, g, elbo_out + t,
+        HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x, g, elbo_out + t,
                            st, en_buf, draw ? p->Peps : 0, seed, offset + (uint64_t)(t + 1) * es));
         if (tm) HIP_TRY(loop_event(0, st));
         const float* en = t + 1 < T ? (eps ? eps + (size_t)(t + 1) * p->Peps : en_buf) : nullptr;
@@ -951,8 +977,8 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
         HIP_TRY(launch_lenet(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr,
                              p->d_lenet_ws, st, &fw));
     else
-        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
-                           nullptr, st, nullptr, 0, 0, 0, &fw));
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, x, nullptr, nullptr,
+                           st, nullptr, 0, 0, 0, &fw));
     if (!ext_coef) {
         // 2. per-sample terms, softmax over samples, loss, backward coefficients
         HIP_TRY(launch_outer_combine(*p, n_pseudo, params, w_all, o.nll, o.stats, loss_out,
@@ -973,8 +999,8 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
     if (p->family == PSVI_FAMILY_FULLCOV) {
         if (p->mchunks > 1)
             HIP_TRY(hipMemsetAsync(g, 0, sizeof(float) * (size_t)p->d.S * p->n_tot, st));
-        HIP_TRY(launch_net(*p, x_all, z_all, w_all, nullptr, nullptr, nullptr, nullptr, x, g,
-                           nullptr, st, nullptr, 0, 0, 0, &bw));
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, nullptr, nullptr, nullptr, x, g, nullptr, st,
+                           nullptr, 0, 0, 0, &bw));
         // 4. reparameterised backward (no KL term: the sampled KL came in through G)
         HIP_TRY(launch_mvn_update(*p, eps, g, const_cast<float*>(params), nullptr, nullptr,
                                   nullptr, nullptr, grad_params, 0, nullptr, nullptr, st));
@@ -984,11 +1010,10 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
         HIP_TRY(launch_mf_update(*p, acc, const_cast<float*>(params), nullptr, nullptr, nullptr,
                                  nullptr, grad_params, 0, st));
     } else {
-        HIP_TRY(hipMemsetAsync(acc, 0, sizeof(float) * p->acc_count, st));
-        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, acc, acc + p->n_tot, nullptr,
-                           nullptr, nullptr, st, nullptr, 0, 0, 0, &bw));
-        HIP_TRY(launch_mf_update(*p, acc, const_cast<float*>(params), nullptr, nullptr, nullptr,
-                                 nullptr, grad_params, 0, st));
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, p->d_mf_slots, nullptr, nullptr,
+                           nullptr, st, nullptr, 0, 0, 0, &bw));
+        HIP_TRY(launch_mf_update(*p, nullptr, const_cast<float*>(params), nullptr, nullptr,
+                                 nullptr, nullptr, grad_params, 0, st, eps));
     }
     // 5. explicit log-det term on the scales; d loss / d u
     HIP_TRY(launch_outer_finish(*p, n_pseudo, params, o.sck, grad_params, o.du, grad_u, st));
@@ -1056,8 +1081,8 @@ int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, cons
         HIP_TRY(launch_lenet(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr,
                              p->d_lenet_ws, st, &fw));
     else
-        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, nullptr, x, nullptr,
-                           nullptr, st, nullptr, 0, 0, 0, &fw));
+        HIP_TRY(launch_net(*p, x_all, z_all, w_all, params, eps, nullptr, x, nullptr, nullptr,
+                           st, nullptr, 0, 0, 0, &fw));
     HIP_TRY(launch_eval(*p, n_pseudo, params, w_all, z_all, o.nll, o.stats, prob,
                         correction ? 1 : 0, W, probs_out, stats_out, st));
     return 0;

@@ -47,7 +47,41 @@ struct MfUpdArgs {
     unsigned kl_mask;  // layers carrying a KL term (LeNet: the VILinear layers only)
     float inv_s0sq, log_s0;
     AdamC adam;
+    // SLOTS: acc from the plan's gradient slots [S_loc][nz][n_tot] and the
+    // step's eps (layer l: weights [S_total][nw], then biases [S_total][dout])
+    const float* slots;
+    const float* seps;
+    int S_loc, nz, s_goff, S_total;
+    int64_t eoff[kMaxL];
+    int nw[kMaxL], dout[kMaxL];
 };
+
+// Fixed-order slot sums for parameter e (layer l, element idx) over the samples
+// s = s0, s0 + sstep, ...: g = sum_s sum_c slot[s][c][e], ge = sum_s (sum_c
+// slot[s][c][e]) eps_s[idx] -- the net kernel's per-(sample, chunk) gradients
+// (VIMixin sampling, neural_net.py:155-162: d mu = sum_s dW_s, d rho via
+// sum_s dW_s eps_s).
+__device__ __forceinline__ void mf_slot_sums(const MfUpdArgs& a, int l, int idx, int e, int s0,
+                                             int sstep, float& g, float& ge) {
+    const int nw = a.nw[l];
+    const bool wt = idx < nw;
+    const float* ep = a.seps + a.eoff[l] + (wt ? idx : (int64_t)a.S_total * nw + (idx - nw));
+    const int64_t es = wt ? nw : a.dout[l];
+    const size_t ss = (size_t)a.nz * a.n_tot;
+    g = 0.f;
+    ge = 0.f;
+#pragma unroll 2
+    for (int s = s0; s < a.S_loc; s += sstep) {
+        const float* q = a.slots + (size_t)s * ss + e;
+        const float ev = ep[(int64_t)(a.s_goff + s) * es];
+        float gs = 0.f;
+        for (int c = 0; c < a.nz; ++c) gs += q[(size_t)c * a.n_tot];
+        g += gs;
+        ge += gs * ev;
+    }
+}
+
+constexpr int kSlotGroups = 16;  // SLOTS: 16 parameters x 16 sample groups per block
 
 template <bool GRAD>
 __device__ __forceinline__ void mf_upd(const MfUpdArgs& a, int64_t pidx, float g) {
@@ -61,21 +95,46 @@ __device__ __forceinline__ void mf_upd(const MfUpdArgs& a, int64_t pidx, float g
     }
 }
 
-template <bool GRAD>
+// SLOTS: thread (group q, parameter lane) sums samples s = q (mod 16); the
+// group partials meet in LDS and group 0 adds them in order q = 0..15.
+template <bool GRAD, bool SLOTS>
 __global__ __launch_bounds__(256) void mf_update_kernel(MfUpdArgs a) {
     __shared__ float red[8];
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ float sred[SLOTS ? 2 * 256 : 1];
+    const int e = SLOTS ? blockIdx.x * kSlotGroups + (threadIdx.x & (kSlotGroups - 1))
+                        : blockIdx.x * blockDim.x + threadIdx.x;
+    const int grp = SLOTS ? threadIdx.x / kSlotGroups : 0;
+    int l = 0;
+    while (l + 1 < a.L && e >= a.woff[l + 1]) ++l;
+    const int idx = e - a.woff[l];
+    float sg_acc = 0.f, sge_acc = 0.f;
+    if (SLOTS) {
+        if (e < a.n_tot) mf_slot_sums(a, l, idx, e, grp, kSlotGroups, sg_acc, sge_acc);
+        sred[threadIdx.x] = sg_acc;
+        sred[256 + threadIdx.x] = sge_acc;
+        __syncthreads();
+        if (grp == 0) {
+            sg_acc = 0.f;
+            sge_acc = 0.f;
+            for (int q = 0; q < kSlotGroups; ++q) {
+                sg_acc += sred[q * kSlotGroups + threadIdx.x];
+                sge_acc += sred[256 + q * kSlotGroups + threadIdx.x];
+            }
+        }
+    }
     float klp = 0.f;
-    if (e < a.n_tot) {
-        int l = 0;
-        while (l + 1 < a.L && e >= a.woff[l + 1]) ++l;
-        const int idx = e - a.woff[l];
+    if (e < a.n_tot && grp == 0) {
         const int64_t pmu = a.poff[l] + idx, prho = pmu + a.n[l];
         const float mu = a.params[pmu], rho = a.params[prho];
         const float sp = softplus_f(rho), sg = sigmoid_f(rho);
-        const float* accMu = a.acc;
-        const float* accRho = accMu + a.n_tot;
-        float gmu = accMu[e], grho = accRho[e] * sg;
+        float gmu, grho;
+        if (SLOTS) {
+            gmu = sg_acc;
+            grho = sge_acc * sg;
+        } else {
+            gmu = a.acc[e];
+            grho = a.acc[a.n_tot + e] * sg;
+        }
         if (a.include_kl && ((a.kl_mask >> l) & 1u)) {
             gmu += mu * a.inv_s0sq;
             grho += (sp * a.inv_s0sq - 1.f / sp) * sg;
@@ -132,16 +191,68 @@ hipError_t launch_adam_adjoint(int64_t n, const float* lt, float* lm, float* lv,
     return hipGetLastError();
 }
 
-hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params, float* m,
-                            float* v, const psvi_adam_hp* hp, double* kl_out,
-                            float* grad_out, int include_kl, hipStream_t st) {
-    MfUpdArgs a{};
+static void mf_slot_args(const psvi_plan& p, const float* eps, MfUpdArgs& a) {
     a.L = p.L;
     for (int l = 0; l < p.L; ++l) {
         a.woff[l] = p.lay[l].woff;
         a.poff[l] = p.lay[l].poff;
         a.n[l] = p.lay[l].n;
+        a.eoff[l] = p.lay[l].eoff;
+        a.nw[l] = p.lay[l].din * p.lay[l].dout;
+        a.dout[l] = p.lay[l].dout;
     }
+    a.woff[p.L] = p.n_tot;
+    a.n_tot = p.n_tot;
+    a.slots = p.d_mf_slots;
+    a.seps = eps;
+    a.S_loc = p.s_cnt[p.rank];
+    a.nz = p.mchunks;
+    a.s_goff = p.s_off[p.rank];
+    a.S_total = p.d.S;
+}
+
+// acc = [sum_s dW_s | sum_s dW_s eps_s] from the slots (psvi_mf_phase_accumulate:
+// the all-reduced accumulator of the sample-sharded mean-field step)
+__global__ __launch_bounds__(256) void mf_slot_acc_kernel(MfUpdArgs a, float* acc) {
+    __shared__ float sred[2 * 256];
+    const int e = blockIdx.x * kSlotGroups + (threadIdx.x & (kSlotGroups - 1));
+    const int grp = threadIdx.x / kSlotGroups;
+    int l = 0;
+    while (l + 1 < a.L && e >= a.woff[l + 1]) ++l;
+    float g = 0.f, ge = 0.f;
+    if (e < a.n_tot) mf_slot_sums(a, l, e - a.woff[l], e, grp, kSlotGroups, g, ge);
+    sred[threadIdx.x] = g;
+    sred[256 + threadIdx.x] = ge;
+    __syncthreads();
+    if (grp == 0 && e < a.n_tot) {
+        g = 0.f;
+        ge = 0.f;
+        for (int q = 0; q < kSlotGroups; ++q) {
+            g += sred[q * kSlotGroups + threadIdx.x];
+            ge += sred[256 + q * kSlotGroups + threadIdx.x];
+        }
+        acc[e] = g;
+        acc[a.n_tot + e] = ge;
+    }
+}
+
+hipError_t launch_mf_slot_acc(const psvi_plan& p, const float* eps, float* acc, hipStream_t st) {
+    if (!p.d_mf_slots) return hipErrorInvalidValue;
+    MfUpdArgs a{};
+    mf_slot_args(p, eps, a);
+    hipLaunchKernelGGL(mf_slot_acc_kernel, dim3((p.n_tot + kSlotGroups - 1) / kSlotGroups),
+                       dim3(256), 0, st, a, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params, float* m,
+                            float* v, const psvi_adam_hp* hp, double* kl_out,
+                            float* grad_out, int include_kl, hipStream_t st,
+                            const float* slot_eps) {
+    const bool slots = acc == nullptr;
+    if (slots && (!p.d_mf_slots || !slot_eps)) return hipErrorInvalidValue;
+    MfUpdArgs a{};
+    mf_slot_args(p, slot_eps, a);
     a.woff[p.L] = p.n_tot;
     a.acc = acc;
     a.n_tot = p.n_tot;
@@ -156,11 +267,15 @@ hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
     a.inv_s0sq = 1.f / (s0 * s0);
     a.log_s0 = logf(s0);
     if (hp) a.adam = make_adam(hp);
-    const int nb = (p.n_tot + 255) / 256;
-    if (grad_out)
-        hipLaunchKernelGGL(mf_update_kernel<true>, dim3(nb), dim3(256), 0, st, a);
+    const int nb = slots ? (p.n_tot + kSlotGroups - 1) / kSlotGroups : (p.n_tot + 255) / 256;
+    if (grad_out && slots)
+        hipLaunchKernelGGL((mf_update_kernel<true, true>), dim3(nb), dim3(256), 0, st, a);
+    else if (grad_out)
+        hipLaunchKernelGGL((mf_update_kernel<true, false>), dim3(nb), dim3(256), 0, st, a);
+    else if (slots)
+        hipLaunchKernelGGL((mf_update_kernel<false, true>), dim3(nb), dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL(mf_update_kernel<false>, dim3(nb), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((mf_update_kernel<false, false>), dim3(nb), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -15,9 +15,12 @@
 // forward pass and the loss head; role 0 then produces layer 0's weight
 // gradient (and the gradient chain down to it), role 1 every other layer's.
 // Each gradient element has exactly one writer -- plain stores into g_send,
-// no zeroing pass, no atomics, deterministic.  (Pseudopoint chunks, whose
-// partial dW are added with atomics onto a zeroed g_send, remain for shapes
-// whose buffers exceed the LDS, and for ranks with very few samples.)
+// no zeroing pass, no atomics, deterministic.  (Full-cov pseudopoint chunks,
+// whose partial dW are added with atomics onto a zeroed g_send, remain for
+// shapes whose buffers exceed the LDS, and for ranks with very few samples.)
+// Mean-field: every (sample, chunk) stores its gradient into its own slot of
+// the plan's d_mf_slots; mf_update_kernel sums the slots in a fixed order
+// (against eps for the rho accumulator), so the step is bitwise reproducible.
 //
 // LDS holds everything a workgroup touches.  Every matrix is row-major with
 // a row stride == 8 (mod 16) floats, and every GEMM operand is read without
@@ -68,8 +71,10 @@ struct NetArgs {
     const float* params;
     const float* eps;
     int64_t poff[kMaxL], eoff[kMaxL];
-    float* accMu;
-    float* accRho;
+    // per-(sample, pseudopoint chunk) gradient slots [S_loc][gridDim.z][slot_ld]
+    // (the plan's d_mf_slots): one plain store per element, summed by the update
+    float* mf_slots;
+    int slot_ld;
     // fused next-step draw (psvi_inner_loop): normals [0, rn_n) of the Philox
     // stream (rn_seed, rn_off) into rn_out, split over the grid's workgroups
     float* rn_out;
@@ -667,12 +672,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     auto emit = [&](int l, int o, float v) {
         if (a.abl & 16) { sink += v; return; }
         if constexpr (FAM == PSVI_FAMILY_MEANFIELD) {
-            const int din = a.din[l], dout = a.dout[l], nw = din * dout;
-            const float e = o < nw ? a.eps[a.eoff[l] + (int64_t)sg * nw + o]
-                                   : a.eps[a.eoff[l] + (int64_t)a.S_total * nw +
-                                           (int64_t)sg * dout + o - nw];
-            atomicAdd(a.accMu + a.woff[l] + o, v);
-            atomicAdd(a.accRho + a.woff[l] + o, v * e);
+            a.mf_slots[((size_t)s * gridDim.z + blockIdx.z) * a.slot_ld + a.woff[l] + o] = v;
         } else {
             float* dst = a.gsend + fc_addr(a, nsrc, srct, l, o, s);
             if (a.atomic_g) atomicAdd(dst, v); else *dst = v;
@@ -763,8 +763,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 }
                 const float s0 = row16_sum(acc.x), s1 = row16_sum(acc.y), s2 = row16_sum(acc.z),
                             s3 = row16_sum(acc.w);
-                // lanes i16 = 0..3 of the row emit one column each (in parallel:
-                // the mean-field emit reads eps and adds atomically)
+                // lanes i16 = 0..3 of the row emit one column each, in parallel
                 if (i16 < 4 && j0 + i16 < dout) {
                     const int j = j0 + i16;
                     float b = i16 == 0 ? s0 : i16 == 1 ? s1 : i16 == 2 ? s2 : s3;
@@ -927,7 +926,7 @@ void net_set_lds_limit() {
 }
 
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
-                      const float* params, const float* eps, float* accMu, float* accRho,
+                      const float* params, const float* eps, float* mf_slots,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out, int64_t rn_n, uint64_t rn_seed, uint64_t rn_off,
                       const NetOuter* outer) {
@@ -964,7 +963,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     }
     net_lds_floats(p, p.mc, &a);
     a.u = u; a.z = z; a.w = w; a.nll_out = nll_out;
-    a.params = params; a.eps = eps; a.accMu = accMu; a.accRho = accRho;
+    a.params = params; a.eps = eps; a.mf_slots = mf_slots; a.slot_ld = p.n_tot;
     a.xrecv = xrecv; a.gsend = gsend;
     if (p.family == PSVI_FAMILY_FULLCOV) {
         const int S_local = p.s_cnt[p.rank];

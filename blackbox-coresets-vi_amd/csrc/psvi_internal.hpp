@@ -278,6 +278,10 @@ struct psvi_plan {
     int64_t acc_count = 0;
     // LeNet: plan-owned activation / gradient scratch (kernels_lenet.hip)
     void* d_lenet_ws = nullptr;
+    // mean-field: plan-owned per-(sample, pseudopoint chunk) gradient slots
+    // [s_cnt[rank]][mchunks][n_tot]; one writer per element, summed in a fixed
+    // order by the update (run-to-run bitwise reproducible, no float atomics)
+    float* d_mf_slots = nullptr;
 };
 
 namespace psvi {
@@ -292,13 +296,18 @@ inline unsigned plan_nkl_mask(const psvi_plan& p) {
 }
 // launchers (defined in the .hip translation units)
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
-                      const float* params, const float* eps, float* accMu, float* accRho,
+                      const float* params, const float* eps, float* mf_slots,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out = nullptr, int64_t rn_n = 0, uint64_t rn_seed = 0,
                       uint64_t rn_off = 0, const NetOuter* outer = nullptr);
+// acc == nullptr: the accumulators come from the plan's mean-field gradient
+// slots, reduced in a fixed order against slot_eps (the step's eps)
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
                             float* m, float* v, const psvi_adam_hp* hp, double* kl_out,
-                            float* grad_out, int include_kl, hipStream_t st);
+                            float* grad_out, int include_kl, hipStream_t st,
+                            const float* slot_eps = nullptr);
+// acc = [sum_s dW_s | sum_s dW_s eps_s] from the plan's mean-field gradient slots
+hipError_t launch_mf_slot_acc(const psvi_plan& p, const float* eps, float* acc, hipStream_t st);
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
                           float* x_shard, hipStream_t st, bool raw_diag = false);
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,

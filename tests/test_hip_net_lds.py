@@ -4,7 +4,8 @@ epilogues) or multiplies a zero weight.  Checked by running the kernel after
 another kernel left NaN / 1e30 in the LDS of every CU (a large torch GEMM on
 NaN-filled operands stages its tiles there): the outputs must equal, bit for
 bit, those of a run after a zero-filled GEMM.  Also the run-to-run
-determinism of the full-cov gradient (plain stores, one writer per element)."""
+determinism of the gradients (plain stores, one writer per element; the
+mean-field slots are summed in a fixed order)."""
 import numpy as np
 import pytest
 import torch
@@ -68,5 +69,5 @@ def test_meanfield_net_ignores_stale_lds(layers, S, M):
         torch.cuda.synchronize()
         outs.append(acc.cpu().numpy())
     assert np.isfinite(outs[0]).all()
-    for a in outs[1:]:  # float atomics: order-dependent in the last bits
-        assert np.allclose(a, outs[0], rtol=1e-5, atol=1e-6 * np.abs(outs[0]).max())
+    for a in outs[1:]:  # per-(sample, chunk) slots summed in a fixed order: bitwise
+        assert np.array_equal(a, outs[0])

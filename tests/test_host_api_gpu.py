@@ -57,8 +57,9 @@ def test_inner_loop_philox_is_deterministic_and_advances():
     assert not torch.equal(e1, e2)  # fresh noise, moved parameters
     f, model = fixture_model("g2r_fn_c2_rand_av")
     b = make_psvi(f, model.cuda(), "cuda")
-    # same Philox stream; mean-field sums use fp32 atomics (order-nondeterministic last bits)
-    assert torch.allclose(b.inner_loop(T=2).cpu(), e1, rtol=1e-7, atol=0)
+    # same Philox stream; the gradient sums are fixed-order, the ELBO's fp64
+    # accumulator adds workgroup partials in arrival order (last bits only)
+    assert torch.allclose(b.inner_loop(T=2).cpu(), e1, rtol=1e-12, atol=0)
 
 
 # ------------------------------------------------------------ outer objective
