@@ -25,6 +25,7 @@ extern int g_stream_off;                 // kernels_mvn.hip
 extern int g_lenet_gemm_valu;            // kernels_lenet.hip
 extern int g_net_split_below;            // kernels_net.hip
 extern int g_net_threads;                // kernels_net.hip
+extern int g_net_wg_target;              // kernels_net.hip
 extern int g_fwd_ablation;               // kernels_mvn.hip
 extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
@@ -414,6 +415,10 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_NET_ABLATION: g_net_ablation = value; return 0;
         case PSVI_DBG_UPD_ABLATION: g_upd_ablation = value; return 0;
         case PSVI_DBG_NET_SPLIT_BELOW: g_net_split_below = value; return 0;
+        case PSVI_DBG_NET_WG_TARGET:
+            if (value < 1) return fail(PSVI_EINVAL, "workgroup target must be >= 1");
+            g_net_wg_target = value;
+            return 0;
         case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;

@@ -883,6 +883,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
 
 int g_net_threads = 0;        // psvi_debug_set(PSVI_DBG_NET_THREADS, n): 0 = by chunk size
 int g_net_split_below = 256;  // split when a rank has fewer samples than CUs (psvi_debug_set(PSVI_DBG_NET_SPLIT_BELOW, n))
+int g_net_wg_target = 256;    // workgroups a split rank aims for (psvi_debug_set(PSVI_DBG_NET_WG_TARGET, n))
 
 size_t net_plan_geometry(psvi_plan& p) {
     // One workgroup per sample and all M pseudopoints when the samples alone
@@ -896,7 +897,7 @@ size_t net_plan_geometry(psvi_plan& p) {
     p.net_roles = (split && p.L > 1) ? 2 : 1;
     int mchunks = 1;
     if (split)
-        while (S_local * p.net_roles * mchunks < 256 && (M + mchunks) / (mchunks + 1) >= 16)
+        while (S_local * p.net_roles * mchunks < g_net_wg_target && (M + mchunks) / (mchunks + 1) >= 16)
             ++mchunks;
     for (;;) {
         const int mc = (M + mchunks - 1) / mchunks;

@@ -430,6 +430,10 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_NET_THREADS 14  /* value: threads per network workgroup (256 or
                                     512; 0 = by chunk size) for plans created
                                     afterwards (A/B diagnostics)               */
+#define PSVI_DBG_NET_WG_TARGET 15 /* value: network workgroups a split rank aims
+                                    for (pseudopoint chunks added until samples x
+                                    roles x chunks reach it; default 256) for
+                                    plans created afterwards (A/B diagnostics) */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

@@ -5,6 +5,7 @@ C3 inner-loop steps/s of a plan created under each value, alternating rounds.
   python tools/knob_ab.py KEY VALUE_A VALUE_B [steps] [rounds]
   e.g. tools/knob_ab.py 14 512 256   (PSVI_DBG_NET_THREADS)
        tools/knob_ab.py 12 0 1       (PSVI_DBG_STREAM_RR)
+       tools/knob_ab.py 15 256 512   (PSVI_DBG_NET_WG_TARGET)
 """
 import os
 import sys
@@ -26,7 +27,7 @@ def main():
     dev = torch.device("cuda")
     u, z, w = synthetic_inputs(dev)
     lib = InnerLoopPlan("fullcov", LAYERS, 128, M).lib
-    default = {14: 0, 12: 0}.get(key, 0)
+    default = {14: 0, 12: 0, 15: 256}.get(key, 0)
     plans = {}
     for val in vals:
         lib.psvi_debug_set(key, val)
