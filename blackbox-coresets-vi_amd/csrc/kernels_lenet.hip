@@ -275,14 +275,18 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
         for (int i = tid; i < 150; i += kConvThreads) w1[i] = ws[i];
         for (int i = tid; i < 6 * 1024; i += kConvThreads) da1[i] = 0.f;
     }
-    // conv2 weight entries owned by this thread: e = tid + r * 320
-    constexpr int kR2 = (2400 + kConvThreads - 1) / kConvThreads;
-    int kb[kR2], pb[kR2];
+    // conv2 weight entries owned by this thread: output channel k2 = tid / 15
+    // (threads < 240), entries (k2, c, i, j) with c * 25 + i * 5 + j = t15 + 15 r.
+    // One output channel per thread: each routed gradient and offset is read
+    // once per 10 MACs (was: three LDS reads per MAC).
+    constexpr int kR2 = 10;
+    const bool own2 = tid < 240;
+    const int k2 = min(tid / 15, 15), t15 = tid % 15;
+    int pb[kR2];
 #pragma unroll
     for (int r = 0; r < kR2; ++r) {
-        const int e = min(tid + r * kConvThreads, 2399);
-        kb[r] = (e / 150) * 25;
-        pb[r] = ((e % 150) / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
+        const int e = t15 + 15 * r;
+        pb[r] = (e / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
     }
     float accw2[kR2];
 #pragma unroll
@@ -317,14 +321,21 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
         }
         __syncthreads();
         // conv2 weight gradient: dW2[k][c][i][j] += sum_p g2[k][p] P1[c][y_p + i][x_p + j]
+        // (per image: acc over p = 0..24 from zero, then into accw2, the order
+        // of the per-entry form; p outer so that g2 / off2 are read once per p)
+        if (own2) {
+            float acc[kR2];
 #pragma unroll
-        for (int r = 0; r < kR2; ++r) {
-            if (tid + r * kConvThreads < 2400) {
-                float acc = 0.f;
+            for (int r = 0; r < kR2; ++r) acc[r] = 0.f;
 #pragma unroll
-                for (int p = 0; p < 25; ++p) acc += g2[kb[r] + p] * p1[pb[r] + off2[kb[r] + p]];
-                accw2[r] += acc;
+            for (int p = 0; p < 25; ++p) {
+                const float gv = g2[k2 * 25 + p];
+                const int op = off2[k2 * 25 + p];
+#pragma unroll
+                for (int r = 0; r < kR2; ++r) acc[r] += gv * p1[pb[r] + op];
             }
+#pragma unroll
+            for (int r = 0; r < kR2; ++r) accw2[r] += acc[r];
         }
         if (tid < 16) {
             float acc = 0.f;
@@ -426,10 +437,9 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
     if (half == 0 && e1 < 156) out[e1] = acc1 + red[e1];
     if (tid < 16) out[2556 + tid] = accb2;
+    if (own2) {
 #pragma unroll
-    for (int r = 0; r < kR2; ++r) {
-        const int e = tid + r * kConvThreads;
-        if (e < 2400) out[156 + e] = accw2[r];
+        for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
     }
 }
 
