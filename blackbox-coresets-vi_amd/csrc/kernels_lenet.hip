@@ -899,16 +899,16 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     const float* wds = a.wdot + (int64_t)s * a.n_tot;
     for (int i = tid; i < 150; i += kConvThreads) { w1[i] = ws[i]; wd1[i] = wds[i]; }
     for (int i = tid; i < 2400; i += kConvThreads) { w2[i] = ws[156 + i]; wd2[i] = wds[156 + i]; }
-    constexpr int kR2 = (2400 + kConvThreads - 1) / kConvThreads;
-    // the conv2 weight e's routed-gradient base (kb) and P1 tap base (pb) are
-    // formed where they are read: kept in 16 registers across the image loop
-    // they pushed the kernel into scratch spills
-    auto kb = [&](int r) __attribute__((always_inline)) {
-        return (min(tid + r * kConvThreads, 2399) / 150) * 25;
-    };
+    // conv2 weight entries: output channel k2 = tid / 15 (threads < 240),
+    // entries c * 25 + i * 5 + j = t15 + 15 r, as in lenet_conv_bwd_kernel.  The
+    // P1 tap base (pb) is formed where it is read: kept in registers across the
+    // image loop it pushed this kernel into scratch spills.
+    constexpr int kR2 = 10;
+    const bool own2 = tid < 240;
+    const int k2 = min(tid / 15, 15), t15 = tid % 15;
     auto pb = [&](int r) __attribute__((always_inline)) {
-        const int e = min(tid + r * kConvThreads, 2399);
-        return ((e % 150) / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
+        const int e = t15 + 15 * r;
+        return (e / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
     };
     float accw2[kR2];
 #pragma unroll
@@ -952,19 +952,25 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
             da2d[da2_at(k, y + 4, x + 4)] = gd;
         }
         __syncthreads();
-        // G_dot conv2: sum_p g2_dot P1 + g2 P1_dot at the routed windows
+        // G_dot conv2: sum_p g2_dot P1 + g2 P1_dot at the routed windows (per
+        // image: acc over p from zero, then into accw2; g2 / g2d / off2 read
+        // once per 10 entries)
+        if (own2) {
+            float acc[kR2];
 #pragma unroll
-        for (int r = 0; r < kR2; ++r) {
-            if (tid + r * kConvThreads < 2400) {
-                float acc = 0.f;
-                const int kbr = kb(r), pbr = pb(r);
+            for (int r = 0; r < kR2; ++r) acc[r] = 0.f;
+#pragma unroll 1
+            for (int p = 0; p < 25; ++p) {
+                const float gv = g2[k2 * 25 + p], gdv = g2d[k2 * 25 + p];
+                const int op = off2[k2 * 25 + p];
 #pragma unroll
-                for (int p = 0; p < 25; ++p) {
-                    const int q = pbr + off2[kbr + p];
-                    acc += g2d[kbr + p] * p1[q] + g2[kbr + p] * p1d[q];
+                for (int r = 0; r < kR2; ++r) {
+                    const int q = pb(r) + op;
+                    acc[r] += gdv * p1[q] + gv * p1d[q];
                 }
-                accw2[r] += acc;
             }
+#pragma unroll
+            for (int r = 0; r < kR2; ++r) accw2[r] += acc[r];
         }
         if (tid < 16) {
             float acc = 0.f;
@@ -1038,10 +1044,9 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
     if (half == 0 && e1 < 156) out[e1] = acc1 + red[e1];
     if (tid < 16) out[2556 + tid] = accb2;
+    if (own2) {
 #pragma unroll
-    for (int r = 0; r < kR2; ++r) {
-        const int e = tid + r * kConvThreads;
-        if (e < 2400) out[156 + e] = accw2[r];
+        for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
     }
 }
 
