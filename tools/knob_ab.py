@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B of a plan-creation diagnostics switch (psvi_debug_set key, two values):
-C3 inner-loop steps/s of a plan created under each value, alternating rounds.
+C3 inner-loop steps/s of a plan created under each value, alternating rounds
+(KNOB_S / KNOB_M in the environment: another fn2 shape, e.g. C4's 1024 / 200).
 
   python tools/knob_ab.py KEY VALUE_A VALUE_B [steps] [rounds]
   e.g. tools/knob_ab.py 14 512 256   (PSVI_DBG_NET_THREADS)
@@ -25,13 +26,21 @@ def main():
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 300
     rounds = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     dev = torch.device("cuda")
-    u, z, w = synthetic_inputs(dev)
-    lib = InnerLoopPlan("fullcov", LAYERS, 128, M).lib
-    default = {14: 0, 12: 0, 15: 256}.get(key, 0)
+    S, Mx = int(os.environ.get("KNOB_S", 128)), int(os.environ.get("KNOB_M", M))
+    if Mx == M:
+        u, z, w = synthetic_inputs(dev)
+    else:
+        g = torch.Generator().manual_seed(5)
+        u = torch.randn(Mx, LAYERS[0][0], generator=g)
+        z = (torch.rand(Mx, generator=g) < torch.sigmoid(5.0 * u.sum(1))).to(torch.int32).to(dev)
+        u = u.to(dev)
+        w = torch.full((Mx,), 1000.0 / Mx, device=dev)
+    lib = InnerLoopPlan("fullcov", LAYERS, S, Mx).lib
+    default = {14: 0, 12: 0, 15: 256, 5: 256}.get(key, 0)
     plans = {}
     for val in vals:
         lib.psvi_debug_set(key, val)
-        plans[val] = InnerLoopPlan("fullcov", LAYERS, 128, M)
+        plans[val] = InnerLoopPlan("fullcov", LAYERS, S, Mx)
     lib.psvi_debug_set(key, default)
     res = {v: [] for v in vals}
     for _ in range(rounds):
