@@ -254,6 +254,7 @@ __device__ __forceinline__ int da2_at(int k, int y, int x) {  // bordered (y, x)
 // DU (outer backward): also d u = the transposed conv1 of the routed conv1
 // gradient (dense, zero-bordered LDS plane, 2x2 pixel blocks per thread) for
 // the pseudopoint rows m < n_pseudo.
+constexpr int kW1Groups = 8;  // conv1 weight-gradient position groups (backward)
 template <bool DU>
 __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a) {
     __shared__ float w1[DU ? 150 : 1];
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     __shared__ float da2[2 * kDAP];  // [parity][k][y][x / 2]
     __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
     __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
-    __shared__ float red[160];
+    __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
     for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
@@ -291,12 +292,15 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     float accw2[kR2];
 #pragma unroll
     for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
-    // conv1: threads [0, 160) and [160, 320) split the 196 routed positions;
-    // e < 150 weight (c, i, j), 150..155 bias
-    const int half = tid / 160, e1 = tid % 160;
-    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * kBS + e1 % 5;
-    const int cb1 = (e1 >= 150 && e1 < 156) ? e1 - 150 : c1;
-    float acc1 = 0.f, accb2 = 0.f;
+    // conv1: thread t < 240 owns the five weights (c1, i1, 0..4) over the
+    // routed positions of p group pg1 (c1 = t / 40, i1 = t / 8 % 5, pg1 = t % 8);
+    // threads 240 .. 287 the bias c1 over group pg1.  The g1 / off1 read of a
+    // position serves five MACs; the 8 group partials are added in group order.
+    const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
+    const int t1 = w1own ? tid : tid - 240;
+    const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
+    const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
+    float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
     for (int m = m0; m < m1; ++m) {
         __syncthreads();
@@ -382,17 +386,22 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
             da2[da2_at(k, q / kP1S + 4, q % kP1S + 4)] = 0.f;
         }
         // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
-        if (e1 < 156) {
-            const int p0 = half * 98;
-            float acc = 0.f;
-            if (e1 < 150) {
-#pragma unroll 7
-                for (int p = p0; p < p0 + 98; ++p) acc += g1[c1 * 196 + p] * in[off1[c1 * 196 + p] + o1];
-            } else {
-#pragma unroll 7
-                for (int p = p0; p < p0 + 98; ++p) acc += g1[cb1 * 196 + p];
+        if (w1own) {
+            float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+            for (int p = pl1; p < ph1; ++p) {
+                const float gv = g1[c1 * 196 + p];
+                const float* ip = in + off1[c1 * 196 + p] + i1 * kBS;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) acc[j] += gv * ip[j];
             }
-            acc1 += acc;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) acc1[j] += acc[j];
+        } else if (b1own) {
+            float acc = 0.f;
+#pragma unroll 5
+            for (int p = pl1; p < ph1; ++p) acc += g1[c1 * 196 + p];
+            acc1[0] += acc;
         }
         if (DU && m < a.n_pseudo) {
             for (int o = tid; o < kP1; o += kConvThreads)
@@ -432,10 +441,20 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
         }
     }
     __syncthreads();
-    if (half == 1) red[e1] = acc1;
+    if (w1own) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) red[pg1 * 156 + c1 * 25 + i1 * 5 + j] = acc1[j];
+    } else if (b1own) {
+        red[pg1 * 156 + 150 + c1] = acc1[0];
+    }
     __syncthreads();
     float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
-    if (half == 0 && e1 < 156) out[e1] = acc1 + red[e1];
+    if (tid < 156) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < kW1Groups; ++q) t += red[q * 156 + tid];
+        out[tid] = t;
+    }
     if (tid < 16) out[2556 + tid] = accb2;
     if (own2) {
 #pragma unroll
