@@ -912,7 +912,7 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     __shared__ float g1[kP1], g1d[kP1];
     __shared__ int off1[kP1];
     __shared__ float plane[kPlane];
-    __shared__ float red[160];
+    __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
     const float* wds = a.wdot + (int64_t)s * a.n_tot;
@@ -932,10 +932,13 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     float accw2[kR2];
 #pragma unroll
     for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
-    const int half = tid / 160, e1 = tid % 160;
-    const int c1 = min(e1, 149) / 25, o1 = ((min(e1, 149) % 25) / 5) * kBS + e1 % 5;
-    const int cb1 = (e1 >= 150 && e1 < 156) ? e1 - 150 : c1;
-    float acc1 = 0.f, accb2 = 0.f;
+    // conv1: five-tap weight rows over 8 routed-position groups, as in
+    // lenet_conv_bwd_kernel
+    const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
+    const int t1 = w1own ? tid : tid - 240;
+    const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
+    const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
+    float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
     float* da2 = plane;
     float* da2d = plane + 2 * kDAP;
     float* da1 = plane;
@@ -1019,18 +1022,22 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
         }
         __syncthreads();
         // G_dot conv1 (the image is constant): sum_p g1_dot in[...]
-        if (e1 < 156) {
-            const int p0 = half * 98;
-            float acc = 0.f;
-            if (e1 < 150) {
-#pragma unroll 7
-                for (int p = p0; p < p0 + 98; ++p)
-                    acc += g1d[c1 * 196 + p] * in[off1[c1 * 196 + p] + o1];
-            } else {
-#pragma unroll 7
-                for (int p = p0; p < p0 + 98; ++p) acc += g1d[cb1 * 196 + p];
+        if (w1own) {
+            float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+            for (int p = pl1; p < ph1; ++p) {
+                const float gv = g1d[c1 * 196 + p];
+                const float* ip = in + off1[c1 * 196 + p] + i1 * kBS;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) acc[j] += gv * ip[j];
             }
-            acc1 += acc;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) acc1[j] += acc[j];
+        } else if (b1own) {
+            float acc = 0.f;
+#pragma unroll 5
+            for (int p = pl1; p < ph1; ++p) acc += g1d[c1 * 196 + p];
+            acc1[0] += acc;
         }
         if (a.du) {
             for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
@@ -1058,10 +1065,20 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
         }
     }
     __syncthreads();
-    if (half == 1) red[e1] = acc1;
+    if (w1own) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) red[pg1 * 156 + c1 * 25 + i1 * 5 + j] = acc1[j];
+    } else if (b1own) {
+        red[pg1 * 156 + 150 + c1] = acc1[0];
+    }
     __syncthreads();
     float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
-    if (half == 0 && e1 < 156) out[e1] = acc1 + red[e1];
+    if (tid < 156) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < kW1Groups; ++q) t += red[q * 156 + tid];
+        out[tid] = t;
+    }
     if (tid < 16) out[2556 + tid] = accb2;
     if (own2) {
 #pragma unroll
