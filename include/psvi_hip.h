@@ -178,8 +178,10 @@ int psvi_inner_loop(const psvi_plan* plan, const float* u, const int32_t* z,
 
 /* ---- sharded phases (any world; the caller runs the collectives) ------------
  * MEANFIELD (sample-parallel, replicated params):
- *   acc (ACC_COUNT floats, zeroed by the call) <- [sum_s dW | sum_s dW*eps]
- *   over this rank's samples, nll_out[0] += their weighted NLL;  caller
+ *   acc (ACC_COUNT floats, overwritten) <- [sum_s dW | sum_s dW*eps] over this
+ *   rank's samples, summed in a fixed order from per-(sample, chunk) slots
+ *   (plan-owned scratch: one call on a plan at a time; bitwise reproducible),
+ *   nll_out[0] += their weighted NLL;  caller
  *   all-reduces acc (sum);  update applies KL gradient + Adam identically on
  *   every rank (grad_out != NULL: write the gradient instead), kl_out[0] +=
  *   KL (nullable; count it on one rank). */
