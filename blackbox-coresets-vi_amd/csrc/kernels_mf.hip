@@ -68,16 +68,36 @@ __device__ __forceinline__ void mf_slot_sums(const MfUpdArgs& a, int l, int idx,
     const float* ep = a.seps + a.eoff[l] + (wt ? idx : (int64_t)a.S_total * nw + (idx - nw));
     const int64_t es = wt ? nw : a.dout[l];
     const size_t ss = (size_t)a.nz * a.n_tot;
+    // two samples x the first kC chunks per round as unconditional loads at
+    // clamped indices (all in flight together); the sums run in the order
+    // s, then c = 0, 1, ... whatever the unroll
+    constexpr int kC = 4;
+    const int ncl = a.nz < kC ? a.nz : kC;
     g = 0.f;
     ge = 0.f;
-#pragma unroll 2
-    for (int s = s0; s < a.S_loc; s += sstep) {
-        const float* q = a.slots + (size_t)s * ss + e;
-        const float ev = ep[(int64_t)(a.s_goff + s) * es];
-        float gs = 0.f;
-        for (int c = 0; c < a.nz; ++c) gs += q[(size_t)c * a.n_tot];
-        g += gs;
-        ge += gs * ev;
+    for (int s = s0; s < a.S_loc; s += 2 * sstep) {
+        const int sb = s + sstep < a.S_loc ? s + sstep : s;
+        float v[2][kC], ev[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int su = u ? sb : s;
+            const float* q = a.slots + (size_t)su * ss + e;
+#pragma unroll
+            for (int c = 0; c < kC; ++c) v[u][c] = q[(size_t)min(c, a.nz - 1) * a.n_tot];
+            ev[u] = ep[(int64_t)(a.s_goff + su) * es];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (u && s + sstep >= a.S_loc) break;
+            const float* q = a.slots + (size_t)(u ? sb : s) * ss + e;
+            float gs = 0.f;
+#pragma unroll
+            for (int c = 0; c < kC; ++c)
+                if (c < ncl) gs += v[u][c];
+            for (int c = kC; c < a.nz; ++c) gs += q[(size_t)c * a.n_tot];
+            g += gs;
+            ge += gs * ev[u];
+        }
     }
 }
 
