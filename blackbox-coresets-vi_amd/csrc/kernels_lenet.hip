@@ -84,12 +84,35 @@ __global__ __launch_bounds__(kThreads) void lenet_acc_kernel(SampleArgs a,
     const int l = lenet_layer(a, j);
     const int idx = j - a.woff[l];
     const bool path = ck != nullptr && l >= 2;
+    // eps of sample s at ep[s * es] (lenet_eps_index with the branches hoisted)
+    const float* ep = eps + lenet_eps_index(a, l, idx, a.s_off);
+    const int64_t es = !a.batched[l] ? 0 : idx < a.nw[l] ? a.nw[l] : a.n[l] - a.nw[l];
     float g = 0.f, ge = 0.f;
-    for (int s = 0; s < a.S_loc; ++s) {
+    // 8 samples' loads issued together, then added in sample order
+    constexpr int kU = 8;
+    int s = 0;
+    for (; s + kU <= a.S_loc; s += kU) {
+        float d[kU], e[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            d[u] = dws[(int64_t)(s + u) * a.n_tot + j];
+            e[u] = ep[(int64_t)(s + u) * es];
+        }
+        if (path) {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) d[u] -= ck[s + u] * wsamp[(int64_t)(s + u) * a.n_tot + j] * inv_s0sq;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            g += d[u];
+            ge += d[u] * e[u];
+        }
+    }
+    for (; s < a.S_loc; ++s) {
         float d = dws[(int64_t)s * a.n_tot + j];
         if (path) d -= ck[s] * wsamp[(int64_t)s * a.n_tot + j] * inv_s0sq;
         g += d;
-        ge += d * eps[lenet_eps_index(a, l, idx, a.s_off + s)];
+        ge += d * ep[(int64_t)s * es];
     }
     acc[j] = g;
     acc[a.n_tot + j] = ge;
