@@ -54,19 +54,24 @@ __device__ __forceinline__ int lenet_layer(const SampleArgs& a, int j) {
 }
 
 // Wsamp[s][j] = mu_j + softplus(rho_j) eps_(s, j)   (VIMixin.rsample, neural_net.py:155-162)
+constexpr int kSampleRun = 16;  // samples per block row of lenet_sample_kernel
 __global__ __launch_bounds__(kThreads) void lenet_sample_kernel(SampleArgs a,
                                                                 const float* __restrict__ params,
                                                                 const float* __restrict__ eps,
                                                                 float* __restrict__ wsamp) {
-    const int64_t total = (int64_t)a.S_loc * a.n_tot;
-    for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * kThreads) {
-        const int s = (int)(i / a.n_tot), j = (int)(i - (int64_t)s * a.n_tot);
-        const int l = lenet_layer(a, j);
-        const int idx = j - a.woff[l];
-        const float mu = params[a.poff[l] + idx], rho = params[a.poff[l] + a.n[l] + idx];
-        wsamp[i] = mu + softplus_f(rho) * eps[lenet_eps_index(a, l, idx, a.s_off + s)];
-    }
+    // thread = parameter j, block row = kSampleRun consecutive samples: mu and
+    // softplus(rho) once, the eps index branches hoisted, 8 draws in flight
+    const int j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.n_tot) return;
+    const int l = lenet_layer(a, j);
+    const int idx = j - a.woff[l];
+    const float mu = params[a.poff[l] + idx], sp = softplus_f(params[a.poff[l] + a.n[l] + idx]);
+    const int s0 = blockIdx.y * kSampleRun, s1 = min(a.S_loc, s0 + kSampleRun);
+    const float* ep = eps + lenet_eps_index(a, l, idx, a.s_off + s0);
+    const int64_t es = !a.batched[l] ? 0 : idx < a.nw[l] ? a.nw[l] : a.n[l] - a.nw[l];
+    float* out = wsamp + (int64_t)s0 * a.n_tot + j;
+#pragma unroll 8
+    for (int s = 0; s < s1 - s0; ++s) out[(int64_t)s * a.n_tot] = mu + sp * ep[(int64_t)s * es];
 }
 
 // acc[j] = sum_s dW[s][j],  acc[n_tot + j] = sum_s dW[s][j] eps_(s, j)
@@ -1251,9 +1256,10 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     if (S == 0) return hipMemsetAsync(acc, 0, sizeof(float) * 2 * nt, st);
     const int64_t rows = (int64_t)S * M;
     {
-        const int64_t nb = std::min<int64_t>(((int64_t)S * nt + kThreads - 1) / kThreads, 8192);
-        hipLaunchKernelGGL(lenet_sample_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, sa,
-                           params, eps, W.wsamp);
+        const dim3 grid((unsigned)((nt + kThreads - 1) / kThreads),
+                        (unsigned)((S + kSampleRun - 1) / kSampleRun));
+        hipLaunchKernelGGL(lenet_sample_kernel, grid, dim3(kThreads), 0, st, sa, params, eps,
+                           W.wsamp);
     }
     ConvArgs ca{};
     ca.M = M;
