@@ -670,8 +670,18 @@ __global__ __launch_bounds__(kThreads) void lenet_colsum_kernel(const float* __r
     const int n = blockIdx.y * 64 + c;
     const float* x = X + (int64_t)b * M * N;
     float acc = 0.f;
-    if (n < N)
-        for (int m = g; m < M; m += 4) acc += x[(int64_t)m * N + n];
+    if (n < N) {
+        // 8 rows' loads in flight, added in row order
+        int m = g;
+        for (; m + 28 < M; m += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = x[(int64_t)(m + 4 * u) * N + n];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; m < M; m += 4) acc += x[(int64_t)m * N + n];
+    }
     red[g][c] = acc;
     __syncthreads();
     if (g == 0 && n < N) out[b * sOb + n] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
