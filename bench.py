@@ -69,13 +69,13 @@ def algorithmic_work_fused(S):
                 flops=w["update"]["flops"] + w["sample"]["flops"])
 
 
-def algorithmic_work(S, rows_frac=1.0):
+def algorithmic_work(S, rows_frac=1.0, layers=LAYERS):
     """Per-launch algorithmic bytes / flops of the two dominant kernels
     (SURVEY.md §8(d)); rows_frac = this rank's share of the rows (nnz).
     update: p, m, v of the owned parameters read + written once (24 B each),
     G of the owned rows and eps (all columns) read once (4 B each), dL = G^T eps
     over the strict lower triangle (2 flops per MAC)."""
-    n = [i * o + o for i, o in LAYERS]
+    n = [i * o + o for i, o in layers]
     n_tot = sum(n)
     nc = sum((k - 1) * (k - 2) // 2 for k in n)
     upd_bytes = 24 * (nc + 2 * n_tot) * rows_frac + 4 * S * n_tot * rows_frac + 4 * S * n_tot
@@ -121,6 +121,71 @@ def pin_cpu_threads():
 def log(msg):
     """Progress on stderr (the JSON line stays alone on stdout)."""
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+class Runtime:
+    """The process's place in the job and the device / collective plumbing the
+    legs share: `dev`, `world`, `rank`, `comm` (psvi.runtime.sharded comm:
+    RCCL through torch.distributed, or gloo with host staging for rehearsals
+    on one GPU or on the CPU), `sync()`, `barrier()`, `max_over_ranks(x)`,
+    `event()` (HIP events on the launch stream; wall-clock stand-ins on the
+    CPU)."""
+
+    def __init__(self, dev, world, rank, comm=None):
+        self.dev, self.world, self.rank, self.comm = dev, int(world), int(rank), comm
+
+    @property
+    def cuda(self):
+        return self.dev.type == "cuda"
+
+    def sync(self):
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return float(x)
+        import torch.distributed as dist
+        t = torch.tensor([float(x)], dtype=torch.float64,
+                         device=self.dev if self.comm_on_device else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    @property
+    def comm_on_device(self):
+        return self.cuda and not getattr(self.comm, "host_staged", False)
+
+    def timed(self, fn):
+        """Wall seconds of fn() between synchronised barriers, the max over ranks."""
+        self.sync()
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        fn()
+        self.sync()
+        self.barrier()
+        self.sync()
+        return self.max_over_ranks(time.perf_counter() - t0)
+
+    def event(self):
+        if self.cuda:
+            return torch.cuda.Event(enable_timing=True)
+        return _WallEvent()
+
+
+class _WallEvent:
+    """torch.cuda.Event's record / elapsed_time on the host clock (CPU rehearsal)."""
+
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
 
 
 def cpu_baseline(budget_s=12.0):
@@ -217,71 +282,129 @@ def _mf_init(layers, init_sd=1e-3):
 C4 = dict(S=1024, M=200)
 
 
-def c4_timings(dev, world, rank, steps=100, warmup=10):
+def draw_eps(t, seed, offset):
+    """The per-step noise of the sharded legs: the psvi_inner_loop Philox
+    stream (every rank draws the same global eps; it never crosses the wire)."""
+    from psvi.runtime import randn_
+    randn_(t, seed, offset)
+
+
+def make_sharded_loop(family, layers, S, M, rt):
+    """This rank's ShardedInnerLoop (rows of L x samples for full-cov, samples
+    for LeNet), collectives on rt.comm."""
+    from psvi.runtime.sharded import ShardedInnerLoop
+    return ShardedInnerLoop(family, layers, S, M, rt.world, rt.rank, device=rt.dev, comm=rt.comm)
+
+
+def fn2_inputs(layers, M, dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    u = torch.randn(M, layers[0][0], generator=g)
+    z = (torch.rand(M, generator=g) < torch.sigmoid(5.0 * u.sum(1))).to(torch.int32)
+    return u.to(dev), z.to(dev), torch.full((M,), N_DATA / M, device=dev)
+
+
+def sharded_steps(rt, loop, u, z, w, eps, params, m, v, seed, k0, n, parts=None, ev=None):
+    """n sharded inner steps (Adam steps k0 + 1 ..): per step the eps draw, the
+    sample phase, the x all_to_all, the network, the G all_to_all and the
+    update -- the phases are the loop's own (ShardedInnerLoop.step's body),
+    split out so HIP events can bracket them.  ev: {step index: 4 events}."""
+    stride = (loop.plan.eps_count + 3) // 4 * 4
+    for k in range(k0, k0 + n):
+        e = ev.get(k) if ev else None
+        draw_eps(eps, seed, k * stride)
+        if loop.family != "fullcov":
+            loop.step(u, z, w, eps, params, m, v, k + 1, LR)
+        else:
+            if e: e[0].record()
+            loop.phase_sample(eps, params)
+            if e: e[1].record()
+            loop.comm.all_to_all(loop.x_recv, loop.x_shard, loop.x_out, loop.x_in)
+            loop.phase_net(u, z, w)
+            loop.comm.all_to_all(loop.g_shard, loop.g_send, loop.g_out, loop.g_in)
+            if e: e[2].record()
+            loop.phase_update(eps, params, m, v, k + 1, LR, "higher")
+            if e: e[3].record()
+        if parts is not None:
+            parts[k].copy_(loop.parts)
+
+
+def sharded_headline(rt, steps, warmup, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M, ev_every=10):
+    """The headline at N > 1: C3 shards weak-scaled (S = 128 N, M = 100), rows
+    of L x samples sharded, two all_to_alls per step.  Returns (elapsed s, the
+    (warmup + steps) x 2 [NLL, KL] parts of this rank, per-phase ms, loop)."""
+    S = s_per_gpu * rt.world
+    loop = make_sharded_loop("fullcov", layers, S, M, rt)
+    u, z, w = fn2_inputs(layers, M, rt.dev, 0)
+    params = reference_init_params(layers, rt.dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    eps = torch.empty(loop.plan.eps_count, device=rt.dev)
+    total = warmup + steps
+    parts = torch.zeros(total, 2, dtype=torch.float64, device=rt.dev)
+    ev = {k: [rt.event() for _ in range(4)]
+          for k in range(warmup, total) if (k - warmup) % ev_every == 0}
+    sharded_steps(rt, loop, u, z, w, eps, params, m, v, 20251015, 0, warmup, parts)
+    elapsed = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, eps, params, m, v, 20251015,
+                                             warmup, steps, parts, ev))
+    ph = {"sample": [], "exchange+net": [], "update": []}
+    for e in ev.values():
+        ph["sample"].append(e[0].elapsed_time(e[1]))
+        ph["exchange+net"].append(e[1].elapsed_time(e[2]))
+        ph["update"].append(e[2].elapsed_time(e[3]))
+    avg_ms = {k: sum(x) / max(len(x), 1) for k, x in ph.items()}
+    return elapsed, parts, avg_ms, loop
+
+
+def c4_timings(rt, steps=100, warmup=10, layers=LAYERS, S=C4["S"], M=C4["M"]):
     """Auxiliary line for BASELINE.json configs[3] (C4): fn2 64-40-40-2 full-cov,
     S = 1024, M = 200 -- the same total work at every N (strong scaling):
     N = 1 runs psvi_inner_loop; N > 1 the rows-of-L x samples sharded step
     (ShardedInnerLoop, two all_to_alls per step).  inner-steps/s of the whole
     job; BASELINE's ">= 6x at 8 GPUs over 1" is this line at N = 8 over N = 1."""
-    from psvi.runtime import InnerLoopPlan, randn_
-    from psvi.runtime.sharded import ShardedInnerLoop, TorchDistComm
+    from psvi.runtime import InnerLoopPlan
 
-    S, Mc = C4["S"], C4["M"]
-    g = torch.Generator().manual_seed(5)
-    u = torch.randn(Mc, 64, generator=g).to(dev)
-    z = (torch.rand(Mc, generator=g) < torch.sigmoid(5.0 * u.cpu().sum(1))).to(torch.int32).to(dev)
-    w = torch.full((Mc,), N_DATA / Mc, device=dev)
-    params = reference_init_params(LAYERS, dev)
+    dev = rt.dev
+    u, z, w = fn2_inputs(layers, M, dev, 5)
+    params = reference_init_params(layers, dev)
     m, v = torch.zeros_like(params), torch.zeros_like(params)
-    if world == 1:
-        plan = InnerLoopPlan("fullcov", LAYERS, S, Mc)
+    if rt.world == 1:
+        plan = InnerLoopPlan("fullcov", layers, S, M)
         ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+        elbo = torch.empty(steps, dtype=torch.float64, device=dev)
         plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=11, ws=ws)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        plan.inner_loop(u, z, w, params, m, v, steps, LR, seed=12, ws=ws)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        dt = rt.timed(lambda: plan.inner_loop(u, z, w, params, m, v, steps, LR, seed=12, ws=ws,
+                                              elbo_out=elbo))
+        negelbo = elbo[-1:]
     else:
-        import torch.distributed as dist
-
-        loop = ShardedInnerLoop("fullcov", LAYERS, S, Mc, world, rank, device=dev,
-                                comm=TorchDistComm())
+        loop = make_sharded_loop("fullcov", layers, S, M, rt)
         eps = torch.empty(loop.plan.eps_count, device=dev)
-        stride = (loop.plan.eps_count + 3) // 4 * 4
-        for k in range(warmup):
-            randn_(eps, 11, k * stride)
-            loop.step(u, z, w, eps, params, m, v, k + 1, LR)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for k in range(steps):
-            randn_(eps, 12, k * stride)
-            loop.step(u, z, w, eps, params, m, v, warmup + k + 1, LR)
-        torch.cuda.synchronize()
-        dist.barrier()
-        dt = time.perf_counter() - t0
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    return {"config": f"C4 fn2 full-cov S={S} M={Mc}, {world} GPU(s) (strong scaling)",
-            "inner_steps_per_s": round(steps / dt, 2), "ms_per_step": round(dt / steps * 1e3, 4)}
+        parts = torch.zeros(warmup + steps, 2, dtype=torch.float64, device=dev)
+        sharded_steps(rt, loop, u, z, w, eps, params, m, v, 11, 0, warmup, parts)
+        dt = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, eps, params, m, v, 11, warmup,
+                                            steps, parts))
+        negelbo = loop.reduce_elbo(parts[-1:])
+    return {"config": f"C4 fn2 full-cov S={S} M={M}, {rt.world} GPU(s) (strong scaling)",
+            "inner_steps_per_s": round(steps / dt, 2), "ms_per_step": round(dt / steps * 1e3, 4),
+            "elbo_finite": bool(torch.isfinite(negelbo).all().item())}
 
 
-def lenet_timings(dev, cpu=True, T=10):
-    """Auxiliary evidence, not the metric: config C5's inner step (make_lenet,
-    S = 256, M = 500 MNIST-shaped synthetic pseudopoints, N = 60000) through
-    psvi_inner_loop with in-library draws, and one op-faithful CPU step of the
-    same model (oracle/cpu_reference.py RefLenetStep: the reference's grouped
-    conv / max-pool / batched matmul sequence with create_graph autograd)."""
+def lenet_timings(rt, cpu=True, T=10, S=256, M=500, second_order=True):
+    """Auxiliary line for BASELINE.json configs[4] (C5, make_lenet, S = 256,
+    M = 500 MNIST-shaped synthetic pseudopoints, N = 60000; strong scaling:
+    the same S at every N).  One GPU: psvi_inner_loop with in-library draws;
+    N GPUs: the samples split over ranks (ShardedInnerLoop: one all-reduce of
+    the accumulator per step).  Then C5's bilevel outer: one psvi_hvp (N > 1:
+    psvi_hvp_partial + all-reduce, SampleShardedPlan) and one hyper_step
+    (inner_it = 10, K = 30, CG_normaleq: /root/reference/psvi/hypergrad/
+    hypergradients.py:199-244) through the reference-shaped PSVILearnV, sample-
+    sharded at N > 1.  At N = 1 also one op-faithful CPU step of the same
+    model (oracle/cpu_reference.py RefLenetStep)."""
     from psvi.models import LENET_LAYERS, make_lenet
     from psvi.runtime import InnerLoopPlan
 
-    S, M = 256, 500
+    dev, world = rt.dev, rt.world
     torch.manual_seed(0)
     net = make_lenet(mc_samples=S, init_sd=0.05)
     p0 = torch.nn.utils.parameters_to_vector(net.parameters()).detach()
-    plan = InnerLoopPlan("lenet", LENET_LAYERS, S, M)
     g = torch.Generator().manual_seed(2)
     u = torch.randn(M, 1, 28, 28, generator=g)
     z = torch.randint(0, 10, (M,), generator=g)
@@ -289,51 +412,67 @@ def lenet_timings(dev, cpu=True, T=10):
     params = p0.to(dev)
     m, v = torch.zeros_like(params), torch.zeros_like(params)
     ud, zd, wd = u.to(dev), z.to(dev, torch.int32), w.to(dev)
-    ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
-    plan.inner_loop(ud, zd, wd, params, m, v, 2, LR, seed=1, ws=ws)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    plan.inner_loop(ud, zd, wd, params, m, v, T, LR, seed=2, ws=ws)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / T * 1e3
+    if world == 1:
+        plan = InnerLoopPlan("lenet", LENET_LAYERS, S, M)
+        ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+        elbo = torch.empty(T, dtype=torch.float64, device=dev)
+        plan.inner_loop(ud, zd, wd, params, m, v, 2, LR, seed=1, ws=ws)
+        dt = rt.timed(lambda: plan.inner_loop(ud, zd, wd, params, m, v, T, LR, seed=2, ws=ws,
+                                              elbo_out=elbo))
+        finite = bool(torch.isfinite(elbo).all().item())
+    else:
+        loop = make_sharded_loop("lenet", LENET_LAYERS, S, M, rt)
+        eps = torch.empty(loop.plan.eps_count, device=dev)
+        parts = torch.zeros(2 + T, 2, dtype=torch.float64, device=dev)
+        sharded_steps(rt, loop, ud, zd, wd, eps, params, m, v, 1, 0, 2, parts)
+        dt = rt.timed(lambda: sharded_steps(rt, loop, ud, zd, wd, eps, params, m, v, 2, 2, T,
+                                            parts))
+        finite = bool(torch.isfinite(loop.reduce_elbo(parts[2:])).all().item())
+    ms = dt / T * 1e3
     # 289.8 GFLOP of algorithmic work per C5 inner step
-    # (106.6 forward + 183.2 backward); fp32 peak 157.3 TFLOP/s (VALU and MFMA alike)
+    # (106.6 forward + 183.2 backward); fp32 peak 157.3 TFLOP/s per GPU (VALU and MFMA alike)
     tfl = 289.8e9 / (ms * 1e-3) / 1e12
-    out = {"config": "C5 lenet S=256 M=500", "gpu_ms_per_inner_step": round(ms, 3),
-           "gpu_inner_steps_per_s": round(1e3 / ms, 2),
+    out = {"config": f"C5 lenet S={S} M={M}, {world} GPU(s) (strong scaling: S/{world} per GPU)",
+           "gpu_ms_per_inner_step": round(ms, 3), "gpu_inner_steps_per_s": round(1e3 / ms, 2),
+           "elbo_finite": finite,
            "roofline": {"bound": "fp32 (VALU = MFMA peak)", "achieved": round(tfl, 2),
-                        "peak": 157.3, "unit": "TFLOP/s", "frac": round(tfl / 157.3, 4),
+                        "peak": round(157.3 * world, 1), "unit": "TFLOP/s",
+                        "frac": round(tfl / (157.3 * world), 4),
                         "algorithmic_gflop_per_step": 289.8}}
-    # C5's bilevel outer: one psvi_hvp, and one hyper_step (inner_it = 10, K = 30,
-    # a 128-image data batch) through the reference-shaped PSVILearnV
+    if not second_order:
+        return out
     from psvi.inference import PSVILearnV
     from psvi.runtime import randn_
 
-    e = torch.empty(plan.eps_count, device=dev)
+    if world == 1:
+        hplan = plan
+    else:
+        from psvi.runtime.sharded import SampleShardedPlan
+        hplan = SampleShardedPlan("lenet", LENET_LAYERS, S, M, world, rt.rank, rt.comm)
+    e = torch.empty(hplan.eps_count, device=dev)
     randn_(e, 5)
-    vec = torch.randn(plan.param_count, generator=g).to(dev)
-    plan.hvp(ud, zd, wd, e, params, vec)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(3):
-        plan.hvp(ud, zd, wd, e, params, vec)
-    torch.cuda.synchronize()
-    out["gpu_hvp_ms"] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
+    vec = torch.randn(hplan.param_count, generator=g).to(dev)
+    hplan.hvp(ud, zd, wd, e, params, vec)
+
+    def hvps():
+        for _ in range(3):
+            hplan.hvp(ud, zd, wd, e, params, vec)
+    out["gpu_hvp_ms"] = round(rt.timed(hvps) / 3 * 1e3, 3)
     net_d = make_lenet(mc_samples=S, init_sd=0.05).to(dev)
     ps = PSVILearnV(u=ud.clone().requires_grad_(True), z=zd.float(), N=60000, model=net_d,
-                    mc_samples=S, device_id=dev.index, inner_it=10, seed=7)
+                    mc_samples=S, device_id=dev.index, inner_it=10, seed=7, world=world,
+                    rank=rt.rank, comm=rt.comm)
     ps.device = dev
     ps.register_elbos = False
     ps.setup_optimizers()
     xb = torch.randn(128, 1, 28, 28, generator=g).to(dev)
     yb = torch.randint(0, 10, (128,), generator=g).float().to(dev)
     ps.hyper_step(xb, yb, K=30)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ps.hyper_step(xb, yb, K=30)
-    torch.cuda.synchronize()
-    out["gpu_hyper_step_T10_K30_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
-    if cpu:
+    res = {}
+    dt = rt.timed(lambda: res.setdefault("ll", ps.hyper_step(xb, yb, K=30)))
+    out["gpu_hyper_step_T10_K30_ms"] = round(dt * 1e3, 1)
+    out["hyper_step_loss_finite"] = bool(math.isfinite(res["ll"]))
+    if cpu and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from cpu_reference import RefLenetStep
 
@@ -406,162 +545,97 @@ def trainer_timings(dev, cpu=True, cpu_T=2):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-lenet", action="store_true",
-                    help="skip the auxiliary C5 (lenet) inner-step timing")
-    ap.add_argument("--no-trainers", action="store_true",
-                    help="skip the auxiliary outer-step (trainer) timings")
-    ap.add_argument("--no-c4", action="store_true",
-                    help="skip the auxiliary C4 (S=1024, M=200) strong-scaling line")
-    ap.add_argument("--no-c2", action="store_true",
-                    help="skip the auxiliary C2 (fn, S=32, M=50) line")
-    args = ap.parse_args()
+def headline_world1(rt, args):
+    """The headline on one GPU: the K timed steps are ONE psvi_inner_loop call
+    (T chained steps, fresh Adam state, tiled corr/m/v, every conversion and the
+    first sample inside the timed region); the W warm-up steps are a separate
+    call.  Per-phase HIP events (PSVI_DBG_LOOP_TIMING) on every 10th step."""
+    from psvi.runtime import InnerLoopPlan
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-
-    from psvi.runtime import InnerLoopPlan, randn_
-    from psvi.runtime.sharded import ShardedInnerLoop, TorchDistComm
-
-    S = S_PER_GPU * world
+    dev = rt.dev
+    plan = InnerLoopPlan("fullcov", LAYERS, S_PER_GPU, M)
     u, z, w = synthetic_inputs(dev)
-    if world == 1:
-        plan = InnerLoopPlan("fullcov", LAYERS, S, M)
-        loop = None
-        rows_frac = 1.0
-    else:
-        loop = ShardedInnerLoop("fullcov", LAYERS, S, M, world, rank, device=dev,
-                                comm=TorchDistComm())
-        plan = loop.plan
-        n = [i * o + o for i, o in LAYERS]
-        info = loop.info[rank]
-        nnz_own = 0
-        for l, k in enumerate(n):
-            lo, hi = info["row_lo"][l], info["row_lo"][l] + info["row_cnt"][l]
-            nnz_own += sum(min(r, k - 1) for r in range(lo, hi))
-        rows_frac = nnz_own / sum((k - 1) * (k - 2) // 2 for k in n)
     params = reference_init_params(LAYERS, dev)
-    m = torch.zeros_like(params)
-    v = torch.zeros_like(params)
-    eps = torch.empty(plan.eps_count, device=dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
     eps_stride = (plan.eps_count + 3) // 4 * 4
-    total_steps = args.warmup + args.steps
-    # per-phase HIP events on every EV_EVERY-th timed step (event records between
-    # kernels add dispatch latency; sampling keeps the timed region representative)
-    EV_EVERY = 10
+    lib = plan.lib
+    ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+    elbo_w = torch.empty(max(args.warmup, 1), dtype=torch.float64, device=dev)
+    elbo_t = torch.empty(args.steps, dtype=torch.float64, device=dev)
+    if args.warmup:
+        plan.inner_loop(u, z, w, params, m, v, args.warmup, LR, seed=20251015,
+                        elbo_out=elbo_w, ws=ws)
+    # the timed loop starts over from the reference init with fresh Adam state
+    params.copy_(reference_init_params(LAYERS, dev))
+    m.zero_()
+    v.zero_()
+    rt.sync()
+    if lib.psvi_debug_set(8, 10):  # PSVI_DBG_LOOP_TIMING: every 10th step
+        raise RuntimeError("psvi_debug_set(PSVI_DBG_LOOP_TIMING) failed")
+    elapsed = rt.timed(lambda: plan.inner_loop(u, z, w, params, m, v, args.steps, LR,
+                                               seed=20251015, offset=args.warmup * eps_stride,
+                                               elbo_out=elbo_t, ws=ws))
+    tm = (ctypes.c_double * 3)()
+    if lib.psvi_debug_loop_timing(tm):
+        raise RuntimeError("psvi_debug_loop_timing failed")
+    lib.psvi_debug_set(8, 0)
+    avg_ms = {"exchange+net": tm[0] * 1e-3, "update": tm[1] * 1e-3}
+    return elapsed, elbo_t, avg_ms, plan.param_count
+
+
+def rows_fraction(loop, layers):
+    """This rank's share of the strict-lower-triangle entries (nnz) of L."""
+    n = [i * o + o for i, o in layers]
+    info = loop.info[loop.rank]
+    nnz_own = 0
+    for l, k in enumerate(n):
+        lo, hi = info["row_lo"][l], info["row_lo"][l] + info["row_cnt"][l]
+        nnz_own += sum(min(r, k - 1) for r in range(lo, hi))
+    return nnz_own / sum((k - 1) * (k - 2) // 2 for k in n)
+
+
+def run(rt, args, shapes=None):
+    """Everything after the process set-up; returns the JSON line's dict on
+    rank 0 (None on the other ranks).  shapes: smaller stand-ins for the
+    configs (CPU rehearsals of the N > 1 control flow under gloo,
+    tests/test_bench_gloo.py); None = the BASELINE configs."""
+    sh = dict(layers=LAYERS, s_per_gpu=S_PER_GPU, M=M, c4={}, c5={})
+    sh.update(shapes or {})
+    world, rank = rt.world, rt.rank
+    S = sh["s_per_gpu"] * world
     if world == 1:
-        lib = plan.lib
-        ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
-        elbo_w = torch.empty(max(args.warmup, 1), dtype=torch.float64, device=dev)
-        elbo_t = torch.empty(args.steps, dtype=torch.float64, device=dev)
-        if args.warmup:
-            plan.inner_loop(u, z, w, params, m, v, args.warmup, LR, seed=20251015,
-                            elbo_out=elbo_w, ws=ws)
-        # the timed loop starts over from the reference init with fresh Adam state
-        params.copy_(reference_init_params(LAYERS, dev))
-        m.zero_()
-        v.zero_()
-        torch.cuda.synchronize()
-        check_rc = lib.psvi_debug_set(8, EV_EVERY)  # PSVI_DBG_LOOP_TIMING
-        if check_rc:
-            raise RuntimeError("psvi_debug_set(PSVI_DBG_LOOP_TIMING) failed")
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        plan.inner_loop(u, z, w, params, m, v, args.steps, LR, seed=20251015,
-                        offset=args.warmup * eps_stride, elbo_out=elbo_t, ws=ws)
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        tm = (ctypes.c_double * 3)()
-        if lib.psvi_debug_loop_timing(tm):
-            raise RuntimeError("psvi_debug_loop_timing failed")
-        lib.psvi_debug_set(8, 0)
-        avg_ms = {"exchange+net": tm[0] * 1e-3, "update": tm[1] * 1e-3}
-        parts = elbo_t[:, None]
+        elapsed, parts, avg_ms, pcount = headline_world1(rt, args)
+        elbo = parts
     else:
-        parts = torch.zeros(total_steps, 2, dtype=torch.float64, device=dev)
-        ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-              for k in range(args.warmup, total_steps) if (k - args.warmup) % EV_EVERY == 0}
-
-        def one_step(k, timed):
-            t = k + 1  # Adam step of one long inner loop (never reset here)
-            e = ev.get(k) if timed else None
-            randn_(eps, seed=20251015, offset=k * eps_stride)
-            if e: e[0].record()
-            loop.phase_sample(eps, params)
-            if e: e[1].record()
-            loop.comm.all_to_all(loop.x_recv, loop.x_shard, loop.x_out, loop.x_in)
-            loop.phase_net(u, z, w)
-            loop.comm.all_to_all(loop.g_shard, loop.g_send, loop.g_out, loop.g_in)
-            if e: e[2].record()
-            loop.phase_update(eps, params, m, v, t, LR, "higher")
-            if e: e[3].record()
-            parts[k].copy_(loop.parts)
-
-        for k in range(args.warmup):
-            one_step(k, False)
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.warmup, total_steps):
-            one_step(k, True)
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        # per-phase device time (HIP events on the launch stream)
-        ph = {"sample": [], "exchange+net": [], "update": []}
-        for e in ev.values():
-            ph["sample"].append(e[0].elapsed_time(e[1]))
-            ph["exchange+net"].append(e[1].elapsed_time(e[2]))
-            ph["update"].append(e[2].elapsed_time(e[3]))
-        avg_ms = {k: sum(x) / len(x) for k, x in ph.items()}
-    elbo = parts.sum(-1)
-    if world > 1:
-        dist.all_reduce(elbo)
+        elapsed, parts, avg_ms, loop = sharded_headline(rt, args.steps, args.warmup,
+                                                        layers=sh["layers"],
+                                                        s_per_gpu=sh["s_per_gpu"], M=sh["M"])
+        elbo = loop.reduce_elbo(parts)
+        pcount = loop.plan.param_count
     finite = bool(torch.isfinite(elbo).all().item())
-
     steps_per_s = args.steps / elapsed
-    value = steps_per_s * (S / S_PER_GPU)
-    upd_s = avg_ms["update"] * 1e-3
+    value = steps_per_s * world   # S = 128 N: N C3 shards per step
+    upd_s = max(avg_ms["update"], 1e-9) * 1e-3
     if world == 1:
         # dominant kernel: the update with the fused next-step sample (plus its
         # small slot-reduce kernel, inside the same event pair)
         wk = algorithmic_work_fused(S)
-        hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
         kname = ("mvn_stream_kernel (fused update + next-step sample, tiled state) + "
                  "mvn_fwd_reduce_kernel")
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
     else:
-        work = algorithmic_work(S, rows_frac)
+        work = algorithmic_work(S, rows_fraction(loop, sh["layers"]), sh["layers"])
         wk = work["update"]
-        hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
         kname = "mvn_update_kernel"
-        smp_s = avg_ms["sample"] * 1e-3
+        smp_s = max(avg_ms["sample"], 1e-9) * 1e-3
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
                    "mvn_fwd_kernel+reduce": dict(avg_us=avg_ms["sample"] * 1e3,
                                                  tflops=work["sample"]["flops"] / smp_s / 1e12),
                    "net_kernel(+exchange)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
+    hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
     if hbm_s >= mfma_s:
         roofline = dict(bound="hbm", achieved=round(wk["bytes"] / upd_s / 1e9, 1),
                         peak=HBM_PEAK_GBS, unit="GB/s")
@@ -579,15 +653,14 @@ def main():
     # the whole inner step's algorithmic work at C3 (2.682 GFLOP,
     # 134.7 MB per S = 128 shard) against the fp32 MFMA peak -- the step's roofline
     # fraction, beside the dominant kernel's own above
-    step_floor_us = 2.682e9 * (S / S_PER_GPU) / world / (FP32_MFMA_PEAK_TFLOPS * 1e12) * 1e6
+    step_floor_us = 2.682e9 / (FP32_MFMA_PEAK_TFLOPS * 1e12) * 1e6
     step_roofline = dict(bound="mfma (ridge: HBM 16.8 us / MFMA 17.05 us per C3 shard)",
-                         algorithmic_gflop_per_gpu=round(2.682 * S / S_PER_GPU / world, 3),
-                         floor_us=round(step_floor_us, 2),
+                         algorithmic_gflop_per_gpu=2.682, floor_us=round(step_floor_us, 2),
                          frac=round(step_floor_us / (elapsed / args.steps * 1e6), 4))
-    log(f"headline: {args.steps / elapsed:.1f} steps/s; C4 line")
+    log(f"headline: {steps_per_s:.1f} steps/s; C4 line")
     c4 = None
     if not args.no_c4:
-        c4 = c4_timings(dev, world, rank)
+        c4 = c4_timings(rt, **sh["c4"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline")
@@ -595,43 +668,94 @@ def main():
     c2 = None
     if rank == 0 and world == 1 and not args.no_c2:
         log("C2 line")
-        c2 = c2_timings(dev, cpu=not args.no_cpu_baseline)
+        c2 = c2_timings(rt.dev, cpu=not args.no_cpu_baseline)
     trainers = None
     if rank == 0 and world == 1 and not args.no_trainers:
         log("trainers")
-        trainers = trainer_timings(dev, cpu=not args.no_cpu_baseline)
+        trainers = trainer_timings(rt.dev, cpu=not args.no_cpu_baseline)
     lenet = None
-    if rank == 0 and world == 1 and not args.no_lenet:
+    if not args.no_lenet:
+        # every rank takes part at N > 1 (C5 is an 8-GPU config: samples sharded)
         log("C5 lenet")
-        lenet = lenet_timings(dev, cpu=not args.no_cpu_baseline)
+        lenet = lenet_timings(rt, cpu=not args.no_cpu_baseline, **sh["c5"])
+    rt.barrier()
+    if rank != 0:
+        return None
+    return {
+        "metric": "ELBO inner-steps/sec (S MC samples x M pseudopoints) at 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "inner-steps/s (S=128 x M=100 fn2 C3 shards; S = 128 x n_gpus)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (make_synthetic-shaped X~N(0,I64), Bernoulli labels; reference init)",
+        "config": {"workload": "C3 fn2 full-cov MLP 64-40-40-2 per GPU (C4 sample count at 8 GPUs)",
+                   "S_total": S, "S_per_gpu": sh["s_per_gpu"], "M": sh["M"], "D": 64, "H": 40,
+                   "C": 2, "params": pcount,
+                   "parallelism": f"rows-of-L x samples sharded over {world}",
+                   "comm": getattr(rt.comm, "name", None) if world > 1 else None,
+                   "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite},
+        "roofline": roofline,
+        "step_roofline": step_roofline,
+        "cpu_baseline": cpu,
+        ("c4_1gpu" if world == 1 else "c4"): c4,
+        "c2": c2,
+        "trainers": trainers,
+        "lenet_c5": lenet,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-lenet", action="store_true",
+                    help="skip the auxiliary C5 (lenet) inner-step / HVP / hyper_step timing")
+    ap.add_argument("--no-trainers", action="store_true",
+                    help="skip the auxiliary outer-step (trainer) timings")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the auxiliary C4 (S=1024, M=200) strong-scaling line")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="skip the auxiliary C2 (fn, S=32, M=50) line")
+    ap.add_argument("--comm", choices=("rccl", "gloo"), default="rccl",
+                    help="N > 1 collectives: RCCL (torch.distributed 'nccl'), or gloo with "
+                         "host staging (a rehearsal of the N > 1 control flow, not a measurement)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on device 0 (rehearsing N ranks on a one-GPU box; "
+                         "needs --comm gloo)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.share_gpu and args.comm != "gloo":
+        raise SystemExit("--share-gpu needs --comm gloo (RCCL takes one rank per GPU)")
+    dev = torch.device("cuda", 0 if args.share_gpu else local)
+    torch.cuda.set_device(dev)
+    comm = None
     if world > 1:
-        dist.barrier()
-    if rank == 0:
-        out = {
-            "metric": "ELBO inner-steps/sec (S MC samples x M pseudopoints) at 1/2/4/8 GPU",
-            "value": round(value, 2),
-            "unit": "inner-steps/s (S=128 x M=100 fn2 C3 shards; S = 128 x n_gpus)",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (make_synthetic-shaped X~N(0,I64), Bernoulli labels; reference init)",
-            "config": {"workload": "C3 fn2 full-cov MLP 64-40-40-2 per GPU (C4 sample count at 8 GPUs)",
-                       "S_total": S, "S_per_gpu": S_PER_GPU, "M": M, "D": 64, "H": 40, "C": 2,
-                       "params": plan.param_count, "parallelism": f"rows-of-L x samples sharded over {world}",
-                       "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite},
-            "roofline": roofline,
-            "step_roofline": step_roofline,
-            "cpu_baseline": cpu,
-            ("c4_1gpu" if world == 1 else "c4"): c4,
-            "c2": c2,
-            "trainers": trainers,
-            "lenet_c5": lenet,
-        }
+        import torch.distributed as dist
+        from psvi.runtime.sharded import HostStagedComm, TorchDistComm
+
+        if args.comm == "rccl":
+            dist.init_process_group("nccl", device_id=dev)
+            comm = TorchDistComm()
+        else:
+            dist.init_process_group("gloo")
+            comm = HostStagedComm()
+    rt = Runtime(dev, world, rank, comm)
+    out = run(rt, args)
+    if out is not None:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -61,6 +61,8 @@ trainers carry the hypergradients of u, v and alpha themselves.  Soft labels
 
 There is no CPU fallback: a missing libpsvi_hip.so or GPU raises.
 """
+import contextlib
+import functools
 import time
 
 import torch
@@ -186,6 +188,15 @@ class HipOuterRowsELBO(torch.autograd.Function):
                 None, None, None, None, None)
 
 
+def _trainer_step(fn):
+    """One outer step of a trainer (PSVI._outer_step's scope)."""
+    @functools.wraps(fn)
+    def run(self, *args, **kwargs):
+        with self._outer_step():
+            return fn(self, *args, **kwargs)
+    return run
+
+
 class PSVI:
     """Pseudodata (coreset) VI with fixed rescaled coefficients v = 1/M
     (psvi_classes.py:83).  Keyword names follow the reference; arguments that
@@ -238,7 +249,9 @@ class PSVI:
         self.v.requires_grad_(self.learn_v)
         self._plans = {}
         self._eps_offset = 0
+        self._eps_feed, self._eps_short = None, False
         self._labels_ok = None
+        self._label_flag, self._label_C, self._defer_labels = None, None, False
         # samples split over `world` ranks (one process per GPU):
         # every objective / HVP sums the ranks' shares with one all-reduce
         self.world, self.rank = int(world), int(rank)
@@ -314,11 +327,44 @@ class PSVI:
             raise ValueError(f"class ids must lie in [0, {C})")
         self._labels_ok = key
 
-    @staticmethod
-    def _batch_labels(y, C):
-        """Minibatch labels as int32 on the device, without a host read: out-of-
-        range ids are clamped for memory safety (the loaders hand out class ids)."""
-        return y.reshape(-1).to(torch.int32).clamp_(0, C - 1).contiguous()
+    def _batch_labels(self, y, C):
+        """Minibatch labels as int32 on the device.  Ids outside [0, C) (or
+        non-integral float ids) raise ValueError as the reference's
+        Categorical.log_prob does: a device-side flag is formed here (the ids
+        are clamped only so the kernels never read out of bounds) and read on
+        the host once -- at once per outer step inside the trainers (before any
+        hyperparameter moves), at once per call otherwise."""
+        yi = y.reshape(-1)
+        bad = (yi < 0) | (yi >= C)
+        if yi.is_floating_point():
+            bad = bad | (yi != yi.round())
+        flag = bad.any()
+        self._label_flag = flag if self._label_flag is None else (self._label_flag | flag)
+        self._label_C = C
+        if not self._defer_labels:
+            self._raise_bad_labels()
+        return yi.to(torch.int32).clamp_(0, C - 1).contiguous()
+
+    def _raise_bad_labels(self):
+        """The one host read of the accumulated minibatch-label flag."""
+        f, self._label_flag = self._label_flag, None
+        if f is not None and bool(f):
+            raise ValueError(f"minibatch class ids must lie in [0, {self._label_C})")
+
+    @contextlib.contextmanager
+    def _outer_step(self):
+        """Scope of one trainer step: minibatch-label checks are deferred to
+        _raise_bad_labels (called before the hyperparameter steps) and a replay
+        feed that the step did not use up is dropped, not served later."""
+        prev = self._defer_labels
+        self._defer_labels = True
+        try:
+            yield
+        finally:
+            self._defer_labels = prev
+            self._eps_feed = None
+        if not prev:
+            self._raise_bad_labels()
 
     def _data(self, plan):
         """(u, z, w) of the inner objective's rows: the pseudopoints, or for
@@ -372,11 +418,12 @@ class PSVI:
 
         fam, layers, prior_sd, S = model_spec(model)
         key = ("rows", fam, tuple(layers), S, plan.M, prior_sd)
-        if key not in self._plans:
-            self._plans[key] = self._new_plan(fam, layers, S, plan.M, prior_sd, outer=True)
-        op = self._plans[key]
 
         def fn():
+            # built on the first backward that asks for d/du or d/dw, not per objective
+            if key not in self._plans:
+                self._plans[key] = self._new_plan(fam, layers, S, plan.M, prior_sd, outer=True)
+            op = self._plans[key]
             one = torch.ones(S, dtype=torch.float64)
             zero = torch.zeros(S, dtype=torch.float64)
             if isinstance(op, ShardedOuter):
@@ -420,14 +467,16 @@ class PSVI:
         to replay the reference's own draws through code that calls
         inner_elbo / psvi_elbo itself (the functional inner loop)."""
         self._eps_feed = iter(list(draws))
+        self._eps_short = False
 
     def _draw_eps(self, plan):
-        feed = getattr(self, "_eps_feed", None)
+        feed = self._eps_feed
         if feed is not None:
             e = next(feed, None)
             if e is not None:
                 return e.to(self.device, torch.float32).reshape(-1).contiguous()
             self._eps_feed = None
+            self._eps_short = True   # asked for more draws than were replayed
         eps = torch.empty(plan.eps_count, device=self.device)
         randn_(eps, self.seed, self._eps_offset)
         self._eps_offset += plan.eps_stride  # Philox offsets move in quads
@@ -561,7 +610,7 @@ class PSVI:
         C = layers[-1][1]
         Mu = int(self.u.shape[0])
         R0 = Mu + Nx
-        key = ("soft-outer", fam, tuple(layers), S, R0 * C)
+        key = ("soft-outer", fam, tuple(layers), S, R0 * C, model_spec(model)[2])
         if key not in self._plans:
             self._plans[key] = self._new_plan(fam, layers, S, R0 * C, model_spec(model)[2],
                                               outer=True)
@@ -605,6 +654,7 @@ class PSVI:
             vp = list(self.model.parameters()) + [self.u] + ([self.v] if self.learn_v else [])
             self.optim = torch.optim.Adam(vp, lr0joint)
 
+    @_trainer_step
     def joint_step(self, xbatch, ybatch):
         """psvi_classes.py:517-525: one Adam step on the outer objective over
         the network, u (and v)."""
@@ -614,9 +664,11 @@ class PSVI:
             if self.register_elbos:
                 self.elbos.append((2, -loss.item()))
         loss.backward()
+        self._raise_bad_labels()
         self.optim.step()
         return loss
 
+    @_trainer_step
     def alternating_step(self, xbatch, ybatch):
         """psvi_classes.py:527-539: a step of optim_net, then of optim_u, each
         on a fresh evaluation of the outer objective."""
@@ -629,6 +681,7 @@ class PSVI:
                     self.elbos.append((1, -loss.item())) if i == 1 else self.elbos.append(
                         (0, -loss.item()))
             loss.backward()
+            self._raise_bad_labels()
             self.optim.step()
         return loss
 
@@ -730,6 +783,7 @@ class PSVI:
         (unless u is frozen), optim_v (learn_v; clamped at 0 unless
         parameterised) and optim_alpha (psvi_classes.py:585-591, 676-681,
         1576-1579, 1610-1612, 1650-1651, 1843-1845, 1873-1875)."""
+        self._raise_bad_labels()
         if self._learn_u:
             self._add_grad(self.u, u_grad)
             self.optim_u.step()
@@ -792,6 +846,7 @@ class PSVI:
                                          grad=grads, grad_u=grads, grad_w=grads)
         return oplan, f
 
+    @_trainer_step
     def hyper_step(self, xbatch, ybatch, T=50, inner_opt_class=None, K=30, linsys_lr=1e-4,
                    hypergrad_approx="CG_normaleq", eps_inner=None, eps_outer=None, **kwargs):
         """psvi_classes.py:602-687 with hypergrad's CG_normaleq
@@ -914,6 +969,7 @@ class PSVI:
         self._cg_x = xk
         return eA
 
+    @_trainer_step
     def nested_step(self, xbatch, ybatch, truncated=False, K=5, eps_inner=None, eps_outer=None):
         """psvi_classes.py:541-600 (and the variants' overrides, 1583-1620,
         1631-1657, 1852-1884): T = self.inner_it higher-Adam steps on the inner
@@ -925,9 +981,14 @@ class PSVI:
         optional replay of the reference's draws; default this instance's
         Philox stream."""
         if truncated or self.learn_z:
-            if eps_inner is not None or eps_outer is not None:
+            replay = eps_inner is not None or eps_outer is not None
+            if replay:
                 self.replay_eps(list(eps_inner or []) + list(eps_outer or []))
-            return self._nested_step_unrolled(xbatch, ybatch, truncated, K)
+            out = self._nested_step_unrolled(xbatch, ybatch, truncated, K)
+            if replay and (self._eps_short or next(self._eps_feed or iter(()), None) is not None):
+                raise ValueError("eps_inner / eps_outer do not hold exactly the draws the step "
+                                 "consumed")
+            return out
         self._zero_hparam_grads()
         self.optim_net.zero_grad()
         model = self.model

@@ -29,6 +29,9 @@ from .engine import InnerLoopPlan, adam_update_, randn_
 class TorchDistComm:
     """Collectives on torch.distributed (backend 'nccl' == RCCL on ROCm)."""
 
+    name = "rccl"
+    host_staged = False
+
     def __init__(self, group=None):
         import torch.distributed as dist
 
@@ -40,6 +43,27 @@ class TorchDistComm:
 
     def all_reduce(self, t):
         self.dist.all_reduce(t, group=self.group)
+
+
+class HostStagedComm(TorchDistComm):
+    """The same collectives over a gloo process group with device tensors
+    staged through host memory (gloo has no device all_to_all).  For
+    rehearsing the N > 1 control flow -- several ranks sharing one GPU, or
+    CPU tensors -- not for measurements: RCCL (TorchDistComm) is the product
+    transport."""
+
+    name = "gloo (host-staged)"
+    host_staged = True
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        self.dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+        out.copy_(o)
+
+    def all_reduce(self, t):
+        h = t.cpu()
+        self.dist.all_reduce(h, group=self.group)
+        t.copy_(h)
 
 
 class ShardedInnerLoop:

@@ -140,3 +140,116 @@ def test_wider_meanfield():
 def test_wide_fullcov_layer():
     # a single wide full-cov layer (n = 1300): many forward split-K items per row tile
     check("fullcov", [(64, 20)], S=64, M=40, seed=11)
+
+
+def test_meanfield_largest_s():
+    """The mean-field plan at the largest sample count it takes (the outer
+    objective's S <= 2048): its plan-owned gradient slots (S x pseudopoint
+    chunks x n_tot floats) are allocated and summed in order, one step vs the
+    oracle."""
+    check("meanfield", [(64, 64), (64, 10)], S=2048, M=200, seed=13)
+
+
+def _offs(splits):
+    return np.concatenate([[0], np.cumsum(splits)]).astype(int)
+
+
+def test_c4_row_sharded_world8_full_size():
+    """C4 as the scaling run executes it: fn2 64-40-40-2, S = 1024, M = 200,
+    rows of L x samples sharded over 8 ranks (nnz-balanced row split over
+    n = 2600 / 1640 / 82, all_to_all split sizes at S = 1024, the chunked update
+    at K = 1024), the 8 ranks run in one process with the two all_to_alls done
+    as device copies of the same blocks.  Checked against world 1 on the same
+    inputs (ELBO, assembled gradient, one Adam step) and against the oracle
+    (each rank's x shard; the gradient from the exchanged G)."""
+    from psvi.runtime import InnerLoopPlan
+    from psvi.runtime.sharded import ShardedInnerLoop
+
+    layers, S, M, W = [(64, 40), (40, 40), (40, 2)], 1024, 200, 8
+    params, u, z, w, eps = make_case("fullcov", layers, S, M, 3)
+    t = lambda x, d=torch.float32: torch.tensor(x, dtype=d, device=DEV)
+    du, dz, dw, de = t(u), t(z, torch.int32), t(w), t(eps)
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    xs1 = torch.empty(plan.xshard_count, device=DEV)
+    gs1 = torch.empty(plan.xshard_count, device=DEV)
+    nll1 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    kl1 = torch.zeros(1, dtype=torch.float64, device=DEV)
+    g1 = torch.empty(plan.param_count, device=DEV)
+    plan.mvn_sample(de, t(params), xs1)
+    plan.mvn_net(du, dz, dw, xs1, gs1, nll1)
+    plan.mvn_update(de, gs1, t(params), grad_out=g1, kl_out=kl1)
+    p1 = t(params)
+    m1, v1 = torch.zeros_like(p1), torch.zeros_like(p1)
+    e1 = plan.inner_step(du, dz, dw, de, p1, m1, v1, step=1, lr=1e-3)
+
+    loops = [ShardedInnerLoop("fullcov", layers, S, M, W, r) for r in range(W)]
+    info = loops[0].info
+    n_l = [a * b + b for a, b in layers]
+    assert sum(i["s_count"] for i in info) == S and [i["s_offset"] for i in info] == \
+        [r * S // W for r in range(W)]
+    for l, n in enumerate(n_l):   # the row shards tile every layer
+        los = [i["row_lo"][l] for i in info]
+        cnt = [i["row_cnt"][l] for i in info]
+        assert los[0] == 0 and all(los[r] + cnt[r] == los[r + 1] for r in range(W - 1))
+        assert los[-1] + cnt[-1] == n
+    for r in range(W):            # all_to_all split sizes agree pairwise
+        for q in range(W):
+            assert loops[r].x_in[q] == loops[q].x_out[r]
+            assert loops[r].g_in[q] == loops[q].g_out[r]
+    # sample phase: each rank's rows of x for all S samples vs the oracle
+    dp = t(params)
+    Xo = np.concatenate([xl for xl in _oracle_x(layers, params, eps, S)], 1)
+    woff = _offs(n_l)
+    for r in range(W):
+        loops[r].phase_sample(de, dp)
+        X = loops[r].x_shard.view(S, -1).cpu().numpy().astype(np.float64)
+        c = 0
+        for l in range(len(layers)):
+            lo, cnt = info[r]["row_lo"][l], info[r]["row_cnt"][l]
+            assert l2rel(X[:, c:c + cnt], Xo[:, woff[l] + lo:woff[l] + lo + cnt]) < 1e-6
+            c += cnt
+    # x exchange, network, G exchange, gradient mode of the update
+    for r in range(W):
+        parts = [loops[p].x_shard[_offs(loops[p].x_in)[r]:_offs(loops[p].x_in)[r + 1]]
+                 for p in range(W)]
+        loops[r].x_recv.copy_(torch.cat(parts))
+    for r in range(W):
+        loops[r].phase_net(du, dz, dw)
+    for p in range(W):
+        parts = [loops[q].g_send[_offs(loops[q].g_in)[p]:_offs(loops[q].g_in)[p + 1]]
+                 for q in range(W)]
+        loops[p].g_shard.copy_(torch.cat(parts))
+    grads = []
+    for r in range(W):
+        g = torch.zeros(plan.param_count, device=DEV)
+        loops[r].phase_update(de, dp, None, None, 1, 1e-3, "higher", grad_out=g)
+        grads.append(g)
+    masks = [l.owned_mask() for l in loops]
+    assert int(torch.stack(masks).sum(0).min()) == 1 and int(torch.stack(masks).sum(0).max()) == 1
+    g8 = sum(grads[r] * masks[r] for r in range(W))
+    negelbo8 = sum(l.parts.sum().item() for l in loops)
+    assert rel(negelbo8, (nll1 + kl1).item()) < 1e-6
+    assert_grad_close(g8.cpu().numpy(), g1.cpu().numpy(), l2tol=1e-5,
+                      what="C4 world 8 vs world 1")
+    # the oracle gradient from the exchanged G (every rank's own rows)
+    G = np.zeros((S, woff[-1]))
+    for r in range(W):
+        Gs = loops[r].g_shard.view(S, -1).cpu().numpy().astype(np.float64)
+        c = 0
+        for l in range(len(layers)):
+            lo, cnt = info[r]["row_lo"][l], info[r]["row_cnt"][l]
+            G[:, woff[l] + lo:woff[l] + lo + cnt] = Gs[:, c:c + cnt]
+            c += cnt
+    go = O.mvn_grad_from_G(layers, params, G, eps, S)
+    assert_grad_close(g8.cpu().numpy(), go, l2tol=1e-5, what="C4 world 8 vs oracle")
+    # one fused Adam step per rank == world 1
+    ps = [t(params) for _ in range(W)]
+    ms = [torch.zeros_like(ps[0]) for _ in range(W)]
+    vs = [torch.zeros_like(ps[0]) for _ in range(W)]
+    from test_hip_parity import _emulated_sharded_step
+
+    e8 = _emulated_sharded_step(loops, du, dz, dw, de, ps, ms, vs, 1, 1e-3, "higher")
+    assert rel(e8, e1.item()) < 1e-6
+    full = sum(ps[r] * masks[r] for r in range(W))
+    assert l2rel(full.cpu().numpy(), p1.cpu().numpy()) < 1e-7
+    assert (full - p1).abs().max().item() < 1e-5

@@ -303,3 +303,54 @@ def test_noiw_rows_reproduce_the_broadcast_objective():
     assert du.shape == (7, 2) and torch.all(du == 3)
     byclass = torch.arange(21.0).reshape(7, 3).sum(0)
     assert torch.equal(dw, byclass[ps.z.long()])
+
+
+def test_minibatch_labels_out_of_range_raise():
+    """psvi_elbo / the trainers take class ids in [0, C) as the reference's
+    Categorical.log_prob does: ids outside that range (1-based, -1, or
+    non-integral floats) raise ValueError instead of being clamped onto
+    another class.  Outside a trainer the flag is read at the call; inside one
+    it is read once per outer step (before the hyperparameters move)."""
+    ps = _variant("PSVILearnV", M=6, C=3)
+    x = torch.randn(5, 2)
+    for bad in (torch.tensor([0, 1, 2, 3, 1]), torch.tensor([-1, 0, 1, 2, 0]),
+                torch.tensor([0.0, 1.5, 2.0, 1.0, 0.0])):
+        with pytest.raises(ValueError, match=r"\[0, 3\)"):
+            ps._outer_rows(x, bad, 3)
+    xb, yb, wd = ps._outer_rows(x, torch.tensor([0, 1, 2, 2, 1]), 3)
+    assert yb.dtype == torch.int32 and yb.tolist() == [0, 1, 2, 2, 1]
+    assert torch.allclose(wd, torch.full((5,), ps.N / 5.0))
+    # deferred inside a trainer step: no read until the step ends, then it raises
+    with pytest.raises(ValueError, match=r"\[0, 3\)"):
+        with ps._outer_step():
+            ps._outer_rows(x, torch.tensor([0, 1, 4, 2, 1]), 3)
+            ps._outer_rows(x, torch.tensor([0, 1, 2, 2, 1]), 3)   # flag stays set
+            assert ps._label_flag is not None
+    assert ps._label_flag is None
+    with ps._outer_step():                                        # a clean step
+        ps._outer_rows(x, torch.tensor([2, 1, 0, 2, 1]), 3)
+    assert ps._label_flag is None
+
+
+def test_replay_feed_does_not_outlive_a_trainer_step():
+    """A replay feed left unconsumed by a trainer step is dropped when the
+    step ends (never served to later objective calls)."""
+    ps = _variant("PSVILearnV", M=6, C=3)
+    ps.replay_eps([torch.zeros(3), torch.ones(3)])
+    with ps._outer_step():
+        assert ps._eps_feed is not None
+    assert ps._eps_feed is None
+
+
+def test_plan_keys_carry_prior_sd():
+    """Plans are cached per (family, layers, S, M, prior_sd): two models that
+    differ only in prior_sd never share one (the soft-label outer plan too)."""
+    import inspect
+
+    from psvi.inference import psvi_classes as PC
+
+    src = inspect.getsource(PC.PSVI._soft_psvi_elbo)
+    assert '"soft-outer", fam, tuple(layers), S, R0 * C, model_spec(model)[2]' in src
+    src = inspect.getsource(PC.PSVI._row_grad_fn)
+    # the rows plan is built on first use inside the backward, not per objective
+    assert src.index("def fn()") < src.index("self._new_plan(")
