@@ -469,12 +469,16 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
 #pragma unroll
                     for (int k = 0; k < kB; ++k) {
                         const int r = base + k * (int)blockDim.x;
+                        // only this source's rows [lo, hi): a source whose run ends
+                        // inside the weights must not write its clamped tail value
+                        // into rows another source's scatter owns (world > 1)
+                        if (r >= hi) continue;
                         if (r < nw) {
                             // exact for r < 2^21: (r + 0.5) / din is >= 0.5/din from an integer
                             const int j = (int)(((float)r + 0.5f) * rdin), i = r - j * din;
                             W[j * ldw + i] = v[k];
                             if (wt) WT[i * ldwt + j] = v[k];
-                        } else if (r < hi) {
+                        } else {
                             Bv[r - nw] = v[k];
                         }
                     }

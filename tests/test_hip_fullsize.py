@@ -154,18 +154,20 @@ def _offs(splits):
     return np.concatenate([[0], np.cumsum(splits)]).astype(int)
 
 
-def test_c4_row_sharded_world8_full_size():
-    """C4 as the scaling run executes it: fn2 64-40-40-2, S = 1024, M = 200,
-    rows of L x samples sharded over 8 ranks (nnz-balanced row split over
-    n = 2600 / 1640 / 82, all_to_all split sizes at S = 1024, the chunked update
-    at K = 1024), the 8 ranks run in one process with the two all_to_alls done
-    as device copies of the same blocks.  Checked against world 1 on the same
+@pytest.mark.parametrize("W,S,M", [(8, 1024, 200), (2, 256, 100), (4, 512, 100), (8, 1024, 100)])
+def test_row_sharded_full_size(W, S, M):
+    """The full-cov steps the scaling run executes: C4 (fn2 64-40-40-2,
+    S = 1024, M = 200) over 8 ranks, and the weak-scaled headline (C3 shards:
+    S = 128 W, M = 100) at W = 2, 4, 8 -- rows of L x samples sharded
+    (nnz-balanced row split over n = 2600 / 1640 / 82, all_to_all split sizes,
+    the chunked update at K = S), the W ranks run in one process with the two
+    all_to_alls done as device copies of the same blocks.  Checked against world 1 on the same
     inputs (ELBO, assembled gradient, one Adam step) and against the oracle
     (each rank's x shard; the gradient from the exchanged G)."""
     from psvi.runtime import InnerLoopPlan
     from psvi.runtime.sharded import ShardedInnerLoop
 
-    layers, S, M, W = [(64, 40), (40, 40), (40, 2)], 1024, 200, 8
+    layers = [(64, 40), (40, 40), (40, 2)]
     params, u, z, w, eps = make_case("fullcov", layers, S, M, 3)
     t = lambda x, d=torch.float32: torch.tensor(x, dtype=d, device=DEV)
     du, dz, dw, de = t(u), t(z, torch.int32), t(w), t(eps)
@@ -227,11 +229,11 @@ def test_c4_row_sharded_world8_full_size():
     masks = [l.owned_mask() for l in loops]
     assert int(torch.stack(masks).sum(0).min()) == 1 and int(torch.stack(masks).sum(0).max()) == 1
     g8 = sum(grads[r] * masks[r] for r in range(W))
-    negelbo8 = sum(l.parts.sum().item() for l in loops)
-    assert rel(negelbo8, (nll1 + kl1).item()) < 1e-6
-    assert_grad_close(g8.cpu().numpy(), g1.cpu().numpy(), l2tol=1e-5,
-                      what="C4 world 8 vs world 1")
-    # the oracle gradient from the exchanged G (every rank's own rows)
+    nll8 = sum(l.parts[0].item() for l in loops)
+    kl8 = sum(l.parts[1].item() for l in loops)
+    print(f"world {W}: nll {nll8!r} kl {kl8!r}; world 1: nll {nll1.item()!r} kl {kl1.item()!r}")
+    assert rel(kl8, kl1.item()) < 1e-6
+    # the exchanged G (every rank's own rows, all samples) vs world 1's G
     G = np.zeros((S, woff[-1]))
     for r in range(W):
         Gs = loops[r].g_shard.view(S, -1).cpu().numpy().astype(np.float64)
@@ -240,8 +242,28 @@ def test_c4_row_sharded_world8_full_size():
             lo, cnt = info[r]["row_lo"][l], info[r]["row_cnt"][l]
             G[:, woff[l] + lo:woff[l] + lo + cnt] = Gs[:, c:c + cnt]
             c += cnt
+    G1 = gs1.view(S, -1).cpu().numpy().astype(np.float64)
+    assert rel(nll8, nll1.item()) < 1e-6
+    # x differs from world 1 in the last bits (the sample phase's split-K items
+    # follow the row shards), so a sample on a ReLU kink may take the other
+    # mask: such samples must be near-kink and rare, every other sample's G
+    # equal to world 1's (as test_c4_fn2_phasewise_single_gpu vs the oracle)
+    per = np.linalg.norm(G - G1, axis=1) / np.maximum(np.linalg.norm(G1, axis=1), 1e-30)
+    bad = np.where(per > 1e-4)[0]
+    X1 = xs1.view(S, -1).cpu().numpy().astype(np.float64)
+    Ws, bs = O.mvn_split_x(layers, X1)
+    marg = O.relu_margin(u.astype(np.float64), Ws, bs)
+    print(f"W={W} S={S} M={M}: {len(bad)} kink samples {bad[:8]} margins {marg[bad][:8]}")
+    assert len(bad) <= 0.01 * S, f"{len(bad)} samples off"
+    assert np.all(marg[bad] < 1e-4), (bad, marg[bad])
+    good = np.setdiff1d(np.arange(S), bad)
+    assert l2rel(G[good], G1[good]) < 1e-6
+    if len(bad) == 0:
+        assert_grad_close(g8.cpu().numpy(), g1.cpu().numpy(), l2tol=1e-5,
+                          what="world W vs world 1")
+    # the oracle gradient from the exchanged G (every rank's own rows)
     go = O.mvn_grad_from_G(layers, params, G, eps, S)
-    assert_grad_close(g8.cpu().numpy(), go, l2tol=1e-5, what="C4 world 8 vs oracle")
+    assert_grad_close(g8.cpu().numpy(), go, l2tol=1e-5, what=f"world {W} vs oracle")
     # one fused Adam step per rank == world 1
     ps = [t(params) for _ in range(W)]
     ms = [torch.zeros_like(ps[0]) for _ in range(W)]
@@ -251,5 +273,4 @@ def test_c4_row_sharded_world8_full_size():
     e8 = _emulated_sharded_step(loops, du, dz, dw, de, ps, ms, vs, 1, 1e-3, "higher")
     assert rel(e8, e1.item()) < 1e-6
     full = sum(ps[r] * masks[r] for r in range(W))
-    assert l2rel(full.cpu().numpy(), p1.cpu().numpy()) < 1e-7
-    assert (full - p1).abs().max().item() < 1e-5
+    assert l2rel(full.cpu().numpy(), p1.cpu().numpy()) < (1e-7 if len(bad) == 0 else 1e-5)
