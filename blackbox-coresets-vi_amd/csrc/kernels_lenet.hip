@@ -25,6 +25,7 @@
 namespace psvi {
 
 int g_lenet_gemm_valu = 0;  // psvi_debug_set(PSVI_DBG_LENET_GEMM_VALU, 1): the VALU head GEMM (A/B)
+int g_lenet_conv_valu = 0;  // psvi_debug_set(PSVI_DBG_LENET_CONV_VALU, 1): the VALU conv towers (A/B)
 
 namespace {
 
@@ -249,6 +250,172 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
             const float v = relu_pool4(acc[0], acc[1], acc[2], acc[3], r);
             a.x2[row * kX2 + o] = v;
             a.r2[row * kX2 + o] = r;
+        }
+    }
+}
+
+// ------------------------------------- conv towers, fwd, on the matrix cores
+// Both convolutions as implicit GEMMs on v_mfma_f32_16x16x4_f32 (fp32 in,
+// fp32 accumulate: an ordered fmaf chain per output, bias in the accumulator).
+// Fragment maps (16x16x4 f32): A[row l & 15][k l >> 4], B[k l >> 4][col l & 15],
+// C/D col l & 15, rows 4 (l >> 4) + i (i = 0..3).  Rows are ordered (pool
+// window, window offset q = 2 dy + dx), so a lane's four accumulators are the
+// four conv values of ONE 2x2 pool window: relu + first-max pool run in the
+// epilogue on registers (window order (0,0) (0,1) (1,0) (1,1), as relu_pool4).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// conv1 (1 -> 6, 5x5, pad 2) of one image for 8 samples at once: the image's
+// im2col [784 conv positions x 25 taps] (padded image in LDS) times the 8
+// samples' filters [25 taps x 48 (sample, channel) columns] -- the image is
+// shared by every sample (VIConv2d's grouped conv over the S-repeated input,
+// neural_net.py:202-246), so one A fragment feeds three column tiles.  K = 25
+// padded to 28 (B rows 25..27 are zero).  49 row tiles of 16 (4 windows x 4
+// offsets) per image, dealt to the 4 waves.
+constexpr int kC1S = 8;           // samples per workgroup (48 columns)
+constexpr int kC1RS = 38;         // padded-image row stride (ds_read_b32 banks: tools/lds_banks)
+constexpr int kC1Img = 32 * kC1RS;
+__global__ __launch_bounds__(256) void lenet_conv1_mfma_kernel(ConvArgs a, int S_loc) {
+    __shared__ float img[2][kC1Img];
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    const int s0 = blockIdx.y * kC1S;
+    const int r16 = lane & 15, kq = lane >> 4;
+    // B fragments and the accumulators' bias: column n = 16 nt + r16 is
+    // (sample s0 + n / 6, channel n % 6)
+    float bf[3][7], bias[3];
+    bool col_ok[3];
+    int64_t col_out[3];
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) {
+        const int n = 16 * nt + r16, sl = n / 6, c = n % 6;
+        col_ok[nt] = s0 + sl < S_loc;
+        const float* ws = a.wsamp + (int64_t)min(s0 + sl, S_loc - 1) * a.n_tot;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int k = 4 * t + kq;
+            bf[nt][t] = (k < 25 && col_ok[nt]) ? ws[c * 25 + k] : 0.f;
+        }
+        bias[nt] = ws[150 + c];
+        col_out[nt] = (int64_t)(s0 + sl) * a.M * kP1 + c * 196;
+    }
+    // A fragment: tap k = 4 t + kq -> (i, j) offset in the padded image
+    int koff[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        const int k = min(4 * t + kq, 24);
+        koff[t] = (k / 5) * kC1RS + k % 5;
+    }
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    auto load_img = [&](int m, float* dst) __attribute__((always_inline)) {
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 1024; i += 256) {
+            const int y = (i >> 5) - 2, x = (i & 31) - 2;
+            dst[(i >> 5) * kC1RS + (i & 31)] =
+                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+        }
+    };
+    if (m0 < m1) load_img(m0, img[0]);
+    int buf = 0;
+    for (int m = m0; m < m1; ++m, buf ^= 1) {
+        __syncthreads();  // img[buf] complete; img[buf ^ 1] free
+        if (m + 1 < m1) load_img(m + 1, img[buf ^ 1]);
+        const float* im = img[buf];
+        for (int mt = wv; mt < 49; mt += 4) {
+            // this lane's A row: window g = 4 mt + r16 / 4, offset q = r16 % 4
+            const int g = 4 * mt + (r16 >> 2), q = r16 & 3;
+            const int rowoff = (2 * (g / 14) + (q >> 1)) * kC1RS + 2 * (g % 14) + (q & 1);
+            f32x4 acc[3];
+#pragma unroll
+            for (int nt = 0; nt < 3; ++nt) acc[nt] = f32x4{bias[nt], bias[nt], bias[nt], bias[nt]};
+            float av[7];
+#pragma unroll
+            for (int t = 0; t < 7; ++t) av[t] = im[rowoff + koff[t]];
+#pragma unroll
+            for (int t = 0; t < 7; ++t)
+#pragma unroll
+                for (int nt = 0; nt < 3; ++nt)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bf[nt][t], acc[nt], 0, 0, 0);
+            // epilogue: lane holds window 4 mt + kq of column r16 (4 offsets)
+            const int gw = 4 * mt + kq;
+#pragma unroll
+            for (int nt = 0; nt < 3; ++nt) {
+                if (!col_ok[nt]) continue;
+                int8_t r;
+                const float v = relu_pool4(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], r);
+                const int64_t o = col_out[nt] + (int64_t)m * kP1 + gw;
+                a.p1[o] = v;
+                a.r1[o] = r;
+            }
+        }
+    }
+}
+
+// conv2 (6 -> 16, 5x5) of one sample: per image the im2col of the pooled
+// conv1 map [100 conv positions x 150 taps (c, i, j)] times the sample's
+// filters [150 x 16 output channels] (K padded to 152: B rows 150, 151 zero).
+// Each wave takes its own image (its P1 map in the wave's LDS slot, rows 15
+// floats, channel planes 211 apart: ds_read_b32 nearly conflict free); 7 row
+// tiles of 16 (4 windows x 4 offsets; the 7th holds window 24 only), two tiles
+// in flight (two accumulator chains against the 40-cycle MFMA latency).
+constexpr int kC2RS = 15, kC2PS = 211, kC2Slot = 6 * kC2PS + 2;
+__global__ __launch_bounds__(256) void lenet_conv2_mfma_kernel(ConvArgs a) {
+    __shared__ float pm[4][kC2Slot];
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    const int s = blockIdx.y;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    // B: k = 4 t + kq, column r16 = output channel: W2[r16][k] (k < 150)
+    float bf[38];
+    int koff[38];
+#pragma unroll
+    for (int t = 0; t < 38; ++t) {
+        const int k = 4 * t + kq, kc = min(k, 149);
+        bf[t] = k < 150 ? ws[156 + r16 * 150 + k] : 0.f;
+        koff[t] = (kc / 25) * kC2PS + ((kc % 25) / 5) * kC2RS + kc % 5;
+    }
+    const float bias = ws[2556 + r16];
+    float* P = pm[wv];
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int mb = m0; mb < m1; mb += 4) {
+        const int m = mb + wv;  // wave-uniform
+        __syncthreads();
+        if (m < m1) {
+            const float* src = a.p1 + ((int64_t)s * a.M + m) * kP1;
+            for (int i = lane; i < kP1; i += 64) {
+                const int c = i / 196, y = (i % 196) / 14, x = i % 14;
+                P[c * kC2PS + y * kC2RS + x] = src[i];
+            }
+        }
+        __syncthreads();
+        if (m >= m1) continue;
+        const int64_t orow = ((int64_t)s * a.M + m) * kX2;
+#pragma unroll 1
+        for (int mt = 0; mt < 7; mt += 2) {
+            const bool two = mt + 1 < 7;  // uniform
+            int ro[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int w = min(4 * (mt + h) + (r16 >> 2), 24), q = r16 & 3;
+                ro[h] = (2 * (w / 5) + (q >> 1)) * kC2RS + 2 * (w % 5) + (q & 1);
+            }
+            f32x4 acc0 = f32x4{bias, bias, bias, bias}, acc1 = acc0;
+#pragma unroll
+            for (int t = 0; t < 38; ++t) {
+                const float a0 = P[ro[0] + koff[t]];
+                const float a1 = P[ro[1] + koff[t]];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[t], acc0, 0, 0, 0);
+                if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[t], acc1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int w = 4 * (mt + h) + kq;
+                if (h == 1 && !two) break;
+                if (w >= 25) continue;
+                const f32x4 c = h ? acc1 : acc0;
+                int8_t r;
+                const float v = relu_pool4(c[0], c[1], c[2], c[3], r);
+                a.x2[orow + r16 * 25 + w] = v;
+                a.r2[orow + r16 * 25 + w] = r;
+            }
         }
     }
 }
@@ -1284,7 +1451,23 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     ca.r2 = W.r2;
     ca.dx2 = W.dx2;
     ca.part = W.part;
-    hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
+    if (g_lenet_conv_valu) {
+        hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
+    } else {
+        // conv1 on the matrix cores, 8 samples per workgroup; then conv2 per
+        // sample (>= ~2048 workgroups each)
+        ConvArgs c1 = ca;
+        const int sg = (S + kC1S - 1) / kC1S;
+        const int n1 = std::max(1, std::min(M, 2048 / sg));
+        c1.chunk = (M + n1 - 1) / n1;
+        hipLaunchKernelGGL(lenet_conv1_mfma_kernel, dim3((M + c1.chunk - 1) / c1.chunk, sg),
+                           dim3(256), 0, st, c1, S);
+        ConvArgs c2 = ca;
+        const int n2 = std::max(1, std::min((M + 3) / 4, 2048 / S));
+        c2.chunk = 4 * (((M + 3) / 4 + n2 - 1) / n2);
+        hipLaunchKernelGGL(lenet_conv2_mfma_kernel, dim3((M + c2.chunk - 1) / c2.chunk, S),
+                           dim3(256), 0, st, c2);
+    }
     const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
     const float* Ws = W.wsamp;
     // head forward: H1 = relu(X2 W1^T + b1), H2 = relu(H1 W2^T + b2), D = H2 W3^T + b3

@@ -436,6 +436,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     for (pseudopoint chunks added until samples x
                                     roles x chunks reach it; default 256) for
                                     plans created afterwards (A/B diagnostics) */
+#define PSVI_DBG_LENET_CONV_VALU 16 /* value: 1 = LeNet's conv towers on the fp32
+                                    VALU kernels instead of the MFMA implicit
+                                    GEMMs (A/B)                                */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
