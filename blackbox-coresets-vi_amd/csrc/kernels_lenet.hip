@@ -657,6 +657,237 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
     }
 }
 
+// The same backward with d P1 on the matrix cores.  Each pool2 window w
+// (5x5 per channel) routes its gradient g2[k][w] to ONE of its four conv2
+// positions q = 2 dy + dx, so the transposed conv2 of the routed map is, per
+// window, a 6x6 patch per input channel:
+//   U[w][(c, ay, ax)] = sum_(k, q) A[w][(k, q)] B[(k, q)][(c, ay, ax)],
+//   A[w][(k, q)] = g2[k][w] if window (k, w) routes to q else 0,
+//   B[(k, q)][(c, ay, ax)] = W2[k][c][ay - dy][ax - dx] (0 outside the 5x5),
+// a [25 windows x 64] x [64 x 216] GEMM per image (v_mfma_f32_16x16x4_f32: 2
+// row tiles, 14 column tiles dealt to the 5 waves, k-step = output channel
+// k, lane group = q); then d P1[c][y][x] = the sum, in window order, of the
+// (<= 9) patches covering (y, x) (stride 2: window (wy, wx) covers rows
+// 2 wy .. 2 wy + 5).  Everything else as lenet_conv_bwd_kernel.
+constexpr int kUS = 217;  // LDS row stride of U (216 patch columns)
+template <bool DU>
+__global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_mfma_kernel(ConvArgs a) {
+    __shared__ float w1[DU ? 150 : 1];
+    __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
+    __shared__ float w2[2400];
+    __shared__ float in[32 * kBS];
+    __shared__ float p1[6 * kP1C];   // [c][y * kP1S + x]
+    __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
+    __shared__ int off2[kX2];        // its conv2 position y * kP1S + x (P1 plane offset)
+    __shared__ int q2[kX2];          // its window offset q = 2 dy + dx
+    __shared__ float U[25 * kUS];    // per-window 6x6 d P1 patches
+    __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
+    __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
+    __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const int lane = tid & 63, wv = wave_id(), r16 = lane & 15, kq = lane >> 4;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
+    if (DU) {
+        for (int i = tid; i < 150; i += kConvThreads) w1[i] = ws[i];
+        for (int i = tid; i < 6 * 1024; i += kConvThreads) da1[i] = 0.f;
+    }
+    __syncthreads();
+    // B fragments of this wave's column tiles nt = wv + 5 j (< 14): k-step t =
+    // output channel k, lane group kq = q = (dy, dx), column n = (c, ay, ax)
+    constexpr int kNT = 3;
+    const int ntw = wv < 4 ? 3 : 2;  // wave-uniform
+    float bf[kNT][16];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+        const int n = 16 * (wv + 5 * j) + r16;
+        const int c = n / 36, ay = (n % 36) / 6 - (kq >> 1), ax = n % 6 - (kq & 1);
+        const bool ok = j < ntw && n < 216 && ay >= 0 && ay < 5 && ax >= 0 && ax < 5;
+        const int wo = ok ? c * 25 + ay * 5 + ax : 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) bf[j][t] = ok ? w2[t * 150 + wo] : 0.f;
+    }
+    constexpr int kR2 = 10;
+    const bool own2 = tid < 240;
+    const int k2 = min(tid / 15, 15), t15 = tid % 15;
+    int pb[kR2];
+#pragma unroll
+    for (int r = 0; r < kR2; ++r) {
+        const int e = t15 + 15 * r;
+        pb[r] = (e / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
+    }
+    float accw2[kR2];
+#pragma unroll
+    for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
+    const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
+    const int t1 = w1own ? tid : tid - 240;
+    const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
+    const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
+    float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        const int64_t row = (int64_t)s * a.M + m;
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 1024; i += kConvThreads) {
+            const int y = (i >> 5) - 2, x = (i & 31) - 2;
+            in[(i >> 5) * kBS + (i & 31)] =
+                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+        }
+        for (int i = tid; i < kP1; i += kConvThreads)
+            p1[(i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14] = a.p1[row * kP1 + i];
+        for (int o = tid; o < kX2; o += kConvThreads) {
+            const int r = a.r2[row * kX2 + o];
+            const int py = (o % 25) / 5, px = o % 5;
+            const int rr = r >= 0 ? r : 0;
+            const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
+            g2[o] = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
+            off2[o] = y * kP1S + x;
+            q2[o] = rr;
+        }
+        __syncthreads();
+        // d P1 patches on the matrix cores (U), two row tiles of windows
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const int w = 16 * mt + r16, wc = min(w, 24);
+            float av[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int o = t * 25 + wc;
+                av[t] = (w < 25 && q2[o] == kq) ? g2[o] : 0.f;
+            }
+            f32x4 acc[kNT];
+#pragma unroll
+            for (int j = 0; j < kNT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+#pragma unroll
+                for (int j = 0; j < kNT; ++j)
+                    if (j < ntw) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bf[j][t], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < kNT; ++j) {
+                const int n = 16 * (wv + 5 * j) + r16;
+                if (j >= ntw || n >= 216) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int wr = 16 * mt + 4 * kq + i;
+                    if (wr < 25) U[wr * kUS + n] = acc[j][i];
+                }
+            }
+        }
+        // conv2 weight gradient (as lenet_conv_bwd_kernel)
+        if (own2) {
+            float acc[kR2];
+#pragma unroll
+            for (int r = 0; r < kR2; ++r) acc[r] = 0.f;
+#pragma unroll 5
+            for (int p = 0; p < 25; ++p) {
+                const float gv = g2[k2 * 25 + p];
+                const int op = off2[k2 * 25 + p];
+#pragma unroll
+                for (int r = 0; r < kR2; ++r) acc[r] += gv * p1[pb[r] + op];
+            }
+#pragma unroll
+            for (int r = 0; r < kR2; ++r) accw2[r] += acc[r];
+        }
+        if (tid < 16) {
+            float acc = 0.f;
+            for (int p = 0; p < 25; ++p) acc += g2[tid * 25 + p];
+            accb2 += acc;
+        }
+        __syncthreads();
+        // d P1 = the covering patches in window order, routed through pool1 / relu
+        for (int o = tid; o < kP1; o += kConvThreads) {
+            const int c = o / 196, y = (o % 196) / 14, x = o % 14;
+            const int wy0 = y >= 4 ? (y - 4) >> 1 : 0, wy1 = min(4, y >> 1);
+            const int wx0 = x >= 4 ? (x - 4) >> 1 : 0, wx1 = min(4, x >> 1);
+            float v = 0.f;
+            for (int wy = wy0; wy <= wy1; ++wy)
+                for (int wx = wx0; wx <= wx1; ++wx)
+                    v += U[(wy * 5 + wx) * kUS + c * 36 + (y - 2 * wy) * 6 + (x - 2 * wx)];
+            const int r = a.r1[row * kP1 + o];
+            const int rr = r >= 0 ? r : 0;
+            g1[o] = r >= 0 ? v : 0.f;
+            off1[o] = (2 * y + (rr >> 1)) * kBS + 2 * x + (rr & 1);
+        }
+        __syncthreads();
+        // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
+        if (w1own) {
+            float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+            for (int p = pl1; p < ph1; ++p) {
+                const float gv = g1[c1 * 196 + p];
+                const float* ip = in + off1[c1 * 196 + p] + i1 * kBS;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) acc[j] += gv * ip[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 5; ++j) acc1[j] += acc[j];
+        } else if (b1own) {
+            float acc = 0.f;
+#pragma unroll 5
+            for (int p = pl1; p < ph1; ++p) acc += g1[c1 * 196 + p];
+            acc1[0] += acc;
+        }
+        if (DU && m < a.n_pseudo) {
+            for (int o = tid; o < kP1; o += kConvThreads)
+                da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = g1[o];
+            __syncthreads();
+            if (tid < 196) {
+                const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
+                float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+                for (int c = 0; c < 6; ++c) {
+                    const float* q = da1 + c * 1024 + yy * 32 + xx;
+                    float Q[6][6];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i)
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * 32 + j];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) {
+                            const float wv1 = w1[c * 25 + i * 5 + j];
+                            acc[0] += wv1 * Q[4 - i][4 - j];
+                            acc[1] += wv1 * Q[4 - i][5 - j];
+                            acc[2] += wv1 * Q[5 - i][4 - j];
+                            acc[3] += wv1 * Q[5 - i][5 - j];
+                        }
+                }
+                float* out = a.du + ((int64_t)s * a.n_pseudo + m) * 784 + yy * 28 + xx;
+                out[0] = acc[0];
+                out[1] = acc[1];
+                out[28] = acc[2];
+                out[29] = acc[3];
+            }
+            __syncthreads();
+            for (int o = tid; o < kP1; o += kConvThreads)
+                da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = 0.f;
+        }
+    }
+    __syncthreads();
+    if (w1own) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) red[pg1 * 156 + c1 * 25 + i1 * 5 + j] = acc1[j];
+    } else if (b1own) {
+        red[pg1 * 156 + 150 + c1] = acc1[0];
+    }
+    __syncthreads();
+    float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
+    if (tid < 156) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < kW1Groups; ++q) t += red[q * 156 + tid];
+        out[tid] = t;
+    }
+    if (tid < 16) out[2556 + tid] = accb2;
+    if (own2) {
+#pragma unroll
+        for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void lenet_conv_reduce_kernel(int S_loc, int nchunk,
                                                                      int n_tot,
                                                                      const float* __restrict__ part,
@@ -1519,11 +1750,14 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     if (du) {
         ca.du = outer->du_part;
         ca.n_pseudo = outer->n_pseudo;
-        hipLaunchKernelGGL(lenet_conv_bwd_kernel<true>, dim3(W.nchunk, S), dim3(kConvThreads), 0,
-                           st, ca);
+    }
+    const dim3 bgrid(W.nchunk, S), bblk(kConvThreads);
+    if (g_lenet_conv_valu) {
+        if (du) hipLaunchKernelGGL(lenet_conv_bwd_kernel<true>, bgrid, bblk, 0, st, ca);
+        else hipLaunchKernelGGL(lenet_conv_bwd_kernel<false>, bgrid, bblk, 0, st, ca);
     } else {
-        hipLaunchKernelGGL(lenet_conv_bwd_kernel<false>, dim3(W.nchunk, S), dim3(kConvThreads), 0,
-                           st, ca);
+        if (du) hipLaunchKernelGGL(lenet_conv_bwd_mfma_kernel<true>, bgrid, bblk, 0, st, ca);
+        else hipLaunchKernelGGL(lenet_conv_bwd_mfma_kernel<false>, bgrid, bblk, 0, st, ca);
     }
     hipLaunchKernelGGL(lenet_conv_reduce_kernel,
                        dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),

@@ -74,36 +74,48 @@ from ..models.neural_net import (VILinear, VILinearMultivariateNormal, categoric
 from ..runtime import InnerLoopPlan, adam_adjoint_, adam_update_, nonfinite_, randn_
 
 __all__ = ["PSVI", "PSVILearnV", "PSVIAV", "PSVIFreeV", "PSVI_No_Rescaling", "PSVI_Ablated",
-           "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipOuterELBO"]
+           "PSVI_No_IW", "PSVIFixedU", "PSVIAFixedU", "HipInnerELBO", "HipInnerRows",
+           "HipOuterELBO"]
 
 class HipInnerELBO(torch.autograd.Function):
     """Negative inner ELBO as an autograd node over one psvi_elbo_grad call
-    (value and parameter gradient computed by the caller, PSVI.inner_elbo).
-    u_g / w_g are the rows' inputs and weights carrying their graphs to u, v
-    and alpha: when the backward is asked for them it forms d/du and d/dw of
-    the weighted NLL with ``rows_fn`` (the outer-objective kernel in
-    coefficient mode, every sample's pseudo term with coefficient 1) -- what
-    the reference's autograd delivers through inner_elbo
-    (psvi_classes.py:488-511)."""
+    (value and parameter gradient computed by the caller, PSVI.inner_elbo)."""
 
     @staticmethod
-    def forward(ctx, pvec, u_g, w_g, elbo, grad, rows_fn):
+    def forward(ctx, pvec, elbo, grad):
         ctx.save_for_backward(grad)
-        ctx.rows_fn = rows_fn
-        ctx.shapes = (u_g.shape, u_g.dtype, w_g.shape, w_g.dtype)
         return elbo.to(pvec.dtype).reshape(()).clone()
 
     @staticmethod
     @once_differentiable
     def backward(ctx, gout):
         (grad,) = ctx.saved_tensors
-        gu = gw = None
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            us, ut, ws, wt = ctx.shapes
-            du, dw = ctx.rows_fn()
-            gu = (gout * du).reshape(us).to(ut) if ctx.needs_input_grad[1] else None
-            gw = (gout * dw).reshape(ws).to(wt) if ctx.needs_input_grad[2] else None
-        return gout * grad, gu, gw, None, None, None
+        return gout * grad, None, None
+
+
+class HipInnerRows(torch.autograd.Function):
+    """The inner objective's dependence on its rows: a zero-valued term whose
+    backward gives d/du and d/dw of the weighted NLL with ``rows_fn`` (the
+    outer-objective kernel in coefficient mode, every sample's pseudo term with
+    coefficient 1) -- what the reference's autograd delivers to u, v and alpha
+    through inner_elbo (psvi_classes.py:488-511).  A separate node, so a
+    gradient asked for the parameters only (the inner optimisers' steps) never
+    runs the row pass."""
+
+    @staticmethod
+    def forward(ctx, u_g, w_g, rows_fn, dtype):
+        ctx.rows_fn = rows_fn
+        ctx.shapes = (u_g.shape, u_g.dtype, w_g.shape, w_g.dtype)
+        return torch.zeros((), dtype=dtype, device=u_g.device)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        us, ut, ws, wt = ctx.shapes
+        du, dw = ctx.rows_fn()
+        gu = (gout * du).reshape(us).to(ut) if ctx.needs_input_grad[0] else None
+        gw = (gout * dw).reshape(ws).to(wt) if ctx.needs_input_grad[1] else None
+        return gu, gw, None, None
 
 
 class HipOuterELBO(torch.autograd.Function):
@@ -505,8 +517,11 @@ class PSVI:
         p = pvec.detach().to(torch.float32).contiguous()
         elbo, grad = plan.elbo_grad(u, z, w, eps, p)
         u_g, w_g = self._rows_graph(plan)
-        out = HipInnerELBO.apply(pvec, u_g, w_g, elbo, grad,
-                                 self._row_grad_fn(model, plan, u, z, w, eps, p))
+        out = HipInnerELBO.apply(pvec, elbo, grad)
+        if u_g.requires_grad or w_g.requires_grad:
+            out = out + HipInnerRows.apply(u_g, w_g,
+                                           self._row_grad_fn(model, plan, u, z, w, eps, p),
+                                           out.dtype)
         if self.learn_z:   # + S sum_m w_m sum_c q log q (KLDivLoss's target entropy term)
             q = torch.softmax(self.z, 0)
             wq = (self.N * self.f(self.v, 0)).reshape(-1, 1) * torch.special.xlogy(q, q)
