@@ -24,6 +24,7 @@ extern int g_upd_ablation;               // kernels_mvn.hip
 extern int g_stream_off;                 // kernels_mvn.hip
 extern int g_lenet_gemm_valu;            // kernels_lenet.hip
 extern int g_lenet_conv_valu;            // kernels_lenet.hip
+extern int g_lenet_abl;                  // kernels_lenet.hip
 extern int g_net_split_below;            // kernels_net.hip
 extern int g_net_threads;                // kernels_net.hip
 extern int g_net_wg_target;              // kernels_net.hip
@@ -427,6 +428,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         case PSVI_DBG_LENET_GEMM_VALU: g_lenet_gemm_valu = value; return 0;
         case PSVI_DBG_LENET_CONV_VALU: g_lenet_conv_valu = value; return 0;
+        case PSVI_DBG_LENET_ABLATION: g_lenet_abl = value; return 0;
         case PSVI_DBG_NET_THREADS:
             if (value != 0 && value != 256 && value != 512) return fail(PSVI_EINVAL, "256 or 512");
             g_net_threads = value;

@@ -25,7 +25,8 @@
 namespace psvi {
 
 int g_lenet_gemm_valu = 0;  // psvi_debug_set(PSVI_DBG_LENET_GEMM_VALU, 1): the VALU head GEMM (A/B)
-int g_lenet_conv_valu = 0;  // psvi_debug_set(PSVI_DBG_LENET_CONV_VALU, 1): the VALU conv towers (A/B)
+int g_lenet_conv_valu = 0;
+int g_lenet_abl = 0;        // psvi_debug_set(PSVI_DBG_LENET_ABLATION, mask): backward parts skipped  // psvi_debug_set(PSVI_DBG_LENET_CONV_VALU, 1): the VALU conv towers (A/B)
 
 namespace {
 
@@ -137,6 +138,7 @@ struct ConvArgs {
     float* part;          // bwd: [S][nchunk][2572]
     float* du;            // bwd <DU>: [S][n_pseudo][784] input gradient of the pseudo rows
     int n_pseudo;
+    int abl;              // diagnostics (PSVI_DBG_LENET_ABLATION): parts of the backward skipped
 };
 
 // relu + first-max 2x2 pool of four conv values in window order (0,0) (0,1)
@@ -671,18 +673,18 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
 // 2 wy .. 2 wy + 5).  Everything else as lenet_conv_bwd_kernel.
 constexpr int kUS = 217;  // LDS row stride of U (216 patch columns)
 template <bool DU>
-__global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_mfma_kernel(ConvArgs a) {
+__global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_kernel(ConvArgs a) {
     __shared__ float w1[DU ? 150 : 1];
     __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
     __shared__ float w2[2400];
     __shared__ float in[32 * kBS];
     __shared__ float p1[6 * kP1C];   // [c][y * kP1S + x]
     __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
-    __shared__ int off2[kX2];        // its conv2 position y * kP1S + x (P1 plane offset)
     __shared__ int q2[kX2];          // its window offset q = 2 dy + dx
-    __shared__ float U[25 * kUS];    // per-window 6x6 d P1 patches
+    __shared__ float U[25 * kUS + 1];  // per-window 6x6 d P1 patches, then one zero
     __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
     __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
+    __shared__ int8_t r1s[kP1];      // the image's pool1 routes
     __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
     const int tid = threadIdx.x, s = blockIdx.y;
     const int lane = tid & 63, wv = wave_id(), r16 = lane & 15, kq = lane >> 4;
@@ -707,48 +709,87 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_mfma_kernel(ConvA
 #pragma unroll
         for (int t = 0; t < 16; ++t) bf[j][t] = ok ? w2[t * 150 + wo] : 0.f;
     }
-    constexpr int kR2 = 10;
-    const bool own2 = tid < 240;
-    const int k2 = min(tid / 15, 15), t15 = tid % 15;
-    int pb[kR2];
+    if (tid == 0) U[25 * kUS] = 0.f;
+    // conv2 weight gradient on the matrix cores, accumulated over the chunk's
+    // images in registers: dW2[k][(c, i, j)] += sum_(w, q) A[k][(w, q)]
+    // P1[c][2 wy + dy + i][2 wx + dx + j] (the routed map as A, k-step = pool
+    // window w, lane group = offset q; the im2col of P1 as B, one LDS read per
+    // MFMA).  Wave wv owns column tiles 2 wv, 2 wv + 1 of the 150 (c, i, j).
+    int nb2[2];
 #pragma unroll
-    for (int r = 0; r < kR2; ++r) {
-        const int e = t15 + 15 * r;
-        pb[r] = (e / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
+    for (int h = 0; h < 2; ++h) {
+        const int n = min(16 * (2 * wv + h) + r16, 149);
+        nb2[h] = (n / 25) * kP1C + ((n % 25) / 5) * kP1S + n % 5;
     }
-    float accw2[kR2];
-#pragma unroll
-    for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
+    const int kqoff = (kq >> 1) * kP1S + (kq & 1);
+    f32x4 accw2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
     const int t1 = w1own ? tid : tid - 240;
     const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
     const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
     float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
+    // the padded image's zero border, once (the interior is rewritten per image)
+    for (int i = tid; i < 1024; i += kConvThreads) {
+        const int y = (i >> 5) - 2, x = (i & 31) - 2;
+        if (!(y >= 0 && y < 28 && x >= 0 && x < 28)) in[(i >> 5) * kBS + (i & 31)] = 0.f;
+    }
+    // Per-image inputs in registers, loaded one image ahead (the next image's
+    // global loads are in flight behind this image's compute): u interior 784,
+    // P1 1176, pool1 routes 1176 bytes, pool2 routes and d X2 400 each
+    constexpr int kLU = (784 + kConvThreads - 1) / kConvThreads;   // 3
+    constexpr int kLP = (kP1 + kConvThreads - 1) / kConvThreads;   // 4
+    constexpr int kLX = (kX2 + kConvThreads - 1) / kConvThreads;   // 2
+    float pu[kLU], pp[kLP], pg[kLX];
+    int8_t pr1[kLP], pr2[kLX];
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
-    for (int m = m0; m < m1; ++m) {
-        __syncthreads();
+    auto fetch = [&](int m) __attribute__((always_inline)) {
         const int64_t row = (int64_t)s * a.M + m;
         const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kConvThreads) {
-            const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[(i >> 5) * kBS + (i & 31)] =
-                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
+#pragma unroll
+        for (int k = 0; k < kLU; ++k) pu[k] = um[min(tid + k * kConvThreads, 783)];
+#pragma unroll
+        for (int k = 0; k < kLP; ++k) {
+            const int i = min(tid + k * kConvThreads, kP1 - 1);
+            pp[k] = a.p1[row * kP1 + i];
+            pr1[k] = a.r1[row * kP1 + i];
         }
-        for (int i = tid; i < kP1; i += kConvThreads)
-            p1[(i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14] = a.p1[row * kP1 + i];
-        for (int o = tid; o < kX2; o += kConvThreads) {
-            const int r = a.r2[row * kX2 + o];
-            const int py = (o % 25) / 5, px = o % 5;
-            const int rr = r >= 0 ? r : 0;
-            const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
-            g2[o] = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
-            off2[o] = y * kP1S + x;
-            q2[o] = rr;
+#pragma unroll
+        for (int k = 0; k < kLX; ++k) {
+            const int o = min(tid + k * kConvThreads, kX2 - 1);
+            pg[k] = a.dx2[row * kX2 + o];
+            pr2[k] = a.r2[row * kX2 + o];
         }
+    };
+    if (m0 < m1) fetch(m0);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kLU; ++k) {
+            const int i = tid + k * kConvThreads;
+            if (i < 784 && !(a.abl & 16)) in[(i / 28 + 2) * kBS + i % 28 + 2] = pu[k];
+        }
+#pragma unroll
+        for (int k = 0; k < kLP; ++k) {
+            const int i = tid + k * kConvThreads;
+            if (i < kP1 && !(a.abl & 32)) {
+                p1[(i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14] = pp[k];
+                r1s[i] = pr1[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kLX; ++k) {
+            const int o = tid + k * kConvThreads;
+            if (o < kX2) {
+                const int r = pr2[k];
+                g2[o] = r >= 0 ? pg[k] : 0.f;
+                q2[o] = r >= 0 ? r : 0;
+            }
+        }
+        if (m + 1 < m1) fetch(m + 1);
         __syncthreads();
         // d P1 patches on the matrix cores (U), two row tiles of windows
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
+        for (int mt = 0; mt < 2 && !(a.abl & 1); ++mt) {
             const int w = 16 * mt + r16, wc = min(w, 24);
             float av[16];
 #pragma unroll
@@ -775,20 +816,18 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_mfma_kernel(ConvA
                 }
             }
         }
-        // conv2 weight gradient (as lenet_conv_bwd_kernel)
-        if (own2) {
-            float acc[kR2];
-#pragma unroll
-            for (int r = 0; r < kR2; ++r) acc[r] = 0.f;
+        // conv2 weight gradient (MFMA, see above)
+        if (!(a.abl & 2)) {
 #pragma unroll 5
-            for (int p = 0; p < 25; ++p) {
-                const float gv = g2[k2 * 25 + p];
-                const int op = off2[k2 * 25 + p];
+            for (int t = 0; t < 25; ++t) {
+                const int o = r16 * 25 + t;
+                const float av = q2[o] == kq ? g2[o] : 0.f;
+                const int po = kqoff + 2 * (t / 5) * kP1S + 2 * (t % 5);
 #pragma unroll
-                for (int r = 0; r < kR2; ++r) acc[r] += gv * p1[pb[r] + op];
+                for (int h = 0; h < 2; ++h)
+                    accw2[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, p1[nb2[h] + po], accw2[h],
+                                                                    0, 0, 0);
             }
-#pragma unroll
-            for (int r = 0; r < kR2; ++r) accw2[r] += acc[r];
         }
         if (tid < 16) {
             float acc = 0.f;
@@ -796,23 +835,40 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_mfma_kernel(ConvA
             accb2 += acc;
         }
         __syncthreads();
-        // d P1 = the covering patches in window order, routed through pool1 / relu
-        for (int o = tid; o < kP1; o += kConvThreads) {
+        // d P1 = the covering patches in window order (windows wy = y / 2 - 2
+        // .. y / 2, the ones off the map read the zero slot), routed through
+        // pool1 / relu; the 9 reads of an output issued together
+#pragma unroll 2
+        for (int k = 0; k < 4; ++k) {
+            const int o = tid + k * kConvThreads;
+            if (o >= kP1 || (a.abl & 4)) break;
             const int c = o / 196, y = (o % 196) / 14, x = o % 14;
-            const int wy0 = y >= 4 ? (y - 4) >> 1 : 0, wy1 = min(4, y >> 1);
-            const int wx0 = x >= 4 ? (x - 4) >> 1 : 0, wx1 = min(4, x >> 1);
+            const int by = (y >> 1) - 2, bx = (x >> 1) - 2;
+            int uo[9];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int wy = by + dy, wx = bx + dx;
+                    const bool in_map = wy >= 0 && wy < 5 && wx >= 0 && wx < 5;
+                    uo[dy * 3 + dx] = in_map ? (wy * 5 + wx) * kUS + c * 36 +
+                                                   ((y & 1) + 4 - 2 * dy) * 6 + (x & 1) + 4 - 2 * dx
+                                             : 25 * kUS;
+                }
+            float uv[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) uv[q] = U[uo[q]];
             float v = 0.f;
-            for (int wy = wy0; wy <= wy1; ++wy)
-                for (int wx = wx0; wx <= wx1; ++wx)
-                    v += U[(wy * 5 + wx) * kUS + c * 36 + (y - 2 * wy) * 6 + (x - 2 * wx)];
-            const int r = a.r1[row * kP1 + o];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) v += uv[q];
+            const int r = r1s[o];
             const int rr = r >= 0 ? r : 0;
             g1[o] = r >= 0 ? v : 0.f;
             off1[o] = (2 * y + (rr >> 1)) * kBS + 2 * x + (rr & 1);
         }
         __syncthreads();
         // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
-        if (w1own) {
+        if (w1own && !(a.abl & 8)) {
             float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 5
             for (int p = pl1; p < ph1; ++p) {
@@ -882,9 +938,13 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_mfma_kernel(ConvA
         out[tid] = t;
     }
     if (tid < 16) out[2556 + tid] = accb2;
-    if (own2) {
 #pragma unroll
-        for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
+    for (int h = 0; h < 2; ++h) {
+        const int n = 16 * (2 * wv + h) + r16;
+        if (n < 150) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) out[156 + (4 * kq + i) * 150 + n] = accw2[h][i];
+        }
     }
 }
 
@@ -1682,6 +1742,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     ca.r2 = W.r2;
     ca.dx2 = W.dx2;
     ca.part = W.part;
+    ca.abl = g_lenet_abl;
     if (g_lenet_conv_valu) {
         hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
     } else {

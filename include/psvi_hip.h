@@ -439,6 +439,10 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_LENET_CONV_VALU 16 /* value: 1 = LeNet's conv towers on the fp32
                                     VALU kernels instead of the MFMA implicit
                                     GEMMs (A/B)                                */
+#define PSVI_DBG_LENET_ABLATION 17 /* value: mask of LeNet MFMA-backward parts to
+                                    skip (timing diagnostics; wrong results):
+                                    1 d P1 GEMM, 2 dW2, 4 patch sums, 8 dW1,
+                                    16 image load, 32 P1 load                  */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

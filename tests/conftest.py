@@ -26,3 +26,19 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_sessionstart(session):
+    """PSVI_DEBUG_SET="key=value,...": psvi_debug_set before any test (A/B
+    runs of the suite on an alternative kernel path, e.g. 16=1 for the VALU
+    LeNet conv towers); unset in normal runs."""
+    spec = os.environ.get("PSVI_DEBUG_SET", "")
+    if not spec:
+        return
+    from psvi.runtime import _lib
+
+    lib = _lib.load()
+    for kv in spec.split(","):
+        k, v = (int(x) for x in kv.split("="))
+        if lib.psvi_debug_set(k, v):
+            raise RuntimeError(f"psvi_debug_set({k}, {v}) failed")

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--hvp", type=int, default=0, help="also time N psvi_hvp calls")
     ap.add_argument("--gemm-valu", action="store_true",
                     help="head GEMMs on the VALU kernel (PSVI_DBG_LENET_GEMM_VALU, A/B)")
+    ap.add_argument("--abl", type=int, default=0,
+                    help="PSVI_DBG_LENET_ABLATION mask (timing diagnostics)")
     ap.add_argument("--conv-valu", action="store_true",
                     help="conv towers on the VALU kernels (PSVI_DBG_LENET_CONV_VALU, A/B)")
     a = ap.parse_args()
@@ -34,6 +36,7 @@ def main():
                          a.S, a.M)
     plan.lib.psvi_debug_set(13, 1 if a.gemm_valu else 0)
     plan.lib.psvi_debug_set(16, 1 if a.conv_valu else 0)
+    plan.lib.psvi_debug_set(17, a.abl)
     u = torch.randn(a.M, 1, 28, 28, device="cuda")
     z = torch.randint(0, 10, (a.M,), device="cuda", dtype=torch.int32)
     w = torch.full((a.M,), 60000.0 / a.M, device="cuda")
