@@ -59,7 +59,7 @@ int hip_fail(hipError_t e, const char* where) {
     } while (0)
 
 constexpr int kFwdKChunk = 256;  // columns of L per forward work item
-constexpr int64_t kLenetRowFloats = 1176 + 400 * 2 + 120 * 2 + 84 * 2 + 10;  // per (s, m)
+constexpr int64_t kLenetRowFloats = 2 * 1176 + 400 * 2 + 120 * 2 + 84 * 2 + 10;  // per (s, m): P1, routed d P1, ...
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 

@@ -139,6 +139,9 @@ struct ConvArgs {
     float* du;            // bwd <DU>: [S][n_pseudo][784] input gradient of the pseudo rows
     int n_pseudo;
     int abl;              // diagnostics (PSVI_DBG_LENET_ABLATION): parts of the backward skipped
+    float* g1g;           // MFMA bwd: [S][M][1176] routed d P1 (0 where relu / pool drop it)
+    float* part1;         // conv1 weight-gradient partials [S][nch1][156]
+    int nch1;
 };
 
 // relu + first-max 2x2 pool of four conv values in window order (0,0) (0,1)
@@ -677,15 +680,14 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
     __shared__ float w1[DU ? 150 : 1];
     __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
     __shared__ float w2[2400];
-    __shared__ float in[32 * kBS];
+    __shared__ float in[DU ? 32 * kBS : 1];
     __shared__ float p1[6 * kP1C];   // [c][y * kP1S + x]
     __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
     __shared__ int q2[kX2];          // its window offset q = 2 dy + dx
     __shared__ float U[25 * kUS + 1];  // per-window 6x6 d P1 patches, then one zero
-    __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
-    __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
+    __shared__ float g1[DU ? kP1 : 1];   // DU: routed gradient of each pooled conv1 output
+    __shared__ int off1[DU ? kP1 : 1];   // DU: its conv1 position y * kBS + x (padded image)
     __shared__ int8_t r1s[kP1];      // the image's pool1 routes
-    __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
     const int tid = threadIdx.x, s = blockIdx.y;
     const int lane = tid & 63, wv = wave_id(), r16 = lane & 15, kq = lane >> 4;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
@@ -723,13 +725,9 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
     }
     const int kqoff = (kq >> 1) * kP1S + (kq & 1);
     f32x4 accw2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
-    const int t1 = w1own ? tid : tid - 240;
-    const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
-    const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
-    float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
-    // the padded image's zero border, once (the interior is rewritten per image)
-    for (int i = tid; i < 1024; i += kConvThreads) {
+    float accb2 = 0.f;
+    // DU: the padded image's zero border, once (the interior is rewritten per image)
+    for (int i = tid; i < 1024 && DU; i += kConvThreads) {
         const int y = (i >> 5) - 2, x = (i & 31) - 2;
         if (!(y >= 0 && y < 28 && x >= 0 && x < 28)) in[(i >> 5) * kBS + (i & 31)] = 0.f;
     }
@@ -746,7 +744,7 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
         const int64_t row = (int64_t)s * a.M + m;
         const float* um = a.u + (int64_t)m * 784;
 #pragma unroll
-        for (int k = 0; k < kLU; ++k) pu[k] = um[min(tid + k * kConvThreads, 783)];
+        for (int k = 0; k < kLU; ++k) pu[k] = DU ? um[min(tid + k * kConvThreads, 783)] : 0.f;
 #pragma unroll
         for (int k = 0; k < kLP; ++k) {
             const int i = min(tid + k * kConvThreads, kP1 - 1);
@@ -766,7 +764,7 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
 #pragma unroll
         for (int k = 0; k < kLU; ++k) {
             const int i = tid + k * kConvThreads;
-            if (i < 784 && !(a.abl & 16)) in[(i / 28 + 2) * kBS + i % 28 + 2] = pu[k];
+            if (DU && i < 784 && !(a.abl & 16)) in[(i / 28 + 2) * kBS + i % 28 + 2] = pu[k];
         }
 #pragma unroll
         for (int k = 0; k < kLP; ++k) {
@@ -862,30 +860,15 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
 #pragma unroll
             for (int q = 0; q < 9; ++q) v += uv[q];
             const int r = r1s[o];
-            const int rr = r >= 0 ? r : 0;
-            g1[o] = r >= 0 ? v : 0.f;
-            off1[o] = (2 * y + (rr >> 1)) * kBS + 2 * x + (rr & 1);
-        }
-        __syncthreads();
-        // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
-        if (w1own && !(a.abl & 8)) {
-            float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 5
-            for (int p = pl1; p < ph1; ++p) {
-                const float gv = g1[c1 * 196 + p];
-                const float* ip = in + off1[c1 * 196 + p] + i1 * kBS;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) acc[j] += gv * ip[j];
+            a.g1g[((int64_t)s * a.M + m) * kP1 + o] = r >= 0 ? v : 0.f;
+            if (DU) {
+                const int rr = r >= 0 ? r : 0;
+                g1[o] = r >= 0 ? v : 0.f;
+                off1[o] = (2 * y + (rr >> 1)) * kBS + 2 * x + (rr & 1);
             }
-#pragma unroll
-            for (int j = 0; j < 5; ++j) acc1[j] += acc[j];
-        } else if (b1own) {
-            float acc = 0.f;
-#pragma unroll 5
-            for (int p = pl1; p < ph1; ++p) acc += g1[c1 * 196 + p];
-            acc1[0] += acc;
         }
         if (DU && m < a.n_pseudo) {
+            __syncthreads();
             for (int o = tid; o < kP1; o += kConvThreads)
                 da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = g1[o];
             __syncthreads();
@@ -922,21 +905,7 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
                 da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = 0.f;
         }
     }
-    __syncthreads();
-    if (w1own) {
-#pragma unroll
-        for (int j = 0; j < 5; ++j) red[pg1 * 156 + c1 * 25 + i1 * 5 + j] = acc1[j];
-    } else if (b1own) {
-        red[pg1 * 156 + 150 + c1] = acc1[0];
-    }
-    __syncthreads();
     float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
-    if (tid < 156) {
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < kW1Groups; ++q) t += red[q * 156 + tid];
-        out[tid] = t;
-    }
     if (tid < 16) out[2556 + tid] = accb2;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -948,16 +917,137 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
     }
 }
 
+// conv1's weight and bias gradients on the matrix cores, 8 samples per
+// workgroup (the image im2col is shared by every sample, as in the forward):
+//   dW1[s][c][(i, j)] = sum over images m, pooled positions p, offsets q of
+//     A[(s, c)][(p, q)] B[(p, q)][(i, j)],
+//   A = g1[s][m][c][p] if the pool1 window (s, m, c, p) routes to q else 0
+//     (g1: the routed d P1 the backward wrote),
+//   B = img_m[2 py + dy + i][2 px + dx + j] (padded image), plus a column of
+//     ones for the bias.
+// Rows (sample, channel) 48 = 3 tiles, columns 25 taps + bias = 2 tiles,
+// k-step = pooled position p, lane group = q.  Wave w takes p in [49 w, 49 w
+// + 49) of every image; its six accumulators live across the chunk's images
+// and the four waves' partials are added in wave order at the end.
+constexpr int kW1S = 8;
+__global__ __launch_bounds__(256) void lenet_conv1_wgrad_mfma_kernel(ConvArgs a, int S_loc) {
+    __shared__ float img[kC1Img];
+    __shared__ float gs[kW1S * kP1];
+    __shared__ int8_t rs[kW1S * kP1];
+    __shared__ float red[3][48 * 26];
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), r16 = lane & 15, kq = lane >> 4;
+    const int s0 = blockIdx.y * kW1S;
+    const int ns = min(kW1S, S_loc - s0);
+    for (int i = tid; i < kC1Img; i += 256) img[i] = 0.f;
+    // A rows of this lane: (sample, channel) = row / 6, row % 6; B columns:
+    // taps n < 25 at (n / 5) * kC1RS + n % 5, n = 25 the bias (B = 1)
+    int aoff[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+        const int row = 16 * mt + r16;
+        aoff[mt] = (row / 6) * kP1 + (row % 6) * 196;
+    }
+    int boff[2];
+    bool btap[2], bone[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int n = 16 * nt + r16;
+        btap[nt] = n < 25;
+        bone[nt] = n == 25;
+        boff[nt] = btap[nt] ? (n / 5) * kC1RS + n % 5 : 0;
+    }
+    const int qoff = (kq >> 1) * kC1RS + (kq & 1);
+    f32x4 acc[3][2];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int p0 = 49 * wv;
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        __syncthreads();
+        const float* um = a.u + (int64_t)m * 784;
+        for (int i = tid; i < 784; i += 256) img[(i / 28 + 2) * kC1RS + i % 28 + 2] = um[i];
+        for (int i = tid; i < kW1S * kP1; i += 256) {
+            const int sl = i / kP1;
+            const int64_t src = ((int64_t)(s0 + min(sl, ns - 1)) * a.M + m) * kP1 + i % kP1;
+            gs[i] = sl < ns ? a.g1g[src] : 0.f;
+            rs[i] = a.r1[src];
+        }
+        __syncthreads();
+#pragma unroll 7
+        for (int pp = 0; pp < 49; ++pp) {
+            const int p = p0 + pp;
+            float av[3], bv[2];
+#pragma unroll
+            for (int mt = 0; mt < 3; ++mt) av[mt] = rs[aoff[mt] + p] == kq ? gs[aoff[mt] + p] : 0.f;
+            const int po = 2 * (p / 14) * kC1RS + 2 * (p % 14) + qoff;
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+                bv[nt] = btap[nt] ? img[po + boff[nt]] : (bone[nt] ? 1.f : 0.f);
+#pragma unroll
+            for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], bv[nt], acc[mt][nt],
+                                                                       0, 0, 0);
+        }
+    }
+    // the four waves' partials, added in wave order (red holds waves 1..3)
+    __syncthreads();
+    if (wv > 0) {
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int n = 16 * nt + r16;
+                if (n < 26)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        red[wv - 1][(16 * mt + 4 * kq + i) * 26 + n] = acc[mt][nt][i];
+            }
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int n = 16 * nt + r16;
+                if (n >= 26) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * mt + 4 * kq + i, sl = row / 6, c = row % 6;
+                    if (sl >= ns) continue;
+                    float v = acc[mt][nt][i];
+#pragma unroll
+                    for (int w = 0; w < 3; ++w) v += red[w][row * 26 + n];
+                    float* out = a.part1 + ((int64_t)(s0 + sl) * a.nch1 + blockIdx.x) * 156;
+                    out[n < 25 ? c * 25 + n : 150 + c] = v;
+                }
+            }
+    }
+}
+
+// dws[s][e] = sum over chunks of the conv weight-gradient partials (fixed
+// order); part1 (nullable): conv1's entries e < 156 from its own partials
 __global__ __launch_bounds__(kThreads) void lenet_conv_reduce_kernel(int S_loc, int nchunk,
                                                                      int n_tot,
                                                                      const float* __restrict__ part,
-                                                                     float* __restrict__ dws) {
+                                                                     float* __restrict__ dws,
+                                                                     const float* __restrict__ part1,
+                                                                     int nch1) {
     const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
     if (i >= (int64_t)S_loc * kNConv) return;
     const int s = (int)(i / kNConv), e = (int)(i % kNConv);
-    const float* p = part + (int64_t)s * nchunk * kNConv + e;
     float g = 0.f;
-    for (int c = 0; c < nchunk; ++c) g += p[(int64_t)c * kNConv];
+    if (part1 && e < 156) {
+        const float* p = part1 + (int64_t)s * nch1 * 156 + e;
+        for (int c = 0; c < nch1; ++c) g += p[(int64_t)c * 156];
+    } else {
+        const float* p = part + (int64_t)s * nchunk * kNConv + e;
+        for (int c = 0; c < nchunk; ++c) g += p[(int64_t)c * kNConv];
+    }
     dws[(int64_t)s * n_tot + e] = g;
 }
 
@@ -1676,6 +1766,11 @@ LenetWs lenet_ws(const psvi_plan& p, void* base) {
     w.dh1 = (float*)take(sizeof(float) * S * M * 120);
     w.dx2 = (float*)take(sizeof(float) * S * M * kX2);
     w.part = (float*)take(sizeof(float) * S * w.nchunk * kNConv);
+    // MFMA backward: the routed d P1 and conv1's weight-gradient partials
+    // (8 samples per workgroup, >= ~1024 workgroups)
+    w.g1 = (float*)take(sizeof(float) * S * M * kP1);
+    w.nch1 = (int)std::max<int64_t>(1, std::min<int64_t>(M, 1024 / ((S + kW1S - 1) / kW1S)));
+    w.part1 = (float*)take(sizeof(float) * S * w.nch1 * 156);
     w.bytes = off;
     return w;
 }
@@ -1813,16 +1908,26 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
         ca.n_pseudo = outer->n_pseudo;
     }
     const dim3 bgrid(W.nchunk, S), bblk(kConvThreads);
+    const float* part1 = nullptr;
     if (g_lenet_conv_valu) {
         if (du) hipLaunchKernelGGL(lenet_conv_bwd_kernel<true>, bgrid, bblk, 0, st, ca);
         else hipLaunchKernelGGL(lenet_conv_bwd_kernel<false>, bgrid, bblk, 0, st, ca);
     } else {
+        ca.g1g = W.g1;
         if (du) hipLaunchKernelGGL(lenet_conv_bwd_mfma_kernel<true>, bgrid, bblk, 0, st, ca);
         else hipLaunchKernelGGL(lenet_conv_bwd_mfma_kernel<false>, bgrid, bblk, 0, st, ca);
+        // conv1's weight gradient from the routed d P1: 8 samples per workgroup
+        ConvArgs c1 = ca;
+        c1.part1 = W.part1;
+        c1.nch1 = W.nch1;
+        c1.chunk = (M + W.nch1 - 1) / W.nch1;
+        hipLaunchKernelGGL(lenet_conv1_wgrad_mfma_kernel, dim3(W.nch1, (S + kW1S - 1) / kW1S),
+                           dim3(256), 0, st, c1, S);
+        part1 = W.part1;
     }
     hipLaunchKernelGGL(lenet_conv_reduce_kernel,
                        dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, st, S, W.nchunk, nt, W.part, dW);
+                       dim3(kThreads), 0, st, S, W.nchunk, nt, W.part, dW, part1, W.nch1);
     hipLaunchKernelGGL(lenet_acc_kernel, dim3((nt + kThreads - 1) / kThreads), dim3(kThreads), 0,
                        st, sa, eps, dW, acc, outer ? outer->ck : nullptr, W.wsamp,
                        1.f / (p.d.prior_sd * p.d.prior_sd));
@@ -1953,7 +2058,7 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
     hipLaunchKernelGGL(lenet_conv_bwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
     hipLaunchKernelGGL(lenet_conv_reduce_kernel,
                        dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, st, S, W.nchunk, nt, T.part, T.gd);
+                       dim3(kThreads), 0, st, S, W.nchunk, nt, T.part, T.gd, nullptr, 0);
     const int64_t n = nt + (d_u ? (int64_t)M * 784 : 0) + (d_w ? M : 0);
     hipLaunchKernelGGL(lenet_hvp_assemble_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
                        dim3(kThreads), 0, st, sa, params, vec, eps, W.dws, T.gd, T.du, T.nlld, hv,

@@ -346,6 +346,8 @@ struct LenetWs {
     float *wsamp, *dws, *p1, *x2, *h1, *h2, *d, *dh2, *dh1, *dx2, *part;
     int8_t *r1, *r2;
     int nchunk;
+    float *g1, *part1;  // MFMA backward: routed d P1 [S][M][1176], conv1 partials [S][nch1][156]
+    int nch1;
     size_t bytes;
 };
 int lenet_nchunk(const psvi_plan& p);
