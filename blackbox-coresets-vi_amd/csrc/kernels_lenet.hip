@@ -932,8 +932,8 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
 constexpr int kW1S = 8;
 __global__ __launch_bounds__(256) void lenet_conv1_wgrad_mfma_kernel(ConvArgs a, int S_loc) {
     __shared__ float img[kC1Img];
-    __shared__ float gs[kW1S * kP1];
-    __shared__ int8_t rs[kW1S * kP1];
+    __shared__ __attribute__((aligned(16))) float gs[kW1S * kP1];
+    __shared__ __attribute__((aligned(16))) int8_t rs[kW1S * kP1];
     __shared__ float red[3][48 * 26];
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), r16 = lane & 15, kq = lane >> 4;
     const int s0 = blockIdx.y * kW1S;
@@ -964,16 +964,47 @@ __global__ __launch_bounds__(256) void lenet_conv1_wgrad_mfma_kernel(ConvArgs a,
         for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int p0 = 49 * wv;
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    // the next image's inputs in registers (loads in flight behind this
+    // image's MFMAs): the 8 samples' routed d P1 as float4, their routes as
+    // 4-byte words, the image as float4 (196 per image)
+    constexpr int kQ = kP1 / 4;                        // 294 quads per (s, m)
+    constexpr int kNQ = (kW1S * kQ + 255) / 256;       // 10 per thread
+    float4 pg[kNQ];
+    int pr[kNQ];
+    float4 pu;
+    const bool u16 = ((uintptr_t)a.u & 15) == 0;  // the caller's u: float4 loads when aligned
+    auto fetch = [&](int m) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < kNQ; ++k) {
+            const int i = min(tid + 256 * k, kW1S * kQ - 1), sl = i / kQ;
+            const int64_t src = ((int64_t)(s0 + min(sl, ns - 1)) * a.M + m) * kQ + i % kQ;
+            pg[k] = reinterpret_cast<const float4*>(a.g1g)[src];
+            pr[k] = reinterpret_cast<const int*>(a.r1)[src];
+        }
+        const float* uq = a.u + (int64_t)m * 784 + 4 * min(tid, 195);
+        if (u16)
+            pu = *reinterpret_cast<const float4*>(uq);
+        else
+            pu = make_float4(uq[0], uq[1], uq[2], uq[3]);
+    };
+    if (m0 < m1) fetch(m0);
     for (int m = m0; m < m1; ++m) {
         __syncthreads();
-        const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 784; i += 256) img[(i / 28 + 2) * kC1RS + i % 28 + 2] = um[i];
-        for (int i = tid; i < kW1S * kP1; i += 256) {
-            const int sl = i / kP1;
-            const int64_t src = ((int64_t)(s0 + min(sl, ns - 1)) * a.M + m) * kP1 + i % kP1;
-            gs[i] = sl < ns ? a.g1g[src] : 0.f;
-            rs[i] = a.r1[src];
+#pragma unroll
+        for (int k = 0; k < kNQ; ++k) {
+            const int i = tid + 256 * k;
+            if (i < kW1S * kQ) {
+                const bool live = i / kQ < ns;
+                reinterpret_cast<float4*>(gs)[i] = live ? pg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+                reinterpret_cast<int*>(rs)[i] = pr[k];
+            }
         }
+        if (tid < 196) {
+            const int y = (4 * tid) / 28, x = (4 * tid) % 28;
+            float* d = img + (y + 2) * kC1RS + x + 2;
+            d[0] = pu.x; d[1] = pu.y; d[2] = pu.z; d[3] = pu.w;
+        }
+        if (m + 1 < m1) fetch(m + 1);
         __syncthreads();
 #pragma unroll 7
         for (int pp = 0; pp < 49; ++pp) {
