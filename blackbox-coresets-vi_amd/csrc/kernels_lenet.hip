@@ -20,6 +20,8 @@
 // conv2's weight gradient), route1/route2 int8 (pool window index of the first
 // maximum, -1 where relu zeroes it), X2 [S][M][400], H1 [S][M][120],
 // H2 [S][M][84], D [S][M][10] (logits, then d logits).
+#include <type_traits>
+
 #include "psvi_internal.hpp"
 
 namespace psvi {
@@ -356,72 +358,93 @@ __global__ __launch_bounds__(256) void lenet_conv1_mfma_kernel(ConvArgs a, int S
 
 // conv2 (6 -> 16, 5x5) of one sample: per image the im2col of the pooled
 // conv1 map [100 conv positions x 150 taps (c, i, j)] times the sample's
-// filters [150 x 16 output channels] (K padded to 152: B rows 150, 151 zero).
-// Each wave takes its own image (its P1 map in the wave's LDS slot, rows 15
-// floats, channel planes 211 apart: ds_read_b32 nearly conflict free); 7 row
-// tiles of 16 (4 windows x 4 offsets; the 7th holds window 24 only), two tiles
-// in flight (two accumulator chains against the 40-cycle MFMA latency).
-constexpr int kC2RS = 15, kC2PS = 211, kC2Slot = 6 * kC2PS + 2;
-__global__ __launch_bounds__(256) void lenet_conv2_mfma_kernel(ConvArgs a) {
-    __shared__ float pm[4][kC2Slot];
-    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+// filters [150 x 16 output channels].  One wave per workgroup, two images per
+// pass: 200 rows = 13 row tiles of 16 (4 windows x 4 offsets; windows 25..49
+// are the second image's), two tiles in flight (two accumulator chains against
+// the 40-cycle MFMA latency).  The pair's P1 maps sit in LDS as they lie in
+// HBM (rows 14 floats, channel planes 196: a straight float4 copy; the reads
+// below average ~3 LDS cycles against the MFMA's 32); 4 waves per SIMD (LDS
+// bound) hide each other's copies (a register prefetch of the next pair cost
+// 40 VGPRs and a wave of occupancy).  K = 150 in 38 steps, ordered
+// so every lane's A address is (row offset) + (its kq times a stride) + an
+// immediate: steps 0..29 tap (c, i, j = kq) for (c, i) = (t / 5, t % 5);
+// steps 30..35 tap (t - 30, i = kq, 4); steps 36, 37 tap (4 (t - 36) + kq, 4,
+// 4), channels 6 and 7 zero in B (their A reads clamped to channel 5).
+constexpr int kC2Pair = 2 * kP1;
+constexpr int kC2Q = kC2Pair / 4 / 64 + 1;  // float4 per lane per pair (588 / 64 -> 10)
+__global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) float pm[kC2Pair];
+    const int lane = threadIdx.x, r16 = lane & 15, kq = lane >> 4;
     const int s = blockIdx.y;
-    const int r16 = lane & 15, kq = lane >> 4;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    // B: k = 4 t + kq, column r16 = output channel: W2[r16][k] (k < 150)
+    const float* w2 = ws + 156 + r16 * 150;
     float bf[38];
-    int koff[38];
 #pragma unroll
-    for (int t = 0; t < 38; ++t) {
-        const int k = 4 * t + kq, kc = min(k, 149);
-        bf[t] = k < 150 ? ws[156 + r16 * 150 + k] : 0.f;
-        koff[t] = (kc / 25) * kC2PS + ((kc % 25) / 5) * kC2RS + kc % 5;
-    }
+    for (int t = 0; t < 30; ++t) bf[t] = w2[(t / 5) * 25 + (t % 5) * 5 + kq];
+#pragma unroll
+    for (int t = 30; t < 36; ++t) bf[t] = w2[(t - 30) * 25 + kq * 5 + 4];
+    bf[36] = w2[kq * 25 + 24];
+    bf[37] = kq < 2 ? w2[(4 + kq) * 25 + 24] : 0.f;
     const float bias = ws[2556 + r16];
-    float* P = pm[wv];
-    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
-    for (int mb = m0; mb < m1; mb += 4) {
-        const int m = mb + wv;  // wave-uniform
-        __syncthreads();
-        if (m < m1) {
-            const float* src = a.p1 + ((int64_t)s * a.M + m) * kP1;
-            for (int i = lane; i < kP1; i += 64) {
-                const int c = i / 196, y = (i % 196) / 14, x = i % 14;
-                P[c * kC2PS + y * kC2RS + x] = src[i];
-            }
+    const int oj = kq, oi = kq * 14, oc = kq * 196, oc2 = min(kq, 1) * 196;
+    const int npair = (a.M + 1) >> 1;
+    const int p0 = blockIdx.x * a.chunk, p1 = min(npair, p0 + a.chunk);
+    if (p0 >= p1) return;
+    const float4* src = reinterpret_cast<const float4*>(a.p1 + (int64_t)s * a.M * kP1);
+    float4* dst = reinterpret_cast<float4*>(pm);
+    float4 pf[kC2Q];
+    auto fetch = [&](int p) __attribute__((always_inline)) {
+        const int n4 = (min(a.M, 2 * p + 2) - 2 * p) * (kP1 / 4);
+        const float4* sp = src + (int64_t)p * (kC2Pair / 4);
+#pragma unroll
+        for (int q = 0; q < kC2Q; ++q) pf[q] = sp[min(lane + 64 * q, n4 - 1)];
+    };
+    for (int p = p0; p < p1; ++p) {
+        fetch(p);
+        __syncthreads();  // the previous pair's reads are done
+#pragma unroll
+        for (int q = 0; q < kC2Q; ++q) {
+            const int i = lane + 64 * q;
+            if (i < kC2Pair / 4) dst[i] = pf[q];
         }
         __syncthreads();
-        if (m >= m1) continue;
-        const int64_t orow = ((int64_t)s * a.M + m) * kX2;
-#pragma unroll 1
-        for (int mt = 0; mt < 7; mt += 2) {
-            const bool two = mt + 1 < 7;  // uniform
-            int ro[2];
+        const bool two_img = 2 * p + 1 < a.M;  // uniform
+        // NT row tiles from tile mt on: 38 MFMA steps each, then relu + pool
+        auto tiles = [&](int mt, auto nt_c) __attribute__((always_inline)) {
+            constexpr int NT = decltype(nt_c)::value;
+            int ro[NT];
+            f32x4 acc[NT];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int w = min(4 * (mt + h) + (r16 >> 2), 24), q = r16 & 3;
-                ro[h] = (2 * (w / 5) + (q >> 1)) * kC2RS + 2 * (w % 5) + (q & 1);
+            for (int h = 0; h < NT; ++h) {
+                const int g = min(4 * (mt + h) + (r16 >> 2), 49), q = r16 & 3;
+                const int im = g >= 25, w = g - 25 * im;
+                ro[h] = im * kP1 + (2 * (w / 5) + (q >> 1)) * 14 + 2 * (w % 5) + (q & 1);
+                acc[h] = f32x4{bias, bias, bias, bias};
             }
-            f32x4 acc0 = f32x4{bias, bias, bias, bias}, acc1 = acc0;
 #pragma unroll
             for (int t = 0; t < 38; ++t) {
-                const float a0 = P[ro[0] + koff[t]];
-                const float a1 = P[ro[1] + koff[t]];
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf[t], acc0, 0, 0, 0);
-                if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf[t], acc1, 0, 0, 0);
+                const int off = t < 30 ? oj + (t / 5) * 196 + (t % 5) * 14
+                              : t < 36 ? oi + (t - 30) * 196 + 4
+                              : t == 36 ? oc + 60 : oc2 + 4 * 196 + 60;
+#pragma unroll
+                for (int h = 0; h < NT; ++h)
+                    acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(pm[ro[h] + off], bf[t], acc[h], 0, 0, 0);
             }
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int w = 4 * (mt + h) + kq;
-                if (h == 1 && !two) break;
-                if (w >= 25) continue;
-                const f32x4 c = h ? acc1 : acc0;
+            for (int h = 0; h < NT; ++h) {
+                const int g = 4 * (mt + h) + kq;
+                if (g >= 50 || (g >= 25 && !two_img)) continue;
+                const int im = g >= 25, w = g - 25 * im;
                 int8_t r;
-                const float v = relu_pool4(c[0], c[1], c[2], c[3], r);
-                a.x2[orow + r16 * 25 + w] = v;
-                a.r2[orow + r16 * 25 + w] = r;
+                const float v = relu_pool4(acc[h][0], acc[h][1], acc[h][2], acc[h][3], r);
+                const int64_t o = ((int64_t)s * a.M + 2 * p + im) * kX2 + r16 * 25 + w;
+                a.x2[o] = v;
+                a.r2[o] = r;
             }
-        }
+        };
+#pragma unroll 1
+        for (int mt = 0; mt < 12; mt += 2) tiles(mt, std::integral_constant<int, 2>{});
+        tiles(12, std::integral_constant<int, 1>{});  // windows 48, 49 (rows 50, 51 clamped)
     }
 }
 
@@ -675,16 +698,22 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
 // (<= 9) patches covering (y, x) (stride 2: window (wy, wx) covers rows
 // 2 wy .. 2 wy + 5).  Everything else as lenet_conv_bwd_kernel.
 constexpr int kUS = 217;  // LDS row stride of U (216 patch columns)
+constexpr int kGK = 33, kGQ = 16 * kGK;  // routed-map rows / offset planes (ga below)
 template <bool DU>
 __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_kernel(ConvArgs a) {
     __shared__ float w1[DU ? 150 : 1];
     __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
-    __shared__ float w2[2400];
     __shared__ float in[DU ? 32 * kBS : 1];
     __shared__ float p1[6 * kP1C];   // [c][y * kP1S + x]
     __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
-    __shared__ int q2[kX2];          // its window offset q = 2 dy + dx
+    // the routed map expanded by window offset: ga[q][k][w] = g2[k][w] if
+    // window (k, w) routes to q else 0 (w 25..32 zero): the A operand of both
+    // GEMMs below, read unconditionally (rows 33 apart, offset planes 528:
+    // both read patterns hit 32 distinct banks per half-wave)
+    __shared__ float ga[4 * kGQ];
     __shared__ float U[25 * kUS + 1];  // per-window 6x6 d P1 patches, then one zero
+    float* w2 = U;  // conv2's filters until the B fragments are loaded (U is first written
+                    // after the image loop's first barrier)
     __shared__ float g1[DU ? kP1 : 1];   // DU: routed gradient of each pooled conv1 output
     __shared__ int off1[DU ? kP1 : 1];   // DU: its conv1 position y * kBS + x (padded image)
     __shared__ int8_t r1s[kP1];      // the image's pool1 routes
@@ -712,6 +741,7 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
         for (int t = 0; t < 16; ++t) bf[j][t] = ok ? w2[t * 150 + wo] : 0.f;
     }
     if (tid == 0) U[25 * kUS] = 0.f;
+    for (int i = tid; i < 4 * kGQ; i += kConvThreads) ga[i] = 0.f;
     // conv2 weight gradient on the matrix cores, accumulated over the chunk's
     // images in registers: dW2[k][(c, i, j)] += sum_(w, q) A[k][(w, q)]
     // P1[c][2 wy + dy + i][2 wx + dx + j] (the routed map as A, k-step = pool
@@ -778,48 +808,56 @@ __global__ __launch_bounds__(kConvThreads, DU ? 2 : 3) void lenet_conv_bwd_mfma_
         for (int k = 0; k < kLX; ++k) {
             const int o = tid + k * kConvThreads;
             if (o < kX2) {
-                const int r = pr2[k];
-                g2[o] = r >= 0 ? pg[k] : 0.f;
-                q2[o] = r >= 0 ? r : 0;
+                const int r = pr2[k], kk = o / 25, w = o % 25;
+                const float g = r >= 0 ? pg[k] : 0.f;
+                g2[o] = g;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ga[q * kGQ + kk * kGK + w] = r == q ? g : 0.f;
             }
         }
         if (m + 1 < m1) fetch(m + 1);
         __syncthreads();
-        // d P1 patches on the matrix cores (U), two row tiles of windows
+        // d P1 patches on the matrix cores (U), two row tiles of windows; the
+        // wave's column-tile count as a template constant (no branch per MFMA)
+        auto dp1 = [&](auto nt_c) __attribute__((always_inline)) {
+            constexpr int NT = decltype(nt_c)::value;
 #pragma unroll
-        for (int mt = 0; mt < 2 && !(a.abl & 1); ++mt) {
-            const int w = 16 * mt + r16, wc = min(w, 24);
-            float av[16];
+            for (int mt = 0; mt < 2; ++mt) {
+                const float* ar = ga + kq * kGQ + 16 * mt + r16;
+                f32x4 acc[NT];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int o = t * 25 + wc;
-                av[t] = (w < 25 && q2[o] == kq) ? g2[o] : 0.f;
-            }
-            f32x4 acc[kNT];
+                for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < kNT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int t = 0; t < 16; ++t) {
+                    const float av = ar[t * kGK];
 #pragma unroll
-            for (int t = 0; t < 16; ++t)
+                    for (int j = 0; j < NT; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j][t], acc[j], 0, 0, 0);
+                }
 #pragma unroll
-                for (int j = 0; j < kNT; ++j)
-                    if (j < ntw) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bf[j][t], acc[j], 0, 0, 0);
+                for (int j = 0; j < NT; ++j) {
+                    const int n = 16 * (wv + 5 * j) + r16;
+                    if (n >= 216) continue;
 #pragma unroll
-            for (int j = 0; j < kNT; ++j) {
-                const int n = 16 * (wv + 5 * j) + r16;
-                if (j >= ntw || n >= 216) continue;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int wr = 16 * mt + 4 * kq + i;
-                    if (wr < 25) U[wr * kUS + n] = acc[j][i];
+                    for (int i = 0; i < 4; ++i) {
+                        const int wr = 16 * mt + 4 * kq + i;
+                        if (wr < 25) U[wr * kUS + n] = acc[j][i];
+                    }
                 }
             }
+        };
+        if (!(a.abl & 1)) {
+            if (ntw == 3)
+                dp1(std::integral_constant<int, 3>{});
+            else
+                dp1(std::integral_constant<int, 2>{});
         }
         // conv2 weight gradient (MFMA, see above)
         if (!(a.abl & 2)) {
+            const float* ar = ga + kq * kGQ + r16 * kGK;
 #pragma unroll 5
             for (int t = 0; t < 25; ++t) {
-                const int o = r16 * 25 + t;
-                const float av = q2[o] == kq ? g2[o] : 0.f;
+                const float av = ar[t];
                 const int po = kqoff + 2 * (t / 5) * kP1S + 2 * (t % 5);
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
@@ -1881,10 +1919,12 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
         hipLaunchKernelGGL(lenet_conv1_mfma_kernel, dim3((M + c1.chunk - 1) / c1.chunk, sg),
                            dim3(256), 0, st, c1, S);
         ConvArgs c2 = ca;
-        const int n2 = std::max(1, std::min((M + 3) / 4, 2048 / S));
-        c2.chunk = 4 * (((M + 3) / 4 + n2 - 1) / n2);
-        hipLaunchKernelGGL(lenet_conv2_mfma_kernel, dim3((M + c2.chunk - 1) / c2.chunk, S),
-                           dim3(256), 0, st, c2);
+        // one wave per workgroup, a chunk of image pairs each (~8192 waves)
+        const int np = (M + 1) / 2;
+        const int n2 = std::max(1, std::min(np, 8192 / S));
+        c2.chunk = (np + n2 - 1) / n2;
+        hipLaunchKernelGGL(lenet_conv2_mfma_kernel, dim3((np + c2.chunk - 1) / c2.chunk, S),
+                           dim3(64), 0, st, c2);
     }
     const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
     const float* Ws = W.wsamp;
