@@ -1414,6 +1414,7 @@ struct TanArgs {
     float* x2d;          // fwd out: tangent X2 [S][M][400]
     float* part;         // bwd out: tangent conv weight gradients [S][nchunk][2572]
     float* du;           // bwd out, nullable: [S][M][784] tangent of d u
+    float* g1g;          // MFMA bwd out: [S][M][1176] routed d P1_dot
 };
 
 // tangent forward of the conv towers: only the routed conv positions matter
@@ -1738,6 +1739,274 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArg
     if (own2) {
 #pragma unroll
         for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
+    }
+}
+
+// The tangent backward on the matrix cores (d/du, when asked for, by
+// lenet_du_tan_kernel afterwards).  Per image, as lenet_conv_bwd_mfma_kernel:
+//   d P1_dot patches  U_dot = [A_dot | A] [B(W2) ; B(W2_dot)]   (K = 2 x 64),
+//     A / A_dot: the routed primal / tangent conv2 gradients expanded by window
+//     offset (ga / gad), B(.): the filters shifted by offset, as there;
+//   G_dot conv2 = sum_(w, q) A_dot P1 + A P1_dot   (K = 2 x 100),
+//   d P1_dot = the covering U_dot patches in window order, routed through pool1
+//     / relu, written to HBM for lenet_conv1_wgrad_mfma_kernel (conv1's G_dot).
+// Eight waves: waves 0..5 own d P1 column tiles wv, wv + 8 and conv2 weight
+// tile wv; waves 6, 7 own d P1 tile wv and conv2 weight tiles 6 + 2 (wv - 6)
+// + {0, 1} (178 / 164 MFMAs per image).  LDS: P1 | P1_dot, then U_dot (the
+// weight-gradient GEMM is done before the patches are written); W2's B
+// fragments in registers, W2_dot's read from LDS per k-step (128 VGPRs: four
+// waves per SIMD, two workgroups per CU).
+constexpr int kTW = 8, kTThreads = 64 * kTW;
+constexpr int kTPP = 2 * 6 * kP1C;
+static_assert(kTPP >= 25 * kUS + 1, "P1 | P1_dot region holds U_dot");
+__global__ __launch_bounds__(kTThreads, 4) void lenet_conv_bwd_tan_mfma_kernel(TanArgs a) {
+    __shared__ float pp[kTPP];
+    __shared__ float ga[4 * kGQ], gad[4 * kGQ];
+    __shared__ float g2d[kX2];
+    __shared__ int8_t r1s[kP1];
+    __shared__ float wd2[2400];  // W2_dot: its B fragments are read per k-step
+    float* const p1 = pp;
+    float* const p1d = pp + 6 * kP1C;
+    float* const U = pp;
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const int lane = tid & 63, wv = wave_id(), r16 = lane & 15, kq = lane >> 4;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    const float* wds = a.wdot + (int64_t)s * a.n_tot;
+    for (int i = tid; i < 2400; i += kTThreads) {
+        pp[i] = ws[156 + i];
+        wd2[i] = wds[156 + i];
+    }
+    for (int i = tid; i < 4 * kGQ; i += kTThreads) ga[i] = gad[i] = 0.f;
+    __syncthreads();
+    // B fragments of the d P1 column tiles wv + 8 j: k-steps 0..15 W2 (in
+    // registers), 16..31 W2_dot (read from LDS at wo, masked by okf)
+    float bf[2][16], okf[2];
+    int wo[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int tile = wv + 8 * j, n = 16 * tile + r16;
+        const int c = n / 36, ay = (n % 36) / 6 - (kq >> 1), ax = n % 6 - (kq & 1);
+        const bool ok = tile < 14 && n < 216 && ay >= 0 && ay < 5 && ax >= 0 && ax < 5;
+        wo[j] = ok ? c * 25 + ay * 5 + ax : 0;
+        okf[j] = ok ? 1.f : 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) bf[j][t] = ok ? pp[t * 150 + wo[j]] : 0.f;
+    }
+    const bool hi = wv >= 6;  // wave-uniform
+    int nb2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int tile = hi ? 6 + 2 * (wv - 6) + h : wv;
+        const int n = min(16 * tile + r16, 149);
+        nb2[h] = (n / 25) * kP1C + ((n % 25) / 5) * kP1S + n % 5;
+    }
+    const int kqoff = (kq >> 1) * kP1S + (kq & 1);
+    f32x4 accw2[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    float accb2 = 0.f;
+    constexpr int kLP = (kP1 + kTThreads - 1) / kTThreads;  // 3
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    // conv2 weight tangent for NW column tiles (k-steps: 25 windows x A_dot P1,
+    // then 25 x A P1_dot)
+    auto wgrad2 = [&](auto nw_c) __attribute__((always_inline)) {
+        constexpr int NW = decltype(nw_c)::value;
+        const float* ad = gad + kq * kGQ + r16 * kGK;
+        const float* ap = ga + kq * kGQ + r16 * kGK;
+#pragma unroll 5
+        for (int t = 0; t < 25; ++t) {
+            const float av = ad[t];
+            const int po = kqoff + 2 * (t / 5) * kP1S + 2 * (t % 5);
+#pragma unroll
+            for (int h = 0; h < NW; ++h)
+                accw2[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, p1[nb2[h] + po], accw2[h], 0, 0, 0);
+        }
+#pragma unroll 5
+        for (int t = 0; t < 25; ++t) {
+            const float av = ap[t];
+            const int po = kqoff + 2 * (t / 5) * kP1S + 2 * (t % 5);
+#pragma unroll
+            for (int h = 0; h < NW; ++h)
+                accw2[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, p1d[nb2[h] + po], accw2[h], 0, 0, 0);
+        }
+    };
+    // U_dot for NT column tiles, two row tiles of windows
+    auto dp1 = [&](auto nt_c) __attribute__((always_inline)) {
+        constexpr int NT = decltype(nt_c)::value;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const float* ad = gad + kq * kGQ + 16 * mt + r16;
+            const float* ap = ga + kq * kGQ + 16 * mt + r16;
+            f32x4 acc[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const float av = ad[t * kGK];
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bf[j][t], acc[j], 0, 0, 0);
+            }
+#pragma unroll 4
+            for (int t = 0; t < 16; ++t) {
+                const float av = ap[t * kGK];
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wd2[wo[j] + t * 150] * okf[j],
+                                                                  acc[j], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = 16 * (wv + 8 * j) + r16;
+                if (n >= 216) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int wr = 16 * mt + 4 * kq + i;
+                    if (wr < 25) U[wr * kUS + n] = acc[j][i];
+                }
+            }
+        }
+    };
+    for (int m = m0; m < m1; ++m) {
+        // this image's inputs (no register prefetch: 128 VGPRs hold 4 waves per
+        // SIMD, two workgroups per CU, one staging while the other multiplies)
+        const int64_t row = (int64_t)s * a.M + m;
+        float pv[kLP], pvd[kLP];
+        int8_t pr1[kLP];
+#pragma unroll
+        for (int k = 0; k < kLP; ++k) {
+            const int i = min(tid + k * kTThreads, kP1 - 1);
+            pv[k] = a.p1[row * kP1 + i];
+            pvd[k] = a.p1d[row * kP1 + i];
+            pr1[k] = a.r1[row * kP1 + i];
+        }
+        const int o2 = min(tid, kX2 - 1);
+        const float pg = a.dx2[row * kX2 + o2], pgd = a.dx2d[row * kX2 + o2];
+        const int pr2 = a.r2[row * kX2 + o2];
+        __syncthreads();  // the previous image's patch reads are done
+#pragma unroll
+        for (int k = 0; k < kLP; ++k) {
+            const int i = tid + k * kTThreads;
+            if (i < kP1) {
+                const int q = (i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14;
+                p1[q] = pv[k];
+                p1d[q] = pvd[k];
+                r1s[i] = pr1[k];
+            }
+        }
+        if (tid < kX2) {
+            const int r = pr2, kk = tid / 25, w = tid % 25;
+            const float g = r >= 0 ? pg : 0.f, gd = r >= 0 ? pgd : 0.f;
+            g2d[tid] = gd;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                ga[q * kGQ + kk * kGK + w] = r == q ? g : 0.f;
+                gad[q * kGQ + kk * kGK + w] = r == q ? gd : 0.f;
+            }
+        }
+        __syncthreads();
+        if (hi)
+            wgrad2(std::integral_constant<int, 2>{});
+        else
+            wgrad2(std::integral_constant<int, 1>{});
+        if (tid < 16) {
+            float acc = 0.f;
+            for (int p = 0; p < 25; ++p) acc += g2d[tid * 25 + p];
+            accb2 += acc;
+        }
+        __syncthreads();  // P1 | P1_dot reads are done: U_dot overwrites them
+        if (tid == 0) U[25 * kUS] = 0.f;
+        if (hi)
+            dp1(std::integral_constant<int, 1>{});
+        else
+            dp1(std::integral_constant<int, 2>{});
+        __syncthreads();
+        // d P1_dot = the covering patches in window order, routed
+#pragma unroll 1
+        for (int k = 0; k < kLP; ++k) {
+            const int o = tid + k * kTThreads;
+            if (o >= kP1) break;
+            const int c = o / 196, y = (o % 196) / 14, x = o % 14;
+            const int by = (y >> 1) - 2, bx = (x >> 1) - 2;
+            int uo[9];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int wy = by + dy, wx = bx + dx;
+                    const bool in_map = wy >= 0 && wy < 5 && wx >= 0 && wx < 5;
+                    uo[dy * 3 + dx] = in_map ? (wy * 5 + wx) * kUS + c * 36 +
+                                                   ((y & 1) + 4 - 2 * dy) * 6 + (x & 1) + 4 - 2 * dx
+                                             : 25 * kUS;
+                }
+            float uv[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) uv[q] = U[uo[q]];
+            float v = 0.f;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) v += uv[q];
+            a.g1g[((int64_t)s * a.M + m) * kP1 + o] = r1s[o] >= 0 ? v : 0.f;
+        }
+    }
+    float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
+    if (tid < 16) out[2556 + tid] = accb2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !hi) break;
+        const int tile = hi ? 6 + 2 * (wv - 6) + h : wv;
+        const int n = 16 * tile + r16;
+        if (n < 150) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) out[156 + (4 * kq + i) * 150 + n] = accw2[h][i];
+        }
+    }
+}
+
+// The tangent of d u (the mixed product d/du) for every row, from the routed
+// primal and tangent d P1 the backward kernels left in HBM:
+//   du_dot = convT(routed d P1_dot, W1) + convT(routed d P1, W1_dot)
+// (each routed value placed at its conv1 position of a zero-bordered 32 x 32
+// plane per channel, 2x2 output blocks per thread, as lenet_conv_bwd_kernel).
+__global__ __launch_bounds__(kThreads) void lenet_du_tan_kernel(TanArgs a, const float* __restrict__ g1p,
+                                                               const float* __restrict__ g1t) {
+    __shared__ float w1[150], wd1[150];
+    __shared__ float da1[6 * 1024], da1d[6 * 1024];
+    __shared__ int off1[kP1];
+    const int tid = threadIdx.x, s = blockIdx.y;
+    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
+    const float* wds = a.wdot + (int64_t)s * a.n_tot;
+    for (int i = tid; i < 150; i += kThreads) {
+        w1[i] = ws[i];
+        wd1[i] = wds[i];
+    }
+    for (int i = tid; i < 6 * 1024; i += kThreads) da1[i] = da1d[i] = 0.f;
+    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    for (int m = m0; m < m1; ++m) {
+        const int64_t row = (int64_t)s * a.M + m;
+        __syncthreads();
+        for (int o = tid; o < kP1; o += kThreads) {
+            const int r = a.r1[row * kP1 + o], rr = r >= 0 ? r : 0;
+            const int c = o / 196, py = (o % 196) / 14, px = o % 14;
+            const int q = c * 1024 + (2 * py + (rr >> 1) + 2) * 32 + 2 * px + (rr & 1) + 2;
+            off1[o] = q;
+            da1[q] = g1p[row * kP1 + o];  // 0 where relu / pool drop it
+            da1d[q] = g1t[row * kP1 + o];
+        }
+        __syncthreads();
+        if (tid < 196) {
+            const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+            for (int c = 0; c < 6; ++c) {
+                convT_block(da1d + c * 1024 + yy * 32 + xx, 32, w1 + c * 25, acc);
+                convT_block(da1 + c * 1024 + yy * 32 + xx, 32, wd1 + c * 25, acc);
+            }
+            float* out = a.du + row * 784 + yy * 28 + xx;
+            out[0] = acc[0];
+            out[1] = acc[1];
+            out[28] = acc[2];
+            out[29] = acc[3];
+        }
+        __syncthreads();
+        for (int o = tid; o < kP1; o += kThreads) da1[off1[o]] = da1d[off1[o]] = 0.f;
     }
 }
 
@@ -2126,10 +2395,35 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
     if (hipError_t e = dX2(84, 120, T.dh2d, W.dh2, w4, T.dh1d, W.h1)) return e;
     if (hipError_t e = dW2(120, 400, T.dh1d, W.x2, W.dh1, T.x2d, w3)) return e;
     if (hipError_t e = dX2(120, 400, T.dh1d, W.dh1, w3, T.dx2d, nullptr)) return e;
-    hipLaunchKernelGGL(lenet_conv_bwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
+    const float* part1 = nullptr;
+    if (g_lenet_conv_valu) {
+        hipLaunchKernelGGL(lenet_conv_bwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
+    } else {
+        // conv2's G_dot and the routed d P1_dot (over P1_dot: each row is read
+        // by its workgroup before its d P1_dot is written), then conv1's G_dot
+        // by the primal's weight-gradient kernel, then d/du from the routed
+        // primal d P1 (the primal backward's, still in W.g1) and its tangent
+        ta.g1g = T.p1d;
+        hipLaunchKernelGGL(lenet_conv_bwd_tan_mfma_kernel, dim3(W.nchunk, S), dim3(kTThreads), 0, st,
+                           ta);
+        ConvArgs c1{};
+        c1.M = M;
+        c1.u = u;
+        c1.r1 = W.r1;
+        c1.g1g = T.p1d;
+        c1.part1 = W.part1;
+        c1.nch1 = W.nch1;
+        c1.chunk = (M + W.nch1 - 1) / W.nch1;
+        hipLaunchKernelGGL(lenet_conv1_wgrad_mfma_kernel, dim3(W.nch1, (S + kW1S - 1) / kW1S),
+                           dim3(256), 0, st, c1, S);
+        part1 = W.part1;
+        if (d_u)
+            hipLaunchKernelGGL(lenet_du_tan_kernel, dim3(W.nchunk, S), dim3(kThreads), 0, st, ta,
+                               (const float*)W.g1, (const float*)T.p1d);
+    }
     hipLaunchKernelGGL(lenet_conv_reduce_kernel,
                        dim3((unsigned)(((int64_t)S * kNConv + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, st, S, W.nchunk, nt, T.part, T.gd, nullptr, 0);
+                       dim3(kThreads), 0, st, S, W.nchunk, nt, T.part, T.gd, part1, W.nch1);
     const int64_t n = nt + (d_u ? (int64_t)M * 784 : 0) + (d_w ? M : 0);
     hipLaunchKernelGGL(lenet_hvp_assemble_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
                        dim3(kThreads), 0, st, sa, params, vec, eps, W.dws, T.gd, T.du, T.nlld, hv,

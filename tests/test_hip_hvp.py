@@ -19,22 +19,28 @@ def _t(x, dtype=torch.float32):
 
 
 def _hvp(family, layers, S, u, z, w, eps, params, vec):
+    """psvi_hvp with its mixed products, and H vec alone (mixed=False: for
+    LeNet no d/du kernel after the tangent backward) -- both returned so each
+    launch path is checked."""
     from psvi.runtime import InnerLoopPlan
 
     plan = InnerLoopPlan(family, layers, S, u.shape[0])
-    hv, du, dw = plan.hvp(_t(u), _t(z.astype(np.int32), torch.int32), _t(w), _t(eps),
-                          _t(params), _t(vec))
+    args = (_t(u), _t(z.astype(np.int32), torch.int32), _t(w), _t(eps), _t(params), _t(vec))
+    hv, du, dw = plan.hvp(*args)
+    hv0, du0, dw0 = plan.hvp(*args, mixed=False)
+    assert du0 is None and dw0 is None
     torch.cuda.synchronize()
-    return hv.cpu().numpy(), du.cpu().numpy(), dw.cpu().numpy()
+    return hv.cpu().numpy(), du.cpu().numpy(), dw.cpu().numpy(), hv0.cpu().numpy()
 
 
 @pytest.mark.parametrize("name", fixture_names("h"))
 def test_hvp_matches_reference_double_backward(name):
     f = load_fixture(name)
     cfg = f["cfg"]
-    hv, du, dw = _hvp(family_of(cfg), plan_layers(cfg), cfg["S"], f["u"], f["z"], f["w"], f["eps"],
-                      f["params0"], f["vec"])
+    hv, du, dw, hv0 = _hvp(family_of(cfg), plan_layers(cfg), cfg["S"], f["u"], f["z"], f["w"],
+                           f["eps"], f["params0"], f["vec"])
     assert l2rel(hv, f["hv"]) < 1e-4, l2rel(hv, f["hv"])
+    assert l2rel(hv0, f["hv"]) < 1e-4, l2rel(hv0, f["hv"])
     assert l2rel(du, f["d_u"]) < 1e-4, l2rel(du, f["d_u"])
     assert l2rel(softmax_T(f["v"].astype(np.float64), dw.astype(np.float64), cfg["N"]),
                  f["d_v"]) < 1e-4
@@ -62,8 +68,9 @@ def test_hvp_fullsize_vs_oracle(case):
     z = rng.integers(0, layers[-1][1], M)
     w = O.coreset_weights(0.2 * rng.standard_normal(M), 800, "softmax").astype(np.float32)
     vec = rng.standard_normal(params.size).astype(np.float32)
-    hv, du, dw = _hvp(family, layers, S, u, z, w, eps, params, vec)
+    hv, du, dw, hv0 = _hvp(family, layers, S, u, z, w, eps, params, vec)
     _, _, hv_o, du_o, dw_o = O.inner_hvp(fam, layers, params, u, z, w, eps, S, vec)
     assert l2rel(hv, hv_o) < 1e-4, l2rel(hv, hv_o)
+    assert l2rel(hv0, hv_o) < 1e-4, l2rel(hv0, hv_o)
     assert l2rel(du, du_o) < 1e-4, l2rel(du, du_o)
     assert l2rel(dw, dw_o) < 1e-4, l2rel(dw, dw_o)

@@ -110,6 +110,9 @@ def test_c5_hvp_rank_samples_match_oracle(case):
     u, z, w = _t(c["u"]), _t(c["z"], torch.int32), _t(c["w"])
     hv, du, dw = plan.hvp(u, z, w, _t(c["eps_loc"]), _t(c["params"]), _t(c["vec"]))
     assert_grad_close(hv.cpu().numpy(), f["hvp"], what="C5 H v")
+    # H v alone (no d/du kernel after the tangent backward)
+    hv0, _, _ = plan.hvp(u, z, w, _t(c["eps_loc"]), _t(c["params"]), _t(c["vec"]), mixed=False)
+    assert_grad_close(hv0.cpu().numpy(), f["hvp"], what="C5 H v (mixed=False)")
     _rows_close(du.cpu().numpy(), f["hvp_du"].reshape(du.shape), "C5 hvp d/du")
     assert l2rel(dw.cpu().numpy(), f["hvp_dw"]) < 1e-4
 
@@ -160,3 +163,11 @@ def test_c5_partial_hvps_of_8_ranks_sum_to_single():
     assert l2rel(hv8.cpu().numpy(), hv1.cpu().numpy()) < 1e-5
     assert l2rel(du8.cpu().numpy(), du1.cpu().numpy()) < 1e-5
     assert l2rel(dw8.cpu().numpy(), dw1.cpu().numpy()) < 1e-5
+    # the same on the H v-only path
+    h1 = single.hvp(u, z, w, eps, params, vec, mixed=False)[0]
+    h8 = torch.zeros_like(h1)
+    for r, (off, cnt) in enumerate(sample_split(S, 8)):
+        h8 += _plan(cnt, M).hvp(u, z, w, local_eps("lenet", LENET, S, off, cnt, eps), params, vec,
+                                mixed=False, include_kl=(r == 0))[0]
+    assert l2rel(h8.cpu().numpy(), h1.cpu().numpy()) < 1e-5
+    assert l2rel(h1.cpu().numpy(), hv1.cpu().numpy()) < 1e-5

@@ -59,13 +59,15 @@ def main():
         e = torch.empty(plan.eps_count, device="cuda")
         randn_(e, 9)
         vec = torch.randn(plan.param_count, device="cuda")
-        plan.hvp(u, z, w, e, params, vec)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.hvp):
-            plan.hvp(u, z, w, e, params, vec)
-        torch.cuda.synchronize()
-        print(f"psvi_hvp: {(time.perf_counter() - t0) / a.hvp * 1e3:.3f} ms", flush=True)
+        for mixed in (False, True):
+            plan.hvp(u, z, w, e, params, vec, mixed=mixed)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.hvp):
+                plan.hvp(u, z, w, e, params, vec, mixed=mixed)
+            torch.cuda.synchronize()
+            print(f"psvi_hvp (mixed={mixed}): {(time.perf_counter() - t0) / a.hvp * 1e3:.3f} ms",
+                  flush=True)
 
 
 if __name__ == "__main__":
