@@ -144,6 +144,8 @@ struct ConvArgs {
     float* g1g;           // MFMA bwd: [S][M][1176] routed d P1 (0 where relu / pool drop it)
     float* part1;         // conv1 weight-gradient partials [S][nch1][156]
     int nch1;
+    const float* wdot;    // tangent forward <TAN>: [S][n_tot] W_dot
+    float* p1dot;         // tangent forward <TAN>: [S][M][1176] P1_dot (conv1 out, conv2 in)
 };
 
 // relu + first-max 2x2 pool of four conv values in window order (0,0) (0,1)
@@ -271,6 +273,11 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a
 // epilogue on registers (window order (0,0) (0,1) (1,0) (1,1), as relu_pool4).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// the conv value at the primal's routed pool offset r (0 where relu / pool drop it)
+__device__ __forceinline__ float routed4(const f32x4& v, int r) {
+    return r == 0 ? v[0] : r == 1 ? v[1] : r == 2 ? v[2] : r == 3 ? v[3] : 0.f;
+}
+
 // conv1 (1 -> 6, 5x5, pad 2) of one image for 8 samples at once: the image's
 // im2col [784 conv positions x 25 taps] (padded image in LDS) times the 8
 // samples' filters [25 taps x 48 (sample, channel) columns] -- the image is
@@ -281,6 +288,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kC1S = 8;           // samples per workgroup (48 columns)
 constexpr int kC1RS = 38;         // padded-image row stride (ds_read_b32 banks: tools/lds_banks)
 constexpr int kC1Img = 32 * kC1RS;
+// TAN: the tangent forward -- W_dot's filters and bias, and instead of relu +
+// pool the value at the primal's routed offset (0 where relu / pool drop it)
+// into a.p1dot, a.r1 read.
+template <bool TAN>
 __global__ __launch_bounds__(256) void lenet_conv1_mfma_kernel(ConvArgs a, int S_loc) {
     __shared__ float img[2][kC1Img];
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(256) void lenet_conv1_mfma_kernel(ConvArgs a, int S
     for (int nt = 0; nt < 3; ++nt) {
         const int n = 16 * nt + r16, sl = n / 6, c = n % 6;
         col_ok[nt] = s0 + sl < S_loc;
-        const float* ws = a.wsamp + (int64_t)min(s0 + sl, S_loc - 1) * a.n_tot;
+        const float* ws = (TAN ? a.wdot : a.wsamp) + (int64_t)min(s0 + sl, S_loc - 1) * a.n_tot;
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
             const int k = 4 * t + kq;
@@ -346,11 +357,14 @@ __global__ __launch_bounds__(256) void lenet_conv1_mfma_kernel(ConvArgs a, int S
 #pragma unroll
             for (int nt = 0; nt < 3; ++nt) {
                 if (!col_ok[nt]) continue;
-                int8_t r;
-                const float v = relu_pool4(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], r);
                 const int64_t o = col_out[nt] + (int64_t)m * kP1 + gw;
-                a.p1[o] = v;
-                a.r1[o] = r;
+                if (TAN) {
+                    a.p1dot[o] = routed4(acc[nt], a.r1[o]);
+                } else {
+                    int8_t r;
+                    a.p1[o] = relu_pool4(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], r);
+                    a.r1[o] = r;
+                }
             }
         }
     }
@@ -372,40 +386,55 @@ __global__ __launch_bounds__(256) void lenet_conv1_mfma_kernel(ConvArgs a, int S
 // 4), channels 6 and 7 zero in B (their A reads clamped to channel 5).
 constexpr int kC2Pair = 2 * kP1;
 constexpr int kC2Q = kC2Pair / 4 / 64 + 1;  // float4 per lane per pair (588 / 64 -> 10)
+//
+// TAN: the tangent forward, X2_dot = conv(P1_dot, W2) + conv(P1, W2_dot) +
+// b2_dot at the primal's routed offsets (a.r2 read, a.x2 written): K = 2 x 150
+// over the pair's P1 | P1_dot maps in LDS (two waves per SIMD).
+template <bool TAN>
 __global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
-    __shared__ __attribute__((aligned(16))) float pm[kC2Pair];
+    __shared__ __attribute__((aligned(16))) float pm[TAN ? 2 * kC2Pair : kC2Pair];
     const int lane = threadIdx.x, r16 = lane & 15, kq = lane >> 4;
     const int s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    const float* w2 = ws + 156 + r16 * 150;
-    float bf[38];
+    auto load_b = [&](const float* w2, float (&b)[38]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 30; ++t) bf[t] = w2[(t / 5) * 25 + (t % 5) * 5 + kq];
+        for (int t = 0; t < 30; ++t) b[t] = w2[(t / 5) * 25 + (t % 5) * 5 + kq];
 #pragma unroll
-    for (int t = 30; t < 36; ++t) bf[t] = w2[(t - 30) * 25 + kq * 5 + 4];
-    bf[36] = w2[kq * 25 + 24];
-    bf[37] = kq < 2 ? w2[(4 + kq) * 25 + 24] : 0.f;
-    const float bias = ws[2556 + r16];
+        for (int t = 30; t < 36; ++t) b[t] = w2[(t - 30) * 25 + kq * 5 + 4];
+        b[36] = w2[kq * 25 + 24];
+        b[37] = kq < 2 ? w2[(4 + kq) * 25 + 24] : 0.f;
+    };
+    float bf[38], bfd[38];
+    load_b(ws + 156 + r16 * 150, bf);
+    const float* wds = TAN ? a.wdot + (int64_t)s * a.n_tot : ws;
+    if (TAN) load_b(wds + 156 + r16 * 150, bfd);
+    const float bias = wds[2556 + r16];
     const int oj = kq, oi = kq * 14, oc = kq * 196, oc2 = min(kq, 1) * 196;
     const int npair = (a.M + 1) >> 1;
     const int p0 = blockIdx.x * a.chunk, p1 = min(npair, p0 + a.chunk);
     if (p0 >= p1) return;
-    const float4* src = reinterpret_cast<const float4*>(a.p1 + (int64_t)s * a.M * kP1);
-    float4* dst = reinterpret_cast<float4*>(pm);
     float4 pf[kC2Q];
-    auto fetch = [&](int p) __attribute__((always_inline)) {
+    auto fetch = [&](const float* base, int p) __attribute__((always_inline)) {
         const int n4 = (min(a.M, 2 * p + 2) - 2 * p) * (kP1 / 4);
-        const float4* sp = src + (int64_t)p * (kC2Pair / 4);
+        const float4* sp = reinterpret_cast<const float4*>(base + (int64_t)s * a.M * kP1) +
+                           (int64_t)p * (kC2Pair / 4);
 #pragma unroll
         for (int q = 0; q < kC2Q; ++q) pf[q] = sp[min(lane + 64 * q, n4 - 1)];
     };
-    for (int p = p0; p < p1; ++p) {
-        fetch(p);
-        __syncthreads();  // the previous pair's reads are done
+    auto store = [&](float* d) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < kC2Q; ++q) {
             const int i = lane + 64 * q;
-            if (i < kC2Pair / 4) dst[i] = pf[q];
+            if (i < kC2Pair / 4) reinterpret_cast<float4*>(d)[i] = pf[q];
+        }
+    };
+    for (int p = p0; p < p1; ++p) {
+        fetch(a.p1, p);
+        __syncthreads();  // the previous pair's reads are done
+        store(pm);
+        if (TAN) {
+            fetch(a.p1dot, p);
+            store(pm + kC2Pair);
         }
         __syncthreads();
         const bool two_img = 2 * p + 1 < a.M;  // uniform
@@ -421,6 +450,8 @@ __global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
                 ro[h] = im * kP1 + (2 * (w / 5) + (q >> 1)) * 14 + 2 * (w % 5) + (q & 1);
                 acc[h] = f32x4{bias, bias, bias, bias};
             }
+            // primal: P1 x W2; tangent: P1_dot x W2, then P1 x W2_dot
+            const float* am = TAN ? pm + kC2Pair : pm;
 #pragma unroll
             for (int t = 0; t < 38; ++t) {
                 const int off = t < 30 ? oj + (t / 5) * 196 + (t % 5) * 14
@@ -428,18 +459,32 @@ __global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
                               : t == 36 ? oc + 60 : oc2 + 4 * 196 + 60;
 #pragma unroll
                 for (int h = 0; h < NT; ++h)
-                    acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(pm[ro[h] + off], bf[t], acc[h], 0, 0, 0);
+                    acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(am[ro[h] + off], bf[t], acc[h], 0, 0, 0);
+            }
+            if (TAN) {
+#pragma unroll
+                for (int t = 0; t < 38; ++t) {
+                    const int off = t < 30 ? oj + (t / 5) * 196 + (t % 5) * 14
+                                  : t < 36 ? oi + (t - 30) * 196 + 4
+                                  : t == 36 ? oc + 60 : oc2 + 4 * 196 + 60;
+#pragma unroll
+                    for (int h = 0; h < NT; ++h)
+                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(pm[ro[h] + off], bfd[t], acc[h], 0, 0, 0);
+                }
             }
 #pragma unroll
             for (int h = 0; h < NT; ++h) {
                 const int g = 4 * (mt + h) + kq;
                 if (g >= 50 || (g >= 25 && !two_img)) continue;
                 const int im = g >= 25, w = g - 25 * im;
-                int8_t r;
-                const float v = relu_pool4(acc[h][0], acc[h][1], acc[h][2], acc[h][3], r);
                 const int64_t o = ((int64_t)s * a.M + 2 * p + im) * kX2 + r16 * 25 + w;
-                a.x2[o] = v;
-                a.r2[o] = r;
+                if (TAN) {
+                    a.x2[o] = routed4(acc[h], a.r2[o]);
+                } else {
+                    int8_t r;
+                    a.x2[o] = relu_pool4(acc[h][0], acc[h][1], acc[h][2], acc[h][3], r);
+                    a.r2[o] = r;
+                }
             }
         };
 #pragma unroll 1
@@ -2139,6 +2184,24 @@ static SampleArgs sample_args(const psvi_plan& p) {
     return a;
 }
 
+// conv1 on the matrix cores, 8 samples per workgroup; then conv2, one wave per
+// workgroup over a chunk of image pairs (>= ~2048 workgroups / ~8192 waves)
+template <bool TAN>
+static void conv_fwd_mfma(const ConvArgs& ca, int S, int M, hipStream_t st) {
+    ConvArgs c1 = ca;
+    const int sg = (S + kC1S - 1) / kC1S;
+    const int n1 = std::max(1, std::min(M, 2048 / sg));
+    c1.chunk = (M + n1 - 1) / n1;
+    hipLaunchKernelGGL(lenet_conv1_mfma_kernel<TAN>, dim3((M + c1.chunk - 1) / c1.chunk, sg),
+                       dim3(256), 0, st, c1, S);
+    ConvArgs c2 = ca;
+    const int np = (M + 1) / 2;
+    const int n2 = std::max(1, std::min(np, 8192 / S));
+    c2.chunk = (np + n2 - 1) / n2;
+    hipLaunchKernelGGL(lenet_conv2_mfma_kernel<TAN>, dim3((np + c2.chunk - 1) / c2.chunk, S),
+                       dim3(64), 0, st, c2);
+}
+
 hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                         const float* params, const float* eps, float* acc, double* nll_out,
                         void* ws, hipStream_t st, const NetOuter* outer) {
@@ -2179,21 +2242,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     if (g_lenet_conv_valu) {
         hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
     } else {
-        // conv1 on the matrix cores, 8 samples per workgroup; then conv2 per
-        // sample (>= ~2048 workgroups each)
-        ConvArgs c1 = ca;
-        const int sg = (S + kC1S - 1) / kC1S;
-        const int n1 = std::max(1, std::min(M, 2048 / sg));
-        c1.chunk = (M + n1 - 1) / n1;
-        hipLaunchKernelGGL(lenet_conv1_mfma_kernel, dim3((M + c1.chunk - 1) / c1.chunk, sg),
-                           dim3(256), 0, st, c1, S);
-        ConvArgs c2 = ca;
-        // one wave per workgroup, a chunk of image pairs each (~8192 waves)
-        const int np = (M + 1) / 2;
-        const int n2 = std::max(1, std::min(np, 8192 / S));
-        c2.chunk = (np + n2 - 1) / n2;
-        hipLaunchKernelGGL(lenet_conv2_mfma_kernel, dim3((np + c2.chunk - 1) / c2.chunk, S),
-                           dim3(64), 0, st, c2);
+        conv_fwd_mfma<false>(ca, S, M, st);
     }
     const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
     const float* Ws = W.wsamp;
@@ -2339,7 +2388,25 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
     ta.x2d = T.x2d;
     ta.part = T.part;
     ta.du = d_u ? T.du : nullptr;
-    hipLaunchKernelGGL(lenet_conv_fwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
+    if (g_lenet_conv_valu) {
+        hipLaunchKernelGGL(lenet_conv_fwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st,
+                           ta);
+    } else {
+        // the forward's kernels in tangent mode: P1_dot from W_dot at conv1's
+        // routed offsets, then X2_dot from [P1_dot | P1] x [W2; W2_dot]
+        ConvArgs ct{};
+        ct.M = M;
+        ct.n_tot = nt;
+        ct.u = u;
+        ct.wsamp = W.wsamp;
+        ct.wdot = T.wdot;
+        ct.p1 = W.p1;
+        ct.p1dot = T.p1d;
+        ct.r1 = W.r1;
+        ct.r2 = W.r2;
+        ct.x2 = T.x2d;
+        conv_fwd_mfma<true>(ct, S, M, st);
+    }
     const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
     const float* Ws = W.wsamp;
     const float* Wd = T.wdot;
