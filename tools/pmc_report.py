@@ -22,7 +22,8 @@ jout = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
 
 
 def short(name):
-    m = re.search(r"psvi::(\w+)", name)
+    """kernel name with its template arguments (instances kept apart)"""
+    m = re.search(r"psvi::(\w+(<[^>]*>)?)", name.replace("(anonymous namespace)::", ""))
     return m.group(1) if m else name[:50]
 
 
