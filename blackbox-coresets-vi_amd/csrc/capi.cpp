@@ -523,6 +523,11 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
             if (hipMalloc((void**)&p->d_mf_slots, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the mean-field gradient slots");
         }
+        if (!rc && p->family == PSVI_FAMILY_FULLCOV && p->fuse_sample && p->tiles_total > 0 &&
+            (hipStreamCreateWithFlags(&p->aux_st, hipStreamNonBlocking) != hipSuccess ||
+             hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+             hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess))
+            rc = fail(PSVI_EUNSUP, "cannot create the inner loop's conversion stream");
         if (!rc && family == PSVI_FAMILY_LENET) {
             const size_t bytes = lenet_ws(*p, nullptr).bytes;
             if (hipMalloc(&p->d_lenet_ws, bytes) != hipSuccess)
@@ -551,6 +556,9 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_upd) (void)hipFree(p->d_upd);
     if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);
     if (p->d_mf_slots) (void)hipFree(p->d_mf_slots);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->aux_st) (void)hipStreamDestroy(p->aux_st);
     delete p;
     return 0;
 }
@@ -918,11 +926,22 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
                                        2 * align256(sizeof(float) * (size_t)es))
                             : nullptr;
     if (T == 0) return 0;
+    // packed -> tiled state on the plan's conversion stream, behind x_0 and the
+    // first network step (joined before the first update)
+    bool join = false;
+    if (ts && p->aux_st) {
+        HIP_TRY(hipEventRecord(p->ev_fork, st));
+        HIP_TRY(hipStreamWaitEvent(p->aux_st, p->ev_fork, 0));
+        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, p->aux_st));
+        HIP_TRY(hipEventRecord(p->ev_join, p->aux_st));
+        join = true;
+    } else if (ts) {
+        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st));
+    }
     const float* e = eps_t(0);
     if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
     HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double) * (size_t)T, st));
     HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
-    if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st));
     for (int t = 0; t < T; ++t) {
         h.step = hp->step + t;
         if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
@@ -936,12 +955,16 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         if (tm) HIP_TRY(loop_event(0, st));
         const float* en = t + 1 < T ? (eps ? eps + (size_t)(t + 1) * p->Peps : en_buf) : nullptr;
         if (tm) HIP_TRY(loop_event(1, st));
+        if (join) {
+            HIP_TRY(hipStreamWaitEvent(st, p->ev_join, 0));
+            join = false;
+        }
+        // the last step (no next sample) writes corr / m / v back to the packed arrays
         HIP_TRY(launch_mvn_update(*p, e, g, params, adam_m, adam_v, &h, elbo_out + t, nullptr, 1,
-                                  en, en ? x : nullptr, st, ts));
+                                  en, en ? x : nullptr, st, ts, ts && !en));
         if (tm) HIP_TRY(loop_event(1, st));
         e = en;
     }
-    if (ts) HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, false, st));
     return 0;
 }
 

@@ -413,15 +413,15 @@ __global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
     const int npair = (a.M + 1) >> 1;
     const int p0 = blockIdx.x * a.chunk, p1 = min(npair, p0 + a.chunk);
     if (p0 >= p1) return;
-    float4 pf[kC2Q];
-    auto fetch = [&](const float* base, int p) __attribute__((always_inline)) {
+    // the pair's maps HBM -> LDS (float4 loads in flight together, then stored;
+    // one function-local array, so it stays in registers)
+    auto copy_pair = [&](const float* base, int p, float* d) __attribute__((always_inline)) {
         const int n4 = (min(a.M, 2 * p + 2) - 2 * p) * (kP1 / 4);
         const float4* sp = reinterpret_cast<const float4*>(base + (int64_t)s * a.M * kP1) +
                            (int64_t)p * (kC2Pair / 4);
+        float4 pf[kC2Q];
 #pragma unroll
         for (int q = 0; q < kC2Q; ++q) pf[q] = sp[min(lane + 64 * q, n4 - 1)];
-    };
-    auto store = [&](float* d) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < kC2Q; ++q) {
             const int i = lane + 64 * q;
@@ -429,13 +429,9 @@ __global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
         }
     };
     for (int p = p0; p < p1; ++p) {
-        fetch(a.p1, p);
         __syncthreads();  // the previous pair's reads are done
-        store(pm);
-        if (TAN) {
-            fetch(a.p1dot, p);
-            store(pm + kC2Pair);
-        }
+        copy_pair(a.p1, p, pm);
+        if (TAN) copy_pair(a.p1dot, p, pm + kC2Pair);
         __syncthreads();
         const bool two_img = 2 * p + 1 < a.M;  // uniform
         // NT row tiles from tile mt on: 38 MFMA steps each, then relu + pool

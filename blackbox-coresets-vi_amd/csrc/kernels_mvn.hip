@@ -381,7 +381,9 @@ struct UpdShared {
 // per c-block, x_next[s][r] += sum_c eps_next[s][c] L_new[r][c] on a second
 // MFMA GEMM (L_new tile through the LDS tile region, eps_next fragments
 // straight from L2 into registers), partial sums to the chunk's slot.
-template <bool GRAD, int MODE, bool FUSE, bool TILED>
+// PKO (tiled state, no fused sample: an inner loop's last step): corr / m / v
+// read from the tiled state, written back to the packed arrays
+template <bool GRAD, int MODE, bool FUSE, bool TILED, bool PKO = false>
 __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                                           UpdShared<MODE == 2>& sh) {
     constexpr bool MULTI = MODE == 2, TWOH = MODE == 1;
@@ -589,8 +591,10 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
         if (TILED) {
             // D[i = c][j = r] (j = lane & 31, i = (q&3) + 8(q>>2) + 4h) is already the
             // tile's fragment order: Adam on the accumulators, float4 in / out
+            static_assert(!PKO || !FUSE, "packed-out: the last step samples nothing");
             const int r = ch.r0 + 32 * wr + l32;
             const bool rv = r >= 1 && r <= n - 2 && !(a.abl & 8);
+            float kp[PKO ? 16 : 1], km[PKO ? 16 : 1], kv[PKO ? 16 : 1];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int cb = (ch.k0 + ti) * UB + 32 * wc + 8 * g + 4 * h;
@@ -612,7 +616,14 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                     mn[i] = mm;
                     vn[i] = vv;
                 }
-                if (!(a.abl & 8)) {
+                if (PKO) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        kp[4 * g + i] = pn[i];
+                        km[4 * g + i] = mn[i];
+                        kv[4 * g + i] = vn[i];
+                    }
+                } else if (!(a.abl & 8)) {
                     *reinterpret_cast<float4*>(a.tp + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
                     *reinterpret_cast<float4*>(a.tm + o) = make_float4(mn[0], mn[1], mn[2], mn[3]);
                     *reinterpret_cast<float4*>(a.tv + o) = make_float4(vn[0], vn[1], vn[2], vn[3]);
@@ -623,6 +634,37 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
             }
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+            if (PKO) {
+                // fragment -> [r][c] through LDS, then the rows' float4 segments
+                // to the packed triangle (as the packed epilogue below)
+                float* T = Es;
+                const int cb = (ch.k0 + ti) * UB + 4 * col4;
+#pragma unroll
+                for (int ai = 0; ai < 3; ++ai) {
+                    const float* kk = ai == 0 ? kp : ai == 1 ? km : kv;
+                    float* dst = ai == 0 ? a.params : ai == 1 ? a.m : a.v;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        *reinterpret_cast<float4*>(&T[(32 * wr + l32) * TLD + 32 * wc + 8 * g + 4 * h]) =
+                            make_float4(kk[4 * g], kk[4 * g + 1], kk[4 * g + 2], kk[4 * g + 3]);
+                    __syncthreads();
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int rr = ch.r0 + srow + 16 * j;
+                        if (!rown[j] || cb >= rr) continue;
+                        const int o = rowp[j] + cb;
+                        const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
+                        if (cb + 3 < rr) {
+                            *reinterpret_cast<float4*>(dst + o) = d4;
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 3; ++i)
+                                if (cb + i < rr) dst[o + i] = f4get(d4, i);
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
             return;
         }
         // D[i = c][j = r]: j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h  ->  T[r][c] in Es
@@ -822,7 +864,7 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
     }
 }
 
-template <bool GRAD, int MODE, bool FUSE = false, bool TILED = false>
+template <bool GRAD, int MODE, bool FUSE = false, bool TILED = false, bool PKO = false>
 __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_kernel(UpdArgs a) {
     __shared__ __attribute__((aligned(16))) UpdShared<MODE == 2> sh;
     UPD_STAMP(0, __builtin_amdgcn_s_memtime());
@@ -830,7 +872,7 @@ __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_ker
     UPD_STAMP(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
     UPD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const UpdChunk ch = a.chunks[blockIdx.x];
-    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE, FUSE, TILED>(a, ch, sh);  // XCD padding chunks are empty
+    if (ch.k1 > ch.k0) upd_chunk<GRAD, MODE, FUSE, TILED, PKO>(a, ch, sh);  // XCD padding chunks are empty
     UPD_STAMP(3, __builtin_amdgcn_s_memtime());
     UPD_STAMP(13, __builtin_amdgcn_s_memrealtime());
 }
@@ -1284,7 +1326,13 @@ static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
     }
 }
 
-// packed <-> tiled corr / m / v: one thread per tiled float4 of each array
+// packed <-> tiled corr / m / v: one workgroup per 64 x 64 tile.  The tile's
+// 64 row segments are contiguous in the packed triangle (row r from poff + 2n +
+// r (r - 1) / 2, columns c < r): they go through LDS (row stride 65) between
+// row-major packed accesses and float4 fragment-order tiled accesses
+// (fragment float4 q = (w * 4 + g) * 64 + lane holds row 32 (w >> 1) + (lane
+// & 31), columns 32 (w & 1) + 8 g + 4 (lane >> 5) + 0..3).  Entries outside
+// the triangle (or rows 0, n - 1) are zero in the tiled copy.
 struct ConvArgs {
     float* params;
     float* m;
@@ -1293,43 +1341,82 @@ struct ConvArgs {
     int64_t tfloats;    // tiles_total * 4096
     int L;
     MvnLayerArgs lay[kMaxL];
-    int nb[kMaxL];
 };
 
 template <bool TO_TILED>
 __global__ __launch_bounds__(256) void mvn_tile_convert_kernel(ConvArgs c) {
-    const int64_t q = blockIdx.x * (int64_t)256 + threadIdx.x;  // float4 index
-    if (q * 4 >= c.tfloats) return;
-    const int64_t tile = q / 1024;
-    const int f = (int)(q % 1024), w = f / 256, g = (f / 64) & 3, lane = f & 63;
+    __shared__ float T[64 * 65];
+    const int tid = threadIdx.x;
+    const int64_t tile = blockIdx.x;
     int l = 0;
-    while (l + 1 < c.L && tile >= c.lay[l + 1].tbase) ++l;
-    const int64_t tb = tile - c.lay[l].tbase;
+#pragma unroll
+    for (int j = 1; j < kMaxL; ++j)
+        if (j < c.L && tile >= c.lay[j].tbase) l = j;
+    int n = c.lay[0].n;
+    int64_t poff = c.lay[0].poff, tbase = c.lay[0].tbase;
+#pragma unroll
+    for (int j = 1; j < kMaxL; ++j)
+        if (j == l) {
+            n = c.lay[j].n;
+            poff = c.lay[j].poff;
+            tbase = c.lay[j].tbase;
+        }
+    const int64_t tb = tile - tbase;
     int b = (int)((sqrtf(8.f * (float)tb + 1.f) - 1.f) * 0.5f);
     while ((int64_t)(b + 1) * (b + 2) / 2 <= tb) ++b;
     while ((int64_t)b * (b + 1) / 2 > tb) --b;
     const int k = (int)(tb - (int64_t)b * (b + 1) / 2);
-    const int n = c.lay[l].n;
-    const int r = 64 * b + 32 * (w >> 1) + (lane & 31);
-    const int c0 = 64 * k + 32 * (w & 1) + 8 * g + 4 * (lane >> 5);
-    const int64_t rowp = c.lay[l].poff + 2 * (int64_t)n + (int64_t)r * (r - 1) / 2;
-    const bool rv = r >= 1 && r <= n - 2;
+    // row-major side: thread -> (row 16 pass + tid / 16, columns 4 (tid % 16) + 0..3)
+    const int cq = 4 * (tid & 15);
+    // fragment side: thread -> float4 q = tid + 256 j
     float* arr[3] = {c.params, c.m, c.v};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        float4* t = reinterpret_cast<float4*>(c.tstate + a * c.tfloats) + q;
+#pragma unroll 1
+    for (int ai = 0; ai < 3; ++ai) {
+        float* A = arr[ai];
+        float4* tt = reinterpret_cast<float4*>(c.tstate + ai * c.tfloats + tile * 4096);
         if (TO_TILED) {
-            float e[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) e[i] = rv && c0 + i < r ? arr[a][rowp + c0 + i] : 0.f;
-            *t = make_float4(e[0], e[1], e[2], e[3]);
+            for (int ps = 0; ps < 4; ++ps) {
+                const int i = 16 * ps + (tid >> 4), r = 64 * b + i;
+                const bool rv = r >= 1 && r <= n - 2;
+                const int64_t rowp = poff + 2 * (int64_t)n + (int64_t)r * (r - 1) / 2 + 64 * k;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int cc = 64 * k + cq + e;
+                    T[i * 65 + cq + e] = rv && cc < r ? A[rowp + cq + e] : 0.f;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int q = tid + 256 * j, w = q >> 8, g = (q >> 6) & 3, lane = q & 63;
+                const int i = 32 * (w >> 1) + (lane & 31), c0 = 32 * (w & 1) + 8 * g + 4 * (lane >> 5);
+                tt[q] = make_float4(T[i * 65 + c0], T[i * 65 + c0 + 1], T[i * 65 + c0 + 2],
+                                    T[i * 65 + c0 + 3]);
+            }
         } else {
-            const float4 v4 = *t;
-            const float e[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (rv && c0 + i < r) arr[a][rowp + c0 + i] = e[i];
+            for (int j = 0; j < 4; ++j) {
+                const int q = tid + 256 * j, w = q >> 8, g = (q >> 6) & 3, lane = q & 63;
+                const int i = 32 * (w >> 1) + (lane & 31), c0 = 32 * (w & 1) + 8 * g + 4 * (lane >> 5);
+                const float4 v4 = tt[q];
+                T[i * 65 + c0] = v4.x;
+                T[i * 65 + c0 + 1] = v4.y;
+                T[i * 65 + c0 + 2] = v4.z;
+                T[i * 65 + c0 + 3] = v4.w;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int ps = 0; ps < 4; ++ps) {
+                const int i = 16 * ps + (tid >> 4), r = 64 * b + i;
+                const bool rv = r >= 1 && r <= n - 2;
+                const int64_t rowp = poff + 2 * (int64_t)n + (int64_t)r * (r - 1) / 2 + 64 * k;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (rv && 64 * k + cq + e < r) A[rowp + cq + e] = T[i * 65 + cq + e];
+            }
         }
+        __syncthreads();  // T reused by the next array
     }
 }
 
@@ -1344,7 +1431,7 @@ hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, 
     c.L = p.L;
     fill_layers(p, c.lay);
     if (c.tfloats == 0) return hipSuccess;
-    const dim3 grid((unsigned)((c.tfloats / 4 + 255) / 256));
+    const dim3 grid((unsigned)p.tiles_total);
     if (to_tiled)
         hipLaunchKernelGGL(mvn_tile_convert_kernel<true>, grid, dim3(256), 0, st, c);
     else
@@ -1397,7 +1484,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
-                             float* tstate) {
+                             float* tstate, bool packed_out) {
     UpdArgs a{};
     a.chunks = p.d_upd;
     a.eps = eps;
@@ -1487,6 +1574,9 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             constexpr int spb = kRedSpb;
             hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_ufrb, (f.S + spb - 1) / spb),
                                dim3(256), 0, st, p.d_ufrb, p.d_upd_part, f, x_next);
+        } else if (packed_out) {
+            if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1, false, true, true>), grid, block, 0, st, a);
+            else hipLaunchKernelGGL((mvn_update_kernel<false, 0, false, true, true>), grid, block, 0, st, a);
         } else {
             if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1, false, true>), grid, block, 0, st, a);
             else hipLaunchKernelGGL((mvn_update_kernel<false, 0, false, true>), grid, block, 0, st, a);

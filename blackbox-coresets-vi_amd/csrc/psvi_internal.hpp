@@ -282,6 +282,11 @@ struct psvi_plan {
     // [s_cnt[rank]][mchunks][n_tot]; one writer per element, summed in a fixed
     // order by the update (run-to-run bitwise reproducible, no float atomics)
     float* d_mf_slots = nullptr;
+    // tiled-state inner loops: the packed -> tiled conversion runs on aux_st,
+    // forked from / joined to the caller's stream by the two events, behind the
+    // first sample and network step (not re-entrant across host threads)
+    hipStream_t aux_st = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace psvi {
@@ -314,7 +319,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
-                             float* tstate = nullptr);
+                             float* tstate = nullptr, bool packed_out = false);
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
                                    float* tstate, bool to_tiled, hipStream_t st);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
