@@ -1,6 +1,16 @@
 """flow_psvi.experiment_driver (psvi/experiments/flow_psvi.py:357-454) over the
 methods the HIP path runs: the PSVI variants' run_psvi and the MFVI
-baselines.  No CLI: method_args is the reference's dict of parsed arguments."""
+baselines.  No CLI: method_args is the reference's dict of parsed arguments.
+
+Multi-GPU (one process per GPU): every rank calls
+experiment_driver with the same arguments and its ``world`` / ``rank`` (or
+``method_args["world"]`` / ``["rank"]``) and, optionally, a collective
+backend ``comm`` (psvi.runtime.sharded: TorchDistComm over RCCL by default,
+HostStagedComm for gloo).  The PSVI methods then split their MC samples over
+the ranks (the objectives, HVPs and trainers all-reduce the ranks' shares:
+every rank holds the same u, v and network after every step); the MFVI
+baselines have no sample-sharded form and run whole on every rank.  Rank 0
+alone writes the results files."""
 from ..inference import (PSVI, PSVIAV, PSVIAFixedU, PSVIFixedU, PSVIFreeV, PSVILearnV,
                          PSVI_Ablated, PSVI_No_IW, PSVI_No_Rescaling, run_mfvi, run_mfvi_subset)
 from .experiments_utils import read_dataset, rec_dd, write_to_files
@@ -27,10 +37,17 @@ inf_dict = {
 }
 
 
-def experiment_driver(datasets, methods, method_args, write=True):
+def experiment_driver(datasets, methods, method_args, write=True, world=None, rank=None,
+                      comm=None):
     """For each dataset, method, trial and coreset size: run the method with
     the reference's keyword set and store its results dict at
-    results[dataset][method][size][trial]; coreset-free methods use size -1."""
+    results[dataset][method][size][trial]; coreset-free methods use size -1.
+    world / rank / comm: this process's place in a multi-GPU run (above)."""
+    world = int(method_args.get("world", 1) if world is None else world)
+    rank = int(method_args.get("rank", 0) if rank is None else rank)
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    shard = dict(world=world, rank=rank, comm=comm) if world > 1 else {}
     results = rec_dd()
     for dnm in datasets:
         x, y, xt, yt, N, D, train_dataset, test_dataset, nc = read_dataset(dnm, method_args)
@@ -43,9 +60,11 @@ def experiment_driver(datasets, methods, method_args, write=True):
                                        and method_args.get("compute_weights_entropy", True))
             sizes = (method_args["coreset_sizes"]
                      if nm_alg.startswith(("psvi", "opsvi", "mfvi_subset")) else [-1])
+            extra = shard if nm_alg.startswith("psvi") else {}
             for t in range(method_args["num_trials"]):
                 for ps in sizes:
                     results[dnm][nm_alg][ps][t] = inf_dict[nm_alg](
+                        **extra,
                         mc_samples=method_args["mc_samples"],
                         num_epochs=method_args["num_epochs"],
                         data_minibatch=method_args["data_minibatch"],
@@ -67,7 +86,7 @@ def experiment_driver(datasets, methods, method_args, write=True):
                         n_layers=method_args.get("n_layers", 1),
                         train_dataset=train_dataset, test_dataset=test_dataset, dnm=dnm, nc=nc,
                         learn_z=method_args.get("learn_z", False))
-    if write:
+    if write and rank == 0:
         return write_to_files(results, method_args.get("fnm", "results"),
                               method_args.get("results_folder", "results"))
     return results

@@ -141,3 +141,38 @@ def c5_global_eps(case, fill=np.nan):
             lo += s_cnt * k
     assert go == out.size and lo == case["eps_loc"].size
     return out
+
+
+def lenet_route_margins(case, rows, S=None):
+    """Smallest route margin of each pseudo-image row over the case's samples
+    (float64 forward of the oracle, psvi_oracle.lenet_forward): per conv layer
+    the gap between a max-pool window's two largest relu'd values (a pool tie)
+    and the magnitude of the window's maximum pre-activation (the relu kink),
+    and per hidden linear layer the pre-activations' magnitude -- each relative
+    to the layer's mean |pre-activation|.  A row whose margin is at fp32's
+    rounding reach (~1e-6) can route its gradient differently in fp32 and fp64
+    (another window position, or a unit on the other side of the kink)."""
+    import psvi_oracle as O
+
+    S = case["s_cnt"] if S is None else S
+    rows = list(rows)
+    Xl = O.lenet_sample(case["params"], case["eps_loc"], S)
+    u = np.asarray(case["u"], np.float64).reshape(-1, 1, 28, 28)[rows]
+    _, cache = O.lenet_forward(Xl, u, S)
+    a1 = O._conv(cache["x0"], cache["W1"], Xl[0]["X"][:, 150:], 2)
+    a2 = O._conv(cache["p1"], cache["W2"], Xl[1]["X"][:, 2400:], 0)
+    best = np.full(len(rows), np.inf)
+    for a in (a1, a2):
+        s_, m_, c_, h_, w_ = a.shape
+        win = a.reshape(s_, m_, c_, h_ // 2, 2, w_ // 2, 2).transpose(0, 1, 2, 3, 5, 4, 6)
+        win = win.reshape(s_, m_, -1, 4)
+        srt = np.sort(np.maximum(win, 0.0), -1)
+        scale = np.abs(a).mean()
+        tie = np.where(srt[..., 3] > 0, srt[..., 3] - srt[..., 2], np.inf) / scale
+        kink = np.abs(np.sort(win, -1)[..., 3]) / scale
+        best = np.minimum(best, np.minimum(tie, kink).min(axis=(0, 2)))
+    hs = cache["hs"]
+    for l, off in ((0, 48000), (1, 10080)):
+        a = np.einsum("smi,soi->smo", hs[l], cache["Wf"][l]) + Xl[2 + l]["X"][:, off:][:, None, :]
+        best = np.minimum(best, (np.abs(a) / np.abs(a).mean()).min(axis=(0, 2)))
+    return best

@@ -45,12 +45,22 @@ def _plan(S, M, world=1, rank=0):
     return InnerLoopPlan("lenet", LENET, S, M, world=world, rank=rank)
 
 
-def _rows_close(got, want, what, tol=1e-4, max_frac=0.01):
-    """Per-row (per pseudo-image) comparison of d/du: at C5's size a few
-    (sample, image) pairs sit on a max-pool tie or a ReLU kink where fp32 and
-    fp64 route the gradient differently (tests/test_hip_fullsize.py has the
-    same boundary at C4); those rows are reported and bounded in number, every
-    other row must match to tol."""
+# fp32's rounding reach on a route margin (relative to the layer's mean
+# |pre-activation|): conv sums of 25 / 150 products
+ROUTE_MARGIN = 1e-6
+
+
+def _rows_close(got, want, what, case=None, tol=1e-4, max_frac=0.01):
+    """Per-row (per pseudo-image) comparison of d/du: every row must match to
+    tol, except a row whose images sit, for some sample, on a max-pool tie or a
+    ReLU kink within fp32's rounding reach of the float64 forward -- there fp32
+    and fp64 route the gradient differently (tests/test_hip_fullsize.py has the
+    same boundary at C4).  With the case given, each such row is checked to
+    have that margin (golden_util.lenet_route_margins < ROUTE_MARGIN): an
+    indexing error confined to a few images cannot pass as one; without it the
+    rows are only counted (<= max_frac)."""
+    from golden_util import lenet_route_margins
+
     got = np.asarray(got, np.float64).reshape(want.shape[0], -1)
     want = np.asarray(want, np.float64).reshape(want.shape[0], -1)
     scale = np.linalg.norm(want) / np.sqrt(want.shape[0])
@@ -59,7 +69,14 @@ def _rows_close(got, want, what, tol=1e-4, max_frac=0.01):
     print(f"{what}: rows over {tol:g}: {int(bad.sum())}/{len(err)}, worst {err.max():.2e} "
           f"(row {int(err.argmax())}), median {np.median(err):.2e}, total l2rel "
           f"{np.linalg.norm(got - want) / np.linalg.norm(want):.2e}")
-    assert bad.mean() <= max_frac, what
+    if case is None:
+        assert bad.mean() <= max_frac, what
+        return
+    rows = np.flatnonzero(bad)
+    if len(rows):
+        m = lenet_route_margins(case, rows)
+        print(f"{what}: route margins of those rows {dict(zip(rows.tolist(), np.round(m, 9)))}")
+        assert (m < ROUTE_MARGIN).all(), (what, rows[m >= ROUTE_MARGIN])
 
 
 def test_c5_inner_rank_shard_matches_oracle(case):
@@ -100,7 +117,7 @@ def test_c5_outer_sharded_passes_match_oracle(case):
         full[k][c["s_off"]:c["s_off"] + c["s_cnt"]] = torch.from_numpy(c[k])
     g = so.local_grads(M, x_all, z_all, w_all, e, params, full["cp"], full["cd"], full["ck"])
     assert_grad_close(g["grad"].cpu().numpy(), f["outer_grad"], what="C5 outer grad")
-    _rows_close(g["grad_u"].cpu().numpy(), f["outer_grad_u"], "C5 outer d/du")
+    _rows_close(g["grad_u"].cpu().numpy(), f["outer_grad_u"], "C5 outer d/du", case=c)
     assert l2rel(g["grad_w"].cpu().numpy(), f["outer_grad_w"]) < 1e-4
 
 
@@ -113,7 +130,7 @@ def test_c5_hvp_rank_samples_match_oracle(case):
     # H v alone (no d/du kernel after the tangent backward)
     hv0, _, _ = plan.hvp(u, z, w, _t(c["eps_loc"]), _t(c["params"]), _t(c["vec"]), mixed=False)
     assert_grad_close(hv0.cpu().numpy(), f["hvp"], what="C5 H v (mixed=False)")
-    _rows_close(du.cpu().numpy(), f["hvp_du"].reshape(du.shape), "C5 hvp d/du")
+    _rows_close(du.cpu().numpy(), f["hvp_du"].reshape(du.shape), "C5 hvp d/du", case=c)
     assert l2rel(dw.cpu().numpy(), f["hvp_dw"]) < 1e-4
 
 

@@ -127,3 +127,71 @@ def test_c3_inner_loop_stream_matches_oracle():
     print(f"C3 T={T}: params l2rel vs oracle stream {e_s:.2e} chunked {e_c:.2e}")
     assert e_s < 2 * e_c + 1e-6 and e_s < 1e-3
     assert np.abs(ps - o_traj[-1]).max() <= 2 * T * 1e-3
+
+
+@pytest.mark.parametrize("kind", ["higher", "hypergrad"])
+def test_stream_step_gradient_matches_oracle(kind):
+    """The gradient the streaming kernel applies, pinned to the float64
+    oracle at C3: one tiled stream step from zero Adam moments leaves m = (1 -
+    beta1) g exactly (one fp32 multiply), so g = m / (1 - beta1) is the
+    kernel's own gradient of the negative ELBO (mean / sd from the diagonal
+    tiles, corr from the dL GEMM, KL included).  Checked in its two factors:
+      * the update arithmetic: g against the oracle's update phase
+        (mvn_grad_from_G) on the network's G, at 1e-5;
+      * the network's per-sample G against the oracle's, at 1e-4, except
+        samples on a ReLU kink (fp32 and fp64 may take the other mask there:
+        margin < 1e-4 in their own rounding units, and rare) --
+    and, when no sample sits on a kink, g against the whole oracle gradient at
+    1e-4 (at this seed the first layer has kink samples: its end-to-end error
+    is the mask flip's, 1e-3, for the chunked update as for the stream)."""
+    from golden_util import assert_grad_close
+    from psvi.runtime import InnerLoopPlan
+
+    layers, S, M = [(64, 40), (40, 40), (40, 2)], 128, 100
+    rng = np.random.default_rng(21)
+    _, p0, _, _ = _case(layers, S, 21)
+    u = rng.standard_normal((M, 64)).astype(np.float32)
+    z = rng.integers(0, 2, M).astype(np.int32)
+    w = O.coreset_weights(0.3 * rng.standard_normal(M), 800).astype(np.float32)
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    e0 = rng.standard_normal(plan.eps_count).astype(np.float32)
+    e1 = rng.standard_normal(plan.eps_count).astype(np.float32)
+    t = lambda a, d=torch.float32: torch.tensor(a, dtype=d, device=DEV)
+    p = t(p0)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    x = torch.empty(plan.xshard_count, device=DEV)
+    g = torch.zeros(plan.xrecv_count, device=DEV)
+    nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+    kl = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.mvn_sample(t(e0), p, x)
+    plan.mvn_net(t(u), t(z, torch.int32), t(w), x, g, nll)
+    G = g.view(S, -1).cpu().numpy().astype(np.float64)
+    ts = plan.tiled_state()
+    plan.tiled_convert(p, m, v, ts, True)
+    xn = torch.empty(plan.xshard_count, device=DEV)
+    plan.mvn_update_tiled(t(e0), g, p, m, v, ts, step=1, lr=1e-3, kind=kind, kl_out=kl,
+                          eps_next=t(e1), x_next=xn)
+    plan.tiled_convert(p, m, v, ts, False)
+    torch.cuda.synchronize()
+    omb1 = np.float32(1.0) - np.float32(0.9)
+    grad = m.cpu().numpy().astype(np.float64) / np.float64(omb1)
+    # the update arithmetic on the same G
+    assert_grad_close(grad, O.mvn_grad_from_G(layers, p0, G, e0, S), l2tol=1e-5,
+                      what=f"stream-step gradient from G ({kind})")
+    # the network's G per sample
+    Ws, bs = O._split(layers, O._sample("mvn", layers, p0.astype(np.float64),
+                                        e0.astype(np.float64), S))
+    val, dWs, dbs = O.net_forward_backward(u.astype(np.float64), z, w.astype(np.float64), Ws, bs)
+    Go = np.concatenate([np.concatenate([dW.reshape(S, -1), db], 1) for dW, db in zip(dWs, dbs)], 1)
+    per = np.linalg.norm(G - Go, axis=1) / np.maximum(np.linalg.norm(Go, axis=1), 1e-30)
+    bad = np.where(per > 1e-4)[0]
+    marg = O.relu_margin(u.astype(np.float64), Ws, bs)
+    good = np.setdiff1d(np.arange(S), bad)
+    print(f"C3 stream step ({kind}): {len(bad)} kink samples {bad[:8]} margins {marg[bad][:8]}; "
+          f"good samples' G l2rel {l2rel(G[good], Go[good]):.2e}")
+    assert len(bad) <= 0.02 * S and np.all(marg[bad] < 1e-4), (bad, marg[bad])
+    assert l2rel(G[good], Go[good]) < 1e-5
+    lv, og = O.mvn_elbo_grad(layers, p0, u, z, w, e0, S)
+    assert rel(nll.item() + kl.item(), lv) < 1e-5
+    if len(bad) == 0:
+        assert_grad_close(grad, og, what=f"stream-step gradient ({kind})")

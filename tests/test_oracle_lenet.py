@@ -69,3 +69,15 @@ def test_lenet_gradient_finite_difference():
                 fd = (fp - fm) / (2 * h)
                 assert abs(fd - g[base + i]) <= 1e-5 * max(1.0, abs(fd)), (base, i, fd, g[base + i])
         po += 2 * n
+
+
+def test_route_margins_flag_the_c5_tie_row():
+    """golden_util.lenet_route_margins (the C5 d/du outlier check): pseudo-image
+    153 of the C5 rank case sits on a conv1 max-pool tie (relative gap ~1e-7:
+    fp32 and fp64 can pick different window positions); typical rows sit
+    orders of magnitude further from any tie or kink."""
+    from golden_util import c5_lenet_case, lenet_route_margins
+
+    m = lenet_route_margins(c5_lenet_case(), [153, 0, 1, 10, 499])
+    assert m[0] < 1e-6
+    assert (m[1:] > 1e-6).all(), m
