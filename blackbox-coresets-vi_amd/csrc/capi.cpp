@@ -576,11 +576,10 @@ struct OuterWs {
 };
 static OuterWs outer_ws(const psvi_plan* p, void* ws);
 
-// psvi_hvp workspace: the step workspace (x), x_dot [S][n_tot], the tangent
-// parameters [P] (full-cov), G and G_dot [S][n_tot], d_u parts [S][M][D],
-// NLL_dot [S][M]
+// psvi_hvp workspace: the step workspace (x), x_dot [S][n_tot], G and G_dot
+// [splits][S][n_tot], d_u parts [S][M][D], NLL_dot [S][M]
 struct HvpWs {
-    float *xd, *T, *G, *Gd, *du, *nlld;
+    float *xd, *G, *Gd, *du, *nlld;
     size_t bytes;
 };
 static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
@@ -598,9 +597,9 @@ static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
         return r;
     };
     o.xd = (float*)take(sizeof(float) * S * nt);
-    o.T = (float*)take(p->family == PSVI_FAMILY_FULLCOV ? sizeof(float) * (size_t)p->P : 0);
-    o.G = (float*)take(sizeof(float) * S * nt);
-    o.Gd = (float*)take(sizeof(float) * S * nt);
+    const size_t ns = rop_splits(*p);  // the R-op's row-block slots (summed into slot 0)
+    o.G = (float*)take(sizeof(float) * ns * S * nt);
+    o.Gd = (float*)take(sizeof(float) * ns * S * nt);
     o.du = (float*)take(sizeof(float) * S * M * D);
     o.nlld = (float*)take(sizeof(float) * S * M);
     o.bytes = off;
@@ -1146,14 +1145,14 @@ int psvi_hvp_partial(const psvi_plan* p, const float* u, const int32_t* z, const
         x = (float*)ws;
         // x = mean + L eps; x_dot = v_mean + (sigmoid(sd) v_sd) eps + v_corr eps
         HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
-        HIP_TRY(launch_hvp_tangent(*p, params, vec, o.T, st));
-        HIP_TRY(launch_mvn_fwd(*p, eps, o.T, o.xd, st, true));
+        HIP_TRY(launch_mvn_fwd(*p, eps, vec, o.xd, st, params));
     }
     HIP_TRY(launch_net_rop(*p, u, z, w, x, o.xd, params, vec, eps, o.G, o.Gd,
                            du_out ? o.du : nullptr, dw_out ? o.nlld : nullptr, st));
-    if (p->family == PSVI_FAMILY_FULLCOV)  // J^T G_dot (mean, sd, corr), no KL
+    if (p->family == PSVI_FAMILY_FULLCOV)  // J^T G_dot (mean, sd, corr; + the corr KL block)
         HIP_TRY(launch_mvn_update(*p, eps, o.Gd, const_cast<float*>(params), nullptr, nullptr,
-                                  nullptr, nullptr, hv_out, 0, nullptr, nullptr, st));
+                                  nullptr, nullptr, hv_out, 0, nullptr, nullptr, st, nullptr,
+                                  false, include_kl ? vec : nullptr));
     HIP_TRY(launch_hvp_assemble(*p, params, vec, eps, o.G, o.Gd, o.du, o.nlld, hv_out, du_out,
                                 dw_out, st, include_kl != 0));
     return 0;

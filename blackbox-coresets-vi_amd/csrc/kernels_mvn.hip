@@ -53,7 +53,8 @@ struct FwdArgs {
     float* part;      // split-K partial slots [n_items][S][32]
     int ldx, S;
     int64_t e_total;  // floats in eps (load guards)
-    int raw_diag;     // 1: the sd slots hold the diagonal itself (HVP tangent sample)
+    const float* diag_of;  // HVP tangent sample: params is the direction vec, and the
+                           // diagonal is sigmoid(diag_of's sd) vec_sd (nullptr: softplus(sd))
     int abl;                     // diagnostics ablation mask (0 in production):
                                  // 1 loads, 2 MFMAs, 4 x atomics
     unsigned long long* stamps;  // diagnostics: 16 slots per workgroup
@@ -265,7 +266,8 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
         a4[i] += p0[(k + i) * st];
         b4[i] += p1[(k + i) * st];
     }
-    const float dg = a.raw_diag ? sdr : softplus_f(sdr);
+    const float dg = a.diag_of ? sigmoid_f(a.diag_of[a.lay[rb.layer].poff + n + r]) * sdr
+                               : softplus_f(sdr);
     x[(int64_t)s0 * a.ldx + rb.xcol + rr] = (mu + dg * e0) + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
     if (two) x[(int64_t)s1 * a.ldx + rb.xcol + rr] = (mu + dg * e1) + ((b4[0] + b4[1]) + (b4[2] + b4[3]));
 }
@@ -288,6 +290,8 @@ struct UpdArgs {
     float* m;
     float* v;
     float* grad_out;   // GRAD mode output
+    const float* kl_vec;  // GRAD mode, nullable: + kl_vec / s0^2 on the corr entries (the
+                          // KL Hessian's corr block in an HVP: kl_vec = the direction)
     double* kl_out;    // nullable
     int64_t pcount;    // parameter vector length
     int include_kl;
@@ -688,6 +692,7 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
             const int o = rowp[j] + cb;
             const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
             const float4 p4 = (a.abl & 4) ? z4 : fix4(pq[j], o, 0, pcount);
+            const float4 kv4 = (GRAD && a.kl_vec) ? fix4(ld4u(a.kl_vec, o, 0, pcount), o, 0, pcount) : z4;
             float4 m4 = z4, v4 = z4;
             if (!GRAD) {
                 m4 = (a.abl & 4) ? z4 : fix4(mq[j], o, 0, pcount);
@@ -698,7 +703,8 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
             for (int i = 0; i < 4; ++i) {
                 const float p = f4get(p4, i);
                 klp += cb + i < r ? p * p : 0.f;
-                const float gval = a.include_kl ? f4get(d4, i) + p * a.inv_s0sq : f4get(d4, i);
+                float gval = a.include_kl ? f4get(d4, i) + p * a.inv_s0sq : f4get(d4, i);
+                if (GRAD && a.kl_vec) gval += f4get(kv4, i) * a.inv_s0sq;
                 if (GRAD) {
                     pn[i] = gval;
                 } else {
@@ -1440,9 +1446,9 @@ hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, 
 }
 
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
-                          float* x_shard, hipStream_t st, bool raw_diag) {
+                          float* x_shard, hipStream_t st, const float* diag_of) {
     FwdArgs a{};
-    a.raw_diag = raw_diag ? 1 : 0;
+    a.diag_of = diag_of;
     a.items = p.d_fwd;
     a.params = params;
     a.eps = eps;
@@ -1484,8 +1490,9 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
-                             float* tstate, bool packed_out) {
+                             float* tstate, bool packed_out, const float* kl_vec) {
     UpdArgs a{};
+    a.kl_vec = kl_vec;
     a.chunks = p.d_upd;
     a.eps = eps;
     a.g = g_shard;

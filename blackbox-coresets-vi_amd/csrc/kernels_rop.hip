@@ -18,7 +18,7 @@
 // (net_rop_kernel: one workgroup per sample, rows in chunks, VALU), then the
 // reparameterised backward of G_dot (the update kernel's gradient mode for
 // full-cov), the softplus curvature sum_s (G_s . eps_s) sigmoid'(sd) v_sd and
-// the KL Hessian (hvp_assemble_kernel).  The mixed products the hypergradient
+// the KL Hessian (hvp_param_kernel).  The mixed products the hypergradient
 // needs come out of the same pass: d/du (vec . grad) = sum_s delta_dot_0 W +
 // delta_0 W_dot, d/dw_m (vec . grad) = sum_s NLL_dot_sm.
 #include <algorithm>
@@ -29,8 +29,8 @@ namespace psvi {
 
 struct RopArgs {
     int L, M, S, n_tot, family, rc, maxd;
-    int nsplit;  // workgroups per sample (row halves); 2: G / G_dot added onto zeroed buffers,
-                 // two addends, so the sum is exact-order independent
+    int nsplit;  // workgroups per sample (row blocks), each storing its G / G_dot partial
+                 // into its own slot [split][S][n_tot]; slot_sum_kernel adds them in order
     int din[kMaxL], dout[kMaxL], woff[kMaxL];
     int64_t poff[kMaxL], eoff[kMaxL];
     int lx, lxd, lg, lgd, lh[kMaxL + 1], lhd[kMaxL + 1], ld0, ld1, ldd0, ldd1;  // LDS carve
@@ -96,7 +96,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             sm[a.lhd[0] + i] = 0.f;
         }
         __syncthreads();
-        // forward + tangent forward
+        // forward + tangent forward: 2 rows x 2 outputs per thread (8 LDS
+        // reads per 12 FMAs; clamped duplicates at odd edges, stored once)
         for (int l = 0; l < L; ++l) {
             const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
             const float* W = X + a.xo[l];
@@ -107,22 +108,51 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             const float* HD = sm + a.lhd[l];
             float* Hn = sm + a.lh[l + 1];
             float* HDn = sm + a.lhd[l + 1];
-            for (int q = tid; q < rc * dout; q += nt) {
-                const int m = q / dout, o = q - m * dout;
-                float acc = b[o], accd = bd[o];
+            const int nbo = (dout + 1) >> 1, nb = ((rc + 1) >> 1) * nbo;
+            for (int q = tid; q < nb; q += nt) {
+                const int bm = q / nbo, bo = q - bm * nbo;
+                const int ma = 2 * bm, o0 = 2 * bo;
+                const int mb = min(ma + 1, rc - 1), o1 = min(o0 + 1, dout - 1);
+                float acc[2][2], accd[2][2];
+                acc[0][0] = acc[1][0] = b[o0];
+                acc[0][1] = acc[1][1] = b[o1];
+                accd[0][0] = accd[1][0] = bd[o0];
+                accd[0][1] = accd[1][1] = bd[o1];
+                const float* h0 = H + ma * din;
+                const float* h1 = H + mb * din;
+                const float* hd0 = HD + ma * din;
+                const float* hd1 = HD + mb * din;
+                const float* w0 = W + o0 * ldw;
+                const float* w1 = W + o1 * ldw;
+                const float* wd0 = Wd + o0 * ldw;
+                const float* wd1 = Wd + o1 * ldw;
+#pragma unroll 4
                 for (int i = 0; i < din; ++i) {
-                    const float h = H[m * din + i], hd = HD[m * din + i];
-                    const float wv = W[o * ldw + i];
-                    acc = fmaf(h, wv, acc);
-                    accd = fmaf(hd, wv, fmaf(h, Wd[o * ldw + i], accd));
+                    const float hv[2] = {h0[i], h1[i]}, hdv[2] = {hd0[i], hd1[i]};
+                    const float wv[2] = {w0[i], w1[i]}, wdv[2] = {wd0[i], wd1[i]};
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            acc[r][c] = fmaf(hv[r], wv[c], acc[r][c]);
+                            accd[r][c] = fmaf(hdv[r], wv[c], fmaf(hv[r], wdv[c], accd[r][c]));
+                        }
                 }
-                if (l < L - 1) {
-                    Hn[q] = acc > 0.f ? acc : 0.f;
-                    HDn[q] = acc > 0.f ? accd : 0.f;
-                } else {
-                    Hn[q] = acc;
-                    HDn[q] = accd;
-                }
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if ((r && mb == ma) || (c && o1 == o0)) continue;
+                        const int qq = (r ? mb : ma) * dout + (c ? o1 : o0);
+                        const float av = acc[r][c], ad = accd[r][c];
+                        if (l < L - 1) {
+                            Hn[qq] = av > 0.f ? av : 0.f;
+                            HDn[qq] = av > 0.f ? ad : 0.f;
+                        } else {
+                            Hn[qq] = av;
+                            HDn[qq] = ad;
+                        }
+                    }
             }
             __syncthreads();
         }
@@ -153,7 +183,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             if (a.nlld) a.nlld[(int64_t)s * a.M + m0 + m] = nd;
         }
         __syncthreads();
-        // R-backward
+        // R-backward: weight gradients 2 outputs x 2 inputs per thread, the
+        // propagation 2 rows x 2 inputs (as the forward)
         for (int l = L - 1; l >= 0; --l) {
             const int din = a.din[l], dout = a.dout[l], nw = din * dout, ldw = a.ldw[l];
             const float* W = X + a.xo[l];
@@ -162,47 +193,84 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             const float* HD = sm + a.lhd[l];
             float* GW = GA + a.woff[l];
             float* GDW = GDA + a.woff[l];
-            for (int q = tid; q < nw + dout; q += nt) {
-                if (q < nw) {
-                    const int o = q / din, i = q - o * din;
-                    float g = 0.f, gd = 0.f;
+            const int md = a.maxd;
+            const int nbi = (din + 1) >> 1, nbw = ((dout + 1) >> 1) * nbi;
+            for (int q = tid; q < nbw + dout; q += nt) {
+                if (q < nbw) {
+                    const int bo = q / nbi, bi = q - bo * nbi;
+                    const int o0 = 2 * bo, i0 = 2 * bi;
+                    const int o1 = min(o0 + 1, dout - 1), i1 = min(i0 + 1, din - 1);
+                    float g[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, gd[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll 4
                     for (int m = 0; m < rc; ++m) {
-                        const float dl = Dl[m * a.maxd + o], ddl = DDl[m * a.maxd + o];
-                        const float h = H[m * din + i];
-                        g = fmaf(dl, h, g);
-                        gd = fmaf(ddl, h, fmaf(dl, HD[m * din + i], gd));
+                        const float dl[2] = {Dl[m * md + o0], Dl[m * md + o1]};
+                        const float ddl[2] = {DDl[m * md + o0], DDl[m * md + o1]};
+                        const float hv[2] = {H[m * din + i0], H[m * din + i1]};
+                        const float hdv[2] = {HD[m * din + i0], HD[m * din + i1]};
+#pragma unroll
+                        for (int r = 0; r < 2; ++r)
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) {
+                                g[r][c] = fmaf(dl[r], hv[c], g[r][c]);
+                                gd[r][c] = fmaf(ddl[r], hv[c], fmaf(dl[r], hdv[c], gd[r][c]));
+                            }
                     }
-                    GW[q] += g;
-                    GDW[q] += gd;
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            if ((r && o1 == o0) || (c && i1 == i0)) continue;
+                            const int qq = (r ? o1 : o0) * din + (c ? i1 : i0);
+                            GW[qq] += g[r][c];
+                            GDW[qq] += gd[r][c];
+                        }
                 } else {
-                    const int o = q - nw;
+                    const int o = q - nbw;
                     float g = 0.f, gd = 0.f;
                     for (int m = 0; m < rc; ++m) {
-                        g += Dl[m * a.maxd + o];
-                        gd += DDl[m * a.maxd + o];
+                        g += Dl[m * md + o];
+                        gd += DDl[m * md + o];
                     }
-                    GW[q] += g;
-                    GDW[q] += gd;
+                    GW[nw + o] += g;
+                    GDW[nw + o] += gd;
                 }
             }
             if (l > 0 || a.du) {
                 // delta' = (delta W) 1[h > 0]   (h = relu(a_{l-1}); none at the input)
-                for (int q = tid; q < rc * din; q += nt) {
-                    const int m = q / din, i = q - m * din;
-                    float t = 0.f, td = 0.f;
+                const int nbp = ((rc + 1) >> 1) * nbi;
+                for (int q = tid; q < nbp; q += nt) {
+                    const int bm = q / nbi, bi = q - bm * nbi;
+                    const int ma = 2 * bm, i0 = 2 * bi;
+                    const int mb = min(ma + 1, rc - 1), i1 = min(i0 + 1, din - 1);
+                    float t[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, td[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll 4
                     for (int o = 0; o < dout; ++o) {
-                        const float dl = Dl[m * a.maxd + o], ddl = DDl[m * a.maxd + o];
-                        const float wv = W[o * ldw + i];
-                        t = fmaf(dl, wv, t);
-                        td = fmaf(ddl, wv, fmaf(dl, Wd[o * ldw + i], td));
+                        const float dl[2] = {Dl[ma * md + o], Dl[mb * md + o]};
+                        const float ddl[2] = {DDl[ma * md + o], DDl[mb * md + o]};
+                        const float wv[2] = {W[o * ldw + i0], W[o * ldw + i1]};
+                        const float wdv[2] = {Wd[o * ldw + i0], Wd[o * ldw + i1]};
+#pragma unroll
+                        for (int r = 0; r < 2; ++r)
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) {
+                                t[r][c] = fmaf(dl[r], wv[c], t[r][c]);
+                                td[r][c] = fmaf(ddl[r], wv[c], fmaf(dl[r], wdv[c], td[r][c]));
+                            }
                     }
-                    if (l > 0) {
-                        const bool on = H[q] > 0.f;
-                        Dn[m * a.maxd + i] = on ? t : 0.f;
-                        DDn[m * a.maxd + i] = on ? td : 0.f;
-                    } else {
-                        a.du[((int64_t)s * a.M + m0 + m) * D + i] = td;
-                    }
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            if ((r && mb == ma) || (c && i1 == i0)) continue;
+                            const int m = r ? mb : ma, i = c ? i1 : i0;
+                            if (l > 0) {
+                                const bool on = H[m * din + i] > 0.f;
+                                Dn[m * md + i] = on ? t[r][c] : 0.f;
+                                DDn[m * md + i] = on ? td[r][c] : 0.f;
+                            } else {
+                                a.du[((int64_t)s * a.M + m0 + m) * D + i] = td[r][c];
+                            }
+                        }
                 }
             }
             __syncthreads();
@@ -210,102 +278,148 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             float* t1 = DDl; DDl = DDn; DDn = t1;
         }
     }
+    // this row block's partial into its own slot (no atomics, no zeroing)
+    const int64_t slot = ((int64_t)blockIdx.y * a.S + s) * a.n_tot;
     for (int o = tid; o < a.n_tot; o += nt) {
-        if (a.nsplit == 1) {
-            a.G[(int64_t)s * a.n_tot + o] = GA[o];
-            a.Gd[(int64_t)s * a.n_tot + o] = GDA[o];
-        } else {
-            atomicAdd(a.G + (int64_t)s * a.n_tot + o, GA[o]);
-            atomicAdd(a.Gd + (int64_t)s * a.n_tot + o, GDA[o]);
-        }
+        a.G[slot + o] = GA[o];
+        a.Gd[slot + o] = GDA[o];
     }
 }
 
-// full-cov tangent parameters: vec with the sd slots scaled by sigmoid(sd),
-// so the sample phase (raw diagonal) yields x_dot = v_mean + Lv eps
-__global__ __launch_bounds__(256) void hvp_tangent_kernel(RopArgs a, float* T) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= a.n_tot) return;
+// G += the other row blocks' slots, G_dot likewise, in slot order (slot 0
+// holds the sum afterwards)
+__global__ __launch_bounds__(256) void slot_sum_kernel(float* __restrict__ G, float* __restrict__ Gd,
+                                                       int64_t n, int nsplit) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float g = G[i], gd = Gd[i];
+    for (int k = 1; k < nsplit; ++k) {
+        g += G[k * n + i];
+        gd += Gd[k * n + i];
+    }
+    G[i] = g;
+    Gd[i] = gd;
+}
+
+// Hv assembly.  The sums over the S samples run in parallel: a workgroup
+// takes 64 consecutive elements (one per lane) and its four waves a quarter
+// of the samples each, in order; the four partials are added in wave order
+// (run-to-run bitwise reproducible).  Per parameter element e of layer l:
+//   ge = sum_s G_s eps_s,  gd = sum_s G_dot_s,  gde = sum_s G_dot_s eps_s,
+// then the softplus curvature ge sigmoid'(sd) v_sd and the KL Hessian (the
+// corr block of full-cov is added by the update kernel's gradient mode, which
+// also wrote sum G_dot, diag(G_dot^T E) sigmoid(sd) for full-cov).
+constexpr int kAsmWaves = 4;
+__device__ __forceinline__ void sample_quarter(int S, int wv, int& s0, int& s1) {
+    const int q = (S + kAsmWaves - 1) / kAsmWaves;
+    s0 = min(S, wv * q);
+    s1 = min(S, s0 + q);
+}
+
+__global__ __launch_bounds__(256) void hvp_param_kernel(RopArgs a, float* hv, float inv_s0sq,
+                                                        float klw) {
+    __shared__ float part[kAsmWaves][3][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
+    const bool live = e < a.n_tot;
+    const int ec = live ? e : a.n_tot - 1;
     int l = 0;
-    while (l + 1 < a.L && e >= a.woff[l + 1]) ++l;
-    const int n = a.din[l] * a.dout[l] + a.dout[l];
-    const int64_t ps = a.poff[l] + n + (e - a.woff[l]);
-    T[ps] = sigmoid_f(a.params[ps]) * a.vec[ps];
+    while (l + 1 < a.L && ec >= a.woff[l + 1]) ++l;
+    const int n = a.din[l] * a.dout[l] + a.dout[l], k = ec - a.woff[l], nw = n - a.dout[l];
+    // eps of sample s at ebase + s * es (mean-field weights and biases are
+    // stored in separate [S][.] blocks)
+    int64_t ebase;
+    int es;
+    if (a.family == PSVI_FAMILY_FULLCOV) {
+        ebase = a.eoff[l] + k;
+        es = n;
+    } else if (k < nw) {
+        ebase = a.eoff[l] + k;
+        es = nw;
+    } else {
+        ebase = a.eoff[l] + (int64_t)a.S * nw + (k - nw);
+        es = a.dout[l];
+    }
+    int s0, s1;
+    sample_quarter(a.S, wv, s0, s1);
+    float ge = 0.f, gd = 0.f, gde = 0.f;
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {  // four samples' loads in flight
+        float g4[4], d4[4], e4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            g4[j] = a.G[(int64_t)(s + j) * a.n_tot + ec];
+            d4[j] = a.Gd[(int64_t)(s + j) * a.n_tot + ec];
+            e4[j] = a.eps[ebase + (int64_t)(s + j) * es];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ge = fmaf(g4[j], e4[j], ge);
+            gd += d4[j];
+            gde = fmaf(d4[j], e4[j], gde);
+        }
+    }
+    for (; s < s1; ++s) {
+        const float g = a.G[(int64_t)s * a.n_tot + ec], dv = a.Gd[(int64_t)s * a.n_tot + ec];
+        const float ev = a.eps[ebase + (int64_t)s * es];
+        ge = fmaf(g, ev, ge);
+        gd += dv;
+        gde = fmaf(dv, ev, gde);
+    }
+    part[wv][0][lane] = ge;
+    part[wv][1][lane] = gd;
+    part[wv][2][lane] = gde;
+    __syncthreads();
+    if (wv != 0 || !live) return;
+    ge = gd = gde = 0.f;
+#pragma unroll
+    for (int w = 0; w < kAsmWaves; ++w) {
+        ge += part[w][0][lane];
+        gd += part[w][1][lane];
+        gde += part[w][2][lane];
+    }
+    const float kls = klw * inv_s0sq;  // klw = 0: a sample shard's partial product without KL
+    const int64_t pm = a.poff[l] + k, ps = pm + n;
+    const float r = a.params[ps], sp = softplus_f(r), sg = sigmoid_f(r);
+    const float vsd = a.vec[ps];
+    const float kl2 = klw * ((1.f / (sp * sp) + inv_s0sq) * sg * sg + (sp * inv_s0sq - 1.f / sp) * sg * (1.f - sg));
+    const float curv = ge * sg * (1.f - sg) * vsd + kl2 * vsd;
+    if (a.family == PSVI_FAMILY_FULLCOV) {
+        hv[pm] += a.vec[pm] * kls;
+        hv[ps] += curv;
+    } else {
+        hv[pm] = gd + a.vec[pm] * kls;
+        hv[ps] = gde * sg + curv;
+    }
 }
 
-// Hv assembly.  Index space: [0, n_tot) mean / sd terms, then (full-cov) the
-// corr prior terms, then d_u (M x D), then d_w (M).
-__global__ __launch_bounds__(256) void hvp_assemble_kernel(RopArgs a, float* hv, float* d_u,
-                                                           float* d_w, int64_t ncorr_tot,
-                                                           float inv_s0sq, float klw) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int D = a.din[0];
-    // klw = 0: a sample shard's partial product without the KL Hessian
-    const float kls = klw * inv_s0sq;
-    if (i < a.n_tot) {
-        const int e = (int)i;
-        int l = 0;
-        while (l + 1 < a.L && e >= a.woff[l + 1]) ++l;
-        const int n = a.din[l] * a.dout[l] + a.dout[l], k = e - a.woff[l], nw = n - a.dout[l];
-        const int64_t pm = a.poff[l] + k, ps = pm + n;
-        float gd = 0.f, gde = 0.f, ge = 0.f;
-        for (int s = 0; s < a.S; ++s) {
-            float ev;
-            if (a.family == PSVI_FAMILY_FULLCOV)
-                ev = a.eps[a.eoff[l] + (int64_t)s * n + k];
-            else
-                ev = k < nw ? a.eps[a.eoff[l] + (int64_t)s * nw + k]
-                            : a.eps[a.eoff[l] + (int64_t)a.S * nw + (int64_t)s * a.dout[l] + k - nw];
-            const float g = a.G[(int64_t)s * a.n_tot + e], gdv = a.Gd[(int64_t)s * a.n_tot + e];
-            ge = fmaf(g, ev, ge);
-            gd += gdv;
-            gde = fmaf(gdv, ev, gde);
-        }
-        const float r = a.params[ps], sp = softplus_f(r), sg = sigmoid_f(r);
-        const float vsd = a.vec[ps];
-        const float kl2 = klw * ((1.f / (sp * sp) + inv_s0sq) * sg * sg + (sp * inv_s0sq - 1.f / sp) * sg * (1.f - sg));
-        const float curv = ge * sg * (1.f - sg) * vsd + kl2 * vsd;
-        if (a.family == PSVI_FAMILY_FULLCOV) {
-            // the update kernel's gradient mode already wrote sum G_dot, diag(G_dot^T E) sg
-            hv[pm] += a.vec[pm] * kls;
-            hv[ps] += curv;
-        } else {
-            hv[pm] = gd + a.vec[pm] * kls;
-            hv[ps] = gde * sg + curv;
-        }
-        return;
+// dst[j] = sum_s src[s * stride + j], j < n: lanes over j, waves over sample
+// quarters, partials in wave order (d_u = sum_s du_dot_s, d_w = sum_s NLL_dot_s)
+__global__ __launch_bounds__(256) void sample_sum_kernel(const float* __restrict__ src,
+                                                         int64_t stride, int S, int64_t n,
+                                                         float* __restrict__ dst) {
+    __shared__ float part[kAsmWaves][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t j = (int64_t)blockIdx.x * 64 + lane, jc = j < n ? j : n - 1;
+    int s0, s1;
+    sample_quarter(S, wv, s0, s1);
+    float t = 0.f;
+    int s = s0;
+    for (; s + 4 <= s1; s += 4) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = src[(int64_t)(s + q) * stride + jc];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += v[q];
     }
-    int64_t j = i - a.n_tot;
-    if (j < ncorr_tot) {
-        // corr prior: + v_corr / s0^2 (layers' corr blocks in order)
-        int64_t base = 0;
-        for (int l = 0; l < a.L; ++l) {
-            const int n = a.din[l] * a.dout[l] + a.dout[l];
-            const int64_t nc = (int64_t)(n - 1) * (n - 2) / 2;
-            if (j < base + nc) {
-                const int64_t pc = a.poff[l] + 2 * n + (j - base);
-                hv[pc] += a.vec[pc] * kls;
-                return;
-            }
-            base += nc;
-        }
-        return;
-    }
-    j -= ncorr_tot;
-    if (j < (int64_t)a.M * D) {
-        if (d_u) {
-            float t = 0.f;
-            for (int s = 0; s < a.S; ++s) t += a.du[(int64_t)s * a.M * D + j];
-            d_u[j] = t;
-        }
-        return;
-    }
-    j -= (int64_t)a.M * D;
-    if (j < a.M && d_w) {
-        float t = 0.f;
-        for (int s = 0; s < a.S; ++s) t += a.nlld[(int64_t)s * a.M + j];
-        d_w[j] = t;
-    }
+    for (; s < s1; ++s) t += src[(int64_t)s * stride + jc];
+    part[wv][lane] = t;
+    __syncthreads();
+    if (wv != 0 || j >= n) return;
+    t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kAsmWaves; ++w) t += part[w][lane];
+    dst[j] = t;
 }
 
 static int rup4(int x) { return (x + 3) & ~3; }
@@ -356,6 +470,9 @@ int rop_rows(const psvi_plan& p) {
     return 0;
 }
 
+// two workgroups per sample while the samples alone leave CUs idle
+int rop_splits(const psvi_plan& p) { return (p.d.S < 256 && p.d.M > 1) ? 2 : 1; }
+
 static void rop_fill(const psvi_plan& p, RopArgs& a) {
     a.L = p.L;
     a.M = p.d.M;
@@ -369,18 +486,6 @@ static void rop_fill(const psvi_plan& p, RopArgs& a) {
         a.poff[l] = p.lay[l].poff;
         a.eoff[l] = p.lay[l].eoff;
     }
-}
-
-hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,
-                              float* T, hipStream_t st) {
-    RopArgs a{};
-    rop_fill(p, a);
-    a.params = params;
-    a.vec = vec;
-    hipError_t e = hipMemcpyAsync(T, vec, sizeof(float) * (size_t)p.P, hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(hvp_tangent_kernel, dim3((p.n_tot + 255) / 256), dim3(256), 0, st, a, T);
-    return hipGetLastError();
 }
 
 hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
@@ -401,15 +506,13 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     a.u = u; a.z = z; a.w = w; a.x = x; a.xd = xd;
     a.params = params; a.vec = vec; a.eps = eps;
     a.G = G; a.Gd = Gd; a.du = du; a.nlld = nlld;
-    // two workgroups per sample while the samples alone leave CUs idle
-    a.nsplit = (p.d.S < 256 && p.d.M > 1) ? 2 : 1;
-    if (a.nsplit > 1) {
-        const size_t bytes = sizeof(float) * (size_t)p.d.S * p.n_tot;
-        hipError_t e = hipMemsetAsync(G, 0, bytes, st);
-        if (e == hipSuccess) e = hipMemsetAsync(Gd, 0, bytes, st);
-        if (e != hipSuccess) return e;
-    }
+    a.nsplit = rop_splits(p);
     hipLaunchKernelGGL(net_rop_kernel, dim3(p.d.S, a.nsplit), dim3(512), lds, st, a);
+    if (a.nsplit > 1) {
+        const int64_t n = (int64_t)p.d.S * p.n_tot;
+        hipLaunchKernelGGL(slot_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, G,
+                           Gd, n, a.nsplit);
+    }
     return hipGetLastError();
 }
 
@@ -422,15 +525,18 @@ hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const fl
     a.params = params; a.vec = vec; a.eps = eps;
     a.G = const_cast<float*>(G);
     a.Gd = const_cast<float*>(Gd);
-    a.du = const_cast<float*>(du);
-    a.nlld = const_cast<float*>(nlld);
-    int64_t nct = 0;
-    if (p.family == PSVI_FAMILY_FULLCOV)
-        for (int l = 0; l < p.L; ++l) nct += p.lay[l].nc;
-    const int64_t total = p.n_tot + nct + (int64_t)p.d.M * p.lay[0].din + p.d.M;
     const float s0 = p.d.prior_sd;
-    hipLaunchKernelGGL(hvp_assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       st, a, hv, d_u, d_w, nct, 1.f / (s0 * s0), include_kl ? 1.f : 0.f);
+    hipLaunchKernelGGL(hvp_param_kernel, dim3((unsigned)((p.n_tot + 63) / 64)), dim3(256), 0, st,
+                       a, hv, 1.f / (s0 * s0), include_kl ? 1.f : 0.f);
+    const int S = p.d.S, M = p.d.M, D = p.lay[0].din;
+    if (d_u) {
+        const int64_t n = (int64_t)M * D;
+        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, du,
+                           n, S, n, d_u);
+    }
+    if (d_w)
+        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((M + 63) / 64)), dim3(256), 0, st,
+                           nlld, (int64_t)M, S, (int64_t)M, d_w);
     return hipGetLastError();
 }
 

@@ -313,13 +313,16 @@ hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
                             const float* slot_eps = nullptr);
 // acc = [sum_s dW_s | sum_s dW_s eps_s] from the plan's mean-field gradient slots
 hipError_t launch_mf_slot_acc(const psvi_plan& p, const float* eps, float* acc, hipStream_t st);
+// diag_of (HVP tangent sample): params is the direction, the diagonal
+// sigmoid(diag_of's sd) * its sd slot
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
-                          float* x_shard, hipStream_t st, bool raw_diag = false);
+                          float* x_shard, hipStream_t st, const float* diag_of = nullptr);
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
-                             float* tstate = nullptr, bool packed_out = false);
+                             float* tstate = nullptr, bool packed_out = false,
+                             const float* kl_vec = nullptr);
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
                                    float* tstate, bool to_tiled, hipStream_t st);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
@@ -381,8 +384,7 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
 hipError_t launch_nonfinite(const void* x, int64_t n, int dtype, int32_t* flag, hipStream_t st);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
-hipError_t launch_hvp_tangent(const psvi_plan& p, const float* params, const float* vec,
-                              float* T, hipStream_t st);
+int rop_splits(const psvi_plan& p);  // row blocks per sample: G / G_dot slots
 hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                           const float* x, const float* xd, const float* params, const float* vec,
                           const float* eps, float* G, float* Gd, float* du, float* nlld,
