@@ -517,6 +517,12 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                 hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the streaming-update scratch");
         }
+        if (!rc && family == PSVI_FAMILY_FULLCOV && p->mchunks > 1) {
+            const size_t bytes = sizeof(float) * (size_t)p->mchunks *
+                                 std::max(1, p->s_cnt[p->rank]) * p->n_tot;
+            if (hipMalloc((void**)&p->d_net_slots, bytes) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the network's pseudopoint-chunk slots");
+        }
         if (!rc && family == PSVI_FAMILY_MEANFIELD) {
             const size_t bytes = sizeof(float) * (size_t)std::max(1, p->s_cnt[p->rank]) *
                                  p->mchunks * p->n_tot;
@@ -556,6 +562,7 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_upd) (void)hipFree(p->d_upd);
     if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);
     if (p->d_mf_slots) (void)hipFree(p->d_mf_slots);
+    if (p->d_net_slots) (void)hipFree(p->d_net_slots);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->aux_st) (void)hipStreamDestroy(p->aux_st);
@@ -703,7 +710,6 @@ static int step_impl(const psvi_plan* p, const float* u, const int32_t* z, const
         float* x = (float*)wsb;
         float* g = (float*)(wsb + align256(xs));
         HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
-        if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
         HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x, g, elbo_out, st));
         HIP_TRY(launch_mvn_update(*p, eps, g, params, m, v, hp, elbo_out, grad_out, include_kl,
                                   nullptr, nullptr, st));
@@ -779,9 +785,6 @@ int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, con
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!u || !z || !w || !x_recv || !g_send || !nll_out) return fail(PSVI_EINVAL, "null pointer");
     hipStream_t st = as_stream(stream);
-    if (p->mchunks > 1)
-        HIP_TRY(hipMemsetAsync(g_send, 0,
-                               sizeof(float) * (size_t)p->s_cnt[p->rank] * p->n_tot, st));
     HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x_recv, g_send, nll_out, st));
     return 0;
 }
@@ -943,7 +946,6 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
     for (int t = 0; t < T; ++t) {
         h.step = hp->step + t;
-        if (p->mchunks > 1) HIP_TRY(hipMemsetAsync(g, 0, xs, st));
         // Philox mode: the network kernel also draws the next step's eps
         const bool draw = !eps && t + 1 < T;
         float* en_buf = draw ? ebuf[(t + 1) & 1] : nullptr;
@@ -1028,8 +1030,6 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
     // 3. backward through the network with the row coefficients (+ sampled-KL path)
     NetOuter bw{2, n_pseudo, nullptr, o.rowcoef, o.ck, grad_u ? o.du : nullptr};
     if (p->family == PSVI_FAMILY_FULLCOV) {
-        if (p->mchunks > 1)
-            HIP_TRY(hipMemsetAsync(g, 0, sizeof(float) * (size_t)p->d.S * p->n_tot, st));
         HIP_TRY(launch_net(*p, x_all, z_all, w_all, nullptr, nullptr, nullptr, x, g, nullptr, st,
                            nullptr, 0, 0, 0, &bw));
         // 4. reparameterised backward (no KL term: the sampled KL came in through G)

@@ -15,9 +15,9 @@
 // forward pass and the loss head; role 0 then produces layer 0's weight
 // gradient (and the gradient chain down to it), role 1 every other layer's.
 // Each gradient element has exactly one writer -- plain stores into g_send,
-// no zeroing pass, no atomics, deterministic.  (Full-cov pseudopoint chunks,
-// whose partial dW are added with atomics onto a zeroed g_send, remain for
-// shapes whose buffers exceed the LDS, and for ranks with very few samples.)
+// no zeroing pass, no atomics, deterministic.  (Full-cov pseudopoint chunks --
+// shapes whose buffers exceed the LDS, ranks with very few samples -- store
+// their partial dW into per-chunk slots of the plan, added in chunk order.)
 // Mean-field: every (sample, chunk) stores its gradient into its own slot of
 // the plan's d_mf_slots; mf_update_kernel sums the slots in a fixed order
 // (against eps for the rho accumulator), so the step is bitwise reproducible.
@@ -51,7 +51,9 @@ namespace psvi {
 constexpr int kMaxC = 16;  // classes the VALU loss head keeps in registers
 
 struct NetArgs {
-    int L, M, mc, S_total, s_goff, atomic_g, nroles, Mp;
+    int L, M, mc, S_total, s_goff, nroles, Mp;
+    float* gslot;   // full-cov, pseudopoint chunks > 1: chunk z's partial dW into slot z
+    int64_t gsz;    // floats per slot (= the g_send buffer)
     int abl;  // diagnostics ablation mask (0 in production): 1 loads, 2 fwd
               // GEMMs, 4 loss head, 8 bwd GEMMs, 16 global gradient writes
     unsigned long long* stamps;  // diagnostics: s_memtime per phase (nullptr in production)
@@ -678,8 +680,11 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         if constexpr (FAM == PSVI_FAMILY_MEANFIELD) {
             a.mf_slots[((size_t)s * gridDim.z + blockIdx.z) * a.slot_ld + a.woff[l] + o] = v;
         } else {
-            float* dst = a.gsend + fc_addr(a, nsrc, srct, l, o, s);
-            if (a.atomic_g) atomicAdd(dst, v); else *dst = v;
+            // one writer per element (per chunk slot when the pseudopoints are
+            // chunked; net_slot_sum_kernel adds the slots in chunk order)
+            float* dst = (a.gslot ? a.gslot + (int64_t)blockIdx.z * a.gsz : a.gsend) +
+                         fc_addr(a, nsrc, srct, l, o, s);
+            *dst = v;
         }
     };
     // outer backward: the sampled-KL path, d nkl_s / d x_s = -x_s / s0^2,
@@ -885,6 +890,18 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     return off;
 }
 
+// g_send = the pseudopoint chunks' dW slots added in chunk order (run-to-run
+// bitwise reproducible; every element of every slot has one writer)
+__global__ __launch_bounds__(256) void net_slot_sum_kernel(const float* __restrict__ slots,
+                                                           int nslot, int64_t n,
+                                                           float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float t = slots[i];
+    for (int z = 1; z < nslot; ++z) t += slots[z * n + i];
+    out[i] = t;
+}
+
 int g_net_threads = 0;        // psvi_debug_set(PSVI_DBG_NET_THREADS, n): 0 = by chunk size
 int g_net_split_below = 256;  // split when a rank has fewer samples than CUs (psvi_debug_set(PSVI_DBG_NET_SPLIT_BELOW, n))
 int g_net_wg_target = 256;    // workgroups a split rank aims for (psvi_debug_set(PSVI_DBG_NET_WG_TARGET, n))
@@ -893,8 +910,8 @@ size_t net_plan_geometry(psvi_plan& p) {
     // One workgroup per sample and all M pseudopoints when the samples alone
     // fill the chip.  Otherwise two role workgroups per sample (disjoint
     // gradient outputs), and pseudopoint chunks only if that still leaves
-    // CUs idle or the buffers exceed the LDS (partial dW summed with atomics
-    // onto a zeroed g_send).  LDS <= 160 KiB per workgroup.
+    // CUs idle or the buffers exceed the LDS (partial dW into per-chunk slots,
+    // summed in chunk order).  LDS <= 160 KiB per workgroup.
     const int S_local = std::max(1, p.s_cnt[p.rank]);
     const int M = p.d.M;
     const bool split = S_local < g_net_split_below;
@@ -955,7 +972,8 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     a.mc = p.mc;
     a.S_total = p.d.S;
     a.s_goff = p.s_off[p.rank];
-    a.atomic_g = p.mchunks > 1;
+    a.gslot = p.family == PSVI_FAMILY_FULLCOV && p.mchunks > 1 ? p.d_net_slots : nullptr;
+    a.gsz = (int64_t)p.s_cnt[p.rank] * p.n_tot;
     a.nroles = p.net_roles;
     a.abl = g_net_ablation;
     a.stamps = g_net_stamps;
@@ -994,6 +1012,9 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true>), grid, block, p.net_lds, st, a);
     else
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false>), grid, block, p.net_lds, st, a);
+    if (a.gslot && a.outer != 1)
+        hipLaunchKernelGGL(net_slot_sum_kernel, dim3((unsigned)((a.gsz + 255) / 256)), dim3(256), 0,
+                           st, (const float*)a.gslot, p.mchunks, a.gsz, gsend);
     return hipGetLastError();
 }
 

@@ -282,6 +282,9 @@ struct psvi_plan {
     // [s_cnt[rank]][mchunks][n_tot]; one writer per element, summed in a fixed
     // order by the update (run-to-run bitwise reproducible, no float atomics)
     float* d_mf_slots = nullptr;
+    // full-cov with pseudopoint chunks: per-chunk dW slots [mchunks][s_cnt[rank]][n_tot],
+    // added in chunk order into g_send (no float atomics)
+    float* d_net_slots = nullptr;
     // tiled-state inner loops: the packed -> tiled conversion runs on aux_st,
     // forked from / joined to the caller's stream by the two events, behind the
     // first sample and network step (not re-entrant across host threads)

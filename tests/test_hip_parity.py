@@ -411,3 +411,36 @@ def test_inner_loop_checkpoint_resume(name):
     assert rel(e2, e1.cpu().numpy()) < 1e-6
     for a, b in ((st["params"], p1), (st["m"], m1), (st["v"], v1)):
         assert l2rel(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("layers,S,M", [
+    ([(64, 40), (40, 40), (40, 2)], 1024, 200),   # C4 at one GPU: two pseudopoint chunks
+    ([(64, 40), (40, 40), (40, 2)], 8, 200),      # few samples: many chunks per sample
+])
+def test_fullcov_step_bitwise_reproducible(layers, S, M):
+    """Pseudopoint-chunked full-cov network: the chunks' partial dW go to
+    per-chunk slots added in chunk order (no float atomics), so two identical
+    inner steps give bitwise identical parameters, Adam state and ELBO."""
+    from psvi.runtime import InnerLoopPlan, randn_
+
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    g = torch.Generator().manual_seed(S + M)
+    u = torch.randn(M, layers[0][0], generator=g).to(DEV)
+    z = torch.randint(0, layers[-1][1], (M,), generator=g).to(torch.int32).to(DEV)
+    w = torch.full((M,), 4.0, device=DEV)
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        parts += [0.1 * torch.randn(n, generator=g), torch.full((n,), -3.0),
+                  1e-3 * torch.randn((n - 1) * (n - 2) // 2, generator=g)]
+    p0 = torch.cat(parts).to(DEV)
+    eps = torch.empty(plan.eps_count, device=DEV)
+    randn_(eps, 5)
+    out = []
+    for _ in range(2):
+        p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+        e = plan.inner_step(u, z, w, eps, p, m, v, step=1, lr=1e-3)
+        out.append((e.item(), p, m, v))
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1:], out[1][1:]):
+        assert torch.equal(a, b)
