@@ -971,8 +971,12 @@ __device__ __forceinline__ float adam_fast_k(const AdamC& a, float p, float g, f
 constexpr int kStrBuf = 128 * 16;  // float4 per eps block buffer ([128 samples][16 slots])
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // plain vector loads / stores (no memcpy)
 
-// NS = S / 32; KIND: Adam variant; DIAG: the diagnostics build (phase stamps)
-template <int NS, int KIND, bool DIAG = false>
+// NS = S / 32; KIND: Adam variant; DIAG: the diagnostics build (phase stamps);
+// SC1: corr / m / v stores write-through with sc1, which drops the lines from
+// the XCD's L2 (MI355X_MICROARCH.md, store flavours): the 60 MB of state written
+// per launch then no longer evicts the eps / eps' blocks and G slices that
+// later tiles re-read from L2 (false: plain stores, A/B)
+template <int NS, int KIND, bool DIAG = false, bool SC1 = true>
 __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     constexpr int KT = 16 * NS;  // K steps of the dL GEMM (2 samples each)
     // [0, 4 kStrBuf): eps / eps' blocks, two buffers; then the band's G slice [128][64]
@@ -1060,6 +1064,11 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     auto frag_off = [&](const StrTile& T, int g) __attribute__((always_inline)) {
         return T.tb + (int64_t)((wv * 4 + g) * 64 + lane) * 4;
     };
+    // tm / tv follow tp in one allocation (tstate) of < 2 GB: one descriptor,
+    // the m / v arrays at a scalar byte offset
+    const rsrc_t rs_t = make_rsrc(a.tp, 0x7fffffff);
+    const int tmb = __builtin_amdgcn_readfirstlane((int)((a.tm - a.tp) * 4));
+    const int tvb = __builtin_amdgcn_readfirstlane((int)((a.tv - a.tp) * 4));
     auto load_pmv = [&](const StrTile& T) __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -1221,9 +1230,20 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
                 Lf[4 * g + e] = pn[e];
             }
             const int64_t o = frag_off(cur, g);
-            *reinterpret_cast<f32x4*>(a.tp + o) = f32x4{pn[0], pn[1], pn[2], pn[3]};
-            *reinterpret_cast<f32x4*>(a.tm + o) = f32x4{mn[0], mn[1], mn[2], mn[3]};
-            *reinterpret_cast<f32x4*>(a.tv + o) = f32x4{vn[0], vn[1], vn[2], vn[3]};
+            if constexpr (SC1) {
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const uint32_t ob = (uint32_t)(o * 4);
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(u32x4, f32x4{pn[0], pn[1], pn[2], pn[3]}), rs_t, ob, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(u32x4, f32x4{mn[0], mn[1], mn[2], mn[3]}), rs_t, ob, tmb, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(u32x4, f32x4{vn[0], vn[1], vn[2], vn[3]}), rs_t, ob, tvb, 16);
+            } else {
+                *reinterpret_cast<f32x4*>(a.tp + o) = f32x4{pn[0], pn[1], pn[2], pn[3]};
+                *reinterpret_cast<f32x4*>(a.tm + o) = f32x4{mn[0], mn[1], mn[2], mn[3]};
+                *reinterpret_cast<f32x4*>(a.tv + o) = f32x4{vn[0], vn[1], vn[2], vn[3]};
+            }
             // x' += eps' L'^T over this group's 8 columns, all sample blocks; the
             // A fragments are read one slot ahead, and each slot is pinned
             // (sched_barrier) so the loads stay spread between the MFMAs
@@ -1318,7 +1338,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     }
 }
 
-int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1)
+int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1: chunked, 3: plain-store stream)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -1470,7 +1490,9 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 
 template <int NS>
 static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
-    if (kind == PSVI_ADAM_HIGHER)
+    if (g_stream_off == 3)  // A/B: plain corr / m / v stores
+        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER, false, false>), g, bl, 0, st, b);
+    else if (kind == PSVI_ADAM_HIGHER)
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER>), g, bl, 0, st, b);
     else
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HYPERGRAD>), g, bl, 0, st, b);
@@ -1523,7 +1545,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         a.tp = tstate;
         a.tm = tstate + tf;
         a.tv = tstate + 2 * tf;
-        if (eps_next && p.n_str > 0 && !g_stream_off && stream_ok(a.S, a.adam.kind)) {
+        if (eps_next && p.n_str > 0 && g_stream_off != 1 && stream_ok(a.S, a.adam.kind)) {
             StrArgs b{};
             b.ranges = p.d_str;
             b.eps = eps;
