@@ -628,9 +628,19 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                         kv[4 * g + i] = vn[i];
                     }
                 } else if (!(a.abl & 8)) {
-                    *reinterpret_cast<float4*>(a.tp + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
-                    *reinterpret_cast<float4*>(a.tm + o) = make_float4(mn[0], mn[1], mn[2], mn[3]);
-                    *reinterpret_cast<float4*>(a.tv + o) = make_float4(vn[0], vn[1], vn[2], vn[3]);
+                    // write-through (sc1): the state leaves the XCD's L2, which keeps
+                    // the eps / G blocks other chunks re-read (as the stream kernel)
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const rsrc_t rs_t = make_rsrc(a.tp, 0x7fffffff);
+                    const int tmb = __builtin_amdgcn_readfirstlane((int)((a.tm - a.tp) * 4));
+                    const int tvb = __builtin_amdgcn_readfirstlane((int)((a.tv - a.tp) * 4));
+                    const uint32_t ob = (uint32_t)(o * 4);
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4, make_float4(pn[0], pn[1], pn[2], pn[3])), rs_t, ob, 0, 16);
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4, make_float4(mn[0], mn[1], mn[2], mn[3])), rs_t, ob, tmb, 16);
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4, make_float4(vn[0], vn[1], vn[2], vn[3])), rs_t, ob, tvb, 16);
                 }
                 if (FUSE)  // L_new fragment -> the [r][c] tile for the sample GEMM
                     *reinterpret_cast<float4*>(&Es[(32 * wr + l32) * TLD + 32 * wc + 8 * g + 4 * h]) =
