@@ -587,6 +587,7 @@ static OuterWs outer_ws(const psvi_plan* p, void* ws);
 // [splits][S][n_tot], d_u parts [S][M][D], NLL_dot [S][M]
 struct HvpWs {
     float *xd, *G, *Gd, *du, *nlld;
+    float* part2;  // full-cov: split-K slots of the tangent sample (pair launch)
     size_t bytes;
 };
 static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
@@ -609,6 +610,8 @@ static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
     o.Gd = (float*)take(sizeof(float) * ns * S * nt);
     o.du = (float*)take(sizeof(float) * S * M * D);
     o.nlld = (float*)take(sizeof(float) * S * M);
+    if (p->family == PSVI_FAMILY_FULLCOV)
+        o.part2 = (float*)take(sizeof(float) * (size_t)p->n_fwd * S * kFwdRows);
     o.bytes = off;
     return o;
 }
@@ -1144,8 +1147,7 @@ int psvi_hvp_partial(const psvi_plan* p, const float* u, const int32_t* z, const
     if (p->family == PSVI_FAMILY_FULLCOV) {
         x = (float*)ws;
         // x = mean + L eps; x_dot = v_mean + (sigmoid(sd) v_sd) eps + v_corr eps
-        HIP_TRY(launch_mvn_fwd(*p, eps, params, x, st));
-        HIP_TRY(launch_mvn_fwd(*p, eps, vec, o.xd, st, params));
+        HIP_TRY(launch_mvn_fwd_pair(*p, eps, params, x, vec, o.xd, o.part2, st));
     }
     HIP_TRY(launch_net_rop(*p, u, z, w, x, o.xd, params, vec, eps, o.G, o.Gd,
                            du_out ? o.du : nullptr, dw_out ? o.nlld : nullptr, st));

@@ -55,6 +55,11 @@ struct FwdArgs {
     int64_t e_total;  // floats in eps (load guards)
     const float* diag_of;  // HVP tangent sample: params is the direction vec, and the
                            // diagonal is sigmoid(diag_of's sd) vec_sd (nullptr: softplus(sd))
+    // pair launches (launch_mvn_fwd_pair, blockIdx.y / .z = 1): the second
+    // sample's parameters, split-K slots and diagonal source
+    const float* params2;
+    float* part2;
+    const float* diag_of2;
     int abl;                     // diagnostics ablation mask (0 in production):
                                  // 1 loads, 2 MFMAs, 4 x atomics
     unsigned long long* stamps;  // diagnostics: 16 slots per workgroup
@@ -108,7 +113,9 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
     FWD_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const FwdItem it = a.items[blockIdx.x];
     const int n = a.lay[it.layer].n;
-    const float* corr = a.params + a.lay[it.layer].poff + 2 * n;
+    const bool second = blockIdx.y == 1;  // pair launch: the second sample
+    const float* corr = (second ? a.params2 : a.params) + a.lay[it.layer].poff + 2 * n;
+    float* const part = second ? a.part2 : a.part;
     const int corr_len = (int)((int64_t)(n - 1) * (n - 2) / 2);
     const int eoff = (int)a.lay[it.layer].eoff;
     const float* E = a.eps + eoff;   // [S][n]; the whole eps buffer is [-eoff, e_rem)
@@ -199,7 +206,7 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int t = 0; t < FT; ++t) {
                 if (it.r0 + 32 * t + l32 >= it.r1) continue;
-                float* slot = a.part + (size_t)it.slot * a.S * kFwdRows + 32 * t + l32;
+                float* slot = part + (size_t)it.slot * a.S * kFwdRows + 32 * t + l32;
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const int s = sb + 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -221,14 +228,23 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
 constexpr int kRedSpb = 2 * 256 / kFwdRows;  // samples per reduce block
 __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* rbs,
                                                              const float* part, FwdArgs a,
-                                                             float* x) {
+                                                             float* x, float* x2 = nullptr) {
     const FwdRowBlock rb = rbs[blockIdx.x];
+    // pair launch: the second sample (locals -- writing into the by-value
+    // argument copies the whole struct to scratch)
+    const bool second = blockIdx.z == 1;
+    if (second) {
+        part = a.part2;
+        x = x2;
+    }
+    const float* const prm = second ? a.params2 : a.params;
+    const float* const dof = second ? a.diag_of2 : a.diag_of;
     const int rr = threadIdx.x & (kFwdRows - 1);
     const int s0 = blockIdx.y * kRedSpb + threadIdx.x / kFwdRows, s1 = s0 + kRedSpb / 2;
     if (s0 >= a.S || rr >= rb.R) return;
     const bool two = s1 < a.S;
     const int n = a.lay[rb.layer].n, r = rb.r0 + rr;
-    const float* mean = a.params + a.lay[rb.layer].poff;
+    const float* mean = prm + a.lay[rb.layer].poff;
     const float* eps = a.eps + a.lay[rb.layer].eoff + r;
     const float e0 = eps[(int64_t)s0 * n], e1 = eps[(int64_t)(two ? s1 : s0) * n];
     const float mu = mean[r], sdr = mean[n + r];
@@ -266,7 +282,7 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
         a4[i] += p0[(k + i) * st];
         b4[i] += p1[(k + i) * st];
     }
-    const float dg = a.diag_of ? sigmoid_f(a.diag_of[a.lay[rb.layer].poff + n + r]) * sdr
+    const float dg = dof ? sigmoid_f(dof[a.lay[rb.layer].poff + n + r]) * sdr
                                : softplus_f(sdr);
     x[(int64_t)s0 * a.ldx + rb.xcol + rr] = (mu + dg * e0) + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
     if (two) x[(int64_t)s1 * a.ldx + rb.xcol + rr] = (mu + dg * e1) + ((b4[0] + b4[1]) + (b4[2] + b4[3]));
@@ -1495,6 +1511,33 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     constexpr int spb = kRedSpb;  // samples per reduce workgroup
     hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb), dim3(256), 0,
                        st, p.d_frb, p.d_fwd_part, a, x_shard);
+    return hipGetLastError();
+}
+
+// x = mean + L eps (params) and x2 = its HVP tangent, v_mean + Lv eps with the
+// diagonal from params (vec), in one launch of each kernel: the items of the
+// two GEMMs share eps through L2 and fill the chip together (psvi_hvp)
+hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float* params,
+                               float* x, const float* vec, float* x2, float* part2,
+                               hipStream_t st) {
+    FwdArgs a{};
+    a.items = p.d_fwd;
+    a.params = params;
+    a.eps = eps;
+    a.part = p.d_fwd_part;
+    a.params2 = vec;
+    a.part2 = part2;
+    a.diag_of2 = params;
+    a.ldx = p.rows_tot[p.rank];
+    a.S = p.d.S;
+    a.e_total = p.Peps;
+    a.abl = g_fwd_ablation;
+    fill_layers(p, a.lay);
+    if (p.n_fwd == 0) return hipSuccess;
+    hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd, 2), dim3(256), 0, st, a);
+    constexpr int spb = kRedSpb;
+    hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb, 2), dim3(256),
+                       0, st, p.d_frb, p.d_fwd_part, a, x, x2);
     return hipGetLastError();
 }
 

@@ -320,6 +320,9 @@ hipError_t launch_mf_slot_acc(const psvi_plan& p, const float* eps, float* acc, 
 // sigmoid(diag_of's sd) * its sd slot
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
                           float* x_shard, hipStream_t st, const float* diag_of = nullptr);
+hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float* params,
+                               float* x, const float* vec, float* x2, float* part2,
+                               hipStream_t st);
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
