@@ -61,15 +61,44 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     float* GDA = sm + a.lgd;
     // sampled weights and their tangents, in the per-sample weight layout
     // (layer l at woff_l: W row-major [dout][din], then b)
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l < L && a.family == PSVI_FAMILY_FULLCOV; ++l) {
+        // full-cov: the layer's x / x_dot loads all in flight (clamped indices,
+        // kB per thread), then the scatter; a load-use per element serialised
+        // the phase on the memory latency
+        constexpr int kB = 8;
+        const int din = a.din[l], dout = a.dout[l], n = din * dout + dout, nw = din * dout;
+        const float rdin = 1.f / (float)din;
+        const float* xr = a.x + (int64_t)s * a.n_tot + a.woff[l];
+        const float* xdr = a.xd + (int64_t)s * a.n_tot + a.woff[l];
+        for (int base = tid; base < n; base += kB * nt) {
+            float xv[kB], xdv[kB];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                const int i = min(base + k * nt, n - 1);
+                xv[k] = xr[i];
+                xdv[k] = xdr[i];
+            }
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                const int i = base + k * nt;
+                if (i >= n) break;
+                // exact for i < 2^21: (i + 0.5) / din is >= 0.5 / din from an integer
+                const int j = (int)(((float)i + 0.5f) * rdin);
+                const int dst = a.xo[l] + (i < nw ? j * a.ldw[l] + (i - j * din)
+                                                  : dout * a.ldw[l] + (i - nw));
+                X[dst] = xv[k];
+                XD[dst] = xdv[k];
+                GA[a.woff[l] + i] = 0.f;
+                GDA[a.woff[l] + i] = 0.f;
+            }
+        }
+    }
+    for (int l = 0; l < L && a.family != PSVI_FAMILY_FULLCOV; ++l) {
         const int din = a.din[l], dout = a.dout[l], n = din * dout + dout, nw = din * dout;
         for (int i = tid; i < n; i += nt) {
             const int o = a.woff[l] + i;
             float xv, xdv;
-            if (a.family == PSVI_FAMILY_FULLCOV) {
-                xv = a.x[(int64_t)s * a.n_tot + o];
-                xdv = a.xd[(int64_t)s * a.n_tot + o];
-            } else {
+            {
                 const float e = i < nw ? a.eps[a.eoff[l] + (int64_t)s * nw + i]
                                        : a.eps[a.eoff[l] + (int64_t)a.S * nw + (int64_t)s * dout + i - nw];
                 const int64_t pm = a.poff[l] + i, pr = pm + n;
@@ -90,10 +119,23 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     const int m_lo = blockIdx.y * rows_per, m_hi = min(a.M, m_lo + rows_per);
     for (int m0 = m_lo; m0 < m_hi; m0 += a.rc) {
         const int rc = min(a.rc, m_hi - m0);
-        // inputs: h_0 = u rows, h_dot_0 = 0
-        for (int i = tid; i < rc * D; i += nt) {
-            sm[a.lh[0] + i] = a.u[(int64_t)m0 * D + i];
-            sm[a.lhd[0] + i] = 0.f;
+        // inputs: h_0 = u rows, h_dot_0 = 0 (the loads of a pass all in flight)
+        {
+            constexpr int kB = 8;
+            const float* ur = a.u + (int64_t)m0 * D;
+            const int nu = rc * D;
+            for (int base = tid; base < nu; base += kB * nt) {
+                float uv[kB];
+#pragma unroll
+                for (int k = 0; k < kB; ++k) uv[k] = ur[min(base + k * nt, nu - 1)];
+#pragma unroll
+                for (int k = 0; k < kB; ++k) {
+                    const int i = base + k * nt;
+                    if (i >= nu) break;
+                    sm[a.lh[0] + i] = uv[k];
+                    sm[a.lhd[0] + i] = 0.f;
+                }
+            }
         }
         __syncthreads();
         // forward + tangent forward: 2 rows x 2 outputs per thread (8 LDS
