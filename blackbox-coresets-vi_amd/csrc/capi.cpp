@@ -31,6 +31,7 @@ extern int g_net_wg_target;              // kernels_net.hip
 extern int g_fwd_ablation;               // kernels_mvn.hip
 extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
+extern unsigned long long* g_rop_stamps; // kernels_rop.hip
 }  // namespace psvi
 
 using namespace psvi;
@@ -460,6 +461,7 @@ int psvi_debug_set_ptr(int32_t key, void* ptr) {
     switch (key) {
         case PSVI_DBG_NET_STAMPS: g_net_stamps = (unsigned long long*)ptr; return 0;
         case PSVI_DBG_UPD_STAMPS: g_upd_stamps = (unsigned long long*)ptr; return 0;
+        case PSVI_DBG_ROP_STAMPS: g_rop_stamps = (unsigned long long*)ptr; return 0;
         case PSVI_DBG_FWD_STAMPS: g_fwd_stamps = (unsigned long long*)ptr; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
     }

@@ -49,7 +49,14 @@ struct RopArgs {
     float* Gd;         // [S][n_tot]
     float* du;         // [S][M][D]
     float* nlld;       // [S][M]
+    unsigned long long* stamps;  // diagnostics: 16 phase-clock sums per workgroup (nullptr)
 };
+
+unsigned long long* g_rop_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_ROP_STAMPS, buf)
+
+// layers at most this wide (the loss head) run the 16-lane K-split forms:
+// the 2 x 2 register blocks leave all but a few threads idle there
+constexpr int kRopNarrow = 8;
 
 __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -59,6 +66,19 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     float* XD = sm + a.lxd;
     float* GA = sm + a.lg;
     float* GDA = sm + a.lgd;
+    // diagnostics (thread 0): shader clocks summed per phase -- 0 weights,
+    // 1 inputs, 2-4 forward layers, 5 head, 6-8 backward layers (top first),
+    // 9 the slot stores; slot 15 = chunks
+    unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+    int nchunk = 0;
+    auto ph = [&](int q) __attribute__((always_inline)) {
+        if (a.stamps && tid == 0) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            if (q >= 0) tph[q] += tt - tlast;
+            tlast = tt;
+        }
+    };
+    ph(-1);
     // sampled weights and their tangents, in the per-sample weight layout
     // (layer l at woff_l: W row-major [dout][din], then b)
     for (int l = 0; l < L && a.family == PSVI_FAMILY_FULLCOV; ++l) {
@@ -115,6 +135,7 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
         }
     }
     __syncthreads();
+    ph(0);
     const int rows_per = (a.M + a.nsplit - 1) / a.nsplit;
     const int m_lo = blockIdx.y * rows_per, m_hi = min(a.M, m_lo + rows_per);
     for (int m0 = m_lo; m0 < m_hi; m0 += a.rc) {
@@ -138,6 +159,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             }
         }
         __syncthreads();
+        ph(1);
+        ++nchunk;
         // forward + tangent forward: 2 rows x 2 outputs per thread (8 LDS
         // reads per 12 FMAs; clamped duplicates at odd edges, stored once)
         for (int l = 0; l < L; ++l) {
@@ -150,6 +173,35 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             const float* HD = sm + a.lhd[l];
             float* Hn = sm + a.lh[l + 1];
             float* HDn = sm + a.lhd[l + 1];
+            if (dout <= kRopNarrow) {
+                // narrow layer (the head): a 16-lane row per (row m, output o),
+                // lane j summing inputs i = j, j + 16, ..; DPP row sums
+                const int np = rc * dout, nrow = nt >> 4, lr = tid & 15;
+                const int trips = (np + nrow - 1) / nrow;
+                for (int t = 0; t < trips; ++t) {  // uniform: every lane of every row active
+                    const int pr = t * nrow + (tid >> 4);
+                    const bool valid = pr < np;
+                    const int m = valid ? pr / dout : 0, o = valid ? pr - m * dout : 0;
+                    float acc = 0.f, accd = 0.f;
+                    for (int i = lr; i < din; i += 16) {
+                        const float hv = H[m * din + i], hdv = HD[m * din + i];
+                        const float wv = W[o * ldw + i], wdv = Wd[o * ldw + i];
+                        acc = fmaf(hv, wv, acc);
+                        accd = fmaf(hdv, wv, fmaf(hv, wdv, accd));
+                    }
+                    acc = row16_sum(acc) + b[o];
+                    accd = row16_sum(accd) + bd[o];
+                    if (valid && lr == 0) {
+                        const int qq = m * dout + o;
+                        const bool on = l == L - 1 || acc > 0.f;
+                        Hn[qq] = l == L - 1 ? acc : (on ? acc : 0.f);
+                        HDn[qq] = on ? accd : 0.f;
+                    }
+                }
+                __syncthreads();
+                ph(2 + min(l, 2));
+                continue;
+            }
             const int nbo = (dout + 1) >> 1, nb = ((rc + 1) >> 1) * nbo;
             for (int q = tid; q < nb; q += nt) {
                 const int bm = q / nbo, bo = q - bm * nbo;
@@ -197,6 +249,7 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                     }
             }
             __syncthreads();
+            ph(2 + min(l, 2));
         }
         // head: delta = w (p - onehot), delta_dot = w p (a_dot - p.a_dot)
         float* Dl = sm + a.ld0;
@@ -225,6 +278,7 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             if (a.nlld) a.nlld[(int64_t)s * a.M + m0 + m] = nd;
         }
         __syncthreads();
+        ph(5);
         // R-backward: weight gradients 2 outputs x 2 inputs per thread, the
         // propagation 2 rows x 2 inputs (as the forward)
         for (int l = L - 1; l >= 0; --l) {
@@ -237,7 +291,39 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             float* GDW = GDA + a.woff[l];
             const int md = a.maxd;
             const int nbi = (din + 1) >> 1, nbw = ((dout + 1) >> 1) * nbi;
-            for (int q = tid; q < nbw + dout; q += nt) {
+            if (dout <= kRopNarrow) {
+                // narrow layer: a 16-lane row per weight (then per bias), lane j
+                // summing rows m = j, j + 16, ..; DPP row sums
+                const int ne = nw + dout, nrow = nt >> 4, lr = tid & 15;
+                const int trips = (ne + nrow - 1) / nrow;
+                for (int t = 0; t < trips; ++t) {  // uniform
+                    const int e = t * nrow + (tid >> 4);
+                    const bool valid = e < ne;
+                    float g = 0.f, gd = 0.f;
+                    if (e < nw) {  // row-uniform
+                        const int o = e / din, i = e - o * din;
+                        for (int m = lr; m < rc; m += 16) {
+                            const float dl = Dl[m * md + o], ddl = DDl[m * md + o];
+                            const float hv = H[m * din + i], hdv = HD[m * din + i];
+                            g = fmaf(dl, hv, g);
+                            gd = fmaf(ddl, hv, fmaf(dl, hdv, gd));
+                        }
+                    } else {
+                        const int o = valid ? e - nw : 0;
+                        for (int m = lr; m < rc; m += 16) {
+                            g += Dl[m * md + o];
+                            gd += DDl[m * md + o];
+                        }
+                    }
+                    g = row16_sum(g);
+                    gd = row16_sum(gd);
+                    if (valid && lr == 0) {
+                        GW[e] += g;
+                        GDW[e] += gd;
+                    }
+                }
+            }
+            for (int q = tid; q < (dout <= kRopNarrow ? 0 : nbw + dout); q += nt) {
                 if (q < nbw) {
                     const int bo = q / nbi, bi = q - bo * nbi;
                     const int o0 = 2 * bo, i0 = 2 * bi;
@@ -316,6 +402,7 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                 }
             }
             __syncthreads();
+            ph(6 + min(L - 1 - l, 2));
             float* t0 = Dl; Dl = Dn; Dn = t0;
             float* t1 = DDl; DDl = DDn; DDn = t1;
         }
@@ -325,6 +412,12 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     for (int o = tid; o < a.n_tot; o += nt) {
         a.G[slot + o] = GA[o];
         a.Gd[slot + o] = GDA[o];
+    }
+    ph(9);
+    if (a.stamps && tid == 0) {
+        unsigned long long* o = a.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+        for (int q = 0; q < 10; ++q) o[q] = tph[q];
+        o[15] = nchunk;
     }
 }
 
@@ -549,6 +642,7 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     a.params = params; a.vec = vec; a.eps = eps;
     a.G = G; a.Gd = Gd; a.du = du; a.nlld = nlld;
     a.nsplit = rop_splits(p);
+    a.stamps = g_rop_stamps;
     hipLaunchKernelGGL(net_rop_kernel, dim3(p.d.S, a.nsplit), dim3(512), lds, st, a);
     if (a.nsplit > 1) {
         const int64_t n = (int64_t)p.d.S * p.n_tot;

@@ -37,6 +37,26 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// sum over each 16-lane row (DPP row rotations; every lane of the row active)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dppf<0x128>(v));
+    v = fmaxf(v, dppf<0x124>(v));
+    v = fmaxf(v, dppf<0x122>(v));
+    v = fmaxf(v, dppf<0x121>(v));
+    return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dppf<0x128>(v);  // row_ror:8
+    v += dppf<0x124>(v);  // row_ror:4
+    v += dppf<0x122>(v);  // row_ror:2
+    v += dppf<0x121>(v);  // row_ror:1
+    return v;
+}
+
 // Block-wide sum; `red` is >= blockDim/64 floats of LDS.  All threads call.
 __device__ __forceinline__ float block_sum(float v, float* red) {
     v = wave_sum(v);

@@ -443,6 +443,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     skip (timing diagnostics; wrong results):
                                     1 d P1 GEMM, 2 dW2, 4 patch sums, 8 dW1,
                                     16 image load, 32 P1 load                  */
+#define PSVI_DBG_ROP_STAMPS 18   /* ptr: device uint64 buffer, 16 slots per
+                                    R-op workgroup (sample + split * S): shader
+                                    clocks summed per phase (tools/rop_stamps.py) */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", default="c3")
     ap.add_argument("--n", type=int, default=50)
+    ap.add_argument("--stamps", action="store_true", help="net_rop_kernel phase clocks")
     a = ap.parse_args()
     from psvi.runtime import InnerLoopPlan, randn_
 
@@ -45,6 +46,23 @@ def main():
         torch.cuda.synchronize()
         print(f"{a.cfg} psvi_hvp mixed={mixed}: {(time.perf_counter() - t0) / a.n * 1e3:.4f} ms",
               flush=True)
+    if a.stamps:
+        # net_rop_kernel phase clocks (PSVI_DBG_ROP_STAMPS), mean over workgroups
+        import ctypes
+        import numpy as np
+        nwg = S * 2
+        st = torch.zeros(nwg * 16, dtype=torch.int64, device=dev)
+        plan.lib.psvi_debug_set_ptr(18, ctypes.c_void_p(st.data_ptr()))
+        plan.hvp(u, z, w, eps, p, vec, mixed=True)
+        torch.cuda.synchronize()
+        plan.lib.psvi_debug_set_ptr(18, None)
+        v = st.cpu().numpy().reshape(nwg, 16).astype(np.float64)
+        v = v[v[:, 15] > 0]
+        names = ["weights", "inputs", "fwd0", "fwd1", "fwd2", "head", "bwd2", "bwd1", "bwd0",
+                 "store"]
+        print("net_rop clocks per workgroup (mean): " +
+              " ".join(f"{n}={v[:, i].mean():.0f}" for i, n in enumerate(names)) +
+              f" total={v[:, :10].sum(1).mean():.0f} chunks={v[:, 15].mean():.1f}", flush=True)
 
 
 if __name__ == "__main__":
