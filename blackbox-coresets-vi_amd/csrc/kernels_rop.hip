@@ -220,17 +220,41 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                 const float* w1 = W + o1 * ldw;
                 const float* wd0 = Wd + o0 * ldw;
                 const float* wd1 = Wd + o1 * ldw;
-#pragma unroll 4
-                for (int i = 0; i < din; ++i) {
-                    const float hv[2] = {h0[i], h1[i]}, hdv[2] = {hd0[i], hd1[i]};
-                    const float wv[2] = {w0[i], w1[i]}, wdv[2] = {wd0[i], wd1[i]};
+                if ((din & 3) == 0) {
+                    // h / h_dot rows as float4 (rows 16-byte aligned when din % 4 == 0)
+                    for (int i = 0; i < din; i += 4) {
+                        const float4 ha = *reinterpret_cast<const float4*>(h0 + i);
+                        const float4 hb = *reinterpret_cast<const float4*>(h1 + i);
+                        const float4 hda = *reinterpret_cast<const float4*>(hd0 + i);
+                        const float4 hdb = *reinterpret_cast<const float4*>(hd1 + i);
+                        const float hv4[2][4] = {{ha.x, ha.y, ha.z, ha.w}, {hb.x, hb.y, hb.z, hb.w}};
+                        const float hdv4[2][4] = {{hda.x, hda.y, hda.z, hda.w},
+                                                  {hdb.x, hdb.y, hdb.z, hdb.w}};
 #pragma unroll
-                    for (int r = 0; r < 2; ++r)
+                        for (int j = 0; j < 4; ++j) {
+                            const float wv[2] = {w0[i + j], w1[i + j]}, wdv[2] = {wd0[i + j], wd1[i + j]};
 #pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            acc[r][c] = fmaf(hv[r], wv[c], acc[r][c]);
-                            accd[r][c] = fmaf(hdv[r], wv[c], fmaf(hv[r], wdv[c], accd[r][c]));
+                            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                                for (int c = 0; c < 2; ++c) {
+                                    acc[r][c] = fmaf(hv4[r][j], wv[c], acc[r][c]);
+                                    accd[r][c] = fmaf(hdv4[r][j], wv[c], fmaf(hv4[r][j], wdv[c], accd[r][c]));
+                                }
                         }
+                    }
+                } else {
+#pragma unroll 4
+                    for (int i = 0; i < din; ++i) {
+                        const float hv[2] = {h0[i], h1[i]}, hdv[2] = {hd0[i], hd1[i]};
+                        const float wv[2] = {w0[i], w1[i]}, wdv[2] = {wd0[i], wd1[i]};
+#pragma unroll
+                        for (int r = 0; r < 2; ++r)
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) {
+                                acc[r][c] = fmaf(hv[r], wv[c], acc[r][c]);
+                                accd[r][c] = fmaf(hdv[r], wv[c], fmaf(hv[r], wdv[c], accd[r][c]));
+                            }
+                    }
                 }
 #pragma unroll
                 for (int r = 0; r < 2; ++r)
@@ -323,7 +347,60 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                     }
                 }
             }
-            for (int q = tid; q < (dout <= kRopNarrow ? 0 : nbw + dout); q += nt) {
+            // wide layers with din % 4 == 0: 2 outputs x 4 inputs per thread, h
+            // and h_dot rows read as float4 (6 LDS reads per 24 FMAs instead of
+            // 8 per 12); the rest keep the 2 x 2 blocks
+            const bool wide4 = dout > kRopNarrow && (din & 3) == 0;
+            if (wide4) {
+                const int nbi4 = din >> 2, nbw4 = ((dout + 1) >> 1) * nbi4;
+                for (int q = tid; q < nbw4 + dout; q += nt) {
+                    if (q < nbw4) {
+                        const int bo = q / nbi4, bi = q - bo * nbi4;
+                        const int o0 = 2 * bo, o1 = min(o0 + 1, dout - 1), i0 = 4 * bi;
+                        float g[2][4], gd[2][4];
+#pragma unroll
+                        for (int r = 0; r < 2; ++r)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) g[r][c] = gd[r][c] = 0.f;
+#pragma unroll 2
+                        for (int m = 0; m < rc; ++m) {
+                            const float dl[2] = {Dl[m * md + o0], Dl[m * md + o1]};
+                            const float ddl[2] = {DDl[m * md + o0], DDl[m * md + o1]};
+                            const float4 h4 = *reinterpret_cast<const float4*>(H + m * din + i0);
+                            const float4 hd4 = *reinterpret_cast<const float4*>(HD + m * din + i0);
+                            const float hv[4] = {h4.x, h4.y, h4.z, h4.w};
+                            const float hdv[4] = {hd4.x, hd4.y, hd4.z, hd4.w};
+#pragma unroll
+                            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                                for (int c = 0; c < 4; ++c) {
+                                    g[r][c] = fmaf(dl[r], hv[c], g[r][c]);
+                                    gd[r][c] = fmaf(ddl[r], hv[c], fmaf(dl[r], hdv[c], gd[r][c]));
+                                }
+                        }
+#pragma unroll
+                        for (int r = 0; r < 2; ++r) {
+                            if (r && o1 == o0) continue;
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) {
+                                const int qq = (r ? o1 : o0) * din + i0 + c;
+                                GW[qq] += g[r][c];
+                                GDW[qq] += gd[r][c];
+                            }
+                        }
+                    } else {
+                        const int o = q - nbw4;
+                        float g = 0.f, gd = 0.f;
+                        for (int m = 0; m < rc; ++m) {
+                            g += Dl[m * md + o];
+                            gd += DDl[m * md + o];
+                        }
+                        GW[nw + o] += g;
+                        GDW[nw + o] += gd;
+                    }
+                }
+            }
+            for (int q = tid; q < (dout <= kRopNarrow || wide4 ? 0 : nbw + dout); q += nt) {
                 if (q < nbw) {
                     const int bo = q / nbi, bi = q - bo * nbi;
                     const int o0 = 2 * bo, i0 = 2 * bi;
