@@ -86,14 +86,20 @@ def algorithmic_work(S, rows_frac=1.0, layers=LAYERS):
                 sample=dict(bytes=fwd_bytes, flops=fwd_flops))
 
 
-def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")):
+def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r03c_pmc_traffic.json")):
     """HBM bytes per launch of the listed kernels (summed: the phase the
     roofline times) from the committed rocprofv3 PMC summary
     (tools/pmc_session.sh -> tools/pmc_report.py --json: separate FETCH_SIZE /
-    WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction), or None."""
+    WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction), or None.  Summary
+    keys carry template arguments ("mvn_stream_kernel<4, 0, false, true>"):
+    a listed name matches the key equal to it or starting with it and "<"."""
     try:
         d = json.load(open(path))["kernels"]
-        return int(sum(d[k]["hbm_bytes_per_launch"] for k in kernels))
+        tot = 0
+        for k in kernels:
+            key = next(x for x in d if x == k or x.startswith(k + "<"))
+            tot += d[key]["hbm_bytes_per_launch"]
+        return int(tot)
     except Exception:
         return None
 
