@@ -31,6 +31,8 @@ struct RopArgs {
     int L, M, S, n_tot, family, rc, maxd;
     int nsplit;  // workgroups per sample (row blocks), each storing its G / G_dot partial
                  // into its own slot [split][S][n_tot]; slot_sum_kernel adds them in order
+    int single;  // 1: the workgroup's rows are one chunk -- weight gradients go straight
+                 // to its slot (no LDS accumulators)
     int din[kMaxL], dout[kMaxL], woff[kMaxL];
     int64_t poff[kMaxL], eoff[kMaxL];
     int lx, lxd, lg, lgd, lh[kMaxL + 1], lhd[kMaxL + 1], ld0, ld1, ldd0, ldd1;  // LDS carve
@@ -108,8 +110,10 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                                                   : dout * a.ldw[l] + (i - nw));
                 X[dst] = xv[k];
                 XD[dst] = xdv[k];
-                GA[a.woff[l] + i] = 0.f;
-                GDA[a.woff[l] + i] = 0.f;
+                if (!a.single) {
+                    GA[a.woff[l] + i] = 0.f;
+                    GDA[a.woff[l] + i] = 0.f;
+                }
             }
         }
     }
@@ -130,8 +134,10 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                                               : dout * a.ldw[l] + (i - nw));
             X[dst] = xv;
             XD[dst] = xdv;
-            GA[o] = 0.f;
-            GDA[o] = 0.f;
+            if (!a.single) {
+                GA[o] = 0.f;
+                GDA[o] = 0.f;
+            }
         }
     }
     __syncthreads();
@@ -311,8 +317,15 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
             const float* Wd = XD + a.xo[l];
             const float* H = sm + a.lh[l];
             const float* HD = sm + a.lhd[l];
-            float* GW = GA + a.woff[l];
-            float* GDW = GDA + a.woff[l];
+            // one chunk: straight into this row block's slot; else the LDS
+            // accumulators (added over chunks, stored at the end)
+            const int64_t gslot = ((int64_t)blockIdx.y * a.S + s) * a.n_tot + a.woff[l];
+            float* GW = a.single ? a.G + gslot : GA + a.woff[l];
+            float* GDW = a.single ? a.Gd + gslot : GDA + a.woff[l];
+            auto put = [&](float* P, int i, float v) __attribute__((always_inline)) {
+                if (a.single) P[i] = v;
+                else P[i] += v;
+            };
             const int md = a.maxd;
             const int nbi = (din + 1) >> 1, nbw = ((dout + 1) >> 1) * nbi;
             if (dout <= kRopNarrow) {
@@ -342,8 +355,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                     g = row16_sum(g);
                     gd = row16_sum(gd);
                     if (valid && lr == 0) {
-                        GW[e] += g;
-                        GDW[e] += gd;
+                        put(GW, e, g);
+                        put(GDW, e, gd);
                     }
                 }
             }
@@ -384,8 +397,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
 #pragma unroll
                             for (int c = 0; c < 4; ++c) {
                                 const int qq = (r ? o1 : o0) * din + i0 + c;
-                                GW[qq] += g[r][c];
-                                GDW[qq] += gd[r][c];
+                                put(GW, qq, g[r][c]);
+                                put(GDW, qq, gd[r][c]);
                             }
                         }
                     } else {
@@ -395,8 +408,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                             g += Dl[m * md + o];
                             gd += DDl[m * md + o];
                         }
-                        GW[nw + o] += g;
-                        GDW[nw + o] += gd;
+                        put(GW, nw + o, g);
+                        put(GDW, nw + o, gd);
                     }
                 }
             }
@@ -426,8 +439,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                         for (int c = 0; c < 2; ++c) {
                             if ((r && o1 == o0) || (c && i1 == i0)) continue;
                             const int qq = (r ? o1 : o0) * din + (c ? i1 : i0);
-                            GW[qq] += g[r][c];
-                            GDW[qq] += gd[r][c];
+                            put(GW, qq, g[r][c]);
+                            put(GDW, qq, gd[r][c]);
                         }
                 } else {
                     const int o = q - nbw;
@@ -436,8 +449,8 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
                         g += Dl[m * md + o];
                         gd += DDl[m * md + o];
                     }
-                    GW[nw + o] += g;
-                    GDW[nw + o] += gd;
+                    put(GW, nw + o, g);
+                    put(GDW, nw + o, gd);
                 }
             }
             if (l > 0 || a.du) {
@@ -486,7 +499,7 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     }
     // this row block's partial into its own slot (no atomics, no zeroing)
     const int64_t slot = ((int64_t)blockIdx.y * a.S + s) * a.n_tot;
-    for (int o = tid; o < a.n_tot; o += nt) {
+    for (int o = tid; o < (a.single ? 0 : a.n_tot); o += nt) {
         a.G[slot + o] = GA[o];
         a.Gd[slot + o] = GDA[o];
     }
@@ -637,7 +650,7 @@ __global__ __launch_bounds__(256) void sample_sum_kernel(const float* __restrict
 static int rup4(int x) { return (x + 3) & ~3; }
 
 // LDS carve for rows in chunks of rc; returns floats
-static size_t rop_carve(const psvi_plan& p, int rc, RopArgs* a) {
+static size_t rop_carve(const psvi_plan& p, int rc, RopArgs* a, bool with_g = true) {
     size_t off = 0;
     auto take = [&](size_t nfl) {
         const size_t o = off;
@@ -653,7 +666,8 @@ static size_t rop_carve(const psvi_plan& p, int rc, RopArgs* a) {
         xo[l] = xtot;
         xtot += p.lay[l].dout * ldw[l] + p.lay[l].dout;
     }
-    const int lx = take(xtot), lxd = take(xtot), lg = take(p.n_tot), lgd = take(p.n_tot);
+    const int lx = take(xtot), lxd = take(xtot);
+    const int lg = with_g ? take(p.n_tot) : 0, lgd = with_g ? take(p.n_tot) : 0;
     int lh[kMaxL + 1], lhd[kMaxL + 1];
     for (int l = 0; l <= p.L; ++l) {
         const int d = l < p.L ? p.lay[l].din : p.lay[p.L - 1].dout;
@@ -712,13 +726,19 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     (void)once;
     RopArgs a{};
     rop_fill(p, a);
-    const int rc = rop_rows(p);
+    a.nsplit = rop_splits(p);
+    // a workgroup's rows in one chunk when they fit without the LDS gradient
+    // accumulators (C3: 50 rows, 146 KB): every phase then runs once per
+    // workgroup instead of once per chunk
+    const int rows_per = (p.d.M + a.nsplit - 1) / a.nsplit;
+    const bool single = rop_carve(p, rows_per, nullptr, false) * 4 <= kRopLds;
+    const int rc = single ? rows_per : rop_rows(p);
     if (rc == 0) return hipErrorInvalidValue;
-    const size_t lds = rop_carve(p, rc, &a) * 4;
+    const size_t lds = rop_carve(p, rc, &a, !single) * 4;
+    a.single = single ? 1 : 0;
     a.u = u; a.z = z; a.w = w; a.x = x; a.xd = xd;
     a.params = params; a.vec = vec; a.eps = eps;
     a.G = G; a.Gd = Gd; a.du = du; a.nlld = nlld;
-    a.nsplit = rop_splits(p);
     a.stamps = g_rop_stamps;
     hipLaunchKernelGGL(net_rop_kernel, dim3(p.d.S, a.nsplit), dim3(512), lds, st, a);
     if (a.nsplit > 1) {
