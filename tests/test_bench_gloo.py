@@ -133,3 +133,24 @@ def test_bench_multi_rank_control_flow(world):
     assert l2rel(m, o_m) < 1e-5 and l2rel(v, o_v) < 1e-5
     for r in res[1:]:
         assert np.array_equal(r[3], params), "replicas differ after gather_params"
+
+
+def test_pmc_traffic_matches_template_keys(tmp_path):
+    """bench.pmc_traffic sums the committed PMC summary's per-launch HBM bytes;
+    the summary's keys carry template arguments, a listed name matches the key
+    equal to it or starting with it and '<' (not a longer kernel name)."""
+    import importlib.util
+    import json
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    f = tmp_path / "t.json"
+    f.write_text(json.dumps({"kernels": {
+        "mvn_stream_kernel<4, 0, false, true>": {"hbm_bytes_per_launch": 100},
+        "mvn_fwd_reduce_kernel": {"hbm_bytes_per_launch": 7},
+        "mvn_fwd_reduce_kernel_x": {"hbm_bytes_per_launch": 1000}}}))
+    assert b.pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"], str(f)) == 107
+    assert b.pmc_traffic(["mvn_update_kernel"], str(f)) is None
+    # the committed summary the bench line reads
+    assert b.pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"]) > 122379280
