@@ -86,7 +86,13 @@ def algorithmic_work(S, rows_frac=1.0, layers=LAYERS):
                 sample=dict(bytes=fwd_bytes, flops=fwd_flops))
 
 
-def pmc_traffic(kernels, path=os.path.join(ROOT, "profiles", "r03c_pmc_traffic.json")):
+# The PMC summary the roofline's `traffic` is read from, and the commit whose
+# bench it profiled (tools/round_session.sh pmc step: separate FETCH_SIZE /
+# WRITE_SIZE rocprofv3 passes of this bench); reported as `traffic_source`
+PMC_TRAFFIC = dict(file="profiles/r03c_pmc_traffic.json", head="dc74b6e")
+
+
+def pmc_traffic(kernels, path=os.path.join(ROOT, PMC_TRAFFIC["file"])):
     """HBM bytes per launch of the listed kernels (summed: the phase the
     roofline times) from the committed rocprofv3 PMC summary
     (tools/pmc_session.sh -> tools/pmc_report.py --json: separate FETCH_SIZE /
@@ -593,17 +599,19 @@ def headline_world1(rt, args, prep=None):
                                                seed=20251015, offset=args.warmup * eps_stride,
                                                elbo_out=elbo_t, ws=ws))
     # the per-phase split from a separate call (its HIP event records on the
-    # stream would otherwise sit inside the timed region)
+    # stream would otherwise sit inside the timed region): 100 steps, events
+    # around the network and the update of every 10th -- 10 samples whatever
+    # the timed call's K
     if lib.psvi_debug_set(8, 10):  # PSVI_DBG_LOOP_TIMING: every 10th step
         raise RuntimeError("psvi_debug_set(PSVI_DBG_LOOP_TIMING) failed")
     pp, mm, vv = params.clone(), torch.zeros_like(m), torch.zeros_like(v)
-    plan.inner_loop(u, z, w, pp, mm, vv, min(args.steps, 50), LR, seed=20251016, ws=ws)
+    plan.inner_loop(u, z, w, pp, mm, vv, 100, LR, seed=20251016, ws=ws)
     rt.sync()
     tm = (ctypes.c_double * 3)()
     if lib.psvi_debug_loop_timing(tm):
         raise RuntimeError("psvi_debug_loop_timing failed")
     lib.psvi_debug_set(8, 0)
-    avg_ms = {"exchange+net": tm[0] * 1e-3, "update": tm[1] * 1e-3}
+    avg_ms = {"exchange+net": tm[0] * 1e-3, "update": tm[1] * 1e-3, "samples": int(tm[2])}
     return elapsed, elbo_t, avg_ms, plan.param_count
 
 
@@ -677,6 +685,11 @@ def run(rt, args, shapes=None):
     roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
                     traffic=pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"]
                                         if world == 1 else ["mvn_update_kernel"]),
+                    traffic_source=dict(PMC_TRAFFIC, measured_in_this_run=False,
+                                        method="rocprofv3 --pmc FETCH_SIZE, then --pmc "
+                                               "WRITE_SIZE (separate passes) over this bench; "
+                                               "FETCH_SIZE x2 (gfx950 correction)"),
+                    timing_samples=avg_ms.get("samples"),
                     kernel=kname, algorithmic_bytes_per_launch=int(wk["bytes"]),
                     algorithmic_flops_per_launch=int(wk["flops"]),
                     floors_us=dict(hbm=round(hbm_s * 1e6, 2), mfma=round(mfma_s * 1e6, 2)),

@@ -825,9 +825,15 @@ int psvi_mvn_phase_update_sample(const psvi_plan* p, const float* eps, const flo
 
 static int64_t eps_stride(const psvi_plan* p) { return (p->Peps + 3) / 4 * 4; }
 
-// tiled corr/m/v state: full-cov, world 1, one LDS pass of samples
+// tiled corr/m/v state: full-cov, world 1, one LDS pass of samples.  The
+// write-through (sc1) stores of the stream kernel and the chunked kernel's
+// tiled epilogue address all three arrays through ONE buffer descriptor
+// (num_records 0x7fffffff, m / v at 32-bit byte offsets), so the whole state
+// must stay below 2^31 bytes; larger plans keep corr / m / v packed (the
+// chunked kernel with plain stores) instead of overflowing those offsets.
 static bool tiled_ok(const psvi_plan* p) {
-    return p->family == PSVI_FAMILY_FULLCOV && p->fuse_sample && p->tiles_total > 0;
+    return p->family == PSVI_FAMILY_FULLCOV && p->fuse_sample && p->tiles_total > 0 &&
+           3 * p->tiles_total * 4096 * (int64_t)sizeof(float) < 0x7fffffff - 16;
 }
 static size_t tiled_floats(const psvi_plan* p) {
     return tiled_ok(p) ? 3 * (size_t)p->tiles_total * 4096 : 0;

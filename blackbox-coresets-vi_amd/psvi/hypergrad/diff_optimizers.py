@@ -23,6 +23,7 @@ objective (it carries ``_psvi_inner``: plan, rows, draw and its gradient):
     grad_outputs=v)`` works on it unchanged.
 
 Any other loss goes through torch autograd exactly as in the reference."""
+import contextlib
 from itertools import repeat
 
 import torch
@@ -64,13 +65,39 @@ class _HipGradStep(torch.autograd.Function):
         meta, lr = ctx.meta, ctx.lr
         v = torch.cat([(g if g is not None else torch.zeros_like(p)).reshape(-1).to(torch.float32)
                        for g, p in zip(gouts, ctx.like)]).contiguous()
-        mixed = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        # needs_input_grad is fixed when the node is built; a solver's J^T
+        # products (torch_grad(w_mapped, params)) discard the rows' gradients,
+        # and say so through params_only(): only the mixed-product pass pays
+        # for d/du, d/dw (at C5 the separate d/du pass of every CG iteration)
+        mixed = (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]) and \
+            not meta.get("params_only", False)
         hv, du, dw = meta["plan"].hvp(meta["u"], meta["z"], meta["w"], meta["eps"],
                                       meta["params"], v, mixed=mixed)
         us, ut, ws, wt = ctx.rows
-        gu = (-lr * du).reshape(us).to(ut) if ctx.needs_input_grad[2] else None
-        gw = (-lr * dw).reshape(ws).to(wt) if ctx.needs_input_grad[3] else None
+        gu = (-lr * du).reshape(us).to(ut) if mixed and ctx.needs_input_grad[2] else None
+        gw = (-lr * dw).reshape(ws).to(wt) if mixed and ctx.needs_input_grad[3] else None
         return (None, None, gu, gw, *_split(v - lr * hv, ctx.like))
+
+
+@contextlib.contextmanager
+def params_only(w_mapped):
+    """Scope of J^T products that only the parameters receive
+    (torch_grad(w_mapped, params, ...)): the map's HIP node skips the mixed
+    products d/du, d/dw its backward would otherwise form.  The flag lives on
+    the map's own objective (one dict per map evaluation), so ranks running
+    in threads do not see each other's setting.  No effect on other maps."""
+    tag = getattr(w_mapped[0], "_psvi_gd", None) if w_mapped is not None and len(w_mapped) \
+        else None
+    if tag is None:
+        yield
+        return
+    meta = tag[0]
+    prev = meta.get("params_only", False)
+    meta["params_only"] = True
+    try:
+        yield
+    finally:
+        meta["params_only"] = prev
 
 
 def hip_jvp(w_mapped, vs):

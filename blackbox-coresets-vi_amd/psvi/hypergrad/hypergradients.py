@@ -20,7 +20,7 @@ import torch
 from torch.autograd import grad as torch_grad
 
 from . import CG_torch
-from .diff_optimizers import hip_jvp
+from .diff_optimizers import hip_jvp, params_only
 
 __all__ = ["reverse_unroll", "reverse", "fixed_point", "CG", "CG_normaleq", "neumann", "exact",
            "grd", "list_dot", "jvp", "get_outer_gradients", "cat_list_to_tensor",
@@ -61,7 +61,8 @@ def reverse(params_history, hparams, update_map_history, outer_loss, set_grad=Tr
         w_mapped = update_map_history[k + 1](hist[k], hparams)
         bs = grad_unused_zero(w_mapped, hparams, grad_outputs=alphas, retain_graph=True)
         grads = [g + b for g, b in zip(grads, bs)]
-        alphas = torch_grad(w_mapped, hist[k], grad_outputs=alphas)
+        with params_only(w_mapped):
+            alphas = torch_grad(w_mapped, hist[k], grad_outputs=alphas)
     grads = [g + v for g, v in zip(grads, g_h)]
     if set_grad:
         update_tensor_grads(hparams, grads)
@@ -83,8 +84,9 @@ def fixed_point(params, hparams, K, fp_map, outer_loss, tol=1e-10, set_grad=True
         prev = vs
         if stochastic:
             w_mapped = fp_map(params, hparams)
-        jt = torch_grad(w_mapped, params, grad_outputs=_like(vs, w_mapped),
-                        retain_graph=not stochastic)
+        with params_only(w_mapped):
+            jt = torch_grad(w_mapped, params, grad_outputs=_like(vs, w_mapped),
+                            retain_graph=not stochastic)
         vs = [j.to(torch.float64) + g for j, g in zip(jt, g64)]
         if _norm([a - b for a, b in zip(vs, prev)]) < tol:
             break
@@ -107,7 +109,8 @@ def CG(params, hparams, K, fp_map, outer_loss, tol=1e-10, set_grad=True, stochas
 
     def A(xs):
         wm = fp_map(params, hparams) if stochastic else w_mapped
-        jt = torch_grad(wm, params, grad_outputs=_like(xs, wm), retain_graph=not stochastic)
+        with params_only(wm):
+            jt = torch_grad(wm, params, grad_outputs=_like(xs, wm), retain_graph=not stochastic)
         return [x - j.to(torch.float64) for x, j in zip(xs, jt)]
 
     vs = CG_torch.cg(A, _f64(g_w), max_iter=K, epsilon=tol)
@@ -134,7 +137,8 @@ def CG_normaleq(params, hparams, K, fp_map, outer_loss, tol=1e-10, set_grad=True
         return fp_map(ps, hparams)
 
     def A(xs):
-        jt = torch_grad(w_mapped, params, grad_outputs=_like(xs, w_mapped), retain_graph=True)
+        with params_only(w_mapped):
+            jt = torch_grad(w_mapped, params, grad_outputs=_like(xs, w_mapped), retain_graph=True)
         r = [x - j.to(torch.float64) for x, j in zip(xs, jt)]
         jr = jvp(fmap, params, r)
         return [a - b.detach().to(torch.float64) for a, b in zip(r, jr)]
@@ -158,7 +162,8 @@ def neumann(params, hparams, K, fp_map, outer_loss, tol=1e-10, set_grad=True):
     vs = gs = _f64(g_w)
     for _ in range(K):
         prev = gs
-        jt = torch_grad(w_mapped, params, grad_outputs=_like(vs, w_mapped), retain_graph=True)
+        with params_only(w_mapped):
+            jt = torch_grad(w_mapped, params, grad_outputs=_like(vs, w_mapped), retain_graph=True)
         vs = [j.to(torch.float64) for j in jt]
         gs = [g + v for g, v in zip(gs, vs)]
         if _norm([a - b for a, b in zip(gs, prev)]) < tol:

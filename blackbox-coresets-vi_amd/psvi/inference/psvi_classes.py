@@ -55,9 +55,15 @@ What runs where
     label (its 2-d logits broadcast in Categorical.log_prob) -- reproduced as
     the standard objective over M*C expanded rows.
 
-``inner_elbo`` treats u and v as constants (no gradient flows to them); the
-trainers carry the hypergradients of u, v and alpha themselves.  Soft labels
-(``learn_z``) and the truncated nested step raise NotImplementedError.
+``inner_elbo`` is differentiable (first order) w.r.t. the parameters and,
+as the reference's autograd, w.r.t. u and v / alpha where they require grad
+(the row node ``HipInnerRows``); the trainers carry the hypergradients of u, v
+and alpha through ``psvi_hvp``'s mixed products.  Soft labels (``learn_z``:
+expanded (row, class) rows, z through the softmax over rows) and
+``nested_step(truncated=True)`` are built (fixtures w01-w05); ``hyper_step``
+with ``learn_z`` raises NotImplementedError as the reference does
+(psvi_classes.py:619-620), and so does ``learn_z`` with samples sharded over
+ranks (world > 1).
 
 There is no CPU fallback: a missing libpsvi_hip.so or GPU raises.
 """
@@ -372,6 +378,12 @@ class PSVI:
         self._defer_labels = True
         try:
             yield
+        except BaseException:
+            # a step that fails for another reason must not leave a flag from
+            # its (possibly bad) batch behind for the next call to raise on
+            if not prev:
+                self._label_flag = None
+            raise
         finally:
             self._defer_labels = prev
             self._eps_feed = None

@@ -26,6 +26,26 @@ import torch
 from .engine import InnerLoopPlan, adam_update_, randn_
 
 
+def check_exchange(out, inp, out_splits, in_splits, world):
+    """The all_to_all contract, asserted before every exchange so that a
+    mismatch fails loudly on the first scaling run instead of moving the
+    wrong bytes: one split per rank, non-negative, summing to each buffer's
+    numel; both buffers contiguous float32 on one device."""
+    for name, t, sp in (("out", out, out_splits), ("inp", inp, in_splits)):
+        if len(sp) != world:
+            raise ValueError(f"all_to_all {name}: {len(sp)} splits for world {world}")
+        if any(int(x) < 0 for x in sp):
+            raise ValueError(f"all_to_all {name}: negative split in {list(sp)}")
+        if sum(int(x) for x in sp) != t.numel():
+            raise ValueError(f"all_to_all {name}: splits sum to {sum(sp)}, buffer has "
+                             f"{t.numel()} elements")
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"all_to_all {name}: contiguous float32 expected (got {t.dtype}, "
+                             f"contiguous={t.is_contiguous()})")
+    if out.device != inp.device:
+        raise ValueError(f"all_to_all: buffers on {out.device} and {inp.device}")
+
+
 class TorchDistComm:
     """Collectives on torch.distributed (backend 'nccl' == RCCL on ROCm)."""
 
@@ -37,11 +57,15 @@ class TorchDistComm:
 
         self.dist = dist
         self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
 
     def all_to_all(self, out, inp, out_splits, in_splits):
+        check_exchange(out, inp, out_splits, in_splits, self.world)
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
     def all_reduce(self, t):
+        if not t.is_contiguous():
+            raise ValueError("all_reduce: contiguous buffer expected")
         self.dist.all_reduce(t, group=self.group)
 
 
@@ -56,6 +80,7 @@ class HostStagedComm(TorchDistComm):
     host_staged = True
 
     def all_to_all(self, out, inp, out_splits, in_splits):
+        check_exchange(out, inp, out_splits, in_splits, self.world)
         o = torch.empty(out.shape, dtype=out.dtype)
         self.dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
         out.copy_(o)
