@@ -620,9 +620,8 @@ def rows_fraction(loop, layers):
     n = [i * o + o for i, o in layers]
     info = loop.info[loop.rank]
     nnz_own = 0
-    for l, k in enumerate(n):
-        lo, hi = info["row_lo"][l], info["row_lo"][l] + info["row_cnt"][l]
-        nnz_own += sum(min(r, k - 1) for r in range(lo, hi))
+    for (l, lo, cnt, _) in info["runs"]:
+        nnz_own += sum(min(r, n[l] - 1) for r in range(lo, lo + cnt))
     return nnz_own / sum((k - 1) * (k - 2) // 2 for k in n)
 
 

@@ -64,24 +64,66 @@ constexpr int64_t kLenetRowFloats = 2 * 1176 + 400 * 2 + 120 * 2 + 84 * 2 + 10; 
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// nnz-balanced contiguous split of rows [0, n) of a full-cov layer: row r
-// owns r strict-lower corr entries (r <= n-2) plus mean and sd.
-void split_rows(int n, int world, int* lo, int* hi) {
-    std::vector<double> cum(n + 1, 0.0);
-    for (int r = 0; r < n; ++r) cum[r + 1] = cum[r] + (r <= n - 2 ? r : 0) + 2.0;
-    const double tot = cum[n];
-    int start = 0;
-    for (int q = 0; q < world; ++q) {
-        int end = n;
-        if (q < world - 1) {
-            const double target = tot * (q + 1) / world;
-            end = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-            end = std::max(start, std::min(end, n));
-        }
-        lo[q] = start;
-        hi[q] = end;
-        start = end;
+// Row shards.  World > 1 full-cov: whole 64-row bands, so that every rank's
+// update and sample work is whole 64 x 64 tiles of L (a band split between
+// two ranks would be computed by both).  Band b of a layer holds b + 1 tiles
+// (its strict-lower triangle); the bands of all layers are dealt largest
+// first to the least-loaded rank (ties: the lower rank), which balances the
+// tile counts to within one small band (C4 at 8 ranks: 151..153 of 1,215
+// tiles; a contiguous nnz split would make a rank compute up to 216 tiles
+// because its partial edge bands count whole).  A rank's rows are the union
+// of its bands -- runs of consecutive bands -- and its x-shard columns run
+// layer-major in row order.  World 1 (and the replicated mean-field / LeNet
+// rows): one run per layer.
+void assign_rows(psvi_plan& p) {
+    for (int q = 0; q < p.world; ++q) {
+        p.rows_tot[q] = 0;
+        p.runs[q].clear();
     }
+    p.band_owner.clear();
+    p.band_coloff.clear();
+    int nbt = 0;
+    for (int l = 0; l < p.L; ++l) {
+        p.band_base[l] = nbt;
+        nbt += (p.lay[l].n - 1) / 64 + 1;
+    }
+    p.band_base[p.L] = nbt;
+    const bool banded = p.family == PSVI_FAMILY_FULLCOV && p.world > 1;
+    std::vector<int> owner(nbt, 0);
+    if (banded) {
+        std::vector<int> order(nbt);
+        std::vector<double> cost(nbt);
+        for (int l = 0; l < p.L; ++l)
+            for (int b = 0; b < p.band_base[l + 1] - p.band_base[l]; ++b)
+                cost[p.band_base[l] + b] = b + 1.0;
+        for (int i = 0; i < nbt; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+        std::vector<double> load(p.world, 0.0);
+        for (int i : order) {
+            const int q = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            owner[i] = q;
+            load[q] += cost[i];
+        }
+    }
+    p.band_coloff.assign(nbt, 0);
+    for (int q = 0; q < p.world; ++q)
+        for (int l = 0; l < p.L; ++l) {
+            const int n = p.lay[l].n;
+            p.xcol_l[q][l] = p.rows_tot[q];
+            for (int b = 0; 64 * b < n; ++b) {
+                const int gb = p.band_base[l] + b;
+                if (banded && owner[gb] != q) continue;
+                const int r0 = 64 * b, r1 = std::min(n, r0 + 64);
+                std::vector<ShardRun>& rv = p.runs[q];
+                if (!rv.empty() && rv.back().layer == l && rv.back().hi == r0)
+                    rv.back().hi = r1;
+                else
+                    rv.push_back(ShardRun{l, r0, r1, p.rows_tot[q]});
+                p.band_coloff[gb] = p.rows_tot[q] - r0;
+                p.rows_tot[q] += r1 - r0;
+            }
+        }
+    p.band_owner = owner;
 }
 
 template <class T>
@@ -226,28 +268,16 @@ int build_plan(psvi_plan& p) {
         p.s_off[q] = q * base + std::min(q, rem);
     }
     // row shards
-    for (int q = 0; q < p.world; ++q) p.rows_tot[q] = 0;
-    for (int l = 0; l < p.L; ++l) {
-        int lo[kMaxWorld], hi[kMaxWorld];
-        if (p.family == PSVI_FAMILY_FULLCOV) {
-            split_rows(p.lay[l].n, p.world, lo, hi);
-        } else {
-            for (int q = 0; q < p.world; ++q) { lo[q] = 0; hi[q] = p.lay[l].n; }
-        }
-        for (int q = 0; q < p.world; ++q) {
-            p.row_lo[q][l] = lo[q];
-            p.row_hi[q][l] = hi[q];
-            p.xcol_l[q][l] = p.rows_tot[q];
-            p.rows_tot[q] += hi[q] - lo[q];
-        }
-    }
+    assign_rows(p);
     p.acc_count = 2 * (int64_t)p.n_tot;
     net_plan_geometry(p);
     if (p.net_lds > 160 * 1024)
         return fail(PSVI_EUNSUP, "layer too wide for the per-sample LDS network kernel");
     // the kernels address parameters, eps and the x / g shards with 32-bit offsets
     const int64_t kMaxOff = (int64_t(1) << 31) - 4096;
-    if (p.P > kMaxOff || p.Peps > kMaxOff || (int64_t)d.S * p.rows_tot[0] > kMaxOff ||
+    int rows_max = 0;
+    for (int q = 0; q < p.world; ++q) rows_max = std::max(rows_max, p.rows_tot[q]);
+    if (p.P > kMaxOff || p.Peps > kMaxOff || (int64_t)d.S * rows_max > kMaxOff ||
         (int64_t)d.S * p.n_tot > kMaxOff)
         return fail(PSVI_EUNSUP, "buffers beyond 2^31 floats are not supported");
 
@@ -260,14 +290,12 @@ int build_plan(psvi_plan& p) {
         // c-blocks per update chunk: about one chunk per workgroup slot
         // (256 CUs x 3 resident update workgroups), at least one
         int tiles = 0;
-        for (int l = 0; l < p.L; ++l) {
-            const int lo = p.row_lo[r][l], hi = p.row_hi[r][l];
-            for (int b = lo / 64; 64 * b < hi; ++b) tiles += b + 1;
-        }
+        for (const ShardRun& run : p.runs[r])
+            for (int b = run.lo / 64; 64 * b < run.hi; ++b) tiles += b + 1;
         const int ch = g_upd_chunk_tiles > 0 ? g_upd_chunk_tiles : std::max(1, (tiles + 511) / 512);
-        for (int l = 0; l < p.L; ++l) {
-            const int n = p.lay[l].n, lo = p.row_lo[r][l], hi = p.row_hi[r][l];
-            const int xc = p.xcol_l[r][l];
+        for (const ShardRun& run : p.runs[r]) {
+            const int l = run.layer, n = p.lay[l].n, lo = run.lo, hi = run.hi;
+            const int xc = run.col;
             for (int r0 = lo; r0 < hi; r0 += kFwdRows) {
                 const int r1 = std::min(r0 + kFwdRows, hi);
                 const int kmax = std::max(0, std::min(r1 - 1, n - 2));
@@ -519,6 +547,13 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                 hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the streaming-update scratch");
         }
+        if (!rc && family == PSVI_FAMILY_FULLCOV) {
+            std::vector<uint32_t> xmap;
+            std::vector<NetBand> bands;
+            net_xmap(*p, xmap, bands);
+            if (!(rc = upload(xmap, &p->d_net_xmap)))
+                rc = upload(bands, &p->d_net_bands);
+        }
         if (!rc && family == PSVI_FAMILY_FULLCOV && p->mchunks > 1) {
             const size_t bytes = sizeof(float) * (size_t)p->mchunks *
                                  std::max(1, p->s_cnt[p->rank]) * p->n_tot;
@@ -565,6 +600,8 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);
     if (p->d_mf_slots) (void)hipFree(p->d_mf_slots);
     if (p->d_net_slots) (void)hipFree(p->d_net_slots);
+    if (p->d_net_xmap) (void)hipFree(p->d_net_xmap);
+    if (p->d_net_bands) (void)hipFree(p->d_net_bands);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->aux_st) (void)hipStreamDestroy(p->aux_st);
@@ -678,8 +715,34 @@ int psvi_plan_shard_info(const psvi_plan* p, int32_t r, int64_t* out) {
     out[1] = p->s_cnt[r];
     out[2] = p->rows_tot[r];
     for (int l = 0; l < PSVI_MAX_LAYERS; ++l) {
-        out[3 + l] = l < p->L ? p->row_lo[r][l] : 0;
-        out[3 + PSVI_MAX_LAYERS + l] = l < p->L ? p->row_hi[r][l] - p->row_lo[r][l] : 0;
+        int cnt = 0, nrun = 0, lo = 0;
+        for (const ShardRun& run : p->runs[r])
+            if (run.layer == l) {
+                if (nrun++ == 0) lo = run.lo;
+                cnt += run.hi - run.lo;
+            }
+        // the first row when the rank's rows of layer l are one run (or none),
+        // -1 when they are several (psvi_plan_shard_runs lists them)
+        out[3 + l] = nrun <= 1 ? lo : -1;
+        out[3 + PSVI_MAX_LAYERS + l] = cnt;
+    }
+    return 0;
+}
+
+int psvi_plan_shard_runs(const psvi_plan* p, int32_t r, int64_t* out, int32_t cap,
+                         int32_t* count) {
+    if (!p || !count) return fail(PSVI_EINVAL, "null argument");
+    if (r < 0 || r >= p->world) return fail(PSVI_EINVAL, "rank out of range");
+    const int n = (int)p->runs[r].size();
+    *count = n;
+    if (!out) return 0;
+    if (cap < n) return fail(PSVI_ENOSPC, "run buffer too small");
+    for (int i = 0; i < n; ++i) {
+        const ShardRun& run = p->runs[r][i];
+        out[4 * i] = run.layer;
+        out[4 * i + 1] = run.lo;
+        out[4 * i + 2] = run.hi - run.lo;
+        out[4 * i + 3] = run.col;
     }
     return 0;
 }

@@ -64,7 +64,7 @@ struct NetArgs {
     int lwt[kMaxL], ldwt[kMaxL];  // W_l^T (l >= 1: the propagation GEMM's k-contiguous operand)
     int lg[2], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // ldl: dlogits [Mp][lddl]; lzw: z, w
     int nslack, nslack_early, slack[4 * kMaxL + 8];  // float offsets of the 64-float zero slacks
-    int lstage, stage_len, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, staged by source
+    int stage_len, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, source blocks back to back
     const float* u;
     const int32_t* z;
     const float* w;
@@ -101,7 +101,15 @@ struct NetArgs {
     int nsrc;
     int64_t src_base[kMaxWorld];
     int src_stride[kMaxWorld];
-    int src_lo[kMaxWorld][kMaxL], src_hi[kMaxWorld][kMaxL], src_col[kMaxWorld][kMaxL];
+    int xcol0[kMaxL];         // one source: x / g column of layer l's row 0
+    // FULLCOV: LDS destination of x row position r (stage order: source blocks
+    // back to back, each in its x-shard column order): W_l / b_l float offset
+    // in the low 16 bits, W_l^T offset (0xFFFF: none) in the high 16
+    const uint32_t* xmap;
+    // several sources: the gradient of row r of layer l goes to
+    // bands[bbase[l] + r / 64].base + s * .stride + r in g_send
+    const NetBand* bands;
+    int nbands, bbase[kMaxL];
 };
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -248,18 +256,18 @@ __device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const 
     }
 }
 
-// FULLCOV: address in x_recv / g_send of row r of layer l (wave-uniform) for
-// local sample s.  One source rank: one contiguous row per sample.  Several:
-// the row's source from the per-workgroup table srct in LDS ([nsrc][L]
-// source-end rows, then [nsrc][L] 64-bit offsets), built at kernel start.
+// FULLCOV: address in g_send of row r of layer l (wave-uniform) for local
+// sample s.  One source rank: one contiguous row per sample.  Several: the
+// row's 64-row band names its owner; the per-workgroup table srct in LDS holds
+// every band's int64 offset for this sample ([nbands]), then the layers'
+// first band index ([L] ints, after the stage's source bases), built at
+// kernel start.
 __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int nsrc, const int* srct, int l, int r,
                                            int s) {
-    if (nsrc == 1) return (int64_t)s * a.src_stride[0] + a.src_col[0][l] + r;
-    const int L = a.L;
-    int p = 0;
-    while (p + 1 < nsrc && r >= srct[p * L + l]) ++p;
-    const int64_t* off = reinterpret_cast<const int64_t*>(srct + 2 * kMaxWorld * kMaxL);
-    return off[p * L + l] + r;
+    if (nsrc == 1) return (int64_t)s * a.src_stride[0] + a.xcol0[l] + r;
+    const int64_t* boff = reinterpret_cast<const int64_t*>(srct);
+    const int* bb = srct + 2 * a.nbands + 3 * kMaxWorld;
+    return boff[bb[l] + (r >> 6)] + r;
 }
 
 // diagnostics: one wave-0 lane of every workgroup records a clock at phase
@@ -305,36 +313,35 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     if (FAM == PSVI_FAMILY_FULLCOV && MSRC) {
         // uniform loops: a per-lane index into the by-value kernel arguments
         // would make the compiler copy the whole argument block to scratch
-        int64_t* off = reinterpret_cast<int64_t*>(srct + 2 * kMaxWorld * kMaxL);
-        int64_t* xb = reinterpret_cast<int64_t*>(srct + 4 * kMaxWorld * kMaxL);
-        int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
-        for (int p = 0; p < nsrc; ++p) {
-            for (int l = 0; l < L; ++l)
-                if (tid == 0) {
-                    srct[p * L + l] = a.src_hi[p][l];
-                    off[p * L + l] = a.src_base[p] + (int64_t)s * a.src_stride[p] +
-                                     a.src_col[p][l] - a.src_lo[p][l];
-                }
-            if (tid == 0) {  // the stage: source p's run at stage_off[p]
+        int64_t* boff = reinterpret_cast<int64_t*>(srct);
+        int64_t* xb = boff + a.nbands;
+        int* xs0 = srct + 2 * a.nbands + 2 * kMaxWorld;
+        int* bb = xs0 + kMaxWorld;
+        for (int i = tid; i < a.nbands; i += blockDim.x) {
+            const NetBand bd = a.bands[i];
+            boff[i] = bd.base + (int64_t)s * bd.stride;
+        }
+        for (int p = 0; p < nsrc; ++p)
+            if (tid == 0) {  // the stage: source p's block at stage_off[p]
                 xs0[p] = a.stage_off[p];
                 xb[p] = a.src_base[p] + (int64_t)s * a.src_stride[p] - a.stage_off[p];
             }
-        }
+        for (int l = 0; l < L; ++l)
+            if (tid == 0) bb[l] = a.bbase[l];
         __syncthreads();
     }
     // Every global load of the phase is issued before its first LDS store:
     // the u chunk (float4 per lane when rows are float4-sized), the labels and
-    // weights, and (full-cov) this sample's x row into a stage -- the source
-    // ranks' runs back to back -- later scattered into the padded W_l, b_l
-    // (LDS-DMA of the rows measured several times slower).  The stage
-    // overlaps the regions written from the forward pass on, whose slacks are
-    // zeroed in the first forward phase.
+    // weights, and (full-cov) this sample's x row -- the source ranks' blocks
+    // back to back -- with each element's LDS destination from the plan's x
+    // map (W_l[j][i] or b_l[j], and W_l^T[i][j]): the elements go straight
+    // into the padded W_l, b_l, W_l^T, no stage, no index arithmetic behind
+    // the loads (LDS-DMA of the rows measured several times slower).
     const int D = a.din[0];
     const int r16 = tid >> 4, c16 = tid & 15, nr16 = blockDim.x >> 4;
     float* zw = sm + a.lzw;  // the chunk's labels (as int bits) and weights
     float* X0 = sm + a.lx[0];
     const int ldx0 = a.ldx[0];
-    float* stage = sm + a.lstage;
     {
         // u chunk as a flat run of nu floats (one load path for every D: two
         // paths -- float4 rows and scalars -- are tail-merged by the compiler
@@ -349,6 +356,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             const int bu = pass * kU * bd + tid, bx = pass * kX * bd + tid;
             float uv[kU];
             float xv[kX];
+            uint32_t xm[kX];
             int zi = 0;
             float wv = 0.f;
             if (!(a.abl & 1)) {
@@ -358,19 +366,24 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     if constexpr (!MSRC) {
                         const float* xr = a.xrecv + (int64_t)s * a.src_stride[0];
 #pragma unroll
-                        for (int k = 0; k < kX; ++k) xv[k] = xr[max(min(bx + k * bd, nx - 1), 0)];
+                        for (int k = 0; k < kX; ++k) {
+                            const int r = max(min(bx + k * bd, nx - 1), 0);
+                            xv[k] = xr[r];
+                            xm[k] = a.xmap[r];
+                        }
                     } else {
-                        // stage position r -> x_recv through the run table in LDS (a
+                        // stage position r -> x_recv through the source table in LDS (a
                         // per-lane pick among the kernel arguments makes the compiler
                         // copy the whole argument block to scratch)
-                        const int64_t* xb = reinterpret_cast<const int64_t*>(srct + 4 * kMaxWorld * kMaxL);
-                        const int* xs0 = srct + 4 * kMaxWorld * kMaxL + 2 * kMaxWorld;
+                        const int64_t* xb = reinterpret_cast<const int64_t*>(srct) + a.nbands;
+                        const int* xs0 = srct + 2 * a.nbands + 2 * kMaxWorld;
 #pragma unroll
                         for (int k = 0; k < kX; ++k) {
                             const int r = max(min(bx + k * bd, nx - 1), 0);
                             int q = 0;
                             while (q + 1 < nsrc && r >= xs0[q + 1]) ++q;
                             xv[k] = a.xrecv[xb[q] + r];
+                            xm[k] = a.xmap[r];
                         }
                     }
                 }
@@ -417,7 +430,10 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
 #pragma unroll
                 for (int k = 0; k < kX; ++k)
-                    if (bx + k * bd < nx) stage[bx + k * bd] = xv[k];
+                    if (bx + k * bd < nx) {
+                        sm[xm[k] & 0xFFFFu] = xv[k];
+                        if ((xm[k] >> 16) != 0xFFFFu) sm[xm[k] >> 16] = xv[k];
+                    }
             }
             if (pass == 0 && tid < mcnt) {
                 zw[tid] = __int_as_float(zi);
@@ -429,45 +445,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             zw[Mp + m] = a.w[m0 + m];
         }
     }
-    if constexpr (FAM == PSVI_FAMILY_FULLCOV) {
-        __syncthreads();  // the stage is complete
-        // scatter: source p's run holds rows [lo, hi) of each layer l at
-        // src_col[p][l]; x row r of layer l is W[j][i] (r = j*din + i) or b
-        constexpr int kB = 8;
-        for (int p = 0; p < nsrc && !(a.abl & 1); ++p) {
-            for (int l = 0; l < L; ++l) {
-                const int lo = a.src_lo[p][l], hi = a.src_hi[p][l];
-                const int din = a.din[l], nw = din * a.dout[l], ldw = a.ldw[l], ldwt = a.ldwt[l];
-                const bool wt = l >= wt_lo;
-                const float rdin = 1.f / (float)din;
-                const float* sl = stage + a.stage_off[p] + a.src_col[p][l] - lo;
-                float* W = sm + a.lw[l];
-                float* WT = sm + a.lwt[l];
-                float* Bv = sm + a.lb[l];
-                for (int base = lo + tid; base < hi; base += kB * (int)blockDim.x) {
-                    float v[kB];
-#pragma unroll
-                    for (int k = 0; k < kB; ++k) v[k] = sl[min(base + k * (int)blockDim.x, hi - 1)];
-#pragma unroll
-                    for (int k = 0; k < kB; ++k) {
-                        const int r = base + k * (int)blockDim.x;
-                        // only this source's rows [lo, hi): a source whose run ends
-                        // inside the weights must not write its clamped tail value
-                        // into rows another source's scatter owns (world > 1)
-                        if (r >= hi) continue;
-                        if (r < nw) {
-                            // exact for r < 2^21: (r + 0.5) / din is >= 0.5/din from an integer
-                            const int j = (int)(((float)r + 0.5f) * rdin), i = r - j * din;
-                            W[j * ldw + i] = v[k];
-                            if (wt) WT[i * ldwt + j] = v[k];
-                        } else {
-                            Bv[r - nw] = v[k];
-                        }
-                    }
-                }
-            }
-        }
-    } else if (!(a.abl & 1)) {
+    if (FAM != PSVI_FAMILY_FULLCOV && !(a.abl & 1)) {
         // Normal.rsample: loc + eps * softplus(rho), elementwise into place
         constexpr int kB = 16;
         for (int l = 0; l < L; ++l) {
@@ -829,11 +807,12 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     const int lred = take(16);
     const int lzw = take(2 * (size_t)Mp);
     const int lstamp = take(48);  // 16 x uint64 diagnostics stamps + 8 wave starts
-    // per-workgroup source tables (world > 1): [nsrc][L] ints, [nsrc][L] int64
-    // (8-byte aligned), the stage's per-source int64 bases and int starts
-    const int lsrc = take(4 * kMaxWorld * kMaxL + 3 * kMaxWorld);
+    // per-workgroup tables (world > 1): every band's int64 g_send offset
+    // (8-byte aligned), the x row's per-source int64 bases and int starts,
+    // the layers' first band index
+    const int nbands = (p.family == PSVI_FAMILY_FULLCOV && p.world > 1) ? p.band_base[p.L] : 0;
+    const int lsrc = take(2 * (size_t)nbands + 3 * kMaxWorld + kMaxL);
     const int ns_early = ns;
-    const size_t lstage = off;
     int ldgmax = 4;
     for (int l = 1; l < p.L; ++l) {
         const int ldx = ld8o(p.lay[l].din);
@@ -848,20 +827,20 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     }
     const int lddl = ld8o(p.lay[p.L - 1].dout);
     const int ldl = take((size_t)Mp * lddl);
-    if (p.family == PSVI_FAMILY_FULLCOV) {
-        size_t st = 0;
+    if (p.family == PSVI_FAMILY_FULLCOV && a) {  // the x row's source blocks (no LDS)
+        int st = 0;
         for (int q = 0; q < p.world; ++q) {
-            if (a) a->stage_off[q] = (int)st;
-            st += (size_t)p.rows_tot[q];
+            a->stage_off[q] = st;
+            st += p.rows_tot[q];
         }
-        if (a) { a->stage_off[p.world] = (int)st; a->stage_len = (int)st; }
-        off = std::max(off, lstage + st);
+        a->stage_off[p.world] = st;
+        a->stage_len = st;
     }
     off = (off + 3) & ~size_t(3);
     if (a) {
         a->lx[0] = lx0; a->ldx[0] = ldx0;
         a->lg[0] = lg0; a->lg[1] = lg1; a->ldl = ldl; a->lddl = lddl;
-        a->lred = lred; a->lsrc = lsrc; a->lzw = lzw; a->lstamp = lstamp; a->lstage = (int)lstage;
+        a->lred = lred; a->lsrc = lsrc; a->lzw = lzw; a->lstamp = lstamp;
         a->Mp = Mp;
         a->nslack = ns;
         a->nslack_early = ns_early;
@@ -912,6 +891,47 @@ size_t net_plan_geometry(psvi_plan& p) {
         }
         ++mchunks;
     }
+}
+
+// The full-cov x map: for every position of a sample's x row as the network
+// kernel loads it (source blocks back to back, each in its x-shard column
+// order: runs of rows), the LDS float offset of W_l[j][i] (row r = j din + i)
+// or b_l[r - din dout], and of W_l^T[i][j] for l >= 1 (0xFFFF: none) -- so
+// the load phase places each element with one lookup.  The world > 1 band
+// table: per 64-row band, g_send's base offset for sample 0 (the owner's
+// block + the band's column - its first row) and the owner's row stride.
+void net_xmap(const psvi_plan& p, std::vector<uint32_t>& xmap, std::vector<NetBand>& bands) {
+    NetArgs a{};
+    net_lds_floats(p, p.mc, &a);
+    xmap.clear();
+    bands.clear();
+    const int S_local = p.s_cnt[p.rank];
+    int64_t base = 0;
+    std::vector<int64_t> src_base(p.world);
+    for (int q = 0; q < p.world; ++q) {
+        src_base[q] = base;
+        base += (int64_t)S_local * p.rows_tot[q];
+        for (const ShardRun& run : p.runs[q]) {
+            const int l = run.layer, din = p.lay[l].din, nw = din * p.lay[l].dout;
+            for (int r = run.lo; r < run.hi; ++r) {
+                uint32_t w, wt = 0xFFFFu;
+                if (r < nw) {
+                    const int j = r / din, i = r - j * din;
+                    w = (uint32_t)(a.lw[l] + j * a.ldw[l] + i);
+                    if (l > 0) wt = (uint32_t)(a.lwt[l] + i * a.ldwt[l] + j);
+                } else {
+                    w = (uint32_t)(a.lb[l] + r - nw);
+                }
+                xmap.push_back(w | wt << 16);
+            }
+        }
+    }
+    if (p.world > 1)
+        for (int l = 0; l < p.L; ++l)
+            for (int b = 0; 64 * b < p.lay[l].n; ++b) {
+                const int gb = p.band_base[l] + b, q = p.band_owner[gb];
+                bands.push_back(NetBand{src_base[q] + p.band_coloff[gb], p.rows_tot[q], 0});
+            }
 }
 
 int g_net_ablation = 0;  // psvi_debug_set(PSVI_DBG_NET_ABLATION, mask)
@@ -975,13 +995,16 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         for (int q = 0; q < p.world; ++q) {
             a.src_base[q] = base;
             a.src_stride[q] = p.rows_tot[q];
-            for (int l = 0; l < p.L; ++l) {
-                a.src_lo[q][l] = p.row_lo[q][l];
-                a.src_hi[q][l] = p.row_hi[q][l];
-                a.src_col[q][l] = p.xcol_l[q][l];
-            }
             base += (int64_t)S_local * p.rows_tot[q];
         }
+        for (int l = 0; l < p.L; ++l) {
+            a.xcol0[l] = p.xcol_l[0][l];
+            a.bbase[l] = p.band_base[l];
+        }
+        a.xmap = p.d_net_xmap;
+        a.bands = p.d_net_bands;
+        a.nbands = p.world > 1 ? p.band_base[p.L] : 0;
+        if (!a.xmap || (p.world > 1 && !a.bands)) return hipErrorInvalidValue;
     }
     // the outer forward pass has no backward: one role
     dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, p.mchunks), block(p.net_threads);

@@ -230,6 +230,21 @@ struct StreamRange {
     uint32_t lbk0;  // tile t0 as layer << 28 | b << 14 | k
 };
 
+// A rank's full-cov rows: rows [lo, hi) of `layer` sit at x-shard columns
+// col .. col + hi - lo (world > 1: runs of whole 64-row bands; world 1 and the
+// replicated families: one run per layer)
+struct ShardRun {
+    int layer, lo, hi, col;
+};
+
+// world > 1 full-cov network kernel: g_send offset of a 64-row band's first
+// row for local sample 0 (owner block + column - first row) and the owner's
+// row stride (its rows_total)
+struct NetBand {
+    int64_t base;
+    int32_t stride, pad;
+};
+
 struct NetArgs;  // kernels_net.hip
 
 // Outer-objective passes of the network kernel (psvi_outer_elbo_grad).
@@ -256,10 +271,21 @@ struct psvi_plan {
     int n_tot = 0;        // per-sample weight-space size (sum n)
     // sample shards
     int s_off[psvi::kMaxWorld], s_cnt[psvi::kMaxWorld];
-    // full-cov row shards: rows [row_lo, row_hi) of each layer per rank
-    int row_lo[psvi::kMaxWorld][psvi::kMaxL], row_hi[psvi::kMaxWorld][psvi::kMaxL];
+    // full-cov row shards: each rank's runs of rows (whole 64-row bands at
+    // world > 1, dealt largest first to the least-loaded rank), its x-shard
+    // columns layer-major in row order
+    std::vector<psvi::ShardRun> runs[psvi::kMaxWorld];
     int rows_tot[psvi::kMaxWorld];
     int xcol_l[psvi::kMaxWorld][psvi::kMaxL];  // column of layer l's first row in a shard
+    // world > 1 full-cov: owner rank and (x-shard column - first row) of every
+    // 64-row band, bands numbered layer by layer from band_base[l]
+    std::vector<int> band_owner, band_coloff;
+    int band_base[psvi::kMaxL + 1] = {0};
+    // network kernel: LDS destination of every x element the workgroup loads
+    // (stage position -> W_l / b_l offset | W_l^T offset << 16, 0xFFFF = none)
+    // and, world > 1, the band table (owner, column offset)
+    uint32_t* d_net_xmap = nullptr;
+    psvi::NetBand* d_net_bands = nullptr;
     // work lists (host copies, then device)
     std::vector<psvi::FwdItem> h_fwd;
     std::vector<psvi::UpdChunk> h_upd;
@@ -322,6 +348,8 @@ inline int plan_in_dim(const psvi_plan& p) {
 inline unsigned plan_nkl_mask(const psvi_plan& p) {
     return p.family == PSVI_FAMILY_LENET ? 0x1Cu : 0xFFu;
 }
+// the full-cov network kernel's x map and band table (kernels_net.hip)
+void net_xmap(const psvi_plan& p, std::vector<uint32_t>& xmap, std::vector<NetBand>& bands);
 // launchers (defined in the .hip translation units)
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                       const float* params, const float* eps, float* mf_slots,

@@ -69,6 +69,7 @@ SIGNATURES = {
     "psvi_plan_destroy": (_I32, [_P]),
     "psvi_plan_query": (_I32, [_P, _I32, ctypes.POINTER(_I64)]),
     "psvi_plan_shard_info": (_I32, [_P, _I32, ctypes.POINTER(_I64)]),
+    "psvi_plan_shard_runs": (_I32, [_P, _I32, _P, _I32, ctypes.POINTER(_I32)]),
     "psvi_inner_step": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P,
                                _SZ, _P]),
     "psvi_elbo_grad": (_I32, [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _SZ, _P]),

@@ -99,12 +99,23 @@ class InnerLoopPlan:
         return v.value
 
     def shard_info(self, r):
+        """Rank r's samples and rows: s_offset, s_count, rows (x-shard columns),
+        row_lo / row_cnt per layer (row_lo -1 when the layer's rows are several
+        runs) and runs = [(layer, first row, count, x-shard column)] in column
+        order (psvi_plan_shard_runs)."""
         out = (ctypes.c_int64 * (3 + 2 * _lib.MAX_LAYERS))()
         check(self.lib.psvi_plan_shard_info(self.handle, r, out), "psvi_plan_shard_info")
         L = len(self.layers)
+        n = ctypes.c_int32()
+        check(self.lib.psvi_plan_shard_runs(self.handle, r, None, 0, ctypes.byref(n)),
+              "psvi_plan_shard_runs")
+        buf = (ctypes.c_int64 * max(4 * n.value, 1))()
+        check(self.lib.psvi_plan_shard_runs(self.handle, r, buf, n.value, ctypes.byref(n)),
+              "psvi_plan_shard_runs")
+        runs = [tuple(int(buf[4 * i + k]) for k in range(4)) for i in range(n.value)]
         return dict(s_offset=out[0], s_count=out[1], rows=out[2],
                     row_lo=[out[3 + l] for l in range(L)],
-                    row_cnt=[out[3 + _lib.MAX_LAYERS + l] for l in range(L)])
+                    row_cnt=[out[3 + _lib.MAX_LAYERS + l] for l in range(L)], runs=runs)
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -91,6 +91,21 @@ class HostStagedComm(TorchDistComm):
         t.copy_(h)
 
 
+def layer_rows(info, l):
+    """(rows, cols): the rows of layer l a rank owns (ascending) and their
+    columns in its x / g shard, from shard_info's runs (numpy int arrays)."""
+    import numpy as np
+
+    rows, cols = [], []
+    for (ll, lo, cnt, col) in info["runs"]:
+        if ll == l:
+            rows.append(np.arange(lo, lo + cnt))
+            cols.append(np.arange(col, col + cnt))
+    if not rows:
+        return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
+    return np.concatenate(rows), np.concatenate(cols)
+
+
 class ShardedInnerLoop:
     def __init__(self, family, layers, S, M, world, rank, prior_sd=1.0, device="cuda",
                  comm=None):
@@ -166,17 +181,19 @@ class ShardedInnerLoop:
             mask[:] = r == 0
             return mask
         info = self.info[r]
-        po = 0
-        for l, (din, dout) in enumerate(self.plan.layers):
+        po = [0]
+        for din, dout in self.plan.layers:
             n = din * dout + dout
-            nc = (n - 1) * (n - 2) // 2
-            lo, hi = info["row_lo"][l], info["row_lo"][l] + info["row_cnt"][l]
-            mask[po + lo:po + hi] = True
-            mask[po + n + lo:po + n + hi] = True
+            po.append(po[-1] + 2 * n + (n - 1) * (n - 2) // 2)
+        for (l, lo, cnt, _) in info["runs"]:
+            din, dout = self.plan.layers[l]
+            n = din * dout + dout
+            hi = lo + cnt
+            mask[po[l] + lo:po[l] + hi] = True
+            mask[po[l] + n + lo:po[l] + n + hi] = True
             clo = min(lo, n - 1)
             chi = min(hi, n - 1)
-            mask[po + 2 * n + clo * (clo - 1) // 2:po + 2 * n + chi * (chi - 1) // 2] = True
-            po += 2 * n + nc
+            mask[po[l] + 2 * n + clo * (clo - 1) // 2:po[l] + 2 * n + chi * (chi - 1) // 2] = True
         return mask
 
     def gather_params(self, *tensors):

@@ -128,17 +128,29 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_EVAL_WS_BYTES 14 /* workspace bytes for psvi_evaluate                  */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
- * Samples are split in contiguous blocks; for FULLCOV the rows of every
- * layer's L are split in nnz-balanced contiguous ranges (ranks own the
- * matching mean/sd/corr slices and their Adam state). */
+ * Samples are split in contiguous blocks; for FULLCOV at world > 1 the rows
+ * of the layers' L are split in whole 64-row bands, balanced by their 64 x 64
+ * tile counts over all layers (ranks own the matching mean/sd/corr rows and
+ * their Adam state; a rank's rows need not be contiguous -- see
+ * psvi_plan_shard_runs). */
 int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world,
                      int32_t rank, psvi_plan** out);
 int psvi_plan_destroy(psvi_plan* plan);
 int psvi_plan_query(const psvi_plan* plan, int32_t key, int64_t* value);
 /* rows (full-cov) and samples owned by rank `r` of the plan's world:
  * out[0] = s_offset, out[1] = s_count, out[2] = rows_total,
- * out[3 + l] = first row of layer l, out[3 + PSVI_MAX_LAYERS + l] = row count. */
+ * out[3 + l] = first row of layer l when the rank's rows of layer l are one
+ * contiguous run (-1 when they are several), out[3 + PSVI_MAX_LAYERS + l] =
+ * row count of layer l. */
 int psvi_plan_shard_info(const psvi_plan* plan, int32_t r, int64_t* out);
+/* The rows of rank `r` as runs, in x-shard column order (layer-major, rows
+ * ascending): out[4 i .. 4 i + 3] = (layer, first row, row count, x-shard
+ * column of the first row) for i < *count.  out == NULL: *count only;
+ * PSVI_ENOSPC when cap < *count.  x_shard / g_shard hold [S][ROWS_LOCAL] in
+ * this column order; x_recv / g_send hold, per source rank q in rank order,
+ * [S_LOCAL][rows_total of q] in q's column order. */
+int psvi_plan_shard_runs(const psvi_plan* plan, int32_t r, int64_t* out, int32_t cap,
+                         int32_t* count);
 
 /* ---- single-process fused step (world == 1) --------------------------------
  * One inner step = reparameterise, batched forward over (S x M), weighted NLL

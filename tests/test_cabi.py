@@ -6,6 +6,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -74,18 +75,33 @@ def test_plan_geometry_fullcov_c3(world):
     assert sum(i["s_count"] for i in infos) == S
     for a, b in zip(infos, infos[1:]):
         assert b["s_offset"] == a["s_offset"] + a["s_count"]
-    # rows: every layer's rows partitioned in order; nnz roughly balanced
-    for l, (din, dout) in enumerate(layers):
-        n = din * dout + dout
-        lo = [i["row_lo"][l] for i in infos]
-        cnt = [i["row_cnt"][l] for i in infos]
-        assert lo[0] == 0 and sum(cnt) == n
-        for r in range(1, world):
-            assert lo[r] == lo[r - 1] + cnt[r - 1]
-    if world > 1:
-        nnz = [sum(sum(rr for rr in range(i["row_lo"][l], i["row_lo"][l] + i["row_cnt"][l]))
-                   for l in range(3)) for i in infos]
-        assert max(nnz) < 1.25 * (sum(nnz) / world)
+    # rows: runs of whole 64-row bands; every layer's rows covered exactly
+    # once; each rank's x-shard columns consecutive, layer-major, rows
+    # ascending; the 64 x 64 tile counts balanced to within one small band
+    ns = [din * dout + dout for din, dout in layers]
+    owner = [np.full(n, -1) for n in ns]
+    tiles = []
+    for r, i in enumerate(infos):
+        col, t = 0, 0
+        prev = (-1, -1)
+        for (l, lo, cnt, c) in i["runs"]:
+            assert c == col and (l, lo) > prev
+            assert lo % 64 == 0 and (cnt % 64 == 0 or lo + cnt == ns[l])
+            assert (owner[l][lo:lo + cnt] == -1).all()
+            owner[l][lo:lo + cnt] = r
+            t += sum(b + 1 for b in range(lo // 64, (lo + cnt - 1) // 64 + 1))
+            col += cnt
+            prev = (l, lo + cnt)
+        assert col == i["rows"] == sum(i["row_cnt"])
+        for l in range(len(layers)):
+            rl = [x for x in i["runs"] if x[0] == l]
+            assert i["row_lo"][l] == (rl[0][1] if len(rl) == 1 else (0 if not rl else -1))
+        tiles.append(t)
+    assert all((o >= 0).all() for o in owner)
+    if world == 1:
+        assert [x[:3] for x in infos[0]["runs"]] == [(l, 0, n) for l, n in enumerate(ns)]
+    else:
+        assert max(tiles) - min(tiles) <= 3, tiles
     for r, p in enumerate(plans):
         me = p.shard_info(r)
         assert p.s_local == me["s_count"] and p.xshard_count == S * me["rows"]

@@ -184,16 +184,17 @@ def test_row_sharded_full_size(W, S, M):
     m1, v1 = torch.zeros_like(p1), torch.zeros_like(p1)
     e1 = plan.inner_step(du, dz, dw, de, p1, m1, v1, step=1, lr=1e-3)
 
+    from psvi.runtime.sharded import layer_rows
+
     loops = [ShardedInnerLoop("fullcov", layers, S, M, W, r) for r in range(W)]
     info = loops[0].info
     n_l = [a * b + b for a, b in layers]
     assert sum(i["s_count"] for i in info) == S and [i["s_offset"] for i in info] == \
         [r * S // W for r in range(W)]
-    for l, n in enumerate(n_l):   # the row shards tile every layer
-        los = [i["row_lo"][l] for i in info]
-        cnt = [i["row_cnt"][l] for i in info]
-        assert los[0] == 0 and all(los[r] + cnt[r] == los[r + 1] for r in range(W - 1))
-        assert los[-1] + cnt[-1] == n
+    rc = [[layer_rows(i, l) for l in range(len(layers))] for i in info]
+    for l, n in enumerate(n_l):   # the row shards (runs of 64-row bands) tile every layer
+        rows = np.sort(np.concatenate([rc[r][l][0] for r in range(W)]))
+        assert np.array_equal(rows, np.arange(n))
     for r in range(W):            # all_to_all split sizes agree pairwise
         for q in range(W):
             assert loops[r].x_in[q] == loops[q].x_out[r]
@@ -205,11 +206,10 @@ def test_row_sharded_full_size(W, S, M):
     for r in range(W):
         loops[r].phase_sample(de, dp)
         X = loops[r].x_shard.view(S, -1).cpu().numpy().astype(np.float64)
-        c = 0
         for l in range(len(layers)):
-            lo, cnt = info[r]["row_lo"][l], info[r]["row_cnt"][l]
-            assert l2rel(X[:, c:c + cnt], Xo[:, woff[l] + lo:woff[l] + lo + cnt]) < 1e-6
-            c += cnt
+            rows, cols = rc[r][l]
+            if len(rows):
+                assert l2rel(X[:, cols], Xo[:, woff[l] + rows]) < 1e-6
     # x exchange, network, G exchange, gradient mode of the update
     for r in range(W):
         parts = [loops[p].x_shard[_offs(loops[p].x_in)[r]:_offs(loops[p].x_in)[r + 1]]
@@ -237,11 +237,9 @@ def test_row_sharded_full_size(W, S, M):
     G = np.zeros((S, woff[-1]))
     for r in range(W):
         Gs = loops[r].g_shard.view(S, -1).cpu().numpy().astype(np.float64)
-        c = 0
         for l in range(len(layers)):
-            lo, cnt = info[r]["row_lo"][l], info[r]["row_cnt"][l]
-            G[:, woff[l] + lo:woff[l] + lo + cnt] = Gs[:, c:c + cnt]
-            c += cnt
+            rows, cols = rc[r][l]
+            G[:, woff[l] + rows] = Gs[:, cols]
     G1 = gs1.view(S, -1).cpu().numpy().astype(np.float64)
     assert rel(nll8, nll1.item()) < 1e-6
     # x differs from world 1 in the last bits (the sample phase's split-K items

@@ -25,22 +25,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _layer_cols(info, layers):
-    """column of each layer's first owned row inside a rank's shard row"""
-    cols, c = [], 0
-    for l in range(len(layers)):
-        cols.append(c)
-        c += info["row_cnt"][l]
-    return cols
-
-
 def _emulate_fullcov(loop, O, layers, S, prior_sd):
-    """Install oracle versions of the three full-cov phases on `loop`."""
+    """Install oracle versions of the three full-cov phases on `loop` (a
+    rank's rows: whole 64-row bands, possibly several runs per layer, at the
+    x-shard columns psvi_plan_shard_runs gives)."""
+    from psvi.runtime.sharded import layer_rows
+
     infos, r = loop.info, loop.rank
     me = infos[r]
     n_l = [a * b + b for a, b in layers]
     woff = np.concatenate([[0], np.cumsum(n_l)]).astype(int)
-    cols = [_layer_cols(i, layers) for i in infos]
+    rc = [[layer_rows(i, l) for l in range(len(layers))] for i in infos]
     s0 = prior_sd
 
     def layer_views(params, eps):
@@ -57,9 +52,9 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
         e = eps.double().numpy()
         X = np.zeros((S, me["rows"]))
         for l, n, mean, sd, corr, E in layer_views(p, e):
-            lo, cnt = me["row_lo"][l], me["row_cnt"][l]
+            rows, cols = rc[r][l]
             L = O.mvn_dense_L(sd, corr, n)
-            X[:, cols[r][l]:cols[r][l] + cnt] = mean[lo:lo + cnt] + E @ L[lo:lo + cnt].T
+            X[:, cols] = mean[rows] + E @ L[rows].T
         loop.x_shard.copy_(torch.from_numpy(X.ravel()).float())
 
     def recv_to_full(buf):
@@ -69,8 +64,8 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
         for p, q in enumerate(infos):
             blk = buf[off:off + s_cnt * q["rows"]].reshape(s_cnt, q["rows"])
             for l in range(len(layers)):
-                lo, cnt = q["row_lo"][l], q["row_cnt"][l]
-                full[:, woff[l] + lo:woff[l] + lo + cnt] = blk[:, cols[p][l]:cols[p][l] + cnt]
+                rows, cols = rc[p][l]
+                full[:, woff[l] + rows] = blk[:, cols]
             off += s_cnt * q["rows"]
         return full
 
@@ -80,8 +75,8 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
         for p, q in enumerate(infos):
             blk = np.zeros((s_cnt, q["rows"]))
             for l in range(len(layers)):
-                lo, cnt = q["row_lo"][l], q["row_cnt"][l]
-                blk[:, cols[p][l]:cols[p][l] + cnt] = full[:, woff[l] + lo:woff[l] + lo + cnt]
+                rows, cols = rc[p][l]
+                blk[:, cols] = full[:, woff[l] + rows]
             out.append(blk.ravel())
         return np.concatenate(out)
 
@@ -103,12 +98,12 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
         G = np.zeros((S, woff[-1]))
         kl = 0.0
         for l, n, mean, sd, corr, E in layer_views(p, e):
-            lo, cnt = me["row_lo"][l], me["row_cnt"][l]
-            G[:, woff[l] + lo:woff[l] + lo + cnt] = Gs[:, cols[r][l]:cols[r][l] + cnt]
-            L = O.mvn_dense_L(sd, corr, n)[lo:lo + cnt]
-            sp = O.softplus(sd[lo:lo + cnt])
+            rows, cols = rc[r][l]
+            G[:, woff[l] + rows] = Gs[:, cols]
+            L = O.mvn_dense_L(sd, corr, n)[rows]
+            sp = O.softplus(sd[rows])
             kl += float(np.sum(np.log(s0) - np.log(sp) - 0.5
-                               + 0.5 * ((L * L).sum(1) + mean[lo:lo + cnt] ** 2) / s0 ** 2))
+                               + 0.5 * ((L * L).sum(1) + mean[rows] ** 2) / s0 ** 2))
         g = O.mvn_grad_from_G(layers, p, G, e, S, prior_sd=s0)
         own = loop.owned_mask().numpy()
         pn, mn, vn = O.adam(kind, p, g, m.double().numpy(), v.double().numpy(), step, lr)

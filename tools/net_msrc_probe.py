@@ -58,8 +58,7 @@ def worldW(split_below, X):
         parts = []
         for q in range(W):
             cols = []
-            for l in range(len(layers)):
-                lo, cnt = info[q]["row_lo"][l], info[q]["row_cnt"][l]
+            for (l, lo, cnt, _) in info[q]["runs"]:
                 cols.append(X[s0:s0 + sc, woff[l] + lo:woff[l] + lo + cnt])
             parts.append(torch.cat(cols, 1).reshape(-1))
         loops[r].x_recv.copy_(torch.cat(parts))
@@ -70,11 +69,8 @@ def worldW(split_below, X):
         o = 0
         for q in range(W):
             blk = gsend[o:o + sc * info[q]["rows"]].reshape(sc, info[q]["rows"])
-            c = 0
-            for l in range(len(layers)):
-                lo, cnt = info[q]["row_lo"][l], info[q]["row_cnt"][l]
+            for (l, lo, cnt, c) in info[q]["runs"]:
                 G[s0:s0 + sc, woff[l] + lo:woff[l] + lo + cnt] = blk[:, c:c + cnt]
-                c += cnt
             o += sc * info[q]["rows"]
     return G, nll
 
