@@ -133,7 +133,9 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
     }
     const int klast = it.k0 + ((it.k1 - it.k0 - 1) / FBK) * FBK;  // last stage start
 
-    for (int sb = 0; sb < a.S; sb += FST) {
+    // sample blocks: gridDim.z workgroups share an item's FST-sample passes
+    // (launch_mvn_fwd spreads them when the items alone leave CUs idle)
+    for (int sb = blockIdx.z * FST; sb < a.S; sb += FST * gridDim.z) {
         floatx16 acc[FT];
 #pragma unroll
         for (int t = 0; t < FT; ++t)
@@ -1491,6 +1493,17 @@ hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, 
     return hipGetLastError();
 }
 
+// Workgroups per forward item along the samples: the items (row blocks x
+// column chunks of the rank's rows) run their FST-sample passes in parallel
+// when they alone would leave the chip's 2 x 256 workgroup slots idle -- the
+// K = S >> 128 shapes (a rank's rows for all S = 1024 samples at 8 ranks, C4
+// on one GPU); every (item, sample) partial still has one writer.
+static int fwd_sample_blocks(const psvi_plan& p, int pairs = 1) {
+    const int nsb = (p.d.S + FST - 1) / FST;
+    const int want = (512 + p.n_fwd * pairs - 1) / (p.n_fwd * pairs);
+    return std::max(1, std::min(nsb, want));
+}
+
 hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* params,
                           float* x_shard, hipStream_t st, const float* diag_of) {
     FwdArgs a{};
@@ -1507,7 +1520,7 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     fill_layers(p, a.lay);
     if (p.n_fwd == 0) return hipSuccess;
     // every x element is written by exactly one reduce thread: no memset
-    hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd, 1, fwd_sample_blocks(p)), dim3(256), 0, st, a);
     constexpr int spb = kRedSpb;  // samples per reduce workgroup
     hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb), dim3(256), 0,
                        st, p.d_frb, p.d_fwd_part, a, x_shard);
@@ -1534,7 +1547,7 @@ hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float
     a.abl = g_fwd_ablation;
     fill_layers(p, a.lay);
     if (p.n_fwd == 0) return hipSuccess;
-    hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd, 2), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd, 2, fwd_sample_blocks(p, 2)), dim3(256), 0, st, a);
     constexpr int spb = kRedSpb;
     hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_frb, (a.S + spb - 1) / spb, 2), dim3(256),
                        0, st, p.d_frb, p.d_fwd_part, a, x, x2);
