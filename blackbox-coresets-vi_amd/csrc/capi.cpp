@@ -22,6 +22,7 @@ extern int g_net_ablation;               // kernels_net.hip
 extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
 extern int g_stream_off;                 // kernels_mvn.hip
+extern int g_ks_off;                     // kernels_mvn.hip
 extern int g_lenet_gemm_valu;            // kernels_lenet.hip
 extern int g_lenet_conv_valu;            // kernels_lenet.hip
 extern int g_lenet_abl;                  // kernels_lenet.hip
@@ -187,6 +188,77 @@ static std::vector<UpdChunk> xcd_order(const std::vector<UpdChunk>& in) {
     for (size_t j = 0; j < len; ++j)
         for (int x = 0; x < kXcd; ++x) out.push_back(j < q[x].size() ? q[x][j] : empty);
     return out;
+}
+
+// K-split streaming update tables (S > 128): the rank's tiles band-major
+// (the diagonal tile last in its band), units (tile, 128-sample pass) cut
+// into equal-cost contiguous runs -- a tile's last unit also carries its
+// Adam epilogue (about half a pass) -- one run per workgroup, two workgroups
+// per CU.  XCD-aware placement as the stream kernel: workgroup w runs on XCD
+// w % 8, so XCD x takes a contiguous eighth of the run list (its bands' G
+// slices and eps column blocks stay in that XCD's L2).
+void build_kstream(psvi_plan& p) {
+    const int r = p.rank, np = (p.d.S + kKsPass - 1) / kKsPass;
+    std::vector<KsTile>& tiles = p.h_ks_tiles;
+    tiles.clear();
+    for (const ShardRun& run : p.runs[r])
+        for (int b = run.lo / 64; 64 * b < run.hi; ++b)
+            for (int k = 0; k <= b; ++k)
+                tiles.push_back(KsTile{run.layer, 64 * b, k, k == b, 64 * b,
+                                       std::min(64 * b + 64, p.lay[run.layer].n), run.col - run.lo, -1});
+    const int T = (int)tiles.size();
+    p.h_ks_segs.clear();
+    p.h_ks_off.clear();
+    p.n_kwg = p.n_ks_slots = p.n_ks_cnt = 0;
+    if (T == 0) return;
+    const int64_t U = (int64_t)T * np;
+    int nwg = (int)std::min<int64_t>(U, 512);
+    if (nwg >= 8) nwg -= nwg % 8;
+    // unit cost: 1 per pass, + 0.5 on a tile's last pass (its epilogue)
+    std::vector<double> cum(U + 1, 0.0);
+    for (int64_t u = 0; u < U; ++u) cum[u + 1] = cum[u] + 1.0 + (u % np == np - 1 ? 0.5 : 0.0);
+    std::vector<int64_t> cut(nwg + 1, 0);
+    cut[nwg] = U;
+    for (int w = 1; w < nwg; ++w) {
+        const double target = cum[U] * w / nwg;
+        int64_t t = (int64_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        cut[w] = std::max(cut[w - 1] + 1, std::min(t, U - (nwg - w)));
+    }
+    // contributors per tile
+    std::vector<int> ncon(T, 0);
+    for (int w = 0; w < nwg; ++w)
+        for (int64_t u = cut[w]; u < cut[w + 1];) {
+            const int t = (int)(u / np);
+            ++ncon[t];
+            u = std::min<int64_t>(cut[w + 1], (int64_t)(t + 1) * np);
+        }
+    std::vector<int> slot0(T, -1), seen(T, 0);
+    for (int t = 0; t < T; ++t)
+        if (ncon[t] > 1) {
+            slot0[t] = p.n_ks_slots;
+            p.n_ks_slots += ncon[t];
+            tiles[t].cnt = p.n_ks_cnt++;
+        }
+    std::vector<std::vector<KsSeg>> per(nwg);
+    for (int w = 0; w < nwg; ++w)
+        for (int64_t u = cut[w]; u < cut[w + 1];) {
+            const int t = (int)(u / np);
+            const int64_t ue = std::min<int64_t>(cut[w + 1], (int64_t)(t + 1) * np);
+            per[w].push_back(KsSeg{t, (int)(u - (int64_t)t * np), (int)(ue - (int64_t)t * np),
+                                   slot0[t], ncon[t], seen[t]++});
+            u = ue;
+        }
+    // XCD placement: workgroup w -> run (w % 8) * (nwg / 8) + w / 8
+    std::vector<int> run_of(nwg);
+    for (int w = 0; w < nwg; ++w)
+        run_of[w] = (nwg % 8 == 0) ? (w % 8) * (nwg / 8) + w / 8 : w;
+    p.h_ks_off.push_back(0);
+    for (int w = 0; w < nwg; ++w) {
+        const auto& v = per[run_of[w]];
+        p.h_ks_segs.insert(p.h_ks_segs.end(), v.begin(), v.end());
+        p.h_ks_off.push_back((int)p.h_ks_segs.size());
+    }
+    p.n_kwg = nwg;
 }
 
 // make_lenet (neural_net.py:334-359): five mean-field-style layers, the first
@@ -400,6 +472,7 @@ int build_plan(psvi_plan& p) {
             p.n_sslots = ns;
         }
         p.upd_tiles = tiles;
+        if (S > kKsPass) build_kstream(p);
         p.n_fwd = (int)fwd.size();
         p.n_upd = (int)p.h_upd.size();
         const size_t xs = sizeof(float) * (size_t)S * p.rows_tot[r];
@@ -453,6 +526,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
+        case PSVI_DBG_KSTREAM_OFF: g_ks_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         case PSVI_DBG_LENET_GEMM_VALU: g_lenet_gemm_valu = value; return 0;
@@ -547,6 +621,18 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                 hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the streaming-update scratch");
         }
+        if (!rc && p->n_kwg > 0) {
+            if (!(rc = upload(p->h_ks_tiles, &p->d_ks_tiles)) &&
+                !(rc = upload(p->h_ks_segs, &p->d_ks_segs)))
+                rc = upload(p->h_ks_off, &p->d_ks_off);
+            const size_t sb = sizeof(float) * (size_t)std::max(1, p->n_ks_slots) * kKsSlotFloats;
+            if (!rc && (hipMalloc((void**)&p->d_ks_slots, sb) != hipSuccess ||
+                        hipMalloc((void**)&p->d_ks_cnt, sizeof(int) * std::max(1, p->n_ks_cnt)) !=
+                            hipSuccess ||
+                        hipMemset(p->d_ks_cnt, 0, sizeof(int) * std::max(1, p->n_ks_cnt)) !=
+                            hipSuccess))
+                rc = fail(PSVI_EUNSUP, "cannot allocate the K-split update's slots");
+        }
         if (!rc && family == PSVI_FAMILY_FULLCOV) {
             std::vector<uint32_t> xmap;
             std::vector<NetBand> bands;
@@ -601,6 +687,11 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_mf_slots) (void)hipFree(p->d_mf_slots);
     if (p->d_net_slots) (void)hipFree(p->d_net_slots);
     if (p->d_net_xmap) (void)hipFree(p->d_net_xmap);
+    if (p->d_ks_tiles) (void)hipFree(p->d_ks_tiles);
+    if (p->d_ks_segs) (void)hipFree(p->d_ks_segs);
+    if (p->d_ks_off) (void)hipFree(p->d_ks_off);
+    if (p->d_ks_slots) (void)hipFree(p->d_ks_slots);
+    if (p->d_ks_cnt) (void)hipFree(p->d_ks_cnt);
     if (p->d_net_bands) (void)hipFree(p->d_net_bands);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);

@@ -911,6 +911,295 @@ __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_ker
     UPD_STAMP(13, __builtin_amdgcn_s_memrealtime());
 }
 
+// ------------------------------------------------ K-split streaming update
+// The full-cov Adam update at K = S > 128 (every rank of the row-sharded step,
+// where a rank's rows take all S samples; C4 on one GPU): the rank's 64 x 64
+// tiles with their K cut in 128-sample passes, units (tile, pass) dealt as
+// equal contiguous runs to persistent workgroups (two per CU; build_kstream).
+// Per pass: the band's G rows and the tile's eps column block staged into LDS
+// (register prefetch of the next pass during the MFMAs), dL^T[c][r] +=
+// sum_s eps[s][c] G[s][r] on v_mfma_f32_32x32x2_f32 (4 waves = 2 x 2 of 32 x
+// 32), the diagonal tile also sum_s G and sum_s G eps per row.  A tile whose
+// passes all sit in one run goes straight to the Adam epilogue (the chunked
+// kernel's packed epilogue: accumulators transposed through LDS, corr / m / v
+// as 256-byte row runs).  A split tile's contributors write their partials to
+// their slots with write-through (sc1) stores, drain them (vmcnt 0), and one
+// lane adds to the tile's counter (relaxed, agent scope); the contributor that
+// draws the last ticket reads every partial with sc1 loads, adds them in pass
+// order (the result does not depend on who arrives last) and runs the
+// epilogue -- the in-launch split-K combine of cdna_hip_programming.md (§6
+// Guideline 16, counter form), correct for any placement of the contributors.
+// No workgroup ever waits on another: the kernel cannot hang on the hand-off.
+struct KsArgs {
+    const KsTile* tiles;
+    const KsSeg* segs;
+    const int* seg_off;
+    float* slots;
+    int* cnt;
+    int64_t slot_bytes;
+    const float* eps;
+    const float* g;
+    int ldg, S;
+    int64_t g_total, e_total;
+    float* params;
+    float* m;
+    float* v;
+    double* kl_out;
+    int64_t pcount;
+    int include_kl;
+    float inv_s0sq, log_s0;
+    AdamC adam;
+    MvnLayerArgs lay[kMaxL];
+};
+
+__global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
+    __shared__ __attribute__((aligned(16))) UpdShared<true> sh;
+    static_assert(kKsPass == USB, "one LDS stage per pass");
+    float* Gs = sh.Gs;
+    float* Es = sh.Es;
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int col4 = tid & 15, srow = tid >> 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int g_total = (int)a.g_total, pcount = (int)a.pcount;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const rsrc_t rs = make_rsrc(a.slots, a.slot_bytes);
+    float klp = 0.f;
+    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
+    for (int si = sbeg; si < send; ++si) {  // uniform
+        const KsSeg sg = a.segs[si];
+        const KsTile tl = a.tiles[sg.tile];
+        int n = a.lay[0].n, eoff = (int)a.lay[0].eoff, poff = (int)a.lay[0].poff;
+#pragma unroll
+        for (int l = 1; l < kMaxL; ++l)  // select: a dynamic index into the arguments goes to scratch
+            if (tl.layer == l) {
+                n = a.lay[l].n;
+                eoff = (int)a.lay[l].eoff;
+                poff = (int)a.lay[l].poff;
+            }
+        const float* E = a.eps + eoff;  // [S][n]; the whole eps buffer is [-eoff, e_rem)
+        const int e_rem = (int)a.e_total - eoff;
+        const int corr_off = poff + 2 * n;
+        const int gcol = tl.xcol + tl.r0 + 4 * col4;
+        auto goff = [&](int s) { return min(s, a.S - 1) * a.ldg + gcol; };
+        auto eofs = [&](int s) { return min(s, a.S - 1) * n + tl.k * UB + 4 * col4; };
+        float4 greg[8], ereg[8];
+        auto load = [&](int pi) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int s = pi * USB + srow + 16 * j;
+                greg[j] = ld4u(a.g, goff(s), 0, g_total);
+                ereg[j] = ld4u(E, eofs(s), -eoff, e_rem);
+            }
+        };
+        auto stage = [&](int pi) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = (srow + 16 * j) * ULD + 4 * col4;
+                const int sr = pi * USB + srow + 16 * j;
+                const bool live = sr < a.S;
+                *reinterpret_cast<float4*>(&Gs[o]) = live ? fix4(greg[j], goff(sr), 0, g_total) : z4;
+                *reinterpret_cast<float4*>(&Es[o]) = live ? fix4(ereg[j], eofs(sr), -eoff, e_rem) : z4;
+            }
+        };
+        // epilogue rows: r_j = r0 + srow + 16 j, columns 64 k + 4 col4 + (0..3)
+        int rowp[4];
+        bool rown[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = tl.r0 + srow + 16 * j;
+            rown[j] = r >= tl.rlo && r < tl.rhi && r >= 1 && r <= n - 2;
+            rowp[j] = corr_off + (int)((int64_t)r * (r - 1) / 2);
+        }
+        float4 pq[4], mq[4], vq[4];
+        auto load_pmv = [&]() {
+            const int cl = tl.k * UB + 4 * col4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                // rows off the band's corr rows load something valid, never stored
+                pq[j] = ld4u(a.params, rowp[j] + cl, 0, pcount);
+                mq[j] = ld4u(a.m, rowp[j] + cl, 0, pcount);
+                vq[j] = ld4u(a.v, rowp[j] + cl, 0, pcount);
+            }
+        };
+        floatx16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        float dgm = 0.f, dgs = 0.f;
+        const bool whole = sg.slot < 0;
+        load(sg.p0);
+        for (int pi = sg.p0; pi < sg.p1; ++pi) {  // uniform
+            stage(pi);
+            __syncthreads();
+            // the next pass's operands behind this pass's MFMAs (corr / m / v
+            // are loaded at the epilogue: prefetched here they keep 48 more
+            // registers live across the MFMAs and the kernel takes scratch)
+            if (pi + 1 < sg.p1) load(pi + 1);
+            const int kend = min(USB, a.S - pi * USB);
+            if (tl.diag) {
+                // column j of Es is row r0 + j of the band
+                for (int s = 32 * wv; s < 32 * wv + 32 && s < kend; ++s) {
+                    const float gv = Gs[s * ULD + lane];
+                    dgm += gv;
+                    dgs = fmaf(gv, Es[s * ULD + lane], dgs);
+                }
+            }
+            const float* Ea = Es + h * ULD + 32 * wc + l32;
+            const float* Gb = Gs + h * ULD + 32 * wr + l32;
+            for (int kk = 0; kk < kend; kk += 16) {
+                float av[8], bv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    av[u] = Ea[(kk + 2 * u) * ULD];
+                    bv[u] = Gb[(kk + 2 * u) * ULD];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+            }
+            __syncthreads();  // every wave done with Gs / Es
+        }
+        if (!whole) {
+            // ---- split tile: publish this contributor's partial (fragment order:
+            // float4 (w * 4 + g) * 64 + lane; then 2 floats of diagonal sums per thread)
+            const uint32_t sbase = (uint32_t)((sg.slot + sg.ci) * kKsSlotFloats) * 4u;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(u32x4, make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2],
+                                                          acc[4 * g + 3])),
+                    rs, sbase + (uint32_t)(((wv * 4 + g) * 64 + lane) * 16), 0, 16);
+            if (tl.diag)
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    __builtin_bit_cast(u32x2, f32x2{dgm, dgs}), rs,
+                    sbase + (uint32_t)(4096 * 4 + tid * 8), 0, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const int old = __hip_atomic_fetch_add(a.cnt + tl.cnt, 1, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                sh.red[0] = __int_as_float(old);
+            }
+            __syncthreads();
+            const int old = __float_as_int(sh.red[0]);
+            __syncthreads();  // everyone has read the ticket before red is reused
+            if (old != sg.nc - 1) continue;  // uniform: another contributor finishes the tile
+            // the last arriver: every partial, in pass order, through sc1 loads
+            if (tid == 0)
+                __hip_atomic_store(a.cnt + tl.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            load_pmv();
+            float4 part[4];
+            f32x2 pd = f32x2{0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+            dgm = dgs = 0.f;
+            for (int c = 0; c < sg.nc; ++c) {  // uniform
+                const uint32_t cb = (uint32_t)((sg.slot + c) * kKsSlotFloats) * 4u;
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    part[g] = __builtin_bit_cast(
+                        float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                    rs, cb + (uint32_t)(((wv * 4 + g) * 64 + lane) * 16), 0, 16));
+                if (tl.diag)
+                    pd = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                        rs, cb + (uint32_t)(4096 * 4 + tid * 8), 0, 16));
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    acc[4 * g] += part[g].x;
+                    acc[4 * g + 1] += part[g].y;
+                    acc[4 * g + 2] += part[g].z;
+                    acc[4 * g + 3] += part[g].w;
+                }
+                dgm += pd[0];
+                dgs += pd[1];
+            }
+        }
+        if (whole) load_pmv();
+        // ---- Adam epilogue: D[i = c][j = r] (j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h)
+        // -> T[r][c] in Es, then the rows' 256-byte runs of corr / m / v
+        float* T = Es;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(&T[(32 * wr + l32) * TLD + 32 * wc + 8 * g + 4 * h]) =
+                make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+        __syncthreads();
+        const int cb = tl.k * UB + 4 * col4;
+        float klt = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = tl.r0 + srow + 16 * j;
+            if (!rown[j] || cb >= r) continue;
+            const int o = rowp[j] + cb;
+            const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
+            const float4 p4 = fix4(pq[j], o, 0, pcount);
+            const float4 m4 = fix4(mq[j], o, 0, pcount);
+            const float4 v4 = fix4(vq[j], o, 0, pcount);
+            float pn[4], mn[4], vn[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float p = f4get(p4, i);
+                klt += cb + i < r ? p * p : 0.f;
+                const float gval = a.include_kl ? f4get(d4, i) + p * a.inv_s0sq : f4get(d4, i);
+                float mm = f4get(m4, i), vv = f4get(v4, i);
+                pn[i] = adam_apply_fast(a.adam, p, gval, mm, vv);
+                mn[i] = mm;
+                vn[i] = vv;
+            }
+            if (cb + 3 < r) {
+                *reinterpret_cast<float4*>(a.params + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
+                *reinterpret_cast<float4*>(a.m + o) = make_float4(mn[0], mn[1], mn[2], mn[3]);
+                *reinterpret_cast<float4*>(a.v + o) = make_float4(vn[0], vn[1], vn[2], vn[3]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    if (cb + i < r) {
+                        a.params[o + i] = pn[i];
+                        a.m[o + i] = mn[i];
+                        a.v[o + i] = vn[i];
+                    }
+            }
+        }
+        klp += klt * (0.5f * a.inv_s0sq);
+        if (tl.diag) {
+            // the band's mean / sd from the four waves' row sums, added in wave order
+            sh.red[wv * 64 + lane] = dgm;
+            sh.red[256 + wv * 64 + lane] = dgs;
+            __syncthreads();
+            const int rr = tl.r0 + tid;
+            if (tid < 64 && rr >= tl.rlo && rr < tl.rhi) {
+                const float* red = sh.red;
+                const float gm = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+                const float gs = red[256 + tid] + red[320 + tid] + red[384 + tid] + red[448 + tid];
+                const int pm = poff + rr, ps = pm + n;
+                const float mu = a.params[pm], sdr = a.params[ps];
+                const float sp = softplus_f(sdr), sgm = sigmoid_f(sdr);
+                float gmean = gm, gsd = gs * sgm;
+                if (a.include_kl) {
+                    gmean += mu * a.inv_s0sq;
+                    gsd += (sp * a.inv_s0sq - 1.f / sp) * sgm;
+                    klp += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
+                }
+                float mm = a.m[pm], vv = a.v[pm];
+                a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
+                a.m[pm] = mm;
+                a.v[pm] = vv;
+                mm = a.m[ps];
+                vv = a.v[ps];
+                a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
+                a.m[ps] = mm;
+                a.v[ps] = vv;
+            }
+        }
+        __syncthreads();  // T / red reads done before the next segment stages
+    }
+    if (a.kl_out && a.include_kl) {
+        const float tot = block_sum(klp, sh.red);
+        if (tid == 0) atomicAdd(a.kl_out, (double)tot);
+    }
+}
+
 // ------------------------------------------------- streaming fused update
 // The inner loop's steady-state update (Adam, tiled corr/m/v state, world 1,
 // S a multiple of 32 up to 128) fused with the next step's sample, as one
@@ -1367,6 +1656,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 }
 
 int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1: chunked, 3: plain-store stream)
+int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128 (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -1675,6 +1965,39 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         } else {
             if (mode == 1) hipLaunchKernelGGL((mvn_update_kernel<false, 1, false, true>), grid, block, 0, st, a);
             else hipLaunchKernelGGL((mvn_update_kernel<false, 0, false, true>), grid, block, 0, st, a);
+        }
+        return hipGetLastError();
+    }
+    if (mode == 2 && !grad_out && p.n_kwg > 0 && !g_ks_off) {
+        // K = S > 128: the K-split streaming update (then the next step's
+        // sample from the new parameters when asked)
+        KsArgs k{};
+        k.tiles = p.d_ks_tiles;
+        k.segs = p.d_ks_segs;
+        k.seg_off = p.d_ks_off;
+        k.slots = p.d_ks_slots;
+        k.cnt = p.d_ks_cnt;
+        k.slot_bytes = (int64_t)sizeof(float) * std::max(1, p.n_ks_slots) * kKsSlotFloats;
+        k.eps = eps;
+        k.g = g_shard;
+        k.ldg = a.ldg;
+        k.S = a.S;
+        k.g_total = a.g_total;
+        k.e_total = a.e_total;
+        k.params = params;
+        k.m = m;
+        k.v = v;
+        k.kl_out = kl_out;
+        k.pcount = p.P;
+        k.include_kl = include_kl;
+        k.inv_s0sq = a.inv_s0sq;
+        k.log_s0 = a.log_s0;
+        k.adam = a.adam;
+        fill_layers(p, k.lay);
+        hipLaunchKernelGGL(mvn_kstream_kernel, dim3(p.n_kwg), block, 0, st, k);
+        if (eps_next) {
+            const hipError_t e = hipGetLastError();
+            return e != hipSuccess ? e : launch_mvn_fwd(p, eps_next, params, x_next, st);
         }
         return hipGetLastError();
     }

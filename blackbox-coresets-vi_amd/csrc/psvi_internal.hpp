@@ -221,6 +221,25 @@ struct UpdChunk {
     int slot;  // fused next-step sample: partial-sum slot ([S][64] floats), -1 if none
 };
 
+// K-split streaming update (mvn_kstream_kernel; Adam, packed state, K = S >
+// 128): the rank's 64 x 64 tiles, each K = S samples cut in passes of 128;
+// the (tile, pass) units, tile-major, are cut into equal contiguous runs, one
+// per workgroup.  A tile whose passes span several runs is "split": each
+// contributor writes its partial dL (and diagonal sums) to its slot, and the
+// contributor whose count comes last adds the partials in pass order and
+// runs the tile's Adam epilogue.
+struct KsTile {
+    int layer, r0, k, diag;  // band rows [r0, r0 + 64), c-block k, k == band
+    int rlo, rhi, xcol;      // rows of the band that exist (< n); g_shard column of row r: xcol + r
+    int cnt;                 // counter index of a split tile (-1: never split)
+};
+constexpr int kKsPass = 128;               // samples per pass (the kernel's LDS stage)
+constexpr int kKsSlotFloats = 4096 + 512;  // a split tile's partial: dL fragments, diagonal sums
+struct KsSeg {
+    int tile, p0, p1;  // passes [p0, p1) of the tile
+    int slot, nc, ci;  // split tiles: first slot, contributors, this one's index (slot -1: whole tile)
+};
+
 // Streaming fused update (mvn_stream_kernel): workgroup w walks tiles
 // [t0, t1) of the layer-major, band-major tile list; its x' partial of each
 // band it touches goes to slots slot0, slot0 + 1, ... (a band's slots are
@@ -317,6 +336,18 @@ struct psvi_plan {
     int n_str = 0, n_sfrb = 0, n_sslots = 0;
     int n_upd = 0;
     int upd_tiles = 0;  // c-blocks over all chunks (work measure)
+    // K-split streaming update (full-cov Adam steps with S > 128): tiles, the
+    // workgroups' segment lists (offsets [n_kwg + 1]), split-tile partial slots
+    // (kKsSlotFloats each) and their arrival counters (zeroed, reset by use)
+    std::vector<psvi::KsTile> h_ks_tiles;
+    std::vector<psvi::KsSeg> h_ks_segs;
+    std::vector<int> h_ks_off;
+    psvi::KsTile* d_ks_tiles = nullptr;
+    psvi::KsSeg* d_ks_segs = nullptr;
+    int* d_ks_off = nullptr;
+    float* d_ks_slots = nullptr;
+    int* d_ks_cnt = nullptr;
+    int n_kwg = 0, n_ks_slots = 0, n_ks_cnt = 0;
     // net kernel geometry
     int mchunks = 1, mc = 0, net_threads = 256, net_roles = 1;
     size_t net_lds = 0;

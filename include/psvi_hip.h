@@ -458,6 +458,8 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_ROP_STAMPS 18   /* ptr: device uint64 buffer, 16 slots per
                                     R-op workgroup (sample + split * S): shader
                                     clocks summed per phase (tools/rop_stamps.py) */
+#define PSVI_DBG_KSTREAM_OFF 19  /* value: 1 = the chunked update kernel instead of
+                                    the K-split streaming one at S > 128 (A/B) */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

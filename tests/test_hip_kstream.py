@@ -1,0 +1,135 @@
+"""The K-split streaming update (mvn_kstream_kernel): the full-cov Adam update
+at K = S > 128 -- every rank of the row-sharded step (a rank's rows take all S
+samples) and C4 on one GPU.  Checked, on seeded synthetic G / eps / state,
+against the float64 oracle's update phase (psvi_oracle.mvn_grad_from_G + the
+reference's Adam: psvi/models/neural_net.py:452-476 reparameterisation
+gradient, robust_higher/optim.py:339-367 / hypergrad/diff_optimizers.py:
+197-213 Adam), against the chunked kernel (PSVI_DBG_KSTREAM_OFF A/B), and for
+run-to-run bitwise reproducibility: a split tile's partials are added in pass
+order whichever contributor arrives last.  Tolerances: parameters and Adam
+state within 1e-6 relative (l2) of the oracle -- fp32 summation over K = S
+samples of an fp64 reference; the Adam moments, which carry the gradient's
+summation error unscaled, within 1e-5 -- and likewise of the chunked kernel."""
+import numpy as np
+import pytest
+import torch
+
+import psvi_oracle as O
+from golden_util import l2rel, rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+FN2 = [(64, 40), (40, 40), (40, 2)]
+
+
+def _state(layers, S, seed):
+    rng = np.random.default_rng(seed)
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        parts += [0.1 * rng.standard_normal(n), rng.uniform(-5, -3, n),
+                  (0.15 / np.sqrt(n)) * rng.standard_normal((n - 1) * (n - 2) // 2)]
+    p = np.concatenate(parts).astype(np.float32)
+    m = (1e-3 * rng.standard_normal(p.size)).astype(np.float32)
+    v = (1e-6 * rng.random(p.size)).astype(np.float32)
+    n_tot = sum(i * o + o for i, o in layers)
+    G = (0.05 * rng.standard_normal((S, n_tot))).astype(np.float32)
+    eps = rng.standard_normal(S * n_tot).astype(np.float32)
+    return p, m, v, G, eps
+
+
+def _run(plan, G_full, eps, p, m, v, step, kind, info, ks_off=0):
+    """One update phase of this plan's rank: g_shard = the rank's columns of
+    G_full in x-shard order; returns (params, m, v, kl) as numpy."""
+    from psvi.runtime.sharded import layer_rows
+
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=DEV)
+    woff = np.concatenate([[0], np.cumsum([i * o + o for i, o in plan.layers])]).astype(int)
+    S = plan.S
+    gs = np.zeros((S, info["rows"]), np.float32)
+    for l in range(len(plan.layers)):
+        rows, cols = layer_rows(info, l)
+        gs[:, cols] = G_full[:, woff[l] + rows]
+    pd, md, vd = t(p), t(m), t(v)
+    kl = torch.zeros(1, dtype=torch.float64, device=DEV)
+    plan.lib.psvi_debug_set(19, ks_off)
+    try:
+        plan.mvn_update(t(eps), t(gs.ravel()), pd, md, vd, step=step, lr=1e-3, kind=kind, kl_out=kl)
+        torch.cuda.synchronize()
+    finally:
+        plan.lib.psvi_debug_set(19, 0)
+    return pd.cpu().numpy(), md.cpu().numpy(), vd.cpu().numpy(), kl.item()
+
+
+def _owned(plan, info):
+    po, mask = 0, np.zeros(plan.param_count, bool)
+    offs = [0]
+    for din, dout in plan.layers:
+        n = din * dout + dout
+        offs.append(offs[-1] + 2 * n + (n - 1) * (n - 2) // 2)
+    for (l, lo, cnt, _) in info["runs"]:
+        din, dout = plan.layers[l]
+        n = din * dout + dout
+        hi = lo + cnt
+        o = offs[l]
+        mask[o + lo:o + hi] = True
+        mask[o + n + lo:o + n + hi] = True
+        clo, chi = min(lo, n - 1), min(hi, n - 1)
+        mask[o + 2 * n + clo * (clo - 1) // 2:o + 2 * n + chi * (chi - 1) // 2] = True
+    return mask
+
+
+@pytest.mark.parametrize("W,S,kind", [(1, 256, "higher"), (1, 1024, "hypergrad"), (1, 300, "higher"),
+                                      (8, 1024, "higher"), (4, 512, "hypergrad"), (2, 256, "higher")])
+def test_kstream_update_matches_oracle_and_chunked(W, S, kind):
+    from psvi.runtime import InnerLoopPlan
+
+    p, m, v, G, eps = _state(FN2, S, 7 + W + S)
+    step = 3
+    g = O.mvn_grad_from_G(FN2, p, G, eps, S)
+    pn_o, mn_o, vn_o = O.adam(kind, p.astype(np.float64), g, m.astype(np.float64),
+                              v.astype(np.float64), step, 1e-3)
+    ranks = range(W) if W <= 2 else (0, W // 2, W - 1)
+    for r in ranks:
+        plan = InnerLoopPlan("fullcov", FN2, S, 100, world=W, rank=r)
+        info = plan.shard_info(r)
+        own = _owned(plan, info)
+        a = _run(plan, G, eps, p, m, v, step, kind, info)
+        b = _run(plan, G, eps, p, m, v, step, kind, info)
+        c = _run(plan, G, eps, p, m, v, step, kind, info, ks_off=1)
+        for x, y in zip(a[:3], b[:3]):   # bitwise run to run
+            assert np.array_equal(x, y)
+        for x, ref, nm, tol in zip(a[:3], (pn_o, mn_o, vn_o), ("params", "m", "v"),
+                                   (1e-6, 1e-5, 1e-5)):
+            assert l2rel(x[own], ref[own]) < tol, (W, r, nm, l2rel(x[own], ref[own]))
+            assert np.array_equal(x[~own], (p, m, v)[("params", "m", "v").index(nm)][~own])
+        for x, y, nm, tol in zip(a[:3], c[:3], ("params", "m", "v"), (1e-6, 1e-5, 1e-5)):
+            assert l2rel(x[own], y[own]) < tol, (W, r, nm)
+        assert rel(a[3], c[3]) < 1e-6
+
+
+def test_kstream_world8_ranks_cover_the_update():
+    """The 8 ranks' K-split updates, each applied to its own rows, assemble the
+    world-1 K-split update of all rows (same G, eps, state)."""
+    from psvi.runtime import InnerLoopPlan
+
+    S, W = 1024, 8
+    p, m, v, G, eps = _state(FN2, S, 99)
+    one = InnerLoopPlan("fullcov", FN2, S, 100)
+    a1 = _run(one, G, eps, p, m, v, 2, "higher", one.shard_info(0))
+    full = [np.zeros_like(p) for _ in range(3)]
+    cover = np.zeros(p.size, int)
+    kl = 0.0
+    for r in range(W):
+        plan = InnerLoopPlan("fullcov", FN2, S, 100, world=W, rank=r)
+        info = plan.shard_info(r)
+        own = _owned(plan, info)
+        res = _run(plan, G, eps, p, m, v, 2, "higher", info)
+        for k in range(3):
+            full[k][own] = res[k][own]
+        cover += own
+        kl += res[3]
+    assert (cover == 1).all()
+    for k, tol in zip(range(3), (1e-6, 1e-5, 1e-5)):
+        assert l2rel(full[k], a1[k]) < tol
+    assert rel(kl, a1[3]) < 1e-6
