@@ -274,7 +274,12 @@ def test_row_sharded_full_size(W, S, M):
     if len(bad) == 0:
         assert l2rel(full, p1.cpu().numpy()) < 1e-6
     # Adam (higher, step 1) applied to the sharded gradient: the kink samples'
-    # G moves near-zero gradient entries, whose Adam step is ~ lr sign(g)
+    # G moves near-zero gradient entries, whose Adam step is ~ lr sign(g).  At
+    # K = S > 128 the step's update is the K-split kernel, which sums dL per
+    # 128-sample pass (and a split tile's passes per contributor) while g8
+    # comes from the chunked gradient mode: an entry whose K = 1024 terms
+    # cancel to |g| ~ 1e-4 carries a few % of fp32 summation noise, and its
+    # step (~ lr g / |g|) moves by that share of lr -- bounded here at 0.1 lr
     p_o, _, _ = O.adam_higher(params.astype(np.float64), g8.cpu().numpy().astype(np.float64),
                               0.0, 0.0, 1, 1e-3)
-    assert l2rel(full, p_o) < 1e-6 and np.abs(full - p_o).max() < 1e-5
+    assert l2rel(full, p_o) < 1e-6 and np.abs(full - p_o).max() < (1e-4 if S > 128 else 1e-5)
