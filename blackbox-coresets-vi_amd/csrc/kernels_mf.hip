@@ -9,23 +9,42 @@
 //   hypergrad adam_step     psvi/hypergrad/diff_optimizers.py:184-213
 // Gradient: d mu = sum_s dW_s + mu/s0^2,
 //   d rho = (sum_s dW_s*eps_s + sp/s0^2 - 1/sp) * sigmoid(rho).
+#include <cstdio>
+#include <cstdlib>
+
 #include "psvi_internal.hpp"
 
 namespace psvi {
 
+// The shortest decimal that rounds to f (what Python's repr shows): the
+// hyperparameters reach the ABI as floats, but the reference forms 1 - beta
+// and the bias corrections 1 - beta^t from the Python doubles (0.999, not
+// 0.999f = 0.99900001287): 1.f - 0.999f = 0.00099998713 would put a 1.3e-5
+// relative error on every (1 - beta2) g^2 term of the second moment.
+static double decimal_of(float f) {
+    char buf[40];
+    for (int digits = 6; digits <= 9; ++digits) {
+        std::snprintf(buf, sizeof buf, "%.*g", digits, (double)f);
+        const double d = std::strtod(buf, nullptr);
+        if ((float)d == f) return d;
+    }
+    return (double)f;
+}
+
 AdamC make_adam(const psvi_adam_hp* hp) {
     AdamC a{};
+    const double b1 = decimal_of(hp->beta1), b2 = decimal_of(hp->beta2), lr = decimal_of(hp->lr);
     a.lr = hp->lr;
     a.b1 = hp->beta1;
     a.b2 = hp->beta2;
     a.eps = hp->eps;
-    a.omb1 = 1.f - hp->beta1;
-    a.omb2 = 1.f - hp->beta2;
-    const double bc1 = 1.0 - std::pow((double)hp->beta1, (double)hp->step);
-    const double bc2 = 1.0 - std::pow((double)hp->beta2, (double)hp->step);
+    a.omb1 = (float)(1.0 - b1);
+    a.omb2 = (float)(1.0 - b2);
+    const double bc1 = 1.0 - std::pow(b1, (double)hp->step);
+    const double bc2 = 1.0 - std::pow(b2, (double)hp->step);
     a.inv_bc1 = (float)(1.0 / bc1);
     a.inv_sqrt_bc2 = (float)(1.0 / std::sqrt(bc2));
-    a.lr_bc1 = (float)(hp->lr / bc1);
+    a.lr_bc1 = (float)(lr / bc1);
     a.inv_bc2 = (float)(1.0 / bc2);
     a.kind = hp->kind;
     return a;
