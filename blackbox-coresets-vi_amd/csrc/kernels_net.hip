@@ -38,17 +38,17 @@
 // to the next multiple of 16 (within the row stride) too (epilogues write
 // them); a k-loop that runs past a row's end reads the next row's (finite)
 // values against zero weights; every region is followed by zeroed slack.
-// The loss head runs on VALU with 4 lanes per pseudopoint (logits in
-// registers up to kMaxC classes, through LDS beyond), fused with the
-// softmax / NLL / dlogits and the first gradient propagation.  Weight
-// gradients leave straight from the MFMA accumulators.
+// Forward, loss head and gradient propagation are row-local: each wave
+// carries whole 16-row tiles through them with no workgroup barrier (the
+// row chain), and the weight gradients -- sums over every row -- follow one
+// barrier.  The loss head runs in the head GEMM's epilogue (C <= 16: a row's
+// logits on a DPP row), else on VALU, one lane per row.  Weight gradients
+// leave straight from the MFMA accumulators.
 #include <algorithm>
 
 #include "psvi_internal.hpp"
 
 namespace psvi {
-
-constexpr int kMaxC = 16;  // classes the VALU loss head keeps in registers
 
 struct NetArgs {
     int L, M, mc, S_total, s_goff, nroles, Mp;
@@ -62,8 +62,8 @@ struct NetArgs {
     // X_0 = u chunk, X_l = relu(a_{l-1})), two gradient buffers, dlogits
     int lw[kMaxL], ldw[kMaxL], lb[kMaxL], lx[kMaxL], ldx[kMaxL];
     int lwt[kMaxL], ldwt[kMaxL];  // W_l^T (l >= 1: the propagation GEMM's k-contiguous operand)
-    int lg[2], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // ldl: dlogits [Mp][lddl]; lzw: z, w
-    int nslack, nslack_early, slack[4 * kMaxL + 8];  // float offsets of the 64-float zero slacks
+    int lg[kMaxL], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // lg[l]: G_l (l < L-1); ldl: dlogits [Mp][lddl]; lzw: z, w
+    int nslack, nslack_early, slack[5 * kMaxL + 8];  // float offsets of the 64-float zero slacks
     int stage_len, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, source blocks back to back
     const float* u;
     const int32_t* z;
@@ -182,8 +182,9 @@ __device__ __forceinline__ int gemm_units(int P, int Q) {
 }
 template <bool ACONT, bool BCONT, int NQ, class Epi>
 __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, const float* A, int lda,
-                                           const float* B, int ldb, Epi epi) {
-    const int nwv = blockDim.x >> 6, lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+                                           const float* B, int ldb, Epi epi, int ustep = 0) {
+    const int nwv = ustep ? ustep : (int)(blockDim.x >> 6), lane = threadIdx.x & 63, i16 = lane & 15,
+              k4 = lane >> 4;
     const int nk = K16 >> 4;
     if (u0 >= nu) return;  // wave-uniform
     const int da = ACONT ? 16 : 16 * lda, db = BCONT ? 16 : 16 * ldb;  // one k-group
@@ -253,6 +254,21 @@ __device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const 
         case 3: gemm_steps<ACONT, BCONT, 3>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
         case 2: gemm_steps<ACONT, BCONT, 2>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
         default: gemm_steps<ACONT, BCONT, 1>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi); break;
+    }
+}
+
+// One 16-row tile by ONE wave: C[p][q] for p < 16, q < Q (every column tile:
+// NQ = all of them up to 3 per unit, so one A read feeds them), K = the
+// contraction.  A / B as mfma_gemm (A at the tile's first row); the epilogue
+// gets rows relative to the tile.
+template <bool ACONT, bool BCONT, class Epi>
+__device__ __forceinline__ void row_gemm(int Q, int K, const float* A, int lda, const float* B, int ldb,
+                                         Epi epi) {
+    const int tq = (Q + 15) >> 4, K16 = (K + 15) & ~15;
+    switch (tq) {
+        case 3: gemm_steps<ACONT, BCONT, 3>(1, 1, K16, 0, A, lda, B, ldb, epi, 1); break;
+        case 2: gemm_steps<ACONT, BCONT, 2>(1, 1, K16, 0, A, lda, B, ldb, epi, 1); break;
+        default: gemm_steps<ACONT, BCONT, 1>(tq, tq, K16, 0, A, lda, B, ldb, epi, 1); break;
     }
 }
 
@@ -415,7 +431,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 for (int m = r16; m < mcnt; m += nr16)
                     if (D + c16 < cend) X0[m * ldx0 + D + c16] = 0.f;
                 for (int i = tid; i < (Mp - mcnt) * ldx0; i += bd) X0[mcnt * ldx0 + i] = 0.f;
-                for (int k = wave_id(); k < a.nslack_early; k += bd >> 6)  // wave-uniform slot
+                for (int k = wave_id(); k < a.nslack; k += bd >> 6)  // wave-uniform slot
                     sm[a.slack[k] + (tid & 63)] = 0.f;
             }
             if (a.abl & 1) continue;
@@ -495,142 +511,156 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         stl[15] = mx;
     }
 
-    // ---- 2. forward: X_{l+1} = relu(X_l W_l^T + b_l), then the logits
-    // X_L = X_{L-1} W_{L-1}^T + b_{L-1} into dl.  Rows past the chunk and
-    // columns past dout (up to the 16-multiple within the stride) are zero.
-    if (FAM == PSVI_FAMILY_FULLCOV)  // the slacks the stage overlapped
-        for (int k = a.nslack_early + wave_id(); k < a.nslack; k += blockDim.x >> 6)
-            sm[a.slack[k] + (tid & 63)] = 0.f;
+    // ---- 2. the row chain.  A layer's output rows depend only on the same
+    // rows of its input, and so do the loss head and the gradient propagation
+    // G_{l-1} = (G_l W_l) * 1[X_l > 0]: wave w carries the chunk's 16-row
+    // tiles w, w + nwaves, ... through the whole forward (every column tile of
+    // a layer), the loss head and the backward propagation without a
+    // workgroup barrier -- it re-reads only LDS rows it wrote itself, after an
+    // lgkmcnt drain.  Rows past the chunk and columns past dout (up to the
+    // 16-multiple within the stride) are written zero.  The weight gradients,
+    // which sum over every row, follow ONE barrier (section 3).
     // The inner objective's loss head (C <= 16: one column tile, a row's
     // logits on the 16 lanes of a DPP row) runs in the head GEMM's epilogue:
     // log-softmax over the lanes, weighted NLL, dlogits w_m (softmax - onehot)
-    // stored in place of the logits -- no separate phase and barrier.
+    // stored in place of the logits.
     const int C = a.dout[L - 1];
     const bool fuse_head = a.outer == 0 && C <= 16 && !(a.abl & 4);
+    const bool bwd = !(a.abl & 8) && a.outer != 1;
+    // outer backward: input gradient of the pseudopoint rows (d loss / d u)
+    const bool dx0 = bwd && a.outer == 2 && a.du_part != nullptr && own_lo == 0;
+    // outer backward: d loss / d pseudo_s and d loss / d data_s scale the rows
+    const float cp = a.outer == 2 ? a.rowcoef[2 * s] : 1.f;
+    const float cd = a.outer == 2 ? a.rowcoef[2 * s + 1] : 1.f;
     float part = 0.f;  // this thread's share of the chunk's weighted NLL
-    for (int l = 0; l < L; ++l) {
-        const int din = a.din[l], dout = a.dout[l];
-        const bool head = l == L - 1;
-        const float* X = sm + a.lx[l];
-        float* Xn = head ? sm + a.ldl : sm + a.lx[l + 1];
-        const float* Bv = sm + a.lb[l];
-        const int ldn = head ? a.lddl : a.ldx[l + 1], jend = min((dout + 15) & ~15, ldn);
-        if (head && fuse_head) {
-            auto epi = [&](int m, int j, floatx4 v, int rot) {  // j = i16: every lane of the row takes part
-                const bool jl = j < C;
-                const float b = Bv[min(j, C - 1)];
+    const int nwv = blockDim.x >> 6, lane = tid & 63;
+    auto drain = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // G_l: dlogits for l = L - 1, else the l-th gradient buffer (stride of X_{l+1})
+    auto gbuf = [&](int l) __attribute__((always_inline)) {
+        return l == L - 1 ? sm + a.ldl : sm + a.lg[l];
+    };
+    auto gld = [&](int l) __attribute__((always_inline)) { return l == L - 1 ? a.lddl : a.ldx[l + 1]; };
+    for (int pt = wave_id(); 16 * pt < Mp; pt += nwv) {  // wave-uniform
+        const int r0 = 16 * pt;
+        for (int l = 0; l < L && !(a.abl & 2); ++l) {
+            const int din = a.din[l], dout = a.dout[l];
+            const bool head = l == L - 1;
+            const float* X = sm + a.lx[l] + r0 * a.ldx[l];
+            float* Xn = (head ? sm + a.ldl : sm + a.lx[l + 1]) + r0 * (head ? a.lddl : a.ldx[l + 1]);
+            const float* Bv = sm + a.lb[l];
+            const int ldn = head ? a.lddl : a.ldx[l + 1], jend = min((dout + 15) & ~15, ldn);
+            if (head && fuse_head) {
+                auto epi = [&](int m, int j, floatx4 v, int rot) {  // j = i16: every lane of the row takes part
+                    const bool jl = j < C;
+                    const float b = Bv[min(j, C - 1)];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m + ((r + rot) & 3);
-                    const float y = v[r] + b;
-                    const float mx = row16_max(jl ? y : -INFINITY);
-                    const float lse = mx + logf(row16_sum(jl ? expf(y - mx) : 0.f));
-                    const int zr = __float_as_int(zw[row]);
-                    const float wr = zw[Mp + row];
-                    const bool ok = row < mcnt;
-                    const float dl = (ok && jl) ? wr * (expf(y - lse) - (j == zr ? 1.f : 0.f)) : 0.f;
-                    if (j < jend) Xn[row * ldn + j] = dl;
-                    if (ok && j == zr) part += wr * (lse - y);
-                }
-            };
-            if (!(a.abl & 2))
-                mfma_gemm<true, true>(Mp, dout, din, 0, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
-            __syncthreads();
-            if (l < 3) NET_STAMP(9 + l, __builtin_amdgcn_s_memtime());
-            continue;
-        }
-        auto epi = [&](int m, int j, floatx4 v, int rot) {
-            if (j < jend) {
-                const bool jl = j < dout;
-                const float b = Bv[min(j, dout - 1)];
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = m + ((r + rot) & 3), rg = r0 + row;
+                        const float y = v[r] + b;
+                        const float mx = row16_max(jl ? y : -INFINITY);
+                        const float lse = mx + logf(row16_sum(jl ? expf(y - mx) : 0.f));
+                        const int zr = __float_as_int(zw[rg]);
+                        const float wr = zw[Mp + rg];
+                        const bool ok = rg < mcnt;
+                        const float dl = (ok && jl) ? wr * (expf(y - lse) - (j == zr ? 1.f : 0.f)) : 0.f;
+                        if (j < jend) Xn[row * ldn + j] = dl;
+                        if (ok && j == zr) part += wr * (lse - y);
+                    }
+                };
+                row_gemm<true, true>(dout, din, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
+            } else {
+                auto epi = [&](int m, int j, floatx4 v, int rot) {
+                    if (j < jend) {
+                        const bool jl = j < dout;
+                        const float b = Bv[min(j, dout - 1)];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float y = v[r] + b;
-                    const int row = m + ((r + rot) & 3);
-                    Xn[row * ldn + j] = (jl && row < mcnt) ? (head ? y : fmaxf(y, 0.f)) : 0.f;
-                }
+                        for (int r = 0; r < 4; ++r) {
+                            const float y = v[r] + b;
+                            const int row = m + ((r + rot) & 3);
+                            Xn[row * ldn + j] = (jl && r0 + row < mcnt) ? (head ? y : fmaxf(y, 0.f)) : 0.f;
+                        }
+                    }
+                };
+                row_gemm<true, true>(dout, din, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
             }
-        };
-        if (l == 0) NET_STAMP(4, __builtin_amdgcn_s_memtime());
-        if (!(a.abl & 2))
-            mfma_gemm<true, true>(Mp, dout, din, 0, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
-        if (l == 0) NET_STAMP(5, __builtin_amdgcn_s_memtime());
-        __syncthreads();
-        if (l < 3) NET_STAMP(9 + l, __builtin_amdgcn_s_memtime());
-    }
-    NET_STAMP(2, __builtin_amdgcn_s_memtime());
-
-    // ---- 3. loss head: one thread per pseudopoint, logits -> weighted NLL,
-    // dlogits w_m (softmax - onehot) in place (rows past the chunk stay 0)
-    if (!fuse_head) {
-        const int ldl = a.lddl;
-        // outer backward: d loss / d pseudo_s and d loss / d data_s scale the rows
-        const float cp = a.outer == 2 ? a.rowcoef[2 * s] : 1.f;
-        const float cd = a.outer == 2 ? a.rowcoef[2 * s + 1] : 1.f;
-        for (int m = tid; m < mcnt && !(a.abl & 4); m += blockDim.x) {
+            drain();
+        }
+        // ---- loss head on VALU (C > 16, the outer objective): lanes 0..15
+        // take the tile's rows, logits -> weighted NLL, dlogits in place
+        if (!fuse_head && !(a.abl & 4) && lane < 16 && r0 + lane < mcnt) {
+            const int m = r0 + lane;
+            const int ldl = a.lddl;
             float* row = sm + a.ldl + m * ldl;
             const int zm = __float_as_int(zw[m]);
             const float wm = zw[Mp + m] * (m0 + m < a.n_pseudo ? cp : cd);
-            if (C <= kMaxC) {
-                float lg[kMaxC];
-                float mx = -INFINITY, lz = 0.f;
-#pragma unroll
-                for (int c = 0; c < kMaxC; ++c)
-                    if (c < C) {
-                        lg[c] = row[c];
-                        mx = fmaxf(mx, lg[c]);
-                        if (c == zm) lz = lg[c];
-                    }
-                float se = 0.f;
-#pragma unroll
-                for (int c = 0; c < kMaxC; ++c)
-                    if (c < C) se += expf(lg[c] - mx);
-                const float lse = mx + logf(se);
-                if (a.outer == 1) {
-                    const int mg = m0 + m;
-                    a.nll_rows[(size_t)s * a.M + mg] = lse - lz;
-                    if (a.prob_rows && mg >= a.n_pseudo) {
-                        float* pr = a.prob_rows + ((size_t)s * (a.M - a.n_pseudo) + mg - a.n_pseudo) * C;
-#pragma unroll
-                        for (int c = 0; c < kMaxC; ++c)
-                            if (c < C) pr[c] = expf(lg[c] - lse);
-                    }
-                    continue;
+            float mx = -INFINITY, lz = 0.f;
+            for (int c = 0; c < C; ++c) {
+                mx = fmaxf(mx, row[c]);
+                if (c == zm) lz = row[c];
+            }
+            float se = 0.f;
+            for (int c = 0; c < C; ++c) se += expf(row[c] - mx);
+            const float lse = mx + logf(se);
+            if (a.outer == 1) {
+                const int mg = m0 + m;
+                a.nll_rows[(size_t)s * a.M + mg] = lse - lz;
+                if (a.prob_rows && mg >= a.n_pseudo) {
+                    float* pr = a.prob_rows + ((size_t)s * (a.M - a.n_pseudo) + mg - a.n_pseudo) * C;
+                    for (int c = 0; c < C; ++c) pr[c] = expf(row[c] - lse);
                 }
-                part += wm * (lse - lz);
-#pragma unroll
-                for (int c = 0; c < kMaxC; ++c)
-                    if (c < C) row[c] = wm * (expf(lg[c] - lse) - (c == zm ? 1.f : 0.f));
             } else {
-                float mx = -INFINITY, lz = 0.f;
-                for (int c = 0; c < C; ++c) {
-                    mx = fmaxf(mx, row[c]);
-                    if (c == zm) lz = row[c];
-                }
-                float se = 0.f;
-                for (int c = 0; c < C; ++c) se += expf(row[c] - mx);
-                const float lse = mx + logf(se);
-                if (a.outer == 1) {
-                    const int mg = m0 + m;
-                    a.nll_rows[(size_t)s * a.M + mg] = lse - lz;
-                    if (a.prob_rows && mg >= a.n_pseudo) {
-                        float* pr = a.prob_rows + ((size_t)s * (a.M - a.n_pseudo) + mg - a.n_pseudo) * C;
-                        for (int c = 0; c < C; ++c) pr[c] = expf(row[c] - lse);
-                    }
-                    continue;
-                }
                 part += wm * (lse - lz);
-                for (int c = 0; c < C; ++c)
-                    row[c] = wm * (expf(row[c] - lse) - (c == zm ? 1.f : 0.f));
+                for (int c = 0; c < C; ++c) row[c] = wm * (expf(row[c] - lse) - (c == zm ? 1.f : 0.f));
             }
         }
-        __syncthreads();
+        drain();
+        if (!bwd) continue;
+        // ---- backward propagation down to the lowest owned layer
+        for (int l = L - 1; l > own_lo; --l) {
+            const int din = a.din[l], dout = a.dout[l];
+            const float* G = gbuf(l) + r0 * gld(l);
+            const int ldx = a.ldx[l];
+            const float* X = sm + a.lx[l] + r0 * ldx;
+            float* Gn = gbuf(l - 1) + r0 * ldx;  // G_{l-1}: the stride of X_l
+            const int iend = min((din + 15) & ~15, ldx);
+            auto epi = [&](int m, int i, floatx4 v, int rot) {
+                if (i < iend) {
+                    const bool il = i < din;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = m + ((r + rot) & 3);
+                        Gn[row * ldx + i] = (il && X[row * ldx + i] > 0.f) ? v[r] : 0.f;
+                    }
+                }
+            };
+            if constexpr (FAM == PSVI_FAMILY_FULLCOV)
+                row_gemm<true, true>(din, dout, G, gld(l), sm + a.lwt[l], a.ldwt[l], epi);
+            else  // mean-field: K = dout is small (the classifier), W read down k
+                row_gemm<true, false>(din, dout, G, gld(l), sm + a.lw[l], a.ldw[l], epi);
+            drain();
+        }
+        if (dx0) {
+            // du[s][m][i] = sum_j G_0[m][j] W_0[j][i] for the tile's pseudopoint rows
+            const int din = a.din[0], dout = a.dout[0];
+            auto epi = [&](int m, int i, floatx4 v, int rot) {
+                if (i < din) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int mm = r0 + m + ((r + rot) & 3), mg = m0 + mm;
+                        if (mm < mcnt && mg < a.n_pseudo)
+                            a.du_part[((size_t)s * a.n_pseudo + mg) * din + i] = v[r];
+                    }
+                }
+            };
+            row_gemm<true, false>(din, dout, gbuf(0) + r0 * gld(0), gld(0), sm + a.lw[0], a.ldw[0], epi);
+        }
     }
-    NET_STAMP(3, __builtin_amdgcn_s_memtime());
+    __syncthreads();  // every tile's rows of X_l and G_l
+    NET_STAMP(2, __builtin_amdgcn_s_memtime());
 
-    // ---- 4. backward, l = L-1 .. 0: dW_l (if owned) and G_{l-1} (if a lower
-    // layer is owned), both from G_l (G_{L-1} = dlogits), their tiles in one
-    // round-robin
+    // ---- 3. weight gradients of the owned layers, dW_l = G_l^T X_l and the
+    // biases' column sums (sums over every row of the chunk), all layers' tiles
+    // in one round-robin over the waves
     float sink = 0.f;
     // gradient element o of layer l: W rows j*din + i, then the biases
     auto emit = [&](int l, int o, float v) {
@@ -648,22 +678,11 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     // outer backward: the sampled-KL path, d nkl_s / d x_s = -x_s / s0^2,
     // added once per sample (pseudopoint chunk 0)
     const float ckv = (a.outer == 2 && blockIdx.z == 0) ? a.ck[s] * a.inv_s0sq : 0.f;
-    int stamp = 4, cur = 0;  // cur: gradient buffer that receives G_{l-1}
-    for (int l = L - 1; l >= 0 && !(a.abl & 8) && a.outer != 1; --l) {
-        const bool own = l >= own_lo && l < own_hi;
-        const bool prop = l >= 1 && own_lo < l;
-        // outer backward: input gradient of the pseudopoint rows (d loss / d u)
-        const bool dx0 = l == 0 && a.outer == 2 && a.du_part != nullptr && own_lo == 0;
-        if (!own && !prop && !dx0) break;
-        const int din = a.din[l], dout = a.dout[l];
-        const float* G = l == L - 1 ? sm + a.ldl : sm + (cur ? a.lg[0] : a.lg[1]);
-        const int ldg = l == L - 1 ? a.lddl : a.ldx[l + 1];  // G_l: the stride of X_{l+1}
-        const float* X = sm + a.lx[l];
-        const int ldx = a.ldx[l];
-        float* Gn = sm + (cur ? a.lg[1] : a.lg[0]);  // G_{l-1}: row stride ldx (of X_l)
+    if (bwd) {
         int first = 0;
-        if (own) {
+        for (int l = own_hi - 1; l >= own_lo; --l) {
             // dW_l[j][i] = sum_m G_l[m][j] X_l[m][i]: both operands k(=m)-strided
+            const int din = a.din[l], dout = a.dout[l];
             const float* Wl = sm + a.lw[l];
             const int ldw = a.ldw[l];
             auto epi = [&](int j0, int i, floatx4 v, int rot) {
@@ -679,49 +698,21 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     }
                 }
             };
-            mfma_gemm<false, false>(dout, din, Mp, 0, G, ldg, X, ldx, epi);
-            first = gemm_units(dout, din);
+            mfma_gemm<false, false>(dout, din, Mp, first, gbuf(l), gld(l), sm + a.lx[l], a.ldx[l], epi);
+            first += gemm_units(dout, din);
         }
-        if (dx0) {
-            // du[s][m][i] = sum_j G_0[m][j] W_0[j][i] for the chunk's pseudopoint rows
-            auto epi = [&](int m0r, int i, floatx4 v, int rot) {
-                if (i < din) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int m = m0r + ((r + rot) & 3), mg = m0 + m;
-                        if (m < mcnt && mg < a.n_pseudo)
-                            a.du_part[((size_t)s * a.n_pseudo + mg) * din + i] = v[r];
-                    }
-                }
-            };
-            mfma_gemm<true, false>(Mp, din, dout, first, G, ldg, sm + a.lw[l], a.ldw[l], epi);
-        }
-        if (prop) {
-            // G_{l-1}[m][i] = (sum_j G_l[m][j] W_l[j][i]) * 1[X_l[m][i] > 0]
-            const int iend = min((din + 15) & ~15, ldx);
-            auto epi = [&](int m, int i, floatx4 v, int rot) {
-                if (i < iend) {
-                    const bool il = i < din;
-                    float h[4];  // the ReLU masks, read before any store (Gn may alias X)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) h[r] = X[(m + ((r + rot) & 3)) * ldx + i];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        Gn[(m + ((r + rot) & 3)) * ldx + i] = (il && h[r] > 0.f) ? v[r] : 0.f;
-                }
-            };
-            if constexpr (FAM == PSVI_FAMILY_FULLCOV)
-                mfma_gemm<true, true>(Mp, din, dout, first, G, ldg, sm + a.lwt[l], a.ldwt[l], epi);
-            else  // mean-field: K = dout is small (the classifier), W read down k
-                mfma_gemm<true, false>(Mp, din, dout, first, G, ldg, sm + a.lw[l], a.ldw[l], epi);
-        }
-        if (own) {
-            // bias gradient: column sums of G_l over the chunk.  Wave q takes
-            // columns 16 q .. 16 q + 15: lane (k4, i16) reads the float4 of
-            // columns 16 q + 4 k4 .. + 3 in rows i16, i16 + 16, ... (the GEMM's
-            // conflict-free ds_read_b128 pattern), then DPP row sums over i16.
-            const int lane = tid & 63, i16 = lane & 15, k4 = lane >> 4;
-            for (int q = wave_id(); 16 * q < dout; q += blockDim.x >> 6) {  // wave-uniform
+        // bias gradients: column sums of G_l over the chunk.  A wave takes
+        // columns 16 q .. 16 q + 15 of one layer: lane (k4, i16) reads the
+        // float4 of columns 16 q + 4 k4 .. + 3 in rows i16, i16 + 16, ... (the
+        // GEMM's conflict-free ds_read_b128 pattern), then DPP row sums over i16.
+        const int i16 = lane & 15, k4 = lane >> 4;
+        int qb = 0;
+        for (int l = own_hi - 1; l >= own_lo; --l) {
+            const int din = a.din[l], dout = a.dout[l];
+            const float* G = gbuf(l);
+            const int ldg = gld(l);
+            const int nq = (dout + 15) >> 4;
+            for (int q = ((wave_id() - first - qb) % nwv + nwv) % nwv; q < nq; q += nwv) {  // wave-uniform
                 const int j0 = 16 * q + 4 * k4;
                 float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
                 for (int m = i16; m < mcnt; m += 16) {
@@ -738,12 +729,10 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                     emit(l, dout * din + j, b);
                 }
             }
+            qb += nq;
         }
-        if (!prop) break;
-        __syncthreads();
-        NET_STAMP(min(stamp++, 8) + 2, __builtin_amdgcn_s_memtime());
-        cur ^= 1;
     }
+    NET_STAMP(3, __builtin_amdgcn_s_memtime());
     asm volatile("" ::"v"(sink));
     if (role == 0 && a.outer == 0) {  // the chunk's weighted NLL (role 1 computed the same)
         const float tot = block_sum(part, sm + a.lred);
@@ -813,17 +802,16 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     const int nbands = (p.family == PSVI_FAMILY_FULLCOV && p.world > 1) ? p.band_base[p.L] : 0;
     const int lsrc = take(2 * (size_t)nbands + 3 * kMaxWorld + kMaxL);
     const int ns_early = ns;
-    int ldgmax = 4;
     for (int l = 1; l < p.L; ++l) {
         const int ldx = ld8o(p.lay[l].din);
         const int lx = take((size_t)Mp * ldx);
-        ldgmax = std::max(ldgmax, ldx);
         if (a) { a->lx[l] = lx; a->ldx[l] = ldx; }
     }
-    int lg0 = 0, lg1 = 0;
-    if (p.L > 1) {
-        lg0 = take((size_t)Mp * ldgmax);
-        lg1 = take((size_t)Mp * ldgmax);
+    // G_l (l < L - 1, the gradient of layer l's output, stride of X_{l+1}):
+    // every one stays until the weight-gradient phase
+    for (int l = 0; l + 1 < p.L; ++l) {
+        const int lgl = take((size_t)Mp * ld8o(p.lay[l + 1].din));
+        if (a) a->lg[l] = lgl;
     }
     const int lddl = ld8o(p.lay[p.L - 1].dout);
     const int ldl = take((size_t)Mp * lddl);
@@ -839,7 +827,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     off = (off + 3) & ~size_t(3);
     if (a) {
         a->lx[0] = lx0; a->ldx[0] = ldx0;
-        a->lg[0] = lg0; a->lg[1] = lg1; a->ldl = ldl; a->lddl = lddl;
+        a->ldl = ldl; a->lddl = lddl;
         a->lred = lred; a->lsrc = lsrc; a->lzw = lzw; a->lstamp = lstamp;
         a->Mp = Mp;
         a->nslack = ns;

@@ -29,16 +29,9 @@ def report(name, t, abl, S):
         d = (r.double() - r[:, 0:1].double())
         print(f"{name} abl={abl} role {role}: {r.shape[0]} workgroups; s_memtime ticks, median per phase:")
         prev = torch.zeros(r.shape[0], dtype=torch.float64)
-        fw = [k for k in (9, 10, 11) if int((r[:, k] != 0).sum()) == r.shape[0]]
-        bw = [k for k in range(6, 9) if int((r[:, k] != 0).sum()) == r.shape[0]]
-        if int((r[:, 4] != 0).sum()) == r.shape[0]:
-            print(f"  (wave 0 in fwd layer 0: setup {float((d[:, 4] - d[:, 1]).median()):.0f}, "
-                  f"own GEMM {float((d[:, 5] - d[:, 4]).median()):.0f}, "
-                  f"barrier wait {float((d[:, 9] - d[:, 5]).median()):.0f})")
-        cols = [1] + fw + [2, 3] + bw + [12]
-        names = (["loads"] + [f"fwd layer {k - 9}" for k in fw] + ["fwd rest", "loss head"] +
-                 [f"bwd phase {k - 5}" for k in bw] + ["last bwd"])
-        for k, nm in zip(cols, names):
+        # phases (kernels_net.hip): 1 loads done, 2 row chain (forward, loss
+        # head, gradient propagation) done, 3 weight gradients done, 12 end
+        for k, nm in ((1, "loads"), (2, "row chain"), (3, "weight grads"), (12, "tail")):
             cur = d[:, k]
             print(f"  {nm:12s} {float((cur - prev).median()):10.0f}")
             prev = cur
