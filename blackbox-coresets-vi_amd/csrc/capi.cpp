@@ -19,6 +19,7 @@ namespace psvi {
 size_t net_plan_geometry(psvi_plan& p);  // kernels_net.hip
 void net_set_lds_limit();                // kernels_net.hip
 extern int g_net_ablation;               // kernels_net.hip
+extern int g_net_scalar_loads;           // kernels_net.hip
 extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
 extern int g_stream_off;                 // kernels_mvn.hip
@@ -527,6 +528,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
         case PSVI_DBG_KSTREAM_OFF: g_ks_off = value; return 0;
+        case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         case PSVI_DBG_LENET_GEMM_VALU: g_lenet_gemm_valu = value; return 0;

@@ -299,8 +299,9 @@ __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int nsrc, const int
 // instantiation has straight-line x loads: with the run-table path in the
 // same kernel the register allocator shares registers across the two paths
 // and the waitcnt pass then serialises the u and x loads (seen in the ISA).
-template <int FAM, bool MSRC>
+template <int FAM, bool MSRC, bool VEC = false>
 __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
+    static_assert(!VEC || (FAM == PSVI_FAMILY_FULLCOV && !MSRC), "float4 loads: one full-cov source");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
@@ -358,7 +359,106 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     float* zw = sm + a.lzw;  // the chunk's labels (as int bits) and weights
     float* X0 = sm + a.lx[0];
     const int ldx0 = a.ldx[0];
-    {
+    if constexpr (VEC) {
+        // one source, D % 4 == 0: the u chunk and the x row as float4 runs (a
+        // quarter of the load instructions), x's < 4 trailing elements by
+        // scalar loads at clamped indices; every load unconditional
+        constexpr int kU4 = 4, kX4 = 3;
+        // ext vectors (a HIP float4 array here went to scratch: SROA gives up
+        // on the struct type)
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const int nu4 = (mcnt * D) >> 2;
+        const float rdu = 1.f / (float)D;
+        const f4* usrc = reinterpret_cast<const f4*>(a.u + (int64_t)m0 * D);
+        const int nx = a.stage_len, nx4 = nx >> 2, nxt = nx & 3;
+        const float* xr = a.xrecv + (int64_t)s * a.src_stride[0];
+        const u4* xm4 = reinterpret_cast<const u4*>(a.xmap);
+        const int bd = blockDim.x;
+        for (int pass = 0; pass * kU4 * bd < nu4 || pass * kX4 * bd < nx4 || pass == 0; ++pass) {  // uniform
+            const int bu = pass * kU4 * bd + tid, bx = pass * kX4 * bd + tid;
+            f4 uv[kU4], xv[kX4];
+            u4 xm[kX4];
+            float xt = 0.f;
+            uint32_t xmt = 0xFFFFFFFFu;
+            int zi = 0;
+            float wv = 0.f;
+            if (!(a.abl & 1)) {
+#pragma unroll
+                for (int k = 0; k < kU4; ++k) uv[k] = usrc[max(min(bu + k * bd, nu4 - 1), 0)];
+#pragma unroll
+                for (int k = 0; k < kX4; ++k) {
+                    const int c = max(min(bx + k * bd, nx4 - 1), 0);
+                    xv[k] = *reinterpret_cast<const f4*>(xr + 4 * c);
+                    xm[k] = xm4[c];
+                }
+                const int rt = min(4 * nx4 + (tid & 3), nx - 1);
+                xt = xr[rt];
+                xmt = a.xmap[rt];
+                if (pass == 0) {
+                    const int mm = min(tid, mcnt - 1);
+                    zi = a.z[m0 + mm];
+                    wv = a.w[m0 + mm];
+                }
+            }
+            if (pass == 0) {
+                // zero padding while the loads are in flight (disjoint from every
+                // loaded element): W columns >= din and rows >= dout, W^T columns
+                // dout .. the 16-multiple, u columns >= D up to the 16-multiple, u
+                // rows past the chunk, the 64-float slacks after every region
+                for (int l = 0; l < L; ++l) {
+                    const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
+                    const int rows = (dout + 15) & ~15;
+                    if (l > 0) {
+                        float* WT = sm + a.lwt[l];
+                        for (int i = r16; i < din; i += nr16)
+                            if (dout + c16 < rows) WT[i * a.ldwt[l] + dout + c16] = 0.f;
+                    }
+                    float* W = sm + a.lw[l];
+                    for (int j = r16; j < dout; j += nr16)
+                        for (int c = din + c16; c < ldw; c += 16) W[j * ldw + c] = 0.f;
+                    for (int i = tid; i < (rows - dout) * ldw; i += bd) W[dout * ldw + i] = 0.f;
+                }
+                const int cend = min((D + 15) & ~15, ldx0);
+                for (int m = r16; m < mcnt; m += nr16)
+                    if (D + c16 < cend) X0[m * ldx0 + D + c16] = 0.f;
+                for (int i = tid; i < (Mp - mcnt) * ldx0; i += bd) X0[mcnt * ldx0 + i] = 0.f;
+                for (int k = wave_id(); k < a.nslack; k += bd >> 6)  // wave-uniform slot
+                    sm[a.slack[k] + (tid & 63)] = 0.f;
+            }
+            if (a.abl & 1) continue;
+#pragma unroll
+            for (int k = 0; k < kU4; ++k) {
+                const int c = bu + k * bd;
+                if (c < nu4) {
+                    const int idx = 4 * c;
+                    const int m = (int)(((float)idx + 0.5f) * rdu);  // exact for idx < 2^21
+                    *reinterpret_cast<f4*>(X0 + m * ldx0 + idx - m * D) = uv[k];
+                }
+            }
+            auto put = [&](float v, uint32_t mp) __attribute__((always_inline)) {
+                sm[mp & 0xFFFFu] = v;
+                if ((mp >> 16) != 0xFFFFu) sm[mp >> 16] = v;
+            };
+#pragma unroll
+            for (int k = 0; k < kX4; ++k)
+                if (bx + k * bd < nx4) {
+                    put(xv[k][0], xm[k][0]);
+                    put(xv[k][1], xm[k][1]);
+                    put(xv[k][2], xm[k][2]);
+                    put(xv[k][3], xm[k][3]);
+                }
+            if (pass == 0 && tid < nxt) put(xt, xmt);
+            if (pass == 0 && tid < mcnt) {
+                zw[tid] = __int_as_float(zi);
+                zw[Mp + tid] = wv;
+            }
+        }
+        for (int m = bd + tid; m < mcnt && !(a.abl & 1); m += bd) {  // chunks past one block
+            zw[m] = __int_as_float(a.z[m0 + m]);
+            zw[Mp + m] = a.w[m0 + m];
+        }
+    } else {
         // u chunk as a flat run of nu floats (one load path for every D: two
         // paths -- float4 rows and scalars -- are tail-merged by the compiler
         // into split loads serialised on s_waitcnt vmcnt, seen in the ISA)
@@ -923,6 +1023,7 @@ void net_xmap(const psvi_plan& p, std::vector<uint32_t>& xmap, std::vector<NetBa
 }
 
 int g_net_ablation = 0;  // psvi_debug_set(PSVI_DBG_NET_ABLATION, mask)
+int g_net_scalar_loads = 0;  // psvi_debug_set(PSVI_DBG_NET_SCALAR_LOADS, 1): the scalar load path (A/B)
 unsigned long long* g_net_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_NET_STAMPS, buf)
 
 void net_set_lds_limit() {
@@ -932,6 +1033,8 @@ void net_set_lds_limit() {
     (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
@@ -1001,6 +1104,8 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
     else if (p.world > 1)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true>), grid, block, p.net_lds, st, a);
+    else if (p.lay[0].din % 4 == 0 && !g_net_scalar_loads)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false, true>), grid, block, p.net_lds, st, a);
     else
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false>), grid, block, p.net_lds, st, a);
     if (a.gslot && a.outer != 1)

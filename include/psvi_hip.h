@@ -460,6 +460,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     clocks summed per phase (tools/rop_stamps.py) */
 #define PSVI_DBG_KSTREAM_OFF 19  /* value: 1 = the chunked update kernel instead of
                                     the K-split streaming one at S > 128 (A/B) */
+#define PSVI_DBG_NET_SCALAR_LOADS 20 /* value: 1 = the full-cov network kernel's
+                                    scalar x / u load path instead of the float4
+                                    one (A/B)                                   */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
