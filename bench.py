@@ -294,13 +294,6 @@ def _mf_init(layers, init_sd=1e-3):
 C4 = dict(S=1024, M=200)
 
 
-def draw_eps(t, seed, offset):
-    """The per-step noise of the sharded legs: the psvi_inner_loop Philox
-    stream (every rank draws the same global eps; it never crosses the wire)."""
-    from psvi.runtime import randn_
-    randn_(t, seed, offset)
-
-
 def make_sharded_loop(family, layers, S, M, rt):
     """This rank's ShardedInnerLoop (rows of L x samples for full-cov, samples
     for LeNet), collectives on rt.comm."""
@@ -315,54 +308,46 @@ def fn2_inputs(layers, M, dev, seed):
     return u.to(dev), z.to(dev), torch.full((M,), N_DATA / M, device=dev)
 
 
-def sharded_steps(rt, loop, u, z, w, eps, params, m, v, seed, k0, n, parts=None, ev=None):
-    """n sharded inner steps (Adam steps k0 + 1 ..): per step the eps draw, the
-    sample phase, the x all_to_all, the network, the G all_to_all and the
-    update -- the phases are the loop's own (ShardedInnerLoop.step's body),
-    split out so HIP events can bracket them.  ev: {step index: 4 events}."""
+def sharded_steps(rt, loop, u, z, w, params, m, v, seed, k0, n, parts=None, ev=None):
+    """n sharded inner steps (Adam steps k0 + 1 ..) -- ShardedInnerLoop.run:
+    full-cov x all_to_all, network, G all_to_all, the update fused with the
+    next step's sample, the next eps drawn on a side stream behind the
+    exchanges (LeNet: the samples' accumulator all-reduced per step).  The
+    draws are the psvi_inner_loop stream at offset k0 * eps_stride.  ev: {step:
+    4 events} around the exchanges + network and the update + sample."""
     stride = (loop.plan.eps_count + 3) // 4 * 4
-    for k in range(k0, k0 + n):
-        e = ev.get(k) if ev else None
-        draw_eps(eps, seed, k * stride)
-        if loop.family != "fullcov":
-            loop.step(u, z, w, eps, params, m, v, k + 1, LR)
-        else:
-            if e: e[0].record()
-            loop.phase_sample(eps, params)
-            if e: e[1].record()
-            loop.comm.all_to_all(loop.x_recv, loop.x_shard, loop.x_out, loop.x_in)
-            loop.phase_net(u, z, w)
-            loop.comm.all_to_all(loop.g_shard, loop.g_send, loop.g_out, loop.g_in)
-            if e: e[2].record()
-            loop.phase_update(eps, params, m, v, k + 1, LR, "higher")
-            if e: e[3].record()
-        if parts is not None:
-            parts[k].copy_(loop.parts)
+    loop.run(u, z, w, params, m, v, n, LR, step0=k0 + 1, seed=seed, offset=k0 * stride,
+             elbo_parts=None if parts is None else parts[k0:k0 + n], phase_events=ev)
 
 
-def sharded_headline(rt, steps, warmup, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M, ev_every=10):
+def sharded_headline(rt, steps, warmup, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M, ev_every=5):
     """The headline at N > 1: C3 shards weak-scaled (S = 128 N, M = 100), rows
-    of L x samples sharded, two all_to_alls per step.  Returns (elapsed s, the
-    (warmup + steps) x 2 [NLL, KL] parts of this rank, per-phase ms, loop)."""
+    of L (whole 64-row bands) x samples sharded, two all_to_alls per step.
+    Returns (elapsed s, the (warmup + steps) x 2 [NLL, KL] parts of this rank,
+    per-phase ms from a separate 50-step call after the timed one, loop)."""
     S = s_per_gpu * rt.world
     loop = make_sharded_loop("fullcov", layers, S, M, rt)
     u, z, w = fn2_inputs(layers, M, rt.dev, 0)
     params = reference_init_params(layers, rt.dev)
     m, v = torch.zeros_like(params), torch.zeros_like(params)
-    eps = torch.empty(loop.plan.eps_count, device=rt.dev)
     total = warmup + steps
     parts = torch.zeros(total, 2, dtype=torch.float64, device=rt.dev)
-    ev = {k: [rt.event() for _ in range(4)]
-          for k in range(warmup, total) if (k - warmup) % ev_every == 0}
-    sharded_steps(rt, loop, u, z, w, eps, params, m, v, 20251015, 0, warmup, parts)
-    elapsed = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, eps, params, m, v, 20251015,
-                                             warmup, steps, parts, ev))
-    ph = {"sample": [], "exchange+net": [], "update": []}
+    sharded_steps(rt, loop, u, z, w, params, m, v, 20251015, 0, warmup, parts)
+    elapsed = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, params, m, v, 20251015,
+                                             warmup, steps, parts))
+    # the per-phase split: HIP events between the launches of a separate call
+    # (outside the timed region), every ev_every-th of 50 steps
+    nph = 50
+    ev = {k: [rt.event() for _ in range(4)] for k in range(nph) if k % ev_every == 0}
+    pp, mm, vv = params.clone(), m.clone(), v.clone()
+    loop.run(u, z, w, pp, mm, vv, nph, LR, step0=total + 1, seed=20251016, phase_events=ev)
+    rt.sync()
+    ph = {"exchange+net": [], "update+sample": []}
     for e in ev.values():
-        ph["sample"].append(e[0].elapsed_time(e[1]))
-        ph["exchange+net"].append(e[1].elapsed_time(e[2]))
-        ph["update"].append(e[2].elapsed_time(e[3]))
+        ph["exchange+net"].append(e[0].elapsed_time(e[1]))
+        ph["update+sample"].append(e[1].elapsed_time(e[2]))
     avg_ms = {k: sum(x) / max(len(x), 1) for k, x in ph.items()}
+    avg_ms["samples"] = len(ev)
     return elapsed, parts, avg_ms, loop
 
 
@@ -388,10 +373,9 @@ def c4_timings(rt, steps=100, warmup=10, layers=LAYERS, S=C4["S"], M=C4["M"]):
         negelbo = elbo[-1:]
     else:
         loop = make_sharded_loop("fullcov", layers, S, M, rt)
-        eps = torch.empty(loop.plan.eps_count, device=dev)
         parts = torch.zeros(warmup + steps, 2, dtype=torch.float64, device=dev)
-        sharded_steps(rt, loop, u, z, w, eps, params, m, v, 11, 0, warmup, parts)
-        dt = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, eps, params, m, v, 11, warmup,
+        sharded_steps(rt, loop, u, z, w, params, m, v, 11, 0, warmup, parts)
+        dt = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, params, m, v, 11, warmup,
                                             steps, parts))
         negelbo = loop.reduce_elbo(parts[-1:])
     return {"config": f"C4 fn2 full-cov S={S} M={M}, {rt.world} GPU(s) (strong scaling)",
@@ -434,10 +418,9 @@ def lenet_timings(rt, cpu=True, T=10, S=256, M=500, second_order=True):
         finite = bool(torch.isfinite(elbo).all().item())
     else:
         loop = make_sharded_loop("lenet", LENET_LAYERS, S, M, rt)
-        eps = torch.empty(loop.plan.eps_count, device=dev)
         parts = torch.zeros(2 + T, 2, dtype=torch.float64, device=dev)
-        sharded_steps(rt, loop, ud, zd, wd, eps, params, m, v, 1, 0, 2, parts)
-        dt = rt.timed(lambda: sharded_steps(rt, loop, ud, zd, wd, eps, params, m, v, 2, 2, T,
+        sharded_steps(rt, loop, ud, zd, wd, params, m, v, 1, 0, 2, parts)
+        dt = rt.timed(lambda: sharded_steps(rt, loop, ud, zd, wd, params, m, v, 2, 2, T,
                                             parts))
         finite = bool(torch.isfinite(loop.reduce_elbo(parts[2:])).all().item())
     ms = dt / T * 1e3
@@ -654,8 +637,8 @@ def run(rt, args, shapes=None):
     finite = bool(torch.isfinite(elbo).all().item())
     steps_per_s = args.steps / elapsed
     value = steps_per_s * world   # S = 128 N: N C3 shards per step
-    upd_s = max(avg_ms["update"], 1e-9) * 1e-3
     if world == 1:
+        upd_s = max(avg_ms["update"], 1e-9) * 1e-3
         # dominant kernel: the update with the fused next-step sample (plus its
         # small slot-reduce kernel, inside the same event pair)
         wk = algorithmic_work_fused(S)
@@ -665,14 +648,15 @@ def run(rt, args, shapes=None):
                                tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
     else:
+        # dominant phase: the update (K-split streaming kernel at K = S) and
+        # the next step's sample on this rank's rows (mvn_fwd + its reduce)
         work = algorithmic_work(S, rows_fraction(loop, sh["layers"]), sh["layers"])
-        wk = work["update"]
-        kname = "mvn_update_kernel"
-        smp_s = max(avg_ms["sample"], 1e-9) * 1e-3
-        kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
-                               tflops=wk["flops"] / upd_s / 1e12),
-                   "mvn_fwd_kernel+reduce": dict(avg_us=avg_ms["sample"] * 1e3,
-                                                 tflops=work["sample"]["flops"] / smp_s / 1e12),
+        wk = dict(bytes=work["update"]["bytes"] + work["sample"]["bytes"],
+                  flops=work["update"]["flops"] + work["sample"]["flops"])
+        upd_s = max(avg_ms["update+sample"], 1e-9) * 1e-3
+        kname = "mvn_kstream_kernel + mvn_fwd_kernel + reduce (update + next-step sample)"
+        kernels = {kname: dict(avg_us=avg_ms["update+sample"] * 1e3,
+                               gbs=wk["bytes"] / upd_s / 1e9, tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel(+exchange)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
     hbm_s, mfma_s = wk["bytes"] / (HBM_PEAK_GBS * 1e9), wk["flops"] / (FP32_MFMA_PEAK_TFLOPS * 1e12)
     if hbm_s >= mfma_s:
@@ -682,12 +666,13 @@ def run(rt, args, shapes=None):
         roofline = dict(bound="mfma", achieved=round(wk["flops"] / upd_s / 1e12, 2),
                         peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s")
     roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
-                    traffic=pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"]
-                                        if world == 1 else ["mvn_update_kernel"]),
+                    traffic=pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"])
+                    if world == 1 else None,
                     traffic_source=dict(PMC_TRAFFIC, measured_in_this_run=False,
                                         method="rocprofv3 --pmc FETCH_SIZE, then --pmc "
                                                "WRITE_SIZE (separate passes) over this bench; "
-                                               "FETCH_SIZE x2 (gfx950 correction)"),
+                                               "FETCH_SIZE x2 (gfx950 correction)")
+                    if world == 1 else None,
                     timing_samples=avg_ms.get("samples"),
                     kernel=kname, algorithmic_bytes_per_launch=int(wk["bytes"]),
                     algorithmic_flops_per_launch=int(wk["flops"]),

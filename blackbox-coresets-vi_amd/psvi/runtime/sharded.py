@@ -5,8 +5,10 @@ independent jobs, psvi/experiments/flow-psvi-parallel.py:457-463).  Here one
 inner step is split across ranks where the math allows it:
 
   full-cov (fn2):  rows of every layer's L (and the matching mean/sd/corr
-      slices + Adam state) are sharded nnz-balanced; MC samples are sharded in
-      contiguous blocks.  Per step:
+      slices + Adam state) are sharded as whole 64-row bands balanced by their
+      64 x 64 tile counts; MC samples are sharded in contiguous blocks.  Per
+      step (ShardedInnerLoop.run fuses the update with the next step's sample
+      and draws the next eps on a side stream behind the exchanges):
         sample  x_shard[S][rows_r] = mean + L eps     (own rows, ALL samples)
         all_to_all  -> x_recv: own samples, all rows   (blocked by source rank)
         net     g_send = per-sample gradients          (own samples)
@@ -144,6 +146,16 @@ class ShardedInnerLoop:
         self.plan.mvn_update(eps, self.g_shard, params, m, v, step=step, lr=lr, kind=kind,
                              kl_out=self.parts[1:2], grad_out=grad_out)
 
+    def phase_update_sample(self, eps, params, m, v, step, lr, kind, eps_next):
+        """The update fused with the next step's sample into x_shard
+        (psvi_mvn_phase_update_sample)."""
+        self.plan.mvn_update(eps, self.g_shard, params, m, v, step=step, lr=lr, kind=kind,
+                             kl_out=self.parts[1:2], eps_next=eps_next, x_next=self.x_shard)
+
+    def draw(self, out, seed, offset):
+        """eps of the global layout from the Philox stream (psvi_randn)."""
+        randn_(out, seed, offset)
+
     # ---------------------------------------------------------------- step
     def step(self, u, z, w, eps, params, m, v, step, lr, kind="higher", elbo_parts=None):
         """One inner step on this rank.  elbo_parts (2 doubles, optional)
@@ -166,6 +178,74 @@ class ShardedInnerLoop:
                                 kl_out=self.parts[1:2] if self.rank == 0 else None)
             if elbo_parts is not None:
                 elbo_parts.copy_(self.parts)
+
+    def run(self, u, z, w, params, m, v, T, lr, kind="higher", step0=1, seed=0, offset=0,
+            elbo_parts=None, phase_events=None):
+        """T chained inner steps on this rank with in-library Philox draws
+        (psvi_inner_loop's stream: step t at offset + t * eps_stride of the
+        global layout, identical on every rank, so eps never crosses the wire).
+
+        Full-cov schedule per step t (x_shard holds x_t on entry):
+          side stream:  eps_{t+1} <- Philox, behind the exchanges and the network
+          x all_to_all -> network -> G all_to_all
+          update of t fused with the next step's sample: Adam on the rank's rows
+            (K-split streaming kernel at K = S > 128), then x_{t+1} = mean' +
+            L' eps_{t+1} on those rows (psvi_mvn_phase_update_sample)
+        The first step's x_0 is sampled before the loop; the last step
+        samples nothing.  elbo_parts (T, 2) float64 receives this rank's [NLL,
+        KL] per step (reduce_elbo sums them).  phase_events: optional {t:
+        [4 events]} recorded around the exchanges + network, the update and
+        the sample (diagnostics; they sit between launches)."""
+        T = int(T)
+        if T <= 0:
+            return
+        dev = params.device
+        stride = self.plan.eps_stride
+        if self.family != "fullcov":
+            e = torch.empty(self.plan.eps_count, device=dev)
+            for t in range(T):
+                self.draw(e, seed, offset + t * stride)
+                self.step(u, z, w, e, params, m, v, step0 + t, lr, kind=kind,
+                          elbo_parts=None if elbo_parts is None else elbo_parts[t])
+            return
+        if getattr(self, "_eps2", None) is None or self._eps2[0].device != dev:
+            self._eps2 = [torch.empty(self.plan.eps_count, device=dev) for _ in range(2)]
+        e_cur, e_nxt = self._eps2
+        cuda = e_cur.is_cuda
+        main = torch.cuda.current_stream(dev) if cuda else None
+        side = torch.cuda.Stream(dev) if cuda else None
+        self.draw(e_cur, seed, offset)
+        self.phase_sample(e_cur, params)
+        for t in range(T):
+            ev = phase_events.get(t) if phase_events else None
+            last = t + 1 == T
+            if not last:
+                if cuda:
+                    # e_nxt was read by the previous update (issued on main)
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        self.draw(e_nxt, seed, offset + (t + 1) * stride)
+                    drawn = torch.cuda.Event()
+                    drawn.record(side)
+                else:
+                    self.draw(e_nxt, seed, offset + (t + 1) * stride)
+            if ev: ev[0].record()
+            self.comm.all_to_all(self.x_recv, self.x_shard, self.x_out, self.x_in)
+            self.phase_net(u, z, w)
+            self.comm.all_to_all(self.g_shard, self.g_send, self.g_out, self.g_in)
+            if ev: ev[1].record()
+            if last:
+                self.phase_update(e_cur, params, m, v, step0 + t, lr, kind)
+            else:
+                if cuda:
+                    main.wait_event(drawn)
+                self.phase_update_sample(e_cur, params, m, v, step0 + t, lr, kind, e_nxt)
+            if ev: ev[2].record()
+            if elbo_parts is not None:
+                elbo_parts[t].copy_(self.parts)
+            e_cur, e_nxt = e_nxt, e_cur
+            if ev: ev[3].record()
+        self._eps2 = [e_cur, e_nxt]
 
     def reduce_elbo(self, elbo_parts):
         """elbo_parts (T, 2) stacked per step -> negative ELBO per step (all ranks)."""

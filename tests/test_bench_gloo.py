@@ -52,6 +52,7 @@ def _rank_main(rank, world, port, out):
             _emulate_fullcov(loop, O, layers, S, 1.0)
         else:
             _emulate_lenet(loop, O, S)
+        loop.draw = _fake_draw
         return loop
 
     bench.make_sharded_loop = make_loop
@@ -75,9 +76,8 @@ def _rank_main(rank, world, port, out):
         params += 0.05 * torch.randn(params.shape, generator=g)  # off the zero init
         p0 = params.clone()
         m, v = torch.zeros_like(params), torch.zeros_like(params)
-        eps = torch.empty(loop.plan.eps_count)
         parts = torch.zeros(3, 2, dtype=torch.float64)
-        bench.sharded_steps(rt, loop, u, z, w, eps, params, m, v, 77, 0, 3, parts)
+        bench.sharded_steps(rt, loop, u, z, w, params, m, v, 77, 0, 3, parts)
         negelbo = loop.reduce_elbo(parts)
         loop.gather_params(params, m, v)
         out.put((rank, line, p0.numpy(), params.numpy(), m.numpy(), v.numpy(),
@@ -108,7 +108,8 @@ def test_bench_multi_rank_control_flow(world):
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert line["config"]["comm"].startswith("gloo")
     ks = line["roofline"]["kernels"]
-    assert set(ks) == {"mvn_update_kernel", "mvn_fwd_kernel+reduce", "net_kernel(+exchange)"}
+    assert set(ks) == {"mvn_kstream_kernel + mvn_fwd_kernel + reduce (update + next-step sample)",
+                       "net_kernel(+exchange)"}
     assert all(d["avg_us"] > 0 for d in ks.values())   # the sampled per-phase events
     c4 = line["c4"]
     assert c4 is not None and c4["inner_steps_per_s"] > 0 and c4["elbo_finite"]

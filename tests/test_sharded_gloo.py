@@ -113,7 +113,12 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
             t.copy_(torch.from_numpy(cur).to(t.dtype))
         loop.parts[1] = kl
 
+    def phase_update_sample(eps, params, m, v, step, lr, kind, eps_next):
+        phase_update(eps, params, m, v, step, lr, kind)
+        phase_sample(eps_next, params)
+
     loop.phase_sample, loop.phase_net, loop.phase_update = phase_sample, phase_net, phase_update
+    loop.phase_update_sample = phase_update_sample
 
 
 def _rank_main(rank, world, port, name, kind_override, out):
