@@ -2,7 +2,7 @@
 """Per-phase shader-clock breakdown of the network kernel (s_memtime stamps,
 diagnostics API), optionally under ablation masks.
 
-  python tools/net_stamps.py [c3|c4] [abl,abl,...]
+  python tools/net_stamps.py [c3|c4] [abl,abl,...] [world rank]
 """
 import ctypes
 import os
@@ -57,17 +57,24 @@ def timeline(t, c0, c1):
 
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c3"
-    abls = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
+    abls = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 and sys.argv[2] else [0]
+    # optional: world rank -- the network phase of one rank of a row-sharded
+    # plan (x_recv from every source rank, gradients through the band table)
+    world = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    rank = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     layers, S, M = CFG[name]
-    plan = InnerLoopPlan("fullcov", layers, S, M)
+    if world > 1 and name == "c3":
+        S = 128 * world
+    plan = InnerLoopPlan("fullcov", layers, S, M, world=world, rank=rank)
     dev = "cuda"
     g = torch.Generator().manual_seed(0)
     u = torch.randn(M, 64, generator=g).to(dev)
     z = torch.randint(0, 2, (M,), generator=g).to(torch.int32).to(dev)
     w = torch.full((M,), 8.0, device=dev)
-    xs = torch.randn(plan.xshard_count, generator=g).to(dev) * 0.1
-    gs = torch.zeros(plan.xshard_count, device=dev)
+    xs = torch.randn(plan.xrecv_count, generator=g).to(dev) * 0.1
+    gs = torch.zeros(plan.xrecv_count, device=dev)
     nll = torch.zeros(1, dtype=torch.float64, device=dev)
+    S = plan.s_local
     nblk = S * 8
     st = torch.zeros(nblk * 16, dtype=torch.int64, device=dev)
     for abl in abls:
