@@ -383,6 +383,30 @@ def c4_timings(rt, steps=100, warmup=10, layers=LAYERS, S=C4["S"], M=C4["M"]):
             "elbo_finite": bool(torch.isfinite(negelbo).all().item())}
 
 
+def dp_timings(rt, steps=20, warmup=3, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M):
+    """The data-parallel alternative to the headline's row-sharded step
+    (N > 1 only; SURVEY.md §8(e) frames the choice): every rank holds all of
+    L, runs its S/N samples' inner objective and gradient on a world-1 plan
+    (psvi_elbo_grad), ONE all-reduce of the 4.73 M-float gradient (18.9 MB)
+    and the ELBO, then the same Adam step on every replica
+    (SampleShardedPlan.inner_loop).  Same weak-scaled shape as the headline."""
+    from psvi.runtime.sharded import SampleShardedPlan
+
+    S = s_per_gpu * rt.world
+    plan = SampleShardedPlan("fullcov", layers, S, M, rt.world, rt.rank, rt.comm)
+    u, z, w = fn2_inputs(layers, M, rt.dev, 0)
+    params = reference_init_params(layers, rt.dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    ws = plan.workspace(rt.dev)
+    plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=3, ws=ws)
+    dt = rt.timed(lambda: plan.inner_loop(u, z, w, params, m, v, steps, LR, step0=warmup + 1,
+                                          seed=3, offset=warmup * plan.eps_stride, ws=ws))
+    return {"config": f"C3 shards x {rt.world} (S={S}, M={M}): data parallel, one all-reduce "
+                      f"of the {plan.param_count}-float gradient per step",
+            "inner_steps_per_s": round(steps / dt, 2), "value": round(steps / dt * rt.world, 2),
+            "ms_per_step": round(dt / steps * 1e3, 4)}
+
+
 def lenet_timings(rt, cpu=True, T=10, S=256, M=500, second_order=True):
     """Auxiliary line for BASELINE.json configs[4] (C5, make_lenet, S = 256,
     M = 500 MNIST-shaped synthetic pseudopoints, N = 60000; strong scaling:
@@ -687,6 +711,10 @@ def run(rt, args, shapes=None):
                          algorithmic_gflop_per_gpu=2.682, floor_us=round(step_floor_us, 2),
                          frac=round(step_floor_us / (elapsed / args.steps * 1e6), 4))
     log(f"headline: {steps_per_s:.1f} steps/s")
+    dp = None
+    if world > 1 and not args.no_dp:
+        log("data-parallel alternative")
+        dp = dp_timings(rt, **sh.get("dp", {}))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline")
@@ -730,6 +758,7 @@ def run(rt, args, shapes=None):
         "step_roofline": step_roofline,
         "cpu_baseline": cpu,
         ("c4_1gpu" if world == 1 else "c4"): c4,
+        "dp_alternative": dp,
         "c2": c2,
         "trainers": trainers,
         "lenet_c5": lenet,
@@ -749,6 +778,9 @@ def main():
                     help="skip the auxiliary outer-step (trainer) timings")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the auxiliary C4 (S=1024, M=200) strong-scaling line")
+    ap.add_argument("--no-dp", action="store_true",
+                    help="skip the N > 1 data-parallel alternative line (one all-reduce of "
+                         "the full gradient per step)")
     ap.add_argument("--no-c2", action="store_true",
                     help="skip the auxiliary C2 (fn, S=32, M=50) line")
     ap.add_argument("--comm", choices=("rccl", "gloo"), default="rccl",

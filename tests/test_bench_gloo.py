@@ -62,7 +62,8 @@ def _rank_main(rank, world, port, out):
     try:
         rt = bench.Runtime(torch.device("cpu"), world, rank, HostStagedComm())
         args = argparse.Namespace(steps=3, warmup=1, no_c4=False, no_cpu_baseline=True,
-                                  no_c2=True, no_trainers=True, no_lenet=False, cpu_budget=1.0)
+                                  no_c2=True, no_trainers=True, no_lenet=False, cpu_budget=1.0,
+                                  no_dp=True)
         shapes = dict(layers=FN2, s_per_gpu=4, M=5,
                       c4=dict(layers=FN2, S=7, M=6, steps=2, warmup=1),
                       c5=dict(S=world + 1, M=3, T=2, second_order=False))

@@ -48,3 +48,5 @@ def test_bench_multi_rank_on_one_gpu(world):
     c5 = out["lenet_c5"]
     assert c5["elbo_finite"] and c5["gpu_inner_steps_per_s"] > 0
     assert c5["gpu_hvp_ms"] > 0 and c5["hyper_step_loss_finite"]
+    dp = out["dp_alternative"]   # the data-parallel alternative to the row-sharded step
+    assert dp is not None and dp["inner_steps_per_s"] > 0 and dp["value"] > 0
