@@ -102,6 +102,7 @@ struct NetArgs {
     int64_t src_base[kMaxWorld];
     int src_stride[kMaxWorld];
     int xcol0[kMaxL];         // one source: x / g column of layer l's row 0
+    int src_chunk0[kMaxWorld + 1];  // several sources, float4 loads: first chunk of each source block
     // FULLCOV: LDS destination of x row position r (stage order: source blocks
     // back to back, each in its x-shard column order): W_l / b_l float offset
     // in the low 16 bits, W_l^T offset (0xFFFF: none) in the high 16
@@ -301,7 +302,7 @@ __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int nsrc, const int
 // and the waitcnt pass then serialises the u and x loads (seen in the ISA).
 template <int FAM, bool MSRC, bool VEC = false>
 __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
-    static_assert(!VEC || (FAM == PSVI_FAMILY_FULLCOV && !MSRC), "float4 loads: one full-cov source");
+    static_assert(!VEC || FAM == PSVI_FAMILY_FULLCOV, "float4 loads: the full-cov x row");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
@@ -345,6 +346,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             }
         for (int l = 0; l < L; ++l)
             if (tid == 0) bb[l] = a.bbase[l];
+        if constexpr (VEC) {
+            int* cs = bb + kMaxL;
+            int* rq = cs + kMaxWorld + 1;
+            for (int p = 0; p <= nsrc; ++p)
+                if (tid == 0) {
+                    cs[p] = a.src_chunk0[p];
+                    if (p < nsrc) rq[p] = a.src_stride[p];
+                }
+        }
         __syncthreads();
     }
     // Every global load of the phase is issued before its first LDS store:
@@ -371,10 +381,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         const int nu4 = (mcnt * D) >> 2;
         const float rdu = 1.f / (float)D;
         const f4* usrc = reinterpret_cast<const f4*>(a.u + (int64_t)m0 * D);
-        const int nx = a.stage_len, nx4 = nx >> 2, nxt = nx & 3;
+        const int nx = a.stage_len, nxt = MSRC ? 0 : nx & 3;
+        // float4 chunks of the x row: one source -- the row's whole float4s;
+        // several -- every source block's ceil(rows / 4) chunks (the last one
+        // loaded at rows - 4 and shifted), chunk prefix per source in LDS
+        const int nx4 = MSRC ? a.src_chunk0[a.nsrc] : nx >> 2;
         const float* xr = a.xrecv + (int64_t)s * a.src_stride[0];
         const u4* xm4 = reinterpret_cast<const u4*>(a.xmap);
         const int bd = blockDim.x;
+        int xsh[kX4];  // MSRC: this lane's shift of each chunk (0: all four valid)
         for (int pass = 0; pass * kU4 * bd < nu4 || pass * kX4 * bd < nx4 || pass == 0; ++pass) {  // uniform
             const int bu = pass * kU4 * bd + tid, bx = pass * kX4 * bd + tid;
             f4 uv[kU4], xv[kX4];
@@ -386,15 +401,33 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             if (!(a.abl & 1)) {
 #pragma unroll
                 for (int k = 0; k < kU4; ++k) uv[k] = usrc[max(min(bu + k * bd, nu4 - 1), 0)];
+                if constexpr (!MSRC) {
 #pragma unroll
-                for (int k = 0; k < kX4; ++k) {
-                    const int c = max(min(bx + k * bd, nx4 - 1), 0);
-                    xv[k] = *reinterpret_cast<const f4*>(xr + 4 * c);
-                    xm[k] = xm4[c];
+                    for (int k = 0; k < kX4; ++k) {
+                        const int c = max(min(bx + k * bd, nx4 - 1), 0);
+                        xv[k] = *reinterpret_cast<const f4*>(xr + 4 * c);
+                        xm[k] = xm4[c];
+                    }
+                    const int rt = min(4 * nx4 + (tid & 3), nx - 1);
+                    xt = xr[rt];
+                    xmt = a.xmap[rt];
+                } else {
+                    const int64_t* xb = reinterpret_cast<const int64_t*>(srct) + a.nbands;
+                    const int* xs0 = srct + 2 * a.nbands + 2 * kMaxWorld;
+                    const int* cs = xs0 + kMaxWorld + kMaxL;  // [nsrc + 1] chunk prefix
+                    const int* rq = cs + kMaxWorld + 1;       // [nsrc] rows per source
+#pragma unroll
+                    for (int k = 0; k < kX4; ++k) {
+                        const int c = max(min(bx + k * bd, nx4 - 1), 0);
+                        int q = 0;
+                        while (q + 1 < nsrc && c >= cs[q + 1]) ++q;
+                        const int off = 4 * (c - cs[q]), st = min(off, rq[q] - 4);
+                        xsh[k] = off - st;
+                        const int pos = xs0[q] + st;  // stage position of the loaded float4
+                        xv[k] = *reinterpret_cast<const f4*>(a.xrecv + xb[q] + pos);
+                        xm[k] = *reinterpret_cast<const u4*>(a.xmap + pos);
+                    }
                 }
-                const int rt = min(4 * nx4 + (tid & 3), nx - 1);
-                xt = xr[rt];
-                xmt = a.xmap[rt];
                 if (pass == 0) {
                     const int mm = min(tid, mcnt - 1);
                     zi = a.z[m0 + mm];
@@ -443,10 +476,19 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
 #pragma unroll
             for (int k = 0; k < kX4; ++k)
                 if (bx + k * bd < nx4) {
-                    put(xv[k][0], xm[k][0]);
-                    put(xv[k][1], xm[k][1]);
-                    put(xv[k][2], xm[k][2]);
-                    put(xv[k][3], xm[k][3]);
+                    if (MSRC && xsh[k]) {
+                        // a source's last chunk: the float4 was loaded d = xsh
+                        // elements early; its components d .. 3 are the chunk's
+                        const int d = xsh[k];
+                        put(xv[k][3], xm[k][3]);
+                        if (d <= 2) put(xv[k][2], xm[k][2]);
+                        if (d <= 1) put(xv[k][1], xm[k][1]);
+                    } else {
+                        put(xv[k][0], xm[k][0]);
+                        put(xv[k][1], xm[k][1]);
+                        put(xv[k][2], xm[k][2]);
+                        put(xv[k][3], xm[k][3]);
+                    }
                 }
             if (pass == 0 && tid < nxt) put(xt, xmt);
             if (pass == 0 && tid < mcnt) {
@@ -900,7 +942,7 @@ static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
     // (8-byte aligned), the x row's per-source int64 bases and int starts,
     // the layers' first band index
     const int nbands = (p.family == PSVI_FAMILY_FULLCOV && p.world > 1) ? p.band_base[p.L] : 0;
-    const int lsrc = take(2 * (size_t)nbands + 3 * kMaxWorld + kMaxL);
+    const int lsrc = take(2 * (size_t)nbands + 3 * kMaxWorld + kMaxL + 2 * kMaxWorld + 1);
     const int ns_early = ns;
     for (int l = 1; l < p.L; ++l) {
         const int ldx = ld8o(p.lay[l].din);
@@ -1036,6 +1078,18 @@ void net_set_lds_limit() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+// float4 loads of the full-cov x row: u rows of D % 4 == 0 floats, and every
+// source block empty or at least one float4 wide (a block's last chunk is
+// loaded at its rows - 4)
+static bool net_vec_ok(const psvi_plan& p) {
+    if (p.lay[0].din % 4 || g_net_scalar_loads) return false;
+    for (int q = 0; q < p.world; ++q)
+        if (p.rows_tot[q] > 0 && p.rows_tot[q] < 4) return false;
+    return true;
 }
 
 hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
@@ -1092,6 +1146,12 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
             a.xcol0[l] = p.xcol_l[0][l];
             a.bbase[l] = p.band_base[l];
         }
+        int c0 = 0;
+        for (int q = 0; q < p.world; ++q) {
+            a.src_chunk0[q] = c0;
+            c0 += (p.rows_tot[q] + 3) / 4;
+        }
+        a.src_chunk0[p.world] = c0;
         a.xmap = p.d_net_xmap;
         a.bands = p.d_net_bands;
         a.nbands = p.world > 1 ? p.band_base[p.L] : 0;
@@ -1102,9 +1162,11 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     if (p.s_cnt[p.rank] == 0) return hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
+    else if (p.world > 1 && net_vec_ok(p))
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true, true>), grid, block, p.net_lds, st, a);
     else if (p.world > 1)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true>), grid, block, p.net_lds, st, a);
-    else if (p.lay[0].din % 4 == 0 && !g_net_scalar_loads)
+    else if (net_vec_ok(p))
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false, true>), grid, block, p.net_lds, st, a);
     else
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false>), grid, block, p.net_lds, st, a);
