@@ -995,9 +995,15 @@ static size_t tiled_floats(const psvi_plan* p) {
     return tiled_ok(p) ? 3 * (size_t)p->tiles_total * 4096 : 0;
 }
 
+// psvi_inner_loop workspace: the step workspace (x, g, a 256-byte tail), two
+// eps buffers each followed by 64 floats of zeros (the streaming update's
+// loads past a layer's last column block land there, unclamped), the tiled
+// state
+static size_t loop_ebuf_bytes(const psvi_plan* p) {
+    return align256(sizeof(float) * ((size_t)eps_stride(p) + 64));
+}
 static size_t loop_ws_bytes(const psvi_plan* p) {
-    return align256(p->ws_bytes) + 2 * align256(sizeof(float) * (size_t)eps_stride(p)) +
-           align256(sizeof(float) * tiled_floats(p));
+    return align256(p->ws_bytes) + 2 * loop_ebuf_bytes(p) + align256(sizeof(float) * tiled_floats(p));
 }
 
 int psvi_mvn_tiled_convert(const psvi_plan* p, float* params, float* adam_m, float* adam_v,
@@ -1044,7 +1050,7 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     char* wsb = (char*)ws;
     const int64_t es = eps_stride(p);
     float* ebuf[2] = {(float*)(wsb + align256(p->ws_bytes)),
-                      (float*)(wsb + align256(p->ws_bytes) + align256(sizeof(float) * (size_t)es))};
+                      (float*)(wsb + align256(p->ws_bytes) + loop_ebuf_bytes(p))};
     // eps of step t: the caller's [T][EPS_COUNT] array, or Philox (seed, offset + t * stride)
     auto eps_t = [&](int t) -> const float* {
         if (eps) return eps + (size_t)t * p->Peps;
@@ -1091,9 +1097,14 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     float* x = (float*)wsb;
     float* g = (float*)(wsb + align256(xs));
     // corr / m / v live in the tiled layout for the whole loop when the plan allows
-    float* ts = tiled_ok(p) ? (float*)(wsb + align256(p->ws_bytes) +
-                                       2 * align256(sizeof(float) * (size_t)es))
+    float* ts = tiled_ok(p) ? (float*)(wsb + align256(p->ws_bytes) + 2 * loop_ebuf_bytes(p))
                             : nullptr;
+    // Philox mode: eps, eps' and G are the loop's own buffers -- their 64-float
+    // pads are zeroed with the tiled conversion and the streaming update reads
+    // them unclamped
+    const bool padded = ts && !eps;
+    float* pads[3] = {padded ? ebuf[0] + p->Peps : nullptr, padded ? ebuf[1] + p->Peps : nullptr,
+                      padded ? g + (size_t)p->d.S * p->rows_tot[0] : nullptr};
     if (T == 0) return 0;
     // packed -> tiled state on the plan's conversion stream, behind x_0 and the
     // first network step (joined before the first update)
@@ -1101,11 +1112,11 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     if (ts && p->aux_st) {
         HIP_TRY(hipEventRecord(p->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(p->aux_st, p->ev_fork, 0));
-        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, p->aux_st));
+        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, p->aux_st, pads));
         HIP_TRY(hipEventRecord(p->ev_join, p->aux_st));
         join = true;
     } else if (ts) {
-        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st));
+        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st, pads));
     }
     const float* e = eps_t(0);
     if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
@@ -1129,7 +1140,7 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         }
         // the last step (no next sample) writes corr / m / v back to the packed arrays
         HIP_TRY(launch_mvn_update(*p, e, g, params, adam_m, adam_v, &h, elbo_out + t, nullptr, 1,
-                                  en, en ? x : nullptr, st, ts, ts && !en));
+                                  en, en ? x : nullptr, st, ts, ts && !en, nullptr, padded));
         if (tm) HIP_TRY(loop_event(1, st));
         e = en;
     }

@@ -1287,13 +1287,38 @@ __device__ __forceinline__ float adam_fast_k(const AdamC& a, float p, float g, f
 
 constexpr int kStrBuf = 128 * 16;  // float4 per eps block buffer ([128 samples][16 slots])
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // plain vector loads / stores (no memcpy)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// adam_fast_k on two entries at once: the arithmetic as v_pk_mul_f32 /
+// v_pk_fma_f32 / v_pk_add_f32 (two fp32 lanes per instruction on gfx950),
+// the square root and reciprocal per entry
+template <int KIND>
+__device__ __forceinline__ f32x2 adam_fast_k2(const AdamC& a, f32x2 p, f32x2 g, f32x2& m, f32x2& v) {
+    const f32x2 b1 = {a.b1, a.b1}, omb1 = {a.omb1, a.omb1}, b2 = {a.b2, a.b2}, omb2 = {a.omb2, a.omb2};
+    m = __builtin_elementwise_fma(b1, m, omb1 * g);
+    f32x2 d;
+    if (KIND == PSVI_ADAM_HIGHER || KIND == PSVI_ADAM_TORCH) {
+        v = __builtin_elementwise_fma(b2, v, (omb2 * g) * g);
+        const f32x2 vv = KIND == PSVI_ADAM_HIGHER ? v + f32x2{1e-8f, 1e-8f} : v;
+        const f32x2 sq = {__builtin_amdgcn_sqrtf(vv[0]), __builtin_amdgcn_sqrtf(vv[1])};
+        d = __builtin_elementwise_fma(sq, f32x2{a.inv_sqrt_bc2, a.inv_sqrt_bc2}, f32x2{a.eps, a.eps});
+        const f32x2 r = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+        return p - (f32x2{a.lr_bc1, a.lr_bc1} * m) * r;
+    } else {
+        v = __builtin_elementwise_fma(b2, v, (omb2 * g) * g) + f32x2{1e-12f, 1e-12f};
+        const f32x2 vb = v * f32x2{a.inv_bc2, a.inv_bc2};
+        d = f32x2{__builtin_amdgcn_sqrtf(vb[0]), __builtin_amdgcn_sqrtf(vb[1])} + f32x2{a.eps, a.eps};
+        const f32x2 r = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+        return p - f32x2{a.lr, a.lr} * (m * f32x2{a.inv_bc1, a.inv_bc1}) * r;
+    }
+}
 
 // NS = S / 32; KIND: Adam variant; DIAG: the diagnostics build (phase stamps);
 // SC1: corr / m / v stores write-through with sc1, which drops the lines from
 // the XCD's L2 (MI355X_MICROARCH.md, store flavours): the 60 MB of state written
 // per launch then no longer evicts the eps / eps' blocks and G slices that
 // later tiles re-read from L2 (false: plain stores, A/B)
-template <int NS, int KIND, bool DIAG = false, bool SC1 = true>
+template <int NS, int KIND, bool DIAG = false, bool SC1 = true, bool PAD = false>
 __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     constexpr int KT = 16 * NS;  // K steps of the dL GEMM (2 samples each)
     // [0, 4 kStrBuf): eps / eps' blocks, two buffers; then the band's G slice [128][64]
@@ -1316,14 +1341,19 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
             tlast = tt;
         }
     };
-    const int e_hi = (int)a.e_total - 4, g_hi = (int)a.g_total - 4;
+    // PAD (psvi_inner_loop's own eps / G buffers, each followed by 64 zeroed
+    // floats): the loads past a layer's last column block run into the pad,
+    // so they need no clamp at the buffer's end and no fix-up at use
+    const int e_hi = PAD ? 0x7fffffff : (int)a.e_total - 4;
+    const int g_hi = PAD ? 0x7fffffff : (int)a.g_total - 4;
+    constexpr int SMAX = 32 * NS - 1;  // the staged sample rows: f >> 4 <= 127 needs no clamp at NS = 4
 
     // eps / eps' block of a tile: 8 + 8 float4 per thread, registers then LDS
     f32x4 ereg[8], enreg[8];
     auto load_E = [&](const StrTile& T) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int f = tid + 256 * j, s = min(f >> 4, SMAX), c4 = f & 15;
             const int off = min(T.eoff + s * T.n + 64 * T.k + 4 * c4, e_hi);
             ereg[j] = *reinterpret_cast<const f32x4*>(a.eps + off);
             enreg[j] = *reinterpret_cast<const f32x4*>(a.eps_next + off);
@@ -1332,9 +1362,10 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     // the float4 clamped at the buffer's end holds columns shifted by d: move
     // them back (applied where the registers are consumed, after the loads land)
     auto fix_E = [&](const StrTile& T) __attribute__((always_inline)) {
+        if constexpr (PAD) return;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int f = tid + 256 * j, s = min(f >> 4, SMAX), c4 = f & 15;
             const int o = T.eoff + s * T.n + 64 * T.k + 4 * c4, d = o - min(o, e_hi);
             if (d > 0) {  // VALU-only: the loads are already unconditional
                 ereg[j] = f32x4{d < 4 ? ereg[j][min(d, 3)] : 0.f, d < 3 ? ereg[j][min(d + 1, 3)] : 0.f,
@@ -1360,7 +1391,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     auto load_G = [&](const StrTile& T) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int f = tid + 256 * j, s = min(f >> 4, SMAX), c4 = f & 15;
             greg[j] = *reinterpret_cast<const f32x4*>(
                 a.g + min(s * a.ldg + T.xc + 64 * T.b + 4 * c4, g_hi));
         }
@@ -1368,10 +1399,10 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
     auto store_G = [&](const StrTile& T) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+            const int f = tid + 256 * j, s = min(f >> 4, SMAX), c4 = f & 15;
             const int o = s * a.ldg + T.xc + 64 * T.b + 4 * c4, d = o - min(o, g_hi);
             f32x4 gv = greg[j];
-            if (d > 0)  // clamped at the buffer's end (see fix_E)
+            if (!PAD && d > 0)  // clamped at the buffer's end (see fix_E)
                 gv = f32x4{d < 4 ? gv[min(d, 3)] : 0.f, d < 3 ? gv[min(d + 1, 3)] : 0.f,
                            d < 2 ? gv[min(d + 2, 3)] : 0.f, 0.f};
             Gl4[tid + 256 * j] = gv;
@@ -1402,6 +1433,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) xacc[sb][q] = 0.f;
     float klp = 0.f, kld = 0.f;  // sum corr^2 (scaled at the end), diagonal KL terms
+    f32x2 kl2 = {0.f, 0.f};      // sum corr^2, two lanes (packed with the Adam arithmetic)
 
     // per-lane LDS offsets of the XOR-swizzled reads
     int okd[8];  // dL A operand (floats): row s = 2t + h, column 32wc + l32; index t & 7
@@ -1516,13 +1548,13 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
             if constexpr (has_next) {
                 if (q < 16) {
                     const int j = q >> 1;
-                    const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+                    const int f = tid + 256 * j, s = min(f >> 4, SMAX), c4 = f & 15;
                     const int off = min(nxt.eoff + s * nxt.n + 64 * nxt.k + 4 * c4, e_hi);
                     if ((q & 1) == 0) ereg[j] = *reinterpret_cast<const f32x4*>(a.eps + off);
                     else enreg[j] = *reinterpret_cast<const f32x4*>(a.eps_next + off);
                 } else if constexpr (newband) {
                     const int j = q - 16;
-                    const int f = tid + 256 * j, s = min(f >> 4, S - 1), c4 = f & 15;
+                    const int f = tid + 256 * j, s = min(f >> 4, SMAX), c4 = f & 15;
                     greg[j] = *reinterpret_cast<const f32x4*>(
                         a.g + min(s * a.ldg + nxt.xc + 64 * nxt.b + 4 * c4, g_hi));
                 }
@@ -1534,17 +1566,24 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
         for (int g = 0; g < 4; ++g) {
             const int cb = 64 * cur.k + 32 * wc + 8 * g + 4 * h;
             float pn[4], mn[4], vn[4];
+            // two entries per packed instruction (entries e, e + 1)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float p = P[g][e];
-                klp += p * p;
-                const bool ok = rv && cb + e < r;
-                const float gv = acc[4 * g + e] + p * kls;
-                float mm = M4[g][e], vv = V4[g][e];
-                pn[e] = adam_fast_k<KIND>(a.adam, p, ok ? gv : 0.f, mm, vv);
-                mn[e] = mm;
-                vn[e] = vv;
+            for (int e = 0; e < 4; e += 2) {
+                const f32x2 p = {P[g][e], P[g][e + 1]};
+                kl2 = __builtin_elementwise_fma(p, p, kl2);
+                const f32x2 gv = __builtin_elementwise_fma(p, f32x2{kls, kls},
+                                                           f32x2{acc[4 * g + e], acc[4 * g + e + 1]});
+                const f32x2 gm = {rv && cb + e < r ? gv[0] : 0.f, rv && cb + e + 1 < r ? gv[1] : 0.f};
+                f32x2 mm = {M4[g][e], M4[g][e + 1]}, vv = {V4[g][e], V4[g][e + 1]};
+                const f32x2 pv = adam_fast_k2<KIND>(a.adam, p, gm, mm, vv);
+                pn[e] = pv[0];
+                pn[e + 1] = pv[1];
+                mn[e] = mm[0];
+                mn[e + 1] = mm[1];
+                vn[e] = vv[0];
+                vn[e + 1] = vv[1];
                 Lf[4 * g + e] = pn[e];
+                Lf[4 * g + e + 1] = pn[e + 1];
             }
             const int64_t o = frag_off(cur, g);
             if constexpr (SC1) {
@@ -1648,7 +1687,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
         o[10] = __builtin_amdgcn_s_memtime();
         o[11] = __builtin_amdgcn_s_memrealtime();
     }
-    klp = klp * (0.5f * a.inv_s0sq) + kld;
+    klp = (klp + (kl2[0] + kl2[1])) * (0.5f * a.inv_s0sq) + kld;
     if (a.kl_out && a.include_kl) {
         const float tot = block_sum(klp, reinterpret_cast<float*>(sm));
         if (tid == 0) atomicAdd(a.kl_out, (double)tot);
@@ -1678,6 +1717,7 @@ static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
 // & 31), columns 32 (w & 1) + 8 g + 4 (lane >> 5) + 0..3).  Entries outside
 // the triangle (or rows 0, n - 1) are zero in the tiled copy.
 struct ConvArgs {
+    float* pad[3];      // nullable: 64 floats to zero each (the inner loop's eps / G pads)
     float* params;
     float* m;
     float* v;
@@ -1692,6 +1732,7 @@ __global__ __launch_bounds__(256) void mvn_tile_convert_kernel(ConvArgs c) {
     __shared__ float T[64 * 65];
     const int tid = threadIdx.x;
     const int64_t tile = blockIdx.x;
+    if (TO_TILED && tile == 0 && tid < 192 && c.pad[tid >> 6]) c.pad[tid >> 6][tid & 63] = 0.f;
     int l = 0;
 #pragma unroll
     for (int j = 1; j < kMaxL; ++j)
@@ -1765,8 +1806,9 @@ __global__ __launch_bounds__(256) void mvn_tile_convert_kernel(ConvArgs c) {
 }
 
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
-                                   float* tstate, bool to_tiled, hipStream_t st) {
+                                   float* tstate, bool to_tiled, hipStream_t st, float* const* pads) {
     ConvArgs c{};
+    for (int i = 0; i < 3; ++i) c.pad[i] = pads ? pads[i] : nullptr;
     c.params = params;
     c.m = m;
     c.v = v;
@@ -1845,9 +1887,13 @@ hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float
 }
 
 template <int NS>
-static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
+static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b, bool pad) {
     if (g_stream_off == 3)  // A/B: plain corr / m / v stores
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER, false, false>), g, bl, 0, st, b);
+    else if (pad && kind == PSVI_ADAM_HIGHER)
+        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER, false, true, true>), g, bl, 0, st, b);
+    else if (pad)
+        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HYPERGRAD, false, true, true>), g, bl, 0, st, b);
     else if (kind == PSVI_ADAM_HIGHER)
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER>), g, bl, 0, st, b);
     else
@@ -1859,16 +1905,17 @@ static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const St
 static bool stream_ok(int S, int kind) {
     return S == 128 && (kind == PSVI_ADAM_HIGHER || kind == PSVI_ADAM_HYPERGRAD);
 }
-static void launch_stream(int ns, int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b) {
+static void launch_stream(int ns, int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b,
+                          bool pad) {
     (void)ns;
-    launch_stream_ns<4>(kind, g, bl, st, b);
+    launch_stream_ns<4>(kind, g, bl, st, b, pad);
 }
 
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
-                             float* tstate, bool packed_out, const float* kl_vec) {
+                             float* tstate, bool packed_out, const float* kl_vec, bool padded) {
     UpdArgs a{};
     a.kl_vec = kl_vec;
     a.chunks = p.d_upd;
@@ -1933,7 +1980,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
             if (b.stamps && a.S == 128 && b.adam.kind == PSVI_ADAM_HIGHER)
                 hipLaunchKernelGGL((mvn_stream_kernel<4, PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
             else
-                launch_stream(a.S / 32, b.adam.kind, sg, block, st, b);
+                launch_stream(a.S / 32, b.adam.kind, sg, block, st, b, padded);
             FwdArgs f{};
             f.params = params;
             f.eps = eps_next;

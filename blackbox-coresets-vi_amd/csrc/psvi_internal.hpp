@@ -407,9 +407,11 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
                              float* tstate = nullptr, bool packed_out = false,
-                             const float* kl_vec = nullptr);
+                             const float* kl_vec = nullptr, bool padded = false);
+// pads (to_tiled, nullable): three 64-float regions the first workgroup zeroes
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
-                                   float* tstate, bool to_tiled, hipStream_t st);
+                                   float* tstate, bool to_tiled, hipStream_t st,
+                                   float* const* pads = nullptr);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);
