@@ -952,6 +952,10 @@ struct KsArgs {
     MvnLayerArgs lay[kMaxL];
 };
 
+// BUF: G / eps / corr / m / v through buffer loads whose per-dword range
+// check returns 0 past the end (and for rows past S, sent to offset kOOB):
+// no clamped addresses, no fix-ups, no zero selects at staging
+template <bool BUF>
 __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     __shared__ __attribute__((aligned(16))) UpdShared<true> sh;
     static_assert(kKsPass == USB, "one LDS stage per pass");
@@ -966,6 +970,9 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const rsrc_t rs = make_rsrc(a.slots, a.slot_bytes);
+    const rsrc_t rg = make_rsrc(a.g, 4 * a.g_total), re = make_rsrc(a.eps, 4 * a.e_total);
+    const rsrc_t rpar = make_rsrc(a.params, 4 * a.pcount), rm = make_rsrc(a.m, 4 * a.pcount),
+                 rv = make_rsrc(a.v, 4 * a.pcount);
     float klp = 0.f;
     const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
     for (int si = sbeg; si < send; ++si) {  // uniform
@@ -990,18 +997,31 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int s = pi * USB + srow + 16 * j;
-                greg[j] = ld4u(a.g, goff(s), 0, g_total);
-                ereg[j] = ld4u(E, eofs(s), -eoff, e_rem);
+                if constexpr (BUF) {
+                    const bool live = s < a.S;
+                    const uint32_t go = live ? (uint32_t)(s * a.ldg + gcol) * 4u : kOOB;
+                    const uint32_t eo = live ? (uint32_t)(eoff + s * n + tl.k * UB + 4 * col4) * 4u : kOOB;
+                    greg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0));
+                    ereg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
+                } else {
+                    greg[j] = ld4u(a.g, goff(s), 0, g_total);
+                    ereg[j] = ld4u(E, eofs(s), -eoff, e_rem);
+                }
             }
         };
         auto stage = [&](int pi) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int o = (srow + 16 * j) * ULD + 4 * col4;
-                const int sr = pi * USB + srow + 16 * j;
-                const bool live = sr < a.S;
-                *reinterpret_cast<float4*>(&Gs[o]) = live ? fix4(greg[j], goff(sr), 0, g_total) : z4;
-                *reinterpret_cast<float4*>(&Es[o]) = live ? fix4(ereg[j], eofs(sr), -eoff, e_rem) : z4;
+                if constexpr (BUF) {
+                    *reinterpret_cast<float4*>(&Gs[o]) = greg[j];
+                    *reinterpret_cast<float4*>(&Es[o]) = ereg[j];
+                } else {
+                    const int sr = pi * USB + srow + 16 * j;
+                    const bool live = sr < a.S;
+                    *reinterpret_cast<float4*>(&Gs[o]) = live ? fix4(greg[j], goff(sr), 0, g_total) : z4;
+                    *reinterpret_cast<float4*>(&Es[o]) = live ? fix4(ereg[j], eofs(sr), -eoff, e_rem) : z4;
+                }
             }
         };
         // epilogue rows: r_j = r0 + srow + 16 j, columns 64 k + 4 col4 + (0..3)
@@ -1019,9 +1039,16 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 // rows off the band's corr rows load something valid, never stored
-                pq[j] = ld4u(a.params, rowp[j] + cl, 0, pcount);
-                mq[j] = ld4u(a.m, rowp[j] + cl, 0, pcount);
-                vq[j] = ld4u(a.v, rowp[j] + cl, 0, pcount);
+                if constexpr (BUF) {
+                    const uint32_t o = (uint32_t)(rowp[j] + cl) * 4u;
+                    pq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpar, o, 0, 0));
+                    mq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rm, o, 0, 0));
+                    vq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
+                } else {
+                    pq[j] = ld4u(a.params, rowp[j] + cl, 0, pcount);
+                    mq[j] = ld4u(a.m, rowp[j] + cl, 0, pcount);
+                    vq[j] = ld4u(a.v, rowp[j] + cl, 0, pcount);
+                }
             }
         };
         floatx16 acc;
@@ -1133,9 +1160,9 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             if (!rown[j] || cb >= r) continue;
             const int o = rowp[j] + cb;
             const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
-            const float4 p4 = fix4(pq[j], o, 0, pcount);
-            const float4 m4 = fix4(mq[j], o, 0, pcount);
-            const float4 v4 = fix4(vq[j], o, 0, pcount);
+            const float4 p4 = BUF ? pq[j] : fix4(pq[j], o, 0, pcount);
+            const float4 m4 = BUF ? mq[j] : fix4(mq[j], o, 0, pcount);
+            const float4 v4 = BUF ? vq[j] : fix4(vq[j], o, 0, pcount);
             float pn[4], mn[4], vn[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1695,7 +1722,7 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 }
 
 int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1: chunked, 3: plain-store stream)
-int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128 (A/B)
+int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128, 2: clamped K-split loads (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -2015,7 +2042,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         }
         return hipGetLastError();
     }
-    if (mode == 2 && !grad_out && p.n_kwg > 0 && !g_ks_off) {
+    if (mode == 2 && !grad_out && p.n_kwg > 0 && g_ks_off != 1) {
         // K = S > 128: the K-split streaming update (then the next step's
         // sample from the new parameters when asked)
         KsArgs k{};
@@ -2041,7 +2068,10 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         k.log_s0 = a.log_s0;
         k.adam = a.adam;
         fill_layers(p, k.lay);
-        hipLaunchKernelGGL(mvn_kstream_kernel, dim3(p.n_kwg), block, 0, st, k);
+        if (g_ks_off == 2)  // A/B: clamped loads with fix-ups
+            hipLaunchKernelGGL(mvn_kstream_kernel<false>, dim3(p.n_kwg), block, 0, st, k);
+        else
+            hipLaunchKernelGGL(mvn_kstream_kernel<true>, dim3(p.n_kwg), block, 0, st, k);
         if (eps_next) {
             const hipError_t e = hipGetLastError();
             return e != hipSuccess ? e : launch_mvn_fwd(p, eps_next, params, x_next, st);
