@@ -118,11 +118,9 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
     float* const part = second ? a.part2 : a.part;
     const int corr_len = (int)((int64_t)(n - 1) * (n - 2) / 2);
     const int eoff = (int)a.lay[it.layer].eoff;
-    const float* E = a.eps + eoff;   // [S][n]; the whole eps buffer is [-eoff, e_rem)
-    const int e_rem = (int)a.e_total - eoff;
+    const rsrc_t re = make_rsrc(a.eps, 4 * a.e_total);
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int col4 = tid & 15, srow = tid >> 4;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr int FT = kFwdRows / 32, LJ = kFwdRows / 16;
     // this thread's staged L rows
     int lrp[LJ];
@@ -143,13 +141,21 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
         const bool wave_live = sb + 32 * wv < a.S;
         float4 lreg[LJ], ereg[8];
-        auto eofs = [&](int j, int kb) { return min(sb + srow + 16 * j, a.S - 1) * n + kb + 4 * col4; };
+        // eps through buffer loads: the per-dword range check returns 0 past
+        // the buffer's end, and rows past S go to offset kOOB (zeros) -- no
+        // clamp, fix-up or select at staging
+        auto eofs = [&](int j, int kb) {
+            const int sr = sb + srow + 16 * j;
+            return sr < a.S ? (uint32_t)(eoff + sr * n + kb + 4 * col4) * 4u : kOOB;
+        };
         auto fetch = [&](int kb) {
 #pragma unroll
             for (int j = 0; j < LJ; ++j)
                 lreg[j] = fld4(corr, (a.abl & 1) ? 0 : lrp[j] + kb + 4 * col4, 0, corr_len);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ereg[j] = fld4(E, (a.abl & 1) ? 0 : eofs(j, kb), -eoff, e_rem);
+            for (int j = 0; j < 8; ++j)
+                ereg[j] = __builtin_bit_cast(
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(re, (a.abl & 1) ? 0u : eofs(j, kb), 0, 0));
         };
         auto stage = [&](int kb) {
             const int c = kb + 4 * col4;
@@ -167,11 +173,7 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_kernel(FwdArgs a) {
                 *reinterpret_cast<float4*>(&Ls[(srow + 16 * j) * FLD + 4 * col4]) = o;
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const bool live = sb + srow + 16 * j < a.S;
-                *reinterpret_cast<float4*>(&Es[(srow + 16 * j) * FLD + 4 * col4]) =
-                    live ? ffix4(ereg[j], eofs(j, kb), -eoff, e_rem) : z4;
-            }
+            for (int j = 0; j < 8; ++j) *reinterpret_cast<float4*>(&Es[(srow + 16 * j) * FLD + 4 * col4]) = ereg[j];
         };
         if (it.k0 < it.k1) fetch(it.k0);
         for (int kb = it.k0; kb < it.k1; kb += FBK) {
