@@ -1,7 +1,7 @@
-#!/bin/bash
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 30 ./tools/probes/buf_oob > gpurun_out/oob.log 2>&1; cat gpurun_out/oob.log
-timeout -k 10 200 python -u tools/sharded_debug.py 2 256 100 3 > gpurun_out/sd.log 2>&1; echo "sd rc=$?"; tail -n 30 gpurun_out/sd.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/t5.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -n 15 gpurun_out/t5.log
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && tail -c 3000 gpurun_out/bench.json &&
+timeout -k 10 200 python -u tools/rank_timing.py --cfg c4 --world 8 --iters 50 > gpurun_out/rt_c4.log 2>&1 && tail -n 12 gpurun_out/rt_c4.log &&
+timeout -k 10 200 python -u tools/rank_timing.py --cfg weak --world 8 --iters 50 > gpurun_out/rt_weak.log 2>&1 && tail -n 3 gpurun_out/rt_weak.log &&
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rt -o rt -- python tools/rank_timing.py --cfg c4 --world 8 --ranks 0,7 --iters 30 > gpurun_out/prof_rt.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_b -o b -- python bench.py --steps 200 > gpurun_out/prof_b.log 2>&1 && echo PROF_OK

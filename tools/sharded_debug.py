@@ -17,6 +17,8 @@ W = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 M = int(sys.argv[3]) if len(sys.argv) > 3 else 100
 T = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+# optional debug switches "key=val,key=val" (include/psvi_hip.h PSVI_DBG_*)
+DBG = [tuple(int(v) for v in kv.split("=")) for kv in sys.argv[5].split(",")] if len(sys.argv) > 5 else []
 from bench import LAYERS, fn2_inputs, reference_init_params  # noqa: E402
 from psvi.runtime import randn_  # noqa: E402
 from psvi.runtime.sharded import ShardedInnerLoop  # noqa: E402
@@ -31,6 +33,9 @@ def offs(splits):
 
 dev = torch.device("cuda", 0)
 loops = [ShardedInnerLoop("fullcov", LAYERS, S, M, W, r, device=dev) for r in range(W)]
+for k, v in DBG:
+    loops[0].plan.lib.psvi_debug_set(k, v)
+    print(f"debug {k} = {v}", flush=True)
 u, z, w = fn2_inputs(LAYERS, M, dev, 0)
 p0 = reference_init_params(LAYERS, dev)
 P = [p0.clone() for _ in range(W)]
