@@ -951,6 +951,7 @@ struct KsArgs {
     int include_kl;
     float inv_s0sq, log_s0;
     AdamC adam;
+    unsigned long long* stamps;  // diagnostics: 16 slots per workgroup (nullptr in production)
     MvnLayerArgs lay[kMaxL];
 };
 
@@ -976,8 +977,25 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     const rsrc_t rpar = make_rsrc(a.params, 4 * a.pcount), rm = make_rsrc(a.m, 4 * a.pcount),
                  rv = make_rsrc(a.v, 4 * a.pcount);
     float klp = 0.f;
+    // diagnostics (a.stamps): shader clocks per phase summed over the segments
+    // -- 1 first-pass load wait, 2 passes (MFMAs + later loads), 3 hand-off,
+    // 4 partial sums, 5 epilogue; 6 segments, 7 combines; 0 / 12 start / end,
+    // 13 / 14 the 100 MHz clock at start / end
+    const bool dg = a.stamps != nullptr;
+    unsigned long long ph[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+    unsigned long long tprev = dg ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long t_start = tprev, rt_start = dg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    int ncomb = 0;
+    auto mark = [&](int k) __attribute__((always_inline)) {
+        if (dg) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            ph[k] += t - tprev;
+            tprev = t;
+        }
+    };
     const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
     for (int si = sbeg; si < send; ++si) {  // uniform
+        if (dg) tprev = __builtin_amdgcn_s_memtime();
         const KsSeg sg = a.segs[si];
         const KsTile tl = a.tiles[sg.tile];
         int n = a.lay[0].n, eoff = (int)a.lay[0].eoff, poff = (int)a.lay[0].poff;
@@ -1062,6 +1080,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
         for (int pi = sg.p0; pi < sg.p1; ++pi) {  // uniform
             stage(pi);
             __syncthreads();
+            if (pi == sg.p0) mark(1);
             // the next pass's operands behind this pass's MFMAs (corr / m / v
             // are loaded at the epilogue: prefetched here they keep 48 more
             // registers live across the MFMAs and the kernel takes scratch)
@@ -1090,6 +1109,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             }
             __syncthreads();  // every wave done with Gs / Es
         }
+        mark(2);
         if (!whole) {
             // ---- split tile: publish this contributor's partial (fragment order:
             // float4 (w * 4 + g) * 64 + lane; then 2 floats of diagonal sums per thread)
@@ -1114,7 +1134,9 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             __syncthreads();
             const int old = __float_as_int(sh.red[0]);
             __syncthreads();  // everyone has read the ticket before red is reused
+            mark(3);
             if (old != sg.nc - 1) continue;  // uniform: another contributor finishes the tile
+            ++ncomb;
             // the last arriver: every partial, in pass order, through sc1 loads
             if (tid == 0)
                 __hip_atomic_store(a.cnt + tl.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1144,6 +1166,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                 dgm += pd[0];
                 dgs += pd[1];
             }
+            mark(4);
         }
         if (whole) load_pmv();
         // ---- Adam epilogue: D[i = c][j = r] (j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h)
@@ -1222,10 +1245,21 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             }
         }
         __syncthreads();  // T / red reads done before the next segment stages
+        mark(5);
     }
     if (a.kl_out && a.include_kl) {
         const float tot = block_sum(klp, sh.red);
         if (tid == 0) atomicAdd(a.kl_out, (double)tot);
+    }
+    if (dg && tid == 0) {
+        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
+        o[0] = t_start;
+        for (int k = 1; k < 6; ++k) o[k] = ph[k];
+        o[6] = (unsigned long long)(send - sbeg);
+        o[7] = (unsigned long long)ncomb;
+        o[12] = __builtin_amdgcn_s_memtime();
+        o[13] = rt_start;
+        o[14] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -2069,6 +2103,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         k.inv_s0sq = a.inv_s0sq;
         k.log_s0 = a.log_s0;
         k.adam = a.adam;
+        k.stamps = g_upd_stamps;
         fill_layers(p, k.lay);
         if (g_ks_off == 2)  // A/B: clamped loads with fix-ups
             hipLaunchKernelGGL(mvn_kstream_kernel<false>, dim3(p.n_kwg), block, 0, st, k);
