@@ -24,6 +24,7 @@ extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
 extern int g_stream_off;                 // kernels_mvn.hip
 extern int g_ks_off;                     // kernels_mvn.hip
+static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
 extern int g_lenet_gemm_valu;            // kernels_lenet.hip
 extern int g_lenet_conv_valu;            // kernels_lenet.hip
 extern int g_lenet_abl;                  // kernels_lenet.hip
@@ -213,7 +214,7 @@ void build_kstream(psvi_plan& p) {
     p.n_kwg = p.n_ks_slots = p.n_ks_cnt = 0;
     if (T == 0) return;
     const int64_t U = (int64_t)T * np;
-    int nwg = (int)std::min<int64_t>(U, 512);
+    int nwg = (int)std::min<int64_t>(U, g_ks_wgs > 0 ? g_ks_wgs : 512);
     if (nwg >= 8) nwg -= nwg % 8;
     // unit cost: 1 per pass, + 0.5 on a tile's last pass (its epilogue)
     std::vector<double> cum(U + 1, 0.0);
@@ -528,6 +529,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
         case PSVI_DBG_KSTREAM_OFF: g_ks_off = value; return 0;
+        case PSVI_DBG_KSTREAM_WGS: g_ks_wgs = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;

@@ -463,6 +463,8 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_NET_SCALAR_LOADS 20 /* value: 1 = the full-cov network kernel's
                                     scalar x / u load path instead of the float4
                                     one (A/B)                                   */
+#define PSVI_DBG_KSTREAM_WGS 21      /* value: workgroups of the K-split update
+                                    for plans created afterwards (0: 512)       */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
