@@ -4,7 +4,7 @@ K-split update (mvn_kstream_kernel) and the sample kernel (mvn_fwd_kernel)
 under the diagnostics API -- event timing and per-workgroup shader-clock
 phase sums / 100 MHz timeline.
 
-  python tools/ks_stamps.py [W] [rank] [S]
+  python tools/ks_stamps.py [W] [rank] [S] [kstream workgroups, 0 = default]
 """
 import ctypes
 import os
@@ -47,6 +47,9 @@ def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     r = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
+    wgs = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    from psvi.runtime import _lib
+    _lib.load().psvi_debug_set(21, wgs)
     plan = InnerLoopPlan("fullcov", LAYERS, S, 200, world=W, rank=r)
     g = torch.Generator().manual_seed(0)
     dev = "cuda"
