@@ -24,6 +24,7 @@ extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
 extern int g_stream_off;                 // kernels_mvn.hip
 extern int g_ks_off;                     // kernels_mvn.hip
+extern int g_fs_off;                     // kernels_mvn.hip
 static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
 extern int g_lenet_gemm_valu;            // kernels_lenet.hip
 extern int g_lenet_conv_valu;            // kernels_lenet.hip
@@ -263,6 +264,82 @@ void build_kstream(psvi_plan& p) {
     p.n_kwg = nwg;
 }
 
+// Segmented sample tables (S > 128): units (row block of 64, 128-sample pass,
+// 64-column block of L) ordered row block-major, then pass, then column block
+// (a run accumulates x over consecutive column blocks of one (row block,
+// pass)); equal-count contiguous runs, one per workgroup, two workgroups per
+// CU; a run's piece of one (row block, pass) is a segment writing its own
+// slot, and the reduce adds a (row block, pass)'s slots in segment order.
+// XCD placement as the K-split update: workgroup w -> run (w % 8) (nwg / 8) + w / 8.
+void build_fseg(psvi_plan& p) {
+    const int r = p.rank, np = (p.d.S + kKsPass - 1) / kKsPass;
+    struct Blk {
+        int layer, r0, r1, xcol, nkb;
+    };
+    std::vector<Blk> blks;
+    for (const ShardRun& run : p.runs[r]) {
+        const int n = p.lay[run.layer].n;
+        for (int r0 = run.lo; r0 < run.hi; r0 += kFwdRows) {
+            const int r1 = std::min(r0 + kFwdRows, run.hi);
+            const int kmax = std::max(0, std::min(r1 - 1, n - 2));
+            blks.push_back(Blk{run.layer, r0, r1, run.col + (r0 - run.lo), (kmax + 63) / 64});
+        }
+    }
+    p.h_fs_segs.clear();
+    p.h_fs_off.clear();
+    p.h_fs_rb.clear();
+    p.n_fswg = p.n_fs_slots = p.n_fs_rb = 0;
+    const int B = (int)blks.size();
+    std::vector<int64_t> ub(B + 1, 0);
+    for (int b = 0; b < B; ++b) ub[b + 1] = ub[b] + (int64_t)blks[b].nkb * np;
+    const int64_t U = ub[B];
+    if (U == 0) return;
+    int nwg = (int)std::min<int64_t>(U, 512);
+    if (nwg >= 8) nwg -= nwg % 8;
+    std::vector<int64_t> cut(nwg + 1);
+    for (int w = 0; w <= nwg; ++w) cut[w] = U * w / nwg;
+    // segments per workgroup; group g = b * np + pass
+    struct Piece {
+        int b, pass, kb0, kb1;
+    };
+    std::vector<std::vector<Piece>> per(nwg);
+    std::vector<int> nseg((size_t)B * np, 0);
+    for (int w = 0; w < nwg; ++w) {
+        int b = (int)(std::upper_bound(ub.begin(), ub.end(), cut[w]) - ub.begin()) - 1;
+        for (int64_t u = cut[w]; u < cut[w + 1];) {
+            while (u >= ub[b + 1]) ++b;
+            const int nkb = blks[b].nkb;
+            const int pass = (int)((u - ub[b]) / nkb), kb = (int)((u - ub[b]) % nkb);
+            const int64_t ue = std::min<int64_t>(cut[w + 1], ub[b] + (int64_t)(pass + 1) * nkb);
+            per[w].push_back(Piece{b, pass, kb, kb + (int)(ue - u)});
+            ++nseg[(size_t)b * np + pass];
+            u = ue;
+        }
+    }
+    std::vector<int> slot0((size_t)B * np), seen((size_t)B * np, 0);
+    for (int b = 0; b < B; ++b)
+        for (int q = 0; q < np; ++q) {
+            const size_t g = (size_t)b * np + q;
+            slot0[g] = p.n_fs_slots;
+            p.n_fs_slots += nseg[g];
+            p.h_fs_rb.push_back(FwdRowBlock{nseg[g] > 0 ? slot0[g] : 0, nseg[g], blks[b].r1 - blks[b].r0,
+                                            blks[b].xcol, blks[b].layer, blks[b].r0, kKsPass * q});
+        }
+    p.h_fs_off.push_back(0);
+    for (int w = 0; w < nwg; ++w) {
+        const int run = (nwg % 8 == 0) ? (w % 8) * (nwg / 8) + w / 8 : w;
+        for (const Piece& pc : per[run]) {
+            const Blk& bk = blks[pc.b];
+            const size_t g = (size_t)pc.b * np + pc.pass;
+            p.h_fs_segs.push_back(FsSeg{bk.layer, bk.r0, bk.r1, pc.pass, 64 * pc.kb0, 64 * pc.kb1,
+                                        slot0[g] + seen[g]++, 0});
+        }
+        p.h_fs_off.push_back((int)p.h_fs_segs.size());
+    }
+    p.n_fswg = nwg;
+    p.n_fs_rb = (int)p.h_fs_rb.size();
+}
+
 // make_lenet (neural_net.py:334-359): five mean-field-style layers, the first
 // two convolutions ("din" = in_channels * 25), the last one a single shared
 // sample.  Samples are sharded like the mean-field family.
@@ -474,7 +551,10 @@ int build_plan(psvi_plan& p) {
             p.n_sslots = ns;
         }
         p.upd_tiles = tiles;
-        if (S > kKsPass) build_kstream(p);
+        if (S > kKsPass) {
+        build_kstream(p);
+        build_fseg(p);
+    }
         p.n_fwd = (int)fwd.size();
         p.n_upd = (int)p.h_upd.size();
         const size_t xs = sizeof(float) * (size_t)S * p.rows_tot[r];
@@ -530,6 +610,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
         case PSVI_DBG_KSTREAM_OFF: g_ks_off = value; return 0;
         case PSVI_DBG_KSTREAM_WGS: g_ks_wgs = value; return 0;
+        case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
@@ -637,6 +718,13 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
                             hipSuccess))
                 rc = fail(PSVI_EUNSUP, "cannot allocate the K-split update's slots");
         }
+        if (!rc && p->n_fswg > 0) {
+            if (!(rc = upload(p->h_fs_segs, &p->d_fs_segs)) && !(rc = upload(p->h_fs_off, &p->d_fs_off)))
+                rc = upload(p->h_fs_rb, &p->d_fs_rb);
+            const size_t sb = sizeof(float) * (size_t)std::max(1, p->n_fs_slots) * kKsPass * kFwdRows;
+            if (!rc && hipMalloc((void**)&p->d_fs_part, sb) != hipSuccess)
+                rc = fail(PSVI_EUNSUP, "cannot allocate the segmented sample's slots");
+        }
         if (!rc && family == PSVI_FAMILY_FULLCOV) {
             std::vector<uint32_t> xmap;
             std::vector<NetBand> bands;
@@ -696,6 +784,10 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_ks_off) (void)hipFree(p->d_ks_off);
     if (p->d_ks_slots) (void)hipFree(p->d_ks_slots);
     if (p->d_ks_cnt) (void)hipFree(p->d_ks_cnt);
+    if (p->d_fs_segs) (void)hipFree(p->d_fs_segs);
+    if (p->d_fs_off) (void)hipFree(p->d_fs_off);
+    if (p->d_fs_rb) (void)hipFree(p->d_fs_rb);
+    if (p->d_fs_part) (void)hipFree(p->d_fs_part);
     if (p->d_net_bands) (void)hipFree(p->d_net_bands);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);

@@ -63,6 +63,14 @@ struct FwdArgs {
     int abl;                     // diagnostics ablation mask (0 in production):
                                  // 1 loads, 2 MFMAs, 4 x atomics
     unsigned long long* stamps;  // diagnostics: 16 slots per workgroup
+    // segmented sample (mvn_fwd_seg_kernel): segments, per-workgroup offsets,
+    // parameter count (buffer range), sample rows per slot (0: S, one slot spans
+    // all samples -- the item grid and the fused updates' slots)
+    const FsSeg* segs;
+    const int* seg_off;
+    int64_t pcount;
+    int slot_rows;
+    int slot_frag;  // slots in MFMA fragment order (the segmented sample)
     MvnLayerArgs lay[kMaxL];
 };
 
@@ -244,17 +252,27 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
     const float* const prm = second ? a.params2 : a.params;
     const float* const dof = second ? a.diag_of2 : a.diag_of;
     const int rr = threadIdx.x & (kFwdRows - 1);
-    const int s0 = blockIdx.y * kRedSpb + threadIdx.x / kFwdRows, s1 = s0 + kRedSpb / 2;
-    if (s0 >= a.S || rr >= rb.R) return;
-    const bool two = s1 < a.S;
+    // slots of slot_rows samples from sample rb.s0 (0 / S: one slot spans all)
+    const int srows = a.slot_rows > 0 ? a.slot_rows : a.S;
+    const int l0 = blockIdx.y * kRedSpb + threadIdx.x / kFwdRows, l1 = l0 + kRedSpb / 2;
+    const int s0 = rb.s0 + l0, s1 = rb.s0 + l1, s_end = min(a.S, rb.s0 + srows);
+    if (s0 >= s_end || rr >= rb.R) return;
+    const bool two = s1 < s_end;
     const int n = a.lay[rb.layer].n, r = rb.r0 + rr;
     const float* mean = prm + a.lay[rb.layer].poff;
     const float* eps = a.eps + a.lay[rb.layer].eoff + r;
     const float e0 = eps[(int64_t)s0 * n], e1 = eps[(int64_t)(two ? s1 : s0) * n];
     const float mu = mean[r], sdr = mean[n + r];
-    const size_t st = (size_t)a.S * kFwdRows;
-    const float* p0 = part + (size_t)rb.slot0 * st + (size_t)s0 * kFwdRows + rr;
-    const float* p1 = part + (size_t)rb.slot0 * st + (size_t)(two ? s1 : s0) * kFwdRows + rr;
+    const size_t st = (size_t)srows * kFwdRows;
+    // slot element (sample l, row rr): row-major [l][rr], or (a.slot_frag, the
+    // segmented sample) the MFMA fragment order of mvn_fwd_seg_kernel
+    auto so = [&](int l) -> size_t {
+        if (!a.slot_frag) return (size_t)l * kFwdRows + rr;
+        const int i = l & 31, hh = (i >> 2) & 1, q = (i & 3) + 4 * (i >> 3);
+        return ((size_t)((l >> 5) * (kFwdRows / 32) + (rr >> 5)) * 16 + q) * 64 + (rr & 31) + 32 * hh;
+    };
+    const float* p0 = part + (size_t)rb.slot0 * st + so(l0);
+    const float* p1 = part + (size_t)rb.slot0 * st + so(two ? l1 : l0);
     // The first 8 slots as unconditional loads at clamped indices (all in
     // flight at once; a row block of C3's streaming update has 1-10 slots),
     // any further ones 4 at a time.  Partial sums s4[k % 4] in slot order k =
@@ -291,6 +309,167 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
     x[(int64_t)s0 * a.ldx + rb.xcol + rr] = (mu + dg * e0) + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
     if (two) x[(int64_t)s1 * a.ldx + rb.xcol + rr] = (mu + dg * e1) + ((b4[0] + b4[1]) + (b4[2] + b4[3]));
 }
+
+// Segmented sample (K = S > 128): one persistent workgroup run of the
+// (row block, pass, column block) unit list (build_fseg), two per CU.  Per
+// segment -- consecutive column blocks of one (row block, 128-sample pass) --
+// D[s][r] = sum_c eps[s][c] L[r][c] accumulates over its column blocks as in
+// mvn_fwd_kernel (64-column LDS stages, k-permuted ds_read_b128 feed, wave w
+// = 32 samples x 64 rows), then goes to the segment's slot ([128][64]); the
+// reduce adds a (row block, pass)'s slots.  The next stage -- the next
+// segment's first after a segment's last -- is loaded behind the MFMAs.  corr
+// and eps through buffer loads: the range check returns 0 past the end (rows
+// past S to offset kOOB); the triangle / row masks are applied at staging.
+__global__ __launch_bounds__(256, 2) void mvn_fwd_seg_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float Es[FST * FLD];       // eps  [s][k]
+    __shared__ __attribute__((aligned(16))) float Ls[kFwdRows * FLD];  // corr [r][k]
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const int col4 = tid & 15, srow = tid >> 4;
+    constexpr int FT = kFwdRows / 32, LJ = kFwdRows / 16;
+    const rsrc_t re = make_rsrc(a.eps, 4 * a.e_total);
+    const rsrc_t rp = make_rsrc(a.params, 4 * a.pcount);
+    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
+    if (sbeg >= send) return;  // uniform, before any barrier
+    struct D {
+        int n, corr, eoff, r0, r1, s0;
+    };
+    auto desc = [&](const FsSeg& g) __attribute__((always_inline)) {
+        D d;
+        int poff = (int)a.lay[0].poff;
+        d.n = a.lay[0].n;
+        d.eoff = (int)a.lay[0].eoff;
+#pragma unroll
+        for (int l = 1; l < kMaxL; ++l)  // select: a dynamic index into the arguments goes to scratch
+            if (g.layer == l) {
+                d.n = a.lay[l].n;
+                d.eoff = (int)a.lay[l].eoff;
+                poff = (int)a.lay[l].poff;
+            }
+        d.corr = poff + 2 * d.n;
+        d.r0 = g.r0;
+        d.r1 = g.r1;
+        d.s0 = g.pass * FST;
+        return d;
+    };
+    float4 lreg[LJ], ereg[8];
+    auto fetch = [&](const D& d, int kb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < LJ; ++j) {
+            const int r = d.r0 + srow + 16 * j;
+            const int ro = r >= 1 ? (int)((int64_t)r * (r - 1) / 2) : 0;
+            lreg[j] = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(rp, (uint32_t)(d.corr + ro + kb + 4 * col4) * 4u, 0, 0));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int sr = d.s0 + srow + 16 * j;
+            const uint32_t eo = sr < a.S ? (uint32_t)(d.eoff + sr * d.n + kb + 4 * col4) * 4u : kOOB;
+            ereg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
+        }
+    };
+    auto stage = [&](const D& d, int kb) __attribute__((always_inline)) {
+        const int c = kb + 4 * col4;
+#pragma unroll
+        for (int j = 0; j < LJ; ++j) {
+            // entries outside the block's rows / the strict lower triangle are 0
+            const int r = d.r0 + srow + 16 * j;
+            const bool rok = r < d.r1 && r <= d.n - 2;
+            const float4 v = lreg[j];
+            float4 o;
+            o.x = rok && c + 0 < r ? v.x : 0.f;
+            o.y = rok && c + 1 < r ? v.y : 0.f;
+            o.z = rok && c + 2 < r ? v.z : 0.f;
+            o.w = rok && c + 3 < r ? v.w : 0.f;
+            *reinterpret_cast<float4*>(&Ls[(srow + 16 * j) * FLD + 4 * col4]) = o;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<float4*>(&Es[(srow + 16 * j) * FLD + 4 * col4]) = ereg[j];
+    };
+    // diagnostics (a.stamps): shader clocks -- 1 until the first stage is in
+    // LDS, 2 stages + MFMAs, 3 slot writes (summed over segments); 6 stages;
+    // 0 / 12 start / end, 13 / 14 the 100 MHz clock at start / end
+    const bool dgn = a.stamps != nullptr;
+    unsigned long long ph[4] = {0ull, 0ull, 0ull, 0ull}, tprev = dgn ? __builtin_amdgcn_s_memtime() : 0ull;
+    const unsigned long long t_start = tprev, rt_start = dgn ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    int nst = 0;
+    auto mark = [&](int q) __attribute__((always_inline)) {
+        if (dgn) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            ph[q] += t - tprev;
+            tprev = t;
+        }
+    };
+    FsSeg gn = a.segs[sbeg];
+    D dn = desc(gn);
+    fetch(dn, gn.k0);
+    for (int si = sbeg; si < send; ++si) {  // uniform
+        const FsSeg g = gn;
+        const D d = dn;
+        const bool more = si + 1 < send;
+        if (more) {
+            gn = a.segs[si + 1];
+            dn = desc(gn);
+        }
+        floatx16 acc[FT];
+#pragma unroll
+        for (int t = 0; t < FT; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+        const bool wave_live = d.s0 + 32 * wv < a.S;
+        for (int kb = g.k0; kb < g.k1; kb += FBK) {  // uniform
+            __syncthreads();  // previous stage's MFMAs done with the LDS
+            stage(d, kb);
+            __syncthreads();
+            if (si == sbeg && kb == g.k0) mark(1);
+            ++nst;
+            {
+                const bool inseg = kb + FBK < g.k1;
+                if (inseg || more) fetch(inseg ? d : dn, inseg ? kb + FBK : gn.k0);
+            }
+            if (wave_live) {
+                // k permutation: per 8 columns, lane half h feeds k = kk + 4h + j to
+                // MFMA j (j = 0..3) for BOTH operands -- the same sum over k
+                const float* Ea = Es + (32 * wv + l32) * FLD + 4 * h;
+                const float* Lb = Ls + l32 * FLD + 4 * h;
+#pragma unroll
+                for (int kk = 0; kk < FBK; kk += 8) {
+                    const float4 av = *reinterpret_cast<const float4*>(Ea + kk);
+                    float4 bv[FT];
+#pragma unroll
+                    for (int t = 0; t < FT; ++t) bv[t] = *reinterpret_cast<const float4*>(Lb + 32 * t * FLD + kk);
+#pragma unroll
+                    for (int t = 0; t < FT; ++t) {
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[t].x, acc[t], 0, 0, 0);
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[t].y, acc[t], 0, 0, 0);
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[t].z, acc[t], 0, 0, 0);
+                        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[t].w, acc[t], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        mark(2);
+        // the accumulators in fragment order ((wave FT + t) 16 + q) 64 + lane: every
+        // store a contiguous 256-byte wave run (the reduce reads the order back)
+        if (wave_live) {
+            float* slot = a.part + (size_t)g.slot * FST * kFwdRows + (size_t)wv * FT * 16 * 64 + lane;
+#pragma unroll
+            for (int t = 0; t < FT; ++t)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) slot[(t * 16 + q) * 64] = acc[t][q];
+        }
+        mark(3);
+    }
+    if (dgn && threadIdx.x == 0) {
+        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
+        o[0] = t_start;
+        for (int q = 1; q < 4; ++q) o[q] = ph[q];
+        o[6] = (unsigned long long)nst;
+        o[12] = __builtin_amdgcn_s_memtime();
+        o[13] = rt_start;
+        o[14] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 
 int g_fwd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_FWD_ABLATION, mask)
 unsigned long long* g_fwd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_FWD_STAMPS, buf)
@@ -955,10 +1134,11 @@ struct KsArgs {
     MvnLayerArgs lay[kMaxL];
 };
 
-// BUF: G / eps / corr / m / v through buffer loads whose per-dword range
-// check returns 0 past the end (and for rows past S, sent to offset kOOB):
-// no clamped addresses, no fix-ups, no zero selects at staging
-template <bool BUF>
+// G / eps / corr / m / v through buffer loads whose per-dword range check
+// returns 0 past the end (rows past S are sent to offset kOOB): no clamped
+// addresses, fix-ups or zero selects at staging.  The first pass of the next
+// segment is loaded behind the last pass of this one (its latency overlaps the
+// hand-off and the epilogue).
 __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     __shared__ __attribute__((aligned(16))) UpdShared<true> sh;
     static_assert(kKsPass == USB, "one LDS stage per pass");
@@ -967,8 +1147,6 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int wr = wv >> 1, wc = wv & 1;
     const int col4 = tid & 15, srow = tid >> 4;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int g_total = (int)a.g_total, pcount = (int)a.pcount;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -993,57 +1171,62 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             tprev = t;
         }
     };
-    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
-    for (int si = sbeg; si < send; ++si) {  // uniform
-        if (dg) tprev = __builtin_amdgcn_s_memtime();
-        const KsSeg sg = a.segs[si];
-        const KsTile tl = a.tiles[sg.tile];
-        int n = a.lay[0].n, eoff = (int)a.lay[0].eoff, poff = (int)a.lay[0].poff;
+    // a segment's pass operands: G columns gcol.., eps [S][n] at eoff, columns ecol..
+    struct Ld {
+        int gcol, eoff, n, ecol;
+    };
+    auto desc = [&](const KsTile& t) __attribute__((always_inline)) {
+        Ld d;
+        d.n = a.lay[0].n;
+        d.eoff = (int)a.lay[0].eoff;
 #pragma unroll
         for (int l = 1; l < kMaxL; ++l)  // select: a dynamic index into the arguments goes to scratch
-            if (tl.layer == l) {
-                n = a.lay[l].n;
-                eoff = (int)a.lay[l].eoff;
-                poff = (int)a.lay[l].poff;
+            if (t.layer == l) {
+                d.n = a.lay[l].n;
+                d.eoff = (int)a.lay[l].eoff;
             }
-        const float* E = a.eps + eoff;  // [S][n]; the whole eps buffer is [-eoff, e_rem)
-        const int e_rem = (int)a.e_total - eoff;
+        d.gcol = t.xcol + t.r0 + 4 * col4;
+        d.ecol = t.k * UB + 4 * col4;
+        return d;
+    };
+    float4 greg[8], ereg[8];
+    auto load = [&](const Ld& d, int pi) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int s = pi * USB + srow + 16 * j;
+            const bool live = s < a.S;
+            const uint32_t go = live ? (uint32_t)(s * a.ldg + d.gcol) * 4u : kOOB;
+            const uint32_t eo = live ? (uint32_t)(d.eoff + s * d.n + d.ecol) * 4u : kOOB;
+            greg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0));
+            ereg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
+        }
+    };
+    auto stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int o = (srow + 16 * j) * ULD + 4 * col4;
+            *reinterpret_cast<float4*>(&Gs[o]) = greg[j];
+            *reinterpret_cast<float4*>(&Es[o]) = ereg[j];
+        }
+    };
+    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
+    KsSeg sg_next = a.segs[sbeg < send ? sbeg : 0];
+    if (sbeg < send) load(desc(a.tiles[sg_next.tile]), sg_next.p0);
+    for (int si = sbeg; si < send; ++si) {  // uniform
+        if (dg) tprev = __builtin_amdgcn_s_memtime();
+        const KsSeg sg = sg_next;
+        const KsTile tl = a.tiles[sg.tile];
+        const Ld cur = desc(tl);
+        const int n = cur.n;
+        int poff = (int)a.lay[0].poff;
+#pragma unroll
+        for (int l = 1; l < kMaxL; ++l)
+            if (tl.layer == l) poff = (int)a.lay[l].poff;
         const int corr_off = poff + 2 * n;
-        const int gcol = tl.xcol + tl.r0 + 4 * col4;
-        auto goff = [&](int s) { return min(s, a.S - 1) * a.ldg + gcol; };
-        auto eofs = [&](int s) { return min(s, a.S - 1) * n + tl.k * UB + 4 * col4; };
-        float4 greg[8], ereg[8];
-        auto load = [&](int pi) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int s = pi * USB + srow + 16 * j;
-                if constexpr (BUF) {
-                    const bool live = s < a.S;
-                    const uint32_t go = live ? (uint32_t)(s * a.ldg + gcol) * 4u : kOOB;
-                    const uint32_t eo = live ? (uint32_t)(eoff + s * n + tl.k * UB + 4 * col4) * 4u : kOOB;
-                    greg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0));
-                    ereg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
-                } else {
-                    greg[j] = ld4u(a.g, goff(s), 0, g_total);
-                    ereg[j] = ld4u(E, eofs(s), -eoff, e_rem);
-                }
-            }
-        };
-        auto stage = [&](int pi) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int o = (srow + 16 * j) * ULD + 4 * col4;
-                if constexpr (BUF) {
-                    *reinterpret_cast<float4*>(&Gs[o]) = greg[j];
-                    *reinterpret_cast<float4*>(&Es[o]) = ereg[j];
-                } else {
-                    const int sr = pi * USB + srow + 16 * j;
-                    const bool live = sr < a.S;
-                    *reinterpret_cast<float4*>(&Gs[o]) = live ? fix4(greg[j], goff(sr), 0, g_total) : z4;
-                    *reinterpret_cast<float4*>(&Es[o]) = live ? fix4(ereg[j], eofs(sr), -eoff, e_rem) : z4;
-                }
-            }
-        };
+        // the segment after this one: its first pass loads behind our last
+        const bool more = si + 1 < send;
+        if (more) sg_next = a.segs[si + 1];
+        const Ld nxt = desc(a.tiles[sg_next.tile]);
         // epilogue rows: r_j = r0 + srow + 16 j, columns 64 k + 4 col4 + (0..3)
         int rowp[4];
         bool rown[4];
@@ -1054,21 +1237,28 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             rowp[j] = corr_off + (int)((int64_t)r * (r - 1) / 2);
         }
         float4 pq[4], mq[4], vq[4];
+        // the diagonal tile's mean / sd rows (thread tid & 63 -> row r0 + (tid & 63)):
+        // value, m, v of both, loaded with corr / m / v (not one round trip each)
+        float dmu = 0.f, dsd = 0.f, dmm = 0.f, dmv = 0.f, dsm = 0.f, dsv = 0.f;
+        const int pm_d = poff + tl.r0 + (tid & 63), ps_d = pm_d + n;
         auto load_pmv = [&]() {
+            if (tl.diag) {  // uniform
+                const uint32_t om = (uint32_t)pm_d * 4u, os = (uint32_t)ps_d * 4u;
+                dmu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpar, om, 0, 0));
+                dsd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpar, os, 0, 0));
+                dmm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, om, 0, 0));
+                dmv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, om, 0, 0));
+                dsm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, os, 0, 0));
+                dsv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, os, 0, 0));
+            }
             const int cl = tl.k * UB + 4 * col4;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 // rows off the band's corr rows load something valid, never stored
-                if constexpr (BUF) {
-                    const uint32_t o = (uint32_t)(rowp[j] + cl) * 4u;
-                    pq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpar, o, 0, 0));
-                    mq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rm, o, 0, 0));
-                    vq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
-                } else {
-                    pq[j] = ld4u(a.params, rowp[j] + cl, 0, pcount);
-                    mq[j] = ld4u(a.m, rowp[j] + cl, 0, pcount);
-                    vq[j] = ld4u(a.v, rowp[j] + cl, 0, pcount);
-                }
+                const uint32_t o = (uint32_t)(rowp[j] + cl) * 4u;
+                pq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpar, o, 0, 0));
+                mq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rm, o, 0, 0));
+                vq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
             }
         };
         floatx16 acc;
@@ -1076,15 +1266,18 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
         float dgm = 0.f, dgs = 0.f;
         const bool whole = sg.slot < 0;
-        load(sg.p0);
         for (int pi = sg.p0; pi < sg.p1; ++pi) {  // uniform
-            stage(pi);
+            stage();
             __syncthreads();
             if (pi == sg.p0) mark(1);
-            // the next pass's operands behind this pass's MFMAs (corr / m / v
-            // are loaded at the epilogue: prefetched here they keep 48 more
+            // the next pass's operands behind this pass's MFMAs -- after the
+            // segment's last pass, the next segment's first (corr / m / v are
+            // loaded at the epilogue: prefetched here they keep 48 more
             // registers live across the MFMAs and the kernel takes scratch)
-            if (pi + 1 < sg.p1) load(pi + 1);
+            {
+                const bool inseg = pi + 1 < sg.p1;
+                if (inseg || more) load(inseg ? cur : nxt, inseg ? pi + 1 : sg_next.p0);
+            }
             const int kend = min(USB, a.S - pi * USB);
             if (tl.diag) {
                 // column j of Es is row r0 + j of the band
@@ -1141,30 +1334,41 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             if (tid == 0)
                 __hip_atomic_store(a.cnt + tl.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             load_pmv();
-            float4 part[4];
-            f32x2 pd = f32x2{0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[q] = 0.f;
             dgm = dgs = 0.f;
-            for (int c = 0; c < sg.nc; ++c) {  // uniform
-                const uint32_t cb = (uint32_t)((sg.slot + c) * kKsSlotFloats) * 4u;
+            // the partials KP at a time (all their loads in flight together),
+            // added in pass order; past nc the last one is loaded again, not added
+            constexpr int KP = 4;
+            for (int c0 = 0; c0 < sg.nc; c0 += KP) {  // uniform
+                float4 part[KP][4];
+                f32x2 pd[KP];
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    part[g] = __builtin_bit_cast(
-                        float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                    rs, cb + (uint32_t)(((wv * 4 + g) * 64 + lane) * 16), 0, 16));
-                if (tl.diag)
-                    pd = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(
-                                                        rs, cb + (uint32_t)(4096 * 4 + tid * 8), 0, 16));
+                for (int i = 0; i < KP; ++i) {
+                    const int c = min(c0 + i, sg.nc - 1);
+                    const uint32_t cb = (uint32_t)((sg.slot + c) * kKsSlotFloats) * 4u;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    acc[4 * g] += part[g].x;
-                    acc[4 * g + 1] += part[g].y;
-                    acc[4 * g + 2] += part[g].z;
-                    acc[4 * g + 3] += part[g].w;
+                    for (int g = 0; g < 4; ++g)
+                        part[i][g] = __builtin_bit_cast(
+                            float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                        rs, cb + (uint32_t)(((wv * 4 + g) * 64 + lane) * 16), 0, 16));
+                    pd[i] = tl.diag ? __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                                   rs, cb + (uint32_t)(4096 * 4 + tid * 8), 0, 16))
+                                    : f32x2{0.f, 0.f};
                 }
-                dgm += pd[0];
-                dgs += pd[1];
+#pragma unroll
+                for (int i = 0; i < KP; ++i) {
+                    if (c0 + i >= sg.nc) break;  // uniform
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        acc[4 * g] += part[i][g].x;
+                        acc[4 * g + 1] += part[i][g].y;
+                        acc[4 * g + 2] += part[i][g].z;
+                        acc[4 * g + 3] += part[i][g].w;
+                    }
+                    dgm += pd[i][0];
+                    dgs += pd[i][1];
+                }
             }
             mark(4);
         }
@@ -1185,9 +1389,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             if (!rown[j] || cb >= r) continue;
             const int o = rowp[j] + cb;
             const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
-            const float4 p4 = BUF ? pq[j] : fix4(pq[j], o, 0, pcount);
-            const float4 m4 = BUF ? mq[j] : fix4(mq[j], o, 0, pcount);
-            const float4 v4 = BUF ? vq[j] : fix4(vq[j], o, 0, pcount);
+            const float4 p4 = pq[j], m4 = mq[j], v4 = vq[j];
             float pn[4], mn[4], vn[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1224,8 +1426,8 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                 const float* red = sh.red;
                 const float gm = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
                 const float gs = red[256 + tid] + red[320 + tid] + red[384 + tid] + red[448 + tid];
-                const int pm = poff + rr, ps = pm + n;
-                const float mu = a.params[pm], sdr = a.params[ps];
+                const int pm = pm_d, ps = ps_d;  // rr = r0 + tid
+                const float mu = dmu, sdr = dsd;
                 const float sp = softplus_f(sdr), sgm = sigmoid_f(sdr);
                 float gmean = gm, gsd = gs * sgm;
                 if (a.include_kl) {
@@ -1233,12 +1435,12 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                     gsd += (sp * a.inv_s0sq - 1.f / sp) * sgm;
                     klp += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
                 }
-                float mm = a.m[pm], vv = a.v[pm];
+                float mm = dmm, vv = dmv;
                 a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
                 a.m[pm] = mm;
                 a.v[pm] = vv;
-                mm = a.m[ps];
-                vv = a.v[ps];
+                mm = dsm;
+                vv = dsv;
                 a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
                 a.m[ps] = mm;
                 a.v[ps] = vv;
@@ -1758,7 +1960,8 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 }
 
 int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1: chunked, 3: plain-store stream)
-int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128, 2: clamped K-split loads (A/B)
+int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128 (A/B)
+int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -1913,6 +2116,20 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
     a.abl = g_fwd_ablation;
     a.stamps = g_fwd_stamps;
     fill_layers(p, a.lay);
+    if (p.n_fswg > 0 && !g_fs_off) {
+        // K = S > 128: the segmented sample, then the (row block, pass) reduce
+        a.segs = p.d_fs_segs;
+        a.seg_off = p.d_fs_off;
+        a.pcount = p.P;
+        a.part = p.d_fs_part;
+        a.slot_rows = FST;
+        a.slot_frag = 1;
+        a.abl = 0;
+        hipLaunchKernelGGL(mvn_fwd_seg_kernel, dim3(p.n_fswg), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_fs_rb, FST / kRedSpb), dim3(256), 0, st,
+                           p.d_fs_rb, p.d_fs_part, a, x_shard);
+        return hipGetLastError();
+    }
     if (p.n_fwd == 0) return hipSuccess;
     // every x element is written by exactly one reduce thread: no memset
     hipLaunchKernelGGL(mvn_fwd_kernel, dim3(p.n_fwd, 1, fwd_sample_blocks(p)), dim3(256), 0, st, a);
@@ -2105,10 +2322,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         k.adam = a.adam;
         k.stamps = g_upd_stamps;
         fill_layers(p, k.lay);
-        if (g_ks_off == 2)  // A/B: clamped loads with fix-ups
-            hipLaunchKernelGGL(mvn_kstream_kernel<false>, dim3(p.n_kwg), block, 0, st, k);
-        else
-            hipLaunchKernelGGL(mvn_kstream_kernel<true>, dim3(p.n_kwg), block, 0, st, k);
+        hipLaunchKernelGGL(mvn_kstream_kernel, dim3(p.n_kwg), block, 0, st, k);
         if (eps_next) {
             const hipError_t e = hipGetLastError();
             return e != hipSuccess ? e : launch_mvn_fwd(p, eps_next, params, x_next, st);

@@ -210,6 +210,16 @@ struct FwdItem {
 struct FwdRowBlock {
     int slot0, nk, R, xcol;
     int layer, r0;  // absolute first row (the reduce adds mean + softplus(sd) eps)
+    int s0;         // first sample of the block's slots (segmented sample: a pass's 128)
+};
+// Segmented sample (mvn_fwd_seg_kernel, K = S > 128): units (row block,
+// 128-sample pass, 64-column block of L), row block-major then pass then
+// column block, cut into equal contiguous runs, one per workgroup; a run's
+// piece of one (row block, pass) is a segment with its own partial slot
+// ([128][kFwdRows] floats), and the reduce adds a (row block, pass)'s slots.
+struct FsSeg {
+    int layer, r0, r1, pass;  // rows [r0, r1) of layer, samples [128 pass, 128 pass + 128)
+    int k0, k1, slot, pad;    // columns [k0, k1) of L (64-column blocks)
 };
 // Full-cov update work item: the 64-row band [r0, r0+64) of layer `layer`
 // (r0 a multiple of 64; the rank owns rows [rlo, rhi)) against the c-blocks
@@ -348,6 +358,16 @@ struct psvi_plan {
     float* d_ks_slots = nullptr;
     int* d_ks_cnt = nullptr;
     int n_kwg = 0, n_ks_slots = 0, n_ks_cnt = 0;
+    // segmented sample (S > 128): segments, per-workgroup offsets, (row block,
+    // pass) reduce blocks, partial slots ([n_fs_slots][128][kFwdRows])
+    std::vector<psvi::FsSeg> h_fs_segs;
+    std::vector<int> h_fs_off;
+    std::vector<psvi::FwdRowBlock> h_fs_rb;
+    psvi::FsSeg* d_fs_segs = nullptr;
+    int* d_fs_off = nullptr;
+    psvi::FwdRowBlock* d_fs_rb = nullptr;
+    float* d_fs_part = nullptr;
+    int n_fswg = 0, n_fs_slots = 0, n_fs_rb = 0;
     // net kernel geometry
     int mchunks = 1, mc = 0, net_threads = 256, net_roles = 1;
     size_t net_lds = 0;

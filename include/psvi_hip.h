@@ -465,6 +465,8 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     one (A/B)                                   */
 #define PSVI_DBG_KSTREAM_WGS 21      /* value: workgroups of the K-split update
                                     for plans created afterwards (0: 512)       */
+#define PSVI_DBG_FWD_SEG_OFF 22      /* value: 1 = the item-grid sample kernel instead
+                                    of the segmented one at S > 128 (A/B)       */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

@@ -133,3 +133,50 @@ def test_kstream_world8_ranks_cover_the_update():
     for k, tol in zip(range(3), (1e-6, 1e-5, 1e-5)):
         assert l2rel(full[k], a1[k]) < tol
     assert rel(kl, a1[3]) < 1e-6
+
+
+@pytest.mark.parametrize("W,S", [(1, 1024), (1, 300), (8, 1024), (3, 257), (2, 256)])
+def test_segmented_sample_matches_oracle(W, S):
+    """The segmented sample (mvn_fwd_seg_kernel + the (row block, pass) reduce,
+    K = S > 128): each rank's rows of x = mean + L eps for all S samples against
+    the float64 oracle (1e-6 relative, l2) and against the item-grid kernel
+    (PSVI_DBG_FWD_SEG_OFF A/B); ragged S leaves a partial last pass."""
+    from psvi.runtime import InnerLoopPlan
+    from psvi.runtime.sharded import layer_rows
+
+    p, _, _, _, eps = _state(FN2, S, 11 + W + S)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=DEV)
+    dp, de = t(p), t(eps)
+    woff = np.concatenate([[0], np.cumsum([i * o + o for i, o in FN2])]).astype(int)
+    Xo = np.zeros((S, woff[-1]))
+    po = eo = 0
+    for l, (din, dout) in enumerate(FN2):
+        n = din * dout + dout
+        nc = (n - 1) * (n - 2) // 2
+        L = O.mvn_dense_L(p[po + n:po + 2 * n], p[po + 2 * n:po + 2 * n + nc], n)
+        E = eps[eo:eo + S * n].reshape(S, n).astype(np.float64)
+        Xo[:, woff[l]:woff[l + 1]] = p[po:po + n][None].astype(np.float64) + E @ L.T
+        po += 2 * n + nc
+        eo += S * n
+    ranks = range(W) if W <= 3 else (0, W - 1)
+    for r in ranks:
+        plan = InnerLoopPlan("fullcov", FN2, S, 100, world=W, rank=r)
+        info = plan.shard_info(r)
+        xs = torch.full((plan.xshard_count,), float("nan"), device=DEV)
+        plan.mvn_sample(de, dp, xs)
+        xa = xs.clone()
+        plan.lib.psvi_debug_set(22, 1)
+        try:
+            xs.fill_(float("nan"))
+            plan.mvn_sample(de, dp, xs)
+            torch.cuda.synchronize()
+        finally:
+            plan.lib.psvi_debug_set(22, 0)
+        X = xa.view(S, -1).cpu().numpy().astype(np.float64)
+        Xb = xs.view(S, -1).cpu().numpy().astype(np.float64)
+        assert np.isfinite(X).all()
+        assert l2rel(X, Xb) < 1e-6
+        for l in range(len(FN2)):
+            rows, cols = layer_rows(info, l)
+            if len(rows):
+                assert l2rel(X[:, cols], Xo[:, woff[l] + rows]) < 1e-6, (W, r, l)

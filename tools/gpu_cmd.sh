@@ -1,7 +1,4 @@
 set -o pipefail
-timeout -k 10 120 python -u tools/ks_stamps.py 8 0 1024 > gpurun_out/ks.log 2>&1 && cat gpurun_out/ks.log &&
-timeout -k 10 120 python -u tools/ks_stamps.py 8 0 1024 256 > gpurun_out/ks256.log 2>&1 && head -n 9 gpurun_out/ks256.log &&
-timeout -k 10 120 python -u tools/ks_stamps.py 1 0 1024 > gpurun_out/ks1.log 2>&1 && cat gpurun_out/ks1.log &&
-timeout -k 10 120 python -u tools/net_stamps.py c3 0 1 0 > gpurun_out/ns1.log 2>&1 && cat gpurun_out/ns1.log &&
-timeout -k 10 120 python -u tools/net_stamps.py c3 0 8 0 > gpurun_out/ns8.log 2>&1 && cat gpurun_out/ns8.log &&
-timeout -k 10 120 python -u tools/net_stamps.py c4 0 8 0 > gpurun_out/ns8c4.log 2>&1 && cat gpurun_out/ns8c4.log
+timeout -k 10 400 python -u -m pytest tests/test_hip_kstream.py tests/test_hip_fullsize.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tk.log 2>&1; rc=$?; tail -n 3 gpurun_out/tk.log; [ $rc = 0 ] &&
+timeout -k 10 120 python -u tools/ks_stamps.py 8 0 1024 > gpurun_out/ks.log 2>&1 && tail -n 8 gpurun_out/ks.log &&
+timeout -k 10 120 python -u tools/ks_stamps.py 1 0 1024 > gpurun_out/ks1.log 2>&1 && tail -n 8 gpurun_out/ks1.log

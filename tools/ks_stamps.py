@@ -89,9 +89,18 @@ def main():
     torch.cuda.synchronize()
     lib.psvi_debug_set_ptr(7, None)
     t = st.view(maxblk, 16).cpu()
+    print(f"sample {us:.1f} us/launch (kernel + reduce)")
+    if bool((t[:, 12] != 0).any()):  # the segmented kernel
+        nblk = int((t[:, 12] != 0).nonzero().max()) + 1
+        t = t[:nblk].double()
+        print(f"  segmented: {nblk} workgroups, stages/wg mean {float(t[:, 6].mean()):.2f} max {float(t[:, 6].max()):.0f}")
+        timeline(t[:, 13], t[:, 14])
+        for k, nm in ((1, "first stage"), (2, "stages+mfma"), (3, "slot write")):
+            print(f"  {nm:11s} {q(t[:, k])}")
+        print(f"  {'total':11s} {q(t[:, 12] - t[:, 0])}")
+        return
     nblk = int((t[:, 3] != 0).nonzero().max()) + 1
     t = t[:nblk].double()
-    print(f"sample {us:.1f} us/launch (kernel + reduce), {nblk} workgroups")
     timeline(t[:, 6], t[:, 7])
     for nm, x in (("first stage", t[:, 1] - t[:, 0]), ("stages+mfma", t[:, 2] - t[:, 1]),
                   ("slot write", t[:, 3] - t[:, 2]), ("total", t[:, 3] - t[:, 0])):
