@@ -154,14 +154,18 @@ struct TileOps {
 #pragma unroll
         for (int c = 0; c < NQ; ++c) b[c] = ld(pb + 16 * c * (BCONT ? ldb : 1), ldb, BCONT);
     }
+    // k-step outer, column tile inner: consecutive MFMAs write different
+    // accumulators (the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32
+    // hides behind the other tiles' 32-cycle issues instead of stalling a chain)
     __device__ __forceinline__ void mma(floatx4 (&acc)[NQ]) const {
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[c].z, acc[c], 0, 0, 0);
-            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[c].w, acc[c], 0, 0, 0);
-        }
+        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[c], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[c], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[c].z, acc[c], 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[c].w, acc[c], 0, 0, 0);
     }
 };
 
@@ -211,20 +215,27 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
         // copies at the back edge, so the reads of the group after next stay
         // in flight across the current group's MFMAs), then a 1- or 2-group tail
         int kg = 0;
+        // the next group's LDS reads stay ahead of this group's MFMAs
+        // (sched_barrier: the scheduler otherwise sinks them next to their use)
         for (; kg + 2 < nk; kg += 2) {
             pa += da;
             pb += db;
             x1.load(pa, lda, pb, ldb);
+            __builtin_amdgcn_sched_barrier(0);
             x0.mma(acc);
+            __builtin_amdgcn_sched_barrier(0);
             pa += da;
             pb += db;
             x0.load(pa, lda, pb, ldb);
+            __builtin_amdgcn_sched_barrier(0);
             x1.mma(acc);
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (kg + 1 < nk) {
             pa += da;
             pb += db;
             x1.load(pa, lda, pb, ldb);
+            __builtin_amdgcn_sched_barrier(0);
             x0.mma(acc);
             x1.mma(acc);
         } else {
@@ -331,14 +342,11 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     if (FAM == PSVI_FAMILY_FULLCOV && MSRC) {
         // uniform loops: a per-lane index into the by-value kernel arguments
         // would make the compiler copy the whole argument block to scratch
-        int64_t* boff = reinterpret_cast<int64_t*>(srct);
-        int64_t* xb = boff + a.nbands;
+        // (the band table -- global loads -- is filled after the load phase: a
+        // global load here would hold the x loads behind its latency)
+        int64_t* xb = reinterpret_cast<int64_t*>(srct) + a.nbands;
         int* xs0 = srct + 2 * a.nbands + 2 * kMaxWorld;
         int* bb = xs0 + kMaxWorld;
-        for (int i = tid; i < a.nbands; i += blockDim.x) {
-            const NetBand bd = a.bands[i];
-            boff[i] = bd.base + (int64_t)s * bd.stride;
-        }
         for (int p = 0; p < nsrc; ++p)
             if (tid == 0) {  // the stage: source p's block at stage_off[p]
                 xs0[p] = a.stage_off[p];
@@ -357,6 +365,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         }
         __syncthreads();
     }
+    NET_STAMP(4, __builtin_amdgcn_s_memtime());
     // Every global load of the phase is issued before its first LDS store:
     // the u chunk (float4 per lane when rows are float4-sized), the labels and
     // weights, and (full-cov) this sample's x row -- the source ranks' blocks
@@ -644,6 +653,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             }
         }
     }
+    NET_STAMP(5, __builtin_amdgcn_s_memtime());
+    if (FAM == PSVI_FAMILY_FULLCOV && MSRC) {
+        // every band's g_send offset for this sample (section 3's fc_addr)
+        int64_t* boff = reinterpret_cast<int64_t*>(srct);
+        for (int i = tid; i < a.nbands; i += blockDim.x) {
+            const NetBand bd = a.bands[i];
+            boff[i] = bd.base + (int64_t)s * bd.stride;
+        }
+    }
     if (a.stamps && (tid & 63) == 0) stl[16 + wave_id()] = wstart;
     __syncthreads();  // the LDS stores
     NET_STAMP(1, __builtin_amdgcn_s_memtime());
@@ -684,6 +702,8 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     auto gld = [&](int l) __attribute__((always_inline)) { return l == L - 1 ? a.lddl : a.ldx[l + 1]; };
     for (int pt = wave_id(); 16 * pt < Mp; pt += nwv) {  // wave-uniform
         const int r0 = 16 * pt;
+        // diagnostics (abl & 64): the first tile's forward twice (its stamps record the second)
+        for (int rep = 0; rep < (((a.abl & 64) && pt == wave_id()) ? 2 : 1); ++rep)
         for (int l = 0; l < L && !(a.abl & 2); ++l) {
             const int din = a.din[l], dout = a.dout[l];
             const bool head = l == L - 1;
@@ -726,6 +746,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 row_gemm<true, true>(dout, din, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
             }
             drain();
+            if (pt == 0 && l < 3) NET_STAMP(6 + l, __builtin_amdgcn_s_memtime());
         }
         // ---- loss head on VALU (C > 16, the outer objective): lanes 0..15
         // take the tile's rows, logits -> weighted NLL, dlogits in place
@@ -756,6 +777,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             }
         }
         drain();
+        if (pt == 0) NET_STAMP(9, __builtin_amdgcn_s_memtime());
         if (!bwd) continue;
         // ---- backward propagation down to the lowest owned layer
         for (int l = L - 1; l > own_lo; --l) {
@@ -781,6 +803,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 row_gemm<true, false>(din, dout, G, gld(l), sm + a.lw[l], a.ldw[l], epi);
             drain();
         }
+        if (pt == 0) NET_STAMP(10, __builtin_amdgcn_s_memtime());
         if (dx0) {
             // du[s][m][i] = sum_j G_0[m][j] W_0[j][i] for the tile's pseudopoint rows
             const int din = a.din[0], dout = a.dout[0];

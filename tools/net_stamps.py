@@ -15,6 +15,7 @@ import torch  # noqa: E402
 from psvi.runtime import InnerLoopPlan  # noqa: E402
 
 CFG = {"c3": ([(64, 40), (40, 40), (40, 2)], 128, 100),
+       "s512": ([(64, 40), (40, 40), (40, 2)], 512, 100),
        "c4": ([(64, 40), (40, 40), (40, 2)], 1024, 200)}
 
 
@@ -36,7 +37,24 @@ def report(name, t, abl, S):
             print(f"  {nm:12s} {float((cur - prev).median()):10.0f}")
             prev = cur
         print(f"  total        {float(d[:, 12].median()):10.0f}  (max {float(d[:, 12].max()):.0f})")
+        # wave 0's finer marks: 4 setup done, 5 load loop done (its own loads
+        # landed and stored), 1 barrier; 6/7/8 forward layers of tile 0, 9 loss
+        # head, 10 backward propagation, 2 barrier
+        for k, nm in ((4, "setup"), (5, "load loop"), (1, "load barrier"), (6, "fwd l0"), (7, "fwd l1"),
+                      (8, "fwd l2"), (9, "head"), (10, "bwd"), (2, "chain barrier")):
+            print(f"    wave0 @ {nm:13s} {float(d[:, k].median()):8.0f}")
+        sk = (r[:, 15].double() - r[:, 0].double())
+        print(f"  wave launch skew (last wave start - workgroup start) median {float(sk.median()):.0f} max {float(sk.max()):.0f}")
         timeline(r, 13, 14)
+        # workgroups that started late (a second round on their CU): warm caches
+        st = r[:, 13].double()
+        late = st > st.min() + 0.5 * (st.max() - st.min())
+        if 0 < int(late.sum()) < r.shape[0]:
+            for nm, msk in (("early", ~late), ("late", late)):
+                dd = d[msk]
+                print(f"  {nm:5s} starters ({int(msk.sum())}): loads {float(dd[:, 1].median()):.0f}"
+                      f" fwd l0 {float((dd[:, 6] - dd[:, 1]).median()):.0f} fwd l1 {float((dd[:, 7] - dd[:, 6]).median()):.0f}"
+                      f" fwd l2 {float((dd[:, 8] - dd[:, 7]).median()):.0f} total {float(dd[:, 12].median()):.0f}")
 
 
 def timeline(t, c0, c1):

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(512) void probe(float* out, unsigned long long* tic
             }
         } else if (MODE == 4 || MODE == 5) {
             // the network kernel's own GEMM driver (MODE 5: without its epilogue stores)
-            auto epi = [&](int m, int j, floatx4 v) {
+            auto epi = [&](int m, int j, floatx4 v, int) {
                 if (MODE == 4 && j < 48) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) C[(m + q) * 52 + j] = fmaxf(v[q] + B[j], 0.f);
