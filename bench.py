@@ -673,12 +673,13 @@ def run(rt, args, shapes=None):
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
     else:
         # dominant phase: the update (K-split streaming kernel at K = S) and
-        # the next step's sample on this rank's rows (mvn_fwd + its reduce)
+        # the next step's sample on this rank's rows (the segmented sample
+        # kernel + its (row block, pass) reduce)
         work = algorithmic_work(S, rows_fraction(loop, sh["layers"]), sh["layers"])
         wk = dict(bytes=work["update"]["bytes"] + work["sample"]["bytes"],
                   flops=work["update"]["flops"] + work["sample"]["flops"])
         upd_s = max(avg_ms["update+sample"], 1e-9) * 1e-3
-        kname = "mvn_kstream_kernel + mvn_fwd_kernel + reduce (update + next-step sample)"
+        kname = "mvn_kstream_kernel + mvn_fwd_seg_kernel + reduce (update + next-step sample)"
         kernels = {kname: dict(avg_us=avg_ms["update+sample"] * 1e3,
                                gbs=wk["bytes"] / upd_s / 1e9, tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel(+exchange)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}

@@ -109,7 +109,7 @@ def test_bench_multi_rank_control_flow(world):
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert line["config"]["comm"].startswith("gloo")
     ks = line["roofline"]["kernels"]
-    assert set(ks) == {"mvn_kstream_kernel + mvn_fwd_kernel + reduce (update + next-step sample)",
+    assert set(ks) == {"mvn_kstream_kernel + mvn_fwd_seg_kernel + reduce (update + next-step sample)",
                        "net_kernel(+exchange)"}
     assert all(d["avg_us"] > 0 for d in ks.values())   # the sampled per-phase events
     c4 = line["c4"]
