@@ -62,8 +62,8 @@ and alpha through ``psvi_hvp``'s mixed products.  Soft labels (``learn_z``:
 expanded (row, class) rows, z through the softmax over rows) and
 ``nested_step(truncated=True)`` are built (fixtures w01-w05); ``hyper_step``
 with ``learn_z`` raises NotImplementedError as the reference does
-(psvi_classes.py:619-620), and so does ``learn_z`` with samples sharded over
-ranks (world > 1).
+(psvi_classes.py:619-620).  With samples sharded over ranks (world > 1) the
+soft-label outer objective runs on ``ShardedOuter`` (``HipOuterRowsELBO``).
 
 There is no CPU fallback: a missing libpsvi_hip.so or GPU raises.
 """
@@ -180,18 +180,31 @@ class HipOuterRowsELBO(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pvec, u_rows, w_rows, plan, x_all, z_all, eps, n_pseudo):
-        from ..runtime.sharded import pack_coef
+        from ..runtime.sharded import ShardedOuter, pack_coef
 
         p = pvec.detach().to(torch.float32).contiguous()
         w = w_rows.detach().to(torch.float32).contiguous()
-        out = plan.outer_elbo_grad(n_pseudo, x_all, z_all, w, eps, p, grad=True,
-                                   grad_u=n_pseudo > 0, grad_w=True, sample_stats=True)
-        R, S = x_all.shape[0], out["samples"].shape[0]
-        W = out["samples"][:, 3].cpu()
-        zero = torch.zeros(S, dtype=torch.float64)
-        gd = plan.outer_grad_coef(R, x_all, z_all, w, eps, p,
-                                  pack_coef(W, zero, zero, 0, S).to(p.device),
-                                  grad_u=False, grad_w=True)["grad_w"][n_pseudo:]
+        R = x_all.shape[0]
+        if isinstance(plan, ShardedOuter):
+            # samples split over ranks: pass 1 + the all-reduced coefficients
+            # give the loss, the gradients and every sample's W_s; the data
+            # rows' weight gradients sum_s W_s NLL_s,row are one more coefficient
+            # pass over this rank's samples, all-reduced
+            out = plan.elbo_grad(n_pseudo, x_all, z_all, w, eps, p, grad_u=n_pseudo > 0,
+                                 grad_w=True, sample_weights=True)
+            W = out["W"]
+            zero = torch.zeros_like(W)
+            gd = plan.coef_grads(R, x_all, z_all, w, eps, p, W, zero, zero, grad_u=False,
+                                 grad_w=True)["grad_w"][n_pseudo:]
+        else:
+            out = plan.outer_elbo_grad(n_pseudo, x_all, z_all, w, eps, p, grad=True,
+                                       grad_u=n_pseudo > 0, grad_w=True, sample_stats=True)
+            S = out["samples"].shape[0]
+            W = out["samples"][:, 3].cpu()
+            zero = torch.zeros(S, dtype=torch.float64)
+            gd = plan.outer_grad_coef(R, x_all, z_all, w, eps, p,
+                                      pack_coef(W, zero, zero, 0, S).to(p.device),
+                                      grad_u=False, grad_w=True)["grad_w"][n_pseudo:]
         gu = out["grad_u"] if n_pseudo > 0 else torch.zeros_like(x_all[:0])
         ctx.save_for_backward(out["grad"], gu, torch.cat([out["grad_w"], gd]))
         ctx.meta = (pvec.dtype, u_rows.shape, u_rows.dtype, w_rows.dtype)
@@ -632,8 +645,6 @@ class PSVI:
         (r, c) with weight w_r Q_rc; the entropy terms shift every sample's
         pseudo term by one constant (no effect on the loss) and its data term
         by cd = N / Nx sum_x sum_c Q_xc log Q_xc, added here."""
-        if self.world > 1:
-            raise NotImplementedError("learn_z with samples split over ranks")
         C = layers[-1][1]
         Mu = int(self.u.shape[0])
         R0 = Mu + Nx

@@ -66,8 +66,13 @@ class TorchDistComm:
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
     def all_reduce(self, t):
+        # a strided view (e.g. one output of a plan's fused result) is reduced
+        # through a contiguous copy and written back in place
         if not t.is_contiguous():
-            raise ValueError("all_reduce: contiguous buffer expected")
+            c = t.contiguous()
+            self.dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+            return
         self.dist.all_reduce(t, group=self.group)
 
 
@@ -386,22 +391,26 @@ class ShardedOuter:
                                          grad_u=grad_u, grad_w=grad_w)
 
     def elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad_u=True, grad_w=True,
-                  grads=True):
+                  grads=True, sample_weights=False):
         """Loss (float64 tensor) and the full gradients on every rank
-        (grads=False: the loss only, pass 1 and one all-reduce)."""
+        (grads=False: the loss only, pass 1 and one all-reduce).
+        sample_weights: also "W", the softmax weights W_s of all S samples
+        (float64; sample_out's fourth column of a world-1 plan)."""
         e, t = self.local_terms(n_pseudo, x_all, z_all, w_all, eps, params)
         terms = torch.zeros(self.S, 3, dtype=torch.float64, device=t.device)
         terms[self.s_off:self.s_off + self.s_cnt] = t
         self.comm.all_reduce(terms)
         loss, cp, cd, ck = outer_coefficients(terms)
         if not grads:
-            return {"loss": loss.reshape(1)}
+            return {"loss": loss.reshape(1)} | ({"W": cd} if sample_weights else {})
         g = self.local_grads(n_pseudo, x_all, z_all, w_all, e, params, cp, cd, ck,
                              grad_u=grad_u, grad_w=grad_w)
         for k in ("grad", "grad_u", "grad_w"):
             if k in g:
                 self.comm.all_reduce(g[k])
         g["loss"] = loss.reshape(1)
+        if sample_weights:
+            g["W"] = cd
         return g
 
     def coef_grads(self, n_pseudo, x_all, z_all, w_all, eps, params, cp, cd, ck, grad_u=True,

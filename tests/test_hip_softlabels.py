@@ -21,7 +21,7 @@ from golden_util import fixture_names, l2rel, load_fixture, rel
 pytestmark = pytest.mark.gpu
 
 
-def _setup(f):
+def _setup(f, world=1, rank=0, comm=None):
     import psvi.inference as I
     from test_host_api import build_model
 
@@ -32,7 +32,8 @@ def _setup(f):
     z = torch.tensor(f["z0"], device=dev)
     ps = getattr(I, cfg["cls"])(u=u, z=z, N=cfg["N"], model=model, mc_samples=cfg["S"],
                                 device_id=0, inner_it=cfg["T"], learn_z=cfg["learn_z"],
-                                lr0alpha=cfg["lr0alpha"], nc=cfg["C"])
+                                lr0alpha=cfg["lr0alpha"], nc=cfg["C"], world=world, rank=rank,
+                                comm=comm)
     ps.device = dev
     ps.register_elbos = False
     ps.v = torch.tensor(f["v0"], device=dev).requires_grad_(True)
@@ -87,3 +88,45 @@ def test_softlabels_and_truncated_match_reference(name):
         big = np.abs(g) > 4 * np.abs(f["z_grad_fp32"] - g) + 1e-2 * np.abs(g).max()
         dz = np.abs(ps.z.detach().cpu().numpy() - f["z"])[big]
         assert dz.max() < 1e-3 * cfg["lr0z"] + 1e-6
+
+
+@pytest.mark.parametrize("name,world", [("w04_learnz_psvi_elbo_fn2", 2), ("w04_learnz_psvi_elbo_fn2", 3),
+                                        ("w01_learnz_nested_fn", 2)])
+def test_softlabels_samples_sharded_match_reference(name, world):
+    """learn_z with the samples split over ranks (ranks as threads of one
+    process, all_reduce through a barrier): the soft-label outer objective on
+    ShardedOuter (psvi_classes.py:445-486) -- loss and gradients into z, u, v
+    and the parameters -- and the nested step that differentiates it, on
+    every rank against the reference's own run."""
+    from test_hip_sharded_trainer import _run_ranks
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+
+    def rank_fn(r, comm):
+        ps, model = _setup(f, world, r, comm)
+        xb = torch.tensor(f["xb"], device="cuda")
+        yb = torch.tensor(f["yb"], device="cuda")
+        if cfg["trainer"] == "psvi_elbo":
+            loss = ps.psvi_elbo(xb, yb)
+            loss.backward()
+        else:
+            loss = ps.nested_step(xb, yb, K=cfg["K"])
+        out = dict(loss=loss.item(),
+                   params=torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy())
+        if "grad_params" in f:
+            out["grad_params"] = torch.cat([q.grad.reshape(-1) for q in model.parameters()]).cpu().numpy()
+        for key, t in (("u_grad", ps.u), ("v_grad", ps.v), ("z_grad", ps.z)):
+            if key in f:
+                out[key] = t.grad.detach().cpu().numpy().reshape(f[key].shape)
+        return out
+
+    for g in _run_ranks(world, rank_fn):
+        assert rel(g["loss"], float(f["out"])) < 1e-5, (g["loss"], float(f["out"]))
+        assert l2rel(g["params"], f["params"]) < 1e-5
+        if "grad_params" in g:
+            assert l2rel(g["grad_params"], f["grad_params"]) < 1e-4
+        for key in ("u_grad", "v_grad", "z_grad"):
+            if key in g:
+                own = l2rel(f[key + "_fp32"], f[key]) if key + "_fp32" in f else 0.0
+                assert l2rel(g[key], f[key]) < max(1e-4, 4 * own), (name, key, l2rel(g[key], f[key]))
