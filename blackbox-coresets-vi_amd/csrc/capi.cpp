@@ -551,10 +551,10 @@ int build_plan(psvi_plan& p) {
             p.n_sslots = ns;
         }
         p.upd_tiles = tiles;
-        if (S > kKsPass) {
-        build_kstream(p);
+        if (S > kKsPass) build_kstream(p);
+        // the segmented sample at every S (x_0 of a loop, the HVP's tangent
+        // sample, the sharded step): equal runs over 512 workgroups
         build_fseg(p);
-    }
         p.n_fwd = (int)fwd.size();
         p.n_upd = (int)p.h_upd.size();
         const size_t xs = sizeof(float) * (size_t)S * p.rows_tot[r];

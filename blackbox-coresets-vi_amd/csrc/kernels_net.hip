@@ -154,18 +154,14 @@ struct TileOps {
 #pragma unroll
         for (int c = 0; c < NQ; ++c) b[c] = ld(pb + 16 * c * (BCONT ? ldb : 1), ldb, BCONT);
     }
-    // k-step outer, column tile inner: consecutive MFMAs write different
-    // accumulators (the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32
-    // hides behind the other tiles' 32-cycle issues instead of stalling a chain)
     __device__ __forceinline__ void mma(floatx4 (&acc)[NQ]) const {
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[c], 0, 0, 0);
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[c], 0, 0, 0);
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[c].z, acc[c], 0, 0, 0);
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[c].w, acc[c], 0, 0, 0);
+        for (int c = 0; c < NQ; ++c) {
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[c].z, acc[c], 0, 0, 0);
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[c].w, acc[c], 0, 0, 0);
+        }
     }
 };
 
@@ -215,27 +211,20 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
         // copies at the back edge, so the reads of the group after next stay
         // in flight across the current group's MFMAs), then a 1- or 2-group tail
         int kg = 0;
-        // the next group's LDS reads stay ahead of this group's MFMAs
-        // (sched_barrier: the scheduler otherwise sinks them next to their use)
         for (; kg + 2 < nk; kg += 2) {
             pa += da;
             pb += db;
             x1.load(pa, lda, pb, ldb);
-            __builtin_amdgcn_sched_barrier(0);
             x0.mma(acc);
-            __builtin_amdgcn_sched_barrier(0);
             pa += da;
             pb += db;
             x0.load(pa, lda, pb, ldb);
-            __builtin_amdgcn_sched_barrier(0);
             x1.mma(acc);
-            __builtin_amdgcn_sched_barrier(0);
         }
         if (kg + 1 < nk) {
             pa += da;
             pb += db;
             x1.load(pa, lda, pb, ldb);
-            __builtin_amdgcn_sched_barrier(0);
             x0.mma(acc);
             x1.mma(acc);
         } else {

@@ -1,3 +1,3 @@
-timeout -k 10 400 python -u -m pytest tests/test_hip_stream.py tests/test_hip_parity.py tests/test_hip_fullsize.py tests/test_hip_net_lds.py tests/test_hip_kstream.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tk.log 2>&1; rc=$?; tail -n 3 gpurun_out/tk.log; [ $rc = 0 ] &&
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-trainers --no-lenet --no-c2 > gpurun_out/bench.json 2> gpurun_out/bench.err && python -c "
-import json;d=json.loads(open('gpurun_out/bench.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']['kernels'],d.get('c4_1gpu'))"
+T2="tests/test_hip_fullsize.py -q --timeout 180 --timeout-method thread"
+timeout -k 10 300 python -u -m pytest tests/test_hip_softlabels.py -k "not sharded" $T2 > gpurun_out/ta.log 2>&1; echo "softlabels(non-thread)+fullsize rc=$?"; grep -E "passed|failed|^FAILED" gpurun_out/ta.log | tail -6
+ROUND=r04 bash tools/round_session.sh
