@@ -312,6 +312,12 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int L = a.L, Mp = a.Mp;
     const int tid = threadIdx.x;
     unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
+    if (a.abl & 128) {
+        // diagnostics: poison the whole LDS with NaN first -- every word the
+        // kernel reads must have been written by it (the padding contract)
+        for (int i = threadIdx.x; i < 4 * a.lds_f4; i += blockDim.x) sm[i] = __builtin_nanf("");
+        __syncthreads();
+    }
     if (a.stamps && threadIdx.x < 16) stl[threadIdx.x] = 0;
     NET_STAMP(0, __builtin_amdgcn_s_memtime());
     // diagnostics: each wave's start, for the launch skew in slot 15
