@@ -154,6 +154,17 @@ struct TileOps {
 #pragma unroll
         for (int c = 0; c < NQ; ++c) b[c] = ld(pb + 16 * c * (BCONT ? ldb : 1), ldb, BCONT);
     }
+    // A's k >= K read as 0 (the last k-group of a row GEMM whose K is not a
+    // 16-multiple: a k-contiguous A row runs past its end into the next row,
+    // which another wave of the row chain may not have written yet -- LDS
+    // left by an earlier kernel, possibly NaN, against zero weights)
+    __device__ __forceinline__ void mask_a(int kb, int K) {
+        const int k0 = kb + 4 * (int)((threadIdx.x & 63) >> 4);
+        a.x = k0 < K ? a.x : 0.f;
+        a.y = k0 + 1 < K ? a.y : 0.f;
+        a.z = k0 + 2 < K ? a.z : 0.f;
+        a.w = k0 + 3 < K ? a.w : 0.f;
+    }
     __device__ __forceinline__ void mma(floatx4 (&acc)[NQ]) const {
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
@@ -183,7 +194,11 @@ __device__ __forceinline__ int gemm_units(int P, int Q) {
 }
 template <bool ACONT, bool BCONT, int NQ, class Epi>
 __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, const float* A, int lda,
-                                           const float* B, int ldb, Epi epi, int ustep = 0) {
+                                           const float* B, int ldb, Epi epi, int ustep = 0,
+                                           int K = 0) {
+    // K (row GEMMs, k-contiguous A): the true contraction length, masked in
+    // the last k-group; 0 = K16 (no mask)
+    const bool kmask = ACONT && K > 0 && K < K16;  // uniform
     const int nwv = ustep ? ustep : (int)(blockDim.x >> 6), lane = threadIdx.x & 63, i16 = lane & 15,
               k4 = lane >> 4;
     const int nk = K16 >> 4;
@@ -226,8 +241,10 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
             pb += db;
             x1.load(pa, lda, pb, ldb);
             x0.mma(acc);
+            if (kmask) x1.mask_a(16 * (nk - 1), K);
             x1.mma(acc);
         } else {
+            if (kmask) x0.mask_a(16 * (nk - 1), K);
             x0.mma(acc);
         }
         const int pe = p0, qe = q0;
@@ -267,9 +284,9 @@ __device__ __forceinline__ void row_gemm(int Q, int K, const float* A, int lda, 
                                          Epi epi) {
     const int tq = (Q + 15) >> 4, K16 = (K + 15) & ~15;
     switch (tq) {
-        case 3: gemm_steps<ACONT, BCONT, 3>(1, 1, K16, 0, A, lda, B, ldb, epi, 1); break;
-        case 2: gemm_steps<ACONT, BCONT, 2>(1, 1, K16, 0, A, lda, B, ldb, epi, 1); break;
-        default: gemm_steps<ACONT, BCONT, 1>(tq, tq, K16, 0, A, lda, B, ldb, epi, 1); break;
+        case 3: gemm_steps<ACONT, BCONT, 3>(1, 1, K16, 0, A, lda, B, ldb, epi, 1, K); break;
+        case 2: gemm_steps<ACONT, BCONT, 2>(1, 1, K16, 0, A, lda, B, ldb, epi, 1, K); break;
+        default: gemm_steps<ACONT, BCONT, 1>(tq, tq, K16, 0, A, lda, B, ldb, epi, 1, K); break;
     }
 }
 
@@ -313,9 +330,19 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int tid = threadIdx.x;
     unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
     if (a.abl & 128) {
-        // diagnostics: poison the whole LDS with NaN first -- every word the
-        // kernel reads must have been written by it (the padding contract)
-        for (int i = threadIdx.x; i < 4 * a.lds_f4; i += blockDim.x) sm[i] = __builtin_nanf("");
+        // diagnostics: poison the LDS with NaN first -- every word the kernel
+        // reads must have been written by it (the padding contract).  abl >> 8
+        // picks one region (0: all; 1 weights, 2 X_0, 3 red / zw / stamps /
+        // tables, 4 X_l (l >= 1), 5 G_l, 6 dlogits and the rest)
+        const int reg = a.abl >> 8;
+        int lo = 0, hi = 4 * a.lds_f4;
+        if (reg == 1) { lo = 0; hi = a.lx[0]; }
+        else if (reg == 2) { lo = a.lx[0]; hi = a.lred; }
+        else if (reg == 3) { lo = a.lred; hi = a.L > 1 ? a.lx[1] : a.ldl; }
+        else if (reg == 4) { lo = a.L > 1 ? a.lx[1] : a.ldl; hi = a.L > 1 ? a.lg[0] : a.ldl; }
+        else if (reg == 5) { lo = a.L > 1 ? a.lg[0] : a.ldl; hi = a.ldl; }
+        else if (reg == 6) { lo = a.ldl; }
+        for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) sm[i] = __builtin_nanf("");
         __syncthreads();
     }
     if (a.stamps && threadIdx.x < 16) stl[threadIdx.x] = 0;

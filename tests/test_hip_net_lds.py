@@ -71,3 +71,52 @@ def test_meanfield_net_ignores_stale_lds(layers, S, M):
     assert np.isfinite(outs[0]).all()
     for a in outs[1:]:  # per-(sample, chunk) slots summed in a fixed order: bitwise
         assert np.array_equal(a, outs[0])
+
+
+@pytest.mark.parametrize("fam,layers,S,M", [
+    ("fullcov", [(64, 40), (40, 40), (40, 2)], 128, 100),
+    ("fullcov", [(64, 40), (40, 40), (40, 2)], 1024, 200),
+    ("fullcov", [(9, 5), (5, 3)], 130, 129),
+    ("meanfield", [(7, 33), (33, 5), (5, 3)], 130, 129),
+    ("meanfield", [(7, 33), (33, 5), (5, 3)], 256, 129),
+    ("meanfield", [(64, 64), (64, 10)], 16, 200)])
+def test_net_reads_only_lds_it_wrote(fam, layers, S, M):
+    """The network kernel with its whole LDS poisoned with NaN before use
+    (diagnostics ablation bit 128) gives the same ELBO and gradient bit for
+    bit: no word is read before the kernel writes it -- in particular the
+    row chain's k-loops that run past a row's end into rows another wave owns
+    (masked to zero in the last k-group).  LDS keeps whatever an earlier
+    kernel left there, NaN included."""
+    import torch
+
+    from psvi.runtime import InnerLoopPlan
+
+    g = torch.Generator().manual_seed(S + M)
+    plan = InnerLoopPlan(fam, layers, S, M)
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        if fam == "meanfield":
+            parts += [0.3 * torch.randn(n, generator=g), -4 + 3 * torch.rand(n, generator=g)]
+        else:
+            parts += [0.1 * torch.randn(n, generator=g), -5 + 2 * torch.rand(n, generator=g),
+                      (0.15 / n ** 0.5) * torch.randn((n - 1) * (n - 2) // 2, generator=g)]
+    p = torch.cat(parts).cuda()
+    u = torch.randn(M, layers[0][0], generator=g).cuda()
+    z = torch.randint(0, layers[-1][1], (M,), generator=g).to(torch.int32).cuda()
+    w = torch.full((M,), 3.0).cuda()
+    eps = torch.randn(plan.eps_count, generator=g).cuda()
+    out = []
+    for abl in (0, 128, 0):
+        plan.lib.psvi_debug_set(1, abl)
+        try:
+            e, gr = plan.elbo_grad(u, z, w, eps, p)
+            torch.cuda.synchronize()
+        finally:
+            plan.lib.psvi_debug_set(1, 0)
+        out.append((e.item(), gr.cpu()))
+    for e, gr in out:
+        assert e == e and torch.isfinite(gr).all()
+        # the ELBO's fp64 partials are added with atomics in arrival order
+        assert abs(e - out[0][0]) <= 1e-12 * abs(out[0][0])
+        assert torch.equal(gr, out[0][1])
