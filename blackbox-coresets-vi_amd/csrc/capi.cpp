@@ -1044,6 +1044,22 @@ int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, con
     return 0;
 }
 
+int psvi_mvn_phase_net_draw(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                            const float* x_recv, float* g_send, double* nll_out, float* eps_out,
+                            int64_t n, uint64_t seed, uint64_t offset, void* stream) {
+    if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    if (!u || !z || !w || !x_recv || !g_send || !nll_out || !eps_out || n < 0)
+        return fail(PSVI_EINVAL, "null pointer or bad count");
+    if (offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");
+    if (reinterpret_cast<uintptr_t>(eps_out) % 16)
+        return fail(PSVI_EINVAL, "eps_out must be 16-byte aligned");
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x_recv, g_send, nll_out, st, eps_out, n,
+                       seed, offset));
+    return 0;
+}
+
 int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_shard,
                           float* params, float* adam_m, float* adam_v, const psvi_adam_hp* hp,
                           double* kl_out, float* grad_out, int32_t include_kl, void* stream) {

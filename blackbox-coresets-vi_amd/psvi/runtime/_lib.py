@@ -78,6 +78,7 @@ SIGNATURES = {
                                     _P]),
     "psvi_mvn_phase_sample": (_I32, [_P, _P, _P, _P, _P]),
     "psvi_mvn_phase_net": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "psvi_mvn_phase_net_draw": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _U64, _U64, _P]),
     "psvi_mvn_phase_update": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P,
                                      _I32, _P]),
     "psvi_mvn_phase_update_sample": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P,

@@ -395,16 +395,26 @@ class InnerLoopPlan:
             _ptr(tstate), ctypes.byref(hp), _ptr(kl_out), int(bool(include_kl)), _ptr(eps_next),
             _ptr(x_next), _stream()), "psvi_mvn_phase_update_tiled")
 
-    def mvn_net(self, u, z, w, x_recv, g_send, nll_out):
+    def mvn_net(self, u, z, w, x_recv, g_send, nll_out, draw=None):
+        """draw = (eps_out, seed, offset): the next step's global eps drawn in the
+        same launch (psvi_mvn_phase_net_draw; psvi_randn's values)."""
         _need(u, "u", self.M * self.in_features)
         _need(z, "z", self.M, torch.int32)
         _need(w, "w", self.M)
         _need(x_recv, "x_recv", self.xrecv_count)
         _need(g_send, "g_send", self.xrecv_count)
         _need(nll_out, "nll_out", 1, torch.float64)
-        check(self.lib.psvi_mvn_phase_net(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv),
-                                          _ptr(g_send), _ptr(nll_out), _stream()),
-              "psvi_mvn_phase_net")
+        if draw is None:
+            check(self.lib.psvi_mvn_phase_net(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv),
+                                              _ptr(g_send), _ptr(nll_out), _stream()),
+                  "psvi_mvn_phase_net")
+            return
+        out, seed, offset = draw
+        _need(out, "eps_out", out.numel())
+        check(self.lib.psvi_mvn_phase_net_draw(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv),
+                                               _ptr(g_send), _ptr(nll_out), _ptr(out), out.numel(),
+                                               int(seed), int(offset), _stream()),
+              "psvi_mvn_phase_net_draw")
 
     def mvn_update(self, eps, g_shard, params, adam_m=None, adam_v=None, step=1, lr=1e-3,
                    kind="higher", kl_out=None, grad_out=None, include_kl=True, eps_next=None,

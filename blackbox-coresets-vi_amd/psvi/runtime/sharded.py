@@ -143,9 +143,14 @@ class ShardedInnerLoop:
     def phase_sample(self, eps, params):
         self.plan.mvn_sample(eps, params, self.x_shard)
 
-    def phase_net(self, u, z, w):
+    def phase_net(self, u, z, w, draw=None):
+        """draw = (eps_out, seed, offset): the next step's global eps drawn by
+        the same launch (psvi_mvn_phase_net_draw)."""
         self.parts.zero_()
-        self.plan.mvn_net(u, z, w, self.x_recv, self.g_send, self.parts[0:1])
+        if draw is None:
+            self.plan.mvn_net(u, z, w, self.x_recv, self.g_send, self.parts[0:1])
+        else:
+            self.plan.mvn_net(u, z, w, self.x_recv, self.g_send, self.parts[0:1], draw=draw)
 
     def phase_update(self, eps, params, m, v, step, lr, kind, grad_out=None):
         self.plan.mvn_update(eps, self.g_shard, params, m, v, step=step, lr=lr, kind=kind,
@@ -191,8 +196,8 @@ class ShardedInnerLoop:
         global layout, identical on every rank, so eps never crosses the wire).
 
         Full-cov schedule per step t (x_shard holds x_t on entry):
-          side stream:  eps_{t+1} <- Philox, behind the exchanges and the network
-          x all_to_all -> network -> G all_to_all
+          x all_to_all -> network (which also draws eps_{t+1}: Philox, split
+          over its workgroups after their gradients) -> G all_to_all
           update of t fused with the next step's sample: Adam on the rank's rows
             (K-split streaming kernel at K = S > 128), then x_{t+1} = mean' +
             L' eps_{t+1} on those rows (psvi_mvn_phase_update_sample)
@@ -217,33 +222,26 @@ class ShardedInnerLoop:
             self._eps2 = [torch.empty(self.plan.eps_count, device=dev) for _ in range(2)]
         e_cur, e_nxt = self._eps2
         cuda = e_cur.is_cuda
-        main = torch.cuda.current_stream(dev) if cuda else None
-        side = torch.cuda.Stream(dev) if cuda else None
         self.draw(e_cur, seed, offset)
         self.phase_sample(e_cur, params)
         for t in range(T):
             ev = phase_events.get(t) if phase_events else None
             last = t + 1 == T
-            if not last:
-                if cuda:
-                    # e_nxt was read by the previous update (issued on main)
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        self.draw(e_nxt, seed, offset + (t + 1) * stride)
-                    drawn = torch.cuda.Event()
-                    drawn.record(side)
-                else:
-                    self.draw(e_nxt, seed, offset + (t + 1) * stride)
+            nxt = None if last else (e_nxt, seed, offset + (t + 1) * stride)
+            if nxt is not None and not cuda:
+                self.draw(*nxt)  # host tensors: the draw on its own
             if ev: ev[0].record()
             self.comm.all_to_all(self.x_recv, self.x_shard, self.x_out, self.x_in)
-            self.phase_net(u, z, w)
+            # e_nxt was last read by the previous update, earlier on this stream
+            if cuda and nxt is not None:
+                self.phase_net(u, z, w, draw=nxt)
+            else:
+                self.phase_net(u, z, w)
             self.comm.all_to_all(self.g_shard, self.g_send, self.g_out, self.g_in)
             if ev: ev[1].record()
             if last:
                 self.phase_update(e_cur, params, m, v, step0 + t, lr, kind)
             else:
-                if cuda:
-                    main.wait_event(drawn)
                 self.phase_update_sample(e_cur, params, m, v, step0 + t, lr, kind, e_nxt)
             if ev: ev[2].record()
             if elbo_parts is not None:

@@ -219,6 +219,15 @@ int psvi_mvn_phase_sample(const psvi_plan* plan, const float* eps,
 int psvi_mvn_phase_net(const psvi_plan* plan, const float* u, const int32_t* z,
                        const float* w, const float* x_recv, float* g_send,
                        double* nll_out, void* stream);
+/* the net phase with the next step's noise drawn in the same launch (the
+ * sharded inner loop: every rank draws the whole global eps of the next step,
+ * normals [0, n) of the psvi_randn stream (seed, offset) into eps_out -- the
+ * same values psvi_randn writes -- split over the network kernel's workgroups
+ * after their gradients; no separate draw launch).  offset % 4 == 0. */
+int psvi_mvn_phase_net_draw(const psvi_plan* plan, const float* u, const int32_t* z,
+                            const float* w, const float* x_recv, float* g_send,
+                            double* nll_out, float* eps_out, int64_t n, uint64_t seed,
+                            uint64_t offset, void* stream);
 int psvi_mvn_phase_update(const psvi_plan* plan, const float* eps,
                           const float* g_shard, float* params, float* adam_m,
                           float* adam_v, const psvi_adam_hp* hp, double* kl_out,

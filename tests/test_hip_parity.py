@@ -166,6 +166,39 @@ def test_sharded_fullcov_equals_single(name, world):
     assert torch.allclose(full, p1, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("name", ["g3r_fn2_tiny_rand", "g4h_fn2_mid_hyper", "g5_logreg_fullcov"])
+def test_net_draw_equals_separate(name, world):
+    """psvi_mvn_phase_net_draw (the sharded loop's network phase with the next
+    step's eps drawn by the same launch) == psvi_mvn_phase_net + psvi_randn,
+    bitwise: gradients, NLL and every drawn normal, for every rank's plan."""
+    from psvi.runtime import randn_
+    from psvi.runtime.sharded import ShardedInnerLoop
+
+    f = load_fixture(name)
+    cfg, _, u, z, w = _setup(f)
+    for r in range(world):
+        plan = ShardedInnerLoop("fullcov", cfg["layers"], cfg["S"], cfg["M"], world, r).plan
+        g = torch.Generator().manual_seed(5 + r)
+        xs = torch.randn(plan.xrecv_count, generator=g).to(DEV)
+        n = plan.eps_count
+        for off in (0, 4 * n + 8):
+            outs = []
+            for fused in (False, True):
+                gs = torch.full((plan.xrecv_count,), float("nan"), device=DEV)
+                nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+                e = torch.full((n,), float("nan"), device=DEV)
+                if fused:
+                    plan.mvn_net(u, z, w, xs, gs, nll, draw=(e, 31, off))
+                else:
+                    plan.mvn_net(u, z, w, xs, gs, nll)
+                    randn_(e, 31, off)
+                outs.append((gs, nll, e))
+            for a, b in zip(*outs):
+                assert torch.equal(a, b), (name, world, r, off)
+            assert torch.isfinite(outs[1][2]).all()
+
+
 def test_randn_moments_and_determinism():
     from psvi.runtime import randn_
 

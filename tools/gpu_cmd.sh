@@ -1,3 +1,6 @@
-timeout -k 10 200 python -u tools/lds_poison.py > gpurun_out/lp.log 2>&1; echo "rc=$?"; cat gpurun_out/lp.log | grep -v amdgpu.ids
-T2="tests/test_hip_fullsize.py -q --timeout 180 --timeout-method thread"
-timeout -k 10 300 python -u -m pytest tests/test_hip_softlabels.py -k "not sharded" $T2 > gpurun_out/ta.log 2>&1; echo "softlabels(non-thread)+fullsize rc=$?"; grep -E "passed|failed|^FAILED" gpurun_out/ta.log | tail -6
+set -o pipefail
+export PYTHONPATH=$PWD/blackbox-coresets-vi_amd:$PWD/oracle:$PWD/tests:$PWD
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_hip_parity.py tests/test_bench_shared_gpu.py tests/test_hip_sharded_trainer.py tests/test_hip_fullsize.py > gpurun_out/t_draw.log 2>&1 && tail -3 gpurun_out/t_draw.log && \
+timeout -k 10 200 python -u tools/rank_timing.py --cfg c4 --world 8 --schedule run --iters 50 > gpurun_out/rt_run_c4.log 2>&1 && tail -1 gpurun_out/rt_run_c4.log && \
+timeout -k 10 200 python -u tools/rank_timing.py --cfg c4 --world 8 --iters 50 > gpurun_out/rt_ph_c4.log 2>&1 && tail -1 gpurun_out/rt_ph_c4.log && \
+timeout -k 10 200 python -u tools/rank_timing.py --cfg weak --world 8 --schedule run --iters 50 > gpurun_out/rt_run_weak.log 2>&1 && tail -1 gpurun_out/rt_run_weak.log

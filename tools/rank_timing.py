@@ -11,6 +11,11 @@ minus the wire.
 
   python tools/rank_timing.py --cfg c4 --world 8 [--ranks 0,3,7] [--iters 50]
   python tools/rank_timing.py --cfg weak --world 8
+  python tools/rank_timing.py --cfg c4 --world 8 --schedule run
+
+--schedule phases (default): randn, sample, net, update as separate launches;
+--schedule run: ShardedInnerLoop.run()'s steady-state step -- the network
+launch also draws the next eps, the update launch also samples the next x.
 
 cfg c4: fn2 64-40-40-2, S = 1024, M = 200 (BASELINE configs[3], strong
 scaling); cfg weak: the bench headline at N = world (S = 128 world, M = 100).
@@ -44,6 +49,7 @@ def main():
     ap.add_argument("--ranks", default="all")
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--schedule", choices=("phases", "run"), default="phases")
     a = ap.parse_args()
     from bench import LR, fn2_inputs, reference_init_params
     from psvi.runtime import randn_
@@ -82,6 +88,9 @@ def main():
         x_exchange(r)
         loops[r].phase_net(u, z, w)
     names = ["randn", "sample", "x_exchange(copy)", "net", "g_exchange(copy)", "update"]
+    if a.schedule == "run":
+        names = ["x_exchange(copy)", "net+draw", "g_exchange(copy)", "update+sample"]
+        e_nxt = torch.empty_like(eps)
     out = []
     for r in ranks:
         lp = loops[r]
@@ -90,6 +99,17 @@ def main():
         for k in range(a.warmup + a.iters):
             e = ev[k - a.warmup] if k >= a.warmup else None
             rec = (lambda i: e[i].record()) if e else (lambda i: None)
+            if a.schedule == "run":
+                rec(0)
+                x_exchange(r)
+                rec(1)
+                lp.phase_net(u, z, w, draw=(e_nxt, 11, (k + 1) * stride))
+                rec(2)
+                g_exchange(r)
+                rec(3)
+                lp.phase_update_sample(eps, params[r], ms[r], vs[r], k + 1, LR, "higher", e_nxt)
+                rec(4)
+                continue
             rec(0)
             randn_(eps, 11, (k + 1) * stride)
             rec(1)
@@ -108,7 +128,7 @@ def main():
               for i, n in enumerate(names)}
         comp = sum(v for k_, v in us.items() if "exchange" not in k_)
         info = lp.info[r]
-        row = dict(rank=r, cfg=a.cfg, world=W, S=S, M=M, s_local=info["s_count"],
+        row = dict(rank=r, cfg=a.cfg, schedule=a.schedule, world=W, S=S, M=M, s_local=info["s_count"],
                    rows=info["rows"], us={k_: round(v, 2) for k_, v in us.items()},
                    compute_us=round(comp, 2))
         print(json.dumps(row), flush=True)
