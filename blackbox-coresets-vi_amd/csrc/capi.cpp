@@ -1168,15 +1168,26 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
         return launch_randn(b, p->Peps, seed, offset + (uint64_t)t * es, st) == hipSuccess ? b
                                                                                          : nullptr;
     };
+    // eps of step 0 with the ELBO accumulators cleared: Philox mode folds the
+    // clear into the draw's launch
+    auto first_eps = [&]() -> const float* {
+        if (eps) {
+            return hipMemsetAsync(elbo_out, 0, sizeof(double) * (size_t)T, st) == hipSuccess
+                       ? eps
+                       : nullptr;
+        }
+        return launch_randn(ebuf[0], p->Peps, seed, offset, st, elbo_out, T) == hipSuccess
+                   ? ebuf[0]
+                   : nullptr;
+    };
     psvi_adam_hp h = *hp;
     if (p->family == PSVI_FAMILY_MEANFIELD) {
         // two launches per step: the network kernel (which also draws the next
         // step's eps in Philox mode) and the slot-reducing update; the ELBO
         // accumulators are cleared once for the whole loop
         if (T == 0) return 0;
-        const float* e = eps_t(0);
+        const float* e = first_eps();
         if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
-        HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double) * (size_t)T, st));
         for (int t = 0; t < T; ++t) {
             h.step = hp->step + t;
             const bool draw = !eps && t + 1 < T;
@@ -1228,9 +1239,8 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     } else if (ts) {
         HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st, pads));
     }
-    const float* e = eps_t(0);
+    const float* e = first_eps();
     if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
-    HIP_TRY(hipMemsetAsync(elbo_out, 0, sizeof(double) * (size_t)T, st));
     HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
     for (int t = 0; t < T; ++t) {
         h.step = hp->step + t;

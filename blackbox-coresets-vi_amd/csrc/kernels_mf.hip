@@ -342,24 +342,32 @@ hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
 }
 
 // ----------------------------------------------------- Philox4x32-10 randn
+// zero != nullptr: the same launch also clears zero[0, nzero) (the inner
+// loop's per-step ELBO accumulators, which the first network launch adds into)
 template <bool VEC>
 __global__ __launch_bounds__(256) void randn_kernel(float* __restrict__ out, int64_t n,
-                                                    uint64_t seed, uint64_t offset) {
+                                                    uint64_t seed, uint64_t offset,
+                                                    double* __restrict__ zero, int64_t nzero) {
     const int64_t nq = (n + 3) / 4;
-    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq;
-         q += (int64_t)gridDim.x * blockDim.x)
+    const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = gid; i < nzero; i += gs) zero[i] = 0.0;
+    for (int64_t q = gid; q < nq; q += gs)
         randn_quad<VEC>(out, n, seed, offset, q);
 }
 
-hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    const int64_t nb = std::min<int64_t>(((n + 3) / 4 + 255) / 256, 4096);
+hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st,
+                        double* zero, int64_t nzero) {
+    if (n <= 0 && nzero <= 0) return hipSuccess;
+    if (!zero) nzero = 0;
+    const int64_t nb = std::max<int64_t>(
+        1, std::min<int64_t>(std::max((n + 3) / 4, nzero) / 256 + 1, 4096));
     if (((uintptr_t)out & 15) == 0)
         hipLaunchKernelGGL(randn_kernel<true>, dim3((unsigned)nb), dim3(256), 0, st, out, n, seed,
-                           offset);
+                           offset, zero, nzero);
     else
         hipLaunchKernelGGL(randn_kernel<false>, dim3((unsigned)nb), dim3(256), 0, st, out, n,
-                           seed, offset);
+                           seed, offset, zero, nzero);
     return hipGetLastError();
 }
 

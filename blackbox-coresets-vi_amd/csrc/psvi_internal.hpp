@@ -432,7 +432,8 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
                                    float* tstate, bool to_tiled, hipStream_t st,
                                    float* const* pads = nullptr);
-hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st);
+hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st,
+                        double* zero = nullptr, int64_t nzero = 0);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);
 AdamC make_adam(const psvi_adam_hp* hp);

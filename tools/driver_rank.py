@@ -54,12 +54,18 @@ def main():
     out = {k: [float(x) for x in r[k]] for k in ("accs", "nlls")}
     out["vs"] = [float(x) for x in r["vs"][-1]]
     out.update(world=world, rank=rank)
-    print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
+    if world == 1:
+        print(json.dumps(out), flush=True)
+        return
+    import torch.distributed as dist
 
+    # one rank at a time: the ranks share the launcher's stdout, and lines
+    # written at once can interleave
+    for r in range(world):
+        if r == rank:
+            print(json.dumps(out), flush=True)
         dist.barrier()
-        dist.destroy_process_group()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":
