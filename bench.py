@@ -311,8 +311,8 @@ def fn2_inputs(layers, M, dev, seed):
 def sharded_steps(rt, loop, u, z, w, params, m, v, seed, k0, n, parts=None, ev=None):
     """n sharded inner steps (Adam steps k0 + 1 ..) -- ShardedInnerLoop.run:
     full-cov x all_to_all, network, G all_to_all, the update fused with the
-    next step's sample, the next eps drawn on a side stream behind the
-    exchanges (LeNet: the samples' accumulator all-reduced per step).  The
+    next step's sample, the next eps drawn by the network launch
+    (LeNet: the samples' accumulator all-reduced per step).  The
     draws are the psvi_inner_loop stream at offset k0 * eps_stride.  ev: {step:
     4 events} around the exchanges + network and the update + sample."""
     stride = (loop.plan.eps_count + 3) // 4 * 4

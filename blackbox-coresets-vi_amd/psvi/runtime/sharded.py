@@ -8,7 +8,7 @@ inner step is split across ranks where the math allows it:
       slices + Adam state) are sharded as whole 64-row bands balanced by their
       64 x 64 tile counts; MC samples are sharded in contiguous blocks.  Per
       step (ShardedInnerLoop.run fuses the update with the next step's sample
-      and draws the next eps on a side stream behind the exchanges):
+      and the network with the next step's eps draw):
         sample  x_shard[S][rows_r] = mean + L eps     (own rows, ALL samples)
         all_to_all  -> x_recv: own samples, all rows   (blocked by source rank)
         net     g_send = per-sample gradients          (own samples)
