@@ -199,6 +199,25 @@ def test_net_draw_equals_separate(name, world):
             assert torch.isfinite(outs[1][2]).all()
 
 
+def test_net_draw_rejects_bad_draw_args():
+    """The fused draw's contract: offset a multiple of 4, eps_out 16-byte
+    aligned (vector stores) -- refused with EINVAL, nothing launched."""
+    from psvi.runtime import PsviError
+    from psvi.runtime.sharded import ShardedInnerLoop
+
+    f = load_fixture("g3r_fn2_tiny_rand")
+    cfg, _, u, z, w = _setup(f)
+    plan = ShardedInnerLoop("fullcov", cfg["layers"], cfg["S"], cfg["M"], 2, 0).plan
+    xs = torch.zeros(plan.xrecv_count, device=DEV)
+    gs = torch.zeros(plan.xrecv_count, device=DEV)
+    nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+    e = torch.zeros(plan.eps_count + 4, device=DEV)
+    with pytest.raises(PsviError, match="multiple of 4"):
+        plan.mvn_net(u, z, w, xs, gs, nll, draw=(e, 1, 2))
+    with pytest.raises(PsviError, match="16-byte"):
+        plan.mvn_net(u, z, w, xs, gs, nll, draw=(e[1:], 1, 0))
+
+
 def test_randn_moments_and_determinism():
     from psvi.runtime import randn_
 
