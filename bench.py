@@ -17,6 +17,7 @@ labels ~ Bernoulli(sigmoid(5 sum x))), parameters at the reference init
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+         (a bare `bench.py --gpus N` starts that itself, as a child process)
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -766,6 +767,40 @@ def run(rt, args, shapes=None):
     }
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(n, argv, script=None):
+    """Run `script argv` (default: this file) as n ranks of one node under
+    torch.distributed.run in a CHILD process and return its exit status.
+    The child's stdout is relayed line by line: a JSON object line (rank 0's
+    result) to stdout, anything else (collective-library chatter) to stderr,
+    so the JSON line stays alone on stdout.  Called before any GPU call: the
+    parent only relays and waits."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={int(n)}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
+    log("launching: " + " ".join(cmd[1:]))
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        try:
+            is_line = isinstance(json.loads(line), dict)
+        except ValueError:
+            is_line = False
+        (sys.stdout if is_line else sys.stderr).write(line)
+        (sys.stdout if is_line else sys.stderr).flush()
+    return proc.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -791,6 +826,11 @@ def main():
                     help="every rank on device 0 (rehearsing N ranks on a one-GPU box; "
                          "needs --comm gloo)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # a bare `bench.py --gpus N`: start the N ranks under torchrun as a
+        # child process (this process never touches the GPU) and exit with
+        # its status; rank 0's JSON line reaches stdout through the child
+        raise SystemExit(relaunch(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

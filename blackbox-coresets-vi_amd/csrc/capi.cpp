@@ -1038,7 +1038,10 @@ int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, con
                        const float* x_recv, float* g_send, double* nll_out, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
-    if (!u || !z || !w || !x_recv || !g_send || !nll_out) return fail(PSVI_EINVAL, "null pointer");
+    // a rank without samples (S < world) has empty x / g blocks
+    const bool none = p->s_cnt[p->rank] == 0;
+    if (!u || !z || !w || (!none && (!x_recv || !g_send)) || !nll_out)
+        return fail(PSVI_EINVAL, "null pointer");
     hipStream_t st = as_stream(stream);
     HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x_recv, g_send, nll_out, st));
     return 0;
@@ -1049,7 +1052,8 @@ int psvi_mvn_phase_net_draw(const psvi_plan* p, const float* u, const int32_t* z
                             int64_t n, uint64_t seed, uint64_t offset, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
-    if (!u || !z || !w || !x_recv || !g_send || !nll_out || !eps_out || n < 0)
+    const bool none = p->s_cnt[p->rank] == 0;  // S < world: empty x / g blocks
+    if (!u || !z || !w || (!none && (!x_recv || !g_send)) || !nll_out || !eps_out || n < 0)
         return fail(PSVI_EINVAL, "null pointer or bad count");
     if (offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");
     if (reinterpret_cast<uintptr_t>(eps_out) % 16)

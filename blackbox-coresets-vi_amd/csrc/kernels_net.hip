@@ -1204,7 +1204,10 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     }
     // the outer forward pass has no backward: one role
     dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, p.mchunks), block(p.net_threads);
-    if (p.s_cnt[p.rank] == 0) return hipSuccess;
+    // a rank without samples still owes the next step's draw (every rank
+    // passes the same global eps to its update): the draw on its own
+    if (p.s_cnt[p.rank] == 0)
+        return rn_out && rn_n > 0 ? launch_randn(rn_out, rn_n, rn_seed, rn_off, st) : hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
     else if (p.world > 1 && net_vec_ok(p))

@@ -199,6 +199,31 @@ def test_net_draw_equals_separate(name, world):
             assert torch.isfinite(outs[1][2]).all()
 
 
+def test_net_draw_rank_without_samples():
+    """S < world: ranks 4 and 5 of a world-6 plan of S = 4 own rows but no
+    samples; their network launch has nothing to compute and must still draw
+    the next step's eps (every rank's update reads the same global draw)."""
+    from psvi.runtime import randn_
+    from psvi.runtime.sharded import ShardedInnerLoop
+
+    f = load_fixture("g5_logreg_fullcov")
+    cfg, _, u, z, w = _setup(f)
+    assert cfg["S"] == 4
+    for r in range(6):
+        plan = ShardedInnerLoop("fullcov", cfg["layers"], cfg["S"], cfg["M"], 6, r).plan
+        n = plan.eps_count
+        xs = torch.randn(max(plan.xrecv_count, 1)).to(DEV)[:plan.xrecv_count]
+        gs = torch.zeros(plan.xrecv_count, device=DEV)
+        nll = torch.zeros(1, dtype=torch.float64, device=DEV)
+        e = torch.full((n,), float("nan"), device=DEV)
+        ref = torch.empty(n, device=DEV)
+        plan.mvn_net(u, z, w, xs, gs, nll, draw=(e, 7, 4 * n))
+        randn_(ref, 7, 4 * n)
+        assert torch.equal(e, ref), r
+        if r >= 4:
+            assert float(nll.item()) == 0.0
+
+
 def test_net_draw_rejects_bad_draw_args():
     """The fused draw's contract: offset a multiple of 4, eps_out 16-byte
     aligned (vector stores) -- refused with EINVAL, nothing launched."""
