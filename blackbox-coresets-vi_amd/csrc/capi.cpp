@@ -1029,7 +1029,9 @@ int psvi_mvn_phase_sample(const psvi_plan* p, const float* eps, const float* par
                           float* x_shard, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
-    if (!eps || !params || !x_shard) return fail(PSVI_EINVAL, "null pointer");
+    // a rank that owns no rows (fewer bands than ranks) has an empty x shard
+    if (!eps || !params || (!x_shard && p->rows_tot[p->rank] > 0))
+        return fail(PSVI_EINVAL, "null pointer");
     HIP_TRY(launch_mvn_fwd(*p, eps, params, x_shard, as_stream(stream)));
     return 0;
 }
@@ -1069,7 +1071,8 @@ int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_s
                           double* kl_out, float* grad_out, int32_t include_kl, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
-    if (!eps || !g_shard || !params) return fail(PSVI_EINVAL, "null pointer");
+    if (!eps || (!g_shard && p->rows_tot[p->rank] > 0) || !params)
+        return fail(PSVI_EINVAL, "null pointer");
     if (!grad_out && (!adam_m || !adam_v || !hp)) return fail(PSVI_EINVAL, "null adam state");
     if (!grad_out && hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
     if (!grad_out && (hp->kind < 0 || hp->kind > 2)) return fail(PSVI_EINVAL, "unknown adam kind");
@@ -1084,7 +1087,9 @@ int psvi_mvn_phase_update_sample(const psvi_plan* p, const float* eps, const flo
                                  const float* eps_next, float* x_next, void* stream) {
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
-    if (!eps || !g_shard || !params || !eps_next || !x_next) return fail(PSVI_EINVAL, "null pointer");
+    const bool rows = p->rows_tot[p->rank] > 0;  // no rows: empty G and x shards
+    if (!eps || !params || !eps_next || (rows && (!g_shard || !x_next)))
+        return fail(PSVI_EINVAL, "null pointer");
     if (!adam_m || !adam_v || !hp) return fail(PSVI_EINVAL, "null adam state");
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
     if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
