@@ -32,6 +32,7 @@ extern int g_lenet_abl;                  // kernels_lenet.hip
 extern int g_net_split_below;            // kernels_net.hip
 extern int g_net_threads;                // kernels_net.hip
 extern int g_net_wg_target;              // kernels_net.hip
+extern int g_net_mloop_off;              // kernels_net.hip
 extern int g_fwd_ablation;               // kernels_mvn.hip
 extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
@@ -612,6 +613,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_KSTREAM_WGS: g_ks_wgs = value; return 0;
         case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
+        case PSVI_DBG_NET_MLOOP_OFF: g_net_mloop_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         case PSVI_DBG_LENET_GEMM_VALU: g_lenet_gemm_valu = value; return 0;

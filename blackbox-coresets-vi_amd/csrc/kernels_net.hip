@@ -111,6 +111,7 @@ struct NetArgs {
     // bands[bbase[l] + r / 64].base + s * .stride + r in g_send
     const NetBand* bands;
     int nbands, bbase[kMaxL];
+    int mloop;  // pseudopoint chunks looped inside one workgroup (1: none)
 };
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -317,15 +318,13 @@ __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int nsrc, const int
 // instantiation has straight-line x loads: with the run-table path in the
 // same kernel the register allocator shares registers across the two paths
 // and the waitcnt pass then serialises the u and x loads (seen in the ISA).
-template <int FAM, bool MSRC, bool VEC = false>
+template <int FAM, bool MSRC, bool VEC = false, bool MLOOP = false>
 __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     static_assert(!VEC || FAM == PSVI_FAMILY_FULLCOV, "float4 loads: the full-cov x row");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
     const int role = blockIdx.y;
-    const int m0 = blockIdx.z * a.mc;
-    const int mcnt = min(a.mc, a.M - m0);
     const int L = a.L, Mp = a.Mp;
     const int tid = threadIdx.x;
     unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
@@ -387,6 +386,19 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         }
         __syncthreads();
     }
+    float part = 0.f;  // this thread's share of the weighted NLL
+    // Pseudopoint chunks: blockIdx.z picks a run of a.mloop chunks, looped
+    // inside the workgroup (full-cov inner objective, buffers past the LDS: the
+    // sample's weights are loaded once, the weight gradients of chunk > 0 are
+    // added to the first chunk's -- by the same lane, in chunk order, so the
+    // sums equal the per-chunk slots added in chunk order)
+    const int nloop = MLOOP ? a.mloop : 1;
+    int ch = 0;
+chunk_top:  // a backward jump only when MLOOP (no loop at all in the other instantiations)
+    {
+    const int m0 = (blockIdx.z * nloop + ch) * a.mc;
+    const int mcnt = min(a.mc, a.M - m0);
+    const bool first = !MLOOP || ch == 0;
     NET_STAMP(4, __builtin_amdgcn_s_memtime());
     // Every global load of the phase is issued before its first LDS store:
     // the u chunk (float4 per lane when rows are float4-sized), the labels and
@@ -412,11 +424,11 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         const int nu4 = (mcnt * D) >> 2;
         const float rdu = 1.f / (float)D;
         const f4* usrc = reinterpret_cast<const f4*>(a.u + (int64_t)m0 * D);
-        const int nx = a.stage_len, nxt = MSRC ? 0 : nx & 3;
+        const int nx = first ? a.stage_len : 0, nxt = MSRC ? 0 : nx & 3;
         // float4 chunks of the x row: one source -- the row's whole float4s;
         // several -- every source block's ceil(rows / 4) chunks (the last one
         // loaded at rows - 4 and shifted), chunk prefix per source in LDS
-        const int nx4 = MSRC ? a.src_chunk0[a.nsrc] : nx >> 2;
+        const int nx4 = MSRC ? (first ? a.src_chunk0[a.nsrc] : 0) : nx >> 2;
         const float* xr = a.xrecv + (int64_t)s * a.src_stride[0];
         const u4* xm4 = reinterpret_cast<const u4*>(a.xmap);
         const int bd = blockDim.x;
@@ -439,7 +451,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                         xv[k] = *reinterpret_cast<const f4*>(xr + 4 * c);
                         xm[k] = xm4[c];
                     }
-                    const int rt = min(4 * nx4 + (tid & 3), nx - 1);
+                    const int rt = max(min(4 * nx4 + (tid & 3), nx - 1), 0);
                     xt = xr[rt];
                     xmt = a.xmap[rt];
                 } else {
@@ -470,7 +482,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 // loaded element): W columns >= din and rows >= dout, W^T columns
                 // dout .. the 16-multiple, u columns >= D up to the 16-multiple, u
                 // rows past the chunk, the 64-float slacks after every region
-                for (int l = 0; l < L; ++l) {
+                for (int l = 0; l < L && first; ++l) {
                     const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
                     const int rows = (dout + 15) & ~15;
                     if (l > 0) {
@@ -587,7 +599,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
                 // loaded element): W columns >= din (16 lanes a row) and rows >=
                 // dout, u columns >= D up to the 16-multiple, u rows past the
                 // chunk, the slacks before the stage
-                for (int l = 0; l < L; ++l) {
+                for (int l = 0; l < L; ++l) {  // (the scalar path is never looped)
                     const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
                     const int rows = (dout + 15) & ~15;
                     if (l > 0) {  // W^T columns dout .. the 16-multiple (K padding of the propagation)
@@ -634,7 +646,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             zw[Mp + m] = a.w[m0 + m];
         }
     }
-    if (FAM != PSVI_FAMILY_FULLCOV && !(a.abl & 1)) {
+    if (FAM != PSVI_FAMILY_FULLCOV && !(a.abl & 1)) {  // (never looped: MLOOP is full-cov only)
         // Normal.rsample: loc + eps * softplus(rho), elementwise into place
         constexpr int kB = 16;
         for (int l = 0; l < L; ++l) {
@@ -676,7 +688,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         }
     }
     NET_STAMP(5, __builtin_amdgcn_s_memtime());
-    if (FAM == PSVI_FAMILY_FULLCOV && MSRC) {
+    if (FAM == PSVI_FAMILY_FULLCOV && MSRC && first) {
         // every band's g_send offset for this sample (section 3's fc_addr)
         int64_t* boff = reinterpret_cast<int64_t*>(srct);
         for (int i = tid; i < a.nbands; i += blockDim.x) {
@@ -714,7 +726,6 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     // outer backward: d loss / d pseudo_s and d loss / d data_s scale the rows
     const float cp = a.outer == 2 ? a.rowcoef[2 * s] : 1.f;
     const float cd = a.outer == 2 ? a.rowcoef[2 * s + 1] : 1.f;
-    float part = 0.f;  // this thread's share of the chunk's weighted NLL
     const int nwv = blockDim.x >> 6, lane = tid & 63;
     auto drain = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
     // G_l: dlogits for l = L - 1, else the l-th gradient buffer (stride of X_{l+1})
@@ -859,12 +870,13 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             // chunked; net_slot_sum_kernel adds the slots in chunk order)
             float* dst = (a.gslot ? a.gslot + (int64_t)blockIdx.z * a.gsz : a.gsend) +
                          fc_addr(a, nsrc, srct, l, o, s);
-            *dst = v;
+            if (first) *dst = v;
+            else *dst += v;  // a looped chunk: this lane wrote the element before
         }
     };
     // outer backward: the sampled-KL path, d nkl_s / d x_s = -x_s / s0^2,
     // added once per sample (pseudopoint chunk 0)
-    const float ckv = (a.outer == 2 && blockIdx.z == 0) ? a.ck[s] * a.inv_s0sq : 0.f;
+    const float ckv = (a.outer == 2 && blockIdx.z == 0 && first) ? a.ck[s] * a.inv_s0sq : 0.f;
     if (bwd) {
         int first = 0;
         for (int l = own_hi - 1; l >= own_lo; --l) {
@@ -919,8 +931,15 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
             qb += nq;
         }
     }
-    NET_STAMP(3, __builtin_amdgcn_s_memtime());
     asm volatile("" ::"v"(sink));
+    }
+    if constexpr (MLOOP) {
+        if (++ch < nloop) {
+            __syncthreads();  // the next chunk overwrites X_l, G_l, z / w
+            goto chunk_top;
+        }
+    }
+    NET_STAMP(3, __builtin_amdgcn_s_memtime());
     if (role == 0 && a.outer == 0) {  // the chunk's weighted NLL (role 1 computed the same)
         const float tot = block_sum(part, sm + a.lred);
         if (tid == 0) atomicAdd(a.nll_out, (double)tot);
@@ -1054,6 +1073,9 @@ size_t net_plan_geometry(psvi_plan& p) {
     if (split)
         while (S_local * p.net_roles * mchunks < g_net_wg_target && (M + mchunks) / (mchunks + 1) >= 16)
             ++mchunks;
+    // chunks forced by the LDS alone (the samples already fill the chip) are
+    // looped inside the workgroups of a full-cov plan (NetArgs::mloop)
+    const bool fill_one = mchunks == 1;
     for (;;) {
         const int mc = (M + mchunks - 1) / mchunks;
         const size_t bytes = net_lds_floats(p, mc, nullptr) * 4;
@@ -1062,6 +1084,7 @@ size_t net_plan_geometry(psvi_plan& p) {
             p.mc = mc;
             p.net_lds = bytes;
             p.net_threads = g_net_threads ? g_net_threads : (rup(mc, 16) >= 48 ? 512 : 256);
+            p.net_mloop = p.family == PSVI_FAMILY_FULLCOV && fill_one && p.mchunks > 1;
             return bytes;
         }
         ++mchunks;
@@ -1110,6 +1133,7 @@ void net_xmap(const psvi_plan& p, std::vector<uint32_t>& xmap, std::vector<NetBa
 }
 
 int g_net_ablation = 0;  // psvi_debug_set(PSVI_DBG_NET_ABLATION, mask)
+int g_net_mloop_off = 0;  // psvi_debug_set(PSVI_DBG_NET_MLOOP_OFF, 1): a workgroup per pseudopoint chunk + slots (A/B)
 int g_net_scalar_loads = 0;  // psvi_debug_set(PSVI_DBG_NET_SCALAR_LOADS, 1): the scalar load path (A/B)
 unsigned long long* g_net_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_NET_STAMPS, buf)
 
@@ -1124,6 +1148,10 @@ void net_set_lds_limit() {
     (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true, true, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
@@ -1202,14 +1230,25 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         a.nbands = p.world > 1 ? p.band_base[p.L] : 0;
         if (!a.xmap || (p.world > 1 && !a.bands)) return hipErrorInvalidValue;
     }
+    // the inner objective of a full-cov plan whose pseudopoints exceed the LDS
+    // loops its chunks inside each workgroup (one x load, no slots, no slot sum)
+    const bool loop = p.net_mloop && a.outer == 0 && !g_net_mloop_off &&
+                      p.family == PSVI_FAMILY_FULLCOV && net_vec_ok(p);
+    a.mloop = loop ? p.mchunks : 1;
+    if (loop) a.gslot = nullptr;
     // the outer forward pass has no backward: one role
-    dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, p.mchunks), block(p.net_threads);
+    dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, loop ? 1 : p.mchunks),
+        block(p.net_threads);
     // a rank without samples still owes the next step's draw (every rank
     // passes the same global eps to its update): the draw on its own
     if (p.s_cnt[p.rank] == 0)
         return rn_out && rn_n > 0 ? launch_randn(rn_out, rn_n, rn_seed, rn_off, st) : hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
+    else if (loop && p.world > 1)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true, true, true>), grid, block, p.net_lds, st, a);
+    else if (loop)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false, true, true>), grid, block, p.net_lds, st, a);
     else if (p.world > 1 && net_vec_ok(p))
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true, true>), grid, block, p.net_lds, st, a);
     else if (p.world > 1)

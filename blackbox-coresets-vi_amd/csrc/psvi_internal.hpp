@@ -370,6 +370,7 @@ struct psvi_plan {
     int n_fswg = 0, n_fs_slots = 0, n_fs_rb = 0;
     // net kernel geometry
     int mchunks = 1, mc = 0, net_threads = 256, net_roles = 1;
+    bool net_mloop = false;  // full-cov inner objective: the LDS-forced chunks looped in a workgroup
     size_t net_lds = 0;
     size_t ws_bytes = 0;
     int64_t acc_count = 0;

@@ -476,6 +476,11 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     for plans created afterwards (0: 512)       */
 #define PSVI_DBG_FWD_SEG_OFF 22      /* value: 1 = the item-grid sample kernel instead
                                     of the segmented one at S > 128 (A/B)       */
+#define PSVI_DBG_NET_MLOOP_OFF 23     /* value: 1 = a full-cov plan whose pseudopoints
+                                    exceed the network kernel's LDS runs one
+                                    workgroup per chunk with per-chunk slots
+                                    and a slot sum, instead of looping the
+                                    chunks inside each workgroup (A/B)          */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
