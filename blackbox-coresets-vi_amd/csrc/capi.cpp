@@ -23,6 +23,8 @@ extern int g_net_scalar_loads;           // kernels_net.hip
 extern unsigned long long* g_net_stamps; // kernels_net.hip
 extern int g_upd_ablation;               // kernels_mvn.hip
 extern int g_stream_off;                 // kernels_mvn.hip
+extern int g_stream_bf_off;              // kernels_mvn.hip
+extern unsigned long long* g_bf_stamps;  // kernels_mvn.hip
 extern int g_ks_off;                     // kernels_mvn.hip
 extern int g_fs_off;                     // kernels_mvn.hip
 static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
@@ -609,6 +611,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_FWD_ABLATION: g_fwd_ablation = value; return 0;
         case PSVI_DBG_UPD_CHUNK: g_upd_chunk_tiles = value; return 0;
         case PSVI_DBG_UPD_STREAM_OFF: g_stream_off = value; return 0;
+        case PSVI_DBG_STREAM_BF_OFF: g_stream_bf_off = value; return 0;
         case PSVI_DBG_KSTREAM_OFF: g_ks_off = value; return 0;
         case PSVI_DBG_KSTREAM_WGS: g_ks_wgs = value; return 0;
         case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
@@ -650,6 +653,7 @@ int psvi_debug_set_ptr(int32_t key, void* ptr) {
     switch (key) {
         case PSVI_DBG_NET_STAMPS: g_net_stamps = (unsigned long long*)ptr; return 0;
         case PSVI_DBG_UPD_STAMPS: g_upd_stamps = (unsigned long long*)ptr; return 0;
+        case PSVI_DBG_BF_STAMPS: g_bf_stamps = (unsigned long long*)ptr; return 0;
         case PSVI_DBG_ROP_STAMPS: g_rop_stamps = (unsigned long long*)ptr; return 0;
         case PSVI_DBG_FWD_STAMPS: g_fwd_stamps = (unsigned long long*)ptr; return 0;
         default: return fail(PSVI_EINVAL, "unknown debug key");
@@ -686,6 +690,26 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
     p->world = world;
     p->rank = rank;
     int rc = build_plan(*p);
+    if (!rc && family == PSVI_FAMILY_FULLCOV && world == 1 && p->fuse_sample && p->tiles_total > 0 &&
+        p->n_str > 0 && p->d.S == 128) {
+        // the streaming update's bf16 planes of every draw (EpsPlanes): rows
+        // padded to 64-column multiples, layers back to back
+        psvi::EpsPlanes& E = p->eps_planes;
+        E.L = p->L;
+        int64_t po = 0, eo = 0;
+        for (int l = 0; l < p->L; ++l) {
+            const int n = p->lay[l].n;
+            E.eoff[l] = eo;
+            E.n[l] = n;
+            E.npad[l] = (n + 63) / 64 * 64;
+            E.poff[l] = po;
+            eo += (int64_t)p->d.S * n;
+            po += (int64_t)p->d.S * E.npad[l];
+        }
+        E.eoff[p->L] = eo;
+        E.pl = (po + 63) / 64 * 64;
+        p->bf_stream = eo == p->Peps;
+    }
     if (!rc && have_dev) {
         // the only device allocations of the library: immutable work lists
         if (!(rc = upload(p->h_fwd, &p->d_fwd)) && !(rc = upload(p->h_frb, &p->d_frb)))
@@ -751,6 +775,10 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
              hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
              hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess))
             rc = fail(PSVI_EUNSUP, "cannot create the inner loop's conversion stream");
+        if (!rc && p->bf_stream) {
+            std::vector<psvi::EpsPlanes> one(1, p->eps_planes);
+            rc = upload(one, &p->d_eps_planes);
+        }
         if (!rc && family == PSVI_FAMILY_LENET) {
             const size_t bytes = lenet_ws(*p, nullptr).bytes;
             if (hipMalloc(&p->d_lenet_ws, bytes) != hipSuccess)
@@ -791,6 +819,7 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_fs_rb) (void)hipFree(p->d_fs_rb);
     if (p->d_fs_part) (void)hipFree(p->d_fs_part);
     if (p->d_net_bands) (void)hipFree(p->d_net_bands);
+    if (p->d_eps_planes) (void)hipFree(p->d_eps_planes);
     if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
     if (p->ev_join) (void)hipEventDestroy(p->ev_join);
     if (p->aux_st) (void)hipStreamDestroy(p->aux_st);
@@ -1123,8 +1152,13 @@ static size_t tiled_floats(const psvi_plan* p) {
 static size_t loop_ebuf_bytes(const psvi_plan* p) {
     return align256(sizeof(float) * ((size_t)eps_stride(p) + 64));
 }
+// the bf16 planes of one draw (three planes of EpsPlanes::pl elements)
+static size_t loop_pbuf_bytes(const psvi_plan* p) {
+    return p->bf_stream ? align256(3 * sizeof(uint16_t) * (size_t)p->eps_planes.pl) : 0;
+}
 static size_t loop_ws_bytes(const psvi_plan* p) {
-    return align256(p->ws_bytes) + 2 * loop_ebuf_bytes(p) + align256(sizeof(float) * tiled_floats(p));
+    return align256(p->ws_bytes) + 2 * loop_ebuf_bytes(p) + align256(sizeof(float) * tiled_floats(p)) +
+           2 * loop_pbuf_bytes(p);
 }
 
 int psvi_mvn_tiled_convert(const psvi_plan* p, float* params, float* adam_m, float* adam_v,
@@ -1157,7 +1191,16 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
                     const float* eps, uint64_t seed, uint64_t offset, int32_t T, float* params,
                     float* adam_m, float* adam_v, const psvi_adam_hp* hp, double* elbo_out,
                     void* ws, size_t ws_bytes, void* stream) {
+    return psvi_inner_loop_ex(p, u, z, w, eps, seed, offset, T, params, adam_m, adam_v, hp,
+                              elbo_out, ws, ws_bytes, 0, stream);
+}
+
+int psvi_inner_loop_ex(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                       const float* eps, uint64_t seed, uint64_t offset, int32_t T, float* params,
+                       float* adam_m, float* adam_v, const psvi_adam_hp* hp, double* elbo_out,
+                       void* ws, size_t ws_bytes, int32_t flags, void* stream) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
+    if (flags & ~(PSVI_LOOP_KEEP | PSVI_LOOP_RESUME)) return fail(PSVI_EINVAL, "unknown loop flags");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "inner loop needs world == 1 (use phases)");
     if (!u || !z || !w || !params || !adam_m || !adam_v || !hp || !elbo_out)
@@ -1235,45 +1278,92 @@ int psvi_inner_loop(const psvi_plan* p, const float* u, const int32_t* z, const 
     // pads are zeroed with the tiled conversion and the streaming update reads
     // them unclamped
     const bool padded = ts && !eps;
+    // Philox mode on a bf-stream plan: every draw also as bf16 planes, one
+    // plane buffer per eps buffer (their row pads zeroed here, never drawn)
+    uint16_t* pbuf[2] = {nullptr, nullptr};
+    if (padded && p->bf_stream) {
+        char* pb = wsb + align256(p->ws_bytes) + 2 * loop_ebuf_bytes(p) +
+                   align256(sizeof(float) * tiled_floats(p));
+        pbuf[0] = (uint16_t*)pb;
+        pbuf[1] = (uint16_t*)(pb + loop_pbuf_bytes(p));
+    }
     float* pads[3] = {padded ? ebuf[0] + p->Peps : nullptr, padded ? ebuf[1] + p->Peps : nullptr,
                       padded ? g + (size_t)p->d.S * p->rows_tot[0] : nullptr};
     if (T == 0) return 0;
-    // packed -> tiled state on the plan's conversion stream, behind x_0 and the
-    // first network step (joined before the first update)
+    // resident state of the last KEEP call (dropped by every call; taken up by
+    // a RESUME call that continues it)
+    const psvi_plan::Resident res = p->resident;
+    p->resident.valid = false;
+    const bool keep = (flags & PSVI_LOOP_KEEP) && padded;
+    const bool resume = (flags & PSVI_LOOP_RESUME) && padded && res.valid && res.ws == ws &&
+                        res.params == params && res.m == adam_m && res.v == adam_v &&
+                        res.seed == seed && res.offset == offset;
+    // eps buffer of step t (a resumed loop's step 0 is where the last one left it)
+    const int eb0 = resume ? res.ebuf : 0;
+    auto bi = [&](int t) { return (t + eb0) & 1; };
     bool join = false;
-    if (ts && p->aux_st) {
-        HIP_TRY(hipEventRecord(p->ev_fork, st));
-        HIP_TRY(hipStreamWaitEvent(p->aux_st, p->ev_fork, 0));
-        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, p->aux_st, pads));
-        HIP_TRY(hipEventRecord(p->ev_join, p->aux_st));
-        join = true;
-    } else if (ts) {
-        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st, pads));
+    const float* e;
+    if (resume) {
+        // the tiled state, step 0's eps (+ planes) and x are in ws already; the
+        // ELBO accumulators cleared by the draw kernel's zero-fill with no draw
+        // (a library kernel: hipMemsetAsync's first use in a process loads the
+        // runtime's own fill kernels inside the caller's timed region)
+        HIP_TRY(launch_randn(ebuf[1 - bi(0)], 0, 0, 0, st, elbo_out, T));
+        e = ebuf[bi(0)];
+    } else {
+        // packed -> tiled state on the plan's conversion stream, behind x_0 and the
+        // first network step (joined before the first update)
+        if (ts && p->aux_st) {
+            HIP_TRY(hipEventRecord(p->ev_fork, st));
+            HIP_TRY(hipStreamWaitEvent(p->aux_st, p->ev_fork, 0));
+            HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, p->aux_st, pads));
+            HIP_TRY(hipEventRecord(p->ev_join, p->aux_st));
+            join = true;
+        } else if (ts) {
+            HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, true, st, pads));
+        }
+        if (pbuf[0]) {
+            HIP_TRY(hipMemsetAsync(pbuf[0], 0, 2 * loop_pbuf_bytes(p), st));
+            HIP_TRY(launch_randn(ebuf[0], p->Peps, seed, offset, st, elbo_out, T, &p->eps_planes, pbuf[0]));
+            e = ebuf[0];
+        } else {
+            e = first_eps();
+        }
+        if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
+        HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
     }
-    const float* e = first_eps();
-    if (!e) return fail(PSVI_EUNSUP, "randn launch failed");
-    HIP_TRY(launch_mvn_fwd(*p, e, params, x, st));
     for (int t = 0; t < T; ++t) {
         h.step = hp->step + t;
-        // Philox mode: the network kernel also draws the next step's eps
-        const bool draw = !eps && t + 1 < T;
-        float* en_buf = draw ? ebuf[(t + 1) & 1] : nullptr;
+        // Philox mode: the network kernel also draws the next step's eps (KEEP:
+        // the last step too, for the next call)
+        const bool last = t + 1 == T;
+        const bool draw = !eps && (!last || keep);
+        float* en_buf = draw ? ebuf[bi(t + 1)] : nullptr;
+        uint16_t* en_pl = draw ? pbuf[bi(t + 1)] : nullptr;
         const bool tm = g_loop_every > 0 && t % g_loop_every == 0;
         if (tm) HIP_TRY(loop_event(0, st));
         HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x, g, elbo_out + t,
-                           st, en_buf, draw ? p->Peps : 0, seed, offset + (uint64_t)(t + 1) * es));
+                           st, en_buf, draw ? p->Peps : 0, seed, offset + (uint64_t)(t + 1) * es,
+                           nullptr, en_pl));
         if (tm) HIP_TRY(loop_event(0, st));
-        const float* en = t + 1 < T ? (eps ? eps + (size_t)(t + 1) * p->Peps : en_buf) : nullptr;
+        const float* en = !last ? (eps ? eps + (size_t)(t + 1) * p->Peps : en_buf) : (keep ? en_buf : nullptr);
         if (tm) HIP_TRY(loop_event(1, st));
         if (join) {
             HIP_TRY(hipStreamWaitEvent(st, p->ev_join, 0));
             join = false;
         }
-        // the last step (no next sample) writes corr / m / v back to the packed arrays
+        // the last step (no next sample) writes corr / m / v back to the packed
+        // arrays; KEEP: it samples as every step, then the tiled state is copied out
         HIP_TRY(launch_mvn_update(*p, e, g, params, adam_m, adam_v, &h, elbo_out + t, nullptr, 1,
-                                  en, en ? x : nullptr, st, ts, ts && !en, nullptr, padded));
+                                  en, en ? x : nullptr, st, ts, ts && !en, nullptr, padded,
+                                  pbuf[bi(t)], en ? en_pl : nullptr));
         if (tm) HIP_TRY(loop_event(1, st));
         e = en;
+    }
+    if (keep) {
+        HIP_TRY(launch_mvn_tile_convert(*p, params, adam_m, adam_v, ts, false, st, nullptr));
+        p->resident = psvi_plan::Resident{true, ws, params, adam_m, adam_v, seed,
+                                          offset + (uint64_t)T * es, bi(T)};
     }
     return 0;
 }

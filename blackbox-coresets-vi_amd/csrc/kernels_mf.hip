@@ -356,12 +356,30 @@ __global__ __launch_bounds__(256) void randn_kernel(float* __restrict__ out, int
         randn_quad<VEC>(out, n, seed, offset, q);
 }
 
+// the same stream, also as the full-cov draw's three bf16 planes (EpsPlanes)
+__global__ __launch_bounds__(256) void randn_planes_kernel(float* __restrict__ out, int64_t n,
+                                                           uint64_t seed, uint64_t offset,
+                                                           double* __restrict__ zero, int64_t nzero,
+                                                           EpsPlanes P, uint16_t* __restrict__ planes) {
+    const int64_t nq = (n + 3) / 4;
+    const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = gid; i < nzero; i += gs) zero[i] = 0.0;
+    for (int64_t q = gid; q < nq; q += gs) randn_quad_planes(out, n, seed, offset, q, P, planes);
+}
+
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st,
-                        double* zero, int64_t nzero) {
+                        double* zero, int64_t nzero, const EpsPlanes* planes_desc, uint16_t* planes) {
     if (n <= 0 && nzero <= 0) return hipSuccess;
     if (!zero) nzero = 0;
     const int64_t nb = std::max<int64_t>(
         1, std::min<int64_t>(std::max((n + 3) / 4, nzero) / 256 + 1, 4096));
+    if (planes && planes_desc) {
+        if ((uintptr_t)out & 15) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(randn_planes_kernel, dim3((unsigned)nb), dim3(256), 0, st, out, n, seed,
+                           offset, zero, nzero, *planes_desc, planes);
+        return hipGetLastError();
+    }
     if (((uintptr_t)out & 15) == 0)
         hipLaunchKernelGGL(randn_kernel<true>, dim3((unsigned)nb), dim3(256), 0, st, out, n, seed,
                            offset, zero, nzero);

@@ -112,6 +112,9 @@ struct NetArgs {
     const NetBand* bands;
     int nbands, bbase[kMaxL];
     int mloop;  // pseudopoint chunks looped inside one workgroup (1: none)
+    // the fused draw also as bf16 planes (the bf16-plane streaming update)
+    const EpsPlanes* rn_P;
+    uint16_t* rn_planes;
 };
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -952,8 +955,14 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         const int nblk = gridDim.x * gridDim.y * gridDim.z;
         const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         const int64_t per = (nq + nblk - 1) / nblk, q1 = min(nq, (b + 1) * per);
-        for (int64_t q = b * per + tid; q < q1; q += blockDim.x)
-            randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
+        if (a.rn_planes) {
+            const EpsPlanes P = *a.rn_P;
+            for (int64_t q = b * per + tid; q < q1; q += blockDim.x)
+                randn_quad_planes(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q, P, a.rn_planes);
+        } else {
+            for (int64_t q = b * per + tid; q < q1; q += blockDim.x)
+                randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
+        }
     }
     NET_STAMP(12, __builtin_amdgcn_s_memtime());
     NET_STAMP(14, __builtin_amdgcn_s_memrealtime());
@@ -1169,7 +1178,7 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
                       const float* params, const float* eps, float* mf_slots,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out, int64_t rn_n, uint64_t rn_seed, uint64_t rn_off,
-                      const NetOuter* outer) {
+                      const NetOuter* outer, uint16_t* rn_planes) {
     NetArgs a{};
     if (outer) {
         a.outer = outer->mode;
@@ -1185,6 +1194,9 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     a.rn_n = rn_n;
     a.rn_seed = rn_seed;
     a.rn_off = rn_off;
+    a.rn_P = p.d_eps_planes;
+    a.rn_planes = rn_planes && p.d_eps_planes ? rn_planes : nullptr;
+    if (rn_planes && !p.d_eps_planes) return hipErrorInvalidValue;
     a.L = p.L;
     a.M = p.d.M;
     a.mc = p.mc;
@@ -1242,7 +1254,9 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     // a rank without samples still owes the next step's draw (every rank
     // passes the same global eps to its update): the draw on its own
     if (p.s_cnt[p.rank] == 0)
-        return rn_out && rn_n > 0 ? launch_randn(rn_out, rn_n, rn_seed, rn_off, st) : hipSuccess;
+        return rn_out && rn_n > 0 ? launch_randn(rn_out, rn_n, rn_seed, rn_off, st, nullptr, 0,
+                                                 rn_planes ? &p.eps_planes : nullptr, rn_planes)
+                                  : hipSuccess;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
     else if (loop && p.world > 1)

@@ -136,6 +136,101 @@ __device__ __forceinline__ void randn_quad(float* __restrict__ out, int64_t n, u
     }
 }
 
+// ------------------------------------------- bf16 planes of a full-cov draw
+// fp32-faithful products on the bf16 matrix cores: x = x0 + x1 + x2, each
+// piece bf16 (round to nearest even) and the sum exact for normal fp32 (the
+// second residual has <= 8 significant bits); a product of two split operands
+// is the six piece products down to 2^-27 relative, below fp32's rounding.
+__device__ __forceinline__ uint16_t bf_bits(float x) {
+    return __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+__device__ __forceinline__ float bf_val(uint32_t b) { return __uint_as_float(b << 16); }
+__device__ __forceinline__ void split3(float x, uint16_t& x0, uint16_t& x1, uint16_t& x2) {
+    x0 = bf_bits(x);
+    const float r1 = x - bf_val(x0);
+    x1 = bf_bits(r1);
+    x2 = bf_bits(r1 - bf_val(x1));
+}
+
+// A full-cov eps draw also as three bf16 planes (the streaming update's MFMA
+// operands): plane p holds piece p of element (l, s, c) at poff[l] + s npad[l]
+// + c, rows padded to npad[l] = a 64-multiple with zeros (the pads are never
+// drawn).  eoff: the layers' [S][n] blocks in the fp32 draw order (eoff[L] =
+// the draw's length).
+struct EpsPlanes {
+    int L;
+    int64_t pl;  // elements per plane; planes back to back
+    int64_t eoff[kMaxL + 1];
+    int n[kMaxL], npad[kMaxL];
+    int64_t poff[kMaxL];
+};
+
+// normals 4q .. 4q+3 of the stream into out[0, n) and, with planes, their
+// three bf16 pieces (randn_quad's values)
+__device__ __forceinline__ void randn_quad_planes(float* __restrict__ out, int64_t n, uint64_t seed,
+                                                  uint64_t offset, int64_t q, const EpsPlanes& P,
+                                                  uint16_t* __restrict__ planes) {
+    const uint64_t ctr = offset / 4 + (uint64_t)q;
+    uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    float r[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const float u1 = ((float)(c[2 * j] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+        const float u2 = (float)(c[2 * j + 1] >> 8) * (1.0f / 16777216.0f);
+        const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+        r[2 * j] = rad * __builtin_amdgcn_cosf(u2);
+        r[2 * j + 1] = rad * __builtin_amdgcn_sinf(u2);
+    }
+    const int64_t base = q * 4;
+    if (base + 3 < n) {
+        *reinterpret_cast<float4*>(out + base) = make_float4(r[0], r[1], r[2], r[3]);
+    } else {
+        for (int j = 0; j < 4 && base + j < n; ++j) out[base + j] = r[j];
+    }
+    if (!planes) return;
+    // element i's place in the planes (selects over the layers: a dynamic
+    // index into P would put it in scratch)
+    auto place = [&](int64_t i, int& c, int& nl) -> int64_t {
+        int64_t e0 = P.eoff[0], po = P.poff[0];
+        int np = P.npad[0];
+        nl = P.n[0];
+#pragma unroll
+        for (int k = 1; k < kMaxL; ++k)
+            if (k < P.L && i >= P.eoff[k]) {
+                e0 = P.eoff[k];
+                po = P.poff[k];
+                np = P.npad[k];
+                nl = P.n[k];
+            }
+        const int64_t rem = i - e0;
+        const int s = (int)(rem / nl);
+        c = (int)(rem - (int64_t)s * nl);
+        return po + (int64_t)s * np + c;
+    };
+    uint16_t pc[3][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split3(r[j], pc[0][j], pc[1][j], pc[2][j]);
+    int c0, nl;
+    const int64_t o = place(base, c0, nl);
+    if (c0 + 3 < nl && base + 3 < n && (o & 3) == 0) {  // the quad in one row
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<u16x4*>(planes + p * P.pl + o) = u16x4{pc[p][0], pc[p][1], pc[p][2], pc[p][3]};
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (base + j >= n) break;
+        int cj, nj;
+        const int64_t oj = place(base + j, cj, nj);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) planes[p * P.pl + oj] = pc[p][j];
+    }
+}
+
 // Adam, both reference variants; returns new p, updates m, v in place.
 struct AdamC {
     float lr, b1, b2, eps, omb1, omb2;
@@ -388,6 +483,24 @@ struct psvi_plan {
     // first sample and network step (not re-entrant across host threads)
     hipStream_t aux_st = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // bf16-plane streaming update (tiled S = 128 loops): every eps draw of
+    // the loop also as three bf16 planes (EpsPlanes; device copy for the
+    // network kernel's fused draw), two plane buffers in the loop workspace
+    bool bf_stream = false;
+    psvi::EpsPlanes eps_planes{};
+    psvi::EpsPlanes* d_eps_planes = nullptr;
+    // psvi_inner_loop_ex(PSVI_LOOP_KEEP): what the last call left in its
+    // workspace -- the tiled corr / m / v, the draw at `offset` (eps buffer
+    // `ebuf`, and its planes) and the sample x from it -- and for which
+    // arrays; any loop call clears it first (mutable: the API's plans are const)
+    struct Resident {
+        bool valid = false;
+        const void* ws = nullptr;
+        const float *params = nullptr, *m = nullptr, *v = nullptr;
+        uint64_t seed = 0, offset = 0;
+        int ebuf = 0;
+    };
+    mutable Resident resident{};
 };
 
 namespace psvi {
@@ -407,7 +520,8 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
                       const float* params, const float* eps, float* mf_slots,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out = nullptr, int64_t rn_n = 0, uint64_t rn_seed = 0,
-                      uint64_t rn_off = 0, const NetOuter* outer = nullptr);
+                      uint64_t rn_off = 0, const NetOuter* outer = nullptr,
+                      uint16_t* rn_planes = nullptr);
 // acc == nullptr: the accumulators come from the plan's mean-field gradient
 // slots, reduced in a fixed order against slot_eps (the step's eps)
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
@@ -428,13 +542,16 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
                              float* tstate = nullptr, bool packed_out = false,
-                             const float* kl_vec = nullptr, bool padded = false);
+                             const float* kl_vec = nullptr, bool padded = false,
+                             const uint16_t* eps_planes = nullptr,
+                             const uint16_t* eps_next_planes = nullptr);
 // pads (to_tiled, nullable): three 64-float regions the first workgroup zeroes
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
                                    float* tstate, bool to_tiled, hipStream_t st,
                                    float* const* pads = nullptr);
 hipError_t launch_randn(float* out, int64_t n, uint64_t seed, uint64_t offset, hipStream_t st,
-                        double* zero = nullptr, int64_t nzero = 0);
+                        double* zero = nullptr, int64_t nzero = 0,
+                        const EpsPlanes* planes_desc = nullptr, uint16_t* planes = nullptr);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v,
                        const psvi_adam_hp* hp, hipStream_t st);
 AdamC make_adam(const psvi_adam_hp* hp);

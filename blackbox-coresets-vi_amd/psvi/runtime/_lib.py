@@ -15,6 +15,8 @@ MAX_LAYERS = 8
 FAMILY_MEANFIELD = 0
 FAMILY_FULLCOV = 1
 FAMILY_LENET = 2
+LOOP_KEEP = 1    # psvi_inner_loop_ex flags
+LOOP_RESUME = 2
 ADAM_HIGHER = 0
 ADAM_HYPERGRAD = 1
 ADAM_TORCH = 2
@@ -88,6 +90,8 @@ SIGNATURES = {
                                            _I32, _P, _P, _P]),
     "psvi_inner_loop": (_I32, [_P, _P, _P, _P, _P, _U64, _U64, _I32, _P, _P, _P,
                                ctypes.POINTER(AdamHP), _P, _P, _SZ, _P]),
+    "psvi_inner_loop_ex": (_I32, [_P, _P, _P, _P, _P, _U64, _U64, _I32, _P, _P, _P,
+                                  ctypes.POINTER(AdamHP), _P, _P, _SZ, _I32, _P]),
     "psvi_outer_elbo_grad": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                     _SZ, _P]),
     "psvi_outer_ablated_elbo_grad": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -8,6 +8,7 @@ torch tensors on the GPU; this module only checks shapes and passes pointers.
 import ctypes
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 from ._lib import AdamHP, NetDesc, check
@@ -34,10 +35,33 @@ def _need(t, name, numel, dtype=torch.float32):
         raise ValueError(f"{name} has {t.numel()} elements, expected {numel}")
 
 
+def _wrote(*tensors):
+    """Bump the version counters of tensors the library wrote in place (no
+    torch op saw the write), so that a resident inner-loop state keyed to
+    them is not taken up after it (InnerLoopPlan.inner_loop(keep=True))."""
+    for t in tensors:
+        if t is not None:
+            increment_version(t)
+
+
 def make_adam(lr, step, kind="higher", betas=(0.9, 0.999), eps=1e-8):
     k = {"higher": _lib.ADAM_HIGHER, "hypergrad": _lib.ADAM_HYPERGRAD,
          "torch": _lib.ADAM_TORCH}[kind]
     return AdamHP(float(lr), float(betas[0]), float(betas[1]), float(eps), int(step), k)
+
+
+class _Token:
+    """What a KEEP inner loop left resident: compared by tensor identity,
+    version counters, seed and the continuing Philox offset."""
+
+    __slots__ = ("tensors", "versions", "seed", "offset")
+
+    def __init__(self, tensors, versions, seed, offset):
+        self.tensors, self.versions, self.seed, self.offset = tensors, versions, seed, offset
+
+    def __eq__(self, o):
+        return (all(a is b for a, b in zip(self.tensors, o.tensors)) and self.versions == o.versions
+                and self.seed == o.seed and self.offset == o.offset)
 
 
 class InnerLoopPlan:
@@ -46,6 +70,7 @@ class InnerLoopPlan:
 
     def __init__(self, family, layers, S, M, prior_sd=1.0, world=1, rank=0):
         self.lib = _lib.load()
+        self._resident = None  # inner_loop(keep=True)'s token
         self.family = family
         fam = {"meanfield": _lib.FAMILY_MEANFIELD, "fullcov": _lib.FAMILY_FULLCOV,
                "lenet": _lib.FAMILY_LENET}[family]
@@ -154,13 +179,27 @@ class InnerLoopPlan:
                                        _ptr(params), _ptr(adam_m), _ptr(adam_v),
                                        ctypes.byref(hp), _ptr(elbo_out), _ptr(ws),
                                        ws.numel(), _stream()), "psvi_inner_step")
+        _wrote(params, adam_m, adam_v)
         return elbo_out
 
     def inner_loop(self, u, z, w, params, adam_m, adam_v, T, lr, kind="higher", step0=1,
-                   eps=None, seed=0, offset=0, elbo_out=None, ws=None):
+                   eps=None, seed=0, offset=0, elbo_out=None, ws=None, keep=False):
         """T chained inner steps (psvi_inner_loop).  eps: (T, eps_count) device
         tensor, or None for in-library Philox draws (seed, offset + t * eps_stride).
-        Returns the (T,) float64 device tensor of negative ELBOs before each step."""
+        Returns the (T,) float64 device tensor of negative ELBOs before each step.
+
+        keep=True (Philox mode, full-cov plans with a tiled state): the loop's
+        state stays in ws -- the tiled corr / m / v, the next step's draw and
+        sample -- and the next call that continues this one takes it up
+        instead of redoing the first steps' fixed work (psvi_inner_loop_ex
+        KEEP / RESUME).  It continues when it passes the same ws, params,
+        adam_m, adam_v tensors, unmodified since (version counters; this
+        plan's own in-place writers bump them), the same seed and offset +
+        T * eps_stride.  The resumed numbers are those of one call over all
+        the steps, bit for bit, when the last call of the run has keep=False
+        (a keep=True call's last step takes the fused update with the next
+        sample, where a plain call's last step takes the packed-out one:
+        the same values up to fp32 rounding)."""
         _need(u, "u", self.M * self.in_features)
         _need(z, "z", self.M, torch.int32)
         _need(w, "w", self.M)
@@ -177,12 +216,33 @@ class InnerLoopPlan:
         if ws is None or ws.numel() < self.loop_ws_bytes:
             ws = torch.empty(self.loop_ws_bytes, dtype=torch.uint8, device=params.device)
         hp = make_adam(lr, step0, kind)
-        check(self.lib.psvi_inner_loop(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps),
-                                       int(seed) & (2**64 - 1), int(offset), T, _ptr(params),
-                                       _ptr(adam_m), _ptr(adam_v), ctypes.byref(hp),
-                                       _ptr(elbo_out), _ptr(ws), ws.numel(), _stream()),
-              "psvi_inner_loop")
+        flags = 0
+        tok, self._resident = self._resident, None
+        if eps is None:
+            if keep:
+                flags |= _lib.LOOP_KEEP
+            if tok is not None and tok == self._loop_token(ws, params, adam_m, adam_v, seed, offset):
+                flags |= _lib.LOOP_RESUME
+        else:
+            keep = False
+        check(self.lib.psvi_inner_loop_ex(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(eps),
+                                          int(seed) & (2**64 - 1), int(offset), T, _ptr(params),
+                                          _ptr(adam_m), _ptr(adam_v), ctypes.byref(hp),
+                                          _ptr(elbo_out), _ptr(ws), ws.numel(), flags, _stream()),
+              "psvi_inner_loop_ex")
+        _wrote(params, adam_m, adam_v, ws)
+        if keep and T > 0:
+            self._resident = self._loop_token(ws, params, adam_m, adam_v, seed,
+                                              int(offset) + T * self.eps_stride)
         return elbo_out[:T]
+
+    @staticmethod
+    def _loop_token(ws, params, adam_m, adam_v, seed, offset):
+        # the tensors themselves (held, so that no new tensor reuses the
+        # addresses) and their version counters: any torch write in between
+        # makes the next call start cold
+        ts = (ws, params, adam_m, adam_v)
+        return _Token(ts, tuple(t._version for t in ts), int(seed) & (2**64 - 1), int(offset))
 
     def elbo_grad(self, u, z, w, eps, params, include_kl=True, ws=None):
         self._inputs(u, z, w, eps)
@@ -353,6 +413,7 @@ class InnerLoopPlan:
                                             _ptr(adam_v), ctypes.byref(hp), _ptr(kl_out),
                                             _ptr(grad_out), int(bool(include_kl)), _stream()),
               "psvi_mf_phase_update")
+        _wrote(params, adam_m, adam_v)
 
     def mvn_sample(self, eps, params, x_shard):
         _need(eps, "eps", self.eps_count)
@@ -373,6 +434,7 @@ class InnerLoopPlan:
         check(self.lib.psvi_mvn_tiled_convert(self.handle, _ptr(params), _ptr(adam_m),
                                               _ptr(adam_v), _ptr(tstate), int(bool(to_tiled)),
                                               _stream()), "psvi_mvn_tiled_convert")
+        _wrote(params, adam_m, adam_v, tstate)
 
     def mvn_update_tiled(self, eps, g_shard, params, adam_m, adam_v, tstate, step, lr,
                          kind="higher", kl_out=None, include_kl=True, eps_next=None,
@@ -394,6 +456,7 @@ class InnerLoopPlan:
             self.handle, _ptr(eps), _ptr(g_shard), _ptr(params), _ptr(adam_m), _ptr(adam_v),
             _ptr(tstate), ctypes.byref(hp), _ptr(kl_out), int(bool(include_kl)), _ptr(eps_next),
             _ptr(x_next), _stream()), "psvi_mvn_phase_update_tiled")
+        _wrote(params, adam_m, adam_v, tstate)
 
     def mvn_net(self, u, z, w, x_recv, g_send, nll_out, draw=None):
         """draw = (eps_out, seed, offset): the next step's global eps drawn in the
@@ -436,12 +499,14 @@ class InnerLoopPlan:
                 self.handle, _ptr(eps), _ptr(g_shard), _ptr(params), _ptr(adam_m), _ptr(adam_v),
                 ctypes.byref(hp), _ptr(kl_out), int(bool(include_kl)), _ptr(eps_next),
                 _ptr(x_next), _stream()), "psvi_mvn_phase_update_sample")
+            _wrote(params, adam_m, adam_v)
             return
         check(self.lib.psvi_mvn_phase_update(self.handle, _ptr(eps), _ptr(g_shard),
                                              _ptr(params), _ptr(adam_m), _ptr(adam_v),
                                              ctypes.byref(hp), _ptr(kl_out), _ptr(grad_out),
                                              int(bool(include_kl)), _stream()),
               "psvi_mvn_phase_update")
+        _wrote(params, adam_m, adam_v)
 
 
 def randn_(out, seed, offset=0):

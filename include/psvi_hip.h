@@ -188,6 +188,39 @@ int psvi_inner_loop(const psvi_plan* plan, const float* u, const int32_t* z,
                     const psvi_adam_hp* hp, double* elbo_out, void* ws, size_t ws_bytes,
                     void* stream);
 
+/* psvi_inner_loop with the loop's state kept across calls (full-cov plans with a
+ * tiled state, Philox mode).  The calls of a run of inner steps split over
+ * several calls repeat the first steps' fixed work -- corr / m / v into the
+ * tiled layout, step 0's draw and sample -- because one call cannot know that
+ * the next continues it:
+ *   PSVI_LOOP_KEEP   the last step also draws (seed, offset + T * stride) and
+ *                    samples the next step's weights (the fused update, as
+ *                    every other step), the tiled corr / m / v stay in ws, and
+ *                    the packed params / adam_m / adam_v are written as usual;
+ *   PSVI_LOOP_RESUME start from that resident state when this call continues
+ *                    the last KEEP call on this plan: the same ws, params,
+ *                    adam_m, adam_v pointers and seed, and offset = its offset
+ *                    + T * stride.  The caller asserts that nothing wrote
+ *                    params / adam_m / adam_v / ws since (the Python
+ *                    InnerLoopPlan checks the tensors' version counters);
+ *                    otherwise -- or when the state does not match -- the call
+ *                    starts cold, as psvi_inner_loop.
+ * Every call drops the resident state first, so a RESUME after any other loop
+ * call on the plan starts cold.  RESUME without KEEP takes the state up and
+ * ends as a plain call.  Calls of T1, T2, ... steps, each resuming the last
+ * and all but the last with KEEP, give the numbers of one call of T1 + T2 +
+ * ... steps bit for bit (a KEEP call's last step is the fused update with the
+ * next sample, as every step but the last of a call; a plain call's last step
+ * writes the packed arrays directly: the same values up to fp32 rounding).
+ * Other plans and eps != NULL: the flags are ignored. */
+#define PSVI_LOOP_KEEP   1
+#define PSVI_LOOP_RESUME 2
+int psvi_inner_loop_ex(const psvi_plan* plan, const float* u, const int32_t* z,
+                       const float* w, const float* eps, uint64_t seed, uint64_t offset,
+                       int32_t T, float* params, float* adam_m, float* adam_v,
+                       const psvi_adam_hp* hp, double* elbo_out, void* ws, size_t ws_bytes,
+                       int32_t flags, void* stream);
+
 /* ---- sharded phases (any world; the caller runs the collectives) ------------
  * MEANFIELD (sample-parallel, replicated params):
  *   acc (ACC_COUNT floats, overwritten) <- [sum_s dW | sum_s dW*eps] over this
@@ -481,6 +514,14 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     workgroup per chunk with per-chunk slots
                                     and a slot sum, instead of looping the
                                     chunks inside each workgroup (A/B)          */
+#define PSVI_DBG_STREAM_BF_OFF 24     /* value: 1 = the tiled inner loop's streaming
+                                    update on the fp32 matrix instructions
+                                    instead of the bf16-piece (fp32-faithful)
+                                    kernel (A/B)                               */
+#define PSVI_DBG_BF_STAMPS 25        /* ptr: device uint64 buffer, 16 slots per
+                                    workgroup of the bf16-piece streaming
+                                    update: shader clocks summed per phase
+                                    (tools/bf_stamps.py)                       */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

@@ -158,12 +158,15 @@ def _offs(splits):
 def test_row_sharded_full_size(W, S, M):
     """The full-cov steps the scaling run executes: C4 (fn2 64-40-40-2,
     S = 1024, M = 200) over 8 ranks, and the weak-scaled headline (C3 shards:
-    S = 128 W, M = 100) at W = 2, 4, 8 -- rows of L x samples sharded
-    (nnz-balanced row split over n = 2600 / 1640 / 82, all_to_all split sizes,
-    the chunked update at K = S), the W ranks run in one process with the two
-    all_to_alls done as device copies of the same blocks.  Checked against world 1 on the same
+    S = 128 W, M = 100) at W = 2, 4, 8 -- rows of L x samples sharded (whole
+    64-row bands dealt by tile count over n = 2600 / 1640 / 82, all_to_all
+    split sizes, the segmented sample, the gradient mode of the update for the
+    assembled gradient and the K-split streaming update for the Adam step at
+    K = S > 128), the W ranks run in one process with the two all_to_alls done
+    as device copies of the same blocks.  Checked against world 1 on the same
     inputs (ELBO, assembled gradient, one Adam step) and against the oracle
-    (each rank's x shard; the gradient from the exchanged G)."""
+    (each rank's x shard; the gradient from the exchanged G).  The whole
+    multi-step schedule run() is pinned in test_hip_sharded_run.py."""
     from psvi.runtime import InnerLoopPlan
     from psvi.runtime.sharded import ShardedInnerLoop
 

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Per-phase shader clocks of the bf16-piece streaming update
+(mvn_stream_bf_kernel, DIAG build through PSVI_DBG_UPD_STAMPS): one C3
+inner loop in Philox mode (its first step runs the kernel), clocks summed over
+each workgroup's tiles, median over workgroups, per tile.
+
+  python3 tools/bf_stamps.py"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "blackbox-coresets-vi_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from psvi.runtime import InnerLoopPlan  # noqa: E402
+
+PH = ["pmv+prefetch", "dL (+diag sums)", "barrier 1", "stage eps+G ld+diag adam", "x' st0",
+      "x' st1", "flush", "barrier 2", "store eps'+split G"]
+
+
+def main():
+    layers, S, M = [(64, 40), (40, 40), (40, 2)], 128, 100
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    g = torch.Generator().manual_seed(0)
+    u = torch.randn(M, 64, generator=g).cuda()
+    z = (torch.rand(M, generator=g) < 0.5).to(torch.int32).cuda()
+    w = torch.full((M,), 8.0, device="cuda")
+    p = (torch.randn(plan.param_count, generator=g) * 0.01).cuda()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    lib = plan.lib
+    nwg = 256
+    st = torch.zeros(nwg * 16, dtype=torch.int64, device="cuda")
+    plan.inner_loop(u, z, w, p.clone(), m.clone(), v.clone(), 3, 1e-3, seed=1)
+    lib.psvi_debug_set_ptr(25, ctypes.c_void_p(st.data_ptr()))
+    plan.inner_loop(u, z, w, p.clone(), m.clone(), v.clone(), 2, 1e-3, seed=1)
+    torch.cuda.synchronize()
+    lib.psvi_debug_set_ptr(25, None)
+    a = st.cpu().numpy().reshape(nwg, 16).astype(np.float64)
+    a = a[a[:, 9] > 0]
+    tiles = a[:, 9]
+    print(f"{len(a)} workgroups, tiles per workgroup median {np.median(tiles):.1f}")
+    tot = 0.0
+    for q, name in enumerate(PH):
+        per = np.median(a[:, q] / tiles)
+        tot += per
+        print(f"  {name:28s} {per:8.0f} clocks / tile")
+    print(f"  {'sum':28s} {tot:8.0f}")
+    life = np.median(a[:, 10] - a[:, 12])
+    print(f"  workgroup life {life:.0f} clocks ({life / np.median(tiles):.0f} / tile)")
+
+
+if __name__ == "__main__":
+    main()
