@@ -40,6 +40,8 @@ N_DATA = 800
 LR = 1e-3
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (MI355X_MICROARCH.md, no sparsity)
+BF_PIECES = 6  # bf16 piece products per fp32-faithful product (mvn_stream_bf_kernel)
 
 
 def synthetic_inputs(device, seed=0):
@@ -90,7 +92,7 @@ def algorithmic_work(S, rows_frac=1.0, layers=LAYERS):
 # The PMC summary the roofline's `traffic` is read from, and the commit whose
 # bench it profiled (tools/round_session.sh pmc step: separate FETCH_SIZE /
 # WRITE_SIZE rocprofv3 passes of this bench); reported as `traffic_source`
-PMC_TRAFFIC = dict(file="profiles/r04_pmc_traffic.json", head="7b671a1")
+PMC_TRAFFIC = dict(file="profiles/r05_pmc_traffic.json", head="c0b54fb")
 
 
 def pmc_traffic(kernels, path=os.path.join(ROOT, PMC_TRAFFIC["file"])):
@@ -679,8 +681,8 @@ def run(rt, args, shapes=None):
         # dominant kernel: the update with the fused next-step sample (plus its
         # small slot-reduce kernel, inside the same event pair)
         wk = algorithmic_work_fused(S)
-        kname = ("mvn_stream_kernel (fused update + next-step sample, tiled state) + "
-                 "mvn_fwd_reduce_kernel")
+        kname = ("mvn_stream_bf_kernel (fused update + next-step sample, tiled state; "
+                 "fp32-faithful bf16-piece MFMA) + mvn_fwd_reduce_kernel")
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
@@ -704,7 +706,7 @@ def run(rt, args, shapes=None):
         roofline = dict(bound="mfma", achieved=round(wk["flops"] / upd_s / 1e12, 2),
                         peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s")
     roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
-                    traffic=pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"])
+                    traffic=pmc_traffic(["mvn_stream_bf_kernel", "mvn_fwd_reduce_kernel"])
                     if world == 1 else None,
                     traffic_source=dict(PMC_TRAFFIC, measured_in_this_run=False,
                                         method="rocprofv3 --pmc FETCH_SIZE, then --pmc "
@@ -715,6 +717,13 @@ def run(rt, args, shapes=None):
                     kernel=kname, algorithmic_bytes_per_launch=int(wk["bytes"]),
                     algorithmic_flops_per_launch=int(wk["flops"]),
                     floors_us=dict(hbm=round(hbm_s * 1e6, 2), mfma=round(mfma_s * 1e6, 2)),
+                    # the instructions the dominant kernel issues: each fp32
+                    # product as six bf16 piece products on v_mfma_f32_32x32x16_bf16
+                    executed=dict(unit="TFLOP/s (bf16 MFMA, 6 piece products per fp32 product)",
+                                  achieved=round(BF_PIECES * wk["flops"] / upd_s / 1e12, 1),
+                                  peak=BF16_MFMA_PEAK_TFLOPS,
+                                  frac=round(BF_PIECES * wk["flops"] / upd_s / 1e12
+                                             / BF16_MFMA_PEAK_TFLOPS, 4)) if world == 1 else None,
                     kernels={k: {kk: round(vv, 2) for kk, vv in d.items()}
                              for k, d in kernels.items()})
     # the whole inner step's algorithmic work at C3 (2.682 GFLOP,
