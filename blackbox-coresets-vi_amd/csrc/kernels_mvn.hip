@@ -46,6 +46,59 @@ constexpr int FBK = 64;    // k (columns of L) per LDS stage
 constexpr int FST = 128;   // samples per pass: 4 waves x 32
 constexpr int FLD = FBK + 4;  // LDS row stride: 16-byte rows (float4 stores, ds_read_b128)
 
+// bf16 pieces (fp32-faithful products on v_mfma_f32_32x32x16_bf16): the
+// helpers of mvn_stream_bf_kernel, mvn_fwd_seg_bf_kernel and the bf16 K-split update
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short bf8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ floatx16 mfma6(const bf8v (&x)[3], const bf8v (&y)[3], floatx16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[2], y[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[0], c, 0, 0, 0);
+    return c;
+}
+__device__ __forceinline__ bf8v cat44(s4v lo, s4v hi) {
+    return bf8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// LDS images of a 128 x 64 bf16 block, 128-byte rows.  Column image (the
+// transposed reads): 16-byte chunk c / 8 XORed with 4 on rows 2, 3 (mod 4), so
+// a 32-lane half's four rows of one 64-byte run fall on four bank ranges.  Row
+// image (x''s A operand, 8 columns per lane: c0 .. c0 + 3 and c0 + 8 .. c0 +
+// 11 for c0 = 16 m + 4 h): each 16-column group stored in the order 0-3, 8-11,
+// 4-7, 12-15, so a lane's 8 columns are one 16-byte chunk 2 m + h, and the
+// chunk XORed with (s / 2) mod 8, so a ds_read_b128 lane group's 16 rows fall
+// on 16 distinct (bank half, chunk) pairs.
+// split3 on two entries at once: packed conversions (v_cvt_pk_bf16_f32) and
+// packed subtractions; word p holds piece p of both entries (entry 0 low)
+__device__ __forceinline__ void split3_pk(f32x2 x, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+    typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+    auto cvt = [](f32x2 v) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf2v)); };
+    auto val = [](uint32_t w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; };
+    w0 = cvt(x);
+    const f32x2 r1 = x - val(w0);
+    w1 = cvt(r1);
+    w2 = cvt(r1 - val(w1));
+}
+// entries j, j + 1 of a fragment as fp32 (the pieces' values)
+__device__ __forceinline__ f32x2 bf_pair(bf8v v, int j) {
+    const uint32_t w = (uint32_t)(uint16_t)v[j] | ((uint32_t)(uint16_t)v[j + 1] << 16);
+    return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+constexpr int kBfImg = 128 * 128;  // bytes per plane image
+__device__ __forceinline__ int img_col(int s, int c) {
+    return s * 128 + (((c >> 3) ^ (((s >> 1) & 1) << 2)) << 4) + ((c & 7) << 1);
+}
+__device__ __forceinline__ int img_row(int s, int c) {
+    // column c: group m = c / 16, quarter q = (c / 4) % 4 -> chunk 2 m + (q & 1),
+    // half q >> 1 of the chunk
+    const int q = (c >> 2) & 3;
+    return s * 128 + ((((c >> 4) * 2 + (q & 1)) ^ ((s >> 1) & 7)) << 4) + ((q >> 1) << 3) + ((c & 3) << 1);
+}
+
 struct FwdArgs {
     const FwdItem* items;
     const float* params;
@@ -1139,11 +1192,28 @@ struct KsArgs {
 // addresses, fix-ups or zero selects at staging.  The first pass of the next
 // segment is loaded behind the last pass of this one (its latency overlaps the
 // hand-off and the epilogue).
+// BF: the dL GEMM on bf16 pieces (fp32-faithful, mvn_stream_bf_kernel's
+// products): a pass's G and eps blocks are split at staging into three bf16
+// planes each, in two halves of 64 samples (column images of 8 KB per plane,
+// read with ds_read_b64_tr_b16; 48 KB of LDS, two workgroups per CU), each
+// half's next loads issued as soon as it is staged.  The diagonal tile's row
+// sums come from the planes (their sum is the fp32 value exactly).
+constexpr int kKsBfImg = 64 * 128;  // bytes per plane image (64 samples x 64 columns)
+struct KsBfShared {
+    uint8_t img[6 * kKsBfImg];  // eps planes, then G planes; the epilogue's T tile after the passes
+    float red[2 * 4 * 64];
+};
+template <bool BF>
 __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
-    __shared__ __attribute__((aligned(16))) UpdShared<true> sh;
+    __shared__ __attribute__((aligned(16))) std::conditional_t<BF, KsBfShared, UpdShared<true>> sh;
     static_assert(kKsPass == USB, "one LDS stage per pass");
-    float* Gs = sh.Gs;
-    float* Es = sh.Es;
+    static_assert(64 * TLD * 4 <= 6 * kKsBfImg, "the epilogue tile fits the images");
+    float* Gs = nullptr;
+    float* Es = nullptr;
+    if constexpr (!BF) {
+        Gs = sh.Gs;
+        Es = sh.Es;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
     const int wr = wv >> 1, wc = wv & 1;
     const int col4 = tid & 15, srow = tid >> 4;
@@ -1209,9 +1279,64 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             *reinterpret_cast<float4*>(&Es[o]) = ereg[j];
         }
     };
+    // BF: half hp of a pass (samples 64 hp + srow + 16 j', registers j = 4 hp + j')
+    uint8_t* const Eb = BF ? reinterpret_cast<uint8_t*>(&sh) : nullptr;
+    uint8_t* const Gb = BF ? reinterpret_cast<uint8_t*>(&sh) + 3 * kKsBfImg : nullptr;
+    auto load_half = [&](const Ld& d, int pi, int hp) __attribute__((always_inline)) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * hp + jj;
+            const int s = pi * USB + srow + 16 * j;
+            const bool live = s < a.S;
+            const uint32_t go = live ? (uint32_t)(s * a.ldg + d.gcol) * 4u : kOOB;
+            const uint32_t eo = live ? (uint32_t)(d.eoff + s * d.n + d.ecol) * 4u : kOOB;
+            greg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0));
+            ereg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
+        }
+    };
+    auto stage_half = [&](int hp) __attribute__((always_inline)) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * hp + jj, sl = srow + 16 * jj;
+            uint32_t x[3][2], y[3][2];
+            split3_pk(f32x2{greg[j].x, greg[j].y}, x[0][0], x[1][0], x[2][0]);
+            split3_pk(f32x2{greg[j].z, greg[j].w}, x[0][1], x[1][1], x[2][1]);
+            split3_pk(f32x2{ereg[j].x, ereg[j].y}, y[0][0], y[1][0], y[2][0]);
+            split3_pk(f32x2{ereg[j].z, ereg[j].w}, y[0][1], y[1][1], y[2][1]);
+            const int o = img_col(sl, 4 * col4);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                *reinterpret_cast<u32x2*>(Gb + p * kKsBfImg + o) = u32x2{x[p][0], x[p][1]};
+                *reinterpret_cast<u32x2*>(Eb + p * kKsBfImg + o) = u32x2{y[p][0], y[p][1]};
+            }
+        }
+    };
+    // the transposed reads (mvn_stream_bf_kernel's): lane 4 qq + pp of its
+    // 16-lane group takes sample row qq, columns 4 pp .. + 3 of its 16
+    const int g16 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const uint8_t* const rda = BF ? Eb + img_col(8 * h + qq, 32 * wc + 16 * (g16 & 1) + 4 * pp) : nullptr;
+    const uint8_t* const rdb = BF ? Gb + img_col(8 * h + qq, 32 * wr + 16 * (g16 & 1) + 4 * pp) : nullptr;
+    auto read_ab = [&](int t, bf8v (&av)[3], bf8v (&bv)[3]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            typedef __attribute__((address_space(3))) s4v* lds_s4;
+            const int o = p * kKsBfImg + 2048 * t;  // sample rows 16 t + 8 h + qq (+ 4)
+            av[p] = cat44(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rda + o)),
+                          __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rda + o + 512)));
+            bv[p] = cat44(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rdb + o)),
+                          __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rdb + o + 512)));
+        }
+    };
     const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
     KsSeg sg_next = a.segs[sbeg < send ? sbeg : 0];
-    if (sbeg < send) load(desc(a.tiles[sg_next.tile]), sg_next.p0);
+    if (sbeg < send) {
+        if constexpr (BF) {
+            load_half(desc(a.tiles[sg_next.tile]), sg_next.p0, 0);
+            load_half(desc(a.tiles[sg_next.tile]), sg_next.p0, 1);
+        } else {
+            load(desc(a.tiles[sg_next.tile]), sg_next.p0);
+        }
+    }
     for (int si = sbeg; si < send; ++si) {  // uniform
         if (dg) tprev = __builtin_amdgcn_s_memtime();
         const KsSeg sg = sg_next;
@@ -1267,6 +1392,46 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
         float dgm = 0.f, dgs = 0.f;
         const bool whole = sg.slot < 0;
         for (int pi = sg.p0; pi < sg.p1; ++pi) {  // uniform
+            const bool inseg = pi + 1 < sg.p1;
+            if constexpr (BF) {
+#pragma unroll
+                for (int hp = 0; hp < 2; ++hp) {
+                    __syncthreads();  // every wave done with the images
+                    stage_half(hp);
+                    __syncthreads();
+                    if (pi == sg.p0 && hp == 0) mark(1);
+                    // this half's registers refilled at once: the next pass's
+                    // half (after the segment's last pass, the next segment's)
+                    if (inseg || more) load_half(inseg ? cur : nxt, inseg ? pi + 1 : sg_next.p0, hp);
+                    if (pi * USB + 64 * hp >= a.S) continue;  // uniform: a ragged last pass
+                    // one K-step of fragments at a time (the other workgroup on
+                    // the CU covers the LDS latency; a second set spills)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bf8v fa[3], fb[3];
+                        read_ab(t, fa, fb);
+                        acc = mfma6(fa, fb, acc);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    if (tl.diag && wc == wr) {
+                        // the diagonal quadrants: lane (c = r, h) reads eps and G of
+                        // the same row for its samples -- sum_s G, sum_s G eps
+#pragma unroll 1
+                        for (int t = 0; t < 4; ++t) {
+                            bf8v av[3], bv[3];
+                            read_ab(t, av, bv);
+#pragma unroll
+                            for (int j = 0; j < 8; j += 2) {
+                                const f32x2 e = (bf_pair(av[0], j) + bf_pair(av[1], j)) + bf_pair(av[2], j);
+                                const f32x2 gg = (bf_pair(bv[0], j) + bf_pair(bv[1], j)) + bf_pair(bv[2], j);
+                                dgm += gg[0] + gg[1];
+                                dgs = fmaf(gg[1], e[1], fmaf(gg[0], e[0], dgs));
+                            }
+                        }
+                    }
+                }
+                continue;
+            }
             stage();
             __syncthreads();
             if (pi == sg.p0) mark(1);
@@ -1274,10 +1439,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             // segment's last pass, the next segment's first (corr / m / v are
             // loaded at the epilogue: prefetched here they keep 48 more
             // registers live across the MFMAs and the kernel takes scratch)
-            {
-                const bool inseg = pi + 1 < sg.p1;
-                if (inseg || more) load(inseg ? cur : nxt, inseg ? pi + 1 : sg_next.p0);
-            }
+            if (inseg || more) load(inseg ? cur : nxt, inseg ? pi + 1 : sg_next.p0);
             const int kend = min(USB, a.S - pi * USB);
             if (tl.diag) {
                 // column j of Es is row r0 + j of the band
@@ -1301,6 +1463,14 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
             }
             __syncthreads();  // every wave done with Gs / Es
+        }
+        if (BF && tl.diag) {
+            // the two halves' sums; row 32 wr + l32 of the band kept by wave 0
+            // in lanes 0..31 and by wave 3 in lanes 32..63, so that the
+            // epilogue's wave sum red[w 64 + j] sees row j once
+            dgm += __shfl_xor(dgm, 32, kWave);
+            dgs += __shfl_xor(dgs, 32, kWave);
+            if (!((wv == 0 && h == 0) || (wv == 3 && h == 1))) dgm = dgs = 0.f;
         }
         mark(2);
         if (!whole) {
@@ -1339,7 +1509,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             dgm = dgs = 0.f;
             // the partials KP at a time (all their loads in flight together),
             // added in pass order; past nc the last one is loaded again, not added
-            constexpr int KP = 4;
+            constexpr int KP = BF ? 2 : 4;  // BF: fewer registers beside the image bases
             for (int c0 = 0; c0 < sg.nc; c0 += KP) {  // uniform
                 float4 part[KP][4];
                 f32x2 pd[KP];
@@ -1375,7 +1545,8 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
         if (whole) load_pmv();
         // ---- Adam epilogue: D[i = c][j = r] (j = lane & 31, i = (q & 3) + 8 (q >> 2) + 4 h)
         // -> T[r][c] in Es, then the rows' 256-byte runs of corr / m / v
-        float* T = Es;
+        float* T = BF ? reinterpret_cast<float*>(&sh) : Es;
+        if constexpr (BF) __syncthreads();  // the images are T now: every wave past its last reads
 #pragma unroll
         for (int g = 0; g < 4; ++g)
             *reinterpret_cast<float4*>(&T[(32 * wr + l32) * TLD + 32 * wc + 8 * g + 4 * h]) =
@@ -1562,7 +1733,6 @@ __device__ __forceinline__ float adam_fast_k(const AdamC& a, float p, float g, f
 
 constexpr int kStrBuf = 128 * 16;  // float4 per eps block buffer ([128 samples][16 slots])
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // plain vector loads / stores (no memcpy)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // adam_fast_k on two entries at once: the arithmetic as v_pk_mul_f32 /
 // v_pk_fma_f32 / v_pk_add_f32 (two fp32 lanes per instruction on gfx950),
@@ -1990,56 +2160,6 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 //   L'   (x''s B operand): the new corr entries, split in the accumulators'
 //        registers (the accumulator-as-operand order of the 32x32x16 form).
 // Tiled state, slots, the diagonal's mean / sd and the KL as mvn_stream_kernel.
-typedef short bf8v __attribute__((ext_vector_type(8)));
-typedef short s4v __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ floatx16 mfma6(const bf8v (&x)[3], const bf8v (&y)[3], floatx16 c) {
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[2], y[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[2], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[0], c, 0, 0, 0);
-    return c;
-}
-__device__ __forceinline__ bf8v cat44(s4v lo, s4v hi) {
-    return bf8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-// LDS images of a 128 x 64 bf16 block, 128-byte rows.  Column image (the
-// transposed reads): 16-byte chunk c / 8 XORed with 4 on rows 2, 3 (mod 4), so
-// a 32-lane half's four rows of one 64-byte run fall on four bank ranges.  Row
-// image (x''s A operand, 8 columns per lane: c0 .. c0 + 3 and c0 + 8 .. c0 +
-// 11 for c0 = 16 m + 4 h): each 16-column group stored in the order 0-3, 8-11,
-// 4-7, 12-15, so a lane's 8 columns are one 16-byte chunk 2 m + h, and the
-// chunk XORed with (s / 2) mod 8, so a ds_read_b128 lane group's 16 rows fall
-// on 16 distinct (bank half, chunk) pairs.
-// split3 on two entries at once: packed conversions (v_cvt_pk_bf16_f32) and
-// packed subtractions; word p holds piece p of both entries (entry 0 low)
-__device__ __forceinline__ void split3_pk(f32x2 x, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
-    typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
-    auto cvt = [](f32x2 v) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf2v)); };
-    auto val = [](uint32_t w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; };
-    w0 = cvt(x);
-    const f32x2 r1 = x - val(w0);
-    w1 = cvt(r1);
-    w2 = cvt(r1 - val(w1));
-}
-// entries j, j + 1 of a fragment as fp32 (the pieces' values)
-__device__ __forceinline__ f32x2 bf_pair(bf8v v, int j) {
-    const uint32_t w = (uint32_t)(uint16_t)v[j] | ((uint32_t)(uint16_t)v[j + 1] << 16);
-    return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-}
-constexpr int kBfImg = 128 * 128;  // bytes per plane image
-__device__ __forceinline__ int img_col(int s, int c) {
-    return s * 128 + (((c >> 3) ^ (((s >> 1) & 1) << 2)) << 4) + ((c & 7) << 1);
-}
-__device__ __forceinline__ int img_row(int s, int c) {
-    // column c: group m = c / 16, quarter q = (c / 4) % 4 -> chunk 2 m + (q & 1),
-    // half q >> 1 of the chunk
-    const int q = (c >> 2) & 3;
-    return s * 128 + ((((c >> 4) * 2 + (q & 1)) ^ ((s >> 1) & 7)) << 4) + ((q >> 1) << 3) + ((c & 3) << 1);
-}
-
 // DIAG: per-phase shader clocks summed over the run's tiles (thread 0) into
 // the stamp buffer (tools/bf_stamps.py)
 template <int KIND, bool DIAG = false>
@@ -2463,6 +2583,8 @@ int g_stream_bf_off = 0;  // psvi_debug_set(PSVI_DBG_STREAM_BF_OFF, 1): the fp32
 unsigned long long* g_bf_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_BF_STAMPS, buf)
 int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128 (A/B)
 int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
+int g_ks_bf_off = 0;   // psvi_debug_set(PSVI_DBG_KSTREAM_BF_OFF, 1): the fp32 K-split update (A/B)
+int g_fs_bf_off = 0;   // psvi_debug_set(PSVI_DBG_FWD_SEG_BF_OFF, 1): the fp32 segmented sample (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -2473,6 +2595,177 @@ static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
         la[l].poff = p.lay[l].poff;
         la[l].eoff = p.lay[l].eoff;
         la[l].tbase = p.lay[l].tbase;
+    }
+}
+
+// mvn_fwd_seg_bf_kernel: mvn_fwd_seg_kernel with the GEMM on the bf16 matrix
+// cores, fp32-faithful (the pieces of mvn_stream_bf_kernel): each stage's eps
+// block [128 s][64 k] and masked L block [64 r][64 k] are split at staging
+// into three bf16 planes each, stored as row images (128-byte rows, 16-byte
+// chunk c of row s at c ^ ((s >> 1) & 7)), and both operands read with one
+// ds_read_b128 per plane: lane (l32, h) of K-step t takes k = 16 t + 8 h ..
+// + 7 of row l32 -- the same k order for A (eps, M = samples) and B (L, N =
+// rows), so the accumulators, slots and reduce are mvn_fwd_seg_kernel's.
+// 72 KB of LDS: two workgroups per CU, as the fp32 kernel.
+constexpr int kSegEImg = FST * 128;       // bytes per eps plane image
+constexpr int kSegLImg = kFwdRows * 128;  // bytes per L plane image
+__device__ __forceinline__ int seg_img(int s, int chunk) {
+    return s * 128 + ((chunk ^ ((s >> 1) & 7)) << 4);
+}
+__global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smb[3 * kSegEImg + 3 * kSegLImg];
+    uint8_t* const Eb = smb;
+    uint8_t* const Lb = smb + 3 * kSegEImg;
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
+    const int col4 = tid & 15, srow = tid >> 4;
+    constexpr int FT = kFwdRows / 32, LJ = kFwdRows / 16;
+    const rsrc_t re = make_rsrc(a.eps, 4 * a.e_total);
+    const rsrc_t rp = make_rsrc(a.params, 4 * a.pcount);
+    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
+    if (sbeg >= send) return;  // uniform, before any barrier
+    // a stage: column block kb of segment si (si == send: past the run's end)
+    struct St {
+        int si, kb, n, corr, eoff, r0, r1, s0, k1;
+    };
+    auto stage_at = [&](int si, int kb) __attribute__((always_inline)) {
+        St d;
+        d.si = si;
+        d.kb = kb;
+        if (si >= send) return d;
+        const FsSeg g = a.segs[si];
+        int poff = (int)a.lay[0].poff;
+        d.n = a.lay[0].n;
+        d.eoff = (int)a.lay[0].eoff;
+#pragma unroll
+        for (int l = 1; l < kMaxL; ++l)  // select: a dynamic index into the arguments goes to scratch
+            if (g.layer == l) {
+                d.n = a.lay[l].n;
+                d.eoff = (int)a.lay[l].eoff;
+                poff = (int)a.lay[l].poff;
+            }
+        d.corr = poff + 2 * d.n;
+        d.r0 = g.r0;
+        d.r1 = g.r1;
+        d.s0 = g.pass * FST;
+        d.k1 = g.k1;
+        if (kb < 0) d.kb = g.k0;
+        return d;
+    };
+    auto next = [&](const St& d) __attribute__((always_inline)) {
+        return d.kb + FBK < d.k1 ? stage_at(d.si, d.kb + FBK) : stage_at(d.si + 1, -1);
+    };
+    // two register sets: stage i + 2 is loaded behind stage i's MFMAs
+    float4 lreg[2][LJ], ereg[2][8];
+    auto fetch = [&](const St& d, float4 (&lr)[LJ], float4 (&er)[8]) __attribute__((always_inline)) {
+        if (d.si >= send) return;  // uniform
+#pragma unroll
+        for (int j = 0; j < LJ; ++j) {
+            const int r = d.r0 + srow + 16 * j;
+            const int ro = r >= 1 ? (int)((int64_t)r * (r - 1) / 2) : 0;
+            lr[j] = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(rp, (uint32_t)(d.corr + ro + d.kb + 4 * col4) * 4u, 0, 0));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int sr = d.s0 + srow + 16 * j;
+            const uint32_t eo = sr < a.S ? (uint32_t)(d.eoff + sr * d.n + d.kb + 4 * col4) * 4u : kOOB;
+            er[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
+        }
+    };
+    // a thread's 4 columns 4 col4 .. + 3: half (col4 & 1) of chunk col4 >> 1
+    const int cw = (col4 & 1) * 8;
+    auto put = [&](uint8_t* img, int pbytes, int row, float4 v) __attribute__((always_inline)) {
+        uint32_t x0[2], x1[2], x2[2];
+        split3_pk(f32x2{v.x, v.y}, x0[0], x1[0], x2[0]);
+        split3_pk(f32x2{v.z, v.w}, x0[1], x1[1], x2[1]);
+        uint8_t* q = img + seg_img(row, col4 >> 1) + cw;
+        *reinterpret_cast<u32x2*>(q) = u32x2{x0[0], x0[1]};
+        *reinterpret_cast<u32x2*>(q + pbytes) = u32x2{x1[0], x1[1]};
+        *reinterpret_cast<u32x2*>(q + 2 * pbytes) = u32x2{x2[0], x2[1]};
+    };
+    auto stage = [&](const St& d, const float4 (&lr)[LJ], const float4 (&er)[8]) __attribute__((always_inline)) {
+        const int c = d.kb + 4 * col4;
+#pragma unroll
+        for (int j = 0; j < LJ; ++j) {
+            // entries outside the block's rows / the strict lower triangle are 0
+            const int r = d.r0 + srow + 16 * j;
+            const bool rok = r < d.r1 && r <= d.n - 2;
+            const float4 v = lr[j];
+            float4 o;
+            o.x = rok && c + 0 < r ? v.x : 0.f;
+            o.y = rok && c + 1 < r ? v.y : 0.f;
+            o.z = rok && c + 2 < r ? v.z : 0.f;
+            o.w = rok && c + 3 < r ? v.w : 0.f;
+            put(Lb, kSegLImg, srow + 16 * j, o);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) put(Eb, kSegEImg, srow + 16 * j, er[j]);
+    };
+    // operand bases: A row 32 wv + l32 of the eps image, B rows 32 t + l32 of
+    // the L image; K-step t, half h -> chunk 2 t + h (the swizzle of row s
+    // depends on s alone: (s >> 1) & 7 = (l32 >> 1) & 7 for both)
+    const int sw = (l32 >> 1) & 7;
+    const uint8_t* const ra = Eb + (32 * wv + l32) * 128;
+    const uint8_t* const rb = Lb + l32 * 128;
+    floatx16 acc[FT];
+#pragma unroll
+    for (int t = 0; t < FT; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+    St cur = stage_at(sbeg, -1);
+    St nx1 = next(cur);
+    fetch(cur, lreg[0], ereg[0]);
+    fetch(nx1, lreg[1], ereg[1]);
+    // one stage with register set P: stage, load the stage after next into P,
+    // the MFMAs; at a segment's last stage its slot is written
+    auto body = [&](auto P_c) __attribute__((always_inline)) {
+        constexpr int P = decltype(P_c)::value;
+        __syncthreads();  // previous stage's MFMAs done with the LDS
+        stage(cur, lreg[P], ereg[P]);
+        __syncthreads();
+        const St nx2 = next(nx1);
+        fetch(nx2, lreg[P], ereg[P]);
+        const bool wave_live = cur.s0 + 32 * wv < a.S;
+        if (wave_live) {
+#pragma unroll
+            for (int t = 0; t < FBK / 16; ++t) {
+                const int co = ((2 * t + h) ^ sw) << 4;
+                bf8v av[3], bv[FT][3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    av[p] = *reinterpret_cast<const bf8v*>(ra + p * kSegEImg + co);
+#pragma unroll
+                    for (int u = 0; u < FT; ++u)
+                        bv[u][p] = *reinterpret_cast<const bf8v*>(rb + p * kSegLImg + 32 * 128 * u + co);
+                }
+#pragma unroll
+                for (int u = 0; u < FT; ++u) acc[u] = mfma6(av, bv[u], acc[u]);
+            }
+        }
+        if (nx1.si != cur.si) {  // uniform: the segment's last stage
+            // the accumulators in fragment order, as mvn_fwd_seg_kernel
+            if (wave_live) {
+                const FsSeg g = a.segs[cur.si];
+                float* slot = a.part + (size_t)g.slot * FST * kFwdRows + (size_t)wv * FT * 16 * 64 + lane;
+#pragma unroll
+                for (int t = 0; t < FT; ++t)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) slot[(t * 16 + q) * 64] = acc[t][q];
+            }
+#pragma unroll
+            for (int t = 0; t < FT; ++t)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+        }
+        cur = nx1;
+        nx1 = nx2;
+    };
+    for (;;) {  // uniform
+        body(std::integral_constant<int, 0>{});
+        if (cur.si >= send) break;
+        body(std::integral_constant<int, 1>{});
+        if (cur.si >= send) break;
     }
 }
 
@@ -2626,7 +2919,10 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
         a.slot_rows = FST;
         a.slot_frag = 1;
         a.abl = 0;
-        hipLaunchKernelGGL(mvn_fwd_seg_kernel, dim3(p.n_fswg), dim3(256), 0, st, a);
+        if (g_fs_bf_off || a.stamps)
+            hipLaunchKernelGGL(mvn_fwd_seg_kernel, dim3(p.n_fswg), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL(mvn_fwd_seg_bf_kernel, dim3(p.n_fswg), dim3(256), 0, st, a);
         hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_fs_rb, FST / kRedSpb), dim3(256), 0, st,
                            p.d_fs_rb, p.d_fs_part, a, x_shard);
         return hipGetLastError();
@@ -2841,7 +3137,10 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         k.adam = a.adam;
         k.stamps = g_upd_stamps;
         fill_layers(p, k.lay);
-        hipLaunchKernelGGL(mvn_kstream_kernel, dim3(p.n_kwg), block, 0, st, k);
+        if (g_ks_bf_off || k.stamps)
+            hipLaunchKernelGGL(mvn_kstream_kernel<false>, dim3(p.n_kwg), block, 0, st, k);
+        else
+            hipLaunchKernelGGL(mvn_kstream_kernel<true>, dim3(p.n_kwg), block, 0, st, k);
         if (eps_next) {
             const hipError_t e = hipGetLastError();
             return e != hipSuccess ? e : launch_mvn_fwd(p, eps_next, params, x_next, st);

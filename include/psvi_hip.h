@@ -522,6 +522,12 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     workgroup of the bf16-piece streaming
                                     update: shader clocks summed per phase
                                     (tools/bf_stamps.py)                       */
+#define PSVI_DBG_FWD_SEG_BF_OFF 26   /* value: 1 = the segmented sample (K = S > 128)
+                                    on the fp32 MFMA kernel instead of the
+                                    bf16-piece (fp32-faithful) one (A/B)      */
+#define PSVI_DBG_KSTREAM_BF_OFF 27   /* value: 1 = the K-split update (K = S > 128)
+                                    on the fp32 MFMA kernel instead of the
+                                    bf16-piece (fp32-faithful) one (A/B)      */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
