@@ -29,6 +29,7 @@ extern int g_ks_off;                     // kernels_mvn.hip
 extern int g_fs_off;                     // kernels_mvn.hip
 extern int g_fs_bf_off;                  // kernels_mvn.hip
 extern int g_ks_bf_off;                  // kernels_mvn.hip
+extern int g_stream_bf2_off;              // kernels_mvn.hip
 static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
 extern int g_lenet_gemm_valu;            // kernels_lenet.hip
 extern int g_lenet_conv_valu;            // kernels_lenet.hip
@@ -619,6 +620,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
         case PSVI_DBG_FWD_SEG_BF_OFF: g_fs_bf_off = value; return 0;
         case PSVI_DBG_KSTREAM_BF_OFF: g_ks_bf_off = value; return 0;
+        case PSVI_DBG_STREAM_BF2_OFF: g_stream_bf2_off = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_NET_MLOOP_OFF: g_net_mloop_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;

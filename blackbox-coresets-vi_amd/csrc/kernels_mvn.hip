@@ -887,11 +887,11 @@ __device__ __forceinline__ void upd_chunk(const UpdArgs& a, const UpdChunk& ch,
                     const int tmb = __builtin_amdgcn_readfirstlane((int)((a.tm - a.tp) * 4));
                     const int tvb = __builtin_amdgcn_readfirstlane((int)((a.tv - a.tp) * 4));
                     const uint32_t ob = (uint32_t)(o * 4);
-                    __builtin_amdgcn_raw_buffer_store_b128(
+                    BSTORE128(
                         __builtin_bit_cast(u32x4, make_float4(pn[0], pn[1], pn[2], pn[3])), rs_t, ob, 0, 16);
-                    __builtin_amdgcn_raw_buffer_store_b128(
+                    BSTORE128(
                         __builtin_bit_cast(u32x4, make_float4(mn[0], mn[1], mn[2], mn[3])), rs_t, ob, tmb, 16);
-                    __builtin_amdgcn_raw_buffer_store_b128(
+                    BSTORE128(
                         __builtin_bit_cast(u32x4, make_float4(vn[0], vn[1], vn[2], vn[3])), rs_t, ob, tvb, 16);
                 }
                 if (FUSE)  // L_new fragment -> the [r][c] tile for the sample GEMM
@@ -1479,7 +1479,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             const uint32_t sbase = (uint32_t)((sg.slot + sg.ci) * kKsSlotFloats) * 4u;
 #pragma unroll
             for (int g = 0; g < 4; ++g)
-                __builtin_amdgcn_raw_buffer_store_b128(
+                BSTORE128(
                     __builtin_bit_cast(u32x4, make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2],
                                                           acc[4 * g + 3])),
                     rs, sbase + (uint32_t)(((wv * 4 + g) * 64 + lane) * 16), 0, 16);
@@ -2034,11 +2034,11 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
             if constexpr (SC1) {
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                 const uint32_t ob = (uint32_t)(o * 4);
-                __builtin_amdgcn_raw_buffer_store_b128(
+                BSTORE128(
                     __builtin_bit_cast(u32x4, f32x4{pn[0], pn[1], pn[2], pn[3]}), rs_t, ob, 0, 16);
-                __builtin_amdgcn_raw_buffer_store_b128(
+                BSTORE128(
                     __builtin_bit_cast(u32x4, f32x4{mn[0], mn[1], mn[2], mn[3]}), rs_t, ob, tmb, 16);
-                __builtin_amdgcn_raw_buffer_store_b128(
+                BSTORE128(
                     __builtin_bit_cast(u32x4, f32x4{vn[0], vn[1], vn[2], vn[3]}), rs_t, ob, tvb, 16);
             } else {
                 *reinterpret_cast<f32x4*>(a.tp + o) = f32x4{pn[0], pn[1], pn[2], pn[3]};
@@ -2454,9 +2454,9 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_bf_kernel(StrArgs a) {
         };
         auto store_g = [&](int g) __attribute__((always_inline)) {
             const uint32_t ob = (uint32_t)(frag_off(cur, g) * 4);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, P[g]), rs_t, ob, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, M4[g]), rs_t, ob, tmb, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, V4[g]), rs_t, ob, tvb, 16);
+            BSTORE128(__builtin_bit_cast(u32x4, P[g]), rs_t, ob, 0, 16);
+            BSTORE128(__builtin_bit_cast(u32x4, M4[g]), rs_t, ob, tmb, 16);
+            BSTORE128(__builtin_bit_cast(u32x4, V4[g]), rs_t, ob, tvb, 16);
         };
         auto lbf = [&](int st, int p) __attribute__((always_inline)) {
             return __builtin_bit_cast(bf8v, u32x4{lw[st][p][0], lw[st][p][1], lw[st][p][2], lw[st][p][3]});
@@ -2538,7 +2538,10 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_bf_kernel(StrArgs a) {
         __syncthreads();  // every wave done with the eps' image
         ph(7);
         if constexpr (has_next) store_row();
-        if constexpr (newband) split_G();
+        if constexpr (newband) {
+            split_G();
+            __syncthreads();  // the new band's G image written before any wave's dL reads it
+        }
         ph(8);
         if (DIAG && tid == 0) ++tph[9];
     };
@@ -2578,8 +2581,435 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_bf_kernel(StrArgs a) {
     }
 }
 
+// mvn_stream_bf2_kernel: mvn_stream_bf_kernel with two waves per SIMD.  Eight
+// waves per workgroup: wave (q, hk) with quadrant q = wv & 3 -- rows 32 wr,
+// columns 32 wc of the 64 x 64 tile, (wr, wc) = (q >> 1, q & 1) -- and sample
+// half hk = wv >> 2 (samples 64 hk .. 64 hk + 63).  The two waves of a
+// quadrant sit on one SIMD (waves w and w + 4), so one's vector work, LDS
+// waits and stores run beside the other's MFMAs:
+//   dL: each wave its samples' half of K (4 K-steps), the halves exchanged
+//       through LDS -- each wave gets the partner's partial of its own two
+//       column groups g = 2 hk, 2 hk + 1 and adds it (hk 0's + hk 1's, the
+//       same sum in both orders);
+//   Adam: each wave its two groups (corr / m / v fragments loaded, stored),
+//       and their L' pieces -- K-half st = hk of x''s B operand -- swapped
+//       with the partner through LDS;
+//   x': each wave its samples' two 32-row blocks over both K-halves (x'
+//       accumulators: 32 registers per wave);
+//   band end: the wc = 1 waves' x' partials added by the wc = 0 waves (per
+//       sample half) and written to the segment's slot, as before.
+// The exchanges use the eps column image after the dL reads (16 + 24 KB); the
+// next tile's eps planes are stored after them.  Images, pieces, swizzles and
+// the slot layout are mvn_stream_bf_kernel's.
+template <int KIND, bool DIAG = false>
+__global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t smb[9 * kBfImg];
+    uint8_t* const Eb = smb;
+    uint8_t* const Gb = smb + 3 * kBfImg;
+    uint8_t* const En = smb + 6 * kBfImg;
+    float* const Xs = reinterpret_cast<float*>(En);
+    float* const Xd = reinterpret_cast<float*>(Eb);                  // dL partials: 8 waves x 8 x 64 (16 KB)
+    uint32_t* const Xl = reinterpret_cast<uint32_t*>(Eb + 16384);    // L' pieces: 8 waves x 12 x 64 (24 KB)
+    float* const Xg = reinterpret_cast<float*>(Eb + 40960);          // diagonal sums: 8 waves x 2 x 64 (4 KB)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
+    const int q = wv & 3, hk = wv >> 2, wr = q >> 1, wc = q & 1, h = lane >> 5, l32 = lane & 31;
+    const int pw = wv ^ 4;  // the partner wave (same quadrant, other sample half)
+    const StreamRange R = a.ranges[blockIdx.x];
+    const int t0 = __builtin_amdgcn_readfirstlane(R.t0);
+    const int t1 = __builtin_amdgcn_readfirstlane(R.t1);
+    int slot = __builtin_amdgcn_readfirstlane(R.slot0);
+    const int S = a.S;  // 128
+    unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+    // (wave 0 as a whole: the stamps stay wave-uniform, in scalar registers)
+    auto ph = [&](int qq) __attribute__((always_inline)) {
+        if (DIAG && wv == 0) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            if (qq >= 0) tph[qq] += tt - tlast;
+            tlast = tt;
+        }
+    };
+
+    // ---- staging: 6 chunks of 16 bytes per thread: chunk j = plane j >> 1, row
+    // (tid >> 3) + 64 (j & 1), chunk tid % 8 of the tile's 64 columns
+    u32x4 stg[6];
+    const int srow0 = tid >> 3, ch = tid & 7;
+    const int st_col = srow0 * 128 + ((ch ^ (((srow0 >> 1) & 1) << 2)) << 4);
+    const int st_row0 = img_row(srow0, 8 * ch), st_row1 = img_row(srow0, 8 * ch + 4);
+    auto store_col = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+            *reinterpret_cast<u32x4*>(Eb + st_col + (j >> 1) * kBfImg + 8192 * (j & 1)) = stg[j];
+    };
+    auto store_row = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            uint8_t* img = En + (j >> 1) * kBfImg + 8192 * (j & 1);
+            *reinterpret_cast<u32x2*>(img + st_row0) = u32x2{stg[j][0], stg[j][1]};
+            *reinterpret_cast<u32x2*>(img + st_row1) = u32x2{stg[j][2], stg[j][3]};
+        }
+    };
+    // ---- the band's G slice [128 samples][64 rows]: 4 float4 per thread
+    f32x4 greg[4];
+    auto split_G = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int f = tid + 512 * j, s = f >> 4, c4 = f & 15;
+            uint32_t x[3][2];
+            split3_pk(f32x2{greg[j][0], greg[j][1]}, x[0][0], x[1][0], x[2][0]);
+            split3_pk(f32x2{greg[j][2], greg[j][3]}, x[0][1], x[1][1], x[2][1]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                *reinterpret_cast<u32x2*>(Gb + p * kBfImg + img_col(s, 4 * c4)) = u32x2{x[p][0], x[p][1]};
+        }
+    };
+    // this wave's two fragment groups g = 2 hk + gi of its quadrant (tiled order)
+    f32x4 P[2], M4[2], V4[2];
+    const rsrc_t rs_t = make_rsrc(a.tp, 0x7fffffff);
+    const rsrc_t rs_e = make_rsrc(a.ep, 0x7fffffff), rs_en = make_rsrc(a.enp, 0x7fffffff);
+    const rsrc_t rs_g = make_rsrc(a.g, 0x7fffffff);
+    const int tmb = __builtin_amdgcn_readfirstlane((int)((a.tm - a.tp) * 4));
+    const int tvb = __builtin_amdgcn_readfirstlane((int)((a.tv - a.tp) * 4));
+    const uint32_t vo_f = (uint32_t)(((q * 4 + 2 * hk) * 64 + lane) * 16);  // + 1024 gi
+    const uint32_t vo_g = (uint32_t)(4 * ((tid >> 4) * a.ldg + 4 * (tid & 15)));  // G rows tid / 16 (+ 32 j)
+    auto vo_planes = [&](const StrTile& T) __attribute__((always_inline)) {
+        return (uint32_t)(2 * (srow0 * T.npad + 8 * ch));
+    };
+    auto so_planes = [&](const StrTile& T, int j) __attribute__((always_inline)) {
+        return __builtin_amdgcn_readfirstlane((int)(2 * (T.pe + (j >> 1) * a.pl + (int64_t)(64 * (j & 1)) * T.npad)));
+    };
+    auto ldb = [&](rsrc_t r, uint32_t vo, int so) __attribute__((always_inline)) {
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+    };
+    auto load_G = [&](const StrTile& T, int j) __attribute__((always_inline)) {
+        const int so = __builtin_amdgcn_readfirstlane(4 * (32 * j * a.ldg + T.xc + 64 * T.b));
+        greg[j] = __builtin_bit_cast(f32x4, ldb(rs_g, vo_g, so));
+    };
+    floatx16 xacc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int qq = 0; qq < 16; ++qq) xacc[j][qq] = 0.f;
+    float kld = 0.f;
+    f32x2 kl2 = {0.f, 0.f};
+    const int g16 = lane >> 4, qq4 = (lane >> 2) & 3, pp = lane & 3;
+    const int ca = 32 * wc + 16 * (g16 & 1) + 4 * pp;  // eps column (dL's A)
+    const int cg = 32 * wr + 16 * (g16 & 1) + 4 * pp;  // G column (dL's B)
+    const uint8_t* const rda = Eb + img_col(8 * h + qq4, ca);
+    const uint8_t* const rdb = Gb + img_col(8 * h + qq4, cg);
+    const int xsw = (l32 >> 1) & 7;
+
+    int tl = __builtin_amdgcn_readfirstlane(R.lbk0 >> 28);
+    int tb_ = __builtin_amdgcn_readfirstlane((R.lbk0 >> 14) & 0x3fff);
+    int tk = __builtin_amdgcn_readfirstlane(R.lbk0 & 0x3fff);
+    StrTile cur = str_tile(a, tl, tb_, tk);
+    {
+        const uint32_t vo = vo_planes(cur);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) load_G(cur, j);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) stg[j] = ldb(rs_e, vo, so_planes(cur, j));
+        store_col();
+#pragma unroll
+        for (int j = 0; j < 6; ++j) stg[j] = ldb(rs_en, vo, so_planes(cur, j));
+        store_row();
+        split_G();
+    }
+    __syncthreads();
+
+    // phase A's loads: 0..5 this tile's corr / m / v fragments (2 groups x 3),
+    // 6..11 the next tile's eps planes
+    auto issue_a = [&](int qi, const StrTile& nxt, bool has_next, uint32_t vo_n) __attribute__((always_inline)) {
+        if (qi < 6) {
+            const int gi = qi / 3, which = qi % 3;
+            const int so = __builtin_amdgcn_readfirstlane((int)(cur.tb * 4));
+            const u32x4 x = ldb(rs_t, vo_f + 1024 * gi, which == 0 ? so : which == 1 ? so + tmb : so + tvb);
+            if (which == 0) P[gi] = __builtin_bit_cast(f32x4, x);
+            else if (which == 1) M4[gi] = __builtin_bit_cast(f32x4, x);
+            else V4[gi] = __builtin_bit_cast(f32x4, x);
+        } else if (has_next) {
+            stg[qi - 6] = ldb(rs_e, vo_n, so_planes(nxt, qi - 6));
+        }
+    };
+    // phase B's loads: 0..5 the next tile's eps' planes, 6..9 the next band's G
+    auto issue_b = [&](int qi, const StrTile& nxt, bool has_next, bool newband, uint32_t vo_n) __attribute__((always_inline)) {
+        if (qi < 6) {
+            if (has_next) stg[qi] = ldb(rs_en, vo_n, so_planes(nxt, qi));
+        } else if (newband) {
+            load_G(nxt, qi - 6);
+        }
+    };
+
+    auto tile = [&](const StrTile& nxt, auto has_next_c, auto newband_c) __attribute__((always_inline)) {
+        constexpr bool has_next = decltype(has_next_c)::value;
+        constexpr bool newband = decltype(newband_c)::value;
+        ph(-1);
+        const bool diag = cur.k == cur.b && wc == wr;  // wave-uniform
+        const uint32_t vo_n = vo_planes(nxt);
+        // ---- phase A: this wave's half of K (sample rows 64 hk + 16 t')
+        floatx16 acc;
+#pragma unroll
+        for (int qq = 0; qq < 16; ++qq) acc[qq] = 0.f;
+        float dgm = 0.f, dgs = 0.f;
+        auto read_ab = [&](int t, bf8v (&av)[3], bf8v (&bv)[3]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                typedef __attribute__((address_space(3))) s4v* lds_s4;
+                const int o = p * kBfImg + 2048 * t;
+                av[p] = cat44(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rda + o)),
+                              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rda + o + 512)));
+                bv[p] = cat44(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rdb + o)),
+                              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rdb + o + 512)));
+            }
+        };
+        // one K-step of fragments at a time: the SIMD's other wave covers the
+        // LDS latency (a second set would spill)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            bf8v fa[3], fb[3];
+            read_ab(4 * hk + t, fa, fb);
+#pragma unroll
+            for (int qi = 3 * t; qi < 3 * t + 3; ++qi) issue_a(qi, nxt, has_next, vo_n);
+            acc = mfma6(fa, fb, acc);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (diag) {
+#pragma unroll 1
+            for (int t = 0; t < 4; ++t) {
+                bf8v av[3], bv[3];
+                read_ab(4 * hk + t, av, bv);
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    const f32x2 e = (bf_pair(av[0], j) + bf_pair(av[1], j)) + bf_pair(av[2], j);
+                    const f32x2 gg = (bf_pair(bv[0], j) + bf_pair(bv[1], j)) + bf_pair(bv[2], j);
+                    dgm += gg[0] + gg[1];
+                    dgs = fmaf(gg[1], e[1], fmaf(gg[0], e[0], dgs));
+                }
+            }
+        }
+        ph(1);
+        __syncthreads();  // B1: every wave done with the eps and G images of this tile
+        ph(2);
+        // ---- the partner's partial of this wave's groups: send the other two
+        // (wave-uniform selects between constant accumulator indices: a
+        // run-time index into the accumulators would go through scratch)
+        auto accg = [&](int gsel, int e) __attribute__((always_inline)) {
+            return hk == 0 ? acc[4 * (gsel + 2) + e] : acc[4 * gsel + e];  // gsel of the OTHER half
+        };
+        auto accown = [&](int gi, int e) __attribute__((always_inline)) {
+            return hk == 0 ? acc[4 * gi + e] : acc[4 * (gi + 2) + e];
+        };
+        {
+#pragma unroll
+            for (int gi = 0; gi < 2; ++gi)
+                *reinterpret_cast<f32x4*>(Xd + ((wv * 2 + gi) * 64 + lane) * 4) =
+                    f32x4{accg(gi, 0), accg(gi, 1), accg(gi, 2), accg(gi, 3)};
+            if (diag && hk == 1) {
+                // the diagonal sums of this half for the partner (hk 0 runs the mean / sd Adam)
+                Xg[wv * 128 + lane] = dgm;
+                Xg[wv * 128 + 64 + lane] = dgs;
+            }
+        }
+        __syncthreads();  // B2
+        float dv[8];
+        {
+#pragma unroll
+            for (int gi = 0; gi < 2; ++gi) {
+                const f32x4 o4 = *reinterpret_cast<const f32x4*>(Xd + ((pw * 2 + gi) * 64 + lane) * 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dv[4 * gi + e] = accown(gi, e) + o4[e];
+            }
+            if (diag && hk == 0) {
+                dgm += Xg[pw * 128 + lane];
+                dgs += Xg[pw * 128 + 64 + lane];
+            }
+        }
+        const int n = cur.n, r = 64 * cur.b + 32 * wr + l32;
+        // ---- diagonal tile: mean / sd of the band's rows (the hk = 0 wave)
+        if (diag && hk == 0) {
+            dgm += __shfl_xor(dgm, 32, kWave);
+            dgs += __shfl_xor(dgs, 32, kWave);
+            if (h == 0 && r < n) {
+                const int pm = (int)cur.poff + r, ps = pm + n;
+                const float mu = a.params[pm], sdr = a.params[ps];
+                const float sp = softplus_f(sdr), sg = sigmoid_f(sdr);
+                float gmean = dgm, gsd = dgs * sg;
+                if (a.include_kl) {
+                    gmean += mu * a.inv_s0sq;
+                    gsd += (sp * a.inv_s0sq - 1.f / sp) * sg;
+                    kld += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
+                }
+                float mm = a.m[pm], vv = a.v[pm];
+                a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
+                a.m[pm] = mm;
+                a.v[pm] = vv;
+                mm = a.m[ps];
+                vv = a.v[ps];
+                a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
+                a.m[ps] = mm;
+                a.v[ps] = vv;
+            }
+        }
+        ph(3);
+        // ---- Adam on this wave's two groups, their stores and L' pieces
+        const bool rv = r >= 1 && r <= n - 2;
+        const float kls = a.include_kl ? a.inv_s0sq : 0.f;
+        uint32_t lwo[3][4], lwp[3][4];  // L' pieces [plane][element pair]: K-half hk, the partner's
+#pragma unroll
+        for (int gi = 0; gi < 2; ++gi) {
+            const int g = 2 * hk + gi;
+            const int cb = 64 * cur.k + 32 * wc + 8 * g + 4 * h;
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+                const f32x2 pv0 = {P[gi][e], P[gi][e + 1]};
+                kl2 = __builtin_elementwise_fma(pv0, pv0, kl2);
+                const f32x2 gvv = __builtin_elementwise_fma(pv0, f32x2{kls, kls}, f32x2{dv[4 * gi + e], dv[4 * gi + e + 1]});
+                const f32x2 gm = {rv && cb + e < r ? gvv[0] : 0.f, rv && cb + e + 1 < r ? gvv[1] : 0.f};
+                f32x2 mm = {M4[gi][e], M4[gi][e + 1]}, vv = {V4[gi][e], V4[gi][e + 1]};
+                const f32x2 pv = adam_fast_k2<KIND>(a.adam, pv0, gm, mm, vv);
+                P[gi][e] = pv[0];
+                P[gi][e + 1] = pv[1];
+                M4[gi][e] = mm[0];
+                M4[gi][e + 1] = mm[1];
+                V4[gi][e] = vv[0];
+                V4[gi][e + 1] = vv[1];
+                uint32_t w0, w1, w2;
+                split3_pk(pv, w0, w1, w2);
+                const int jp = (4 * gi + e) >> 1;  // g & 1 == gi
+                lwo[0][jp] = w0;
+                lwo[1][jp] = w1;
+                lwo[2][jp] = w2;
+            }
+            const uint32_t ob = (uint32_t)((cur.tb + (int64_t)((q * 4 + g) * 64 + lane) * 4) * 4);
+            BSTORE128(__builtin_bit_cast(u32x4, P[gi]), rs_t, ob, 0, 16);
+            BSTORE128(__builtin_bit_cast(u32x4, M4[gi]), rs_t, ob, tmb, 16);
+            BSTORE128(__builtin_bit_cast(u32x4, V4[gi]), rs_t, ob, tvb, 16);
+        }
+        // the pieces of K-half hk to the partner, its K-half back
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            *reinterpret_cast<u32x4*>(Xl + ((wv * 3 + p) * 64 + lane) * 4) =
+                u32x4{lwo[p][0], lwo[p][1], lwo[p][2], lwo[p][3]};
+        ph(4);
+        __syncthreads();  // B3
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            const u32x4 o4 = *reinterpret_cast<const u32x4*>(Xl + ((pw * 3 + p) * 64 + lane) * 4);
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) lwp[p][jp] = o4[jp];
+        }
+        __syncthreads();  // B4: the exchange scratch read; the eps image is free
+        if constexpr (has_next) store_col();  // the next tile's eps image
+        // ---- x' += eps' L'^T for this wave's sample blocks sb = 2 hk + j, both K-halves
+        // this wave's K-half first, then the partner's (st = hk, 1 - hk)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            const int st = ss == 0 ? hk : 1 - hk;
+            const uint8_t* const rx = En + l32 * 128 + (((2 * (2 * wc + st) + h) ^ xsw) << 4);
+            bf8v lb[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                lb[p] = ss == 0 ? __builtin_bit_cast(bf8v, u32x4{lwo[p][0], lwo[p][1], lwo[p][2], lwo[p][3]})
+                                : __builtin_bit_cast(bf8v, u32x4{lwp[p][0], lwp[p][1], lwp[p][2], lwp[p][3]});
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int sb = 2 * hk + j;
+                bf8v fx[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) fx[p] = *reinterpret_cast<const bf8v*>(rx + p * kBfImg + 4096 * sb);
+                xacc[j] = mfma6(fx, lb, xacc[j]);
+                {
+                    const int kk = 2 * ss + j, q0 = (10 * kk) / 4, q1 = (10 * (kk + 1)) / 4;
+#pragma unroll
+                    for (int qi = q0; qi < q1; ++qi) issue_b(qi, nxt, has_next, newband, vo_n);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        ph(5);
+        // ---- band end (or run end): the two column halves' x' partials -> the slot
+        if constexpr (!has_next || newband) {
+            __syncthreads();  // every wave done reading the eps' image (the scratch)
+            if (wc == 1) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int qq = 0; qq < 16; ++qq)
+                        Xs[(((wr * 2 + hk) * 2 + j) * 16 + qq) * 64 + lane] = xacc[j][qq];
+            }
+            __syncthreads();
+            if (wc == 0) {
+                // buffer stores: a scalar slot base, a per-lane 32-bit offset
+                const rsrc_t rs_p = make_rsrc(a.part, 0x7fffffff);
+                const int sob = __builtin_amdgcn_readfirstlane(slot * S * 64 * 4);
+                const uint32_t vb = (uint32_t)((32 * wr + l32 + 64 * (64 * hk + 4 * h)) * 4);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int qq = 0; qq < 16; ++qq) {
+                        const int sl = 32 * j + (qq & 3) + 8 * (qq >> 2);  // sample - 64 hk - 4 h
+                        const float v = xacc[j][qq] + Xs[(((wr * 2 + hk) * 2 + j) * 16 + qq) * 64 + lane];
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rs_p,
+                                                              vb + (uint32_t)(sl * 256), sob, 0);
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int qq = 0; qq < 16; ++qq) xacc[j][qq] = 0.f;
+            ++slot;
+        }
+        ph(6);
+        __syncthreads();  // every wave done with the eps' image
+        ph(7);
+        if constexpr (has_next) store_row();
+        if constexpr (newband) {
+            split_G();
+            __syncthreads();  // the new band's G image written before any wave's dL reads it
+        }
+        ph(8);
+        if (DIAG && wv == 0) ++tph[9];
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    for (int i = t0; i + 1 < t1; ++i) {
+        if (++tk > tb_) {
+            tk = 0;
+            int nbl = a.nb[0];
+#pragma unroll
+            for (int l = 1; l < kMaxL; ++l)
+                if (tl == l) nbl = a.nb[l];
+            if (++tb_ == nbl) {
+                tb_ = 0;
+                ++tl;
+            }
+        }
+        const StrTile nxt = str_tile(a, tl, tb_, tk);
+        if (nxt.l != cur.l || nxt.b != cur.b)
+            tile(nxt, T_{}, T_{});
+        else
+            tile(nxt, T_{}, F_{});
+        cur = nxt;
+    }
+    tile(cur, F_{}, F_{});
+    if (DIAG && tid == 0) {
+        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
+#pragma unroll
+        for (int qq = 0; qq < 10; ++qq) o[qq] = tph[qq];
+        o[10] = __builtin_amdgcn_s_memtime();
+        o[11] = __builtin_amdgcn_s_memrealtime();
+    }
+    float klp = (kl2[0] + kl2[1]) * (0.5f * a.inv_s0sq) + kld;
+    if (a.kl_out && a.include_kl) {
+        const float tot = block_sum(klp, Xs);
+        if (tid == 0) atomicAdd(a.kl_out, (double)tot);
+    }
+}
+
 int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1: chunked, 3: plain-store stream)
 int g_stream_bf_off = 0;  // psvi_debug_set(PSVI_DBG_STREAM_BF_OFF, 1): the fp32-MFMA streaming kernel (A/B)
+int g_stream_bf2_off = 0; // psvi_debug_set(PSVI_DBG_STREAM_BF2_OFF, 1): the four-wave bf16-piece kernel (A/B)
 unsigned long long* g_bf_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_BF_STAMPS, buf)
 int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128 (A/B)
 int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
@@ -3066,12 +3496,21 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                     b.ppoff[l] = p.eps_planes.poff[l];
                     b.npad[l] = p.eps_planes.npad[l];
                 }
-                if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
-                    hipLaunchKernelGGL((mvn_stream_bf_kernel<PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
+                const dim3 b8(512);
+                if (g_stream_bf2_off) {
+                    // A/B: four waves, one per SIMD
+                    if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
+                        hipLaunchKernelGGL((mvn_stream_bf_kernel<PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
+                    else if (b.adam.kind == PSVI_ADAM_HIGHER)
+                        hipLaunchKernelGGL(mvn_stream_bf_kernel<PSVI_ADAM_HIGHER>, sg, block, 0, st, b);
+                    else
+                        hipLaunchKernelGGL(mvn_stream_bf_kernel<PSVI_ADAM_HYPERGRAD>, sg, block, 0, st, b);
+                } else if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
+                    hipLaunchKernelGGL((mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER, true>), sg, b8, 0, st, b);
                 else if (b.adam.kind == PSVI_ADAM_HIGHER)
-                    hipLaunchKernelGGL(mvn_stream_bf_kernel<PSVI_ADAM_HIGHER>, sg, block, 0, st, b);
+                    hipLaunchKernelGGL(mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER>, sg, b8, 0, st, b);
                 else
-                    hipLaunchKernelGGL(mvn_stream_bf_kernel<PSVI_ADAM_HYPERGRAD>, sg, block, 0, st, b);
+                    hipLaunchKernelGGL(mvn_stream_bf2_kernel<PSVI_ADAM_HYPERGRAD>, sg, b8, 0, st, b);
             } else if (b.stamps && a.S == 128 && b.adam.kind == PSVI_ADAM_HIGHER)
                 hipLaunchKernelGGL((mvn_stream_kernel<4, PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
             else

@@ -82,6 +82,20 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nb,
                                              0x00020000);
 }
+// A 16-byte buffer store whose data registers stay untouched for the two wait
+// states after it.  hipcc (ROCm 7.2) does not pad the VMEM-store data hazard
+// for __builtin_amdgcn_raw_buffer_store_b128 (it does for global stores): a
+// VALU write of a data VGPR in the next instruction can reach memory instead
+// of the stored value -- seen as LDS-offset bit patterns in the streaming
+// update's tiled Adam state.  The asm reads the data after the store, so no
+// instruction in between may redefine those registers, and pads two states.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+#define BSTORE128(v, r, voff, soff, aux)                                    \
+    do {                                                                    \
+        const u32x4_t bst_v_ = (v);                                         \
+        __builtin_amdgcn_raw_buffer_store_b128(bst_v_, r, voff, soff, aux); \
+        asm volatile("s_nop 1" ::"v"(bst_v_));                              \
+    } while (0)
 __device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
     // the builtin returns the raw 32 bits as an integer
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));

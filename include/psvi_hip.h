@@ -528,6 +528,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_KSTREAM_BF_OFF 27   /* value: 1 = the K-split update (K = S > 128)
                                     on the fp32 MFMA kernel instead of the
                                     bf16-piece (fp32-faithful) one (A/B)      */
+#define PSVI_DBG_STREAM_BF2_OFF 28   /* value: 1 = the bf16-piece streaming update
+                                    with four waves (one per SIMD) instead of
+                                    eight (A/B)                               */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
