@@ -371,21 +371,29 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         int64_t* xb = reinterpret_cast<int64_t*>(srct) + a.nbands;
         int* xs0 = srct + 2 * a.nbands + 2 * kMaxWorld;
         int* bb = xs0 + kMaxWorld;
-        for (int p = 0; p < nsrc; ++p)
-            if (tid == 0) {  // the stage: source p's block at stage_off[p]
-                xs0[p] = a.stage_off[p];
-                xb[p] = a.src_base[p] + (int64_t)s * a.src_stride[p] - a.stage_off[p];
-            }
-        for (int l = 0; l < L; ++l)
-            if (tid == 0) bb[l] = a.bbase[l];
-        if constexpr (VEC) {
-            int* cs = bb + kMaxL;
-            int* rq = cs + kMaxWorld + 1;
-            for (int p = 0; p <= nsrc; ++p)
-                if (tid == 0) {
-                    cs[p] = a.src_chunk0[p];
-                    if (p < nsrc) rq[p] = a.src_stride[p];
+        // constant trip counts: the argument reads are scalar loads at constant
+        // offsets, issued together (a run-time bound made each iteration wait for
+        // its own scalar load: ~4 k clocks for 8 sources)
+        if (tid == 0) {
+#pragma unroll
+            for (int p = 0; p < kMaxWorld; ++p)
+                if (p < nsrc) {  // the stage: source p's block at stage_off[p]
+                    xs0[p] = a.stage_off[p];
+                    xb[p] = a.src_base[p] + (int64_t)s * a.src_stride[p] - a.stage_off[p];
                 }
+#pragma unroll
+            for (int l = 0; l < kMaxL; ++l)
+                if (l < L) bb[l] = a.bbase[l];
+            if constexpr (VEC) {
+                int* cs = bb + kMaxL;
+                int* rq = cs + kMaxWorld + 1;
+#pragma unroll
+                for (int p = 0; p <= kMaxWorld; ++p)
+                    if (p <= nsrc) {
+                        cs[p] = a.src_chunk0[p];
+                        if (p < nsrc) rq[p] = a.src_stride[p];
+                    }
+            }
         }
         __syncthreads();
     }

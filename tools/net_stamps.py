@@ -16,7 +16,8 @@ from psvi.runtime import InnerLoopPlan  # noqa: E402
 
 CFG = {"c3": ([(64, 40), (40, 40), (40, 2)], 128, 100),
        "s512": ([(64, 40), (40, 40), (40, 2)], 512, 100),
-       "c4": ([(64, 40), (40, 40), (40, 2)], 1024, 200)}
+       "c4": ([(64, 40), (40, 40), (40, 2)], 1024, 200),
+       "w8": ([(64, 40), (40, 40), (40, 2)], 1024, 100)}
 
 
 def report(name, t, abl, S):
