@@ -92,7 +92,7 @@ def algorithmic_work(S, rows_frac=1.0, layers=LAYERS):
 # The PMC summary the roofline's `traffic` is read from, and the commit whose
 # bench it profiled (tools/round_session.sh pmc step: separate FETCH_SIZE /
 # WRITE_SIZE rocprofv3 passes of this bench); reported as `traffic_source`
-PMC_TRAFFIC = dict(file="profiles/r05_pmc_traffic.json", head="c0b54fb")
+PMC_TRAFFIC = dict(file="profiles/r05_pmc_traffic.json", head="b86117e")
 
 
 def pmc_traffic(kernels, path=os.path.join(ROOT, PMC_TRAFFIC["file"])):
@@ -681,8 +681,8 @@ def run(rt, args, shapes=None):
         # dominant kernel: the update with the fused next-step sample (plus its
         # small slot-reduce kernel, inside the same event pair)
         wk = algorithmic_work_fused(S)
-        kname = ("mvn_stream_bf_kernel (fused update + next-step sample, tiled state; "
-                 "fp32-faithful bf16-piece MFMA) + mvn_fwd_reduce_kernel")
+        kname = ("mvn_stream_bf2_kernel (fused update + next-step sample, tiled state; "
+                 "fp32-faithful bf16-piece MFMA, eight waves) + mvn_fwd_reduce_kernel")
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
@@ -706,7 +706,7 @@ def run(rt, args, shapes=None):
         roofline = dict(bound="mfma", achieved=round(wk["flops"] / upd_s / 1e12, 2),
                         peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s")
     roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
-                    traffic=pmc_traffic(["mvn_stream_bf_kernel", "mvn_fwd_reduce_kernel"])
+                    traffic=pmc_traffic(["mvn_stream_bf2_kernel", "mvn_fwd_reduce_kernel"])
                     if world == 1 else None,
                     traffic_source=dict(PMC_TRAFFIC, measured_in_this_run=False,
                                         method="rocprofv3 --pmc FETCH_SIZE, then --pmc "
