@@ -2891,7 +2891,36 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         for (int p = 0; p < 3; ++p)
             *reinterpret_cast<u32x4*>(Xl + ((wv * 3 + p) * 64 + lane) * 4) =
                 u32x4{lwo[p][0], lwo[p][1], lwo[p][2], lwo[p][3]};
+        // ---- x' += eps' L'^T for this wave's sample blocks sb = 2 hk + j: its own
+        // K-half (st = hk) first, before the partner's pieces are waited for --
+        // the SIMD's other wave may still be in its Adam
+        auto xprime = [&](int ss, const uint32_t (&lwx)[3][4]) __attribute__((always_inline)) {
+            const int st = ss == 0 ? hk : 1 - hk;
+            const uint8_t* const rx = En + l32 * 128 + (((2 * (2 * wc + st) + h) ^ xsw) << 4);
+            bf8v lb[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                lb[p] = __builtin_bit_cast(bf8v, u32x4{lwx[p][0], lwx[p][1], lwx[p][2], lwx[p][3]});
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int sb = 2 * hk + j;
+                bf8v fx[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) fx[p] = *reinterpret_cast<const bf8v*>(rx + p * kBfImg + 4096 * sb);
+                xacc[j] = mfma6(fx, lb, xacc[j]);
+                // the own half issues the next band's G (6..9), the partner's half
+                // the next tile's eps' planes (0..5: stg holds the next eps planes
+                // until store_col, between the halves)
+                {
+                    const int q0 = ss == 0 ? 6 + 2 * j : 3 * j, q1 = ss == 0 ? 8 + 2 * j : 3 * j + 3;
+#pragma unroll
+                    for (int qi = q0; qi < q1; ++qi) issue_b(qi, nxt, has_next, newband, vo_n);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
         ph(4);
+        xprime(0, lwo);
         __syncthreads();  // B3
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -2901,32 +2930,7 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         }
         __syncthreads();  // B4: the exchange scratch read; the eps image is free
         if constexpr (has_next) store_col();  // the next tile's eps image
-        // ---- x' += eps' L'^T for this wave's sample blocks sb = 2 hk + j, both K-halves
-        // this wave's K-half first, then the partner's (st = hk, 1 - hk)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-            const int st = ss == 0 ? hk : 1 - hk;
-            const uint8_t* const rx = En + l32 * 128 + (((2 * (2 * wc + st) + h) ^ xsw) << 4);
-            bf8v lb[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                lb[p] = ss == 0 ? __builtin_bit_cast(bf8v, u32x4{lwo[p][0], lwo[p][1], lwo[p][2], lwo[p][3]})
-                                : __builtin_bit_cast(bf8v, u32x4{lwp[p][0], lwp[p][1], lwp[p][2], lwp[p][3]});
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int sb = 2 * hk + j;
-                bf8v fx[3];
-#pragma unroll
-                for (int p = 0; p < 3; ++p) fx[p] = *reinterpret_cast<const bf8v*>(rx + p * kBfImg + 4096 * sb);
-                xacc[j] = mfma6(fx, lb, xacc[j]);
-                {
-                    const int kk = 2 * ss + j, q0 = (10 * kk) / 4, q1 = (10 * (kk + 1)) / 4;
-#pragma unroll
-                    for (int qi = q0; qi < q1; ++qi) issue_b(qi, nxt, has_next, newband, vo_n);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
+        xprime(1, lwp);
         ph(5);
         // ---- band end (or run end): the two column halves' x' partials -> the slot
         if constexpr (!has_next || newband) {
