@@ -42,6 +42,7 @@ extern int g_fwd_ablation;               // kernels_mvn.hip
 extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_rop_stamps; // kernels_rop.hip
+extern int g_rop_valu;                     // kernels_rop.hip
 }  // namespace psvi
 
 using namespace psvi;
@@ -557,7 +558,9 @@ int build_plan(psvi_plan& p) {
             p.n_sslots = ns;
         }
         p.upd_tiles = tiles;
-        if (S > kKsPass) build_kstream(p);
+        // the K-split tables at every S: the Adam update at S > 128, the
+        // gradient mode (the HVP's reparameterised backward) at any S
+        build_kstream(p);
         // the segmented sample at every S (x_0 of a loop, the HVP's tangent
         // sample, the sharded step): equal runs over 512 workgroups
         build_fseg(p);
@@ -621,6 +624,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_FWD_SEG_BF_OFF: g_fs_bf_off = value; return 0;
         case PSVI_DBG_KSTREAM_BF_OFF: g_ks_bf_off = value; return 0;
         case PSVI_DBG_STREAM_BF2_OFF: g_stream_bf2_off = value; return 0;
+        case PSVI_DBG_ROP_VALU: g_rop_valu = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_NET_MLOOP_OFF: g_net_mloop_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;

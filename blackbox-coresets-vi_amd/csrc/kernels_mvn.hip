@@ -1185,6 +1185,10 @@ struct KsArgs {
     AdamC adam;
     unsigned long long* stamps;  // diagnostics: 16 slots per workgroup (nullptr in production)
     MvnLayerArgs lay[kMaxL];
+    // GRAD: the reparameterised gradient into grad_out instead of Adam (the
+    // HVP's J^T G_dot), + kl_vec / s0^2 on the corr entries when kl_vec is set
+    float* grad_out;
+    const float* kl_vec;
 };
 
 // G / eps / corr / m / v through buffer loads whose per-dword range check
@@ -1203,7 +1207,7 @@ struct KsBfShared {
     uint8_t img[6 * kKsBfImg];  // eps planes, then G planes; the epilogue's T tile after the passes
     float red[2 * 4 * 64];
 };
-template <bool BF>
+template <bool BF, bool GRAD = false>
 __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     __shared__ __attribute__((aligned(16))) std::conditional_t<BF, KsBfShared, UpdShared<true>> sh;
     static_assert(kKsPass == USB, "one LDS stage per pass");
@@ -1222,7 +1226,9 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const rsrc_t rs = make_rsrc(a.slots, a.slot_bytes);
     const rsrc_t rg = make_rsrc(a.g, 4 * a.g_total), re = make_rsrc(a.eps, 4 * a.e_total);
-    const rsrc_t rpar = make_rsrc(a.params, 4 * a.pcount), rm = make_rsrc(a.m, 4 * a.pcount),
+    // GRAD: m reads kl_vec (0 when none: an empty range), v is not read
+    const rsrc_t rpar = make_rsrc(a.params, 4 * a.pcount),
+                 rm = make_rsrc(GRAD ? a.kl_vec : a.m, GRAD && !a.kl_vec ? 0 : 4 * a.pcount),
                  rv = make_rsrc(a.v, 4 * a.pcount);
     float klp = 0.f;
     // diagnostics (a.stamps): shader clocks per phase summed over the segments
@@ -1371,10 +1377,12 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                 const uint32_t om = (uint32_t)pm_d * 4u, os = (uint32_t)ps_d * 4u;
                 dmu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpar, om, 0, 0));
                 dsd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rpar, os, 0, 0));
-                dmm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, om, 0, 0));
-                dmv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, om, 0, 0));
-                dsm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, os, 0, 0));
-                dsv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, os, 0, 0));
+                if (!GRAD) {
+                    dmm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, om, 0, 0));
+                    dmv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, om, 0, 0));
+                    dsm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, os, 0, 0));
+                    dsv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, os, 0, 0));
+                }
             }
             const int cl = tl.k * UB + 4 * col4;
 #pragma unroll
@@ -1383,7 +1391,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                 const uint32_t o = (uint32_t)(rowp[j] + cl) * 4u;
                 pq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rpar, o, 0, 0));
                 mq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rm, o, 0, 0));
-                vq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
+                if (!GRAD) vq[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rv, o, 0, 0));
             }
         };
         floatx16 acc;
@@ -1560,17 +1568,33 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             if (!rown[j] || cb >= r) continue;
             const int o = rowp[j] + cb;
             const float4 d4 = *reinterpret_cast<const float4*>(&T[(srow + 16 * j) * TLD + 4 * col4]);
-            const float4 p4 = pq[j], m4 = mq[j], v4 = vq[j];
+            const float4 p4 = pq[j], m4 = mq[j], v4 = GRAD ? float4{} : vq[j];
             float pn[4], mn[4], vn[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float p = f4get(p4, i);
                 klt += cb + i < r ? p * p : 0.f;
-                const float gval = a.include_kl ? f4get(d4, i) + p * a.inv_s0sq : f4get(d4, i);
+                float gval = a.include_kl ? f4get(d4, i) + p * a.inv_s0sq : f4get(d4, i);
+                if (GRAD) {
+                    // the chunked kernel's gradient mode (upd_chunk): + kl_vec / s0^2
+                    if (a.kl_vec) gval += f4get(m4, i) * a.inv_s0sq;
+                    pn[i] = gval;
+                    continue;
+                }
                 float mm = f4get(m4, i), vv = f4get(v4, i);
                 pn[i] = adam_apply_fast(a.adam, p, gval, mm, vv);
                 mn[i] = mm;
                 vn[i] = vv;
+            }
+            if (GRAD) {
+                if (cb + 3 < r) {
+                    *reinterpret_cast<float4*>(a.grad_out + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 3; ++i)
+                        if (cb + i < r) a.grad_out[o + i] = pn[i];
+                }
+                continue;
             }
             if (cb + 3 < r) {
                 *reinterpret_cast<float4*>(a.params + o) = make_float4(pn[0], pn[1], pn[2], pn[3]);
@@ -1606,6 +1630,10 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                     gsd += (sp * a.inv_s0sq - 1.f / sp) * sgm;
                     klp += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
                 }
+                if (GRAD) {
+                    a.grad_out[pm] = gmean;
+                    a.grad_out[ps] = gsd;
+                } else {
                 float mm = dmm, vv = dmv;
                 a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
                 a.m[pm] = mm;
@@ -1615,6 +1643,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
                 a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
                 a.m[ps] = mm;
                 a.v[ps] = vv;
+                }
             }
         }
         __syncthreads();  // T / red reads done before the next segment stages
@@ -3553,7 +3582,9 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         }
         return hipGetLastError();
     }
-    if (mode == 2 && !grad_out && p.n_kwg > 0 && g_ks_off != 1) {
+    // gradient mode (the HVP's J^T G_dot) at any S on the bf16-piece K-split kernel
+    const bool ks_grad = grad_out && p.n_kwg > 0 && !g_ks_off && !g_ks_bf_off && !g_upd_stamps;
+    if ((mode == 2 && !grad_out && p.n_kwg > 0 && g_ks_off != 1) || ks_grad) {
         // K = S > 128: the K-split streaming update (then the next step's
         // sample from the new parameters when asked)
         KsArgs k{};
@@ -3579,8 +3610,12 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         k.log_s0 = a.log_s0;
         k.adam = a.adam;
         k.stamps = g_upd_stamps;
+        k.grad_out = grad_out;
+        k.kl_vec = kl_vec;
         fill_layers(p, k.lay);
-        if (g_ks_bf_off || k.stamps)
+        if (ks_grad)
+            hipLaunchKernelGGL((mvn_kstream_kernel<true, true>), dim3(p.n_kwg), block, 0, st, k);
+        else if (g_ks_bf_off || k.stamps)
             hipLaunchKernelGGL(mvn_kstream_kernel<false>, dim3(p.n_kwg), block, 0, st, k);
         else
             hipLaunchKernelGGL(mvn_kstream_kernel<true>, dim3(p.n_kwg), block, 0, st, k);

@@ -23,6 +23,7 @@
 // delta_0 W_dot, d/dw_m (vec . grad) = sum_s NLL_dot_sm.
 #include <algorithm>
 
+#include "mfma_tiles.hpp"
 #include "psvi_internal.hpp"
 
 namespace psvi {
@@ -39,6 +40,13 @@ struct RopArgs {
     // W_l / W_dot_l in LDS: rows of an odd stride ldw[l] (a lane per output row
     // then hits its own bank), layer l at xo[l] of the X / XD regions, b after W
     int ldw[kMaxL], xo[kMaxL];
+    // MFMA form (net_rop_mfma_kernel): X_l (l = 0..L) at mxo[l], rows of
+    // ldxm[l] floats = [h | h_dot] halves of kx[l] = rup16(width) (X_0: the u
+    // rows alone; X_L: logits and their tangents); W2_l at mwo[l], rup16(dout)
+    // rows of ldwm[l] = [W | W_dot] halves of kx[l]; b_l | b_dot_l at mbo[l]
+    // (halves of kx[l + 1])
+    int mxo[kMaxL + 1], ldxm[kMaxL + 1], kx[kMaxL + 1], mwo[kMaxL], ldwm[kMaxL], mbo[kMaxL], lstamp;
+    int jw[kMaxL], jbl[kMaxL], jb, ju;  // load jobs: layer l's W2 rows from jw[l], bias rows from jb + jbl[l], u rows from ju
     const float* u;
     const int32_t* z;
     const float* w;
@@ -511,6 +519,421 @@ __global__ __launch_bounds__(512) void net_rop_kernel(RopArgs a) {
     }
 }
 
+// ------------------------------------------------------------ MFMA R-op
+// The R-op's GEMMs come in pairs -- a product and its tangent -- over the same
+// operands and their tangent halves:
+//   X[p][q] = sum_k A(p,k) B(q,k)
+//   Y[p][q] = sum_k A(p,k) B'(q,k) + A'(p,k) B(q,k)
+// with A' = A + oa, B' = B + ob (each row holds [value | tangent]).  TA / TB
+// false: that tangent operand is zero (the u rows); WX false: X is not formed.
+// Operands as the network kernel's tiles (mfma_tiles.hpp): k-contiguous as one
+// float4 per lane and k-group, k-strided as four rows in the kbase / kstep
+// order; v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation).
+template <bool ACONT, bool BCONT, int NQ, bool TA, bool TB, bool WX>
+struct RopFrag {
+    using T = TileOps<ACONT, BCONT, NQ>;
+    static constexpr bool PERM = T::PERM;
+    floatx4 a, at, b[NQ], bt[NQ];
+    __device__ __forceinline__ static floatx4 ld(const float* p, int ldx, bool cont) {
+        return __builtin_bit_cast(floatx4, T::ld(p, ldx, cont));
+    }
+    __device__ __forceinline__ void load(const float* pa, int lda, int oa, const float* pb, int ldb,
+                                         int ob) {
+        a = ld(pa, lda, ACONT);
+        if (TA) at = ld(pa + oa, lda, ACONT);
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            const float* q = pb + 16 * c * (BCONT ? ldb : 1);
+            b[c] = ld(q, ldb, BCONT);
+            if (TB) bt[c] = ld(q + ob, ldb, BCONT);
+        }
+    }
+    // a contraction over rows (both operands k-strided): rows r0 + kstep(j)
+    // at or past kv read as 0 -- selected, so stale LDS past the rows is inert
+    __device__ __forceinline__ void mask(int r0, int kv) {
+        auto m = [&](floatx4& v) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = r0 + kstep<PERM>(j) < kv ? v[j] : 0.f;
+        };
+        m(a);
+        if (TA) m(at);
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            m(b[c]);
+            if (TB) m(bt[c]);
+        }
+    }
+    __device__ __forceinline__ void mma(floatx4 (&x)[NQ], floatx4 (&y)[NQ]) const {
+#pragma unroll
+        for (int c = 0; c < NQ; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (WX) x[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[c][j], x[c], 0, 0, 0);
+                if (TB) y[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bt[c][j], y[c], 0, 0, 0);
+                if (TA) y[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(at[j], b[c][j], y[c], 0, 0, 0);
+            }
+    }
+};
+
+// Units of one 16-row tile x NQ column tiles dealt round-robin to the waves
+// (from wave `first`); per unit the k-groups run two deep (the next group's
+// LDS reads issued before the current group's MFMAs).  The epilogue gets
+// (first row of the lane's four, column, X and Y of the four rows, rotation):
+// odd lane-groups hand their rows over rotated by two, as the network kernel's
+// epilogues (row (r + rot) & 3 of the four is value r).
+template <bool ACONT, bool BCONT, int NQ, bool TA, bool TB, bool WX, class Epi>
+__device__ __forceinline__ void rop_steps(int nu, int tqu, int nk, int u0, int nwv, const float* A,
+                                          int lda, int oa, const float* B, int ldb, int ob, int kv,
+                                          Epi epi) {
+    using F = RopFrag<ACONT, BCONT, NQ, TA, TB, WX>;
+    constexpr bool PERM = F::PERM;
+    const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+    const bool km = !ACONT && !BCONT && kv < 16 * nk;  // uniform
+    const int da = ACONT ? 16 : 16 * lda, db = BCONT ? 16 : 16 * ldb;
+    const int rot = (k4 & 1) << 1, r0 = kbase<PERM>(k4);
+    for (int u = u0; u < nu; u += nwv) {  // wave-uniform
+        const int pt = u / tqu, p0 = pt << 4, q0 = ((u - pt * tqu) * NQ) << 4;
+        const float* pa = ACONT ? A + (p0 + i16) * lda + 4 * k4 : A + r0 * lda + p0 + i16;
+        const float* pb = BCONT ? B + (q0 + i16) * ldb + 4 * k4 : B + r0 * ldb + q0 + i16;
+        auto fetch = [&](F& f, int kg) __attribute__((always_inline)) {
+            f.load(pa + kg * da, lda, oa, pb + kg * db, ldb, ob);
+            if (km && kg == nk - 1) f.mask(16 * kg + r0, kv);
+        };
+        floatx4 x[NQ], y[NQ];
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) x[c] = y[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+        F f0, f1;
+        fetch(f0, 0);
+        for (int kg = 0; kg < nk; kg += 2) {  // uniform
+            if (kg + 1 < nk) fetch(f1, kg + 1);
+            f0.mma(x, y);
+            if (kg + 1 < nk) {
+                if (kg + 2 < nk) fetch(f0, kg + 2);
+                f1.mma(x, y);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            const floatx4 vx = x[c], vy = y[c];
+            epi(p0 + 4 * k4, q0 + 16 * c + i16, rot ? floatx4{vx[2], vx[3], vx[0], vx[1]} : vx,
+                rot ? floatx4{vy[2], vy[3], vy[0], vy[1]} : vy, rot);
+        }
+    }
+}
+
+// P x Q outputs, contraction over nk k-groups of 16 (kv: the true length when
+// both operands are k-strided).  A row of column tiles per unit (one A read
+// per NQ tiles) when that still gives each SIMD a unit, else single tiles.
+template <bool WIDE, bool ACONT, bool BCONT, bool TA, bool TB, bool WX, class Epi>
+__device__ __forceinline__ void rop_gemm(int P, int Q, int K16, int kv, int first, const float* A,
+                                         int lda, int oa, const float* B, int ldb, int ob, Epi epi) {
+    const int nwv = blockDim.x >> 6, wid = wave_id();
+    const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, nk = K16 >> 4;
+    const int u0 = ((wid - first) % nwv + nwv) % nwv;
+    const int nq = (WIDE && tq <= 3 && tp >= 4) ? tq : 1;
+    if constexpr (WIDE) {
+        if (nq == 3) {
+            rop_steps<ACONT, BCONT, 3, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, kv, epi);
+            return;
+        }
+        if (nq == 2) {
+            rop_steps<ACONT, BCONT, 2, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, kv, epi);
+            return;
+        }
+    }
+    rop_steps<ACONT, BCONT, 1, TA, TB, WX>(tp * tq, tq, nk, u0, nwv, A, lda, oa, B, ldb, ob, kv, epi);
+}
+
+// The R-op on the matrix cores: one workgroup per (sample, row block), its
+// rows in one pass (launch_net_rop takes this form when the carve fits the LDS).
+// Per layer l, forward: [a | a_dot] = X_l [W | W_dot]^T pairs (X = h W^T,
+// Y = h W_dot^T + h_dot W^T) + [b | b_dot], the ReLU and its mask in the
+// epilogue into X_{l+1}; the head in place on X_L (delta | delta_dot); per
+// layer backward: the weight gradients [G | G_dot] = D^T [h | h_dot] pairs
+// (a contraction over the rows, both operands k-strided) straight into the
+// row block's slot, then the propagation D W / D W_dot + D_dot W masked by
+// 1[h > 0] in place over X_l (after a barrier: the weight gradients read it),
+// or at the input the d/du tangent rows.  Every region's padding (columns to
+// kx, W rows to rup16(dout)) is written zero; rows past the block's are never
+// written: their over-reads feed only output rows that are not stored, and the
+// contraction over rows masks them.
+__device__ __forceinline__ void lds_dma4(rsrc_t r, float* lds, uint32_t voff) {
+    // one dword per lane into LDS at the wave-uniform base `lds` + 4 lane
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
+}
+
+template <bool WIDE, bool FC>
+__global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+    const int L = a.L, D = a.din[0], C = a.dout[L - 1];
+    const int rows_per = (a.M + a.nsplit - 1) / a.nsplit;
+    const int m0 = blockIdx.y * rows_per, rc = max(0, min(a.M, m0 + rows_per) - m0);
+    // diagnostics (thread 0): phase clocks summed into LDS past the carve
+    // (a register array indexed at run time would live in scratch)
+    unsigned long long* tph = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
+    unsigned long long tlast = 0;
+    auto ph = [&](int q) __attribute__((always_inline)) {
+        if (a.stamps && tid == 0) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            if (q >= 0) tph[q] += tt - tlast;
+            tlast = tt;
+        }
+    };
+    if (a.stamps && tid == 0)
+        for (int q = 0; q < 10; ++q) tph[q] = 0;
+    ph(-1);
+    // ---- the load phase as wave jobs (a job: one row of up to 64 columns,
+    // lane = column; no per-element index arithmetic, coalesced loads, the
+    // padding columns written by the same instruction): W2_l rows (value and
+    // tangent halves), then the [b | b_dot] rows, then the u rows into X_0
+    // (tangent half zero).  Full-cov: buffer loads straight into LDS, every
+    // job's loads in flight at once (a lane past the row's data reads the
+    // buffer's out-of-range 0).  Mean-field: the sampled values are formed in
+    // registers, a few jobs' loads in flight.
+    {
+        const int lane = tid & 63, wid = wave_id(), nwv = nt >> 6;
+        const int nch0 = (a.kx[0] + 63) >> 6;
+        const int njobs = a.ju + rc * nch0;
+        // job j -> kind (0 W2 row, 1 bias row, 2 u row), layer, row, first column (uniform)
+        auto decode = [&](int j, int& kind, int& l, int& row, int& c0) __attribute__((always_inline)) {
+            l = 0;
+            if (j < a.jb) {
+                kind = 0;
+                while (l + 1 < L && j >= a.jw[l + 1]) ++l;
+                const int r = j - a.jw[l], nch = (a.kx[l] + 63) >> 6;
+                row = nch == 1 ? r : r / nch;
+                c0 = (r - row * nch) << 6;
+            } else if (j < a.ju) {
+                kind = 1;
+                while (l + 1 < L && j >= a.jb + a.jbl[l + 1]) ++l;
+                row = 0;
+                c0 = (j - a.jb - a.jbl[l]) << 6;
+            } else {
+                kind = 2;
+                const int r = j - a.ju;
+                row = nch0 == 1 ? r : r / nch0;
+                c0 = (r - row * nch0) << 6;
+            }
+        };
+        if constexpr (FC) {
+            // per layer (its dimensions read once), the layer's rows dealt to
+            // the waves; the DMAs are fire-and-forget, so the deal's imbalance
+            // costs issue slots only
+            const rsrc_t rx = make_rsrc(a.x + (int64_t)s * a.n_tot, 4 * (int64_t)a.n_tot);
+            const rsrc_t rxd = make_rsrc(a.xd + (int64_t)s * a.n_tot, 4 * (int64_t)a.n_tot);
+            const rsrc_t ru = make_rsrc(a.u + (int64_t)m0 * D, 4 * (int64_t)rc * D);
+            for (int l = 0; l < L; ++l) {  // uniform
+                const int din = a.din[l], dout = a.dout[l], kxl = a.kx[l], kq = a.kx[l + 1];
+                const int ldw = a.ldwm[l], nch = (kxl + 63) >> 6, woff = a.woff[l];
+                float* const W2 = sm + a.mwo[l];
+                for (int r = wid; r < kq * nch; r += nwv) {  // wave-uniform
+                    const int row = nch == 1 ? r : r / nch, c0 = (r - row * nch) << 6, c = c0 + lane;
+                    float* d = W2 + row * ldw + c0;
+                    if (c < kxl) {
+                        const uint32_t vo = row < dout && c < din ? 4u * (uint32_t)(woff + row * din + c) : kOOB;
+                        lds_dma4(rx, d, vo);
+                        lds_dma4(rxd, d + kxl, vo);
+                    }
+                }
+                float* const bb = sm + a.mbo[l];
+                for (int c0 = 64 * ((wid + l) % nwv); c0 < kq; c0 += 64 * nwv) {  // wave-uniform
+                    const int c = c0 + lane;
+                    if (c < kq) {
+                        const uint32_t vo = c < dout ? 4u * (uint32_t)(woff + din * dout + c) : kOOB;
+                        lds_dma4(rx, bb + c0, vo);
+                        lds_dma4(rxd, bb + kq + c0, vo);
+                    }
+                }
+            }
+            {
+                const int kx0 = a.kx[0], ld0 = a.ldxm[0];
+                for (int r = wid; r < rc * nch0; r += nwv) {  // wave-uniform
+                    const int row = nch0 == 1 ? r : r / nch0, c0 = (r - row * nch0) << 6, c = c0 + lane;
+                    float* d = sm + a.mxo[0] + row * ld0 + c0;
+                    if (c < kx0) {
+                        lds_dma4(ru, d, c < D ? 4u * (uint32_t)(row * D + c) : kOOB);
+                        lds_dma4(ru, d + kx0, kOOB);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            auto fetch_w = [&](int l, int i, float& xv, float& xdv) __attribute__((always_inline)) {
+                // element i of layer l's sampled weights (W row-major, then b) and its tangent
+                const int dout = a.dout[l], nw = a.din[l] * dout, n = nw + dout;
+                const float e = i < nw ? a.eps[a.eoff[l] + (int64_t)s * nw + i]
+                                       : a.eps[a.eoff[l] + (int64_t)a.S * nw + (int64_t)s * dout + i - nw];
+                const int64_t pm = a.poff[l] + i, pr = pm + n;
+                const float rho = a.params[pr];
+                xv = a.params[pm] + softplus_f(rho) * e;
+                xdv = a.vec[pm] + sigmoid_f(rho) * a.vec[pr] * e;
+            };
+            for (int j = wid; j < njobs; j += nwv) {  // wave-uniform
+                int kind, l, row, c0;
+                decode(j, kind, l, row, c0);
+                const int c = c0 + lane;
+                float v0 = 0.f, v1 = 0.f;
+                if (kind == 0) {
+                    if (row < a.dout[l] && c < a.din[l]) fetch_w(l, row * a.din[l] + c, v0, v1);
+                    if (c < a.kx[l]) {
+                        float* w2 = sm + a.mwo[l] + row * a.ldwm[l] + c;
+                        w2[0] = v0;
+                        w2[a.kx[l]] = v1;
+                    }
+                } else if (kind == 1) {
+                    if (c < a.dout[l]) fetch_w(l, a.din[l] * a.dout[l] + c, v0, v1);
+                    if (c < a.kx[l + 1]) {
+                        sm[a.mbo[l] + c] = v0;
+                        sm[a.mbo[l] + a.kx[l + 1] + c] = v1;
+                    }
+                } else {
+                    if (c < D) v0 = a.u[(int64_t)(m0 + row) * D + c];
+                    if (c < a.kx[0]) {
+                        float* x0 = sm + a.mxo[0] + row * a.ldxm[0] + c;
+                        x0[0] = v0;
+                        x0[a.kx[0]] = 0.f;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    ph(0);
+    // ---- forward + tangent forward
+    for (int l = 0; l < L; ++l) {
+        const int dout = a.dout[l], kxl = a.kx[l], kq = a.kx[l + 1], ldn = a.ldxm[l + 1];
+        const float* bl = sm + a.mbo[l];
+        float* Xn = sm + a.mxo[l + 1];
+        const bool last = l == L - 1;
+        auto epi = [&](int pr, int q, floatx4 vx, floatx4 vy, int rot) __attribute__((always_inline)) {
+            const float b = bl[q], bd = bl[kq + q];  // zero past dout, as the W2 rows
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = pr + ((r + rot) & 3);
+                if (m < rc) {
+                    const float av = vx[r] + b, ad = vy[r] + bd;
+                    const bool on = last || av > 0.f;
+                    Xn[m * ldn + q] = on ? av : 0.f;
+                    Xn[m * ldn + kq + q] = on ? ad : 0.f;
+                }
+            }
+        };
+        const float* Xl = sm + a.mxo[l];
+        const float* W2 = sm + a.mwo[l];
+        rop_gemm<WIDE, true, true, true, true, true>(rc, dout, kxl, kxl, 0, Xl, a.ldxm[l], kxl, W2, a.ldwm[l], kxl, epi);
+        __syncthreads();
+        ph(2 + min(l, 2));
+    }
+    // ---- head, in place on X_L: delta = w (p - onehot), delta_dot = w p (a_dot - p.a_dot)
+    {
+        const int ldh = a.ldxm[L], kc = a.kx[L];
+        for (int m = tid; m < rc; m += nt) {
+            float* lg = sm + a.mxo[L] + m * ldh;
+            float* ld = lg + kc;
+            const int zm = a.z[m0 + m];
+            const float wm = a.w[m0 + m];
+            float mx = -INFINITY;
+            for (int c = 0; c < C; ++c) mx = fmaxf(mx, lg[c]);
+            float se = 0.f;
+            for (int c = 0; c < C; ++c) se += expf(lg[c] - mx);
+            const float lse = mx + logf(se);
+            float pad = 0.f, nd = 0.f;
+            for (int c = 0; c < C; ++c) pad += expf(lg[c] - lse) * ld[c];
+            for (int c = 0; c < C; ++c) {
+                const float p = expf(lg[c] - lse), ldc = ld[c];
+                const float pmo = p - (c == zm ? 1.f : 0.f);
+                nd = fmaf(pmo, ldc, nd);
+                lg[c] = wm * pmo;
+                ld[c] = wm * p * (ldc - pad);
+            }
+            if (a.nlld) a.nlld[(int64_t)s * a.M + m0 + m] = nd;
+        }
+    }
+    __syncthreads();
+    ph(5);
+    // ---- R-backward
+    for (int l = L - 1; l >= 0; --l) {
+        const int din = a.din[l], dout = a.dout[l], nw = din * dout, kxl = a.kx[l], kq = a.kx[l + 1];
+        const float* Dl = sm + a.mxo[l + 1];  // [delta | delta_dot] rows
+        const int ldd = a.ldxm[l + 1], ldx = a.ldxm[l];
+        float* Xl = sm + a.mxo[l];
+        const float* W2 = sm + a.mwo[l];
+        const int64_t gslot = ((int64_t)blockIdx.y * a.S + s) * a.n_tot + a.woff[l];
+        float* GW = a.G + gslot;
+        float* GDW = a.Gd + gslot;
+        // weight gradients: G[o][i] = sum_m delta[m][o] h[m][i],
+        // G_dot[o][i] = sum_m delta[m][o] h_dot[m][i] + delta_dot[m][o] h[m][i]
+        auto wepi = [&](int pr, int q, floatx4 vx, floatx4 vy, int rot) __attribute__((always_inline)) {
+            if (q >= din) return;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = pr + ((r + rot) & 3);
+                if (o < dout) {
+                    GW[o * din + q] = vx[r];
+                    GDW[o * din + q] = vy[r];
+                }
+            }
+        };
+        const int K16 = (rc + 15) & ~15;
+        rop_gemm<WIDE, false, false, true, true, true>(dout, din, K16, rc, 0, Dl, ldd, kq, Xl, ldx, kxl, wepi);
+        ph(1);
+        // bias gradients: column sums of delta / delta_dot, a wave per column
+        {
+            const int lane = tid & 63, nwv = nt >> 6;
+            for (int o = wave_id(); o < dout; o += nwv) {  // wave-uniform
+                float g = 0.f, gd = 0.f;
+                for (int m = lane; m < rc; m += 64) {
+                    g += Dl[m * ldd + o];
+                    gd += Dl[m * ldd + kq + o];
+                }
+                g = wave_sum(g);
+                gd = wave_sum(gd);
+                if (lane == 0) {
+                    GW[nw + o] = g;
+                    GDW[nw + o] = gd;
+                }
+            }
+        }
+        ph(9);
+        if (l > 0) {
+            __syncthreads();  // the weight gradients have read X_l
+            // delta' = (delta W) 1[h > 0], delta_dot' = (delta W_dot + delta_dot W) 1[h > 0]
+            auto pepi = [&](int pr, int q, floatx4 vx, floatx4 vy, int rot) __attribute__((always_inline)) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = pr + ((r + rot) & 3);
+                    if (m < rc) {
+                        float* xr = Xl + m * ldx;
+                        const bool on = xr[q] > 0.f;  // zero in the padding columns
+                        xr[q] = on ? vx[r] : 0.f;
+                        xr[kxl + q] = on ? vy[r] : 0.f;
+                    }
+                }
+            };
+            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, kq, 0, Dl, ldd, kq, W2, a.ldwm[l], kxl, pepi);
+            __syncthreads();
+        } else if (a.du) {
+            // d/du of (vec . grad): the input rows' delta_dot (no mask at the input)
+            auto uepi = [&](int pr, int q, floatx4 vx, floatx4 vy, int rot) __attribute__((always_inline)) {
+                if (q >= D) return;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = pr + ((r + rot) & 3);
+                    if (m < rc) a.du[((int64_t)s * a.M + m0 + m) * D + q] = vy[r];
+                }
+            };
+            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, kq, 0, Dl, ldd, kq, W2, a.ldwm[0], kxl, uepi);
+        }
+        ph(6 + min(L - 1 - l, 2));
+    }
+    if (a.stamps && tid == 0) {
+        unsigned long long* o = a.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+        for (int q = 0; q < 10; ++q) o[q] = tph[q];
+        o[15] = 1;
+    }
+}
+
 // G += the other row blocks' slots, G_dot likewise, in slot order (slot 0
 // holds the sum afterwards)
 __global__ __launch_bounds__(256) void slot_sum_kernel(float* __restrict__ G, float* __restrict__ Gd,
@@ -687,7 +1110,59 @@ static size_t rop_carve(const psvi_plan& p, int rc, RopArgs* a, bool with_g = tr
     return off;
 }
 
+// LDS carve of the MFMA form for a row block of `rows`; returns floats.  The
+// activation regions come first, so a 16-row tile's over-read past a region's
+// rows stays inside the allocation (tail slack when the weights after the last
+// one are shorter than that).
+static size_t rop_mfma_carve(const psvi_plan& p, int rows, RopArgs* a) {
+    const int L = p.L;
+    int kx[kMaxL + 1], mxo[kMaxL + 1], ldxm[kMaxL + 1], mwo[kMaxL], ldwm[kMaxL], mbo[kMaxL];
+    for (int l = 0; l < L; ++l) kx[l] = (p.lay[l].din + 15) & ~15;
+    kx[L] = (p.lay[L - 1].dout + 15) & ~15;
+    size_t off = 0;
+    for (int l = 0; l <= L; ++l) {
+        ldxm[l] = 2 * kx[l] + 8;  // == 8 (mod 16); X_0's tangent half is zero
+        mxo[l] = (int)off;
+        off += (size_t)rows * ldxm[l];
+    }
+    const size_t x_end = off;
+    for (int l = 0; l < L; ++l) {
+        ldwm[l] = 2 * kx[l] + 8;
+        mwo[l] = (int)off;
+        off += (size_t)kx[l + 1] * ldwm[l];
+    }
+    for (int l = 0; l < L; ++l) {
+        mbo[l] = (int)off;
+        off += 2 * (size_t)kx[l + 1];
+    }
+    const size_t over = (size_t)(((rows + 15) & ~15) - rows) * ldxm[L];
+    if (off - x_end < over) off = x_end + over;
+    off = (off + 3) & ~size_t(3);
+    const int lstamp = (int)off;
+    off += 20;  // 10 uint64 phase clocks (diagnostics)
+    if (a) {
+        int j = 0;
+        for (int l = 0; l < L; ++l) {
+            a->jw[l] = j;
+            j += kx[l + 1] * ((kx[l] + 63) >> 6);
+        }
+        a->jb = j;
+        for (int l = 0; l < L; ++l) {
+            a->jbl[l] = j - a->jb;
+            j += (kx[l + 1] + 63) >> 6;
+        }
+        a->ju = j;
+        a->lstamp = lstamp;
+        for (int l = 0; l <= L; ++l) { a->kx[l] = kx[l]; a->mxo[l] = mxo[l]; a->ldxm[l] = ldxm[l]; }
+        for (int l = 0; l < L; ++l) { a->mwo[l] = mwo[l]; a->ldwm[l] = ldwm[l]; a->mbo[l] = mbo[l]; }
+    }
+    return off;
+}
+
 constexpr size_t kRopLds = 160 * 1024;
+// psvi_debug_set(PSVI_DBG_ROP_VALU, v): 1 = the VALU R-op kernel, 2 = the
+// matrix-core one with rows of column tiles per unit (A/B)
+int g_rop_valu = 0;
 
 // rows per chunk that fit the LDS (0: the model's weights alone do not fit)
 int rop_rows(const psvi_plan& p) {
@@ -721,12 +1196,45 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     static bool once = [] {
         (void)hipFuncSetAttribute((const void*)net_rop_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRopLds);
+        for (const void* f : {(const void*)net_rop_mfma_kernel<false, false>,
+                              (const void*)net_rop_mfma_kernel<false, true>,
+                              (const void*)net_rop_mfma_kernel<true, false>,
+                              (const void*)net_rop_mfma_kernel<true, true>})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRopLds);
         return true;
     }();
     (void)once;
     RopArgs a{};
     rop_fill(p, a);
     a.nsplit = rop_splits(p);
+    {
+        // the matrix-core form when a row block fits the LDS in one pass
+        const int rows = (p.d.M + a.nsplit - 1) / a.nsplit;
+        const size_t lds = rop_mfma_carve(p, rows, &a) * 4;
+        if (g_rop_valu != 1 && lds <= kRopLds) {
+            a.u = u; a.z = z; a.w = w; a.x = x; a.xd = xd;
+            a.params = params; a.vec = vec; a.eps = eps;
+            a.G = G; a.Gd = Gd; a.du = du; a.nlld = nlld;
+            a.stamps = g_rop_stamps;
+            a.single = 1;
+            const dim3 grid(p.d.S, a.nsplit), block(512);
+            const bool fc = p.family == PSVI_FAMILY_FULLCOV;
+            if (g_rop_valu == 2 && fc)
+                hipLaunchKernelGGL((net_rop_mfma_kernel<true, true>), grid, block, lds, st, a);
+            else if (g_rop_valu == 2)
+                hipLaunchKernelGGL((net_rop_mfma_kernel<true, false>), grid, block, lds, st, a);
+            else if (fc)
+                hipLaunchKernelGGL((net_rop_mfma_kernel<false, true>), grid, block, lds, st, a);
+            else
+                hipLaunchKernelGGL((net_rop_mfma_kernel<false, false>), grid, block, lds, st, a);
+            if (a.nsplit > 1) {
+                const int64_t n = (int64_t)p.d.S * p.n_tot;
+                hipLaunchKernelGGL(slot_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                                   G, Gd, n, a.nsplit);
+            }
+            return hipGetLastError();
+        }
+    }
     // a workgroup's rows in one chunk when they fit without the LDS gradient
     // accumulators (C3: 50 rows, 146 KB): every phase then runs once per
     // workgroup instead of once per chunk

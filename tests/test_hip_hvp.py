@@ -74,3 +74,54 @@ def test_hvp_fullsize_vs_oracle(case):
     assert l2rel(hv0, hv_o) < 1e-4, l2rel(hv0, hv_o)
     assert l2rel(du, du_o) < 1e-4, l2rel(du, du_o)
     assert l2rel(dw, dw_o) < 1e-4, l2rel(dw, dw_o)
+
+
+@pytest.mark.parametrize("family,layers,S,M", [
+    ("fullcov", [(64, 40), (40, 40), (40, 2)], 128, 100),   # C3: 50-row blocks
+    ("fullcov", [(33, 17), (17, 5)], 6, 37),                # ragged: 19 / 18 rows, K not a 16-multiple
+    ("fullcov", [(7, 5), (5, 3)], 4, 3),                    # 2 / 1 rows
+    ("meanfield", [(2, 100), (100, 4)], 32, 50),            # C2
+    ("meanfield", [(5, 7), (7, 7), (7, 3)], 6, 70),
+])
+def test_hvp_kernel_forms_agree(family, layers, S, M):
+    """The matrix-core R-op (net_rop_mfma_kernel, the default where a row block
+    fits the LDS) against the VALU kernel (PSVI_DBG_ROP_VALU A/B), and the
+    full-cov J^T G_dot on the bf16-piece K-split kernel's gradient mode (the
+    default) against the chunked fp32 kernel (PSVI_DBG_KSTREAM_OFF A/B): H vec
+    and both mixed products within 1e-5 relative (l2) -- fp32 sums in another
+    order -- and the default result bitwise run to run."""
+    from psvi.runtime import InnerLoopPlan
+
+    rng = np.random.default_rng(S * 7 + M)
+    fam = "mf" if family == "meanfield" else "mvn"
+    parts = []
+    for din, dout in layers:
+        n = din * dout + dout
+        parts += [0.15 * rng.standard_normal(n), rng.uniform(-5, -4, n)]
+        if fam == "mvn":
+            parts += [2e-4 * rng.standard_normal((n - 1) * (n - 2) // 2)]
+    params = np.concatenate(parts).astype(np.float32)
+    eps = rng.standard_normal(sum(S * (i * o + o) for i, o in layers)).astype(np.float32)
+    u = rng.standard_normal((M, layers[0][0])).astype(np.float32)
+    z = rng.integers(0, layers[-1][1], M).astype(np.int32)
+    w = (1.0 + rng.random(M)).astype(np.float32)
+    vec = rng.standard_normal(params.size).astype(np.float32)
+    plan = InnerLoopPlan(family, layers, S, M)
+    args = (_t(u), _t(z, torch.int32), _t(w), _t(eps), _t(params), _t(vec))
+
+    def run():
+        return [t.cpu().numpy() for t in plan.hvp(*args)]
+
+    a, b = run(), run()
+    alt = []
+    for key in (29, 19):   # the VALU R-op; the chunked gradient-mode update
+        plan.lib.psvi_debug_set(key, 1)
+        try:
+            alt.append(run())
+        finally:
+            plan.lib.psvi_debug_set(key, 0)
+    for x, y, r, c in zip(a, b, *alt):
+        assert np.isfinite(x).all()
+        assert np.array_equal(x, y)
+        assert l2rel(x, r) < 1e-5, l2rel(x, r)
+        assert l2rel(x, c) < 1e-5, l2rel(x, c)

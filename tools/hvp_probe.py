@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--cfg", default="c3")
     ap.add_argument("--n", type=int, default=50)
     ap.add_argument("--stamps", action="store_true", help="net_rop_kernel phase clocks")
+    ap.add_argument("--dbg", action="append", default=[], help="KEY=VALUE psvi_debug_set before timing")
     a = ap.parse_args()
     from psvi.runtime import InnerLoopPlan, randn_
 
@@ -36,6 +37,9 @@ def main():
     eps = torch.empty(plan.eps_count, device=dev)
     randn_(eps, 3)
     ws = plan.workspace()
+    for kv in a.dbg:
+        k, v = kv.split("=")
+        plan.lib.psvi_debug_set(int(k), int(v))
     for mixed in (False, True):
         for _ in range(3):
             plan.hvp(u, z, w, eps, p, vec, mixed=mixed)
@@ -44,7 +48,7 @@ def main():
         for _ in range(a.n):
             plan.hvp(u, z, w, eps, p, vec, mixed=mixed)
         torch.cuda.synchronize()
-        print(f"{a.cfg} psvi_hvp mixed={mixed}: {(time.perf_counter() - t0) / a.n * 1e3:.4f} ms",
+        print(f"{a.cfg} psvi_hvp mixed={mixed} {' '.join(a.dbg)}: {(time.perf_counter() - t0) / a.n * 1e3:.4f} ms",
               flush=True)
     if a.stamps:
         # net_rop_kernel phase clocks (PSVI_DBG_ROP_STAMPS), mean over workgroups
@@ -58,8 +62,8 @@ def main():
         plan.lib.psvi_debug_set_ptr(18, None)
         v = st.cpu().numpy().reshape(nwg, 16).astype(np.float64)
         v = v[v[:, 15] > 0]
-        names = ["weights", "inputs", "fwd0", "fwd1", "fwd2", "head", "bwd2", "bwd1", "bwd0",
-                 "store"]
+        names = ["weights", "inputs|wgrad", "fwd0", "fwd1", "fwd2", "head", "bwd2", "bwd1", "bwd0",
+                 "store|bias"]
         print("net_rop clocks per workgroup (mean): " +
               " ".join(f"{n}={v[:, i].mean():.0f}" for i, n in enumerate(names)) +
               f" total={v[:, :10].sum(1).mean():.0f} chunks={v[:, 15].mean():.1f}", flush=True)
