@@ -1555,14 +1555,21 @@ int psvi_hvp_partial(const psvi_plan* p, const float* u, const int32_t* z, const
         // x = mean + L eps; x_dot = v_mean + (sigmoid(sd) v_sd) eps + v_corr eps
         HIP_TRY(launch_mvn_fwd_pair(*p, eps, params, x, vec, o.xd, o.part2, st));
     }
+    // two row-block slots per sample: added by their consumers (the K-split
+    // gradient mode at staging, the assembly at its loads) rather than by a
+    // slot-sum launch, when the K-split gradient mode runs
+    const bool two = rop_splits(*p) == 2 &&
+                     (p->family != PSVI_FAMILY_FULLCOV || mvn_grad_takes_slots(*p));
+    const int64_t slot2 = two ? (int64_t)p->d.S * p->n_tot : 0;
     HIP_TRY(launch_net_rop(*p, u, z, w, x, o.xd, params, vec, eps, o.G, o.Gd,
-                           du_out ? o.du : nullptr, dw_out ? o.nlld : nullptr, st));
+                           du_out ? o.du : nullptr, dw_out ? o.nlld : nullptr, st, !two));
     if (p->family == PSVI_FAMILY_FULLCOV)  // J^T G_dot (mean, sd, corr; + the corr KL block)
         HIP_TRY(launch_mvn_update(*p, eps, o.Gd, const_cast<float*>(params), nullptr, nullptr,
                                   nullptr, nullptr, hv_out, 0, nullptr, nullptr, st, nullptr,
-                                  false, include_kl ? vec : nullptr));
+                                  false, include_kl ? vec : nullptr, false, nullptr, nullptr,
+                                  two ? o.Gd + slot2 : nullptr));
     HIP_TRY(launch_hvp_assemble(*p, params, vec, eps, o.G, o.Gd, o.du, o.nlld, hv_out, du_out,
-                                dw_out, st, include_kl != 0));
+                                dw_out, st, include_kl != 0, slot2));
     return 0;
 }
 

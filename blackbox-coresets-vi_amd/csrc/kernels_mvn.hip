@@ -1189,6 +1189,7 @@ struct KsArgs {
     // HVP's J^T G_dot), + kl_vec / s0^2 on the corr entries when kl_vec is set
     float* grad_out;
     const float* kl_vec;
+    const float* g2;  // GRAD: a second G slot added at staging (slot 0 + slot 1, as slot_sum_kernel)
 };
 
 // G / eps / corr / m / v through buffer loads whose per-dword range check
@@ -1226,6 +1227,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const rsrc_t rs = make_rsrc(a.slots, a.slot_bytes);
     const rsrc_t rg = make_rsrc(a.g, 4 * a.g_total), re = make_rsrc(a.eps, 4 * a.e_total);
+    const rsrc_t rg2 = make_rsrc(a.g2, GRAD && a.g2 ? 4 * a.g_total : 0);
     // GRAD: m reads kl_vec (0 when none: an empty range), v is not read
     const rsrc_t rpar = make_rsrc(a.params, 4 * a.pcount),
                  rm = make_rsrc(GRAD ? a.kl_vec : a.m, GRAD && !a.kl_vec ? 0 : 4 * a.pcount),
@@ -1265,7 +1267,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
         d.ecol = t.k * UB + 4 * col4;
         return d;
     };
-    float4 greg[8], ereg[8];
+    float4 greg[8], ereg[8], greg2[GRAD ? 8 : 1];
     auto load = [&](const Ld& d, int pi) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1298,12 +1300,19 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             const uint32_t eo = live ? (uint32_t)(d.eoff + s * d.n + d.ecol) * 4u : kOOB;
             greg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0));
             ereg[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
+            if (GRAD) greg2[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg2, go, 0, 0));
         }
     };
     auto stage_half = [&](int hp) __attribute__((always_inline)) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
             const int j = 4 * hp + jj, sl = srow + 16 * jj;
+            if (GRAD && a.g2) {
+                greg[j].x += greg2[j].x;
+                greg[j].y += greg2[j].y;
+                greg[j].z += greg2[j].z;
+                greg[j].w += greg2[j].w;
+            }
             uint32_t x[3][2], y[3][2];
             split3_pk(f32x2{greg[j].x, greg[j].y}, x[0][0], x[1][0], x[2][0]);
             split3_pk(f32x2{greg[j].z, greg[j].w}, x[0][1], x[1][1], x[2][1]);
@@ -3451,12 +3460,17 @@ static void launch_stream(int ns, int kind, dim3 g, dim3 bl, hipStream_t st, con
     launch_stream_ns<4>(kind, g, bl, st, b, pad);
 }
 
+bool mvn_grad_takes_slots(const psvi_plan& p) {
+    return p.n_kwg > 0 && !g_ks_off && !g_ks_bf_off && !g_upd_stamps;
+}
+
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,
                              float* params, float* m, float* v, const psvi_adam_hp* hp,
                              double* kl_out, float* grad_out, int include_kl,
                              const float* eps_next, float* x_next, hipStream_t st,
                              float* tstate, bool packed_out, const float* kl_vec, bool padded,
-                             const uint16_t* eps_planes, const uint16_t* eps_next_planes) {
+                             const uint16_t* eps_planes, const uint16_t* eps_next_planes,
+                             const float* g_shard2) {
     UpdArgs a{};
     a.kl_vec = kl_vec;
     a.chunks = p.d_upd;
@@ -3583,7 +3597,8 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         return hipGetLastError();
     }
     // gradient mode (the HVP's J^T G_dot) at any S on the bf16-piece K-split kernel
-    const bool ks_grad = grad_out && p.n_kwg > 0 && !g_ks_off && !g_ks_bf_off && !g_upd_stamps;
+    const bool ks_grad = grad_out && mvn_grad_takes_slots(p);
+    if (g_shard2 && !ks_grad) return hipErrorInvalidValue;
     if ((mode == 2 && !grad_out && p.n_kwg > 0 && g_ks_off != 1) || ks_grad) {
         // K = S > 128: the K-split streaming update (then the next step's
         // sample from the new parameters when asked)
@@ -3612,6 +3627,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
         k.stamps = g_upd_stamps;
         k.grad_out = grad_out;
         k.kl_vec = kl_vec;
+        k.g2 = g_shard2;
         fill_layers(p, k.lay);
         if (ks_grad)
             hipLaunchKernelGGL((mvn_kstream_kernel<true, true>), dim3(p.n_kwg), block, 0, st, k);

@@ -548,21 +548,6 @@ struct RopFrag {
             if (TB) bt[c] = ld(q + ob, ldb, BCONT);
         }
     }
-    // a contraction over rows (both operands k-strided): rows r0 + kstep(j)
-    // at or past kv read as 0 -- selected, so stale LDS past the rows is inert
-    __device__ __forceinline__ void mask(int r0, int kv) {
-        auto m = [&](floatx4& v) __attribute__((always_inline)) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = r0 + kstep<PERM>(j) < kv ? v[j] : 0.f;
-        };
-        m(a);
-        if (TA) m(at);
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-            m(b[c]);
-            if (TB) m(bt[c]);
-        }
-    }
     __device__ __forceinline__ void mma(floatx4 (&x)[NQ], floatx4 (&y)[NQ]) const {
 #pragma unroll
         for (int c = 0; c < NQ; ++c)
@@ -583,34 +568,42 @@ struct RopFrag {
 // epilogues (row (r + rot) & 3 of the four is value r).
 template <bool ACONT, bool BCONT, int NQ, bool TA, bool TB, bool WX, class Epi>
 __device__ __forceinline__ void rop_steps(int nu, int tqu, int nk, int u0, int nwv, const float* A,
-                                          int lda, int oa, const float* B, int ldb, int ob, int kv,
-                                          Epi epi) {
+                                          int lda, int oa, const float* B, int ldb, int ob, Epi epi) {
     using F = RopFrag<ACONT, BCONT, NQ, TA, TB, WX>;
     constexpr bool PERM = F::PERM;
     const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
-    const bool km = !ACONT && !BCONT && kv < 16 * nk;  // uniform
     const int da = ACONT ? 16 : 16 * lda, db = BCONT ? 16 : 16 * ldb;
     const int rot = (k4 & 1) << 1, r0 = kbase<PERM>(k4);
     for (int u = u0; u < nu; u += nwv) {  // wave-uniform
         const int pt = u / tqu, p0 = pt << 4, q0 = ((u - pt * tqu) * NQ) << 4;
         const float* pa = ACONT ? A + (p0 + i16) * lda + 4 * k4 : A + r0 * lda + p0 + i16;
         const float* pb = BCONT ? B + (q0 + i16) * ldb + 4 * k4 : B + r0 * ldb + q0 + i16;
-        auto fetch = [&](F& f, int kg) __attribute__((always_inline)) {
-            f.load(pa + kg * da, lda, oa, pb + kg * db, ldb, ob);
-            if (km && kg == nk - 1) f.mask(16 * kg + r0, kv);
-        };
         floatx4 x[NQ], y[NQ];
 #pragma unroll
         for (int c = 0; c < NQ; ++c) x[c] = y[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // two k-groups per trip with fixed registers (the next group's LDS
+        // reads in flight across the current group's MFMAs), then the tail
         F f0, f1;
-        fetch(f0, 0);
-        for (int kg = 0; kg < nk; kg += 2) {  // uniform
-            if (kg + 1 < nk) fetch(f1, kg + 1);
+        f0.load(pa, lda, oa, pb, ldb, ob);
+        int kg = 0;
+        for (; kg + 2 < nk; kg += 2) {
+            pa += da;
+            pb += db;
+            f1.load(pa, lda, oa, pb, ldb, ob);
             f0.mma(x, y);
-            if (kg + 1 < nk) {
-                if (kg + 2 < nk) fetch(f0, kg + 2);
-                f1.mma(x, y);
-            }
+            pa += da;
+            pb += db;
+            f0.load(pa, lda, oa, pb, ldb, ob);
+            f1.mma(x, y);
+        }
+        if (kg + 1 < nk) {
+            pa += da;
+            pb += db;
+            f1.load(pa, lda, oa, pb, ldb, ob);
+            f0.mma(x, y);
+            f1.mma(x, y);
+        } else {
+            f0.mma(x, y);
         }
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
@@ -621,11 +614,11 @@ __device__ __forceinline__ void rop_steps(int nu, int tqu, int nk, int u0, int n
     }
 }
 
-// P x Q outputs, contraction over nk k-groups of 16 (kv: the true length when
-// both operands are k-strided).  A row of column tiles per unit (one A read
+// P x Q outputs, contraction over K16 / 16 k-groups of 16 (operand rows or
+// columns past the true length are zero in LDS).  A row of column tiles per unit (one A read
 // per NQ tiles) when that still gives each SIMD a unit, else single tiles.
 template <bool WIDE, bool ACONT, bool BCONT, bool TA, bool TB, bool WX, class Epi>
-__device__ __forceinline__ void rop_gemm(int P, int Q, int K16, int kv, int first, const float* A,
+__device__ __forceinline__ void rop_gemm(int P, int Q, int K16, int first, const float* A,
                                          int lda, int oa, const float* B, int ldb, int ob, Epi epi) {
     const int nwv = blockDim.x >> 6, wid = wave_id();
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, nk = K16 >> 4;
@@ -633,15 +626,15 @@ __device__ __forceinline__ void rop_gemm(int P, int Q, int K16, int kv, int firs
     const int nq = (WIDE && tq <= 3 && tp >= 4) ? tq : 1;
     if constexpr (WIDE) {
         if (nq == 3) {
-            rop_steps<ACONT, BCONT, 3, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, kv, epi);
+            rop_steps<ACONT, BCONT, 3, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, epi);
             return;
         }
         if (nq == 2) {
-            rop_steps<ACONT, BCONT, 2, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, kv, epi);
+            rop_steps<ACONT, BCONT, 2, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, epi);
             return;
         }
     }
-    rop_steps<ACONT, BCONT, 1, TA, TB, WX>(tp * tq, tq, nk, u0, nwv, A, lda, oa, B, ldb, ob, kv, epi);
+    rop_steps<ACONT, BCONT, 1, TA, TB, WX>(tp * tq, tq, nk, u0, nwv, A, lda, oa, B, ldb, ob, epi);
 }
 
 // The R-op on the matrix cores: one workgroup per (sample, row block), its
@@ -753,11 +746,33 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                     float* d = sm + a.mxo[0] + row * ld0 + c0;
                     if (c < kx0) {
                         lds_dma4(ru, d, c < D ? 4u * (uint32_t)(row * D + c) : kOOB);
-                        lds_dma4(ru, d + kx0, kOOB);
                     }
                 }
             }
+            // rows rc .. rup16(rc) of every activation region (contiguous) and
+            // the u rows' tangent half: zero, by plain stores (disjoint from the DMAs)
+            {
+                const int nz = ((rc + 15) & ~15) - rc;
+                for (int l = 0; l <= L; ++l) {
+                    float4* z4 = reinterpret_cast<float4*>(sm + a.mxo[l] + rc * a.ldxm[l]);
+                    for (int i = tid; i < (nz * a.ldxm[l]) >> 2; i += nt) z4[i] = float4{0.f, 0.f, 0.f, 0.f};
+                }
+                const int kx0 = a.kx[0], q4 = kx0 >> 2;
+                for (int i = tid; i < rc * q4; i += nt) {
+                    const int row = i / q4;
+                    reinterpret_cast<float4*>(sm + a.mxo[0] + row * a.ldxm[0] + kx0)[i - row * q4] =
+                        float4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (D < a.kx[0]) {
+                // layer 0's ones column, over this wave's own DMA'd rows
+                const int ld0 = a.ldxm[0];
+                for (int r = wid; r < rc * nch0; r += nwv) {  // wave-uniform
+                    const int row = nch0 == 1 ? r : r / nch0, c0 = (r - row * nch0) << 6;
+                    if (c0 + lane == D) sm[a.mxo[0] + row * ld0 + D] = 1.f;
+                }
+            }
         } else {
             auto fetch_w = [&](int l, int i, float& xv, float& xdv) __attribute__((always_inline)) {
                 // element i of layer l's sampled weights (W row-major, then b) and its tangent
@@ -769,6 +784,11 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                 xv = a.params[pm] + softplus_f(rho) * e;
                 xdv = a.vec[pm] + sigmoid_f(rho) * a.vec[pr] * e;
             };
+            {
+                const int nz = ((rc + 15) & ~15) - rc;
+                for (int l = 0; l <= L; ++l)
+                    for (int i = tid; i < nz * a.ldxm[l]; i += nt) sm[a.mxo[l] + rc * a.ldxm[l] + i] = 0.f;
+            }
             for (int j = wid; j < njobs; j += nwv) {  // wave-uniform
                 int kind, l, row, c0;
                 decode(j, kind, l, row, c0);
@@ -788,6 +808,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                         sm[a.mbo[l] + a.kx[l + 1] + c] = v1;
                     }
                 } else {
+                    v0 = c == D ? 1.f : 0.f;  // the ones column
                     if (c < D) v0 = a.u[(int64_t)(m0 + row) * D + c];
                     if (c < a.kx[0]) {
                         float* x0 = sm + a.mxo[0] + row * a.ldxm[0] + c;
@@ -800,7 +821,12 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
     }
     __syncthreads();
     ph(0);
-    // ---- forward + tangent forward
+    // ---- forward + tangent forward, a workgroup barrier per layer.  A layer
+    // whose input width is not a 16-multiple gets a column of ones at din in h
+    // (W's padding column there is zero), so the weight-gradient GEMM yields
+    // the bias gradient as its column din.  (A row chain -- each wave carrying
+    // its 16-row tiles through every layer with no barrier -- leaves half the
+    // waves idle at C3's 50-row blocks and measured slower.)
     for (int l = 0; l < L; ++l) {
         const int dout = a.dout[l], kxl = a.kx[l], kq = a.kx[l + 1], ldn = a.ldxm[l + 1];
         const float* bl = sm + a.mbo[l];
@@ -808,47 +834,44 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
         const bool last = l == L - 1;
         auto epi = [&](int pr, int q, floatx4 vx, floatx4 vy, int rot) __attribute__((always_inline)) {
             const float b = bl[q], bd = bl[kq + q];  // zero past dout, as the W2 rows
+            const bool one = !last && q == dout;     // the next layer's ones column
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = pr + ((r + rot) & 3);
                 if (m < rc) {
                     const float av = vx[r] + b, ad = vy[r] + bd;
                     const bool on = last || av > 0.f;
-                    Xn[m * ldn + q] = on ? av : 0.f;
+                    Xn[m * ldn + q] = one ? 1.f : on ? av : 0.f;
                     Xn[m * ldn + kq + q] = on ? ad : 0.f;
                 }
             }
         };
-        const float* Xl = sm + a.mxo[l];
-        const float* W2 = sm + a.mwo[l];
-        rop_gemm<WIDE, true, true, true, true, true>(rc, dout, kxl, kxl, 0, Xl, a.ldxm[l], kxl, W2, a.ldwm[l], kxl, epi);
+        rop_gemm<WIDE, true, true, true, true, true>(rc, dout, kxl, 0, sm + a.mxo[l], a.ldxm[l], kxl,
+                                                     sm + a.mwo[l], a.ldwm[l], kxl, epi);
         __syncthreads();
         ph(2 + min(l, 2));
     }
     // ---- head, in place on X_L: delta = w (p - onehot), delta_dot = w p (a_dot - p.a_dot)
-    {
-        const int ldh = a.ldxm[L], kc = a.kx[L];
-        for (int m = tid; m < rc; m += nt) {
-            float* lg = sm + a.mxo[L] + m * ldh;
-            float* ld = lg + kc;
-            const int zm = a.z[m0 + m];
-            const float wm = a.w[m0 + m];
-            float mx = -INFINITY;
-            for (int c = 0; c < C; ++c) mx = fmaxf(mx, lg[c]);
-            float se = 0.f;
-            for (int c = 0; c < C; ++c) se += expf(lg[c] - mx);
-            const float lse = mx + logf(se);
-            float pad = 0.f, nd = 0.f;
-            for (int c = 0; c < C; ++c) pad += expf(lg[c] - lse) * ld[c];
-            for (int c = 0; c < C; ++c) {
-                const float p = expf(lg[c] - lse), ldc = ld[c];
-                const float pmo = p - (c == zm ? 1.f : 0.f);
-                nd = fmaf(pmo, ldc, nd);
-                lg[c] = wm * pmo;
-                ld[c] = wm * p * (ldc - pad);
-            }
-            if (a.nlld) a.nlld[(int64_t)s * a.M + m0 + m] = nd;
+    for (int m = tid; m < rc; m += nt) {
+        float* lg = sm + a.mxo[L] + m * a.ldxm[L];
+        float* ld = lg + a.kx[L];
+        const int zm = a.z[m0 + m];
+        const float wm = a.w[m0 + m];
+        float mx = -INFINITY;
+        for (int c = 0; c < C; ++c) mx = fmaxf(mx, lg[c]);
+        float se = 0.f;
+        for (int c = 0; c < C; ++c) se += expf(lg[c] - mx);
+        const float lse = mx + logf(se);
+        float pad = 0.f, nd = 0.f;
+        for (int c = 0; c < C; ++c) pad += expf(lg[c] - lse) * ld[c];
+        for (int c = 0; c < C; ++c) {
+            const float p = expf(lg[c] - lse), ldc = ld[c];
+            const float pmo = p - (c == zm ? 1.f : 0.f);
+            nd = fmaf(pmo, ldc, nd);
+            lg[c] = wm * pmo;
+            ld[c] = wm * p * (ldc - pad);
         }
+        if (a.nlld) a.nlld[(int64_t)s * a.M + m0 + m] = nd;
     }
     __syncthreads();
     ph(5);
@@ -864,22 +887,26 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
         float* GDW = a.Gd + gslot;
         // weight gradients: G[o][i] = sum_m delta[m][o] h[m][i],
         // G_dot[o][i] = sum_m delta[m][o] h_dot[m][i] + delta_dot[m][o] h[m][i]
+        // (the ones column: column din is the bias gradient)
+        const bool ones = din < kxl;
         auto wepi = [&](int pr, int q, floatx4 vx, floatx4 vy, int rot) __attribute__((always_inline)) {
-            if (q >= din) return;
+            if (q > din || (q == din && !ones)) return;
+            const int e0 = q < din ? q : nw, es = q < din ? din : 1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int o = pr + ((r + rot) & 3);
                 if (o < dout) {
-                    GW[o * din + q] = vx[r];
-                    GDW[o * din + q] = vy[r];
+                    GW[o * es + e0] = vx[r];
+                    GDW[o * es + e0] = vy[r];
                 }
             }
         };
         const int K16 = (rc + 15) & ~15;
-        rop_gemm<WIDE, false, false, true, true, true>(dout, din, K16, rc, 0, Dl, ldd, kq, Xl, ldx, kxl, wepi);
+        rop_gemm<WIDE, false, false, true, true, true>(dout, din + (ones ? 1 : 0), K16, 0, Dl, ldd, kq, Xl,
+                                                       ldx, kxl, wepi);
         ph(1);
-        // bias gradients: column sums of delta / delta_dot, a wave per column
-        {
+        // bias gradients without a ones column: column sums of delta / delta_dot, a wave per column
+        if (!ones) {
             const int lane = tid & 63, nwv = nt >> 6;
             for (int o = wave_id(); o < dout; o += nwv) {  // wave-uniform
                 float g = 0.f, gd = 0.f;
@@ -911,7 +938,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                     }
                 }
             };
-            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, kq, 0, Dl, ldd, kq, W2, a.ldwm[l], kxl, pepi);
+            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, 0, Dl, ldd, kq, W2, a.ldwm[l], kxl, pepi);
             __syncthreads();
         } else if (a.du) {
             // d/du of (vec . grad): the input rows' delta_dot (no mask at the input)
@@ -923,7 +950,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                     if (m < rc) a.du[((int64_t)s * a.M + m0 + m) * D + q] = vy[r];
                 }
             };
-            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, kq, 0, Dl, ldd, kq, W2, a.ldwm[0], kxl, uepi);
+            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, 0, Dl, ldd, kq, W2, a.ldwm[0], kxl, uepi);
         }
         ph(6 + min(L - 1 - l, 2));
     }
@@ -964,8 +991,15 @@ __device__ __forceinline__ void sample_quarter(int S, int wv, int& s0, int& s1) 
     s1 = min(S, s0 + q);
 }
 
+template <bool SLOTS, bool FC>
 __global__ __launch_bounds__(256) void hvp_param_kernel(RopArgs a, float* hv, float inv_s0sq,
-                                                        float klw) {
+                                                        float klw, int64_t slot2) {
+    // SLOTS: G / G_dot still in the R-op's two row-block slots (slot 1 at
+    // + slot2), added here as slot_sum_kernel would: slot 0 + slot 1.  FC:
+    // full-cov needs sum_s G eps alone (the update kernel's gradient mode did G_dot)
+    auto gl = [&](const float* P, int64_t i) __attribute__((always_inline)) {
+        return SLOTS ? P[i] + P[slot2 + i] : P[i];
+    };
     __shared__ float part[kAsmWaves][3][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
@@ -996,8 +1030,8 @@ __global__ __launch_bounds__(256) void hvp_param_kernel(RopArgs a, float* hv, fl
         float g4[4], d4[4], e4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            g4[j] = a.G[(int64_t)(s + j) * a.n_tot + ec];
-            d4[j] = a.Gd[(int64_t)(s + j) * a.n_tot + ec];
+            g4[j] = gl(a.G, (int64_t)(s + j) * a.n_tot + ec);
+            d4[j] = FC ? 0.f : gl(a.Gd, (int64_t)(s + j) * a.n_tot + ec);
             e4[j] = a.eps[ebase + (int64_t)(s + j) * es];
         }
 #pragma unroll
@@ -1008,7 +1042,7 @@ __global__ __launch_bounds__(256) void hvp_param_kernel(RopArgs a, float* hv, fl
         }
     }
     for (; s < s1; ++s) {
-        const float g = a.G[(int64_t)s * a.n_tot + ec], dv = a.Gd[(int64_t)s * a.n_tot + ec];
+        const float g = gl(a.G, (int64_t)s * a.n_tot + ec), dv = FC ? 0.f : gl(a.Gd, (int64_t)s * a.n_tot + ec);
         const float ev = a.eps[ebase + (int64_t)s * es];
         ge = fmaf(g, ev, ge);
         gd += dv;
@@ -1192,7 +1226,7 @@ static void rop_fill(const psvi_plan& p, RopArgs& a) {
 hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                           const float* x, const float* xd, const float* params, const float* vec,
                           const float* eps, float* G, float* Gd, float* du, float* nlld,
-                          hipStream_t st) {
+                          hipStream_t st, bool sum_slots) {
     static bool once = [] {
         (void)hipFuncSetAttribute((const void*)net_rop_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRopLds);
@@ -1209,7 +1243,9 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     a.nsplit = rop_splits(p);
     {
         // the matrix-core form when a row block fits the LDS in one pass
-        const int rows = (p.d.M + a.nsplit - 1) / a.nsplit;
+        // rows padded to a 16-multiple: the rows past a block's own are zero
+        // (the contraction over rows runs to the 16-multiple)
+        const int rows = (((p.d.M + a.nsplit - 1) / a.nsplit) + 15) & ~15;
         const size_t lds = rop_mfma_carve(p, rows, &a) * 4;
         if (g_rop_valu != 1 && lds <= kRopLds) {
             a.u = u; a.z = z; a.w = w; a.x = x; a.xd = xd;
@@ -1227,7 +1263,7 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
                 hipLaunchKernelGGL((net_rop_mfma_kernel<false, true>), grid, block, lds, st, a);
             else
                 hipLaunchKernelGGL((net_rop_mfma_kernel<false, false>), grid, block, lds, st, a);
-            if (a.nsplit > 1) {
+            if (a.nsplit > 1 && sum_slots) {
                 const int64_t n = (int64_t)p.d.S * p.n_tot;
                 hipLaunchKernelGGL(slot_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                                    G, Gd, n, a.nsplit);
@@ -1249,7 +1285,7 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     a.G = G; a.Gd = Gd; a.du = du; a.nlld = nlld;
     a.stamps = g_rop_stamps;
     hipLaunchKernelGGL(net_rop_kernel, dim3(p.d.S, a.nsplit), dim3(512), lds, st, a);
-    if (a.nsplit > 1) {
+    if (a.nsplit > 1 && sum_slots) {
         const int64_t n = (int64_t)p.d.S * p.n_tot;
         hipLaunchKernelGGL(slot_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, G,
                            Gd, n, a.nsplit);
@@ -1260,15 +1296,20 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
 hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const float* vec,
                                const float* eps, const float* G, const float* Gd, const float* du,
                                const float* nlld, float* hv, float* d_u, float* d_w,
-                               hipStream_t st, bool include_kl) {
+                               hipStream_t st, bool include_kl, int64_t slot2) {
     RopArgs a{};
     rop_fill(p, a);
     a.params = params; a.vec = vec; a.eps = eps;
     a.G = const_cast<float*>(G);
     a.Gd = const_cast<float*>(Gd);
     const float s0 = p.d.prior_sd;
-    hipLaunchKernelGGL(hvp_param_kernel, dim3((unsigned)((p.n_tot + 63) / 64)), dim3(256), 0, st,
-                       a, hv, 1.f / (s0 * s0), include_kl ? 1.f : 0.f);
+    const dim3 pg((unsigned)((p.n_tot + 63) / 64)), pb(256);
+    const float is2 = 1.f / (s0 * s0), klw = include_kl ? 1.f : 0.f;
+    const bool fc = p.family == PSVI_FAMILY_FULLCOV;
+    if (slot2 && fc) hipLaunchKernelGGL((hvp_param_kernel<true, true>), pg, pb, 0, st, a, hv, is2, klw, slot2);
+    else if (slot2) hipLaunchKernelGGL((hvp_param_kernel<true, false>), pg, pb, 0, st, a, hv, is2, klw, slot2);
+    else if (fc) hipLaunchKernelGGL((hvp_param_kernel<false, true>), pg, pb, 0, st, a, hv, is2, klw, slot2);
+    else hipLaunchKernelGGL((hvp_param_kernel<false, false>), pg, pb, 0, st, a, hv, is2, klw, slot2);
     const int S = p.d.S, M = p.d.M, D = p.lay[0].din;
     if (d_u) {
         const int64_t n = (int64_t)M * D;

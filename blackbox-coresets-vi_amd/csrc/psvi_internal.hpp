@@ -558,7 +558,11 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                              float* tstate = nullptr, bool packed_out = false,
                              const float* kl_vec = nullptr, bool padded = false,
                              const uint16_t* eps_planes = nullptr,
-                             const uint16_t* eps_next_planes = nullptr);
+                             const uint16_t* eps_next_planes = nullptr,
+                             const float* g_shard2 = nullptr);
+// the gradient-mode update takes a second G slot (g_shard2: added to g_shard at
+// staging, the R-op's row-block slots unsummed) when this holds
+bool mvn_grad_takes_slots(const psvi_plan& p);
 // pads (to_tiled, nullable): three 64-float regions the first workgroup zeroes
 hipError_t launch_mvn_tile_convert(const psvi_plan& p, float* params, float* m, float* v,
                                    float* tstate, bool to_tiled, hipStream_t st,
@@ -628,9 +632,9 @@ int rop_splits(const psvi_plan& p);  // row blocks per sample: G / G_dot slots
 hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, const float* w,
                           const float* x, const float* xd, const float* params, const float* vec,
                           const float* eps, float* G, float* Gd, float* du, float* nlld,
-                          hipStream_t st);
+                          hipStream_t st, bool sum_slots = true);
 hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const float* vec,
                                const float* eps, const float* G, const float* Gd, const float* du,
                                const float* nlld, float* hv, float* d_u, float* d_w,
-                               hipStream_t st, bool include_kl = true);
+                               hipStream_t st, bool include_kl = true, int64_t slot2 = 0);
 }  // namespace psvi
