@@ -3461,7 +3461,7 @@ static void launch_stream(int ns, int kind, dim3 g, dim3 bl, hipStream_t st, con
 }
 
 bool mvn_grad_takes_slots(const psvi_plan& p) {
-    return p.n_kwg > 0 && !g_ks_off && !g_ks_bf_off && !g_upd_stamps;
+    return p.n_kwg > 0 && !g_ks_off && !g_ks_bf_off;
 }
 
 hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* g_shard,

@@ -533,7 +533,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     eight (A/B)                               */
 #define PSVI_DBG_ROP_VALU 29         /* value: 1 = the R-op (psvi_hvp's tangent
                                     forward and R-backward) on the VALU kernel
-                                    instead of the matrix-core one (A/B)       */
+                                    instead of the matrix-core one; 2 = the
+                                    matrix-core one with a row of up to three
+                                    column tiles per wave unit (A/B)           */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */

@@ -4,7 +4,9 @@ K-split update (mvn_kstream_kernel) and the sample kernel (mvn_fwd_kernel)
 under the diagnostics API -- event timing and per-workgroup shader-clock
 phase sums / 100 MHz timeline.
 
-  python tools/ks_stamps.py [W] [rank] [S] [kstream workgroups, 0 = default]
+  python tools/ks_stamps.py [W] [rank] [S] [kstream workgroups, 0 = default] [grad]
+
+"grad": the gradient mode (grad_out, no KL: the HVP's J^T G_dot) instead of Adam.
 """
 import ctypes
 import os
@@ -64,7 +66,12 @@ def main():
     maxblk = 1 << 14
     st = torch.zeros(maxblk * 16, dtype=torch.int64, device=dev)
 
-    upd = lambda: plan.mvn_update(eps, gs, params, m, v, step=3, lr=1e-3, kind="higher", kl_out=kl)
+    grad = len(sys.argv) > 5 and sys.argv[5] == "grad"
+    gout = torch.zeros_like(params)
+    if grad:
+        upd = lambda: plan.mvn_update(eps, gs, params, grad_out=gout, include_kl=False)
+    else:
+        upd = lambda: plan.mvn_update(eps, gs, params, m, v, step=3, lr=1e-3, kind="higher", kl_out=kl)
     us = timed(upd)
     st.zero_()
     lib.psvi_debug_set_ptr(4, ctypes.c_void_p(st.data_ptr()))
