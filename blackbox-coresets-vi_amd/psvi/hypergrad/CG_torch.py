@@ -15,19 +15,36 @@ def cat_list_to_tensor(list_tx):
 
 
 def cg(Ax, b, max_iter=100, epsilon=1.0e-5):
-    x = [torch.zeros_like(t) for t in b]
-    r = [t.clone() for t in b]
-    p = [t.clone() for t in r]
+    """The reference's iteration on one flat buffer per vector (the lists Ax
+    sees are views into it), with its stopping test kept on the device: once
+    ||r_new|| < epsilon the iterate freezes (torch.where) -- the same x the
+    reference's ``break`` returns -- so no iteration waits on a host read of
+    the norm.  After convergence the remaining iterations still evaluate Ax
+    (discarded); on a GPU the host otherwise idles the device once per
+    iteration (the fused HVPs take ~0.13 ms, the round trip about as long)."""
+    shapes = [t.shape for t in b]
+    sizes = [t.numel() for t in b]
+
+    def flat(ts):
+        return cat_list_to_tensor(ts) if len(ts) > 1 else ts[0].reshape(-1)
+
+    def views(v):
+        return [c.view(sh) for c, sh in zip(torch.split(v, sizes), shapes)]
+
+    r = flat(b).clone()
+    x = torch.zeros_like(r)
+    p = r.clone()
+    done = torch.zeros((), dtype=torch.bool, device=r.device)
     for _ in range(max_iter):
-        Ap = Ax(p)
-        rr = torch.sum(cat_list_to_tensor(r) ** 2)
-        alpha = rr / torch.sum(cat_list_to_tensor(p) * cat_list_to_tensor(Ap))
-        x_new = [xi + alpha * pi for xi, pi in zip(x, p)]
-        r_new = [ri - alpha * api for ri, api in zip(r, Ap)]
-        rn = cat_list_to_tensor(r_new)
-        if float(torch.linalg.vector_norm(rn)) < epsilon:
-            break
-        beta = torch.sum(rn * rn) / rr
-        p = [ri + beta * pi for ri, pi in zip(r_new, p)]
-        x, r = x_new, r_new
-    return x
+        Ap = flat(Ax(views(p)))
+        rr = torch.dot(r, r)
+        alpha = rr / torch.dot(p, Ap)
+        x_new = x + alpha * p
+        r_new = r - alpha * Ap
+        done = done | (torch.linalg.vector_norm(r_new) < epsilon)
+        beta = torch.dot(r_new, r_new) / rr
+        p_new = r_new + beta * p
+        x = torch.where(done, x, x_new)
+        r = torch.where(done, r, r_new)
+        p = torch.where(done, p, p_new)
+    return views(x)

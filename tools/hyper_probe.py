@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """C3 hyper_step (inner_it = 100, K = 30) and nested_step wall time, as
 bench.py's trainer timings (the reference init, a 128-row data batch):
-  python tools/hyper_probe.py [n]"""
+  python tools/hyper_probe.py [n] [hyper|nested]"""
 import os
 import sys
 import time
@@ -32,8 +32,11 @@ def main():
     ps.device = dev
     ps.register_elbos = False
     ps.setup_optimizers()
+    only = sys.argv[2] if len(sys.argv) > 2 else ""
     for name, fn in (("hyper_step_T100_K30", lambda: ps.hyper_step(xb, yb, K=30)),
                      ("nested_step_T100", lambda: ps.nested_step(xb, yb))):
+        if only and not name.startswith(only):
+            continue
         fn()
         torch.cuda.synchronize()
         ts = []
