@@ -31,20 +31,24 @@ def cg(Ax, b, max_iter=100, epsilon=1.0e-5):
     def views(v):
         return [c.view(sh) for c, sh in zip(torch.split(v, sizes), shapes)]
 
+    # per iteration six passes over the vectors (two dots, four fused
+    # x + a y): alpha / beta stay 0-dim device tensors; where the reference
+    # breaks, the step length is zeroed instead (x and r keep their values;
+    # p no longer enters them)
     r = flat(b).clone()
     x = torch.zeros_like(r)
     p = r.clone()
+    rr = torch.dot(r, r)
     done = torch.zeros((), dtype=torch.bool, device=r.device)
+    zero = torch.zeros((), dtype=r.dtype, device=r.device)
     for _ in range(max_iter):
         Ap = flat(Ax(views(p)))
-        rr = torch.dot(r, r)
         alpha = rr / torch.dot(p, Ap)
-        x_new = x + alpha * p
-        r_new = r - alpha * Ap
-        done = done | (torch.linalg.vector_norm(r_new) < epsilon)
-        beta = torch.dot(r_new, r_new) / rr
-        p_new = r_new + beta * p
-        x = torch.where(done, x, x_new)
+        rn = torch.dot(r_new := torch.addcmul(r, alpha, Ap, value=-1), r_new)
+        done = done | (torch.sqrt(rn) < epsilon)
+        a_eff = torch.where(done, zero, alpha)
+        x = torch.addcmul(x, a_eff, p)
         r = torch.where(done, r, r_new)
-        p = torch.where(done, p, p_new)
+        p = torch.addcmul(r, rn / rr, p)
+        rr = torch.where(done, rr, rn)
     return views(x)

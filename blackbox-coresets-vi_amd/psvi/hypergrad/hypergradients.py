@@ -111,7 +111,7 @@ def CG(params, hparams, K, fp_map, outer_loss, tol=1e-10, set_grad=True, stochas
         wm = fp_map(params, hparams) if stochastic else w_mapped
         with params_only(wm):
             jt = torch_grad(wm, params, grad_outputs=_like(xs, wm), retain_graph=not stochastic)
-        return [x - j.to(torch.float64) for x, j in zip(xs, jt)]
+        return [torch.sub(x, j) for x, j in zip(xs, jt)]  # fp64 - fp32: promoted in the one kernel
 
     vs = CG_torch.cg(A, _f64(g_w), max_iter=K, epsilon=tol)
     if stochastic:
@@ -139,9 +139,9 @@ def CG_normaleq(params, hparams, K, fp_map, outer_loss, tol=1e-10, set_grad=True
     def A(xs):
         with params_only(w_mapped):
             jt = torch_grad(w_mapped, params, grad_outputs=_like(xs, w_mapped), retain_graph=True)
-        r = [x - j.to(torch.float64) for x, j in zip(xs, jt)]
+        r = [torch.sub(x, j) for x, j in zip(xs, jt)]  # fp64 - fp32: promoted in the one kernel
         jr = jvp(fmap, params, r)
-        return [a - b.detach().to(torch.float64) for a, b in zip(r, jr)]
+        return [torch.sub(a, b.detach()) for a, b in zip(r, jr)]
 
     g64 = _f64(g_w)
     b = [g - j.detach().to(torch.float64) for g, j in zip(g64, jvp(fmap, params, g64))]
