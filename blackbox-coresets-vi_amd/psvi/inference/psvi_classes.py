@@ -944,12 +944,12 @@ class PSVI:
         lr = float(linsys_lr)
         hws = torch.empty(plan.hvp_ws_bytes, dtype=torch.uint8, device=params.device)
 
-        def hvp(e, x, mixed=False):
+        def hvp(e, x, mixed=False, f64=True):
             hv, du, dw = plan.hvp(u, z, w, e, params, x.to(torch.float32).contiguous(),
                                   mixed=mixed, ws=hws)
             if mixed:
                 du, dw = self._fold(plan, du, dw)
-            return hv.to(torch.float64), du, dw
+            return (hv.to(torch.float64) if f64 else hv), du, dw
 
         if hypergrad_approx == "fixed_point":
             # hypergradients.py:83-140 with stochastic=True: a fresh fp_map per iteration
@@ -981,29 +981,38 @@ class PSVI:
         returns the draw of w_mapped, leaves the solution in self._cg_x."""
         eA = draw_inner()                       # w_mapped = fp_map(params, hparams)
 
+        def hv32(e, x):                         # H x (fp32, as psvi_hvp returns it)
+            return hvp(e, x, f64=False)[0]
+
         def jvp(x):                             # J x = x - lr H x (fp_map drawn twice)
             draw_inner()
-            return x - lr * hvp(draw_inner(), x)[0]
+            return torch.sub(x, hv32(draw_inner(), x), alpha=lr)  # fp32 H x promoted in the one pass
 
         def A(x):                               # dfp_map_dw
-            vmj = lr * hvp(eA, x)[0]
+            vmj = hv32(eA, x).to(torch.float64).mul_(lr)
             return vmj - jvp(vmj)
 
         b = g_w - jvp(g_w)
+        # CG_torch.cg(Ax, b, max_iter=K, epsilon=1e-10) with fused x + a y passes
+        # and 0-dim device step lengths; the stopping test stays on the device:
+        # where the reference breaks, the step length is zeroed (x and r keep
+        # their values), so no iteration waits on a host read of the norm
         xk = torch.zeros_like(b)
         r = b.clone()
         pk = r.clone()
-        for _ in range(int(K)):                 # CG_torch.cg(Ax, b, max_iter=K, epsilon=1e-10)
+        rTr = torch.dot(r, r)
+        done = torch.zeros((), dtype=torch.bool, device=b.device)
+        zero = torch.zeros((), dtype=b.dtype, device=b.device)
+        for _ in range(int(K)):
             Ap = A(pk)
-            rTr = torch.dot(r, r)
             alpha = rTr / torch.dot(pk, Ap)
-            xn = xk + alpha * pk
-            rn = r - alpha * Ap
-            if float(torch.linalg.vector_norm(rn)) < 1e-10:
-                break
-            beta = torch.dot(rn, rn) / rTr
-            pk = rn + beta * pk
-            xk, r = xn, rn
+            rn = torch.addcmul(r, alpha, Ap, value=-1)
+            rnrn = torch.dot(rn, rn)
+            done = done | (torch.sqrt(rnrn) < 1e-10)
+            xk = torch.addcmul(xk, torch.where(done, zero, alpha), pk)
+            r = torch.where(done, r, rn)
+            pk = torch.addcmul(r, rnrn / rTr, pk)
+            rTr = torch.where(done, rTr, rnrn)
         self._cg_x = xk
         return eA
 
