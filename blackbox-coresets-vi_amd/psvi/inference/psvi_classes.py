@@ -988,8 +988,12 @@ class PSVI:
             draw_inner()
             return torch.sub(x, hv32(draw_inner(), x), alpha=lr)  # fp32 H x promoted in the one pass
 
+        # lr as a one-element float64 tensor: lr * (fp32 H x) promotes to
+        # float64 in one pass (a 0-dim operand would not promote)
+        lr_t = torch.full((1,), lr, dtype=torch.float64, device=g_w.device)
+
         def A(x):                               # dfp_map_dw
-            vmj = hv32(eA, x).to(torch.float64).mul_(lr)
+            vmj = torch.mul(hv32(eA, x), lr_t)
             return vmj - jvp(vmj)
 
         b = g_w - jvp(g_w)
