@@ -977,14 +977,14 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(float* __restrict__ G, fl
 }
 
 // Hv assembly.  The sums over the S samples run in parallel: a workgroup
-// takes 64 consecutive elements (one per lane) and its four waves a quarter
-// of the samples each, in order; the four partials are added in wave order
+// takes 64 consecutive elements (one per lane) and its sixteen waves a
+// sixteenth of the samples each, in order; the partials are added in wave order
 // (run-to-run bitwise reproducible).  Per parameter element e of layer l:
 //   ge = sum_s G_s eps_s,  gd = sum_s G_dot_s,  gde = sum_s G_dot_s eps_s,
 // then the softplus curvature ge sigmoid'(sd) v_sd and the KL Hessian (the
 // corr block of full-cov is added by the update kernel's gradient mode, which
 // also wrote sum G_dot, diag(G_dot^T E) sigmoid(sd) for full-cov).
-constexpr int kAsmWaves = 4;
+constexpr int kAsmWaves = 16;  // 1024 threads: a C3 grid is 68 workgroups, so depth per CU matters
 __device__ __forceinline__ void sample_quarter(int S, int wv, int& s0, int& s1) {
     const int q = (S + kAsmWaves - 1) / kAsmWaves;
     s0 = min(S, wv * q);
@@ -992,7 +992,7 @@ __device__ __forceinline__ void sample_quarter(int S, int wv, int& s0, int& s1) 
 }
 
 template <bool SLOTS, bool FC>
-__global__ __launch_bounds__(256) void hvp_param_kernel(RopArgs a, float* hv, float inv_s0sq,
+__global__ __launch_bounds__(1024) void hvp_param_kernel(RopArgs a, float* hv, float inv_s0sq,
                                                         float klw, int64_t slot2) {
     // SLOTS: G / G_dot still in the R-op's two row-block slots (slot 1 at
     // + slot2), added here as slot_sum_kernel would: slot 0 + slot 1.  FC:
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(256) void hvp_param_kernel(RopArgs a, float* hv, fl
 
 // dst[j] = sum_s src[s * stride + j], j < n: lanes over j, waves over sample
 // quarters, partials in wave order (d_u = sum_s du_dot_s, d_w = sum_s NLL_dot_s)
-__global__ __launch_bounds__(256) void sample_sum_kernel(const float* __restrict__ src,
+__global__ __launch_bounds__(1024) void sample_sum_kernel(const float* __restrict__ src,
                                                          int64_t stride, int S, int64_t n,
                                                          float* __restrict__ dst) {
     __shared__ float part[kAsmWaves][64];
@@ -1303,7 +1303,7 @@ hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const fl
     a.G = const_cast<float*>(G);
     a.Gd = const_cast<float*>(Gd);
     const float s0 = p.d.prior_sd;
-    const dim3 pg((unsigned)((p.n_tot + 63) / 64)), pb(256);
+    const dim3 pg((unsigned)((p.n_tot + 63) / 64)), pb(64 * kAsmWaves);
     const float is2 = 1.f / (s0 * s0), klw = include_kl ? 1.f : 0.f;
     const bool fc = p.family == PSVI_FAMILY_FULLCOV;
     if (slot2 && fc) hipLaunchKernelGGL((hvp_param_kernel<true, true>), pg, pb, 0, st, a, hv, is2, klw, slot2);
@@ -1313,11 +1313,11 @@ hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const fl
     const int S = p.d.S, M = p.d.M, D = p.lay[0].din;
     if (d_u) {
         const int64_t n = (int64_t)M * D;
-        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, du,
+        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kAsmWaves), 0, st, du,
                            n, S, n, d_u);
     }
     if (d_w)
-        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((M + 63) / 64)), dim3(256), 0, st,
+        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((M + 63) / 64)), dim3(64 * kAsmWaves), 0, st,
                            nlld, (int64_t)M, S, (int64_t)M, d_w);
     return hipGetLastError();
 }
