@@ -992,8 +992,8 @@ __device__ __forceinline__ void sample_quarter(int S, int wv, int& s0, int& s1) 
 }
 
 template <bool SLOTS, bool FC>
-__global__ __launch_bounds__(1024) void hvp_param_kernel(RopArgs a, float* hv, float inv_s0sq,
-                                                        float klw, int64_t slot2) {
+__device__ __forceinline__ void hvp_param_body(const RopArgs& a, float* hv, float inv_s0sq, float klw,
+                                               int64_t slot2, int bx) {
     // SLOTS: G / G_dot still in the R-op's two row-block slots (slot 1 at
     // + slot2), added here as slot_sum_kernel would: slot 0 + slot 1.  FC:
     // full-cov needs sum_s G eps alone (the update kernel's gradient mode did G_dot)
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(1024) void hvp_param_kernel(RopArgs a, float* hv, f
     };
     __shared__ float part[kAsmWaves][3][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;
+    const int e = bx * 64 + lane;
     const bool live = e < a.n_tot;
     const int ec = live ? e : a.n_tot - 1;
     int l = 0;
@@ -1077,12 +1077,11 @@ __global__ __launch_bounds__(1024) void hvp_param_kernel(RopArgs a, float* hv, f
 
 // dst[j] = sum_s src[s * stride + j], j < n: lanes over j, waves over sample
 // quarters, partials in wave order (d_u = sum_s du_dot_s, d_w = sum_s NLL_dot_s)
-__global__ __launch_bounds__(1024) void sample_sum_kernel(const float* __restrict__ src,
-                                                         int64_t stride, int S, int64_t n,
-                                                         float* __restrict__ dst) {
+__device__ __forceinline__ void sample_sum_body(const float* __restrict__ src, int64_t stride, int S,
+                                                int64_t n, float* __restrict__ dst, int bx) {
     __shared__ float part[kAsmWaves][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t j = (int64_t)blockIdx.x * 64 + lane, jc = j < n ? j : n - 1;
+    const int64_t j = (int64_t)bx * 64 + lane, jc = j < n ? j : n - 1;
     int s0, s1;
     sample_quarter(S, wv, s0, s1);
     float t = 0.f;
@@ -1102,6 +1101,23 @@ __global__ __launch_bounds__(1024) void sample_sum_kernel(const float* __restric
 #pragma unroll
     for (int w = 0; w < kAsmWaves; ++w) t += part[w][lane];
     dst[j] = t;
+}
+
+// The assembly and both mixed-product sums in one launch: workgroups
+// [0, nbp) the parameter elements, then nbu of d_u, then the d_w ones (a
+// workgroup-uniform branch; three launches before)
+template <bool SLOTS, bool FC>
+__global__ __launch_bounds__(1024) void hvp_assemble_kernel(RopArgs a, float* hv, float inv_s0sq, float klw,
+                                                           int64_t slot2, int nbp, const float* du,
+                                                           int64_t ndu, float* d_u, int nbu,
+                                                           const float* nlld, float* d_w) {
+    const int b = blockIdx.x;
+    if (b < nbp)
+        hvp_param_body<SLOTS, FC>(a, hv, inv_s0sq, klw, slot2, b);
+    else if (b < nbp + nbu)
+        sample_sum_body(du, ndu, a.S, ndu, d_u, b - nbp);
+    else
+        sample_sum_body(nlld, a.M, a.S, a.M, d_w, b - nbp - nbu);
 }
 
 static int rup4(int x) { return (x + 3) & ~3; }
@@ -1303,22 +1319,20 @@ hipError_t launch_hvp_assemble(const psvi_plan& p, const float* params, const fl
     a.G = const_cast<float*>(G);
     a.Gd = const_cast<float*>(Gd);
     const float s0 = p.d.prior_sd;
-    const dim3 pg((unsigned)((p.n_tot + 63) / 64)), pb(64 * kAsmWaves);
+    const int nbp = (int)((p.n_tot + 63) / 64), M = p.d.M, D = p.lay[0].din;
+    const int64_t ndu = (int64_t)M * D;
+    const int nbu = d_u ? (int)((ndu + 63) / 64) : 0, nbw = d_w ? (M + 63) / 64 : 0;
+    const dim3 pg((unsigned)(nbp + nbu + nbw)), pb(64 * kAsmWaves);
     const float is2 = 1.f / (s0 * s0), klw = include_kl ? 1.f : 0.f;
     const bool fc = p.family == PSVI_FAMILY_FULLCOV;
-    if (slot2 && fc) hipLaunchKernelGGL((hvp_param_kernel<true, true>), pg, pb, 0, st, a, hv, is2, klw, slot2);
-    else if (slot2) hipLaunchKernelGGL((hvp_param_kernel<true, false>), pg, pb, 0, st, a, hv, is2, klw, slot2);
-    else if (fc) hipLaunchKernelGGL((hvp_param_kernel<false, true>), pg, pb, 0, st, a, hv, is2, klw, slot2);
-    else hipLaunchKernelGGL((hvp_param_kernel<false, false>), pg, pb, 0, st, a, hv, is2, klw, slot2);
-    const int S = p.d.S, M = p.d.M, D = p.lay[0].din;
-    if (d_u) {
-        const int64_t n = (int64_t)M * D;
-        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kAsmWaves), 0, st, du,
-                           n, S, n, d_u);
-    }
-    if (d_w)
-        hipLaunchKernelGGL(sample_sum_kernel, dim3((unsigned)((M + 63) / 64)), dim3(64 * kAsmWaves), 0, st,
-                           nlld, (int64_t)M, S, (int64_t)M, d_w);
+    if (slot2 && fc)
+        hipLaunchKernelGGL((hvp_assemble_kernel<true, true>), pg, pb, 0, st, a, hv, is2, klw, slot2, nbp, du, ndu, d_u, nbu, nlld, d_w);
+    else if (slot2)
+        hipLaunchKernelGGL((hvp_assemble_kernel<true, false>), pg, pb, 0, st, a, hv, is2, klw, slot2, nbp, du, ndu, d_u, nbu, nlld, d_w);
+    else if (fc)
+        hipLaunchKernelGGL((hvp_assemble_kernel<false, true>), pg, pb, 0, st, a, hv, is2, klw, slot2, nbp, du, ndu, d_u, nbu, nlld, d_w);
+    else
+        hipLaunchKernelGGL((hvp_assemble_kernel<false, false>), pg, pb, 0, st, a, hv, is2, klw, slot2, nbp, du, ndu, d_u, nbu, nlld, d_w);
     return hipGetLastError();
 }
 
