@@ -26,6 +26,10 @@ def main():
     from psvi.runtime import InnerLoopPlan, randn_
 
     fam, layers, S, M = CFG[a.cfg]
+    from psvi.runtime import _lib
+    for kv in a.dbg:  # before the plan: some keys shape its tables
+        k, v = kv.split("=")
+        _lib.load().psvi_debug_set(int(k), int(v))
     plan = InnerLoopPlan(fam, layers, S, M)
     g = torch.Generator().manual_seed(0)
     dev = "cuda"
@@ -37,9 +41,6 @@ def main():
     eps = torch.empty(plan.eps_count, device=dev)
     randn_(eps, 3)
     ws = plan.workspace()
-    for kv in a.dbg:
-        k, v = kv.split("=")
-        plan.lib.psvi_debug_set(int(k), int(v))
     for mixed in (False, True):
         for _ in range(3):
             plan.hvp(u, z, w, eps, p, vec, mixed=mixed)
