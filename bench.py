@@ -323,27 +323,28 @@ def sharded_steps(rt, loop, u, z, w, params, m, v, seed, k0, n, parts=None, ev=N
              elbo_parts=None if parts is None else parts[k0:k0 + n], phase_events=ev)
 
 
-def sharded_headline(rt, steps, warmup, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M, ev_every=5):
-    """The headline at N > 1: C3 shards weak-scaled (S = 128 N, M = 100), rows
-    of L (whole 64-row bands) x samples sharded, two all_to_alls per step.
-    Returns (elapsed s, the (warmup + steps) x 2 [NLL, KL] parts of this rank,
-    per-phase ms from a separate 50-step call after the timed one, loop)."""
-    S = s_per_gpu * rt.world
+def sharded_timed(rt, steps, warmup, layers, S, M, ev_every=5, seed=20251015):
+    """K timed sharded inner steps of fn2 at (S, M) after W warm-up steps
+    (ShardedInnerLoop.run: rows of L (whole 64-row bands) x samples sharded,
+    two all_to_alls per step), the timed call continuing the warm-up's Philox
+    stream and Adam steps.  Returns (elapsed s, the (warmup + steps) x 2 [NLL,
+    KL] parts of this rank, per-phase ms from a separate 50-step call after the
+    timed one, loop)."""
     loop = make_sharded_loop("fullcov", layers, S, M, rt)
     u, z, w = fn2_inputs(layers, M, rt.dev, 0)
     params = reference_init_params(layers, rt.dev)
     m, v = torch.zeros_like(params), torch.zeros_like(params)
     total = warmup + steps
     parts = torch.zeros(total, 2, dtype=torch.float64, device=rt.dev)
-    sharded_steps(rt, loop, u, z, w, params, m, v, 20251015, 0, warmup, parts)
-    elapsed = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, params, m, v, 20251015,
+    sharded_steps(rt, loop, u, z, w, params, m, v, seed, 0, warmup, parts)
+    elapsed = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, params, m, v, seed,
                                              warmup, steps, parts))
     # the per-phase split: HIP events between the launches of a separate call
     # (outside the timed region), every ev_every-th of 50 steps
     nph = 50
     ev = {k: [rt.event() for _ in range(4)] for k in range(nph) if k % ev_every == 0}
     pp, mm, vv = params.clone(), m.clone(), v.clone()
-    loop.run(u, z, w, pp, mm, vv, nph, LR, step0=total + 1, seed=20251016, phase_events=ev)
+    loop.run(u, z, w, pp, mm, vv, nph, LR, step0=total + 1, seed=seed + 1, phase_events=ev)
     rt.sync()
     ph = {"exchange+net": [], "update+sample": []}
     for e in ev.values():
@@ -354,48 +355,84 @@ def sharded_headline(rt, steps, warmup, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M,
     return elapsed, parts, avg_ms, loop
 
 
+def weak_line(rt, steps, warmup, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M):
+    """Side line at N > 1: C3 shards weak-scaled (S = 128 N, M = 100), the same
+    sharded step.  inner-steps/s of the whole job (one step = all S samples;
+    not multiplied by N)."""
+    S = s_per_gpu * rt.world
+    elapsed, parts, _, loop = sharded_timed(rt, steps, warmup, layers, S, M)
+    negelbo = loop.reduce_elbo(parts)
+    return {"config": f"C3 shards x {rt.world}: fn2 full-cov S={S} ({s_per_gpu} per GPU), "
+                      f"M={M} (weak scaling)",
+            "inner_steps_per_s": round(steps / elapsed, 2),
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "elbo_finite": bool(torch.isfinite(negelbo).all().item())}
+
+
+def c4_single_gpu(rt, steps=100, warmup=10, layers=LAYERS, S=None, M=None):
+    """At N > 1, on rank 0 alone (the other ranks wait at the next barrier):
+    C4 on ONE GPU of the same node in the same run (psvi_inner_loop, the
+    c4_1gpu line of an N = 1 run), the denominator of the strong-scaling
+    speed-up the N > 1 headline reports."""
+    from psvi.runtime import InnerLoopPlan
+
+    S, M = S or C4["S"], M or C4["M"]
+    dev = rt.dev
+    u, z, w = fn2_inputs(layers, M, dev, 5)
+    params = reference_init_params(layers, dev)
+    m, v = torch.zeros_like(params), torch.zeros_like(params)
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+    plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=11, ws=ws)
+    rt.sync()
+    t0 = time.perf_counter()
+    plan.inner_loop(u, z, w, params, m, v, steps, LR, seed=12, ws=ws)
+    rt.sync()
+    dt = time.perf_counter() - t0
+    return {"config": f"C4 fn2 full-cov S={S} M={M} on 1 GPU (rank 0's device, same run)",
+            "inner_steps_per_s": round(steps / dt, 2), "ms_per_step": round(dt / steps * 1e3, 4)}
+
+
+def step_flops(layers, S, M):
+    """SURVEY.md section 8(d)'s algorithmic flops of one full-cov inner step:
+    the two triangular GEMMs (x = L eps and dL = G^T eps, each sum n(n+1) S)
+    and the network (forward, weight gradients, propagation below the head's
+    input except into the first layer's input)."""
+    n = [i * o + o for i, o in layers]
+    io = [i * o for i, o in layers]
+    return 2.0 * S * sum(k * (k + 1) for k in n) + 2.0 * S * M * (2 * sum(io) + sum(io[1:]))
+
+
 def c4_timings(rt, steps=100, warmup=10, layers=LAYERS, S=C4["S"], M=C4["M"]):
-    """Auxiliary line for BASELINE.json configs[3] (C4): fn2 64-40-40-2 full-cov,
-    S = 1024, M = 200 -- the same total work at every N (strong scaling):
-    N = 1 runs psvi_inner_loop; N > 1 the rows-of-L x samples sharded step
-    (ShardedInnerLoop, two all_to_alls per step).  inner-steps/s of the whole
-    job; BASELINE's ">= 6x at 8 GPUs over 1" is this line at N = 8 over N = 1."""
+    """Auxiliary line of an N = 1 run for BASELINE.json configs[3] (C4): fn2
+    64-40-40-2 full-cov, S = 1024, M = 200 on one GPU (psvi_inner_loop) -- the
+    denominator of the N > 1 headline, which is C4 itself (strong scaling)."""
     from psvi.runtime import InnerLoopPlan
 
     dev = rt.dev
     u, z, w = fn2_inputs(layers, M, dev, 5)
     params = reference_init_params(layers, dev)
     m, v = torch.zeros_like(params), torch.zeros_like(params)
-    if rt.world == 1:
-        plan = InnerLoopPlan("fullcov", layers, S, M)
-        ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
-        elbo = torch.empty(steps, dtype=torch.float64, device=dev)
-        plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=11, ws=ws)
-        dt = rt.timed(lambda: plan.inner_loop(u, z, w, params, m, v, steps, LR, seed=12, ws=ws,
-                                              elbo_out=elbo))
-        negelbo = elbo[-1:]
-    else:
-        loop = make_sharded_loop("fullcov", layers, S, M, rt)
-        parts = torch.zeros(warmup + steps, 2, dtype=torch.float64, device=dev)
-        sharded_steps(rt, loop, u, z, w, params, m, v, 11, 0, warmup, parts)
-        dt = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, params, m, v, 11, warmup,
-                                            steps, parts))
-        negelbo = loop.reduce_elbo(parts[-1:])
-    return {"config": f"C4 fn2 full-cov S={S} M={M}, {rt.world} GPU(s) (strong scaling)",
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    ws = torch.empty(plan.loop_ws_bytes, dtype=torch.uint8, device=dev)
+    elbo = torch.empty(steps, dtype=torch.float64, device=dev)
+    plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=11, ws=ws)
+    dt = rt.timed(lambda: plan.inner_loop(u, z, w, params, m, v, steps, LR, seed=12, ws=ws,
+                                          elbo_out=elbo))
+    return {"config": f"C4 fn2 full-cov S={S} M={M}, 1 GPU",
             "inner_steps_per_s": round(steps / dt, 2), "ms_per_step": round(dt / steps * 1e3, 4),
-            "elbo_finite": bool(torch.isfinite(negelbo).all().item())}
+            "elbo_finite": bool(torch.isfinite(elbo[-1:]).all().item())}
 
 
-def dp_timings(rt, steps=20, warmup=3, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M):
+def dp_timings(rt, steps=20, warmup=3, layers=LAYERS, S=C4["S"], M=C4["M"]):
     """The data-parallel alternative to the headline's row-sharded step
     (N > 1 only; SURVEY.md §8(e) frames the choice): every rank holds all of
     L, runs its S/N samples' inner objective and gradient on a world-1 plan
     (psvi_elbo_grad), ONE all-reduce of the 4.73 M-float gradient (18.9 MB)
     and the ELBO, then the same Adam step on every replica
-    (SampleShardedPlan.inner_loop).  Same weak-scaled shape as the headline."""
+    (SampleShardedPlan.inner_loop).  Same workload as the headline (C4)."""
     from psvi.runtime.sharded import SampleShardedPlan
 
-    S = s_per_gpu * rt.world
     plan = SampleShardedPlan("fullcov", layers, S, M, rt.world, rt.rank, rt.comm)
     u, z, w = fn2_inputs(layers, M, rt.dev, 0)
     params = reference_init_params(layers, rt.dev)
@@ -404,10 +441,9 @@ def dp_timings(rt, steps=20, warmup=3, layers=LAYERS, s_per_gpu=S_PER_GPU, M=M):
     plan.inner_loop(u, z, w, params, m, v, warmup, LR, seed=3, ws=ws)
     dt = rt.timed(lambda: plan.inner_loop(u, z, w, params, m, v, steps, LR, step0=warmup + 1,
                                           seed=3, offset=warmup * plan.eps_stride, ws=ws))
-    return {"config": f"C3 shards x {rt.world} (S={S}, M={M}): data parallel, one all-reduce "
+    return {"config": f"C4 fn2 S={S} M={M} over {rt.world} GPUs: data parallel, one all-reduce "
                       f"of the {plan.param_count}-float gradient per step",
-            "inner_steps_per_s": round(steps / dt, 2), "value": round(steps / dt * rt.world, 2),
-            "ms_per_step": round(dt / steps * 1e3, 4)}
+            "inner_steps_per_s": round(steps / dt, 2), "ms_per_step": round(dt / steps * 1e3, 4)}
 
 
 def lenet_timings(rt, cpu=True, T=10, S=256, M=500, second_order=True):
@@ -620,6 +656,17 @@ def headline_world1(rt, args, prep=None):
                                                step0=args.warmup + 1, seed=20251015,
                                                offset=args.warmup * eps_stride,
                                                elbo_out=elbo_t, ws=ws))
+    # the same K steps as a cold call (fresh Adam state and packed arrays: the
+    # packed -> tiled conversion, the first draw and sample inside), as every
+    # hyper_step / nested_step inner loop runs: the per-call fixed cost the
+    # resumed headline leaves out
+    pc, mc_, vc = p_init.clone(), torch.zeros_like(m), torch.zeros_like(v)
+    cold_s = rt.timed(lambda: plan.inner_loop(u, z, w, pc, mc_, vc, args.steps, LR,
+                                              seed=20251017, ws=ws))
+    cold = {"inner_steps_per_s": round(args.steps / cold_s, 2),
+            "ms_per_step": round(cold_s / args.steps * 1e3, 5),
+            "fixed_cost_us_per_call": round((cold_s - elapsed) * 1e6, 1)}
+    del pc, mc_, vc
     # the per-phase split from a separate call (its HIP event records on the
     # stream would otherwise sit inside the timed region): 100 steps, events
     # around the network and the update of every 10th -- 10 samples whatever
@@ -634,7 +681,7 @@ def headline_world1(rt, args, prep=None):
         raise RuntimeError("psvi_debug_loop_timing failed")
     lib.psvi_debug_set(8, 0)
     avg_ms = {"exchange+net": tm[0] * 1e-3, "update": tm[1] * 1e-3, "samples": int(tm[2])}
-    return elapsed, elbo_t, avg_ms, plan.param_count
+    return elapsed, elbo_t, avg_ms, plan.param_count, cold
 
 
 def rows_fraction(loop, layers):
@@ -651,31 +698,41 @@ def run(rt, args, shapes=None):
     """Everything after the process set-up; returns the JSON line's dict on
     rank 0 (None on the other ranks).  shapes: smaller stand-ins for the
     configs (CPU rehearsals of the N > 1 control flow under gloo,
-    tests/test_bench_gloo.py); None = the BASELINE configs."""
+    tests/test_bench_gloo.py); None = the BASELINE configs.
+
+    N = 1: the headline is C3 (BASELINE configs[2]: fn2 S = 128, M = 100 on one
+    GPU), with C4 on one GPU as the side line `c4_1gpu`.  N > 1: the headline
+    is C4 (configs[3]: S = 1024, M = 200 over the N GPUs, strong scaling; one
+    step is one step of all 1024 samples), with C4 on one GPU of the same run
+    as `c4_1gpu` and the speed-up over it, and the weak-scaled C3 shards as
+    the side line `weak`."""
     sh = dict(layers=LAYERS, s_per_gpu=S_PER_GPU, M=M, c4={}, c5={})
     sh.update(shapes or {})
     world, rank = rt.world, rt.rank
-    S = sh["s_per_gpu"] * world
-    # the C4 line first: the headline's one short timed call (K = 20 steps,
-    # ~1.7 ms, in the driver's run) then starts on a GPU at its working clocks
-    # rather than straight after process start-up
+    c4sh = dict(layers=LAYERS, S=C4["S"], M=C4["M"])
+    c4sh.update({k: sh["c4"][k] for k in ("layers", "S", "M") if k in sh["c4"]})
+    # N = 1: the C4 line first, so that the headline's one short timed call
+    # (K = 20 steps, ~1.4 ms, in the driver's run) starts on a GPU at its
+    # working clocks rather than straight after process start-up
     c4 = None
-    prep = headline_prep(rt, args) if world == 1 and shapes is None else None
-    if not args.no_c4:
-        log("C4 line")
-        c4 = c4_timings(rt, **sh["c4"])
     if world == 1:
-        elapsed, parts, avg_ms, pcount = headline_world1(rt, args, prep)
+        prep = headline_prep(rt, args) if shapes is None else None
+        if not args.no_c4:
+            log("C4 line")
+            c4 = c4_timings(rt, **sh["c4"])
+        elapsed, parts, avg_ms, pcount, cold = headline_world1(rt, args, prep)
         elbo = parts
+        S, Mh, layers = sh["s_per_gpu"], sh["M"], sh["layers"]
     else:
-        elapsed, parts, avg_ms, loop = sharded_headline(rt, args.steps, args.warmup,
-                                                        layers=sh["layers"],
-                                                        s_per_gpu=sh["s_per_gpu"], M=sh["M"])
+        S, Mh, layers = c4sh["S"], c4sh["M"], c4sh["layers"]
+        log(f"C4 headline over {world} ranks")
+        elapsed, parts, avg_ms, loop = sharded_timed(rt, args.steps, args.warmup, layers, S, Mh)
         elbo = loop.reduce_elbo(parts)
         pcount = loop.plan.param_count
+        cold = None
     finite = bool(torch.isfinite(elbo).all().item())
     steps_per_s = args.steps / elapsed
-    value = steps_per_s * world   # S = 128 N: N C3 shards per step
+    value = steps_per_s  # one step = one inner step of ALL S samples, on every N
     if world == 1:
         upd_s = max(avg_ms["update"], 1e-9) * 1e-3
         # dominant kernel: the update with the fused next-step sample (plus its
@@ -690,7 +747,7 @@ def run(rt, args, shapes=None):
         # dominant phase: the update (K-split streaming kernel at K = S) and
         # the next step's sample on this rank's rows (the segmented sample
         # kernel + its (row block, pass) reduce)
-        work = algorithmic_work(S, rows_fraction(loop, sh["layers"]), sh["layers"])
+        work = algorithmic_work(S, rows_fraction(loop, layers), layers)
         wk = dict(bytes=work["update"]["bytes"] + work["sample"]["bytes"],
                   flops=work["update"]["flops"] + work["sample"]["flops"])
         upd_s = max(avg_ms["update+sample"], 1e-9) * 1e-3
@@ -726,18 +783,30 @@ def run(rt, args, shapes=None):
                                              / BF16_MFMA_PEAK_TFLOPS, 4)) if world == 1 else None,
                     kernels={k: {kk: round(vv, 2) for kk, vv in d.items()}
                              for k, d in kernels.items()})
-    # the whole inner step's algorithmic work at C3 (2.682 GFLOP,
-    # 134.7 MB per S = 128 shard) against the fp32 MFMA peak -- the step's roofline
-    # fraction, beside the dominant kernel's own above
-    step_floor_us = 2.682e9 / (FP32_MFMA_PEAK_TFLOPS * 1e12) * 1e6
-    step_roofline = dict(bound="mfma (ridge: HBM 16.8 us / MFMA 17.05 us per C3 shard)",
-                         algorithmic_gflop_per_gpu=2.682, floor_us=round(step_floor_us, 2),
+    # the whole inner step's algorithmic work (C3: 2.682
+    # GFLOP per step; C4: 23.54 GFLOP, split over the N GPUs) against the fp32
+    # MFMA peak of the N GPUs -- the step's roofline fraction, beside the
+    # dominant kernel's own above
+    gflop = step_flops(layers, S, Mh) / 1e9
+    step_floor_us = gflop * 1e9 / (FP32_MFMA_PEAK_TFLOPS * 1e12 * world) * 1e6
+    step_roofline = dict(bound="mfma (fp32)", algorithmic_gflop_per_step=round(gflop, 3),
+                         gpus=world, floor_us=round(step_floor_us, 2),
                          frac=round(step_floor_us / (elapsed / args.steps * 1e6), 4))
     log(f"headline: {steps_per_s:.1f} steps/s")
+    weak = one = None
+    if world > 1:
+        log("weak-scaled C3 shards")
+        weak = weak_line(rt, args.steps, args.warmup, layers=sh["layers"],
+                         s_per_gpu=sh["s_per_gpu"], M=sh["M"])
+        if rank == 0 and not args.no_c4:
+            log("C4 on one GPU (rank 0)")
+            one = c4_single_gpu(rt, **c4sh)
+            one["speedup_of_headline"] = round(value / one["inner_steps_per_s"], 3)
+        rt.barrier()
     dp = None
     if world > 1 and not args.no_dp:
         log("data-parallel alternative")
-        dp = dp_timings(rt, **sh.get("dp", {}))
+        dp = dp_timings(rt, **dict(c4sh, **sh.get("dp", {})))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline")
@@ -758,31 +827,42 @@ def run(rt, args, shapes=None):
     rt.barrier()
     if rank != 0:
         return None
+    if world == 1:
+        workload = "C3 fn2 full-cov MLP 64-40-40-2, S=128, M=100, one GPU (BASELINE configs[2])"
+        unit = "inner-steps/s (one step: all S=128 samples x M=100 pseudopoints)"
+        par = "one GPU"
+    else:
+        workload = (f"C4 fn2 full-cov MLP 64-40-40-2, S={S}, M={Mh}, over {world} GPUs "
+                    f"(BASELINE configs[3], strong scaling)")
+        unit = f"inner-steps/s (one step: all S={S} samples x M={Mh} pseudopoints)"
+        par = f"rows-of-L x samples sharded over {world}"
     return {
         "metric": "ELBO inner-steps/sec (S MC samples x M pseudopoints) at 1/2/4/8 GPU",
         "value": round(value, 2),
-        "unit": "inner-steps/s (S=128 x M=100 fn2 C3 shards; S = 128 x n_gpus)",
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if world == 1 else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (make_synthetic-shaped X~N(0,I64), Bernoulli labels; reference init)",
-        "config": {"workload": "C3 fn2 full-cov MLP 64-40-40-2 per GPU (C4 sample count at 8 GPUs)",
-                   "S_total": S, "S_per_gpu": sh["s_per_gpu"], "M": sh["M"], "D": 64, "H": 40,
-                   "C": 2, "params": pcount,
-                   "parallelism": f"rows-of-L x samples sharded over {world}",
+        "config": {"workload": workload, "S_total": S, "M": Mh, "D": 64, "H": 40,
+                   "C": 2, "params": pcount, "parallelism": par,
                    "comm": getattr(rt.comm, "name", None) if world > 1 else None,
                    "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite,
                    "timed_call": ("continues the warm-up call (resident loop state)"
-                                  if world == 1 and args.warmup else "cold call")},
+                                  if world == 1 and args.warmup else "continues the warm-up's "
+                                  "Philox stream and Adam steps")},
+        "cold_call": cold,
+        "speedup_over_1gpu": None if world == 1 or one is None else one["speedup_of_headline"],
         "roofline": roofline,
         "step_roofline": step_roofline,
         "cpu_baseline": cpu,
-        ("c4_1gpu" if world == 1 else "c4"): c4,
+        "c4_1gpu": c4 if world == 1 else one,
+        "weak": weak,
         "dp_alternative": dp,
         "c2": c2,
         "trainers": trainers,

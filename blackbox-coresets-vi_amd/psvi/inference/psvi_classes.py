@@ -961,7 +961,11 @@ class PSVI:
                     break
             xk, eA = vs, draw_inner()
         else:
-            eA = self._cg_normaleq(hvp, draw_inner, g_w, lr, K)
+            # replayed draws: the reference's exact number of fp_map draws (the
+            # host reads the stopping flag every iteration); the Philox stream:
+            # every 5th iteration (up to 4 discarded iterations after convergence)
+            eA = self._cg_normaleq(hvp, draw_inner, g_w, lr, K,
+                                   sync_every=1 if it_in is not None else 5)
             xk = self._cg_x
         _, du, dw = hvp(eA, xk, mixed=True)     # torch_grad(w_mapped, hparams, vs)
         # 3. hypergradient = -lr * mixed products + the outer objective's direct gradients
@@ -976,9 +980,13 @@ class PSVI:
             nn.utils.vector_to_parameters(params.to(plist[0].dtype), plist)
         return float(ll.item())
 
-    def _cg_normaleq(self, hvp, draw_inner, g_w, lr, K):
+    def _cg_normaleq(self, hvp, draw_inner, g_w, lr, K, sync_every=1):
         """CG_normaleq's linear solve (hypergradients.py:199-244, CG_torch.py:9-45);
-        returns the draw of w_mapped, leaves the solution in self._cg_x."""
+        returns the draw of w_mapped, leaves the solution in self._cg_x.
+        The stopping test runs on the device (psvi.hypergrad.CG_torch.cg):
+        x, r, p freeze where the reference breaks, and the host leaves the
+        loop when it reads the flag, every ``sync_every`` iterations (1: the
+        reference's number of A calls, hence of draws)."""
         eA = draw_inner()                       # w_mapped = fp_map(params, hparams)
 
         def hv32(e, x):                         # H x (fp32, as psvi_hvp returns it)
@@ -998,16 +1006,16 @@ class PSVI:
 
         b = g_w - jvp(g_w)
         # CG_torch.cg(Ax, b, max_iter=K, epsilon=1e-10) with fused x + a y passes
-        # and 0-dim device step lengths; the stopping test stays on the device:
-        # where the reference breaks, the step length is zeroed (x and r keep
-        # their values), so no iteration waits on a host read of the norm
+        # and 0-dim device step lengths; where the reference breaks, the step
+        # length is zeroed and r, p, rTr keep their values
         xk = torch.zeros_like(b)
         r = b.clone()
         pk = r.clone()
         rTr = torch.dot(r, r)
         done = torch.zeros((), dtype=torch.bool, device=b.device)
         zero = torch.zeros((), dtype=b.dtype, device=b.device)
-        for _ in range(int(K)):
+        sync_every = max(1, int(sync_every))
+        for it in range(int(K)):
             Ap = A(pk)
             alpha = rTr / torch.dot(pk, Ap)
             rn = torch.addcmul(r, alpha, Ap, value=-1)
@@ -1015,8 +1023,10 @@ class PSVI:
             done = done | (torch.sqrt(rnrn) < 1e-10)
             xk = torch.addcmul(xk, torch.where(done, zero, alpha), pk)
             r = torch.where(done, r, rn)
-            pk = torch.addcmul(r, rnrn / rTr, pk)
+            pk = torch.where(done, pk, torch.addcmul(r, rnrn / rTr, pk))
             rTr = torch.where(done, rTr, rnrn)
+            if (it + 1) % sync_every == 0 and bool(done):
+                break
         self._cg_x = xk
         return eA
 

@@ -38,7 +38,10 @@ def _need(t, name, numel, dtype=torch.float32):
 def _wrote(*tensors):
     """Bump the version counters of tensors the library wrote in place (no
     torch op saw the write), so that a resident inner-loop state keyed to
-    them is not taken up after it (InnerLoopPlan.inner_loop(keep=True))."""
+    them is not taken up after it (InnerLoopPlan.inner_loop(keep=True)).
+    Every method that hands a workspace to the library marks it written (the
+    library also drops its resident state in every entry point but the loop's
+    own)."""
     for t in tensors:
         if t is not None:
             increment_version(t)
@@ -179,7 +182,7 @@ class InnerLoopPlan:
                                        _ptr(params), _ptr(adam_m), _ptr(adam_v),
                                        ctypes.byref(hp), _ptr(elbo_out), _ptr(ws),
                                        ws.numel(), _stream()), "psvi_inner_step")
-        _wrote(params, adam_m, adam_v)
+        _wrote(params, adam_m, adam_v, ws)
         return elbo_out
 
     def inner_loop(self, u, z, w, params, adam_m, adam_v, T, lr, kind="higher", step0=1,
@@ -255,6 +258,7 @@ class InnerLoopPlan:
                                       _ptr(params), int(bool(include_kl)), _ptr(elbo),
                                       _ptr(grad), _ptr(ws), ws.numel(), _stream()),
               "psvi_elbo_grad")
+        _wrote(ws)
         return elbo, grad
 
     def outer_elbo_grad(self, n_pseudo, x_all, z_all, w_all, eps, params, grad=True,
@@ -288,6 +292,7 @@ class InnerLoopPlan:
             _ptr(params), _ptr(out["loss"]), _ptr(out.get("grad")), _ptr(out.get("grad_u")),
             _ptr(out.get("grad_w")), _ptr(out.get("samples")), _ptr(ws), ws.numel(),
             _stream()), "psvi_outer_elbo_grad")
+        _wrote(ws)
         return out
 
     def outer_ablated_elbo_grad(self, x_all, z_all, w_all, eps, params, grad=True,
@@ -313,6 +318,7 @@ class InnerLoopPlan:
             self.handle, _ptr(x_all), _ptr(z_all), _ptr(w_all), _ptr(eps), _ptr(params),
             _ptr(out["loss"]), _ptr(out.get("grad")), _ptr(out.get("samples")), _ptr(ws),
             ws.numel(), _stream()), "psvi_outer_ablated_elbo_grad")
+        _wrote(ws)
         return out
 
     def outer_grad_coef(self, n_pseudo, x_all, z_all, w_all, eps, params, coef, grad_u=True,
@@ -343,6 +349,7 @@ class InnerLoopPlan:
             _ptr(params), _ptr(coef), _ptr(out["grad"]), _ptr(out.get("grad_u")),
             _ptr(out.get("grad_w")), _ptr(ws), ws.numel(), _stream()),
             "psvi_outer_elbo_grad_coef")
+        _wrote(ws)
         return out
 
     def evaluate(self, n_pseudo, x_all, z_all, w_all, eps, params, correction=True, probs=False,
@@ -366,6 +373,7 @@ class InnerLoopPlan:
                                      _ptr(w_all), _ptr(eps), _ptr(params), int(bool(correction)),
                                      _ptr(pr), _ptr(stats), _ptr(ws), ws.numel(), _stream()),
               "psvi_evaluate")
+        _wrote(ws)
         return stats, pr
 
     def hvp(self, u, z, w, eps, params, vec, mixed=True, out=None, ws=None, include_kl=True):
@@ -388,6 +396,7 @@ class InnerLoopPlan:
                                         _ptr(params), _ptr(vec), int(bool(include_kl)), _ptr(hv),
                                         _ptr(du), _ptr(dw), _ptr(ws), ws.numel(), _stream()),
               "psvi_hvp_partial")
+        _wrote(ws)
         return hv, du, dw
 
     # ------------------------------------------------------------ phases

@@ -1,8 +1,9 @@
 """bench.py's N > 1 control flow on CPU: world_size 2 and 3 over gloo.
 
 The driver's scaling run launches ``bench.py --gpus N`` under torchrun; this
-test runs bench's own N > 1 code -- ``run()``: the weak-scaled headline
-(``sharded_headline``), the C4 strong-scaling leg (``c4_timings``) and the C5
+test runs bench's own N > 1 code -- ``run()``: the C4 strong-scaling headline
+and the weak-scaled C3 side line (``sharded_timed``), the one-GPU C4 reference
+of rank 0 (stubbed: it is a HIP loop) and the C5
 leg (``lenet_timings``: LeNet samples split over ranks) with their barriers,
 max-over-ranks timing and the rank-0 JSON line -- over torch.distributed
 (gloo, host-staged comm) on small stand-in shapes.  Only the HIP phases are
@@ -56,6 +57,9 @@ def _rank_main(rank, world, port, out):
         return loop
 
     bench.make_sharded_loop = make_loop
+    # the one-GPU C4 reference runs psvi_inner_loop on rank 0's device
+    bench.c4_single_gpu = lambda rt, **kw: {"config": "stub", "inner_steps_per_s": 123.0,
+                                            "ms_per_step": 8.13}
     bench.draw_eps = _fake_draw
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -104,17 +108,26 @@ def test_bench_multi_rank_control_flow(world):
         assert p.exitcode == 0
     line = res[0][1]
     assert all(r[1] is None for r in res[1:]), "only rank 0 prints the JSON line"
-    assert line["n_gpus"] == world and line["scaling"] == "weak"
-    assert line["config"]["S_total"] == 4 * world and line["config"]["elbo_finite"]
+    # the headline at N > 1 is C4 itself (stand-in S = 7, M = 6), strong
+    # scaling: value = timed steps / elapsed, not multiplied by N
+    assert line["n_gpus"] == world and line["scaling"] == "strong"
+    assert line["config"]["S_total"] == 7 and line["config"]["M"] == 6
+    assert line["config"]["workload"].startswith("C4") and "S=7, M=6" in line["config"]["workload"]
+    assert line["config"]["elbo_finite"]
     assert line["value"] > 0 and line["ms_per_step"] > 0
+    assert abs(line["value"] - 1e3 / line["ms_per_step"]) <= 1e-3 * line["value"] + 0.01
     assert line["config"]["comm"].startswith("gloo")
     ks = line["roofline"]["kernels"]
     assert set(ks) == {"mvn_kstream_kernel + mvn_fwd_seg_kernel + reduce (update + next-step sample)",
                        "net_kernel(+exchange)"}
     assert all(d["avg_us"] > 0 for d in ks.values())   # the sampled per-phase events
-    c4 = line["c4"]
-    assert c4 is not None and c4["inner_steps_per_s"] > 0 and c4["elbo_finite"]
-    assert "S=7 M=6, %d GPU" % world in c4["config"]
+    one = line["c4_1gpu"]
+    assert one["inner_steps_per_s"] == 123.0
+    assert one["speedup_of_headline"] == round(line["value"] / 123.0, 3)
+    assert line["speedup_over_1gpu"] == one["speedup_of_headline"]
+    weak = line["weak"]
+    assert weak["inner_steps_per_s"] > 0 and weak["elbo_finite"]
+    assert "S=%d" % (4 * world) in weak["config"] and "M=5" in weak["config"]
     c5 = line["lenet_c5"]
     assert c5 is not None and c5["gpu_inner_steps_per_s"] > 0 and c5["elbo_finite"]
     assert "gpu_hvp_ms" not in c5      # second order: the GPU rehearsal covers it

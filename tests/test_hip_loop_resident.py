@@ -120,3 +120,48 @@ def test_modified_state_starts_cold():
         assert torch.equal(e, e_ref), case
         for a, b in zip((p, m, v), ref):
             assert torch.equal(a, b), case
+
+
+@pytest.mark.parametrize("call", ["elbo_grad", "hvp", "elbo_grad_c"])
+def test_other_calls_on_the_workspace_drop_the_state(call):
+    """A KEEP loop, then another library call on the same workspace (it writes
+    the draw / x / tiled scratch the state lives in), then a call that would
+    continue the loop: it starts cold -- its numbers are those of a plain call
+    from the packed state.  elbo_grad_c: through the C ABI alone (the
+    library's own drop, not the host's version counter)."""
+    import ctypes
+
+    from psvi.runtime import InnerLoopPlan, randn_
+    from psvi.runtime import _lib
+
+    layers, S, M, seed, lr = C3, 128, 40, 12, 1e-3
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    p0, u, z, w = _case(layers, M, 8)
+    ws = torch.empty(max(plan.loop_ws_bytes, plan.hvp_ws_bytes), dtype=torch.uint8, device=DEV)
+    ws2 = torch.empty_like(ws)
+    e = torch.empty(plan.eps_count, device=DEV)
+    randn_(e, 99)
+    p, m, v = _state(p0)
+    plan.inner_loop(u, z, w, p, m, v, 3, lr, seed=seed, ws=ws, keep=True)
+    if call == "elbo_grad":
+        plan.elbo_grad(u, z, w, e, p, ws=ws)
+    elif call == "hvp":
+        plan.hvp(u, z, w, e, p, torch.randn_like(p), ws=ws)
+    else:
+        elbo = torch.empty(1, dtype=torch.float64, device=DEV)
+        grad = torch.empty_like(p)
+        f = lambda t: ctypes.c_void_p(t.data_ptr())
+        rc = plan.lib.psvi_elbo_grad(plan.handle, f(u), f(z), f(w), f(e), f(p), 1, f(elbo),
+                                     f(grad), f(ws), ws.numel(),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0
+        # the host token still matches: RESUME is passed, the library refuses it
+        assert plan._resident is not None
+    ref = [t.clone() for t in (p, m, v)]
+    off = 3 * plan.eps_stride
+    got = plan.inner_loop(u, z, w, p, m, v, 4, lr, step0=4, seed=seed, offset=off, ws=ws).clone()
+    want = plan.inner_loop(u, z, w, *ref, 4, lr, step0=4, seed=seed, offset=off, ws=ws2)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want), call
+    for a, b in zip((p, m, v), ref):
+        assert torch.equal(a, b), call

@@ -112,3 +112,48 @@ def test_bf_stream_runs_in_the_loop():
         assert np.array_equal(x, y)
     f = _loop(plan, u, z, w, p0, 4, "higher", 5, False)
     assert not np.array_equal(a[1], f[1]), "the bf16-piece kernel did not run"
+
+
+@pytest.mark.parametrize("kind", ["higher", "hypergrad"])
+def test_bf_stream_at_the_bench_inputs(kind):
+    """The headline kernel at bench.py's own inputs: C3 (fn2 64-40-40-2, S =
+    128, M = 100), bench.synthetic_inputs, the reference init (mean = 0, corr =
+    0, sd = 1e-6: reference neural_net.py:425-428 with init_sd = 1e-6), the
+    bench's Philox seed, T = 3 -- diagonal entries around 1e-6 beside corr
+    entries around lr after the first step.  Held to the float64 oracle on the
+    same draws as the generic shapes above."""
+    import importlib.util
+    import os
+
+    from psvi.runtime import InnerLoopPlan, randn_
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    B = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(B)
+    layers, S, M, T, seed = B.LAYERS, B.S_PER_GPU, B.M, 3, 20251015
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    du, dz, dw = B.synthetic_inputs(DEV)
+    p0 = B.reference_init_params(layers, "cpu").numpy()
+    eb, pb, mb, vb = _loop(plan, du, dz, dw, p0, T, kind, seed, True)
+    ef, pf, mf, vf = _loop(plan, du, dz, dw, p0, T, kind, seed, False)
+    assert np.isfinite(pb).all() and np.isfinite(eb).all()
+    draws = []
+    for k in range(T):
+        e = torch.empty(plan.eps_count, device=DEV)
+        randn_(e, seed, k * plan.eps_stride)
+        draws.append(e.cpu().numpy().astype(np.float64))
+    u, z, w = (x.cpu().numpy() for x in (du, dz, dw))
+    o_e, _, o_traj, o_m, o_v = O.run_inner_loop("mvn", layers, p0, u.astype(np.float64), z,
+                                                w.astype(np.float64), draws, S, 1e-3, kind)
+    print(f"bench inputs {kind}: ELBO bf16 pieces {eb}, fp32 {ef}, oracle {o_e}")
+    for k in range(T):
+        assert abs(eb[k] - o_e[k]) <= 2 * abs(ef[k] - o_e[k]) + 1e-6 * abs(o_e[k]), k
+        assert rel(eb[k], o_e[k]) < 1e-4, k      # the north star's ELBO bar
+    for tag, (a_b, a_f, ref) in {"p": (pb, pf, o_traj[-1]), "m": (mb, mf, o_m),
+                                 "v": (vb, vf, o_v)}.items():
+        e_b, e_f = l2rel(a_b, ref), l2rel(a_f, ref)
+        print(f"  {tag}: l2 vs oracle bf16 pieces {e_b:.2e}, fp32 {e_f:.2e}")
+        assert e_b < 2 * e_f + 1e-7, (tag, e_b, e_f)
+    assert l2rel(pb, o_traj[-1]) < 1e-4
+    assert np.abs(pb - pf).max() < 2 * T * 1e-3

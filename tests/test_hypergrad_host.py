@@ -81,6 +81,64 @@ def test_cg_solves_spd_system_and_keeps_previous_iterate_on_convergence():
     assert torch.allclose(x1, alpha * b)
 
 
+def test_cg_after_convergence_stays_finite_and_calls_ax_like_the_reference():
+    """max_iter >> n on a non-symmetric, indefinite A: once the residual test
+    fires, the iterate is the reference's (the one before), nothing computed
+    after convergence reaches it (no inf / NaN), and with sync_every = 1 Ax is
+    called exactly as often as the reference's loop calls it (CG_torch.py:21-37:
+    a stochastic Ax draws the same noise)."""
+    from psvi.hypergrad.CG_torch import cg
+
+    g = torch.Generator().manual_seed(11)
+    n = 5
+    A = torch.randn(n, n, generator=g, dtype=torch.float64)   # non-symmetric, indefinite
+    b = torch.randn(n, generator=g, dtype=torch.float64)
+
+    def ref_cg(Ax, b, max_iter, eps):
+        x, r, p = torch.zeros_like(b), b.clone(), b.clone()
+        calls = 0
+        for _ in range(max_iter):
+            Ap = Ax(p)
+            calls += 1
+            rTr = r @ r
+            alpha = rTr / (p @ Ap)
+            xn, rn = x + alpha * p, r - alpha * Ap
+            if float(torch.norm(rn)) < eps:
+                break
+            p = rn + (rn @ rn) / rTr * p
+            x, r = xn, rn
+        return x, calls
+
+    # an SPD system solved to round-off, then 200 more iterations
+    S = A @ A.T + n * torch.eye(n, dtype=torch.float64)
+    # S: converges in ~n iterations, then 190+ iterations of A(p) on a
+    # vanishing residual (p.Ap -> 0: inf / NaN step lengths that must not
+    # reach x); A with a residual test: the reference's break; A with eps 0:
+    # no break, both run all iterations
+    for M, eps in ((S, 1e-9), (A, 1e-6), (A, 0.0)):
+        ncall = [0]
+
+        def Ax(xs, M=M):
+            ncall[0] += 1
+            return [M @ xs[0]]
+
+        x = cg(Ax, [b], max_iter=200, epsilon=eps)[0]
+        xr, calls = ref_cg(lambda v, M=M: M @ v, b, 200, eps)
+        # the reference's loop may itself break down on an indefinite A (p.Ap
+        # = 0 before any residual test fires): then both agree on non-finite
+        assert bool(torch.isfinite(x).all()) == bool(torch.isfinite(xr).all())
+        if torch.isfinite(xr).all():
+            assert torch.allclose(x, xr, rtol=1e-9, atol=1e-12)
+        if eps > 0 and M is S:
+            assert ncall[0] == calls < 200    # the reference's exit
+        # a host read every 8 iterations: at most 7 Ax calls more, same x
+        ncall[0] = 0
+        x8 = cg(Ax, [b], max_iter=200, epsilon=eps, sync_every=8)[0]
+        assert torch.allclose(x8, x, rtol=0, atol=0, equal_nan=True)
+        if eps > 0 and M is S:
+            assert calls <= ncall[0] < calls + 8
+
+
 def test_hypergrad_adam_step_arithmetic():
     """adam_step (diff_optimizers.py:184-213): v stored with + 1e-12,
     w' = w - lr (m'/(1-b1^t)) / (sqrt(v'/(1-b2^t)) + eps); DifferentiableAdam
