@@ -38,6 +38,7 @@ extern int g_net_split_below;            // kernels_net.hip
 extern int g_net_threads;                // kernels_net.hip
 extern int g_net_wg_target;              // kernels_net.hip
 extern int g_net_mloop_off;              // kernels_net.hip
+extern int g_net_geo_off;                // kernels_net.hip
 extern int g_fwd_ablation;               // kernels_mvn.hip
 extern unsigned long long* g_fwd_stamps; // kernels_mvn.hip
 extern unsigned long long* g_upd_stamps; // kernels_mvn.hip
@@ -627,6 +628,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_ROP_VALU: g_rop_valu = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_NET_MLOOP_OFF: g_net_mloop_off = value; return 0;
+        case PSVI_DBG_NET_GEO_OFF: g_net_geo_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         case PSVI_DBG_LENET_GEMM_VALU: g_lenet_gemm_valu = value; return 0;
@@ -975,6 +977,13 @@ int psvi_plan_shard_runs(const psvi_plan* p, int32_t r, int64_t* out, int32_t ca
     return 0;
 }
 
+// Every entry point that runs on a plan, except the loop that takes it up,
+// drops the resident state of a PSVI_LOOP_KEEP call: it may have written the
+// workspace, the parameters or the Adam state the state stands for.
+static void drop_resident(const psvi_plan* p) {
+    if (p) p->resident.valid = false;
+}
+
 static int check_step(const psvi_plan* p, const void* u, const void* z, const void* w,
                       const void* eps, size_t ws_bytes, const void* ws) {
     if (!p) return fail(PSVI_EINVAL, "null plan");
@@ -1017,6 +1026,7 @@ int psvi_inner_step(const psvi_plan* p, const float* u, const int32_t* z, const 
                     const float* eps, float* params, float* adam_m, float* adam_v,
                     const psvi_adam_hp* hp, double* elbo_out, void* ws, size_t ws_bytes,
                     void* stream) {
+    drop_resident(p);
     if (int rc = check_step(p, u, z, w, eps, ws_bytes, ws)) return rc;
     if (!params || !adam_m || !adam_v || !hp || !elbo_out)
         return fail(PSVI_EINVAL, "null state pointer");
@@ -1029,6 +1039,7 @@ int psvi_inner_step(const psvi_plan* p, const float* u, const int32_t* z, const 
 int psvi_elbo_grad(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
                    const float* eps, const float* params, int32_t include_kl, double* elbo_out,
                    float* grad_out, void* ws, size_t ws_bytes, void* stream) {
+    drop_resident(p);
     if (int rc = check_step(p, u, z, w, eps, ws_bytes, ws)) return rc;
     if (!params || !elbo_out || !grad_out) return fail(PSVI_EINVAL, "null pointer");
     return step_impl(p, u, z, w, eps, const_cast<float*>(params), nullptr, nullptr, nullptr,
@@ -1038,6 +1049,7 @@ int psvi_elbo_grad(const psvi_plan* p, const float* u, const int32_t* z, const f
 int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* z,
                              const float* w, const float* eps, const float* params, float* acc,
                              double* nll_out, void* stream) {
+    drop_resident(p);
     if (!p || p->family == PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a mean-field plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!u || !z || !w || !eps || !params || !acc || !nll_out)
@@ -1055,6 +1067,7 @@ int psvi_mf_phase_accumulate(const psvi_plan* p, const float* u, const int32_t* 
 int psvi_mf_phase_update(const psvi_plan* p, const float* acc, float* params, float* adam_m,
                          float* adam_v, const psvi_adam_hp* hp, double* kl_out,
                          float* grad_out, int32_t include_kl, void* stream) {
+    drop_resident(p);
     if (!p || p->family == PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a mean-field plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!acc || !params) return fail(PSVI_EINVAL, "null pointer");
@@ -1068,6 +1081,7 @@ int psvi_mf_phase_update(const psvi_plan* p, const float* acc, float* params, fl
 
 int psvi_mvn_phase_sample(const psvi_plan* p, const float* eps, const float* params,
                           float* x_shard, void* stream) {
+    drop_resident(p);
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     // a rank that owns no rows (fewer bands than ranks) has an empty x shard
@@ -1079,6 +1093,7 @@ int psvi_mvn_phase_sample(const psvi_plan* p, const float* eps, const float* par
 
 int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
                        const float* x_recv, float* g_send, double* nll_out, void* stream) {
+    drop_resident(p);
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     // a rank without samples (S < world) has empty x / g blocks
@@ -1093,6 +1108,7 @@ int psvi_mvn_phase_net(const psvi_plan* p, const float* u, const int32_t* z, con
 int psvi_mvn_phase_net_draw(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
                             const float* x_recv, float* g_send, double* nll_out, float* eps_out,
                             int64_t n, uint64_t seed, uint64_t offset, void* stream) {
+    drop_resident(p);
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     const bool none = p->s_cnt[p->rank] == 0;  // S < world: empty x / g blocks
@@ -1110,6 +1126,7 @@ int psvi_mvn_phase_net_draw(const psvi_plan* p, const float* u, const int32_t* z
 int psvi_mvn_phase_update(const psvi_plan* p, const float* eps, const float* g_shard,
                           float* params, float* adam_m, float* adam_v, const psvi_adam_hp* hp,
                           double* kl_out, float* grad_out, int32_t include_kl, void* stream) {
+    drop_resident(p);
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!eps || (!g_shard && p->rows_tot[p->rank] > 0) || !params)
@@ -1126,6 +1143,7 @@ int psvi_mvn_phase_update_sample(const psvi_plan* p, const float* eps, const flo
                                  float* params, float* adam_m, float* adam_v,
                                  const psvi_adam_hp* hp, double* kl_out, int32_t include_kl,
                                  const float* eps_next, float* x_next, void* stream) {
+    drop_resident(p);
     if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     const bool rows = p->rows_tot[p->rank] > 0;  // no rows: empty G and x shards
@@ -1173,6 +1191,7 @@ static size_t loop_ws_bytes(const psvi_plan* p) {
 
 int psvi_mvn_tiled_convert(const psvi_plan* p, float* params, float* adam_m, float* adam_v,
                            float* tstate, int32_t to_tiled, void* stream) {
+    drop_resident(p);
     if (!p || !tiled_ok(p)) return fail(PSVI_EUNSUP, "plan has no tiled state (full-cov, world 1, S <= 128)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!params || !adam_m || !adam_v || !tstate) return fail(PSVI_EINVAL, "null pointer");
@@ -1185,6 +1204,7 @@ int psvi_mvn_phase_update_tiled(const psvi_plan* p, const float* eps, const floa
                                 float* params, float* adam_m, float* adam_v, float* tstate,
                                 const psvi_adam_hp* hp, double* kl_out, int32_t include_kl,
                                 const float* eps_next, float* x_next, void* stream) {
+    drop_resident(p);
     if (!p || !tiled_ok(p)) return fail(PSVI_EUNSUP, "plan has no tiled state (full-cov, world 1, S <= 128)");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (!eps || !g_shard || !params || !adam_m || !adam_v || !tstate || !hp)
@@ -1387,6 +1407,7 @@ static int outer_impl(const psvi_plan* p, int32_t n_pseudo, const float* x_all,
                       float* grad_u, float* grad_w, double* sample_out,
                       const float* ext_coef, void* ws, size_t ws_bytes, void* stream,
                       int ablated = 0) {
+    drop_resident(p);
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "the outer objective needs world == 1");
@@ -1495,6 +1516,7 @@ int psvi_outer_elbo_grad_coef(const psvi_plan* p, int32_t n_pseudo, const float*
 int psvi_evaluate(const psvi_plan* p, int32_t n_pseudo, const float* x_all, const int32_t* z_all,
                   const float* w_all, const float* eps, const float* params, int32_t correction,
                   float* probs_out, double* stats_out, void* ws, size_t ws_bytes, void* stream) {
+    drop_resident(p);
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "evaluate needs world == 1");
@@ -1532,6 +1554,7 @@ int psvi_hvp_partial(const psvi_plan* p, const float* u, const int32_t* z, const
                      const float* eps, const float* params, const float* vec,
                      int32_t include_kl, float* hv_out, float* du_out, float* dw_out, void* ws,
                      size_t ws_bytes, void* stream) {
+    drop_resident(p);
     if (!p) return fail(PSVI_EINVAL, "null plan");
     if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
     if (p->world != 1) return fail(PSVI_ESTATE, "psvi_hvp needs world == 1");

@@ -64,7 +64,7 @@ struct NetArgs {
     int lw[kMaxL], ldw[kMaxL], lb[kMaxL], lx[kMaxL], ldx[kMaxL];
     int lwt[kMaxL], ldwt[kMaxL];  // W_l^T (l >= 1: the propagation GEMM's k-contiguous operand)
     int lg[kMaxL], ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4;  // lg[l]: G_l (l < L-1); ldl: dlogits [Mp][lddl]; lzw: z, w
-    int nslack, nslack_early, slack[5 * kMaxL + 8];  // float offsets of the 64-float zero slacks
+    int nslack, nslack_early, slack[5 * kMaxL + 8];  // kNetSlack  // float offsets of the 64-float zero slacks
     int stage_len, stage_off[kMaxWorld + 1];  // FULLCOV: this sample's x row, source blocks back to back
     const float* u;
     const int32_t* z;
@@ -118,6 +118,146 @@ struct NetArgs {
     uint16_t* rn_planes;
 };
 
+// ---- LDS carve (float offsets, row strides) of the network kernel.  Row
+// strides are 4 x odd (== 8 mod 16): a 16-lane float4 read along k (rows i16
+// = 0..15) and a 64-lane float read down k (lanes 16 k4 + i16, rows 4 k4
+// apart) both hit distinct banks.  Regions read before the forward pass come
+// first; every region is followed by a 64-float zero slack.
+constexpr int kNetSlack = 5 * kMaxL + 8;
+struct NetDims {
+    int L;
+    int din[kMaxL], dout[kMaxL];
+};
+struct NetCarve {
+    int lw[kMaxL], ldw[kMaxL], lb[kMaxL], lx[kMaxL], ldx[kMaxL], lwt[kMaxL], ldwt[kMaxL],
+        lg[kMaxL];
+    int ldl, lddl, lred, lsrc, lzw, lstamp, lds_f4, Mp, nslack, nslack_early;
+    int slack[kNetSlack];
+};
+constexpr int net_rup(int x, int m) { return (x + m - 1) / m * m; }
+constexpr int net_ld8o(int x) { return x + (24 - x % 16) % 16; }  // >= x, == 8 (mod 16)
+// nbands: world > 1 full-cov plans, the band table's entries (per-workgroup
+// source tables in LDS); 0 otherwise
+constexpr NetCarve net_carve(const NetDims& d, int mc, int nbands) {
+    NetCarve c{};
+    int off = 0, ns = 0;
+    auto take = [&](int nfl) {
+        const int o = off;
+        off += (nfl + 3) & ~3;
+        c.slack[ns] = off;
+        ++ns;
+        off += 64;
+        return o;
+    };
+    const int Mp = net_rup(mc, 16);
+    for (int l = 0; l < d.L; ++l) {
+        const int din = d.din[l], dout = d.dout[l];
+        const int ldw = net_ld8o(net_rup(din, 16));
+        c.lw[l] = take(net_rup(dout, 16) * ldw);
+        c.ldw[l] = ldw;
+        c.lb[l] = take(dout);
+        if (l > 0) {  // W^T: rows i < din (16-multiple), columns j < dout (16-multiple)
+            const int ldwt = net_ld8o(net_rup(dout, 16));
+            c.lwt[l] = take(net_rup(din, 16) * ldwt);
+            c.ldwt[l] = ldwt;
+        } else {
+            c.lwt[0] = c.lw[0];  // unused (no propagation below layer 0)
+            c.ldwt[0] = ldw;
+        }
+    }
+    const int ldx0 = net_ld8o(d.din[0]);
+    const int lx0 = take(Mp * ldx0);
+    c.lred = take(16);
+    c.lzw = take(2 * Mp);
+    c.lstamp = take(48);  // 16 x uint64 diagnostics stamps + 8 wave starts
+    // per-workgroup tables (world > 1): every band's int64 g_send offset
+    // (8-byte aligned), the x row's per-source int64 bases and int starts,
+    // the layers' first band index
+    c.lsrc = take(2 * nbands + 3 * kMaxWorld + kMaxL + 2 * kMaxWorld + 1);
+    c.nslack_early = ns;
+    for (int l = 1; l < d.L; ++l) {
+        c.ldx[l] = net_ld8o(d.din[l]);
+        c.lx[l] = take(Mp * c.ldx[l]);
+    }
+    // G_l (l < L - 1, the gradient of layer l's output, stride of X_{l+1}):
+    // every one stays until the weight-gradient phase
+    for (int l = 0; l + 1 < d.L; ++l) c.lg[l] = take(Mp * net_ld8o(d.din[l + 1]));
+    c.lddl = net_ld8o(d.dout[d.L - 1]);
+    c.ldl = take(Mp * c.lddl);
+    off = (off + 3) & ~3;
+    c.lx[0] = lx0;
+    c.ldx[0] = ldx0;
+    c.Mp = Mp;
+    c.nslack = ns;
+    c.lds_f4 = off / 4;
+    return c;
+}
+
+// Geometry the kernel reads: GEO 0 the plan's (NetArgs, any stack, at run
+// time); GEO 1 / 2 the fn2 stack of configs C3 / C4 (64 -> 40 -> 40 -> 2,
+// 100-row pseudopoint chunks: Mp = 112), one source rank / several (the
+// band table's 69 entries) -- every layer size, row stride and LDS offset a
+// compile-time constant, so layer loops unroll, LDS addresses become
+// instruction offsets and no kernel argument is loaded for them.
+constexpr NetDims kFn2Dims{3, {64, 40, 40}, {40, 40, 2}};
+constexpr int kFn2Mp = 112, kFn2Bands = 41 + 26 + 2;
+template <int GEO>
+struct NetGeo {
+    static constexpr bool kFixed = true;
+    static constexpr int kUnroll = kMaxL;
+    static constexpr NetCarve C = net_carve(kFn2Dims, kFn2Mp, GEO == 2 ? kFn2Bands : 0);
+    __device__ explicit NetGeo(const NetArgs&) {}
+    __device__ static constexpr int L() { return kFn2Dims.L; }
+    __device__ static constexpr int din(int l) { return kFn2Dims.din[l]; }
+    __device__ static constexpr int dout(int l) { return kFn2Dims.dout[l]; }
+    __device__ static constexpr int lw(int l) { return C.lw[l]; }
+    __device__ static constexpr int ldw(int l) { return C.ldw[l]; }
+    __device__ static constexpr int lb(int l) { return C.lb[l]; }
+    __device__ static constexpr int lx(int l) { return C.lx[l]; }
+    __device__ static constexpr int ldx(int l) { return C.ldx[l]; }
+    __device__ static constexpr int lwt(int l) { return C.lwt[l]; }
+    __device__ static constexpr int ldwt(int l) { return C.ldwt[l]; }
+    __device__ static constexpr int lg(int l) { return C.lg[l]; }
+    __device__ static constexpr int slack(int k) { return C.slack[k]; }
+    __device__ static constexpr int ldl() { return C.ldl; }
+    __device__ static constexpr int lddl() { return C.lddl; }
+    __device__ static constexpr int lred() { return C.lred; }
+    __device__ static constexpr int lsrc() { return C.lsrc; }
+    __device__ static constexpr int lzw() { return C.lzw; }
+    __device__ static constexpr int lstamp() { return C.lstamp; }
+    __device__ static constexpr int lds_f4() { return C.lds_f4; }
+    __device__ static constexpr int Mp() { return C.Mp; }
+    __device__ static constexpr int nslack() { return C.nslack; }
+};
+template <>
+struct NetGeo<0> {
+    static constexpr bool kFixed = false;
+    static constexpr int kUnroll = 1;
+    const NetArgs& a;
+    __device__ explicit NetGeo(const NetArgs& args) : a(args) {}
+    __device__ int L() const { return a.L; }
+    __device__ int din(int l) const { return a.din[l]; }
+    __device__ int dout(int l) const { return a.dout[l]; }
+    __device__ int lw(int l) const { return a.lw[l]; }
+    __device__ int ldw(int l) const { return a.ldw[l]; }
+    __device__ int lb(int l) const { return a.lb[l]; }
+    __device__ int lx(int l) const { return a.lx[l]; }
+    __device__ int ldx(int l) const { return a.ldx[l]; }
+    __device__ int lwt(int l) const { return a.lwt[l]; }
+    __device__ int ldwt(int l) const { return a.ldwt[l]; }
+    __device__ int lg(int l) const { return a.lg[l]; }
+    __device__ int slack(int k) const { return a.slack[k]; }
+    __device__ int ldl() const { return a.ldl; }
+    __device__ int lddl() const { return a.lddl; }
+    __device__ int lred() const { return a.lred; }
+    __device__ int lsrc() const { return a.lsrc; }
+    __device__ int lzw() const { return a.lzw; }
+    __device__ int lstamp() const { return a.lstamp; }
+    __device__ int lds_f4() const { return a.lds_f4; }
+    __device__ int Mp() const { return a.Mp; }
+    __device__ int nslack() const { return a.nslack; }
+};
+
 // One GEMM's tiles (P x Q outputs rounded up to 16-tiles): units of one
 // 16-row tile x NQ column tiles -- a whole row of column tiles (NQ = tq <= 3:
 // one A read per NQ MFMAs) when that still gives every SIMD a unit, else
@@ -134,12 +274,19 @@ __device__ __forceinline__ int gemm_units(int P, int Q) {
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4;
     return tp * (tq / gemm_nq(tp, tq));
 }
-template <bool ACONT, bool BCONT, int NQ, class Epi>
+template <bool ACONT, bool BCONT, int NQ, int CARRY = 0, class Epi>
 __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, const float* A, int lda,
                                            const float* B, int ldb, Epi epi, int ustep = 0,
-                                           int K = 0) {
+                                           int K = 0, floatx4 (*carry)[NQ] = nullptr,
+                                           int cmode = 0) {
     // K (row GEMMs, k-contiguous A): the true contraction length, masked in
     // the last k-group; 0 = K16 (no mask)
+    // CARRY > 0 (looped pseudopoint chunks, fixed geometry): the wave's units
+    // k = 0 .. CARRY - 1 (u = u0 + k nwaves) keep their sums in carry[k]
+    // across the chunks -- cmode 1 (first chunk): store the chunk's sums
+    // there, no epilogue; 3 (a middle chunk): add them; 2 (the last): the
+    // epilogue gets carry[k] + the chunk's sums (the chunks added in chunk
+    // order, as the run-time geometry's read-modify-write of g_send does)
     const bool kmask = ACONT && K > 0 && K < K16;  // uniform
     const int nwv = ustep ? ustep : (int)(blockDim.x >> 6), lane = threadIdx.x & 63, i16 = lane & 15,
               k4 = lane >> 4;
@@ -160,8 +307,9 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
     ptrs(u0, pa, pb, p0, q0);
     TileOps<ACONT, BCONT, NQ> x0, x1;
     x0.load(pa, lda, pb, ldb);
-    for (int u = u0; u < nu; u += nwv) {  // wave-uniform
-        floatx4 acc[NQ];
+    // one unit: the k-groups into acc, then the next unit's first group read
+    // before the epilogue; returns the unit's first row / column
+    auto unit = [&](int u, floatx4 (&acc)[NQ], int& pe, int& qe) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < NQ; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
         // x0 holds group 0; two groups per trip with fixed registers (no
@@ -189,18 +337,48 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
             if (kmask) x0.mask_a(16 * (nk - 1), K);
             x0.mma(acc);
         }
-        const int pe = p0, qe = q0;
+        pe = p0;
+        qe = q0;
         if (u + nwv < nu) {
             ptrs(u + nwv, pa, pb, p0, q0);
             x0.load(pa, lda, pb, ldb);
         }
-        // odd lane-groups hand over their four rows rotated by two: the
-        // epilogue's row-wise LDS accesses of the two groups of a 32-lane half
-        // are then 2 or 6 rows apart (16 banks at strides == 8 mod 16), not 4
+    };
+    // odd lane-groups hand over their four rows rotated by two: the
+    // epilogue's row-wise LDS accesses of the two groups of a 32-lane half
+    // are then 2 or 6 rows apart (16 banks at strides == 8 mod 16), not 4
+    auto out = [&](const floatx4 (&acc)[NQ], int pe, int qe) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
             const floatx4 v = acc[c];
             epi(pe + 4 * k4, qe + 16 * c + i16, rot ? floatx4{v[2], v[3], v[0], v[1]} : v, rot);
+        }
+    };
+    if constexpr (CARRY == 0) {
+        for (int u = u0; u < nu; u += nwv) {  // wave-uniform
+            floatx4 acc[NQ];
+            int pe, qe;
+            unit(u, acc, pe, qe);
+            out(acc, pe, qe);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < CARRY; ++k) {
+            const int u = u0 + k * nwv;
+            if (u >= nu) break;  // wave-uniform
+            floatx4 acc[NQ];
+            int pe, qe;
+            unit(u, acc, pe, qe);
+            if (cmode == 1 || cmode == 3) {
+#pragma unroll
+                for (int c = 0; c < NQ; ++c) carry[k][c] = cmode == 3 ? carry[k][c] + acc[c] : acc[c];
+            } else {
+                if (cmode == 2) {
+#pragma unroll
+                    for (int c = 0; c < NQ; ++c) acc[c] = carry[k][c] + acc[c];
+                }
+                out(acc, pe, qe);
+            }
         }
     }
 }
@@ -215,6 +393,21 @@ __device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const 
         case 2: gemm_steps<ACONT, BCONT, 2>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
         default: gemm_steps<ACONT, BCONT, 1>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi); break;
     }
+}
+
+// mfma_gemm with the units' sums carried across looped pseudopoint chunks
+// (gemm_steps CARRY): the fixed fn2 geometry's weight gradients, one column
+// tile per unit (NQ = 1) and at most CARRY units per wave and layer
+template <int CARRY, class Epi>
+__device__ __forceinline__ void mfma_gemm_carry(int P, int Q, int K, int first, const float* A,
+                                                int lda, const float* B, int ldb, Epi epi,
+                                                floatx4 (*carry)[1], int cmode) {
+    const int wid = wave_id(), nwv = blockDim.x >> 6;
+    const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, K16 = (K + 15) & ~15;
+    const int u0 = ((wid - first) % nwv + nwv) % nwv;
+    // (the host gates the fixed geometry to 512 threads: tp tq <= CARRY nwaves
+    // for every fn2 layer, and gemm_nq is 1 for all of them)
+    gemm_steps<false, false, 1, CARRY>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi, 0, 0, carry, cmode);
 }
 
 // One 16-row tile by ONE wave: C[p][q] for p < 16, q < Q (every column tile:
@@ -259,29 +452,32 @@ __device__ __forceinline__ int64_t fc_addr(const NetArgs& a, int nsrc, const int
 // instantiation has straight-line x loads: with the run-table path in the
 // same kernel the register allocator shares registers across the two paths
 // and the waitcnt pass then serialises the u and x loads (seen in the ISA).
-template <int FAM, bool MSRC, bool VEC = false, bool MLOOP = false>
+template <int FAM, bool MSRC, bool VEC = false, bool MLOOP = false, int GEO = 0>
 __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
+    using Geo = NetGeo<GEO>;
+    const Geo g(a);
+    constexpr int kUL = Geo::kUnroll;  // layer loops: fully unrolled for a fixed geometry
     static_assert(!VEC || FAM == PSVI_FAMILY_FULLCOV, "float4 loads: the full-cov x row");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
     const int role = blockIdx.y;
-    const int L = a.L, Mp = a.Mp;
+    const int L = g.L(), Mp = g.Mp();
     const int tid = threadIdx.x;
-    unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + a.lstamp);
+    unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + g.lstamp());
     if (a.abl & 128) {
         // diagnostics: poison the LDS with NaN first -- every word the kernel
         // reads must have been written by it (the padding contract).  abl >> 8
         // picks one region (0: all; 1 weights, 2 X_0, 3 red / zw / stamps /
         // tables, 4 X_l (l >= 1), 5 G_l, 6 dlogits and the rest)
         const int reg = a.abl >> 8;
-        int lo = 0, hi = 4 * a.lds_f4;
-        if (reg == 1) { lo = 0; hi = a.lx[0]; }
-        else if (reg == 2) { lo = a.lx[0]; hi = a.lred; }
-        else if (reg == 3) { lo = a.lred; hi = a.L > 1 ? a.lx[1] : a.ldl; }
-        else if (reg == 4) { lo = a.L > 1 ? a.lx[1] : a.ldl; hi = a.L > 1 ? a.lg[0] : a.ldl; }
-        else if (reg == 5) { lo = a.L > 1 ? a.lg[0] : a.ldl; hi = a.ldl; }
-        else if (reg == 6) { lo = a.ldl; }
+        int lo = 0, hi = 4 * g.lds_f4();
+        if (reg == 1) { lo = 0; hi = g.lx(0); }
+        else if (reg == 2) { lo = g.lx(0); hi = g.lred(); }
+        else if (reg == 3) { lo = g.lred(); hi = g.L() > 1 ? g.lx(1) : g.ldl(); }
+        else if (reg == 4) { lo = g.L() > 1 ? g.lx(1) : g.ldl(); hi = g.L() > 1 ? g.lg(0) : g.ldl(); }
+        else if (reg == 5) { lo = g.L() > 1 ? g.lg(0) : g.ldl(); hi = g.ldl(); }
+        else if (reg == 6) { lo = g.ldl(); }
         for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) sm[i] = __builtin_nanf("");
         __syncthreads();
     }
@@ -299,7 +495,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int own_hi = (a.nroles == 1 || role == 1) ? L : 1;
 
     // ---- 1. loads --------------------------------------------------------
-    int* srct = reinterpret_cast<int*>(sm + a.lsrc);
+    int* srct = reinterpret_cast<int*>(sm + g.lsrc());
     const int nsrc = MSRC ? a.nsrc : 1;
     if (FAM == PSVI_FAMILY_FULLCOV && MSRC) {
         // uniform loops: a per-lane index into the by-value kernel arguments
@@ -342,6 +538,14 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     // added to the first chunk's -- by the same lane, in chunk order, so the
     // sums equal the per-chunk slots added in chunk order)
     const int nloop = MLOOP ? a.mloop : 1;
+    // looped chunks under the fixed geometry: the weight-gradient sums of the
+    // chunks stay in registers (wc: two 16x16 units per wave and layer; bc:
+    // the bias column sums) and leave once, after the last chunk, instead of
+    // each chunk's read-modify-write of g_send
+    constexpr bool kCarry = MLOOP && Geo::kFixed;
+    constexpr int kWcUnits = 2;
+    floatx4 wc[kMaxL][kWcUnits][1];
+    float bc[kMaxL];
     int ch = 0;
 chunk_top:  // a backward jump only when MLOOP (no loop at all in the other instantiations)
     {
@@ -356,11 +560,11 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     // map (W_l[j][i] or b_l[j], and W_l^T[i][j]): the elements go straight
     // into the padded W_l, b_l, W_l^T, no stage, no index arithmetic behind
     // the loads (LDS-DMA of the rows measured several times slower).
-    const int D = a.din[0];
+    const int D = g.din(0);
     const int r16 = tid >> 4, c16 = tid & 15, nr16 = blockDim.x >> 4;
-    float* zw = sm + a.lzw;  // the chunk's labels (as int bits) and weights
-    float* X0 = sm + a.lx[0];
-    const int ldx0 = a.ldx[0];
+    float* zw = sm + g.lzw();  // the chunk's labels (as int bits) and weights
+    float* X0 = sm + g.lx(0);
+    const int ldx0 = g.ldx(0);
     if constexpr (VEC) {
         // one source, D % 4 == 0: the u chunk and the x row as float4 runs (a
         // quarter of the load instructions), x's < 4 trailing elements by
@@ -431,15 +635,17 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                 // loaded element): W columns >= din and rows >= dout, W^T columns
                 // dout .. the 16-multiple, u columns >= D up to the 16-multiple, u
                 // rows past the chunk, the 64-float slacks after every region
-                for (int l = 0; l < L && first; ++l) {
-                    const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
+#pragma unroll kUL
+                for (int l = 0; l < L; ++l) {
+                    if (!first) break;
+                    const int din = g.din(l), dout = g.dout(l), ldw = g.ldw(l);
                     const int rows = (dout + 15) & ~15;
                     if (l > 0) {
-                        float* WT = sm + a.lwt[l];
+                        float* WT = sm + g.lwt(l);
                         for (int i = r16; i < din; i += nr16)
-                            if (dout + c16 < rows) WT[i * a.ldwt[l] + dout + c16] = 0.f;
+                            if (dout + c16 < rows) WT[i * g.ldwt(l) + dout + c16] = 0.f;
                     }
-                    float* W = sm + a.lw[l];
+                    float* W = sm + g.lw(l);
                     for (int j = r16; j < dout; j += nr16)
                         for (int c = din + c16; c < ldw; c += 16) W[j * ldw + c] = 0.f;
                     for (int i = tid; i < (rows - dout) * ldw; i += bd) W[dout * ldw + i] = 0.f;
@@ -448,8 +654,15 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                 for (int m = r16; m < mcnt; m += nr16)
                     if (D + c16 < cend) X0[m * ldx0 + D + c16] = 0.f;
                 for (int i = tid; i < (Mp - mcnt) * ldx0; i += bd) X0[mcnt * ldx0 + i] = 0.f;
-                for (int k = wave_id(); k < a.nslack; k += bd >> 6)  // wave-uniform slot
-                    sm[a.slack[k] + (tid & 63)] = 0.f;
+                if constexpr (Geo::kFixed) {
+                    // every slack's offset a constant: one store per slack, wave k % nwaves
+#pragma unroll
+                    for (int k = 0; k < Geo::nslack(); ++k)
+                        if (k % (int)(bd >> 6) == wave_id()) sm[Geo::slack(k) + (tid & 63)] = 0.f;
+                } else {
+                    for (int k = wave_id(); k < g.nslack(); k += bd >> 6)  // wave-uniform slot
+                        sm[g.slack(k) + (tid & 63)] = 0.f;
+                }
             }
             if (a.abl & 1) continue;
 #pragma unroll
@@ -549,14 +762,14 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                 // dout, u columns >= D up to the 16-multiple, u rows past the
                 // chunk, the slacks before the stage
                 for (int l = 0; l < L; ++l) {  // (the scalar path is never looped)
-                    const int din = a.din[l], dout = a.dout[l], ldw = a.ldw[l];
+                    const int din = g.din(l), dout = g.dout(l), ldw = g.ldw(l);
                     const int rows = (dout + 15) & ~15;
                     if (l > 0) {  // W^T columns dout .. the 16-multiple (K padding of the propagation)
-                        float* WT = sm + a.lwt[l];
+                        float* WT = sm + g.lwt(l);
                         for (int i = r16; i < din; i += nr16)
-                            if (dout + c16 < rows) WT[i * a.ldwt[l] + dout + c16] = 0.f;
+                            if (dout + c16 < rows) WT[i * g.ldwt(l) + dout + c16] = 0.f;
                     }
-                    float* W = sm + a.lw[l];
+                    float* W = sm + g.lw(l);
                     for (int j = r16; j < dout; j += nr16)
                         for (int c = din + c16; c < ldw; c += 16) W[j * ldw + c] = 0.f;
                     for (int i = tid; i < (rows - dout) * ldw; i += bd) W[dout * ldw + i] = 0.f;
@@ -565,8 +778,15 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                 for (int m = r16; m < mcnt; m += nr16)
                     if (D + c16 < cend) X0[m * ldx0 + D + c16] = 0.f;
                 for (int i = tid; i < (Mp - mcnt) * ldx0; i += bd) X0[mcnt * ldx0 + i] = 0.f;
-                for (int k = wave_id(); k < a.nslack; k += bd >> 6)  // wave-uniform slot
-                    sm[a.slack[k] + (tid & 63)] = 0.f;
+                if constexpr (Geo::kFixed) {
+                    // every slack's offset a constant: one store per slack, wave k % nwaves
+#pragma unroll
+                    for (int k = 0; k < Geo::nslack(); ++k)
+                        if (k % (int)(bd >> 6) == wave_id()) sm[Geo::slack(k) + (tid & 63)] = 0.f;
+                } else {
+                    for (int k = wave_id(); k < g.nslack(); k += bd >> 6)  // wave-uniform slot
+                        sm[g.slack(k) + (tid & 63)] = 0.f;
+                }
             }
             if (a.abl & 1) continue;
 #pragma unroll
@@ -599,11 +819,11 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         // Normal.rsample: loc + eps * softplus(rho), elementwise into place
         constexpr int kB = 16;
         for (int l = 0; l < L; ++l) {
-            const int din = a.din[l], dout = a.dout[l], nw = din * dout, n = nw + dout;
-            float* W = sm + a.lw[l];
-            float* WT = sm + a.lwt[l];
-            float* Bv = sm + a.lb[l];
-            const int ldw = a.ldw[l], ldwt = a.ldwt[l];
+            const int din = g.din(l), dout = g.dout(l), nw = din * dout, n = nw + dout;
+            float* W = sm + g.lw(l);
+            float* WT = sm + g.lwt(l);
+            float* Bv = sm + g.lb(l);
+            const int ldw = g.ldw(l), ldwt = g.ldwt(l);
             const bool wt = l >= wt_lo;
             const float* mu = a.params + a.poff[l];
             const float* rho = mu + n;
@@ -667,7 +887,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     // logits on the 16 lanes of a DPP row) runs in the head GEMM's epilogue:
     // log-softmax over the lanes, weighted NLL, dlogits w_m (softmax - onehot)
     // stored in place of the logits.
-    const int C = a.dout[L - 1];
+    const int C = g.dout(L - 1);
     const bool fuse_head = a.outer == 0 && C <= 16 && !(a.abl & 4);
     const bool bwd = !(a.abl & 8) && a.outer != 1;
     // outer backward: input gradient of the pseudopoint rows (d loss / d u)
@@ -679,20 +899,22 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     auto drain = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
     // G_l: dlogits for l = L - 1, else the l-th gradient buffer (stride of X_{l+1})
     auto gbuf = [&](int l) __attribute__((always_inline)) {
-        return l == L - 1 ? sm + a.ldl : sm + a.lg[l];
+        return l == L - 1 ? sm + g.ldl() : sm + g.lg(l);
     };
-    auto gld = [&](int l) __attribute__((always_inline)) { return l == L - 1 ? a.lddl : a.ldx[l + 1]; };
+    auto gld = [&](int l) __attribute__((always_inline)) { return l == L - 1 ? g.lddl() : g.ldx(l + 1); };
     for (int pt = wave_id(); 16 * pt < Mp; pt += nwv) {  // wave-uniform
         const int r0 = 16 * pt;
         // diagnostics (abl & 64): the first tile's forward twice (its stamps record the second)
         for (int rep = 0; rep < (((a.abl & 64) && pt == wave_id()) ? 2 : 1); ++rep)
-        for (int l = 0; l < L && !(a.abl & 2); ++l) {
-            const int din = a.din[l], dout = a.dout[l];
+#pragma unroll kUL
+        for (int l = 0; l < L; ++l) {
+            if (a.abl & 2) break;
+            const int din = g.din(l), dout = g.dout(l);
             const bool head = l == L - 1;
-            const float* X = sm + a.lx[l] + r0 * a.ldx[l];
-            float* Xn = (head ? sm + a.ldl : sm + a.lx[l + 1]) + r0 * (head ? a.lddl : a.ldx[l + 1]);
-            const float* Bv = sm + a.lb[l];
-            const int ldn = head ? a.lddl : a.ldx[l + 1], jend = min((dout + 15) & ~15, ldn);
+            const float* X = sm + g.lx(l) + r0 * g.ldx(l);
+            float* Xn = (head ? sm + g.ldl() : sm + g.lx(l + 1)) + r0 * (head ? g.lddl() : g.ldx(l + 1));
+            const float* Bv = sm + g.lb(l);
+            const int ldn = head ? g.lddl() : g.ldx(l + 1), jend = min((dout + 15) & ~15, ldn);
             if (head && fuse_head) {
                 auto epi = [&](int m, int j, floatx4 v, int rot) {  // j = i16: every lane of the row takes part
                     const bool jl = j < C;
@@ -711,7 +933,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                         if (ok && j == zr) part += wr * (lse - y);
                     }
                 };
-                row_gemm<true, true>(dout, din, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
+                row_gemm<true, true>(dout, din, X, g.ldx(l), sm + g.lw(l), g.ldw(l), epi);
             } else {
                 auto epi = [&](int m, int j, floatx4 v, int rot) {
                     if (j < jend) {
@@ -725,7 +947,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                         }
                     }
                 };
-                row_gemm<true, true>(dout, din, X, a.ldx[l], sm + a.lw[l], a.ldw[l], epi);
+                row_gemm<true, true>(dout, din, X, g.ldx(l), sm + g.lw(l), g.ldw(l), epi);
             }
             drain();
             if (pt == 0 && l < 3) NET_STAMP(6 + l, __builtin_amdgcn_s_memtime());
@@ -734,8 +956,8 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         // take the tile's rows, logits -> weighted NLL, dlogits in place
         if (!fuse_head && !(a.abl & 4) && lane < 16 && r0 + lane < mcnt) {
             const int m = r0 + lane;
-            const int ldl = a.lddl;
-            float* row = sm + a.ldl + m * ldl;
+            const int ldl = g.lddl();
+            float* row = sm + g.ldl() + m * ldl;
             const int zm = __float_as_int(zw[m]);
             const float wm = zw[Mp + m] * (m0 + m < a.n_pseudo ? cp : cd);
             float mx = -INFINITY, lz = 0.f;
@@ -762,11 +984,13 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         if (pt == 0) NET_STAMP(9, __builtin_amdgcn_s_memtime());
         if (!bwd) continue;
         // ---- backward propagation down to the lowest owned layer
-        for (int l = L - 1; l > own_lo; --l) {
-            const int din = a.din[l], dout = a.dout[l];
+#pragma unroll kUL
+        for (int l = L - 1; l > 0; --l) {
+            if (l <= own_lo) continue;  // (uniform: the role)
+            const int din = g.din(l), dout = g.dout(l);
             const float* G = gbuf(l) + r0 * gld(l);
-            const int ldx = a.ldx[l];
-            const float* X = sm + a.lx[l] + r0 * ldx;
+            const int ldx = g.ldx(l);
+            const float* X = sm + g.lx(l) + r0 * ldx;
             float* Gn = gbuf(l - 1) + r0 * ldx;  // G_{l-1}: the stride of X_l
             const int iend = min((din + 15) & ~15, ldx);
             auto epi = [&](int m, int i, floatx4 v, int rot) {
@@ -780,15 +1004,15 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                 }
             };
             if constexpr (FAM == PSVI_FAMILY_FULLCOV)
-                row_gemm<true, true>(din, dout, G, gld(l), sm + a.lwt[l], a.ldwt[l], epi);
+                row_gemm<true, true>(din, dout, G, gld(l), sm + g.lwt(l), g.ldwt(l), epi);
             else  // mean-field: K = dout is small (the classifier), W read down k
-                row_gemm<true, false>(din, dout, G, gld(l), sm + a.lw[l], a.ldw[l], epi);
+                row_gemm<true, false>(din, dout, G, gld(l), sm + g.lw(l), g.ldw(l), epi);
             drain();
         }
         if (pt == 0) NET_STAMP(10, __builtin_amdgcn_s_memtime());
         if (dx0) {
             // du[s][m][i] = sum_j G_0[m][j] W_0[j][i] for the tile's pseudopoint rows
-            const int din = a.din[0], dout = a.dout[0];
+            const int din = g.din(0), dout = g.dout(0);
             auto epi = [&](int m, int i, floatx4 v, int rot) {
                 if (i < din) {
 #pragma unroll
@@ -799,7 +1023,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                     }
                 }
             };
-            row_gemm<true, false>(din, dout, gbuf(0) + r0 * gld(0), gld(0), sm + a.lw[0], a.ldw[0], epi);
+            row_gemm<true, false>(din, dout, gbuf(0) + r0 * gld(0), gld(0), sm + g.lw(0), g.ldw(0), epi);
         }
     }
     __syncthreads();  // every tile's rows of X_l and G_l
@@ -819,7 +1043,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
             // chunked; net_slot_sum_kernel adds the slots in chunk order)
             float* dst = (a.gslot ? a.gslot + (int64_t)blockIdx.z * a.gsz : a.gsend) +
                          fc_addr(a, nsrc, srct, l, o, s);
-            if (first) *dst = v;
+            if (first || kCarry) *dst = v;
             else *dst += v;  // a looped chunk: this lane wrote the element before
         }
     };
@@ -828,25 +1052,34 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     const float ckv = (a.outer == 2 && blockIdx.z == 0 && first) ? a.ck[s] * a.inv_s0sq : 0.f;
     if (bwd) {
         int first = 0;
-        for (int l = own_hi - 1; l >= own_lo; --l) {
+#pragma unroll kUL
+        for (int l = L - 1; l >= 0; --l) {
+            if (l >= own_hi || l < own_lo) continue;  // (uniform: the role)
             // dW_l[j][i] = sum_m G_l[m][j] X_l[m][i]: both operands k(=m)-strided
-            const int din = a.din[l], dout = a.dout[l];
-            const float* Wl = sm + a.lw[l];
-            const int ldw = a.ldw[l];
+            const int din = g.din(l), dout = g.dout(l);
+            const float* Wl = sm + g.lw(l);
+            const int ldw = g.ldw(l);
             auto epi = [&](int j0, int i, floatx4 v, int rot) {
                 if (i < din) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int j = j0 + ((r + rot) & 3);
                         if (j < dout) {
-                            float g = v[r];
-                            if (a.outer == 2) g -= ckv * Wl[j * ldw + i];
-                            emit(l, j * din + i, g);
+                            float gv = v[r];
+                            if (a.outer == 2) gv -= ckv * Wl[j * ldw + i];
+                            emit(l, j * din + i, gv);
                         }
                     }
                 }
             };
-            mfma_gemm<false, false>(dout, din, Mp, first, gbuf(l), gld(l), sm + a.lx[l], a.ldx[l], epi);
+            if constexpr (kCarry) {
+                const int cm = nloop == 1 ? 0 : ch == 0 ? 1 : ch + 1 < nloop ? 3 : 2;
+                mfma_gemm_carry<kWcUnits>(dout, din, Mp, first, gbuf(l), gld(l), sm + g.lx(l),
+                                          g.ldx(l), epi, wc[l], cm);
+            } else {
+                mfma_gemm<false, false>(dout, din, Mp, first, gbuf(l), gld(l), sm + g.lx(l),
+                                        g.ldx(l), epi);
+            }
             first += gemm_units(dout, din);
         }
         // bias gradients: column sums of G_l over the chunk.  A wave takes
@@ -855,8 +1088,10 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         // GEMM's conflict-free ds_read_b128 pattern), then DPP row sums over i16.
         const int i16 = lane & 15, k4 = lane >> 4;
         int qb = 0;
-        for (int l = own_hi - 1; l >= own_lo; --l) {
-            const int din = a.din[l], dout = a.dout[l];
+#pragma unroll kUL
+        for (int l = L - 1; l >= 0; --l) {
+            if (l >= own_hi || l < own_lo) continue;  // (uniform: the role)
+            const int din = g.din(l), dout = g.dout(l);
             const float* G = gbuf(l);
             const int ldg = gld(l);
             const int nq = (dout + 15) >> 4;
@@ -873,9 +1108,21 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                 if (i16 < 4 && j0 + i16 < dout) {
                     const int j = j0 + i16;
                     float b = i16 == 0 ? s0 : i16 == 1 ? s1 : i16 == 2 ? s2 : s3;
-                    if (a.outer == 2) b -= ckv * sm[a.lb[l] + j];
-                    emit(l, dout * din + j, b);
+                    if (a.outer == 2) b -= ckv * sm[g.lb(l) + j];
+                    if constexpr (kCarry) {
+                        // (a wave holds at most one column tile of a layer: nq <= waves)
+                        if (nloop > 1 && ch == 0) {
+                            bc[l] = b;
+                        } else if (ch + 1 < nloop) {
+                            bc[l] += b;
+                        } else {
+                            emit(l, dout * din + j, nloop > 1 ? bc[l] + b : b);
+                        }
+                    } else {
+                        emit(l, dout * din + j, b);
+                    }
                 }
+                if constexpr (kCarry) break;  // one column tile per wave (fixed shapes)
             }
             qb += nq;
         }
@@ -890,7 +1137,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     }
     NET_STAMP(3, __builtin_amdgcn_s_memtime());
     if (role == 0 && a.outer == 0) {  // the chunk's weighted NLL (role 1 computed the same)
-        const float tot = block_sum(part, sm + a.lred);
+        const float tot = block_sum(part, sm + g.lred());
         if (tid == 0) atomicAdd(a.nll_out, (double)tot);
     }
     if (a.rn_out) {
@@ -918,84 +1165,42 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
 }
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
-static inline int ld8o(int x) { return x + (24 - x % 16) % 16; }  // >= x, == 8 (mod 16)
 
 // LDS floats for a chunk of `mc` pseudopoints (layout and padding contract
-// in the header comment); fills the carve into `a` when given.  Row strides
-// are 4 x odd: a 16-lane float4 read along k (rows i16 = 0..15) and a 64-lane
-// float read down k (lanes 16 k4 + i16, rows 4 k4 apart) both hit distinct
-// banks.  Regions read before the forward pass come first; the full-cov x
-// stage overlaps the rest.
+// in the header comment); fills the carve into `a` when given.  The full-cov
+// x stage bookkeeping (source blocks) is added here; the carve itself is
+// net_carve's, the same function the fixed-geometry kernels evaluate at
+// compile time.
 static size_t net_lds_floats(const psvi_plan& p, int mc, NetArgs* a) {
-    size_t off = 0;
-    int ns = 0;
-    auto take = [&](size_t nfl) {
-        const size_t o = off;
-        off += (nfl + 3) & ~size_t(3);
-        if (a) a->slack[ns] = (int)off;
-        ++ns;
-        off += 64;
-        return (int)o;
-    };
-    const int Mp = rup(mc, 16);
+    NetDims d{};
+    d.L = p.L;
     for (int l = 0; l < p.L; ++l) {
-        const int din = p.lay[l].din, dout = p.lay[l].dout;
-        const int ldw = ld8o(rup(din, 16));
-        const int lw = take((size_t)rup(dout, 16) * ldw), lb = take(dout);
-        if (a) { a->lw[l] = lw; a->ldw[l] = ldw; a->lb[l] = lb; }
-        if (l > 0) {  // W^T: rows i < din (16-multiple), columns j < dout (16-multiple)
-            const int ldwt = ld8o(rup(dout, 16));
-            const int lwt = take((size_t)rup(din, 16) * ldwt);
-            if (a) { a->lwt[l] = lwt; a->ldwt[l] = ldwt; }
-        } else if (a) {
-            a->lwt[0] = lw;  // unused (no propagation below layer 0)
-            a->ldwt[0] = ldw;
-        }
+        d.din[l] = p.lay[l].din;
+        d.dout[l] = p.lay[l].dout;
     }
-    const int ldx0 = ld8o(p.lay[0].din);
-    const int lx0 = take((size_t)Mp * ldx0);
-    const int lred = take(16);
-    const int lzw = take(2 * (size_t)Mp);
-    const int lstamp = take(48);  // 16 x uint64 diagnostics stamps + 8 wave starts
-    // per-workgroup tables (world > 1): every band's int64 g_send offset
-    // (8-byte aligned), the x row's per-source int64 bases and int starts,
-    // the layers' first band index
     const int nbands = (p.family == PSVI_FAMILY_FULLCOV && p.world > 1) ? p.band_base[p.L] : 0;
-    const int lsrc = take(2 * (size_t)nbands + 3 * kMaxWorld + kMaxL + 2 * kMaxWorld + 1);
-    const int ns_early = ns;
-    for (int l = 1; l < p.L; ++l) {
-        const int ldx = ld8o(p.lay[l].din);
-        const int lx = take((size_t)Mp * ldx);
-        if (a) { a->lx[l] = lx; a->ldx[l] = ldx; }
-    }
-    // G_l (l < L - 1, the gradient of layer l's output, stride of X_{l+1}):
-    // every one stays until the weight-gradient phase
-    for (int l = 0; l + 1 < p.L; ++l) {
-        const int lgl = take((size_t)Mp * ld8o(p.lay[l + 1].din));
-        if (a) a->lg[l] = lgl;
-    }
-    const int lddl = ld8o(p.lay[p.L - 1].dout);
-    const int ldl = take((size_t)Mp * lddl);
-    if (p.family == PSVI_FAMILY_FULLCOV && a) {  // the x row's source blocks (no LDS)
-        int st = 0;
-        for (int q = 0; q < p.world; ++q) {
-            a->stage_off[q] = st;
-            st += p.rows_tot[q];
-        }
-        a->stage_off[p.world] = st;
-        a->stage_len = st;
-    }
-    off = (off + 3) & ~size_t(3);
+    const NetCarve c = net_carve(d, mc, nbands);
     if (a) {
-        a->lx[0] = lx0; a->ldx[0] = ldx0;
-        a->ldl = ldl; a->lddl = lddl;
-        a->lred = lred; a->lsrc = lsrc; a->lzw = lzw; a->lstamp = lstamp;
-        a->Mp = Mp;
-        a->nslack = ns;
-        a->nslack_early = ns_early;
-        a->lds_f4 = (int)(off / 4);
+        for (int l = 0; l < kMaxL; ++l) {
+            a->lw[l] = c.lw[l]; a->ldw[l] = c.ldw[l]; a->lb[l] = c.lb[l];
+            a->lx[l] = c.lx[l]; a->ldx[l] = c.ldx[l]; a->lwt[l] = c.lwt[l];
+            a->ldwt[l] = c.ldwt[l]; a->lg[l] = c.lg[l];
+        }
+        for (int k = 0; k < kNetSlack; ++k) a->slack[k] = c.slack[k];
+        a->ldl = c.ldl; a->lddl = c.lddl; a->lred = c.lred; a->lsrc = c.lsrc;
+        a->lzw = c.lzw; a->lstamp = c.lstamp; a->Mp = c.Mp;
+        a->nslack = c.nslack; a->nslack_early = c.nslack_early; a->lds_f4 = c.lds_f4;
+        if (p.family == PSVI_FAMILY_FULLCOV) {  // the x row's source blocks (no LDS)
+            int st = 0;
+            for (int q = 0; q < p.world; ++q) {
+                a->stage_off[q] = st;
+                st += p.rows_tot[q];
+            }
+            a->stage_off[p.world] = st;
+            a->stage_len = st;
+        }
     }
-    return off;
+    return (size_t)c.lds_f4 * 4;
 }
 
 // g_send = the pseudopoint chunks' dW slots added in chunk order (run-to-run
@@ -1090,6 +1295,7 @@ void net_xmap(const psvi_plan& p, std::vector<uint32_t>& xmap, std::vector<NetBa
 int g_net_ablation = 0;  // psvi_debug_set(PSVI_DBG_NET_ABLATION, mask)
 int g_net_mloop_off = 0;  // psvi_debug_set(PSVI_DBG_NET_MLOOP_OFF, 1): a workgroup per pseudopoint chunk + slots (A/B)
 int g_net_scalar_loads = 0;  // psvi_debug_set(PSVI_DBG_NET_SCALAR_LOADS, 1): the scalar load path (A/B)
+int g_net_geo_off = 0;  // psvi_debug_set(PSVI_DBG_NET_GEO_OFF, 1): the run-time geometry for fn2 too (A/B)
 unsigned long long* g_net_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_NET_STAMPS, buf)
 
 void net_set_lds_limit() {
@@ -1108,6 +1314,24 @@ void net_set_lds_limit() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true, true, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false, true, false, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true, true, false, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, false, true, true, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)net_kernel<PSVI_FAMILY_FULLCOV, true, true, true, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+// The fixed fn2 geometry (NetGeo<1 / 2>) applies: the 64 -> 40 -> 40 -> 2
+// full-cov stack with 100-row pseudopoint chunks (Mp = 112), float4 loads;
+// the run-time carve then equals the compile-time one (the same net_carve)
+static bool net_fn2_geo(const psvi_plan& p) {
+    if (g_net_geo_off || p.family != PSVI_FAMILY_FULLCOV || p.L != kFn2Dims.L) return false;
+    for (int l = 0; l < p.L; ++l)
+        if (p.lay[l].din != kFn2Dims.din[l] || p.lay[l].dout != kFn2Dims.dout[l]) return false;
+    return net_rup(p.mc, 16) == kFn2Mp && p.net_threads == 512;
 }
 
 // float4 loads of the full-cov x row: u rows of D % 4 == 0 floats, and every
@@ -1203,8 +1427,18 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         return rn_out && rn_n > 0 ? launch_randn(rn_out, rn_n, rn_seed, rn_off, st, nullptr, 0,
                                                  rn_planes ? &p.eps_planes : nullptr, rn_planes)
                                   : hipSuccess;
+    const bool fn2 = net_vec_ok(p) && net_fn2_geo(p);
+    if (fn2 && p.world > 1 && a.nbands != kFn2Bands) return hipErrorInvalidValue;
     if (p.family == PSVI_FAMILY_MEANFIELD)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_MEANFIELD, false>), grid, block, p.net_lds, st, a);
+    else if (fn2 && loop && p.world > 1)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true, true, true, 2>), grid, block, p.net_lds, st, a);
+    else if (fn2 && loop)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false, true, true, 1>), grid, block, p.net_lds, st, a);
+    else if (fn2 && p.world > 1)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true, true, false, 2>), grid, block, p.net_lds, st, a);
+    else if (fn2)
+        hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false, true, false, 1>), grid, block, p.net_lds, st, a);
     else if (loop && p.world > 1)
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, true, true, true>), grid, block, p.net_lds, st, a);
     else if (loop)

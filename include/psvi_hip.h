@@ -536,6 +536,9 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     instead of the matrix-core one; 2 = the
                                     matrix-core one with a row of up to three
                                     column tiles per wave unit (A/B)           */
+#define PSVI_DBG_NET_GEO_OFF 30      /* value: 1 = the network kernel's run-time
+                                    geometry for the fn2 64-40-40-2 stack too,
+                                    instead of its compile-time one (A/B)      */
 /* mean device microseconds of the recorded windows: out[0] network kernel,
    out[1] update (+ its slot reduce), out[2] windows; synchronizes on them and
    drops the records */
