@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "psvi_diag.h"
 #include "psvi_internal.hpp"
 
 namespace psvi {
@@ -29,10 +30,7 @@ extern int g_ks_off;                     // kernels_mvn.hip
 extern int g_fs_off;                     // kernels_mvn.hip
 extern int g_fs_bf_off;                  // kernels_mvn.hip
 extern int g_ks_bf_off;                  // kernels_mvn.hip
-extern int g_stream_bf2_off;              // kernels_mvn.hip
 static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
-extern int g_lenet_gemm_valu;            // kernels_lenet.hip
-extern int g_lenet_conv_valu;            // kernels_lenet.hip
 extern int g_lenet_abl;                  // kernels_lenet.hip
 extern int g_net_split_below;            // kernels_net.hip
 extern int g_net_threads;                // kernels_net.hip
@@ -624,15 +622,12 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
         case PSVI_DBG_FWD_SEG_BF_OFF: g_fs_bf_off = value; return 0;
         case PSVI_DBG_KSTREAM_BF_OFF: g_ks_bf_off = value; return 0;
-        case PSVI_DBG_STREAM_BF2_OFF: g_stream_bf2_off = value; return 0;
         case PSVI_DBG_ROP_VALU: g_rop_valu = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
         case PSVI_DBG_NET_MLOOP_OFF: g_net_mloop_off = value; return 0;
         case PSVI_DBG_NET_GEO_OFF: g_net_geo_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
-        case PSVI_DBG_LENET_GEMM_VALU: g_lenet_gemm_valu = value; return 0;
-        case PSVI_DBG_LENET_CONV_VALU: g_lenet_conv_valu = value; return 0;
         case PSVI_DBG_LENET_ABLATION: g_lenet_abl = value; return 0;
         case PSVI_DBG_NET_THREADS:
             if (value != 0 && value != 256 && value != 512) return fail(PSVI_EINVAL, "256 or 512");

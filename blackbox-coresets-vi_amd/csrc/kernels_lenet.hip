@@ -26,9 +26,7 @@
 
 namespace psvi {
 
-int g_lenet_gemm_valu = 0;  // psvi_debug_set(PSVI_DBG_LENET_GEMM_VALU, 1): the VALU head GEMM (A/B)
-int g_lenet_conv_valu = 0;
-int g_lenet_abl = 0;        // psvi_debug_set(PSVI_DBG_LENET_ABLATION, mask): backward parts skipped  // psvi_debug_set(PSVI_DBG_LENET_CONV_VALU, 1): the VALU conv towers (A/B)
+int g_lenet_abl = 0;        // psvi_debug_set(PSVI_DBG_LENET_ABLATION, mask): backward parts skipped
 
 namespace {
 
@@ -165,103 +163,6 @@ __device__ __forceinline__ float relu_pool4(float a0, float a1, float a2, float 
 // LDS while the chunk's images stream through.  320 threads (5 waves): the
 // bwd kernel's 294 transposed-conv blocks fit in one pass.
 constexpr int kConvThreads = 320;
-
-// LDS planes of the forward split by column parity: a 2x2-pool window's
-// patch starts at an even column, so adjacent lanes read 2 columns apart --
-// 2-3-way ds_read_b32 bank conflicts in one 32-bank group.  With the even and
-// odd columns in separate planes, lanes read consecutive words; the row
-// strides put a wave's 3 (conv1) or 5 (conv2) patch rows on disjoint banks.
-constexpr int kInH = 23;   // padded image: 32 rows x 16 half-columns, stride 23
-constexpr int kInP = 32 * kInH;
-constexpr int kP1H = 13;   // pooled conv1 map: 6 x 14 rows x 7 half-columns, stride 13
-constexpr int kP1P = 6 * 14 * kP1H;
-
-__global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_kernel(ConvArgs a) {
-    __shared__ float w1[150], b1[6], w2[2400], b2[16];
-    __shared__ float in[2 * kInP];      // 28x28 image, zero padding 2, [parity][y][x / 2]
-    __shared__ float p1[2 * kP1P];      // [parity][c][y][x / 2]
-    const int tid = threadIdx.x, s = blockIdx.y;
-    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    for (int i = tid; i < kNConv; i += kConvThreads) {
-        const float v = ws[i];
-        if (i < 150) w1[i] = v;
-        else if (i < 156) b1[i - 150] = v;
-        else if (i < 2556) w2[i - 156] = v;
-        else b2[i - 2556] = v;
-    }
-    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
-    for (int m = m0; m < m1; ++m) {
-        __syncthreads();
-        const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kConvThreads) {
-            const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[(i & 1) * kInP + (i >> 5) * kInH + ((i & 31) >> 1)] =
-                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
-        }
-        __syncthreads();
-        const int64_t row = (int64_t)s * a.M + m;
-        // conv1 (1 -> 6, 5x5, pad 2) + relu + pool: one pooled output (its 2x2
-        // conv window from a 6x6 patch in registers) per item
-        for (int o = tid; o < kP1; o += kConvThreads) {
-            const int c = o / 196, py = (o % 196) / 14, px = o % 14;
-            float patch[6][6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int j = 0; j < 6; ++j)
-                    patch[i][j] = in[(j & 1) * kInP + (2 * py + i) * kInH + px + (j >> 1)];
-            float acc[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = b1[c];
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    const float wv = w1[c * 25 + i * 5 + j];
-                    acc[0] += wv * patch[i][j];
-                    acc[1] += wv * patch[i][j + 1];
-                    acc[2] += wv * patch[i + 1][j];
-                    acc[3] += wv * patch[i + 1][j + 1];
-                }
-            int8_t r;
-            const float v = relu_pool4(acc[0], acc[1], acc[2], acc[3], r);
-            p1[(px & 1) * kP1P + (c * 14 + py) * kP1H + (px >> 1)] = v;
-            a.p1[row * kP1 + o] = v;
-            a.r1[row * kP1 + o] = r;
-        }
-        __syncthreads();
-        // conv2 (6 -> 16, 5x5) + relu + pool, same blocking per input channel
-        for (int o = tid; o < kX2; o += kConvThreads) {
-            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
-            float acc[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = b2[k];
-            for (int c = 0; c < 6; ++c) {
-                const float* pc = p1 + (c * 14 + 2 * py) * kP1H + px;
-                const float* wk = w2 + k * 150 + c * 25;
-                float patch[6][6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i)
-#pragma unroll
-                    for (int j = 0; j < 6; ++j) patch[i][j] = pc[(j & 1) * kP1P + i * kP1H + (j >> 1)];
-#pragma unroll
-                for (int i = 0; i < 5; ++i)
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) {
-                        const float wv = wk[i * 5 + j];
-                        acc[0] += wv * patch[i][j];
-                        acc[1] += wv * patch[i][j + 1];
-                        acc[2] += wv * patch[i + 1][j];
-                        acc[3] += wv * patch[i + 1][j + 1];
-                    }
-            }
-            int8_t r;
-            const float v = relu_pool4(acc[0], acc[1], acc[2], acc[3], r);
-            a.x2[row * kX2 + o] = v;
-            a.r2[row * kX2 + o] = r;
-        }
-    }
-}
 
 // ------------------------------------- conv towers, fwd, on the matrix cores
 // Both convolutions as implicit GEMMs on v_mfma_f32_16x16x4_f32 (fp32 in,
@@ -497,235 +398,17 @@ __global__ __launch_bounds__(64) void lenet_conv2_mfma_kernel(ConvArgs a) {
 // route through pool1/relu, accumulate conv1's weight gradient against the
 // padded image.  Per-(s, chunk) partial sums, reduced over chunks in fixed
 // order by lenet_conv_reduce_kernel: bitwise run-to-run reproducible.
-constexpr int kDA = 18;  // routed conv2 gradient plane, 10x10 plus a 4-wide zero border
-// The backward's LDS planes, laid out against ds_read_b32 bank conflicts (32
-// banks per 32-lane group): the routed conv2 plane split by column parity
-// (lanes read 2 columns apart) with 10-word rows, so the 5 patch rows of a
-// half-wave land on (nearly) disjoint banks; the padded image with 37-word
-// rows, so the 25 taps (i, j) of one conv1 weight row block sit on 25 banks.
-constexpr int kDAH = 10;              // half-columns per row of a parity plane
-constexpr int kDAK = kDA * kDAH;      // one output channel's parity plane
-constexpr int kDAP = 16 * kDAK;       // one parity plane (16 channels)
+// The backward's LDS layouts, against ds_read_b32 bank conflicts: the padded
+// image with 37-word rows, so the 25 taps (i, j) of one conv1 weight row
+// block sit on 25 banks.
 constexpr int kBS = 37;               // padded-image row stride in the backward
 // the pooled conv1 map P1 likewise: 37-word rows, channel planes 537 words
 // apart, so the 25 taps of a conv2 weight block and the next channel's first
 // taps fall on distinct banks
 constexpr int kP1S = 37, kP1C = 14 * kP1S + 19;
-__device__ __forceinline__ int da2_at(int k, int y, int x) {  // bordered (y, x)
-    return (x & 1) * kDAP + k * kDAK + y * kDAH + (x >> 1);
-}
-
 // DU (outer backward): also d u = the transposed conv1 of the routed conv1
 // gradient (dense, zero-bordered LDS plane, 2x2 pixel blocks per thread) for
 // the pseudopoint rows m < n_pseudo.
-constexpr int kW1Groups = 8;  // conv1 weight-gradient position groups (backward)
-template <bool DU>
-__global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a) {
-    __shared__ float w1[DU ? 150 : 1];
-    __shared__ float da1[DU ? 6 * 1024 : 1];  // routed conv1 gradient, 28x28 + 2-wide zero border
-    __shared__ float w2[2400];
-    __shared__ float in[32 * kBS];
-    __shared__ float p1[6 * kP1C];   // [c][y * kP1S + x]
-    __shared__ float g2[kX2];        // routed gradient of each pooled conv2 output
-    __shared__ int off2[kX2];        // its conv2 position y * kP1S + x (P1 plane offset)
-    __shared__ float da2[2 * kDAP];  // [parity][k][y][x / 2]
-    __shared__ float g1[kP1];        // routed gradient of each pooled conv1 output
-    __shared__ int off1[kP1];        // its conv1 position y * kBS + x (padded image)
-    __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
-    const int tid = threadIdx.x, s = blockIdx.y;
-    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
-    for (int i = tid; i < 2 * kDAP; i += kConvThreads) da2[i] = 0.f;
-    if (DU) {
-        for (int i = tid; i < 150; i += kConvThreads) w1[i] = ws[i];
-        for (int i = tid; i < 6 * 1024; i += kConvThreads) da1[i] = 0.f;
-    }
-    // conv2 weight entries owned by this thread: output channel k2 = tid / 15
-    // (threads < 240), entries (k2, c, i, j) with c * 25 + i * 5 + j = t15 + 15 r.
-    // One output channel per thread: each routed gradient and offset is read
-    // once per 10 MACs (was: three LDS reads per MAC).
-    constexpr int kR2 = 10;
-    const bool own2 = tid < 240;
-    const int k2 = min(tid / 15, 15), t15 = tid % 15;
-    int pb[kR2];
-#pragma unroll
-    for (int r = 0; r < kR2; ++r) {
-        const int e = t15 + 15 * r;
-        pb[r] = (e / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
-    }
-    float accw2[kR2];
-#pragma unroll
-    for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
-    // conv1: thread t < 240 owns the five weights (c1, i1, 0..4) over the
-    // routed positions of p group pg1 (c1 = t / 40, i1 = t / 8 % 5, pg1 = t % 8);
-    // threads 240 .. 287 the bias c1 over group pg1.  The g1 / off1 read of a
-    // position serves five MACs; the 8 group partials are added in group order.
-    const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
-    const int t1 = w1own ? tid : tid - 240;
-    const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
-    const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
-    float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
-    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
-    for (int m = m0; m < m1; ++m) {
-        __syncthreads();
-        const int64_t row = (int64_t)s * a.M + m;
-        const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kConvThreads) {
-            const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[(i >> 5) * kBS + (i & 31)] =
-                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
-        }
-        for (int i = tid; i < kP1; i += kConvThreads)
-            p1[(i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14] = a.p1[row * kP1 + i];
-        for (int o = tid; o < kX2; o += kConvThreads) {
-            const int r = a.r2[row * kX2 + o];
-            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
-            const int rr = r >= 0 ? r : 0;
-            const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
-            const float g = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
-            g2[o] = g;
-            off2[o] = y * kP1S + x;
-            if (r >= 0) da2[da2_at(k, y + 4, x + 4)] = g;
-        }
-        __syncthreads();
-        // conv2 weight gradient: dW2[k][c][i][j] += sum_p g2[k][p] P1[c][y_p + i][x_p + j]
-        // (per image: acc over p = 0..24 from zero, then into accw2, the order
-        // of the per-entry form; p outer so that g2 / off2 are read once per p)
-        if (own2) {
-            float acc[kR2];
-#pragma unroll
-            for (int r = 0; r < kR2; ++r) acc[r] = 0.f;
-#pragma unroll
-            for (int p = 0; p < 25; ++p) {
-                const float gv = g2[k2 * 25 + p];
-                const int op = off2[k2 * 25 + p];
-#pragma unroll
-                for (int r = 0; r < kR2; ++r) acc[r] += gv * p1[pb[r] + op];
-            }
-#pragma unroll
-            for (int r = 0; r < kR2; ++r) accw2[r] += acc[r];
-        }
-        if (tid < 16) {
-            float acc = 0.f;
-            for (int p = 0; p < 25; ++p) acc += g2[tid * 25 + p];
-            accb2 += acc;
-        }
-        // d P1 (transposed conv, 2x2 output blocks), routed through pool1 / relu
-        if (tid < 294) {
-            const int c = tid / 49, yy = 2 * ((tid % 49) / 7), xx = 2 * (tid % 7);
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int k = 0; k < 16; ++k) {
-                const float* q = da2 + k * kDAK + yy * kDAH + (xx >> 1);
-                float Q[6][6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i)
-#pragma unroll
-                    for (int j = 0; j < 6; ++j) Q[i][j] = q[(j & 1) * kDAP + i * kDAH + (j >> 1)];
-                const float* wk = w2 + k * 150 + c * 25;
-#pragma unroll
-                for (int i = 0; i < 5; ++i)
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) {
-                        const float wv = wk[i * 5 + j];
-                        acc[0] += wv * Q[4 - i][4 - j];
-                        acc[1] += wv * Q[4 - i][5 - j];
-                        acc[2] += wv * Q[5 - i][4 - j];
-                        acc[3] += wv * Q[5 - i][5 - j];
-                    }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int yq = yy + (q >> 1), xq = xx + (q & 1);
-                const int o = c * 196 + yq * 14 + xq;
-                const int r = a.r1[row * kP1 + o];
-                const int rr = r >= 0 ? r : 0;
-                g1[o] = r >= 0 ? acc[q] : 0.f;
-                off1[o] = (2 * yq + (rr >> 1)) * kBS + 2 * xq + (rr & 1);
-            }
-        }
-        __syncthreads();
-        // clear the routed entries of the dense plane for the next image
-        for (int o = tid; o < kX2; o += kConvThreads) {
-            const int k = o / 25, q = off2[o];
-            da2[da2_at(k, q / kP1S + 4, q % kP1S + 4)] = 0.f;
-        }
-        // conv1 weight gradient: dW1[c][i][j] += sum_p g1[c][p] in[y_p + i][x_p + j]
-        if (w1own) {
-            float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 5
-            for (int p = pl1; p < ph1; ++p) {
-                const float gv = g1[c1 * 196 + p];
-                const float* ip = in + off1[c1 * 196 + p] + i1 * kBS;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) acc[j] += gv * ip[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 5; ++j) acc1[j] += acc[j];
-        } else if (b1own) {
-            float acc = 0.f;
-#pragma unroll 5
-            for (int p = pl1; p < ph1; ++p) acc += g1[c1 * 196 + p];
-            acc1[0] += acc;
-        }
-        if (DU && m < a.n_pseudo) {
-            for (int o = tid; o < kP1; o += kConvThreads)
-                da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = g1[o];
-            __syncthreads();
-            if (tid < 196) {
-                const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
-                float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-                for (int c = 0; c < 6; ++c) {
-                    const float* q = da1 + c * 1024 + yy * 32 + xx;
-                    float Q[6][6];
-#pragma unroll
-                    for (int i = 0; i < 6; ++i)
-#pragma unroll
-                        for (int j = 0; j < 6; ++j) Q[i][j] = q[i * 32 + j];
-#pragma unroll
-                    for (int i = 0; i < 5; ++i)
-#pragma unroll
-                        for (int j = 0; j < 5; ++j) {
-                            const float wv = w1[c * 25 + i * 5 + j];
-                            acc[0] += wv * Q[4 - i][4 - j];
-                            acc[1] += wv * Q[4 - i][5 - j];
-                            acc[2] += wv * Q[5 - i][4 - j];
-                            acc[3] += wv * Q[5 - i][5 - j];
-                        }
-                }
-                float* out = a.du + ((int64_t)s * a.n_pseudo + m) * 784 + yy * 28 + xx;
-                out[0] = acc[0];
-                out[1] = acc[1];
-                out[28] = acc[2];
-                out[29] = acc[3];
-            }
-            __syncthreads();
-            for (int o = tid; o < kP1; o += kConvThreads)
-                da1[(o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2] = 0.f;
-        }
-    }
-    __syncthreads();
-    if (w1own) {
-#pragma unroll
-        for (int j = 0; j < 5; ++j) red[pg1 * 156 + c1 * 25 + i1 * 5 + j] = acc1[j];
-    } else if (b1own) {
-        red[pg1 * 156 + 150 + c1] = acc1[0];
-    }
-    __syncthreads();
-    float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
-    if (tid < 156) {
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < kW1Groups; ++q) t += red[q * 156 + tid];
-        out[tid] = t;
-    }
-    if (tid < 16) out[2556 + tid] = accb2;
-    if (own2) {
-#pragma unroll
-        for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
-    }
-}
-
 // The same backward with d P1 on the matrix cores.  Each pool2 window w
 // (5x5 per channel) routes its gradient g2[k][w] to ONE of its four conv2
 // positions q = 2 dy + dx, so the transposed conv2 of the routed map is, per
@@ -737,7 +420,8 @@ __global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_kernel(ConvArgs a
 // row tiles, 14 column tiles dealt to the 5 waves, k-step = output channel
 // k, lane group = q); then d P1[c][y][x] = the sum, in window order, of the
 // (<= 9) patches covering (y, x) (stride 2: window (wy, wx) covers rows
-// 2 wy .. 2 wy + 5).  Everything else as lenet_conv_bwd_kernel.
+// 2 wy .. 2 wy + 5).  Per (image chunk, sample) partials as the other conv
+// kernels (fixed-order chunk sums).
 constexpr int kUS = 217;  // LDS row stride of U (216 patch columns)
 constexpr int kGK = 33, kGQ = 16 * kGK;  // routed-map rows / offset planes (ga below)
 template <bool DU>
@@ -1163,10 +847,9 @@ __global__ __launch_bounds__(kThreads) void lenet_conv_reduce_kernel(int S_loc, 
 
 // ---------------------------------------------------------- head GEMMs
 // C[b](m, n) = sum_k A[b](m, k) B[b](k, n) with arbitrary element strides,
-// 64x64 tiles, k-steps of 16 through LDS, 4x4 outputs per thread (fp32 VALU:
-// the head is 1/7 of the step's flops).  Epilogue flags, in order: 8 add the
+// on the matrix cores (the head is 1/7 of the step's flops).  Epilogue flags, in order: 8 add the
 // existing C (a second product of a tangent), 1 add bias[b][n], 2 relu, 4
-// multiply by (mask[b](m, n) > 0) (relu's backward).
+// multiply by (mask[b](m, n) > 0) (relu's backward).  GemmArgs:
 struct GemmArgs {
     int M, N, K;
     const float* A; int64_t sAb; int sAm, sAk;
@@ -1177,74 +860,13 @@ struct GemmArgs {
     const float* mask; int64_t sMb; int sMm;
 };
 
-__global__ __launch_bounds__(kThreads) void lenet_gemm_kernel(GemmArgs g) {
-    __shared__ float As[16][64 + 4];
-    __shared__ float Bs[16][64 + 4];
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-    const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64, b = blockIdx.z;
-    const float* A = g.A + b * g.sAb;
-    const float* B = g.B + b * g.sBb;
-    float acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-    const bool a_kfast = g.sAk == 1, b_nfast = g.sBn == 1;
-    for (int k0 = 0; k0 < g.K; k0 += 16) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int e = tid + r * kThreads;
-            int mm, kk;
-            if (a_kfast) { kk = e & 15; mm = e >> 4; } else { mm = e & 63; kk = e >> 6; }
-            const int gm = m0 + mm, gk = k0 + kk;
-            As[kk][mm] = (gm < g.M && gk < g.K) ? A[(int64_t)gm * g.sAm + (int64_t)gk * g.sAk] : 0.f;
-            int nn, kb;
-            if (b_nfast) { nn = e & 63; kb = e >> 6; } else { kb = e & 15; nn = e >> 4; }
-            const int gn = n0 + nn, gkb = k0 + kb;
-            Bs[kb][nn] = (gn < g.N && gkb < g.K) ? B[(int64_t)gkb * g.sBk + (int64_t)gn * g.sBn] : 0.f;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-            float av[4], bv[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) av[i] = As[kk][ty * 4 + i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tx * 4 + j];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
-        }
-        __syncthreads();
-    }
-    float* C = g.C + b * g.sCb;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = m0 + ty * 4 + i;
-        if (m >= g.M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + tx * 4 + j;
-            if (n >= g.N) continue;
-            float v = acc[i][j];
-            if (g.epi & 8) v += C[(int64_t)m * g.sCm + n];  // accumulate onto C
-            if (g.epi & 1) v += g.bias[b * g.sbias + n];
-            if (g.epi & 2) v = fmaxf(v, 0.f);
-            if (g.epi & 4) v = g.mask[b * g.sMb + (int64_t)m * g.sMm + n] > 0.f ? v : 0.f;
-            C[(int64_t)m * g.sCm + n] = v;
-        }
-    }
-}
-
-// The same batched GEMM on the matrix cores: 64x64 tiles, four waves of one
-// 32x32 v_mfma_f32_32x32x2_f32 accumulator each, k-steps of 16 staged through
+// 64x64 tiles, four waves of one 32x32 v_mfma_f32_32x32x2_f32 accumulator each, k-steps of 16 staged through
 // two LDS buffers (the next step's operands are loaded into registers before
 // this step's MFMAs and written to the other buffer after them: one barrier
 // per step).  Operand reads: lane l takes A(m0 + 32 wr + l % 32, k + l / 32)
 // and B(k + l / 32, n0 + 32 wc + l % 32) -- 68-word LDS rows, conflict free.
 // Accumulator element q of lane l is C(32 wr + 8 (q / 4) + 4 (l / 32) + q % 4,
-// 32 wc + l % 32).  Same epilogue flags as lenet_gemm_kernel.
+// 32 wc + l % 32).
 typedef float gemm_f32x16 __attribute__((ext_vector_type(16)));
 __global__ __launch_bounds__(kThreads) void lenet_gemm_mfma_kernel(GemmArgs g) {
     __shared__ float As[2][16][68];
@@ -1458,67 +1080,6 @@ struct TanArgs {
     float* g1g;          // MFMA bwd out: [S][M][1176] routed d P1_dot
 };
 
-// tangent forward of the conv towers: only the routed conv positions matter
-__global__ __launch_bounds__(kConvThreads) void lenet_conv_fwd_tan_kernel(TanArgs a) {
-    __shared__ float w2[2400], wd[kNConv];
-    __shared__ float in[32 * 32];
-    __shared__ float p1[kP1], p1d[kP1];
-    const int tid = threadIdx.x, s = blockIdx.y;
-    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    const float* wds = a.wdot + (int64_t)s * a.n_tot;
-    for (int i = tid; i < 2400; i += kConvThreads) w2[i] = ws[156 + i];
-    for (int i = tid; i < kNConv; i += kConvThreads) wd[i] = wds[i];
-    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
-    for (int m = m0; m < m1; ++m) {
-        __syncthreads();
-        const int64_t row = (int64_t)s * a.M + m;
-        const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kConvThreads) {
-            const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[i] = (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
-        }
-        for (int i = tid; i < kP1; i += kConvThreads) p1[i] = a.p1[row * kP1 + i];
-        __syncthreads();
-        for (int o = tid; o < kP1; o += kConvThreads) {
-            const int r = a.r1[row * kP1 + o];
-            float v = 0.f;
-            if (r >= 0) {
-                const int c = o / 196, py = (o % 196) / 14, px = o % 14;
-                const int y = 2 * py + (r >> 1), x = 2 * px + (r & 1);
-                v = wd[150 + c];
-#pragma unroll
-                for (int i = 0; i < 5; ++i)
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) v += wd[c * 25 + i * 5 + j] * in[(y + i) * 32 + x + j];
-            }
-            p1d[o] = v;
-            a.p1d[row * kP1 + o] = v;
-        }
-        __syncthreads();
-        for (int o = tid; o < kX2; o += kConvThreads) {
-            const int r = a.r2[row * kX2 + o];
-            float v = 0.f;
-            if (r >= 0) {
-                const int k = o / 25, py = (o % 25) / 5, px = o % 5;
-                const int y = 2 * py + (r >> 1), x = 2 * px + (r & 1);
-                v = wd[2556 + k];
-                for (int c = 0; c < 6; ++c) {
-                    const float* wk = w2 + k * 150 + c * 25;
-                    const float* wdk = wd + 156 + k * 150 + c * 25;
-                    const int base = c * 196 + y * 14 + x;
-#pragma unroll
-                    for (int i = 0; i < 5; ++i)
-#pragma unroll
-                        for (int j = 0; j < 5; ++j)
-                            v += wk[i * 5 + j] * p1d[base + i * 14 + j] +
-                                 wdk[i * 5 + j] * p1[base + i * 14 + j];
-                }
-            }
-            a.x2d[row * kX2 + o] = v;
-        }
-    }
-}
-
 // tangent of d logits and of each row's NLL:
 //   dd = w (P . l_dot - P (P . l_dot)),  nll_dot = (P - onehot) . l_dot
 __global__ __launch_bounds__(kThreads) void lenet_loss_tan_kernel(int rows, int M,
@@ -1566,221 +1127,6 @@ __device__ __forceinline__ void convT_block(const float* q, int ld, const float*
             acc[2] += wv * Q[5 - i][4 - j];
             acc[3] += wv * Q[5 - i][5 - j];
         }
-}
-
-// convT_block for two weight sets over one patch: acc_a += wa * Q, acc_b += wb * Q
-template <int PAR = 0>
-__device__ __forceinline__ void convT_block2(const float* q, int ld, const float* wa,
-                                             const float* wb, float (&acc_a)[4],
-                                             float (&acc_b)[4]) {
-    float Q[6][6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Q[i][j] = PAR ? q[(j & 1) * PAR + i * ld + (j >> 1)] : q[i * ld + j];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const float va = wa[i * 5 + j], vb = wb[i * 5 + j];
-            acc_a[0] += va * Q[4 - i][4 - j];
-            acc_a[1] += va * Q[4 - i][5 - j];
-            acc_a[2] += va * Q[5 - i][4 - j];
-            acc_a[3] += va * Q[5 - i][5 - j];
-            acc_b[0] += vb * Q[4 - i][4 - j];
-            acc_b[1] += vb * Q[4 - i][5 - j];
-            acc_b[2] += vb * Q[5 - i][4 - j];
-            acc_b[3] += vb * Q[5 - i][5 - j];
-        }
-}
-
-// tangent backward of the conv towers: G_dot for conv2 and conv1, and the
-// tangent of d u (the mixed product d/du) for every row.  One LDS plane
-// region serves the routed conv2 gradients (primal and tangent, 18x18 with a
-// 4-wide border) and then the routed conv1 gradients (32x32 with a 2-wide
-// border); it is re-zeroed per image.
-constexpr int kPlane = 2 * 6 * 1024;  // >= 2 * 2 * kDAP (primal + tangent conv2 planes)
-__global__ __launch_bounds__(kConvThreads) void lenet_conv_bwd_tan_kernel(TanArgs a) {
-    __shared__ float w1[150], wd1[150], w2[2400], wd2[2400];
-    __shared__ float in[32 * kBS];                  // the backward's layouts (see kDAH)
-    __shared__ float p1[6 * kP1C], p1d[6 * kP1C];
-    __shared__ float g2[kX2], g2d[kX2];
-    __shared__ int off2[kX2];
-    __shared__ float g1[kP1], g1d[kP1];
-    __shared__ int off1[kP1];
-    __shared__ float plane[kPlane];
-    __shared__ float red[kW1Groups * 156];  // conv1 weight-gradient partials per p group
-    const int tid = threadIdx.x, s = blockIdx.y;
-    const float* ws = a.wsamp + (int64_t)s * a.n_tot;
-    const float* wds = a.wdot + (int64_t)s * a.n_tot;
-    for (int i = tid; i < 150; i += kConvThreads) { w1[i] = ws[i]; wd1[i] = wds[i]; }
-    for (int i = tid; i < 2400; i += kConvThreads) { w2[i] = ws[156 + i]; wd2[i] = wds[156 + i]; }
-    // conv2 weight entries: output channel k2 = tid / 15 (threads < 240),
-    // entries c * 25 + i * 5 + j = t15 + 15 r, as in lenet_conv_bwd_kernel.  The
-    // P1 tap base (pb) is formed where it is read: kept in registers across the
-    // image loop it pushed this kernel into scratch spills.
-    constexpr int kR2 = 10;
-    const bool own2 = tid < 240;
-    const int k2 = min(tid / 15, 15), t15 = tid % 15;
-    auto pb = [&](int r) __attribute__((always_inline)) {
-        const int e = t15 + 15 * r;
-        return (e / 25) * kP1C + ((e % 25) / 5) * kP1S + e % 5;
-    };
-    float accw2[kR2];
-#pragma unroll
-    for (int r = 0; r < kR2; ++r) accw2[r] = 0.f;
-    // conv1: five-tap weight rows over 8 routed-position groups, as in
-    // lenet_conv_bwd_kernel
-    const bool w1own = tid < 240, b1own = tid >= 240 && tid < 288;
-    const int t1 = w1own ? tid : tid - 240;
-    const int c1 = w1own ? t1 / 40 : min(t1 / 8, 5), i1 = (t1 / 8) % 5, pg1 = t1 % 8;
-    const int pl1 = (196 * pg1) / kW1Groups, ph1 = (196 * (pg1 + 1)) / kW1Groups;
-    float acc1[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, accb2 = 0.f;
-    float* da2 = plane;
-    float* da2d = plane + 2 * kDAP;
-    float* da1 = plane;
-    float* da1d = plane + 6 * 1024;
-    const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
-    for (int m = m0; m < m1; ++m) {
-        __syncthreads();
-        const int64_t row = (int64_t)s * a.M + m;
-        const float* um = a.u + (int64_t)m * 784;
-        for (int i = tid; i < 1024; i += kConvThreads) {
-            const int y = (i >> 5) - 2, x = (i & 31) - 2;
-            in[(i >> 5) * kBS + (i & 31)] =
-                (y >= 0 && y < 28 && x >= 0 && x < 28) ? um[y * 28 + x] : 0.f;
-        }
-        for (int i = tid; i < kP1; i += kConvThreads) {
-            const int q = (i / 196) * kP1C + ((i % 196) / 14) * kP1S + i % 14;
-            p1[q] = a.p1[row * kP1 + i];
-            p1d[q] = a.p1d[row * kP1 + i];
-        }
-        for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
-        __syncthreads();
-        for (int o = tid; o < kX2; o += kConvThreads) {
-            const int r = a.r2[row * kX2 + o];
-            const int k = o / 25, py = (o % 25) / 5, px = o % 5;
-            const int rr = r >= 0 ? r : 0;
-            const int y = 2 * py + (rr >> 1), x = 2 * px + (rr & 1);
-            const float g = r >= 0 ? a.dx2[row * kX2 + o] : 0.f;
-            const float gd = r >= 0 ? a.dx2d[row * kX2 + o] : 0.f;
-            g2[o] = g;
-            g2d[o] = gd;
-            off2[o] = y * kP1S + x;
-            da2[da2_at(k, y + 4, x + 4)] = g;
-            da2d[da2_at(k, y + 4, x + 4)] = gd;
-        }
-        __syncthreads();
-        // G_dot conv2: sum_p g2_dot P1 + g2 P1_dot at the routed windows (per
-        // image: acc over p from zero, then into accw2; g2 / g2d / off2 read
-        // once per 10 entries)
-        if (own2) {
-            float acc[kR2];
-#pragma unroll
-            for (int r = 0; r < kR2; ++r) acc[r] = 0.f;
-#pragma unroll 1
-            for (int p = 0; p < 25; ++p) {
-                const float gv = g2[k2 * 25 + p], gdv = g2d[k2 * 25 + p];
-                const int op = off2[k2 * 25 + p];
-#pragma unroll
-                for (int r = 0; r < kR2; ++r) {
-                    const int q = pb(r) + op;
-                    acc[r] += gdv * p1[q] + gv * p1d[q];
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < kR2; ++r) accw2[r] += acc[r];
-        }
-        if (tid < 16) {
-            float acc = 0.f;
-            for (int p = 0; p < 25; ++p) acc += g2d[tid * 25 + p];
-            accb2 += acc;
-        }
-        // d P1 and its tangent (transposed conv2), routed through pool1 / relu
-        if (tid < 294) {
-            const int c = tid / 49, yy = 2 * ((tid % 49) / 7), xx = 2 * (tid % 7);
-            float acc[4] = {0.f, 0.f, 0.f, 0.f}, accd[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int k = 0; k < 16; ++k) {
-                const int po = k * kDAK + yy * kDAH + (xx >> 1);
-                convT_block2<kDAP>(da2 + po, kDAH, w2 + k * 150 + c * 25,
-                                   wd2 + k * 150 + c * 25, acc, accd);
-                convT_block<kDAP>(da2d + po, kDAH, w2 + k * 150 + c * 25, accd);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int yq = yy + (q >> 1), xq = xx + (q & 1);
-                const int o = c * 196 + yq * 14 + xq;
-                const int r = a.r1[row * kP1 + o];
-                const int rr = r >= 0 ? r : 0;
-                g1[o] = r >= 0 ? acc[q] : 0.f;
-                g1d[o] = r >= 0 ? accd[q] : 0.f;
-                off1[o] = (2 * yq + (rr >> 1)) * kBS + 2 * xq + (rr & 1);
-            }
-        }
-        __syncthreads();
-        // G_dot conv1 (the image is constant): sum_p g1_dot in[...]
-        if (w1own) {
-            float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 5
-            for (int p = pl1; p < ph1; ++p) {
-                const float gv = g1d[c1 * 196 + p];
-                const float* ip = in + off1[c1 * 196 + p] + i1 * kBS;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) acc[j] += gv * ip[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 5; ++j) acc1[j] += acc[j];
-        } else if (b1own) {
-            float acc = 0.f;
-#pragma unroll 5
-            for (int p = pl1; p < ph1; ++p) acc += g1d[c1 * 196 + p];
-            acc1[0] += acc;
-        }
-        if (a.du) {
-            for (int i = tid; i < kPlane; i += kConvThreads) plane[i] = 0.f;
-            __syncthreads();
-            for (int o = tid; o < kP1; o += kConvThreads) {
-                const int q = (o / 196) * 1024 + (off1[o] / kBS + 2) * 32 + off1[o] % kBS + 2;
-                da1[q] = g1[o];
-                da1d[q] = g1d[o];
-            }
-            __syncthreads();
-            if (tid < 196) {
-                const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
-                float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-                for (int c = 0; c < 6; ++c) {
-                    convT_block(da1d + c * 1024 + yy * 32 + xx, 32, w1 + c * 25, acc);
-                    convT_block(da1 + c * 1024 + yy * 32 + xx, 32, wd1 + c * 25, acc);
-                }
-                float* out = a.du + row * 784 + yy * 28 + xx;
-                out[0] = acc[0];
-                out[1] = acc[1];
-                out[28] = acc[2];
-                out[29] = acc[3];
-            }
-        }
-    }
-    __syncthreads();
-    if (w1own) {
-#pragma unroll
-        for (int j = 0; j < 5; ++j) red[pg1 * 156 + c1 * 25 + i1 * 5 + j] = acc1[j];
-    } else if (b1own) {
-        red[pg1 * 156 + 150 + c1] = acc1[0];
-    }
-    __syncthreads();
-    float* out = a.part + ((int64_t)s * a.nchunk + blockIdx.x) * kNConv;
-    if (tid < 156) {
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < kW1Groups; ++q) t += red[q * 156 + tid];
-        out[tid] = t;
-    }
-    if (tid < 16) out[2556 + tid] = accb2;
-    if (own2) {
-#pragma unroll
-        for (int r = 0; r < kR2; ++r) out[156 + k2 * 150 + t15 + 15 * r] = accw2[r];
-    }
 }
 
 // The tangent backward on the matrix cores (d/du, when asked for, by
@@ -2005,7 +1351,7 @@ __global__ __launch_bounds__(kTThreads, 4) void lenet_conv_bwd_tan_mfma_kernel(T
 // primal and tangent d P1 the backward kernels left in HBM:
 //   du_dot = convT(routed d P1_dot, W1) + convT(routed d P1, W1_dot)
 // (each routed value placed at its conv1 position of a zero-bordered 32 x 32
-// plane per channel, 2x2 output blocks per thread, as lenet_conv_bwd_kernel).
+// plane per channel, 2x2 output blocks per thread).
 __global__ __launch_bounds__(kThreads) void lenet_du_tan_kernel(TanArgs a, const float* __restrict__ g1p,
                                                                const float* __restrict__ g1t) {
     __shared__ float w1[150], wd1[150];
@@ -2101,10 +1447,7 @@ __global__ __launch_bounds__(kThreads) void lenet_hvp_assemble_kernel(
 
 hipError_t gemm(const GemmArgs& g, int batch, hipStream_t st) {
     dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, batch);
-    if (g_lenet_gemm_valu)
-        hipLaunchKernelGGL(lenet_gemm_kernel, grid, dim3(kThreads), 0, st, g);
-    else
-        hipLaunchKernelGGL(lenet_gemm_mfma_kernel, grid, dim3(kThreads), 0, st, g);
+    hipLaunchKernelGGL(lenet_gemm_mfma_kernel, grid, dim3(kThreads), 0, st, g);
     return hipGetLastError();
 }
 
@@ -2235,11 +1578,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     ca.dx2 = W.dx2;
     ca.part = W.part;
     ca.abl = g_lenet_abl;
-    if (g_lenet_conv_valu) {
-        hipLaunchKernelGGL(lenet_conv_fwd_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ca);
-    } else {
-        conv_fwd_mfma<false>(ca, S, M, st);
-    }
+    conv_fwd_mfma<false>(ca, S, M, st);
     const int w3 = p.lay[2].woff, w4 = p.lay[3].woff, w5 = p.lay[4].woff;
     const float* Ws = W.wsamp;
     // head forward: H1 = relu(X2 W1^T + b1), H2 = relu(H1 W2^T + b2), D = H2 W3^T + b3
@@ -2294,10 +1633,7 @@ hipError_t launch_lenet(const psvi_plan& p, const float* u, const int32_t* z, co
     }
     const dim3 bgrid(W.nchunk, S), bblk(kConvThreads);
     const float* part1 = nullptr;
-    if (g_lenet_conv_valu) {
-        if (du) hipLaunchKernelGGL(lenet_conv_bwd_kernel<true>, bgrid, bblk, 0, st, ca);
-        else hipLaunchKernelGGL(lenet_conv_bwd_kernel<false>, bgrid, bblk, 0, st, ca);
-    } else {
+    {
         ca.g1g = W.g1;
         if (du) hipLaunchKernelGGL(lenet_conv_bwd_mfma_kernel<true>, bgrid, bblk, 0, st, ca);
         else hipLaunchKernelGGL(lenet_conv_bwd_mfma_kernel<false>, bgrid, bblk, 0, st, ca);
@@ -2384,10 +1720,7 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
     ta.x2d = T.x2d;
     ta.part = T.part;
     ta.du = d_u ? T.du : nullptr;
-    if (g_lenet_conv_valu) {
-        hipLaunchKernelGGL(lenet_conv_fwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st,
-                           ta);
-    } else {
+    {
         // the forward's kernels in tangent mode: P1_dot from W_dot at conv1's
         // routed offsets, then X2_dot from [P1_dot | P1] x [W2; W2_dot]
         ConvArgs ct{};
@@ -2459,9 +1792,7 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
     if (hipError_t e = dW2(120, 400, T.dh1d, W.x2, W.dh1, T.x2d, w3)) return e;
     if (hipError_t e = dX2(120, 400, T.dh1d, W.dh1, w3, T.dx2d, nullptr)) return e;
     const float* part1 = nullptr;
-    if (g_lenet_conv_valu) {
-        hipLaunchKernelGGL(lenet_conv_bwd_tan_kernel, dim3(W.nchunk, S), dim3(kConvThreads), 0, st, ta);
-    } else {
+    {
         // conv2's G_dot and the routed d P1_dot (over P1_dot: each row is read
         // by its workgroup before its d P1_dot is written), then conv1's G_dot
         // by the primal's weight-gradient kernel, then d/du from the routed

@@ -47,7 +47,7 @@ constexpr int FST = 128;   // samples per pass: 4 waves x 32
 constexpr int FLD = FBK + 4;  // LDS row stride: 16-byte rows (float4 stores, ds_read_b128)
 
 // bf16 pieces (fp32-faithful products on v_mfma_f32_32x32x16_bf16): the
-// helpers of mvn_stream_bf_kernel, mvn_fwd_seg_bf_kernel and the bf16 K-split update
+// helpers of mvn_stream_bf2_kernel, mvn_fwd_seg_bf_kernel and the bf16 K-split update
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short bf8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -1197,7 +1197,7 @@ struct KsArgs {
 // addresses, fix-ups or zero selects at staging.  The first pass of the next
 // segment is loaded behind the last pass of this one (its latency overlaps the
 // hand-off and the epilogue).
-// BF: the dL GEMM on bf16 pieces (fp32-faithful, mvn_stream_bf_kernel's
+// BF: the dL GEMM on bf16 pieces (fp32-faithful, mvn_stream_bf2_kernel's
 // products): a pass's G and eps blocks are split at staging into three bf16
 // planes each, in two halves of 64 samples (column images of 8 KB per plane,
 // read with ds_read_b64_tr_b16; 48 KB of LDS, two workgroups per CU), each
@@ -1326,7 +1326,7 @@ __global__ __launch_bounds__(256, 2) void mvn_kstream_kernel(KsArgs a) {
             }
         }
     };
-    // the transposed reads (mvn_stream_bf_kernel's): lane 4 qq + pp of its
+    // the transposed reads (mvn_stream_bf2_kernel's): lane 4 qq + pp of its
     // 16-lane group takes sample row qq, columns 4 pp .. + 3 of its 16
     const int g16 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
     const uint8_t* const rda = BF ? Eb + img_col(8 * h + qq, 32 * wc + 16 * (g16 & 1) + 4 * pp) : nullptr;
@@ -1720,7 +1720,7 @@ struct StrArgs {
     AdamC adam;
     int xcol[kMaxL];
     MvnLayerArgs lay[kMaxL];
-    // mvn_stream_bf_kernel: the bf16 planes of eps / eps_next (EpsPlanes layout)
+    // mvn_stream_bf2_kernel: the bf16 planes of eps / eps_next (EpsPlanes layout)
     const uint16_t* ep;
     const uint16_t* enp;
     int64_t pl;
@@ -2179,8 +2179,8 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// mvn_stream_bf_kernel: mvn_stream_kernel's tile walk with both products on the
-// bf16 matrix cores, fp32-faithful.  Every operand is split into three bf16
+// The bf16-piece streaming update: mvn_stream_kernel's tile walk with both
+// products on the bf16 matrix cores, fp32-faithful.  Every operand is split into three bf16
 // pieces (split3: exact) and each product is the six piece products that
 // matter (the dropped ones are below 2^-26 of the product, under fp32's own
 // rounding); the matrix cores accumulate in fp32.  v_mfma_f32_32x32x16_bf16
@@ -2198,428 +2198,9 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 //   L'   (x''s B operand): the new corr entries, split in the accumulators'
 //        registers (the accumulator-as-operand order of the 32x32x16 form).
 // Tiled state, slots, the diagonal's mean / sd and the KL as mvn_stream_kernel.
-// DIAG: per-phase shader clocks summed over the run's tiles (thread 0) into
-// the stamp buffer (tools/bf_stamps.py)
-template <int KIND, bool DIAG = false>
-__global__ __launch_bounds__(256, 1) void mvn_stream_bf_kernel(StrArgs a) {
-    // column images of eps and G, row image of eps' (three planes each); the
-    // band end's x' exchange reuses the eps' image (read by then)
-    __shared__ __attribute__((aligned(16))) uint8_t smb[9 * kBfImg];
-    uint8_t* const Eb = smb;
-    uint8_t* const Gb = smb + 3 * kBfImg;
-    uint8_t* const En = smb + 6 * kBfImg;
-    float* const Xs = reinterpret_cast<float*>(En);
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id();
-    const int wr = wv >> 1, wc = wv & 1, h = lane >> 5, l32 = lane & 31;
-    const StreamRange R = a.ranges[blockIdx.x];
-    const int t0 = __builtin_amdgcn_readfirstlane(R.t0);
-    const int t1 = __builtin_amdgcn_readfirstlane(R.t1);
-    int slot = __builtin_amdgcn_readfirstlane(R.slot0);
-    const int S = a.S;  // 128
-    unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
-    auto ph = [&](int q) __attribute__((always_inline)) {
-        if (DIAG && tid == 0) {
-            const unsigned long long tt = __builtin_amdgcn_s_memtime();
-            if (q >= 0) tph[q] += tt - tlast;
-            tlast = tt;
-        }
-    };
-    if (DIAG && tid == 0) {
-        a.stamps[(size_t)blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
-        a.stamps[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
-    }
-
-    // ---- staging of a tile's plane blocks: 12 chunks of 16 bytes per thread
-    // (plane p, row s, chunk ch of the tile's 64 columns)
-    // chunk j of a thread: plane j / 4, row (tid >> 3) + 32 (j % 4), chunk tid % 8;
-    // the rows' swizzle bits come from tid alone, so every LDS address is a
-    // per-thread base plus a constant
-    u32x4 stg[12];
-    const int srow0 = tid >> 3, ch = tid & 7;
-    const int st_col = srow0 * 128 + ((ch ^ (((srow0 >> 1) & 1) << 2)) << 4);
-    // global chunk ch = columns 8 ch .. 8 ch + 7: its halves go to img_row
-    // (columns 8 ch and 8 ch + 4), both in row srow0 (+ 32 j)
-    const int st_row0 = img_row(srow0, 8 * ch), st_row1 = img_row(srow0, 8 * ch + 4);
-    auto load_planes = [&](const uint16_t* base, const StrTile& T) __attribute__((always_inline)) {
-        const uint16_t* b0 = base + T.pe + (int64_t)srow0 * T.npad + 8 * ch;
-#pragma unroll
-        for (int j = 0; j < 12; ++j)
-            stg[j] = *reinterpret_cast<const u32x4*>(b0 + (j >> 2) * a.pl + (int64_t)(32 * (j & 3)) * T.npad);
-    };
-    auto store_col = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < 12; ++j)
-            *reinterpret_cast<u32x4*>(Eb + st_col + (j >> 2) * kBfImg + 4096 * (j & 3)) = stg[j];
-    };
-    auto store_row = [&]() __attribute__((always_inline)) {
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int j = 0; j < 12; ++j) {
-            uint8_t* img = En + (j >> 2) * kBfImg + 4096 * (j & 3);
-            *reinterpret_cast<u32x2*>(img + st_row0) = u32x2{stg[j][0], stg[j][1]};
-            *reinterpret_cast<u32x2*>(img + st_row1) = u32x2{stg[j][2], stg[j][3]};
-        }
-    };
-    // ---- the band's G slice [128 samples][64 rows]: 8 float4 per thread, split
-    // into the three planes of the G column image
-    f32x4 greg[8];
-    auto load_G = [&](const StrTile& T) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int f = tid + 256 * j, s = f >> 4, c4 = f & 15;
-            greg[j] = *reinterpret_cast<const f32x4*>(a.g + (int64_t)s * a.ldg + T.xc + 64 * T.b + 4 * c4);
-        }
-    };
-    auto split_G = [&]() __attribute__((always_inline)) {
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int f = tid + 256 * j, s = f >> 4, c4 = f & 15;
-            uint32_t x[3][2];
-            split3_pk(f32x2{greg[j][0], greg[j][1]}, x[0][0], x[1][0], x[2][0]);
-            split3_pk(f32x2{greg[j][2], greg[j][3]}, x[0][1], x[1][1], x[2][1]);
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                *reinterpret_cast<u32x2*>(Gb + p * kBfImg + img_col(s, 4 * c4)) = u32x2{x[p][0], x[p][1]};
-        }
-    };
-    f32x4 P[4], M4[4], V4[4];
-    auto frag_off = [&](const StrTile& T, int g) __attribute__((always_inline)) {
-        return T.tb + (int64_t)((wv * 4 + g) * 64 + lane) * 4;
-    };
-    const rsrc_t rs_t = make_rsrc(a.tp, 0x7fffffff);
-    const int tmb = __builtin_amdgcn_readfirstlane((int)((a.tm - a.tp) * 4));
-    const int tvb = __builtin_amdgcn_readfirstlane((int)((a.tv - a.tp) * 4));
-    auto load_pmv = [&](const StrTile& T) __attribute__((always_inline)) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int64_t o = frag_off(T, g);
-            P[g] = *reinterpret_cast<const f32x4*>(a.tp + o);
-            M4[g] = *reinterpret_cast<const f32x4*>(a.tm + o);
-            V4[g] = *reinterpret_cast<const f32x4*>(a.tv + o);
-        }
-    };
-    floatx16 xacc[4];
-#pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) xacc[sb][q] = 0.f;
-    float kld = 0.f;
-    f32x2 kl2 = {0.f, 0.f};
-    // the transposed read's address: lane 4 qq + pp of its 16-lane group takes
-    // row qq, columns 4 pp .. 4 pp + 3 of the group's 16 columns
-    const int g16 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-    const int ca = 32 * wc + 16 * (g16 & 1) + 4 * pp;  // eps column (dL's A)
-    const int cg = 32 * wr + 16 * (g16 & 1) + 4 * pp;  // G column (dL's B)
-    // img_col(16 t + 8 h + qq (+ 4), c) = img_col(8 h + qq, c) + 2048 t (+ 512):
-    // the row's swizzle bit is qq's, so a K-step and a half-read are constants
-    const uint8_t* const rda = Eb + img_col(8 * h + qq, ca);
-    const uint8_t* const rdb = Gb + img_col(8 * h + qq, cg);
-    // the row image's chunk XOR for sample row 32 sb + l32: (l32 >> 1) & 7
-    // does not depend on sb, so sb is a constant 4096 sb
-    const int xsw = (l32 >> 1) & 7;
-
-    int tl = __builtin_amdgcn_readfirstlane(R.lbk0 >> 28);
-    int tb_ = __builtin_amdgcn_readfirstlane((R.lbk0 >> 14) & 0x3fff);
-    int tk = __builtin_amdgcn_readfirstlane(R.lbk0 & 0x3fff);
-    StrTile cur = str_tile(a, tl, tb_, tk);
-    load_G(cur);
-    load_planes(a.ep, cur);
-    store_col();
-    load_planes(a.enp, cur);
-    store_row();
-    split_G();
-    __syncthreads();
-
-    // the next tile's loads, spread between the MFMAs (a burst of vector-memory
-    // instructions stalls the in-order wave on the memory queue): 0..11 this
-    // tile's corr / m / v fragments, 12..23 the next tile's eps planes.  Buffer
-    // loads: a per-thread offset fixed for the run (or the tile), the tile's and
-    // the chunk's parts in the scalar offset, so no 64-bit address is live
-    const rsrc_t rs_e = make_rsrc(a.ep, 0x7fffffff), rs_en = make_rsrc(a.enp, 0x7fffffff);
-    const rsrc_t rs_g = make_rsrc(a.g, 0x7fffffff);
-    const uint32_t vo_f = (uint32_t)((wv * 256 + lane) * 16);                     // + 1024 g
-    const uint32_t vo_g = (uint32_t)(4 * ((tid >> 4) * a.ldg + 4 * (tid & 15)));  // G rows tid / 16 (+ 16 j)
-    auto vo_planes = [&](const StrTile& T) __attribute__((always_inline)) {
-        return (uint32_t)(2 * (srow0 * T.npad + 8 * ch));
-    };
-    auto so_planes = [&](const StrTile& T, int j) __attribute__((always_inline)) {
-        return __builtin_amdgcn_readfirstlane((int)(2 * (T.pe + (j >> 2) * a.pl + (int64_t)(32 * (j & 3)) * T.npad)));
-    };
-    auto ldb = [&](rsrc_t r, uint32_t vo, int so) __attribute__((always_inline)) {
-        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
-    };
-    auto issue_a = [&](int q, const StrTile& nxt, bool has_next, uint32_t vo_n) __attribute__((always_inline)) {
-        if (q < 12) {
-            const int g = q / 3, which = q % 3;
-            const int so = __builtin_amdgcn_readfirstlane((int)(cur.tb * 4));
-            const u32x4 x = ldb(rs_t, vo_f + 1024 * g, which == 0 ? so : which == 1 ? so + tmb : so + tvb);
-            if (which == 0) P[g] = __builtin_bit_cast(f32x4, x);
-            else if (which == 1) M4[g] = __builtin_bit_cast(f32x4, x);
-            else V4[g] = __builtin_bit_cast(f32x4, x);
-        } else if (has_next) {
-            const int j = q - 12;
-            stg[j] = ldb(rs_e, vo_n, so_planes(nxt, j));
-        }
-    };
-    // phase B's loads: 0..11 the next tile's eps' planes, 12..19 the next band's G
-    auto issue_b = [&](int q, const StrTile& nxt, bool has_next, bool newband, uint32_t vo_n) __attribute__((always_inline)) {
-        if (q < 12) {
-            if (has_next) stg[q] = ldb(rs_en, vo_n, so_planes(nxt, q));
-        } else if (newband) {
-            const int j = q - 12;
-            const int so = __builtin_amdgcn_readfirstlane(4 * (16 * j * a.ldg + nxt.xc + 64 * nxt.b));
-            greg[j] = __builtin_bit_cast(f32x4, ldb(rs_g, vo_g, so));
-        }
-    };
-
-    auto tile = [&](const StrTile& nxt, auto has_next_c, auto newband_c) __attribute__((always_inline)) {
-        constexpr bool has_next = decltype(has_next_c)::value;
-        constexpr bool newband = decltype(newband_c)::value;
-        ph(-1);
-        asm volatile("" : "+a"(xacc[0]), "+a"(xacc[1]), "+a"(xacc[2]), "+a"(xacc[3]));
-        const bool diag = cur.k == cur.b && wc == wr;  // wave-uniform
-        // ---- phase A: dL^T = eps^T G over the samples, 8 K-steps of 16
-        floatx16 acc;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-        float dgm = 0.f, dgs = 0.f;
-        const uint32_t vo_n = vo_planes(nxt);
-        auto read_ab = [&](int t, bf8v (&av)[3], bf8v (&bv)[3]) __attribute__((always_inline)) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                typedef __attribute__((address_space(3))) s4v* lds_s4;
-                const int o = p * kBfImg + 2048 * t;  // rows 16 t + 8 h + qq (+ 4)
-                av[p] = cat44(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rda + o)),
-                              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rda + o + 512)));
-                bv[p] = cat44(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rdb + o)),
-                              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4)(rdb + o + 512)));
-            }
-        };
-        bf8v fa[2][3], fb[2][3];
-        read_ab(0, fa[0], fb[0]);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            // one K-step of fragments ahead; the barrier keeps the scheduler
-            // from hoisting further reads (all K-steps' fragments at once spill)
-            if (t + 1 < 8) read_ab(t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
-#pragma unroll
-            for (int q = 3 * t; q < 3 * t + 3; ++q) issue_a(q, nxt, has_next, vo_n);
-            const bf8v(&av)[3] = fa[t & 1];
-            const bf8v(&bv)[3] = fb[t & 1];
-            acc = mfma6(av, bv, acc);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (diag) {
-            // the diagonal quadrant (1 tile in ~20, its own pass so that the
-            // K-steps stay free of it): lane (c = r, h) reads eps and G of the
-            // same row for its 64 samples -- sum_s G and sum_s G eps
-#pragma unroll 1
-            for (int t = 0; t < 8; ++t) {
-                bf8v av[3], bv[3];
-                read_ab(t, av, bv);
-#pragma unroll
-                for (int j = 0; j < 8; j += 2) {
-                    const f32x2 e = (bf_pair(av[0], j) + bf_pair(av[1], j)) + bf_pair(av[2], j);
-                    const f32x2 gg = (bf_pair(bv[0], j) + bf_pair(bv[1], j)) + bf_pair(bv[2], j);
-                    dgm += gg[0] + gg[1];
-                    dgs = fmaf(gg[1], e[1], fmaf(gg[0], e[0], dgs));
-                }
-            }
-        }
-        ph(1);
-        __syncthreads();  // every wave done with the eps and G images
-        ph(2);
-        if constexpr (has_next) store_col();  // the next tile's eps image
-        const int n = cur.n, r = 64 * cur.b + 32 * wr + l32;
-        // ---- diagonal tile: mean / sd of the band's rows
-        if (diag) {
-            dgm += __shfl_xor(dgm, 32, kWave);
-            dgs += __shfl_xor(dgs, 32, kWave);
-            if (h == 0 && r < n) {
-                const int pm = (int)cur.poff + r, ps = pm + n;
-                const float mu = a.params[pm], sdr = a.params[ps];
-                const float sp = softplus_f(sdr), sg = sigmoid_f(sdr);
-                float gmean = dgm, gsd = dgs * sg;
-                if (a.include_kl) {
-                    gmean += mu * a.inv_s0sq;
-                    gsd += (sp * a.inv_s0sq - 1.f / sp) * sg;
-                    kld += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
-                }
-                float mm = a.m[pm], vv = a.v[pm];
-                a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
-                a.m[pm] = mm;
-                a.v[pm] = vv;
-                mm = a.m[ps];
-                vv = a.v[ps];
-                a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
-                a.m[ps] = mm;
-                a.v[ps] = vv;
-            }
-        }
-        ph(3);
-        // ---- phase B: Adam on the accumulators (fragment order = tiled order),
-        // the stores, x' += eps' L'^T.  Column pair e2 of group g: Adam, then
-        // its L' pieces; group-pair st = 0's Adam is exposed, st = 1's runs
-        // beside st = 0's x' MFMAs, and the next tile's loads beside st = 1's
-        const bool rv = r >= 1 && r <= n - 2;
-        const float kls = a.include_kl ? a.inv_s0sq : 0.f;
-        uint32_t lw[2][3][4];  // L' pieces: [st][plane][element pair]
-        auto adam_pair = [&](int g, int e) __attribute__((always_inline)) {
-            // entries e, e + 1 of group g (acc registers 4 g + e, + 1)
-            const int cb = 64 * cur.k + 32 * wc + 8 * g + 4 * h;
-            const f32x2 pv0 = {P[g][e], P[g][e + 1]};
-            kl2 = __builtin_elementwise_fma(pv0, pv0, kl2);
-            const f32x2 gvv = __builtin_elementwise_fma(pv0, f32x2{kls, kls},
-                                                        f32x2{acc[4 * g + e], acc[4 * g + e + 1]});
-            const f32x2 gm = {rv && cb + e < r ? gvv[0] : 0.f, rv && cb + e + 1 < r ? gvv[1] : 0.f};
-            f32x2 mm = {M4[g][e], M4[g][e + 1]}, vv = {V4[g][e], V4[g][e + 1]};
-            const f32x2 pv = adam_fast_k2<KIND>(a.adam, pv0, gm, mm, vv);
-            P[g][e] = pv[0];
-            P[g][e + 1] = pv[1];
-            M4[g][e] = mm[0];
-            M4[g][e + 1] = mm[1];
-            V4[g][e] = vv[0];
-            V4[g][e + 1] = vv[1];
-            // element pair (4 (g & 1) + e) / 2 of K-step g >> 1
-            uint32_t w0, w1, w2;
-            split3_pk(pv, w0, w1, w2);
-            const int jp = (4 * (g & 1) + e) >> 1;
-            lw[g >> 1][0][jp] = w0;
-            lw[g >> 1][1][jp] = w1;
-            lw[g >> 1][2][jp] = w2;
-        };
-        auto store_g = [&](int g) __attribute__((always_inline)) {
-            const uint32_t ob = (uint32_t)(frag_off(cur, g) * 4);
-            BSTORE128(__builtin_bit_cast(u32x4, P[g]), rs_t, ob, 0, 16);
-            BSTORE128(__builtin_bit_cast(u32x4, M4[g]), rs_t, ob, tmb, 16);
-            BSTORE128(__builtin_bit_cast(u32x4, V4[g]), rs_t, ob, tvb, 16);
-        };
-        auto lbf = [&](int st, int p) __attribute__((always_inline)) {
-            return __builtin_bit_cast(bf8v, u32x4{lw[st][p][0], lw[st][p][1], lw[st][p][2], lw[st][p][3]});
-        };
-        // group pair 0: exposed
-        adam_pair(0, 0);
-        adam_pair(0, 2);
-        adam_pair(1, 0);
-        adam_pair(1, 2);
-        store_g(0);
-        store_g(1);
-        ph(4);
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            // columns c0 .. c0 + 3 and c0 + 8 .. c0 + 11, c0 = 32 wc + 16 st + 4 h:
-            // chunk 2 (2 wc + st) + h of the row image, one ds_read_b128
-            const uint8_t* const rx = En + l32 * 128 + (((2 * (2 * wc + st) + h) ^ xsw) << 4);
-            auto read_x = [&](int sb, bf8v (&av)[3]) __attribute__((always_inline)) {
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    av[p] = *reinterpret_cast<const bf8v*>(rx + p * kBfImg + 4096 * sb);
-            };
-            const bf8v lb[3] = {lbf(st, 0), lbf(st, 1), lbf(st, 2)};
-            bf8v fx[2][3];
-            read_x(0, fx[0]);
-#pragma unroll
-            for (int sb = 0; sb < 4; ++sb) {
-                if (sb + 1 < 4) read_x(sb + 1, fx[(sb + 1) & 1]);
-                xacc[sb] = mfma6(fx[sb & 1], lb, xacc[sb]);
-                if (st == 0) {
-                    // group pair 1's Adam, one element pair per sample block
-                    adam_pair(2 + (sb >> 1), 2 * (sb & 1));
-                    if (sb == 3) {
-                        store_g(2);
-                        store_g(3);
-                    }
-                }
-                // the next tile's eps' planes and band G: 20 loads over the 8
-                // sample blocks of both group pairs
-                {
-                    const int k = 4 * st + sb, q0 = (20 * k) / 8, q1 = (20 * (k + 1)) / 8;
-#pragma unroll
-                    for (int q = q0; q < q1; ++q) issue_b(q, nxt, has_next, newband, vo_n);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        // x' lives in the accumulation registers across the band (the compiler
-        // otherwise parks it in VGPRs and moves it in and out around the MFMAs)
-        asm volatile("" : "+a"(xacc[0]), "+a"(xacc[1]), "+a"(xacc[2]), "+a"(xacc[3]));
-        ph(5);
-        // ---- band end (or run end): the two column halves' x' partials -> the slot
-        if constexpr (!has_next || newband) {
-            __syncthreads();  // every wave done reading the eps' image (the scratch)
-            if (wc == 1) {
-#pragma unroll
-                for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) Xs[((wr * 4 + sb) * 16 + q) * 64 + lane] = xacc[sb][q];
-            }
-            __syncthreads();
-            if (wc == 0) {
-                float* dst = a.part + (size_t)slot * S * 64 + 32 * wr + l32;
-#pragma unroll
-                for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        const int s = 32 * sb + (q & 3) + 8 * (q >> 2) + 4 * h;
-                        dst[(size_t)s * 64] = xacc[sb][q] + Xs[((wr * 4 + sb) * 16 + q) * 64 + lane];
-                    }
-            }
-#pragma unroll
-            for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-                for (int q = 0; q < 16; ++q) xacc[sb][q] = 0.f;
-            ++slot;
-        }
-        ph(6);
-        __syncthreads();  // every wave done with the eps' image
-        ph(7);
-        if constexpr (has_next) store_row();
-        if constexpr (newband) {
-            split_G();
-            __syncthreads();  // the new band's G image written before any wave's dL reads it
-        }
-        ph(8);
-        if (DIAG && tid == 0) ++tph[9];
-    };
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    for (int i = t0; i + 1 < t1; ++i) {
-        if (++tk > tb_) {
-            tk = 0;
-            int nbl = a.nb[0];
-#pragma unroll
-            for (int l = 1; l < kMaxL; ++l)
-                if (tl == l) nbl = a.nb[l];
-            if (++tb_ == nbl) {
-                tb_ = 0;
-                ++tl;
-            }
-        }
-        const StrTile nxt = str_tile(a, tl, tb_, tk);
-        if (nxt.l != cur.l || nxt.b != cur.b)
-            tile(nxt, T_{}, T_{});
-        else
-            tile(nxt, T_{}, F_{});
-        cur = nxt;
-    }
-    tile(cur, F_{}, F_{});
-    if (DIAG && tid == 0) {
-        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
-#pragma unroll
-        for (int q = 0; q < 10; ++q) o[q] = tph[q];
-        o[10] = __builtin_amdgcn_s_memtime();
-        o[11] = __builtin_amdgcn_s_memrealtime();
-    }
-    float klp = (kl2[0] + kl2[1]) * (0.5f * a.inv_s0sq) + kld;
-    if (a.kl_out && a.include_kl) {
-        const float tot = block_sum(klp, Xs);
-        if (tid == 0) atomicAdd(a.kl_out, (double)tot);
-    }
-}
-
-// mvn_stream_bf2_kernel: mvn_stream_bf_kernel with two waves per SIMD.  Eight
+//
+// mvn_stream_bf2_kernel: that tile walk with two waves per SIMD (the round-5
+// four-wave form, one wave per SIMD, ran 37.6 us against 33.8 at C3).  Eight
 // waves per workgroup: wave (q, hk) with quadrant q = wv & 3 -- rows 32 wr,
 // columns 32 wc of the 64 x 64 tile, (wr, wc) = (q >> 1, q & 1) -- and sample
 // half hk = wv >> 2 (samples 64 hk .. 64 hk + 63).  The two waves of a
@@ -2638,7 +2219,8 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_bf_kernel(StrArgs a) {
 //       sample half) and written to the segment's slot, as before.
 // The exchanges use the eps column image after the dL reads (16 + 24 KB); the
 // next tile's eps planes are stored after them.  Images, pieces, swizzles and
-// the slot layout are mvn_stream_bf_kernel's.
+// the slot layout as described above.  DIAG: per-phase shader clocks summed
+// over the run's tiles (thread 0) into the stamp buffer (tools/bf_stamps.py).
 template <int KIND, bool DIAG = false>
 __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smb[9 * kBfImg];
@@ -3049,9 +2631,8 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
     }
 }
 
-int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1: chunked, 3: plain-store stream)
+int g_stream_off = 0;  // psvi_debug_set(PSVI_DBG_UPD_STREAM_OFF, 1): the chunked kernel (A/B)
 int g_stream_bf_off = 0;  // psvi_debug_set(PSVI_DBG_STREAM_BF_OFF, 1): the fp32-MFMA streaming kernel (A/B)
-int g_stream_bf2_off = 0; // psvi_debug_set(PSVI_DBG_STREAM_BF2_OFF, 1): the four-wave bf16-piece kernel (A/B)
 unsigned long long* g_bf_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_BF_STAMPS, buf)
 int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked kernel at S > 128 (A/B)
 int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
@@ -3071,7 +2652,7 @@ static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
 }
 
 // mvn_fwd_seg_bf_kernel: mvn_fwd_seg_kernel with the GEMM on the bf16 matrix
-// cores, fp32-faithful (the pieces of mvn_stream_bf_kernel): each stage's eps
+// cores, fp32-faithful (the pieces of mvn_stream_bf2_kernel): each stage's eps
 // block [128 s][64 k] and masked L block [64 r][64 k] are split at staging
 // into three bf16 planes each, stored as row images (128-byte rows, 16-byte
 // chunk c of row s at c ^ ((s >> 1) & 7)), and both operands read with one
@@ -3437,9 +3018,7 @@ hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float
 
 template <int NS>
 static void launch_stream_ns(int kind, dim3 g, dim3 bl, hipStream_t st, const StrArgs& b, bool pad) {
-    if (g_stream_off == 3)  // A/B: plain corr / m / v stores
-        hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER, false, false>), g, bl, 0, st, b);
-    else if (pad && kind == PSVI_ADAM_HIGHER)
+    if (pad && kind == PSVI_ADAM_HIGHER)
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HIGHER, false, true, true>), g, bl, 0, st, b);
     else if (pad)
         hipLaunchKernelGGL((mvn_stream_kernel<NS, PSVI_ADAM_HYPERGRAD, false, true, true>), g, bl, 0, st, b);
@@ -3544,15 +3123,7 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                     b.npad[l] = p.eps_planes.npad[l];
                 }
                 const dim3 b8(512);
-                if (g_stream_bf2_off) {
-                    // A/B: four waves, one per SIMD
-                    if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
-                        hipLaunchKernelGGL((mvn_stream_bf_kernel<PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
-                    else if (b.adam.kind == PSVI_ADAM_HIGHER)
-                        hipLaunchKernelGGL(mvn_stream_bf_kernel<PSVI_ADAM_HIGHER>, sg, block, 0, st, b);
-                    else
-                        hipLaunchKernelGGL(mvn_stream_bf_kernel<PSVI_ADAM_HYPERGRAD>, sg, block, 0, st, b);
-                } else if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
+                if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
                     hipLaunchKernelGGL((mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER, true>), sg, b8, 0, st, b);
                 else if (b.adam.kind == PSVI_ADAM_HIGHER)
                     hipLaunchKernelGGL(mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER>, sg, b8, 0, st, b);

@@ -206,6 +206,10 @@ struct NetGeo {
     static constexpr bool kFixed = true;
     static constexpr int kUnroll = kMaxL;
     static constexpr NetCarve C = net_carve(kFn2Dims, kFn2Mp, GEO == 2 ? kFn2Bands : 0);
+    // lanes of the loss head's reductions: the smallest power of two >= C
+    static constexpr int kHeadLanes = kFn2Dims.dout[kFn2Dims.L - 1] <= 2   ? 2
+                                      : kFn2Dims.dout[kFn2Dims.L - 1] <= 4 ? 4
+                                                                          : 16;
     __device__ explicit NetGeo(const NetArgs&) {}
     __device__ static constexpr int L() { return kFn2Dims.L; }
     __device__ static constexpr int din(int l) { return kFn2Dims.din[l]; }
@@ -233,6 +237,7 @@ template <>
 struct NetGeo<0> {
     static constexpr bool kFixed = false;
     static constexpr int kUnroll = 1;
+    static constexpr int kHeadLanes = 16;
     const NetArgs& a;
     __device__ explicit NetGeo(const NetArgs& args) : a(args) {}
     __device__ int L() const { return a.L; }
@@ -384,14 +389,15 @@ __device__ __forceinline__ void gemm_steps(int nu, int tqu, int K16, int u0, con
 }
 template <bool ACONT, bool BCONT, class Epi>
 __device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const float* A, int lda,
-                                          const float* B, int ldb, Epi epi) {
-    const int wid = wave_id(), nwv = blockDim.x >> 6;
+                                          const float* B, int ldb, Epi epi, int nwaves = 0) {
+    // nwaves: the workgroup's waves when known at compile time (0: blockDim)
+    const int wid = wave_id(), nwv = nwaves ? nwaves : (int)(blockDim.x >> 6);
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, K16 = (K + 15) & ~15;
     const int u0 = ((wid - first) % nwv + nwv) % nwv;
     switch (gemm_nq(tp, tq)) {
-        case 3: gemm_steps<ACONT, BCONT, 3>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
-        case 2: gemm_steps<ACONT, BCONT, 2>(tp, 1, K16, u0, A, lda, B, ldb, epi); break;
-        default: gemm_steps<ACONT, BCONT, 1>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi); break;
+        case 3: gemm_steps<ACONT, BCONT, 3>(tp, 1, K16, u0, A, lda, B, ldb, epi, nwv); break;
+        case 2: gemm_steps<ACONT, BCONT, 2>(tp, 1, K16, u0, A, lda, B, ldb, epi, nwv); break;
+        default: gemm_steps<ACONT, BCONT, 1>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi, nwv); break;
     }
 }
 
@@ -401,13 +407,13 @@ __device__ __forceinline__ void mfma_gemm(int P, int Q, int K, int first, const 
 template <int CARRY, class Epi>
 __device__ __forceinline__ void mfma_gemm_carry(int P, int Q, int K, int first, const float* A,
                                                 int lda, const float* B, int ldb, Epi epi,
-                                                floatx4 (*carry)[1], int cmode) {
-    const int wid = wave_id(), nwv = blockDim.x >> 6;
+                                                floatx4 (*carry)[1], int cmode, int nwaves = 0) {
+    const int wid = wave_id(), nwv = nwaves ? nwaves : (int)(blockDim.x >> 6);
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, K16 = (K + 15) & ~15;
     const int u0 = ((wid - first) % nwv + nwv) % nwv;
     // (the host gates the fixed geometry to 512 threads: tp tq <= CARRY nwaves
     // for every fn2 layer, and gemm_nq is 1 for all of them)
-    gemm_steps<false, false, 1, CARRY>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi, 0, 0, carry, cmode);
+    gemm_steps<false, false, 1, CARRY>(tp * tq, tq, K16, u0, A, lda, B, ldb, epi, nwv, 0, carry, cmode);
 }
 
 // One 16-row tile by ONE wave: C[p][q] for p < 16, q < Q (every column tile:
@@ -457,6 +463,9 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     using Geo = NetGeo<GEO>;
     const Geo g(a);
     constexpr int kUL = Geo::kUnroll;  // layer loops: fully unrolled for a fixed geometry
+    // threads per workgroup: the fixed geometry runs 512 (the host gates it),
+    // so no implicit-argument load for blockDim
+    const int nthr = Geo::kFixed ? 512 : (int)blockDim.x;
     static_assert(!VEC || FAM == PSVI_FAMILY_FULLCOV, "float4 loads: the full-cov x row");
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x;                 // local sample
@@ -465,6 +474,14 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int L = g.L(), Mp = g.Mp();
     const int tid = threadIdx.x;
     unsigned long long* stl = reinterpret_cast<unsigned long long*>(sm + g.lstamp());
+    if constexpr (Geo::kFixed) {
+        // the load phase's kernel arguments in one batch of scalar loads: the
+        // diagnostics branches below would otherwise each wait for their own
+        // before the first global load is issued
+        asm volatile("" ::"s"(a.u), "s"(a.xrecv), "s"(a.xmap), "s"(a.z), "s"(a.w), "s"(a.abl),
+                     "s"(a.stamps), "s"(a.mc), "s"(a.M), "s"(a.stage_len), "s"(a.src_stride[0]),
+                     "s"(a.rn_P));  // (rn_P: the cache line of the implicit arguments)
+    }
     if (a.abl & 128) {
         // diagnostics: poison the LDS with NaN first -- every word the kernel
         // reads must have been written by it (the padding contract).  abl >> 8
@@ -478,7 +495,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
         else if (reg == 4) { lo = g.L() > 1 ? g.lx(1) : g.ldl(); hi = g.L() > 1 ? g.lg(0) : g.ldl(); }
         else if (reg == 5) { lo = g.L() > 1 ? g.lg(0) : g.ldl(); hi = g.ldl(); }
         else if (reg == 6) { lo = g.ldl(); }
-        for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) sm[i] = __builtin_nanf("");
+        for (int i = lo + (int)threadIdx.x; i < hi; i += nthr) sm[i] = __builtin_nanf("");
         __syncthreads();
     }
     if (a.stamps && threadIdx.x < 16) stl[threadIdx.x] = 0;
@@ -561,7 +578,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     // into the padded W_l, b_l, W_l^T, no stage, no index arithmetic behind
     // the loads (LDS-DMA of the rows measured several times slower).
     const int D = g.din(0);
-    const int r16 = tid >> 4, c16 = tid & 15, nr16 = blockDim.x >> 4;
+    const int r16 = tid >> 4, c16 = tid & 15, nr16 = nthr >> 4;
     float* zw = sm + g.lzw();  // the chunk's labels (as int bits) and weights
     float* X0 = sm + g.lx(0);
     const int ldx0 = g.ldx(0);
@@ -584,7 +601,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         const int nx4 = MSRC ? (first ? a.src_chunk0[a.nsrc] : 0) : nx >> 2;
         const float* xr = a.xrecv + (int64_t)s * a.src_stride[0];
         const u4* xm4 = reinterpret_cast<const u4*>(a.xmap);
-        const int bd = blockDim.x;
+        const int bd = nthr;
         int xsh[kX4];  // MSRC: this lane's shift of each chunk (0: all four valid)
         for (int pass = 0; pass * kU4 * bd < nu4 || pass * kX4 * bd < nx4 || pass == 0; ++pass) {  // uniform
             const int bu = pass * kU4 * bd + tid, bx = pass * kX4 * bd + tid;
@@ -630,25 +647,20 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                     wv = a.w[m0 + mm];
                 }
             }
-            if (pass == 0) {
-                // zero padding while the loads are in flight (disjoint from every
-                // loaded element): W columns >= din and rows >= dout, W^T columns
-                // dout .. the 16-multiple, u columns >= D up to the 16-multiple, u
-                // rows past the chunk, the 64-float slacks after every region
-#pragma unroll kUL
-                for (int l = 0; l < L; ++l) {
-                    if (!first) break;
-                    const int din = g.din(l), dout = g.dout(l), ldw = g.ldw(l);
-                    const int rows = (dout + 15) & ~15;
-                    if (l > 0) {
-                        float* WT = sm + g.lwt(l);
-                        for (int i = r16; i < din; i += nr16)
-                            if (dout + c16 < rows) WT[i * g.ldwt(l) + dout + c16] = 0.f;
-                    }
-                    float* W = sm + g.lw(l);
-                    for (int j = r16; j < dout; j += nr16)
-                        for (int c = din + c16; c < ldw; c += 16) W[j * ldw + c] = 0.f;
-                    for (int i = tid; i < (rows - dout) * ldw; i += bd) W[dout * ldw + i] = 0.f;
+            NET_STAMP(11, __builtin_amdgcn_s_memtime());
+            if (pass == 0 && !(a.abl & 4096)) {
+                // zero padding while the loads are in flight (diagnostics: abl &
+                // 4096 skips it -- wrong results).  The weight regions (W_l, b_l,
+                // W_l^T and their slacks: the carve's first, up to X_0) are zeroed
+                // whole with float4 stores, and after a barrier the x scatter
+                // writes the sampled values over them; then u rows past the chunk,
+                // u columns >= D up to the 16-multiple and the other slacks
+                if (first) {
+                    f4* z4 = reinterpret_cast<f4*>(sm);
+                    const int nz4 = g.lx(0) >> 2;
+                    constexpr int kZU = Geo::kFixed ? 8 : 1;
+#pragma unroll kZU
+                    for (int i = tid; i < nz4; i += bd) z4[i] = f4{0.f, 0.f, 0.f, 0.f};
                 }
                 const int cend = min((D + 15) & ~15, ldx0);
                 for (int m = r16; m < mcnt; m += nr16)
@@ -658,11 +670,13 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                     // every slack's offset a constant: one store per slack, wave k % nwaves
 #pragma unroll
                     for (int k = 0; k < Geo::nslack(); ++k)
-                        if (k % (int)(bd >> 6) == wave_id()) sm[Geo::slack(k) + (tid & 63)] = 0.f;
+                        if (Geo::slack(k) >= Geo::lx(0) && k % (int)(bd >> 6) == wave_id())
+                            sm[Geo::slack(k) + (tid & 63)] = 0.f;
                 } else {
                     for (int k = wave_id(); k < g.nslack(); k += bd >> 6)  // wave-uniform slot
-                        sm[g.slack(k) + (tid & 63)] = 0.f;
+                        if (g.slack(k) >= g.lx(0)) sm[g.slack(k) + (tid & 63)] = 0.f;
                 }
+                if (first) __syncthreads();  // the zeroed weights before the x scatter
             }
             if (a.abl & 1) continue;
 #pragma unroll
@@ -714,7 +728,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         const float rdu = 1.f / (float)D;
         const float* usrc = a.u + (int64_t)m0 * D;
         const int nx = FAM == PSVI_FAMILY_FULLCOV ? a.stage_len : 0;
-        const int bd = blockDim.x;
+        const int bd = nthr;
         for (int pass = 0; pass * kU * bd < nu || pass * kX * bd < nx || pass == 0; ++pass) {  // uniform
             const int bu = pass * kU * bd + tid, bx = pass * kX * bd + tid;
             float uv[kU];
@@ -830,18 +844,18 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
             const float* eW = a.eps + a.eoff[l] + (int64_t)sg * nw;
             const float* eB = a.eps + a.eoff[l] + (int64_t)a.S_total * nw + (int64_t)sg * dout;
             const float rdin = 1.f / (float)din;
-            for (int base = tid; base < n; base += kB * blockDim.x) {
+            for (int base = tid; base < n; base += kB * nthr) {
                 float vm[kB], vr[kB], ve[kB];
 #pragma unroll
                 for (int k = 0; k < kB; ++k) {
-                    const int idx = min(base + k * (int)blockDim.x, n - 1);
+                    const int idx = min(base + k * nthr, n - 1);
                     vm[k] = mu[idx];
                     vr[k] = rho[idx];
                     ve[k] = idx < nw ? eW[idx] : eB[idx - nw];
                 }
 #pragma unroll
                 for (int k = 0; k < kB; ++k) {
-                    const int idx = base + k * (int)blockDim.x;
+                    const int idx = base + k * nthr;
                     if (idx >= n) break;
                     const float val = vm[k] + ve[k] * softplus_f(vr[k]);
                     if (idx < nw) {
@@ -860,7 +874,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     if (FAM == PSVI_FAMILY_FULLCOV && MSRC && first) {
         // every band's g_send offset for this sample (section 3's fc_addr)
         int64_t* boff = reinterpret_cast<int64_t*>(srct);
-        for (int i = tid; i < a.nbands; i += blockDim.x) {
+        for (int i = tid; i < a.nbands; i += nthr) {
             const NetBand bd = a.bands[i];
             boff[i] = bd.base + (int64_t)s * bd.stride;
         }
@@ -870,7 +884,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     NET_STAMP(1, __builtin_amdgcn_s_memtime());
     if (a.stamps && tid == 0) {
         unsigned long long mx = 0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) mx = max(mx, stl[16 + q]);
+        for (int q = 0; q < (nthr >> 6); ++q) mx = max(mx, stl[16 + q]);
         stl[15] = mx;
     }
 
@@ -895,7 +909,7 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
     // outer backward: d loss / d pseudo_s and d loss / d data_s scale the rows
     const float cp = a.outer == 2 ? a.rowcoef[2 * s] : 1.f;
     const float cd = a.outer == 2 ? a.rowcoef[2 * s + 1] : 1.f;
-    const int nwv = blockDim.x >> 6, lane = tid & 63;
+    const int nwv = nthr >> 6, lane = tid & 63;
     auto drain = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
     // G_l: dlogits for l = L - 1, else the l-th gradient buffer (stride of X_{l+1})
     auto gbuf = [&](int l) __attribute__((always_inline)) {
@@ -916,6 +930,10 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
             const float* Bv = sm + g.lb(l);
             const int ldn = head ? g.lddl() : g.ldx(l + 1), jend = min((dout + 15) & ~15, ldn);
             if (head && fuse_head) {
+                // the row's logits sit on lanes j < C of its 16: the reductions
+                // span the smallest power of two >= C (the fixed geometry: C = 2,
+                // one lane exchange) -- a row of 16 otherwise
+                constexpr int kHeadLanes = Geo::kHeadLanes;
                 auto epi = [&](int m, int j, floatx4 v, int rot) {  // j = i16: every lane of the row takes part
                     const bool jl = j < C;
                     const float b = Bv[min(j, C - 1)];
@@ -923,8 +941,8 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
                     for (int r = 0; r < 4; ++r) {
                         const int row = m + ((r + rot) & 3), rg = r0 + row;
                         const float y = v[r] + b;
-                        const float mx = row16_max(jl ? y : -INFINITY);
-                        const float lse = mx + logf(row16_sum(jl ? expf(y - mx) : 0.f));
+                        const float mx = lanes_max<kHeadLanes>(jl ? y : -INFINITY);
+                        const float lse = mx + logf(lanes_sum<kHeadLanes>(jl ? expf(y - mx) : 0.f));
                         const int zr = __float_as_int(zw[rg]);
                         const float wr = zw[Mp + rg];
                         const bool ok = rg < mcnt;
@@ -1075,10 +1093,10 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
             if constexpr (kCarry) {
                 const int cm = nloop == 1 ? 0 : ch == 0 ? 1 : ch + 1 < nloop ? 3 : 2;
                 mfma_gemm_carry<kWcUnits>(dout, din, Mp, first, gbuf(l), gld(l), sm + g.lx(l),
-                                          g.ldx(l), epi, wc[l], cm);
+                                          g.ldx(l), epi, wc[l], cm, nthr >> 6);
             } else {
                 mfma_gemm<false, false>(dout, din, Mp, first, gbuf(l), gld(l), sm + g.lx(l),
-                                        g.ldx(l), epi);
+                                        g.ldx(l), epi, nthr >> 6);
             }
             first += gemm_units(dout, din);
         }
@@ -1150,10 +1168,10 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         const int64_t per = (nq + nblk - 1) / nblk, q1 = min(nq, (b + 1) * per);
         if (a.rn_planes) {
             const EpsPlanes P = *a.rn_P;
-            for (int64_t q = b * per + tid; q < q1; q += blockDim.x)
+            for (int64_t q = b * per + tid; q < q1; q += nthr)
                 randn_quad_planes(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q, P, a.rn_planes);
         } else {
-            for (int64_t q = b * per + tid; q < q1; q += blockDim.x)
+            for (int64_t q = b * per + tid; q < q1; q += nthr)
                 randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
         }
     }

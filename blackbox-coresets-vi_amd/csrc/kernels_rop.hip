@@ -615,25 +615,15 @@ __device__ __forceinline__ void rop_steps(int nu, int tqu, int nk, int u0, int n
 }
 
 // P x Q outputs, contraction over K16 / 16 k-groups of 16 (operand rows or
-// columns past the true length are zero in LDS).  A row of column tiles per unit (one A read
-// per NQ tiles) when that still gives each SIMD a unit, else single tiles.
-template <bool WIDE, bool ACONT, bool BCONT, bool TA, bool TB, bool WX, class Epi>
+// columns past the true length are zero in LDS), single 16 x 16 tiles dealt
+// round-robin to the waves (rows of up to three column tiles per unit were
+// measured slower in round 5: 256 VGPRs).
+template <bool ACONT, bool BCONT, bool TA, bool TB, bool WX, class Epi>
 __device__ __forceinline__ void rop_gemm(int P, int Q, int K16, int first, const float* A,
                                          int lda, int oa, const float* B, int ldb, int ob, Epi epi) {
     const int nwv = blockDim.x >> 6, wid = wave_id();
     const int tp = (P + 15) >> 4, tq = (Q + 15) >> 4, nk = K16 >> 4;
     const int u0 = ((wid - first) % nwv + nwv) % nwv;
-    const int nq = (WIDE && tq <= 3 && tp >= 4) ? tq : 1;
-    if constexpr (WIDE) {
-        if (nq == 3) {
-            rop_steps<ACONT, BCONT, 3, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, epi);
-            return;
-        }
-        if (nq == 2) {
-            rop_steps<ACONT, BCONT, 2, TA, TB, WX>(tp, 1, nk, u0, nwv, A, lda, oa, B, ldb, ob, epi);
-            return;
-        }
-    }
     rop_steps<ACONT, BCONT, 1, TA, TB, WX>(tp * tq, tq, nk, u0, nwv, A, lda, oa, B, ldb, ob, epi);
 }
 
@@ -655,7 +645,7 @@ __device__ __forceinline__ void lds_dma4(rsrc_t r, float* lds, uint32_t voff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
 }
 
-template <bool WIDE, bool FC>
+template <bool FC>
 __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int s = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
@@ -846,7 +836,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                 }
             }
         };
-        rop_gemm<WIDE, true, true, true, true, true>(rc, dout, kxl, 0, sm + a.mxo[l], a.ldxm[l], kxl,
+        rop_gemm<true, true, true, true, true>(rc, dout, kxl, 0, sm + a.mxo[l], a.ldxm[l], kxl,
                                                      sm + a.mwo[l], a.ldwm[l], kxl, epi);
         __syncthreads();
         ph(2 + min(l, 2));
@@ -902,7 +892,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
             }
         };
         const int K16 = (rc + 15) & ~15;
-        rop_gemm<WIDE, false, false, true, true, true>(dout, din + (ones ? 1 : 0), K16, 0, Dl, ldd, kq, Xl,
+        rop_gemm<false, false, true, true, true>(dout, din + (ones ? 1 : 0), K16, 0, Dl, ldd, kq, Xl,
                                                        ldx, kxl, wepi);
         ph(1);
         // bias gradients without a ones column: column sums of delta / delta_dot, a wave per column
@@ -938,7 +928,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                     }
                 }
             };
-            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, 0, Dl, ldd, kq, W2, a.ldwm[l], kxl, pepi);
+            rop_gemm<true, false, true, true, true>(rc, din, kq, 0, Dl, ldd, kq, W2, a.ldwm[l], kxl, pepi);
             __syncthreads();
         } else if (a.du) {
             // d/du of (vec . grad): the input rows' delta_dot (no mask at the input)
@@ -950,7 +940,7 @@ __global__ __launch_bounds__(512) void net_rop_mfma_kernel(RopArgs a) {
                     if (m < rc) a.du[((int64_t)s * a.M + m0 + m) * D + q] = vy[r];
                 }
             };
-            rop_gemm<WIDE, true, false, true, true, true>(rc, din, kq, 0, Dl, ldd, kq, W2, a.ldwm[0], kxl, uepi);
+            rop_gemm<true, false, true, true, true>(rc, din, kq, 0, Dl, ldd, kq, W2, a.ldwm[0], kxl, uepi);
         }
         ph(6 + min(L - 1 - l, 2));
     }
@@ -1210,8 +1200,8 @@ static size_t rop_mfma_carve(const psvi_plan& p, int rows, RopArgs* a) {
 }
 
 constexpr size_t kRopLds = 160 * 1024;
-// psvi_debug_set(PSVI_DBG_ROP_VALU, v): 1 = the VALU R-op kernel, 2 = the
-// matrix-core one with rows of column tiles per unit (A/B)
+// psvi_debug_set(PSVI_DBG_ROP_VALU, 1): the VALU R-op kernel (the form for
+// row blocks past the LDS) on every shape (A/B)
 int g_rop_valu = 0;
 
 // rows per chunk that fit the LDS (0: the model's weights alone do not fit)
@@ -1246,10 +1236,8 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
     static bool once = [] {
         (void)hipFuncSetAttribute((const void*)net_rop_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRopLds);
-        for (const void* f : {(const void*)net_rop_mfma_kernel<false, false>,
-                              (const void*)net_rop_mfma_kernel<false, true>,
-                              (const void*)net_rop_mfma_kernel<true, false>,
-                              (const void*)net_rop_mfma_kernel<true, true>})
+        for (const void* f : {(const void*)net_rop_mfma_kernel<false>,
+                              (const void*)net_rop_mfma_kernel<true>})
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRopLds);
         return true;
     }();
@@ -1271,14 +1259,10 @@ hipError_t launch_net_rop(const psvi_plan& p, const float* u, const int32_t* z, 
             a.single = 1;
             const dim3 grid(p.d.S, a.nsplit), block(512);
             const bool fc = p.family == PSVI_FAMILY_FULLCOV;
-            if (g_rop_valu == 2 && fc)
-                hipLaunchKernelGGL((net_rop_mfma_kernel<true, true>), grid, block, lds, st, a);
-            else if (g_rop_valu == 2)
-                hipLaunchKernelGGL((net_rop_mfma_kernel<true, false>), grid, block, lds, st, a);
-            else if (fc)
-                hipLaunchKernelGGL((net_rop_mfma_kernel<false, true>), grid, block, lds, st, a);
+            if (fc)
+                hipLaunchKernelGGL((net_rop_mfma_kernel<true>), grid, block, lds, st, a);
             else
-                hipLaunchKernelGGL((net_rop_mfma_kernel<false, false>), grid, block, lds, st, a);
+                hipLaunchKernelGGL((net_rop_mfma_kernel<false>), grid, block, lds, st, a);
             if (a.nsplit > 1 && sum_slots) {
                 const int64_t n = (int64_t)p.d.S * p.n_tot;
                 hipLaunchKernelGGL(slot_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,

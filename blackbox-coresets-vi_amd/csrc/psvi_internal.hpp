@@ -49,6 +49,37 @@ __device__ __forceinline__ float row16_max(float v) {
     v = fmaxf(v, dppf<0x121>(v));
     return v;
 }
+// max / sum over the first W lanes of each aligned group of W (W = 2, 4:
+// quad permutes; 16: the row reductions above); the result is valid on those
+// lanes
+template <int W>
+__device__ __forceinline__ float lanes_max(float v) {
+    static_assert(W == 2 || W == 4 || W == 16, "2, 4 or 16 lanes");
+    if constexpr (W == 16) {
+        v = fmaxf(v, dppf<0x128>(v));
+        v = fmaxf(v, dppf<0x124>(v));
+        v = fmaxf(v, dppf<0x122>(v));
+        return fmaxf(v, dppf<0x121>(v));
+    } else {
+        v = fmaxf(v, dppf<0xB1>(v));              // quad_perm [1, 0, 3, 2]: lane ^ 1
+        if constexpr (W == 4) v = fmaxf(v, dppf<0x4E>(v));  // quad_perm [2, 3, 0, 1]: lane ^ 2
+        return v;
+    }
+}
+template <int W>
+__device__ __forceinline__ float lanes_sum(float v) {
+    static_assert(W == 2 || W == 4 || W == 16, "2, 4 or 16 lanes");
+    if constexpr (W == 16) {
+        v += dppf<0x128>(v);
+        v += dppf<0x124>(v);
+        v += dppf<0x122>(v);
+        return v + dppf<0x121>(v);
+    } else {
+        v += dppf<0xB1>(v);
+        if constexpr (W == 4) v += dppf<0x4E>(v);
+        return v;
+    }
+}
 __device__ __forceinline__ float row16_sum(float v) {
     v += dppf<0x128>(v);  // row_ror:8
     v += dppf<0x124>(v);  // row_ror:4

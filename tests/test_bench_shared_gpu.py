@@ -4,9 +4,10 @@ The driver's scaling run (N = 2, 4, 8 under torchrun, one rank per GPU over
 RCCL) is the first time the N > 1 bench meets hardware.  This test launches
 the same command under torchrun with every rank on device 0 and the
 collectives over gloo (``--comm gloo --share-gpu``, host-staged: RCCL takes one
-rank per GPU), so every HIP path the scaling run takes -- the weak-scaled
-headline (rows of L x samples, two all_to_alls per step), the C4 leg, the C5
-leg (LeNet samples split over ranks, psvi_hvp_partial + all-reduce, a sharded
+rank per GPU), so every HIP path the scaling run takes -- the C4 headline
+(strong scaling: rows of L x samples, two all_to_alls per step), the one-GPU
+C4 reference of rank 0, the weak-scaled C3 shards, the data-parallel
+alternative, the C5 leg (LeNet samples split over ranks, psvi_hvp_partial + all-reduce, a sharded
 hyper_step) -- executes here at full size and must produce a finite rank-0 JSON
 line with every key.  Timings from such a run mean nothing."""
 import json
@@ -41,12 +42,17 @@ def test_bench_multi_rank_on_one_gpu(world):
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     print(json.dumps(out)[:3000])
-    assert out["n_gpus"] == world and out["config"]["S_total"] == 128 * world
+    assert out["n_gpus"] == world and out["config"]["S_total"] == 1024 and out["config"]["M"] == 200
+    assert out["scaling"] == "strong" and out["config"]["workload"].startswith("C4")
     assert out["config"]["elbo_finite"] and out["value"] > 0
+    assert abs(out["value"] - 1e3 / out["ms_per_step"]) <= 1e-3 * out["value"] + 0.01
     assert out["config"]["comm"].startswith("gloo")
-    assert out["c4"]["elbo_finite"] and out["c4"]["inner_steps_per_s"] > 0
+    one = out["c4_1gpu"]
+    assert one["inner_steps_per_s"] > 0
+    assert out["speedup_over_1gpu"] == round(out["value"] / one["inner_steps_per_s"], 3)
+    assert out["weak"]["elbo_finite"] and out["weak"]["inner_steps_per_s"] > 0
     c5 = out["lenet_c5"]
     assert c5["elbo_finite"] and c5["gpu_inner_steps_per_s"] > 0
     assert c5["gpu_hvp_ms"] > 0 and c5["hyper_step_loss_finite"]
     dp = out["dp_alternative"]   # the data-parallel alternative to the row-sharded step
-    assert dp is not None and dp["inner_steps_per_s"] > 0 and dp["value"] > 0
+    assert dp is not None and dp["inner_steps_per_s"] > 0 and "C4" in dp["config"]

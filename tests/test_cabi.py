@@ -11,10 +11,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "psvi_hip.h")
+# the library's diagnostics (not the drop-in interface): exported for tools
+DIAG = os.path.join(ROOT, "blackbox-coresets-vi_amd", "csrc", "psvi_diag.h")
 
 
-def header_functions():
-    text = open(HEADER).read()
+def header_functions(path=HEADER):
+    text = open(path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(psvi_\w+)\s*\(", text, re.M)))
 
@@ -31,10 +33,13 @@ def test_library_exports_every_declared_symbol():
     from psvi.runtime import _lib
 
     lib = _lib.load()
-    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    missing = [f for f in header_functions() + header_functions(DIAG) if not hasattr(lib, f)]
     assert not missing, missing
     # the Python binding declares a signature for each of them, and nothing else
-    assert sorted(_lib.SIGNATURES) == header_functions()
+    assert sorted(_lib.SIGNATURES) == sorted(header_functions() + header_functions(DIAG))
+    # the diagnostics stay out of the public header
+    assert not any(f.startswith("psvi_debug") for f in header_functions())
+    assert "PSVI_DBG_" not in open(HEADER).read()
 
 
 def test_symbols_are_c_abi_unmangled():

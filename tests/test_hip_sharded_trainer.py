@@ -157,8 +157,7 @@ def test_c5_outer_world8_decomposition_identical_params():
     sample shards of 32 (psvi_outer_elbo_grad_coef with the global softmax
     coefficients, as ShardedOuter runs it).  Same parameters, same draw: the
     two decompositions differ by fp32 summation order only, so d/du and the
-    parameter gradient must agree tightly (measured 2e-7,
-    tools/c5_outer_probe.py) -- the check the hyper_step comparison above
+    parameter gradient must agree tightly (measured 2e-7) -- the check the hyper_step comparison above
     cannot make through the softmax's sensitivity."""
     from psvi.models import LENET_LAYERS, make_lenet
     from psvi.runtime import InnerLoopPlan, randn_

@@ -19,12 +19,8 @@ def main():
     ap.add_argument("--T", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--hvp", type=int, default=0, help="also time N psvi_hvp calls")
-    ap.add_argument("--gemm-valu", action="store_true",
-                    help="head GEMMs on the VALU kernel (PSVI_DBG_LENET_GEMM_VALU, A/B)")
     ap.add_argument("--abl", type=int, default=0,
                     help="PSVI_DBG_LENET_ABLATION mask (timing diagnostics)")
-    ap.add_argument("--conv-valu", action="store_true",
-                    help="conv towers on the VALU kernels (PSVI_DBG_LENET_CONV_VALU, A/B)")
     a = ap.parse_args()
     from psvi.models import make_lenet
     from psvi.runtime import InnerLoopPlan
@@ -34,8 +30,6 @@ def main():
     params = torch.nn.utils.parameters_to_vector(net.parameters()).detach().cuda()
     plan = InnerLoopPlan("lenet", [(25, 6), (150, 16), (400, 120), (120, 84), (84, 10)],
                          a.S, a.M)
-    plan.lib.psvi_debug_set(13, 1 if a.gemm_valu else 0)
-    plan.lib.psvi_debug_set(16, 1 if a.conv_valu else 0)
     plan.lib.psvi_debug_set(17, a.abl)
     u = torch.randn(a.M, 1, 28, 28, device="cuda")
     z = torch.randint(0, 10, (a.M,), device="cuda", dtype=torch.int32)

@@ -41,7 +41,7 @@ def report(name, t, abl, S):
         # wave 0's finer marks: 4 setup done, 5 load loop done (its own loads
         # landed and stored), 1 barrier; 6/7/8 forward layers of tile 0, 9 loss
         # head, 10 backward propagation, 2 barrier
-        for k, nm in ((4, "setup"), (5, "load loop"), (1, "load barrier"), (6, "fwd l0"), (7, "fwd l1"),
+        for k, nm in ((4, "setup"), (11, "loads issued"), (5, "load loop"), (1, "load barrier"), (6, "fwd l0"), (7, "fwd l1"),
                       (8, "fwd l2"), (9, "head"), (10, "bwd"), (2, "chain barrier")):
             print(f"    wave0 @ {nm:13s} {float(d[:, k].median()):8.0f}")
         sk = (r[:, 15].double() - r[:, 0].double())
