@@ -311,7 +311,7 @@ def fn2_inputs(layers, M, dev, seed):
     return u.to(dev), z.to(dev), torch.full((M,), N_DATA / M, device=dev)
 
 
-def sharded_steps(rt, loop, u, z, w, params, m, v, seed, k0, n, parts=None, ev=None):
+def sharded_steps(rt, loop, u, z, w, params, m, v, seed, k0, n, parts=None, ev=None, overlap=False):
     """n sharded inner steps (Adam steps k0 + 1 ..) -- ShardedInnerLoop.run:
     full-cov x all_to_all, network, G all_to_all, the update fused with the
     next step's sample, the next eps drawn by the network launch
@@ -320,10 +320,11 @@ def sharded_steps(rt, loop, u, z, w, params, m, v, seed, k0, n, parts=None, ev=N
     4 events} around the exchanges + network and the update + sample."""
     stride = (loop.plan.eps_count + 3) // 4 * 4
     loop.run(u, z, w, params, m, v, n, LR, step0=k0 + 1, seed=seed, offset=k0 * stride,
-             elbo_parts=None if parts is None else parts[k0:k0 + n], phase_events=ev)
+             elbo_parts=None if parts is None else parts[k0:k0 + n], phase_events=ev,
+             overlap=overlap)
 
 
-def sharded_timed(rt, steps, warmup, layers, S, M, ev_every=5, seed=20251015):
+def sharded_timed(rt, steps, warmup, layers, S, M, ev_every=5, seed=20251015, overlap=False):
     """K timed sharded inner steps of fn2 at (S, M) after W warm-up steps
     (ShardedInnerLoop.run: rows of L (whole 64-row bands) x samples sharded,
     two all_to_alls per step), the timed call continuing the warm-up's Philox
@@ -336,15 +337,16 @@ def sharded_timed(rt, steps, warmup, layers, S, M, ev_every=5, seed=20251015):
     m, v = torch.zeros_like(params), torch.zeros_like(params)
     total = warmup + steps
     parts = torch.zeros(total, 2, dtype=torch.float64, device=rt.dev)
-    sharded_steps(rt, loop, u, z, w, params, m, v, seed, 0, warmup, parts)
+    sharded_steps(rt, loop, u, z, w, params, m, v, seed, 0, warmup, parts, overlap=overlap)
     elapsed = rt.timed(lambda: sharded_steps(rt, loop, u, z, w, params, m, v, seed,
-                                             warmup, steps, parts))
+                                             warmup, steps, parts, overlap=overlap))
     # the per-phase split: HIP events between the launches of a separate call
     # (outside the timed region), every ev_every-th of 50 steps
     nph = 50
     ev = {k: [rt.event() for _ in range(4)] for k in range(nph) if k % ev_every == 0}
     pp, mm, vv = params.clone(), m.clone(), v.clone()
-    loop.run(u, z, w, pp, mm, vv, nph, LR, step0=total + 1, seed=seed + 1, phase_events=ev)
+    loop.run(u, z, w, pp, mm, vv, nph, LR, step0=total + 1, seed=seed + 1, phase_events=ev,
+             overlap=overlap)
     rt.sync()
     ph = {"exchange+net": [], "update+sample": []}
     for e in ev.values():
@@ -715,6 +717,7 @@ def run(rt, args, shapes=None):
     # (K = 20 steps, ~1.4 ms, in the driver's run) starts on a GPU at its
     # working clocks rather than straight after process start-up
     c4 = None
+    schedules = None
     if world == 1:
         prep = headline_prep(rt, args) if shapes is None else None
         if not args.no_c4:
@@ -725,8 +728,20 @@ def run(rt, args, shapes=None):
         S, Mh, layers = sh["s_per_gpu"], sh["M"], sh["layers"]
     else:
         S, Mh, layers = c4sh["S"], c4sh["M"], c4sh["layers"]
-        log(f"C4 headline over {world} ranks")
-        elapsed, parts, avg_ms, loop = sharded_timed(rt, args.steps, args.warmup, layers, S, Mh)
+        # two complete schedules of the same step (ShardedInnerLoop.run): the
+        # exchanges in series with the network, and overlapped with it (sample
+        # halves, x(B) beside net(A), G(A) beside net(B)); the headline is the
+        # faster, both are reported
+        sched = {}
+        for ov in (False, True):
+            log(f"C4 headline over {world} ranks ({'overlapped' if ov else 'plain'} exchanges)")
+            r_ = sharded_timed(rt, args.steps, args.warmup, layers, S, Mh, overlap=ov)
+            sched["overlap" if ov else "plain"] = r_
+        pick = min(sched, key=lambda k: sched[k][0])
+        elapsed, parts, avg_ms, loop = sched[pick]
+        schedules = {k: {"inner_steps_per_s": round(args.steps / v_[0], 2),
+                         "ms_per_step": round(v_[0] / args.steps * 1e3, 4)} for k, v_ in sched.items()}
+        schedules["headline"] = pick
         elbo = loop.reduce_elbo(parts)
         pcount = loop.plan.param_count
         cold = None
@@ -855,7 +870,8 @@ def run(rt, args, shapes=None):
                    "adam": "robust_higher DifferentiableAdam", "elbo_finite": finite,
                    "timed_call": ("continues the warm-up call (resident loop state)"
                                   if world == 1 and args.warmup else "continues the warm-up's "
-                                  "Philox stream and Adam steps")},
+                                  "Philox stream and Adam steps"),
+                   "exchange_schedules": schedules},
         "cold_call": cold,
         "speedup_over_1gpu": None if world == 1 or one is None else one["speedup_of_headline"],
         "roofline": roofline,

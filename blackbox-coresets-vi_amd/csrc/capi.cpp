@@ -28,6 +28,7 @@ extern int g_stream_bf_off;              // kernels_mvn.hip
 extern unsigned long long* g_bf_stamps;  // kernels_mvn.hip
 extern int g_ks_off;                     // kernels_mvn.hip
 extern int g_fs_off;                     // kernels_mvn.hip
+extern int g_fwd_pair_fp32;                // kernels_mvn.hip
 extern int g_fs_bf_off;                  // kernels_mvn.hip
 extern int g_ks_bf_off;                  // kernels_mvn.hip
 static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
@@ -621,6 +622,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_KSTREAM_WGS: g_ks_wgs = value; return 0;
         case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
         case PSVI_DBG_FWD_SEG_BF_OFF: g_fs_bf_off = value; return 0;
+        case PSVI_DBG_FWD_PAIR_FP32: g_fwd_pair_fp32 = value; return 0;
         case PSVI_DBG_KSTREAM_BF_OFF: g_ks_bf_off = value; return 0;
         case PSVI_DBG_ROP_VALU: g_rop_valu = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
@@ -928,6 +930,9 @@ int psvi_plan_query(const psvi_plan* p, int32_t key, int64_t* value) {
         case PSVI_Q_OUTER_WS_BYTES: *value = (int64_t)outer_ws(p, nullptr).bytes; break;
         case PSVI_Q_HVP_WS_BYTES: *value = (int64_t)hvp_ws(p, nullptr).bytes; break;
         case PSVI_Q_EVAL_WS_BYTES: *value = (int64_t)eval_ws_bytes(p); break;
+        case PSVI_Q_NET_PART_OK:
+            *value = p->family == PSVI_FAMILY_FULLCOV && !(p->mchunks > 1 && !p->net_mloop);
+            break;
         default: return fail(PSVI_EINVAL, "unknown query key");
     }
     return 0;
@@ -1115,6 +1120,32 @@ int psvi_mvn_phase_net_draw(const psvi_plan* p, const float* u, const int32_t* z
     hipStream_t st = as_stream(stream);
     HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x_recv, g_send, nll_out, st, eps_out, n,
                        seed, offset));
+    return 0;
+}
+
+int psvi_mvn_phase_net_part(const psvi_plan* p, const float* u, const int32_t* z, const float* w,
+                            const float* x_recv, float* g_send, double* nll_out, int32_t s_begin,
+                            int32_t s_count, float* eps_out, int64_t n, uint64_t seed,
+                            uint64_t offset, int32_t part, int32_t nparts, void* stream) {
+    drop_resident(p);
+    if (!p || p->family != PSVI_FAMILY_FULLCOV) return fail(PSVI_ESTATE, "not a full-cov plan");
+    if (!p->on_device) return fail(PSVI_ESTATE, "plan was created without a HIP device");
+    const int S_loc = p->s_cnt[p->rank];
+    if (s_begin < 0 || s_count < 0 || s_begin + s_count > S_loc)
+        return fail(PSVI_EINVAL, "sample range outside the rank's samples");
+    if (nparts < 1 || part < 0 || part >= nparts) return fail(PSVI_EINVAL, "bad draw part");
+    if (!u || !z || !w || (s_count > 0 && (!x_recv || !g_send)) || !nll_out || n < 0 ||
+        (n > 0 && !eps_out))
+        return fail(PSVI_EINVAL, "null pointer or bad count");
+    if (offset % 4) return fail(PSVI_EINVAL, "randn offset must be a multiple of 4");
+    if (eps_out && reinterpret_cast<uintptr_t>(eps_out) % 16)
+        return fail(PSVI_EINVAL, "eps_out must be 16-byte aligned");
+    if (p->mchunks > 1 && !p->net_mloop && (s_begin != 0 || s_count != S_loc))
+        return fail(PSVI_EUNSUP, "per-chunk gradient slots: whole sample launches only");
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(launch_net(*p, u, z, w, nullptr, nullptr, nullptr, x_recv, g_send, nll_out, st,
+                       n > 0 ? eps_out : nullptr, n, seed, offset, nullptr, nullptr, s_begin, s_count,
+                       part, nparts));
     return 0;
 }
 
@@ -1632,6 +1663,38 @@ int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m,
     if (hp->step < 1) return fail(PSVI_EINVAL, "adam step must be >= 1");
     if (hp->kind < 0 || hp->kind > 2) return fail(PSVI_EINVAL, "unknown adam kind");
     HIP_TRY(launch_adam(n, params, grad, adam_m, adam_v, hp, as_stream(stream)));
+    return 0;
+}
+
+size_t psvi_cg_ws_bytes(void) { return cg_ws_bytes(); }
+
+int psvi_cg_scale(int64_t n, const float* hv, double lr, float* out, void* stream) {
+    if (n < 0 || !hv || !out) return fail(PSVI_EINVAL, "bad cg_scale arguments");
+    HIP_TRY(launch_cg_scale(n, hv, lr, out, as_stream(stream)));
+    return 0;
+}
+
+int psvi_cg_pap(int64_t n, const float* hv1, const float* hv2, double lr, const double* p,
+                double* state, void* ws, size_t ws_bytes, void* stream) {
+    if (n < 0 || !hv1 || !hv2 || !p || !state || !ws) return fail(PSVI_EINVAL, "bad cg_pap arguments");
+    if (ws_bytes < cg_ws_bytes()) return fail(PSVI_EINVAL, "cg workspace too small");
+    HIP_TRY(launch_cg_pap(n, hv1, hv2, lr, p, state, ws, as_stream(stream)));
+    return 0;
+}
+
+int psvi_cg_residual(int64_t n, const float* hv1, const float* hv2, double lr, double* r,
+                     double* state, double tol, void* ws, size_t ws_bytes, void* stream) {
+    if (n < 0 || !hv1 || !hv2 || !r || !state || !ws)
+        return fail(PSVI_EINVAL, "bad cg_residual arguments");
+    if (ws_bytes < cg_ws_bytes()) return fail(PSVI_EINVAL, "cg workspace too small");
+    HIP_TRY(launch_cg_residual(n, hv1, hv2, lr, r, state, tol, ws, as_stream(stream)));
+    return 0;
+}
+
+int psvi_cg_update(int64_t n, double* x, double* p, float* p32, const double* r,
+                   const double* state, void* stream) {
+    if (n < 0 || !x || !p || !p32 || !r || !state) return fail(PSVI_EINVAL, "bad cg_update arguments");
+    HIP_TRY(launch_cg_update(n, x, p, p32, r, state, as_stream(stream)));
     return 0;
 }
 

@@ -1164,6 +1164,13 @@ __global__ __launch_bounds__(256, MODE == 2 || FUSE ? 2 : 3) void mvn_update_ker
 // epilogue -- the in-launch split-K combine of cdna_hip_programming.md (§6
 // Guideline 16, counter form), correct for any placement of the contributors.
 // No workgroup ever waits on another: the kernel cannot hang on the hand-off.
+// The ticket stays relaxed on purpose: sc1 stores + the vmcnt(0) drain before
+// the add is the first row of MI355X_MICROARCH.md's hand-off table (release by
+// drain, acquire by sc1 loads); an acq_rel atomic would add an L2 writeback /
+// invalidate per contributor (1.7 - 3.5 us per launch at C4 W = 8) for no
+// ordering the drain does not give.  The last arriver resets the counter in
+// the same launch; an aborted launch ends the process, so no half-counted
+// ticket reaches a later launch.
 struct KsArgs {
     const KsTile* tiles;
     const KsSeg* segs;
@@ -2638,6 +2645,7 @@ int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked k
 int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
 int g_ks_bf_off = 0;   // psvi_debug_set(PSVI_DBG_KSTREAM_BF_OFF, 1): the fp32 K-split update (A/B)
 int g_fs_bf_off = 0;   // psvi_debug_set(PSVI_DBG_FWD_SEG_BF_OFF, 1): the fp32 segmented sample (A/B)
+int g_fwd_pair_fp32 = 0;  // psvi_debug_set(PSVI_DBG_FWD_PAIR_FP32, 1): the HVP's sample pair on the fp32 item grid (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -2995,6 +3003,13 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float* params,
                                float* x, const float* vec, float* x2, float* part2,
                                hipStream_t st) {
+    if (p.n_fswg > 0 && !g_fs_off && !g_fs_bf_off && !g_fwd_pair_fp32) {
+        // the segmented sample on bf16 pieces (fp32-faithful), twice on the
+        // plan's slots: x, then the tangent x2 with the diagonal from params
+        // (C3: 2 x (seg + reduce) against the fp32 item-grid pair's 38.5 + 7.6 us)
+        if (hipError_t e = launch_mvn_fwd(p, eps, params, x, st)) return e;
+        return launch_mvn_fwd(p, eps, vec, x2, st, params);
+    }
     FwdArgs a{};
     a.items = p.d_fwd;
     a.params = params;

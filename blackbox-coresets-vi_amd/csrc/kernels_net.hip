@@ -113,6 +113,10 @@ struct NetArgs {
     const NetBand* bands;
     int nbands, bbase[kMaxL];
     int mloop;  // pseudopoint chunks looped inside one workgroup (1: none)
+    // this launch's local samples [s_begin, s_begin + gridDim.x) (the sharded
+    // loop's sample halves); the fused draw's part rn_part of rn_nparts
+    // contiguous quad ranges
+    int s_begin, rn_part, rn_nparts;
     // the fused draw also as bf16 planes (the bf16-plane streaming update)
     const EpsPlanes* rn_P;
     uint16_t* rn_planes;
@@ -468,7 +472,7 @@ __global__ __launch_bounds__(512) void net_kernel(NetArgs a) {
     const int nthr = Geo::kFixed ? 512 : (int)blockDim.x;
     static_assert(!VEC || FAM == PSVI_FAMILY_FULLCOV, "float4 loads: the full-cov x row");
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int s = blockIdx.x;                 // local sample
+    const int s = blockIdx.x + a.s_begin;     // local sample
     const int sg = a.s_goff + s;              // global sample (eps indexing)
     const int role = blockIdx.y;
     const int L = g.L(), Mp = g.Mp();
@@ -1162,16 +1166,17 @@ chunk_top:  // a backward jump only when MLOOP (no loop at all in the other inst
         // the next step's normals (psvi_randn's stream), split over the grid's
         // workgroups.  Last, so that no s_waitcnt of the phases above waits for
         // these stores to retire.
-        const int64_t nq = (a.rn_n + 3) / 4;
+        const int64_t nqa = (a.rn_n + 3) / 4;
+        const int64_t qlo = nqa * a.rn_part / a.rn_nparts, nq = nqa * (a.rn_part + 1) / a.rn_nparts;
         const int nblk = gridDim.x * gridDim.y * gridDim.z;
         const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-        const int64_t per = (nq + nblk - 1) / nblk, q1 = min(nq, (b + 1) * per);
+        const int64_t per = (nq - qlo + nblk - 1) / nblk, q1 = min(nq, qlo + (b + 1) * per);
         if (a.rn_planes) {
             const EpsPlanes P = *a.rn_P;
-            for (int64_t q = b * per + tid; q < q1; q += nthr)
+            for (int64_t q = qlo + b * per + tid; q < q1; q += nthr)
                 randn_quad_planes(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q, P, a.rn_planes);
         } else {
-            for (int64_t q = b * per + tid; q < q1; q += nthr)
+            for (int64_t q = qlo + b * per + tid; q < q1; q += nthr)
                 randn_quad<true>(a.rn_out, a.rn_n, a.rn_seed, a.rn_off, q);
         }
     }
@@ -1366,8 +1371,17 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
                       const float* params, const float* eps, float* mf_slots,
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out, int64_t rn_n, uint64_t rn_seed, uint64_t rn_off,
-                      const NetOuter* outer, uint16_t* rn_planes) {
+                      const NetOuter* outer, uint16_t* rn_planes, int s_begin, int s_count,
+                      int rn_part, int rn_nparts) {
     NetArgs a{};
+    const int S_loc = p.s_cnt[p.rank];
+    if (s_count < 0) s_count = S_loc - s_begin;
+    if (s_begin < 0 || s_count < 0 || s_begin + s_count > S_loc || rn_nparts < 1 || rn_part < 0 ||
+        rn_part >= rn_nparts)
+        return hipErrorInvalidValue;
+    a.s_begin = s_begin;
+    a.rn_part = rn_part;
+    a.rn_nparts = rn_nparts;
     if (outer) {
         a.outer = outer->mode;
         a.n_pseudo = outer->n_pseudo;
@@ -1437,14 +1451,18 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
     a.mloop = loop ? p.mchunks : 1;
     if (loop) a.gslot = nullptr;
     // the outer forward pass has no backward: one role
-    dim3 grid(p.s_cnt[p.rank], a.outer == 1 ? 1 : p.net_roles, loop ? 1 : p.mchunks),
+    dim3 grid(s_count, a.outer == 1 ? 1 : p.net_roles, loop ? 1 : p.mchunks),
         block(p.net_threads);
-    // a rank without samples still owes the next step's draw (every rank
-    // passes the same global eps to its update): the draw on its own
-    if (p.s_cnt[p.rank] == 0)
-        return rn_out && rn_n > 0 ? launch_randn(rn_out, rn_n, rn_seed, rn_off, st, nullptr, 0,
-                                                 rn_planes ? &p.eps_planes : nullptr, rn_planes)
-                                  : hipSuccess;
+    // a launch without samples still owes its part of the next step's draw
+    // (every rank passes the same global eps to its update): the draw on its
+    // own (the whole of it when this is its only part)
+    if (s_count == 0) {
+        if (!rn_out || rn_n <= 0 || rn_part > 0) return hipSuccess;
+        return launch_randn(rn_out, rn_n, rn_seed, rn_off, st, nullptr, 0,
+                            rn_planes ? &p.eps_planes : nullptr, rn_planes);
+    }
+    // per-chunk slots are summed over all the rank's samples: whole launches only
+    if (a.gslot && a.outer != 1 && (s_begin != 0 || s_count != S_loc)) return hipErrorInvalidValue;
     const bool fn2 = net_vec_ok(p) && net_fn2_geo(p);
     if (fn2 && p.world > 1 && a.nbands != kFn2Bands) return hipErrorInvalidValue;
     if (p.family == PSVI_FAMILY_MEANFIELD)
@@ -1469,9 +1487,10 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false, true>), grid, block, p.net_lds, st, a);
     else
         hipLaunchKernelGGL((net_kernel<PSVI_FAMILY_FULLCOV, false>), grid, block, p.net_lds, st, a);
-    if (a.gslot && a.outer != 1)
+    if (a.gslot && a.outer != 1) {
         hipLaunchKernelGGL(net_slot_sum_kernel, dim3((unsigned)((a.gsz + 255) / 256)), dim3(256), 0,
                            st, (const float*)a.gslot, p.mchunks, a.gsz, gsend);
+    }
     return hipGetLastError();
 }
 

@@ -566,7 +566,8 @@ hipError_t launch_net(const psvi_plan& p, const float* u, const int32_t* z, cons
                       const float* xrecv, float* gsend, double* nll_out, hipStream_t st,
                       float* rn_out = nullptr, int64_t rn_n = 0, uint64_t rn_seed = 0,
                       uint64_t rn_off = 0, const NetOuter* outer = nullptr,
-                      uint16_t* rn_planes = nullptr);
+                      uint16_t* rn_planes = nullptr, int s_begin = 0, int s_count = -1,
+                      int rn_part = 0, int rn_nparts = 1);
 // acc == nullptr: the accumulators come from the plan's mean-field gradient
 // slots, reduced in a fixed order against slot_eps (the step's eps)
 hipError_t launch_mf_update(const psvi_plan& p, const float* acc, float* params,
@@ -657,6 +658,15 @@ hipError_t launch_lenet_hvp(const psvi_plan& p, const float* u, const int32_t* z
                             float* d_u, float* d_w, void* tws, hipStream_t st,
                             bool include_kl = true);
 hipError_t launch_nonfinite(const void* x, int64_t n, int dtype, int32_t* flag, hipStream_t st);
+// hyper_step's conjugate-gradient iteration (kernels_cg.hip)
+size_t cg_ws_bytes();
+hipError_t launch_cg_scale(int64_t n, const float* hv, double lr, float* out, hipStream_t st);
+hipError_t launch_cg_pap(int64_t n, const float* hv1, const float* hv2, double lr, const double* p,
+                         double* state, void* ws, hipStream_t st);
+hipError_t launch_cg_residual(int64_t n, const float* hv1, const float* hv2, double lr, double* r,
+                              double* state, double tol, void* ws, hipStream_t st);
+hipError_t launch_cg_update(int64_t n, double* x, double* p, float* p32, const double* r,
+                            const double* state, hipStream_t st);
 // Hessian-vector products (kernels_rop.hip)
 int rop_rows(const psvi_plan& p);
 int rop_splits(const psvi_plan& p);  // row blocks per sample: G / G_dot slots

@@ -983,50 +983,40 @@ class PSVI:
     def _cg_normaleq(self, hvp, draw_inner, g_w, lr, K, sync_every=1):
         """CG_normaleq's linear solve (hypergradients.py:199-244, CG_torch.py:9-45);
         returns the draw of w_mapped, leaves the solution in self._cg_x.
-        The stopping test runs on the device (psvi.hypergrad.CG_torch.cg):
-        x, r, p freeze where the reference breaks, and the host leaves the
-        loop when it reads the flag, every ``sync_every`` iterations (1: the
-        reference's number of A calls, hence of draws)."""
+        The iteration's vector work runs fused on the device
+        (psvi.runtime.cg.DeviceCG: psvi_cg_*), its stopping test too: x and p
+        freeze where the reference breaks, and the host leaves the loop when
+        it reads the flag, every ``sync_every`` iterations (1: the reference's
+        number of A calls, hence of draws)."""
+        from psvi.runtime.cg import DeviceCG
+
         eA = draw_inner()                       # w_mapped = fp_map(params, hparams)
 
-        def hv32(e, x):                         # H x (fp32, as psvi_hvp returns it)
-            return hvp(e, x, f64=False)[0]
+        def hv_a(x32):                          # H_A x (fp32, as psvi_hvp returns it)
+            return hvp(eA, x32, f64=False)[0]
 
-        def jvp(x):                             # J x = x - lr H x (fp_map drawn twice)
+        def hv_b(x32):                          # J's product: fp_map drawn twice
             draw_inner()
-            return torch.sub(x, hv32(draw_inner(), x), alpha=lr)  # fp32 H x promoted in the one pass
+            return hvp(draw_inner(), x32, f64=False)[0]
 
-        # lr as a one-element float64 tensor: lr * (fp32 H x) promotes to
-        # float64 in one pass (a 0-dim operand would not promote)
-        lr_t = torch.full((1,), lr, dtype=torch.float64, device=g_w.device)
+        # b = g_w - J g_w, J g_w = g_w - lr H g_w (fp32 H g_w promoted in the one pass)
+        b = g_w - torch.sub(g_w, hv_b(g_w.to(torch.float32)), alpha=lr)
+        if not b.is_cuda:
+            # host tensors (the CPU rehearsals of the sharded trainers, whose
+            # plans are stand-ins): the same iteration in torch
+            from psvi.hypergrad.CG_torch import cg as torch_cg
 
-        def A(x):                               # dfp_map_dw
-            vmj = torch.mul(hv32(eA, x), lr_t)
-            return vmj - jvp(vmj)
+            def A(xs):
+                vmj = hv_a(xs[0].to(torch.float32)).to(torch.float64) * lr
+                return [vmj - torch.sub(vmj, hv_b(vmj.to(torch.float32)), alpha=lr)]
 
-        b = g_w - jvp(g_w)
-        # CG_torch.cg(Ax, b, max_iter=K, epsilon=1e-10) with fused x + a y passes
-        # and 0-dim device step lengths; where the reference breaks, the step
-        # length is zeroed and r, p, rTr keep their values
-        xk = torch.zeros_like(b)
-        r = b.clone()
-        pk = r.clone()
-        rTr = torch.dot(r, r)
-        done = torch.zeros((), dtype=torch.bool, device=b.device)
-        zero = torch.zeros((), dtype=b.dtype, device=b.device)
-        sync_every = max(1, int(sync_every))
-        for it in range(int(K)):
-            Ap = A(pk)
-            alpha = rTr / torch.dot(pk, Ap)
-            rn = torch.addcmul(r, alpha, Ap, value=-1)
-            rnrn = torch.dot(rn, rn)
-            done = done | (torch.sqrt(rnrn) < 1e-10)
-            xk = torch.addcmul(xk, torch.where(done, zero, alpha), pk)
-            r = torch.where(done, r, rn)
-            pk = torch.where(done, pk, torch.addcmul(r, rnrn / rTr, pk))
-            rTr = torch.where(done, rTr, rnrn)
-            if (it + 1) % sync_every == 0 and bool(done):
-                break
+            self._cg_x = torch_cg(A, [b], max_iter=int(K), epsilon=1e-10,
+                                  sync_every=sync_every)[0]
+            return eA
+        cg = getattr(self, "_cg_dev", None)
+        if cg is None or cg.n != b.numel() or cg.state.device != b.device:
+            cg = self._cg_dev = DeviceCG(b.numel(), b.device)
+        xk = cg.solve(hv_a, hv_b, b.contiguous(), lr, K, tol=1e-10, sync_every=sync_every)
         self._cg_x = xk
         return eA
 

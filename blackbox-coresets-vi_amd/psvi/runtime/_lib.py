@@ -35,6 +35,7 @@ Q_TILED_FLOATS = 11
 Q_OUTER_WS_BYTES = 12
 Q_HVP_WS_BYTES = 13
 Q_EVAL_WS_BYTES = 14
+Q_NET_PART_OK = 15
 
 ERRORS = {-1: "PSVI_EINVAL", -2: "PSVI_ENOSPC", -3: "PSVI_EUNSUP", -4: "PSVI_ESTATE"}
 
@@ -81,6 +82,8 @@ SIGNATURES = {
     "psvi_mvn_phase_sample": (_I32, [_P, _P, _P, _P, _P]),
     "psvi_mvn_phase_net": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "psvi_mvn_phase_net_draw": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _U64, _U64, _P]),
+    "psvi_mvn_phase_net_part": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _P, _I64, _U64, _U64,
+                                       _I32, _I32, _P]),
     "psvi_mvn_phase_update": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P, _P,
                                      _I32, _P]),
     "psvi_mvn_phase_update_sample": (_I32, [_P, _P, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P,
@@ -105,6 +108,12 @@ SIGNATURES = {
     "psvi_randn": (_I32, [_P, _I64, _U64, _U64, _P]),
     "psvi_nonfinite": (_I32, [_P, _I64, _I32, _P, _P]),
     "psvi_adam_update": (_I32, [_I64, _P, _P, _P, _P, ctypes.POINTER(AdamHP), _P]),
+    "psvi_cg_ws_bytes": (ctypes.c_size_t, []),
+    "psvi_cg_scale": (_I32, [_I64, _P, ctypes.c_double, _P, _P]),
+    "psvi_cg_pap": (_I32, [_I64, _P, _P, ctypes.c_double, _P, _P, _P, ctypes.c_size_t, _P]),
+    "psvi_cg_residual": (_I32, [_I64, _P, _P, ctypes.c_double, _P, _P, ctypes.c_double, _P,
+                                ctypes.c_size_t, _P]),
+    "psvi_cg_update": (_I32, [_I64, _P, _P, _P, _P, _P, _P]),
     "psvi_debug_set": (_I32, [_I32, _I32]),
     "psvi_debug_set_ptr": (_I32, [_I32, _P]),
     "psvi_debug_loop_timing": (_I32, [_P]),

@@ -118,6 +118,7 @@ class InnerLoopPlan:
         self.outer_ws_bytes = q(_lib.Q_OUTER_WS_BYTES)
         self.hvp_ws_bytes = q(_lib.Q_HVP_WS_BYTES)
         self.eval_ws_bytes = q(_lib.Q_EVAL_WS_BYTES)
+        self.net_part_ok = bool(q(_lib.Q_NET_PART_OK))
         self.eps_stride = (self.eps_count + 3) // 4 * 4   # Philox offset per loop step
         self.n_tot = sum(i * o + o for i, o in layers)
 
@@ -467,15 +468,25 @@ class InnerLoopPlan:
             _ptr(x_next), _stream()), "psvi_mvn_phase_update_tiled")
         _wrote(params, adam_m, adam_v, tstate)
 
-    def mvn_net(self, u, z, w, x_recv, g_send, nll_out, draw=None):
+    def mvn_net(self, u, z, w, x_recv, g_send, nll_out, draw=None, samples=None, draw_part=(0, 1)):
         """draw = (eps_out, seed, offset): the next step's global eps drawn in the
-        same launch (psvi_mvn_phase_net_draw; psvi_randn's values)."""
+        same launch (psvi_mvn_phase_net_draw; psvi_randn's values).  samples =
+        (s_begin, s_count): only those local samples (psvi_mvn_phase_net_part),
+        with part draw_part[0] of draw_part[1] of the draw."""
         _need(u, "u", self.M * self.in_features)
         _need(z, "z", self.M, torch.int32)
         _need(w, "w", self.M)
         _need(x_recv, "x_recv", self.xrecv_count)
         _need(g_send, "g_send", self.xrecv_count)
         _need(nll_out, "nll_out", 1, torch.float64)
+        if samples is not None:
+            out, seed, offset = draw if draw is not None else (None, 0, 0)
+            n = 0 if out is None else out.numel()
+            check(self.lib.psvi_mvn_phase_net_part(
+                self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv), _ptr(g_send), _ptr(nll_out),
+                int(samples[0]), int(samples[1]), _ptr(out), n, int(seed), int(offset),
+                int(draw_part[0]), int(draw_part[1]), _stream()), "psvi_mvn_phase_net_part")
+            return
         if draw is None:
             check(self.lib.psvi_mvn_phase_net(self.handle, _ptr(u), _ptr(z), _ptr(w), _ptr(x_recv),
                                               _ptr(g_send), _ptr(nll_out), _stream()),

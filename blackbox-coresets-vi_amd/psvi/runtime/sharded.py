@@ -48,6 +48,20 @@ def check_exchange(out, inp, out_splits, in_splits, world):
         raise ValueError(f"all_to_all: buffers on {out.device} and {inp.device}")
 
 
+def check_exchange_list(outs, ins, world):
+    """all_to_all_list's contract: one block per rank on each side, contiguous
+    float32, one device."""
+    for name, ts in (("outs", outs), ("ins", ins)):
+        if len(ts) != world:
+            raise ValueError(f"all_to_all {name}: {len(ts)} blocks for world {world}")
+        for t in ts:
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"all_to_all {name}: contiguous float32 blocks expected")
+    devs = {t.device for t in list(outs) + list(ins)}
+    if len(devs) > 1:
+        raise ValueError(f"all_to_all: blocks on {devs}")
+
+
 class TorchDistComm:
     """Collectives on torch.distributed (backend 'nccl' == RCCL on ROCm)."""
 
@@ -60,10 +74,39 @@ class TorchDistComm:
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._checked = set()
 
     def all_to_all(self, out, inp, out_splits, in_splits):
-        check_exchange(out, inp, out_splits, in_splits, self.world)
+        # the contract is checked once per (buffers, splits): the sharded loop
+        # exchanges the same buffers every step (host time per step matters at
+        # N = 8, where a step is ~0.1 ms of device work)
+        key = (out.data_ptr(), inp.data_ptr(), out.numel(), inp.numel(), tuple(out_splits),
+               tuple(in_splits))
+        if key not in self._checked:
+            check_exchange(out, inp, out_splits, in_splits, self.world)
+            self._checked.add(key)
         self.dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def all_to_all_list(self, outs, ins):
+        """One block per peer as lists of contiguous tensors (views into the
+        exchange buffers; grouped point-to-point sends and receives on RCCL).
+        Backends without a list all_to_all (gloo) go through one staged
+        all_to_all_single."""
+        key = tuple((t.data_ptr(), t.numel()) for t in list(outs) + list(ins))
+        if key not in self._checked:
+            check_exchange_list(outs, ins, self.world)
+            self._checked.add(key)
+        if self.dist.get_backend(self.group) == "nccl":
+            self.dist.all_to_all(list(outs), list(ins), group=self.group)
+            return
+        src = torch.cat([t.reshape(-1) for t in ins])
+        dst = torch.empty(sum(t.numel() for t in outs), dtype=torch.float32, device=src.device)
+        self.dist.all_to_all_single(dst, src, [t.numel() for t in outs], [t.numel() for t in ins],
+                                    group=self.group)
+        o = 0
+        for t in outs:
+            t.copy_(dst[o:o + t.numel()].view(t.shape))
+            o += t.numel()
 
     def all_reduce(self, t):
         # a strided view (e.g. one output of a plan's fused result) is reduced
@@ -91,6 +134,17 @@ class HostStagedComm(TorchDistComm):
         o = torch.empty(out.shape, dtype=out.dtype)
         self.dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
         out.copy_(o)
+
+    def all_to_all_list(self, outs, ins):
+        check_exchange_list(outs, ins, self.world)
+        src = torch.cat([t.reshape(-1).cpu() for t in ins])
+        dst = torch.empty(sum(t.numel() for t in outs), dtype=torch.float32)
+        self.dist.all_to_all_single(dst, src, [t.numel() for t in outs], [t.numel() for t in ins],
+                                    group=self.group)
+        o = 0
+        for t in outs:
+            t.copy_(dst[o:o + t.numel()].view(t.shape))
+            o += t.numel()
 
     def all_reduce(self, t):
         h = t.cpu()
@@ -189,8 +243,59 @@ class ShardedInnerLoop:
             if elbo_parts is not None:
                 elbo_parts.copy_(self.parts)
 
+    # ------------------------------------------------- overlapped exchanges
+    def _halves(self, q):
+        """Rank q's local samples split in two: [(lo, count), (lo, count)]."""
+        n = self.info[q]["s_count"]
+        a = (n + 1) // 2
+        return [(0, a), (a, n - a)]
+
+    def _views(self):
+        """Per half h, the exchange blocks as views: x send / receive, G send /
+        receive (one per peer, in rank order; see run(overlap=True))."""
+        if getattr(self, "_hv", None) is not None:
+            return self._hv
+        W, me = self.world, self.rank
+        S = self.plan.S
+        rows = [q["rows"] for q in self.info]
+        s_off = [q["s_offset"] for q in self.info]
+        S_loc = self.info[me]["s_count"]
+        xs = self.x_shard.view(S, rows[me])
+        gs = self.g_shard.view(S, rows[me])
+        base = [0]
+        for q in range(W):
+            base.append(base[-1] + S_loc * rows[q])
+        hv = []
+        for h in range(2):
+            lo_me, n_me = self._halves(me)[h]
+            xo, xi, go, gi = [], [], [], []
+            for q in range(W):
+                lo_q, n_q = self._halves(q)[h]
+                # x: my rows of q's half-h samples out; q's rows of my half-h samples in
+                xi.append(xs[s_off[q] + lo_q:s_off[q] + lo_q + n_q].reshape(-1))
+                blk = self.x_recv[base[q]:base[q + 1]].view(S_loc, rows[q])
+                xo.append(blk[lo_me:lo_me + n_me].reshape(-1))
+                # G: q's rows of my half-h samples out; my rows of q's half-h samples in
+                gblk = self.g_send[base[q]:base[q + 1]].view(S_loc, rows[q])
+                gi.append(gblk[lo_me:lo_me + n_me].reshape(-1))
+                go.append(gs[s_off[q] + lo_q:s_off[q] + lo_q + n_q].reshape(-1))
+            hv.append(dict(xo=xo, xi=xi, go=go, gi=gi, lo=lo_me, n=n_me))
+        self._hv = hv
+        return hv
+
+    def phase_net_half(self, u, z, w, h, draw=None):
+        """The network on half h of this rank's samples (psvi_mvn_phase_net_part),
+        adding to parts[0]; draw: part h of 2 of the next step's eps."""
+        hv = self._views()[h]
+        self.plan.mvn_net(u, z, w, self.x_recv, self.g_send, self.parts[0:1], draw=draw,
+                          samples=(hv["lo"], hv["n"]), draw_part=(h, 2))
+
+    def _net_half(self, u, z, w, h, nxt):
+        self.phase_net_half(u, z, w, h, draw=nxt if (nxt is not None and self.x_recv.is_cuda)
+                            else None)
+
     def run(self, u, z, w, params, m, v, T, lr, kind="higher", step0=1, seed=0, offset=0,
-            elbo_parts=None, phase_events=None):
+            elbo_parts=None, phase_events=None, overlap=False):
         """T chained inner steps on this rank with in-library Philox draws
         (psvi_inner_loop's stream: step t at offset + t * eps_stride of the
         global layout, identical on every rank, so eps never crosses the wire).
@@ -205,7 +310,16 @@ class ShardedInnerLoop:
         samples nothing.  elbo_parts (T, 2) float64 receives this rank's [NLL,
         KL] per step (reduce_elbo sums them).  phase_events: optional {t:
         [4 events]} recorded around the exchanges + network, the update and
-        the sample (diagnostics; they sit between launches)."""
+        the sample (diagnostics; they sit between launches).
+
+        overlap=True (full-cov): the rank's samples in two halves A, B and each
+        exchange in two (list all_to_alls of per-peer views, no copies):
+          x(A) -> net(A) on the compute stream, x(B) beside it on a side stream;
+          net(B) once x(B) is in, G(A) beside it on the side stream (after
+          net(A)); G(B), then the update once G(A) is in.
+        The per-sample work and the exchanged bytes are those of the plain
+        schedule (the same parameters bit for bit; the NLL's atomic adds come in
+        another order); the draw is split between the two network launches."""
         T = int(T)
         if T <= 0:
             return
@@ -224,6 +338,12 @@ class ShardedInnerLoop:
         cuda = e_cur.is_cuda
         self.draw(e_cur, seed, offset)
         self.phase_sample(e_cur, params)
+        if overlap and getattr(self.plan, "net_part_ok", True):
+            # (plans whose pseudopoint chunks use per-chunk gradient slots take
+            # whole network launches: the plain schedule)
+            self._run_overlap(u, z, w, params, m, v, T, lr, kind, step0, seed, offset, elbo_parts,
+                              phase_events, e_cur, e_nxt, stride, cuda)
+            return
         for t in range(T):
             ev = phase_events.get(t) if phase_events else None
             last = t + 1 == T
@@ -238,6 +358,56 @@ class ShardedInnerLoop:
             else:
                 self.phase_net(u, z, w)
             self.comm.all_to_all(self.g_shard, self.g_send, self.g_out, self.g_in)
+            if ev: ev[1].record()
+            if last:
+                self.phase_update(e_cur, params, m, v, step0 + t, lr, kind)
+            else:
+                self.phase_update_sample(e_cur, params, m, v, step0 + t, lr, kind, e_nxt)
+            if ev: ev[2].record()
+            if elbo_parts is not None:
+                elbo_parts[t].copy_(self.parts)
+            e_cur, e_nxt = e_nxt, e_cur
+            if ev: ev[3].record()
+        self._eps2 = [e_cur, e_nxt]
+
+    def _run_overlap(self, u, z, w, params, m, v, T, lr, kind, step0, seed, offset, elbo_parts,
+                     phase_events, e_cur, e_nxt, stride, cuda):
+        import contextlib
+
+        hv = self._views()
+        cs = None
+        if cuda:
+            if getattr(self, "_cs", None) is None:
+                self._cs = torch.cuda.Stream(device=e_cur.device)
+            cs = self._cs
+            main = torch.cuda.current_stream(e_cur.device)
+        side = (lambda: torch.cuda.stream(cs)) if cuda else contextlib.nullcontext
+        for t in range(T):
+            ev = phase_events.get(t) if phase_events else None
+            last = t + 1 == T
+            nxt = None if last else (e_nxt, seed, offset + (t + 1) * stride)
+            if nxt is not None and not cuda:
+                self.draw(*nxt)
+            if ev: ev[0].record()
+            self.parts.zero_()
+            self.comm.all_to_all_list(hv[0]["xo"], hv[0]["xi"])          # x(A)
+            if cuda:
+                cs.wait_stream(main)        # x_shard written by the last update
+            with side():
+                self.comm.all_to_all_list(hv[1]["xo"], hv[1]["xi"])      # x(B) beside net(A)
+            self._net_half(u, z, w, 0, nxt)
+            if cuda:
+                ev_a = torch.cuda.Event()
+                ev_a.record(main)
+                main.wait_stream(cs)        # x(B) in
+            self._net_half(u, z, w, 1, nxt)
+            with side():
+                if cuda:
+                    cs.wait_event(ev_a)     # G(A) written by net(A)
+                self.comm.all_to_all_list(hv[0]["go"], hv[0]["gi"])      # G(A) beside net(B)
+            self.comm.all_to_all_list(hv[1]["go"], hv[1]["gi"])          # G(B)
+            if cuda:
+                main.wait_stream(cs)        # G(A) in
             if ev: ev[1].record()
             if last:
                 self.phase_update(e_cur, params, m, v, step0 + t, lr, kind)

@@ -126,6 +126,8 @@ typedef struct psvi_plan psvi_plan;       /* opaque, immutable after create */
 #define PSVI_Q_OUTER_WS_BYTES 12 /* workspace bytes for psvi_outer_elbo_grad          */
 #define PSVI_Q_HVP_WS_BYTES  13 /* workspace bytes for psvi_hvp                       */
 #define PSVI_Q_EVAL_WS_BYTES 14 /* workspace bytes for psvi_evaluate                  */
+#define PSVI_Q_NET_PART_OK   15 /* full-cov: 1 if psvi_mvn_phase_net_part takes sample
+                                   ranges (no per-chunk gradient slots), else 0    */
 
 /* Create a plan for `family` over `world` ranks, this process being `rank`.
  * Samples are split in contiguous blocks; for FULLCOV at world > 1 the rows
@@ -261,6 +263,19 @@ int psvi_mvn_phase_net_draw(const psvi_plan* plan, const float* u, const int32_t
                             const float* w, const float* x_recv, float* g_send,
                             double* nll_out, float* eps_out, int64_t n, uint64_t seed,
                             uint64_t offset, void* stream);
+/* the net phase (with, optionally, one part of the next step's draw) for the
+ * rank's local samples [s_begin, s_begin + s_count) only -- the sharded loop's
+ * sample halves, whose exchanges overlap the other half's network.  The
+ * buffers are the whole rank's (x_recv / g_send [source rank][S_LOCAL][rows]);
+ * this launch reads and writes its samples' rows.  Draw: normals of quad range
+ * part of nparts (contiguous, in order) of [0, n) into eps_out (NULL, n = 0:
+ * none).  Plans whose pseudopoint chunks use per-chunk slots (not looped)
+ * take whole launches only (PSVI_EUNSUP). */
+int psvi_mvn_phase_net_part(const psvi_plan* plan, const float* u, const int32_t* z,
+                            const float* w, const float* x_recv, float* g_send,
+                            double* nll_out, int32_t s_begin, int32_t s_count, float* eps_out,
+                            int64_t n, uint64_t seed, uint64_t offset, int32_t part,
+                            int32_t nparts, void* stream);
 int psvi_mvn_phase_update(const psvi_plan* plan, const float* eps,
                           const float* g_shard, float* params, float* adam_m,
                           float* adam_v, const psvi_adam_hp* hp, double* kl_out,
@@ -426,6 +441,34 @@ int psvi_nonfinite(const void* data, int64_t n, int32_t dtype, int32_t* flag, vo
 /* Generic fused Adam over n floats (either variant). */
 int psvi_adam_update(int64_t n, float* params, const float* grad, float* adam_m,
                      float* adam_v, const psvi_adam_hp* hp, void* stream);
+
+/* ---- hyper_step's conjugate-gradient iteration (CG_normaleq) ----
+ * Replaces the vector work of one iteration of the reference's
+ * psvi/hypergrad/CG_torch.py:21-43 cg() over hypergradients.py:217-230's
+ * normal-equation operator A(p) = vmj - J vmj, vmj = lr H_A p, J y = y - lr
+ * H_B y, given the two fp32 Hessian-vector products hv1 = H_A p (from p32)
+ * and hv2 = H_B vmj32 (psvi_hvp):
+ *   psvi_cg_scale:    vmj32 = float(lr hv1)  (hv2's input)
+ *   psvi_cg_pap:      state[1] = p . A p
+ *   psvi_cg_residual: alpha = state[0] / state[1]; r -= alpha A p; state[2] =
+ *                     r . r; done (state[3]) |= sqrt(state[2]) < tol; the step
+ *                     length for x (state[4]: 0 once done), beta (state[5]),
+ *                     and rTr (state[0]) unless done
+ *   psvi_cg_update:   x += state[4] p; unless done p = r + beta p, p32 = float(p)
+ * state: 7 float64 on the device, [0] = r . r and the rest 0 on entry to the
+ * first iteration; x = 0, r = p = b (float64), p32 = float(b).  Where the
+ * reference breaks, x keeps its last iterate and p freezes (the step length
+ * is selected, never multiplied by a non-finite alpha); the caller reads
+ * state[3] when it wants to stop.  ws: psvi_cg_ws_bytes() bytes, zeroed once
+ * (the grid sums leave their counter at 0).  The sums are deterministic. */
+size_t psvi_cg_ws_bytes(void);
+int psvi_cg_scale(int64_t n, const float* hv, double lr, float* out, void* stream);
+int psvi_cg_pap(int64_t n, const float* hv1, const float* hv2, double lr, const double* p,
+                double* state, void* ws, size_t ws_bytes, void* stream);
+int psvi_cg_residual(int64_t n, const float* hv1, const float* hv2, double lr, double* r,
+                     double* state, double tol, void* ws, size_t ws_bytes, void* stream);
+int psvi_cg_update(int64_t n, double* x, double* p, float* p32, const double* r,
+                   const double* state, void* stream);
 
 const char* psvi_last_error(void);
 const char* psvi_version(void);

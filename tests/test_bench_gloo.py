@@ -125,6 +125,9 @@ def test_bench_multi_rank_control_flow(world):
     assert one["inner_steps_per_s"] == 123.0
     assert one["speedup_of_headline"] == round(line["value"] / 123.0, 3)
     assert line["speedup_over_1gpu"] == one["speedup_of_headline"]
+    sch = line["config"]["exchange_schedules"]
+    assert set(sch) == {"plain", "overlap", "headline"} and sch["headline"] in ("plain", "overlap")
+    assert sch[sch["headline"]]["inner_steps_per_s"] == round(line["value"], 2)
     weak = line["weak"]
     assert weak["inner_steps_per_s"] > 0 and weak["elbo_finite"]
     assert "S=%d" % (4 * world) in weak["config"] and "M=5" in weak["config"]

@@ -88,3 +88,32 @@ def test_pred_on_grid_shape_and_normalisation():
     p = ps.pred_on_grid(n_test_per_dim=40)
     assert p.shape == (1600, 3)
     assert torch.allclose(p.sum(-1), torch.ones(1600, device=DEV), atol=1e-5)
+
+
+@pytest.mark.parametrize("name", fixture_names("p"))
+def test_pred_on_grid_matches_reference(name):
+    """PSVI.pred_on_grid through psvi_evaluate against the reference's own
+    pred_on_grid (tests/golden/p*.npz, tools/gen_golden_grid.py), with and
+    without the importance-weight correction (fp32 path against the float64
+    reference run: 1e-5 absolute on probabilities)."""
+    from psvi.inference import PSVIAV, PSVILearnV
+    from test_host_api import build_model
+
+    f = load_fixture(name)
+    cfg = f["cfg"]
+    model = build_model(cfg, f["params0"]).cuda()
+    cls = PSVIAV if cfg["f"] == "exp_alpha_softmax" else PSVILearnV
+    ps = cls(u=_t(f["u"]), z=_t(f["z"]), N=cfg["N"], model=model, mc_samples=cfg["S"],
+             device_id=0)
+    ps.device = torch.device(DEV)
+    ps.v = _t(f["v"])
+    if cls is PSVIAV:
+        ps.alpha = _t([cfg["alpha"]])
+    n = cfg["n_test_per_dim"]
+    for tag, corr in (("", True), ("_nc", False)):
+        p = ps.pred_on_grid(n_test_per_dim=n, correction=corr, eps=_t(f["eps" + tag]))
+        ref = f["probs" + tag]
+        assert p.shape == ref.shape
+        err = float(np.abs(p.cpu().numpy() - ref).max())
+        print(f"{name}{tag}: max |p - ref| {err:.2e}")
+        assert err < 1e-5

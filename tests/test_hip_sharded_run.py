@@ -56,6 +56,22 @@ class _DevComm:
                     o += n
                 outer.bar.wait()
 
+            def all_to_all_list(self, outs, ins):
+                # per-peer views; each rank copies on its current stream (a side
+                # stream in run(overlap=True)) after the sources' producers
+                from psvi.runtime.sharded import check_exchange_list
+                check_exchange_list(outs, ins, outer.world)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+                outer.slots[rank] = (list(ins), ev)
+                outer.bar.wait()
+                for q in range(outer.world):
+                    src, qev = outer.slots[q]
+                    torch.cuda.current_stream().wait_event(qev)
+                    assert src[rank].numel() == outs[q].numel(), (q, rank)
+                    outs[q].copy_(src[rank])
+                outer.bar.wait()
+
             def all_reduce(self, t):
                 outer.slots[rank] = t.clone()
                 outer.bar.wait()
@@ -87,7 +103,7 @@ def _run_ranks(world, fn):
     return res
 
 
-def _sharded_run(layers, S, M, world, u, z, w, p0, T, lr, kind, seed, offset):
+def _sharded_run(layers, S, M, world, u, z, w, p0, T, lr, kind, seed, offset, overlap=False):
     """run() on every thread-rank; returns (negative ELBO per step, params,
     m, v) after gather_params (identical on every rank)."""
     from psvi.runtime.sharded import ShardedInnerLoop
@@ -98,7 +114,7 @@ def _sharded_run(layers, S, M, world, u, z, w, p0, T, lr, kind, seed, offset):
         m, v = torch.zeros_like(p), torch.zeros_like(p)
         parts = torch.zeros(T, 2, dtype=torch.float64, device=DEV)
         loop.run(u, z, w, p, m, v, T, lr, kind=kind, seed=seed, offset=offset,
-                 elbo_parts=parts)
+                 elbo_parts=parts, overlap=overlap)
         neg = loop.reduce_elbo(parts)
         loop.gather_params(p, m, v)
         return neg, p, m, v
@@ -226,3 +242,29 @@ def test_run_full_size(W, S, M):
     print(f"  entries off by > 0.1 lr: {int(off.sum())} of {d.size}")
     assert off.sum() < 1e-3 * d.size and d.max() < 2.05 * lr
     assert l2rel(p8[~off], p1[~off]) < 1e-6
+
+
+@pytest.mark.parametrize("W,S,M", [(8, 1024, 200), (2, 256, 100), (3, 768, 40), (3, 257, 40)])
+def test_run_overlap_equals_plain(W, S, M):
+    """run(overlap=True): the rank's samples in two halves, each exchange as
+    two list all_to_alls of per-peer views on a side stream beside the other
+    half's network (psvi_mvn_phase_net_part), the draw split between the two
+    launches -- the same parameters, Adam state and draws as the plain
+    schedule, bit for bit (the NLL's atomic adds come in another order).
+    (3, 257, 40): a plan with per-chunk gradient slots (not looped), which
+    takes the plain schedule.)"""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from test_hip_fullsize import make_case
+
+    layers = [(64, 40), (40, 40), (40, 2)] if M >= 100 else [(12, 20), (20, 4)]
+    params, u, z, w, _ = make_case("fullcov", layers, S, M, 5)
+    t = lambda x, d=torch.float32: torch.tensor(x, dtype=d, device=DEV)
+    du, dz, dw, p0 = t(u), t(z, torch.int32), t(w), t(params)
+    eA, pA, mA, vA = _sharded_run(layers, S, M, W, du, dz, dw, p0, 3, 1e-3, "higher", 7, 0)
+    eB, pB, mB, vB = _sharded_run(layers, S, M, W, du, dz, dw, p0, 3, 1e-3, "higher", 7, 0,
+                                  overlap=True)
+    for a, b, n in ((pA, pB, "params"), (mA, mB, "m"), (vA, vB, "v")):
+        assert np.array_equal(a, b), (n, np.abs(a - b).max())
+    for k in range(3):
+        assert rel(eA[k], eB[k]) < 1e-12, (k, eA[k], eB[k])

@@ -91,6 +91,29 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
         loop.g_send.copy_(torch.from_numpy(full_to_send(G)).float())
         loop.parts[0] = data
 
+    def phase_net_half(u, z, w, h, draw=None):
+        # the same network on half h of the rank's samples: their rows of
+        # g_send, their NLL added
+        lo, n = loop._halves(r)[h]
+        X = recv_to_full(loop.x_recv.double().numpy())[lo:lo + n]
+        Ws, bs = O.mvn_split_x(layers, X)
+        data, dWs, dbs = O.net_forward_backward(u.double().numpy(), z.numpy(),
+                                                w.double().numpy(), Ws, bs)
+        G = np.concatenate([np.concatenate([dWs[l].reshape(X.shape[0], -1), dbs[l]], 1)
+                            for l in range(len(layers))], 1)
+        full = np.zeros((me["s_count"], woff[-1]))
+        full[lo:lo + n] = G
+        send = full_to_send(full)
+        cur = loop.g_send.double().numpy()
+        off = 0
+        for q in infos:
+            blk_c = cur[off:off + me["s_count"] * q["rows"]].reshape(me["s_count"], q["rows"])
+            blk_n = send[off:off + me["s_count"] * q["rows"]].reshape(me["s_count"], q["rows"])
+            blk_c[lo:lo + n] = blk_n[lo:lo + n]
+            off += me["s_count"] * q["rows"]
+        loop.g_send.copy_(torch.from_numpy(cur).float())
+        loop.parts[0] += data
+
     def phase_update(eps, params, m, v, step, lr, kind, grad_out=None):
         p = params.double().numpy()
         e = eps.double().numpy()
@@ -119,6 +142,7 @@ def _emulate_fullcov(loop, O, layers, S, prior_sd):
 
     loop.phase_sample, loop.phase_net, loop.phase_update = phase_sample, phase_net, phase_update
     loop.phase_update_sample = phase_update_sample
+    loop.phase_net_half = phase_net_half
 
 
 def _rank_main(rank, world, port, name, kind_override, out):
@@ -184,6 +208,73 @@ def test_sharded_fullcov_step_matches_world1(world, name, kind):
     assert rel(negelbo, o_elbo[0]) < 1e-6, (negelbo, o_elbo[0])
     assert l2rel(params, o_traj[0]) < 1e-6
     assert l2rel(m, o_m) < 1e-5 and l2rel(v, o_v) < 1e-5
+
+
+def _run_overlap_rank(rank, world, port, out):
+    import sys
+    for p in (os.path.join(ROOT, "blackbox-coresets-vi_amd"), os.path.join(ROOT, "oracle"),
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import psvi_oracle as O
+    from psvi.runtime.sharded import ShardedInnerLoop, TorchDistComm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        layers, S, M = [(8, 6), (6, 3)], 4 * world + 1, 7
+        g = torch.Generator().manual_seed(5)
+        u = torch.randn(M, 8, generator=g)
+        z = torch.randint(0, 3, (M,), generator=g).to(torch.int32)
+        w = torch.rand(M, generator=g) * 10 + 1
+
+        def draw(t, seed, offset):
+            gg = torch.Generator().manual_seed(int(seed) * 1000003 + int(offset))
+            t.copy_(torch.randn(t.numel(), generator=gg))
+
+        res = []
+        for overlap in (False, True):
+            loop = ShardedInnerLoop("fullcov", layers, S, M, world, rank, device="cpu",
+                                    comm=TorchDistComm())
+            _emulate_fullcov(loop, O, layers, S, 1.0)
+            loop.draw = draw
+            assert loop.plan.net_part_ok   # the overlapped schedule runs (no chunk slots)
+            n = [a * b + b for a, b in layers]
+            params = torch.cat([torch.cat([0.1 * torch.randn(k, generator=torch.Generator().manual_seed(k)),
+                                           torch.full((k,), -4.0),
+                                           0.05 * torch.randn((k - 1) * (k - 2) // 2,
+                                                              generator=torch.Generator().manual_seed(k + 1))])
+                                for k in n])
+            m, v = torch.zeros_like(params), torch.zeros_like(params)
+            parts = torch.zeros(3, 2, dtype=torch.float64)
+            loop.run(u, z, w, params, m, v, 3, 1e-3, seed=9, elbo_parts=parts, overlap=overlap)
+            negelbo = loop.reduce_elbo(parts)
+            loop.gather_params(params, m, v)
+            res.append((negelbo.numpy(), params.numpy(), m.numpy(), v.numpy()))
+        out.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_run_overlap_matches_plain(world):
+    """run(overlap=True) -- two sample halves, each exchange in two list
+    all_to_alls of per-peer views, the network launched per half -- against
+    the plain schedule on the same draws: the same steps (float64 oracle
+    phases: equal up to the NLL's split sum)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_overlap_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, ((e0, p0, m0, v0), (e1, p1, m1, v1)) in res:
+        assert np.allclose(e0, e1, rtol=1e-12, atol=0)
+        for a, b in ((p0, p1), (m0, m1), (v0, v1)):
+            assert np.allclose(a, b, rtol=1e-6, atol=1e-12)
 
 
 def _emulate_lenet(loop, O, S):
