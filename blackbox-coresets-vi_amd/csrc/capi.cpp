@@ -28,7 +28,8 @@ extern int g_stream_bf_off;              // kernels_mvn.hip
 extern unsigned long long* g_bf_stamps;  // kernels_mvn.hip
 extern int g_ks_off;                     // kernels_mvn.hip
 extern int g_fs_off;                     // kernels_mvn.hip
-extern int g_fwd_pair_fp32;                // kernels_mvn.hip
+extern int g_fwd_pair_bf;                  // kernels_mvn.hip
+extern int g_stream_fold_off;              // kernels_mvn.hip
 extern int g_fs_bf_off;                  // kernels_mvn.hip
 extern int g_ks_bf_off;                  // kernels_mvn.hip
 static int g_ks_wgs = 0;                 // psvi_debug_set(PSVI_DBG_KSTREAM_WGS): plan creation
@@ -531,8 +532,13 @@ int build_plan(psvi_plan& p) {
             for (int w = 0; w < nwg; ++w) {
                 const int t0 = cut[w], t1 = cut[w + 1];
                 p.h_str.push_back(StreamRange{t0, t1, ns, t0 < T ? tmap[t0] : 0u});
+                int ends = 0;
                 for (int t = t0; t < t1; ++t)
-                    if (t == t0 || tband[t] != tband[t - 1]) band_slots[tband[t]].push_back(ns++);
+                    if (t == t0 || tband[t] != tband[t - 1]) {
+                        band_slots[tband[t]].push_back(ns++);
+                        ++ends;
+                    }
+                p.str_max_ends = std::max(p.str_max_ends, ends);
             }
             int bid = 0;
             for (int l = 0; l < p.L; ++l)
@@ -622,7 +628,8 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_KSTREAM_WGS: g_ks_wgs = value; return 0;
         case PSVI_DBG_FWD_SEG_OFF: g_fs_off = value; return 0;
         case PSVI_DBG_FWD_SEG_BF_OFF: g_fs_bf_off = value; return 0;
-        case PSVI_DBG_FWD_PAIR_FP32: g_fwd_pair_fp32 = value; return 0;
+        case PSVI_DBG_FWD_PAIR_BF: g_fwd_pair_bf = value; return 0;
+        case PSVI_DBG_STREAM_FOLD_OFF: g_stream_fold_off = value; return 0;
         case PSVI_DBG_KSTREAM_BF_OFF: g_ks_bf_off = value; return 0;
         case PSVI_DBG_ROP_VALU: g_rop_valu = value; return 0;
         case PSVI_DBG_NET_SCALAR_LOADS: g_net_scalar_loads = value; return 0;
@@ -738,7 +745,10 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
         if (!rc && p->n_str > 0) {
             const size_t bytes = sizeof(float) * (size_t)p->n_sslots * p->d.S * 64;
             if (!(rc = upload(p->h_str, &p->d_str)) && !(rc = upload(p->h_sfrb, &p->d_sfrb)) &&
-                hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess)
+                (hipMalloc((void**)&p->d_str_part, bytes) != hipSuccess ||
+                 hipMalloc((void**)&p->d_str_cnt, sizeof(int) * (size_t)std::max(1, p->n_sfrb)) != hipSuccess ||
+                 hipMemset(p->d_str_cnt, 0, sizeof(int) * (size_t)std::max(1, p->n_sfrb)) != hipSuccess ||
+                 hipMalloc((void**)&p->d_str_bms, sizeof(float) * 128 * (size_t)std::max(1, p->n_sfrb)) != hipSuccess))
                 rc = fail(PSVI_EUNSUP, "cannot allocate the streaming-update scratch");
         }
         if (!rc && p->n_kwg > 0) {
@@ -812,6 +822,8 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_str) (void)hipFree(p->d_str);
     if (p->d_sfrb) (void)hipFree(p->d_sfrb);
     if (p->d_str_part) (void)hipFree(p->d_str_part);
+    if (p->d_str_cnt) (void)hipFree(p->d_str_cnt);
+    if (p->d_str_bms) (void)hipFree(p->d_str_bms);
     if (p->d_upd_part) (void)hipFree(p->d_upd_part);
     if (p->d_upd) (void)hipFree(p->d_upd);
     if (p->d_lenet_ws) (void)hipFree(p->d_lenet_ws);

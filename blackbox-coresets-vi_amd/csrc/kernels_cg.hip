@@ -24,8 +24,9 @@
 // The grid sums are deterministic: each workgroup's fp64 partial goes to its
 // slot with an sc1 store; after the storing wave's vmcnt drain one lane adds
 // to the pass's counter (agent scope); the workgroup whose add returns the
-// last count adds the slots in slot order with sc1 loads (MI355X_MICROARCH.md
-// hand-off table, first row), writes the scalars and resets the counter.
+// last count reads the slots with sc1 loads (MI355X_MICROARCH.md hand-off
+// table, first row) and adds them in a fixed order, writes the scalars and
+// resets the counter.
 #include "psvi_internal.hpp"
 
 namespace psvi {
@@ -54,24 +55,33 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
     return t;
 }
 
-// The grid sum's hand-off: thread 0 holds this block's partial.  Returns true
-// in thread 0 of the last-arriving block, with the total in *tot.
-__device__ __forceinline__ bool grid_sum(double part, double* slots, unsigned* cnt, double* tot) {
-    bool last = false;
+// The grid sum's hand-off: thread 0 holds this block's partial.  Every thread
+// calls it; returns true in thread 0 of the last-arriving block, with the
+// total in *tot.  The last block reads the slots with all its threads (four
+// loads per thread in flight, then the block sum in wave order: a fixed order,
+// whichever block arrives last).
+__device__ __forceinline__ bool grid_sum(double part, double* slots, unsigned* cnt, double* tot, double* red) {
+    __shared__ unsigned last;
     if (threadIdx.x == 0) {
         __hip_atomic_store(slots + blockIdx.x, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == gridDim.x - 1;
-        if (last) {
-            double t = 0.0;
-            for (unsigned b = 0; b < gridDim.x; ++b)
-                t += __hip_atomic_load(slots + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *tot = t;
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
-    return last;
+    __syncthreads();
+    if (!last) return false;  // uniform
+    static_assert(kCgBlocks <= 4 * kCgThreads, "four slots per thread");
+    double v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const unsigned b = threadIdx.x + i * kCgThreads;
+        v[i] = b < gridDim.x ? __hip_atomic_load(slots + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    }
+    const double t = block_sum_d((v[0] + v[1]) + (v[2] + v[3]), red);
+    if (threadIdx.x == 0) {
+        *tot = t;
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return threadIdx.x == 0;
 }
 
 __device__ __forceinline__ double cg_ap(float h1, float h2, double lr) {
@@ -98,7 +108,8 @@ __global__ __launch_bounds__(kCgThreads) void cg_pap_kernel(int64_t n, const flo
         acc += p[i] * cg_ap(hv1[i], hv2[i], lr);
     const double part = block_sum_d(acc, red);
     double tot;
-    if (grid_sum(part, slots, cnt, &tot)) state[kPap] = tot;
+    __syncthreads();  // red reused by the grid sum
+    if (grid_sum(part, slots, cnt, &tot, red)) state[kPap] = tot;
 }
 
 __global__ __launch_bounds__(kCgThreads) void cg_residual_kernel(int64_t n, const float* __restrict__ hv1,
@@ -117,7 +128,8 @@ __global__ __launch_bounds__(kCgThreads) void cg_residual_kernel(int64_t n, cons
     }
     const double part = block_sum_d(acc, red);
     double rnrn;
-    if (grid_sum(part, slots, cnt, &rnrn)) {
+    __syncthreads();  // red reused by the grid sum
+    if (grid_sum(part, slots, cnt, &rnrn, red)) {
         // every block has read rTr and pAp: the scalars of the next pass
         const bool done = state[kDone] != 0.0 || sqrt(rnrn) < tol;
         state[kRnrn] = rnrn;

@@ -359,8 +359,12 @@ __global__ __launch_bounds__(256) void mvn_fwd_reduce_kernel(const FwdRowBlock* 
     }
     const float dg = dof ? sigmoid_f(dof[a.lay[rb.layer].poff + n + r]) * sdr
                                : softplus_f(sdr);
-    x[(int64_t)s0 * a.ldx + rb.xcol + rr] = (mu + dg * e0) + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-    if (two) x[(int64_t)s1 * a.ldx + rb.xcol + rr] = (mu + dg * e1) + ((b4[0] + b4[1]) + (b4[2] + b4[3]));
+    // mean + (softplus(sd) eps, rounded) + the slots: the product never fused
+    // into an fma, here and in the streaming update's in-kernel combine, so
+    // the two give the same bits
+    x[(int64_t)s0 * a.ldx + rb.xcol + rr] = (mu + mul_unfused(dg, e0)) + ((a4[0] + a4[1]) + (a4[2] + a4[3]));
+    if (two)
+        x[(int64_t)s1 * a.ldx + rb.xcol + rr] = (mu + mul_unfused(dg, e1)) + ((b4[0] + b4[1]) + (b4[2] + b4[3]));
 }
 
 // Segmented sample (K = S > 128): one persistent workgroup run of the
@@ -1733,6 +1737,14 @@ struct StrArgs {
     int64_t pl;
     int64_t ppoff[kMaxL];
     int npad[kMaxL];
+    // mvn_stream_bf2_kernel<FOLD>: the band combine in the kernel (the
+    // stream's row-block table, one arrival counter per band, x' and its row
+    // stride)
+    const FwdRowBlock* rbs;
+    int* bcnt;
+    float* bms;  // per band: the new mean (64) and softplus(sd) (64)
+    float* x;
+    int ldx;
 };
 
 struct StrTile {
@@ -1776,6 +1788,7 @@ __device__ __forceinline__ float adam_fast_k(const AdamC& a, float p, float g, f
     }
 }
 
+constexpr int kFoldMax = 64;  // band ends per run the in-kernel combine can take (FOLD)
 constexpr int kStrBuf = 128 * 16;  // float4 per eps block buffer ([128 samples][16 slots])
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // plain vector loads / stores (no memcpy)
 
@@ -2228,7 +2241,19 @@ __global__ __launch_bounds__(256, 1) void mvn_stream_kernel(StrArgs a) {
 // next tile's eps planes are stored after them.  Images, pieces, swizzles and
 // the slot layout as described above.  DIAG: per-phase shader clocks summed
 // over the run's tiles (thread 0) into the stamp buffer (tools/bf_stamps.py).
-template <int KIND, bool DIAG = false>
+//
+// FOLD: the band's x' rows are finished in the kernel instead of by
+// mvn_fwd_reduce_kernel.  At a band's end each segment stores its slot
+// write-through (sc1), drains (vmcnt 0), and one lane adds to the band's
+// counter (relaxed, agent scope); the segment that draws the last ticket
+// reads the band's slots with sc1 loads and writes x' = mean + softplus(sd)
+// eps' + the slots' sum, in the reduce's order (slot k into partial k mod 4),
+// so the result is the reduce's bit for bit.  The band's new mean / sd come
+// from its diagonal tile, the band's last: stored write-through by that
+// segment before its own drain and ticket, read with agent-scope loads.  The
+// hand-off is the K-split update's (MI355X_MICROARCH.md hand-off table, first
+// row); no workgroup waits on another.
+template <int KIND, bool DIAG = false, bool FOLD = false>
 __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t smb[9 * kBfImg];
     uint8_t* const Eb = smb;
@@ -2248,7 +2273,7 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
     const int t1 = __builtin_amdgcn_readfirstlane(R.t1);
     int slot = __builtin_amdgcn_readfirstlane(R.slot0);
     const int S = a.S;  // 128
-    unsigned long long tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+    unsigned long long tph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
     // (wave 0 as a whole: the stamps stay wave-uniform, in scalar registers)
     auto ph = [&](int qq) __attribute__((always_inline)) {
         if (DIAG && wv == 0) {
@@ -2368,6 +2393,100 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         }
     };
 
+    // the band's index in the stream's row-block table (layer-major)
+    auto band_id = [&](const StrTile& T) __attribute__((always_inline)) {
+        int bid = T.b;
+#pragma unroll
+        for (int l = 0; l < kMaxL - 1; ++l)
+            if (l < T.l) bid += a.nb[l];
+        return __builtin_amdgcn_readfirstlane(bid);
+    };
+    // FOLD: the band's arrival after its slot is stored; the last arriver
+    // notes the band and finishes its x' rows after the walk, where the tile
+    // walk's prefetch registers are free (see above)
+    __shared__ int fold_list[kFoldMax];
+    int nfold = 0;
+    auto band_arrive = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slot (and mean / sd) stores
+        __syncthreads();                                 // ... and every other wave's
+        const int bid = band_id(cur);
+        const int nk = __builtin_amdgcn_readfirstlane(a.rbs[bid].nk);
+        if (nk > 1) {
+            if (tid == 0)
+                Xs[0] = __int_as_float(
+                    __hip_atomic_fetch_add(a.bcnt + bid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            __syncthreads();
+            const int old = __builtin_amdgcn_readfirstlane(__float_as_int(Xs[0]));
+            if (old != nk - 1) return;  // uniform: another segment finishes the band
+            if (tid == 0) __hip_atomic_store(a.bcnt + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) fold_list[nfold] = bid;  // read after the walk's later barriers
+        ++nfold;
+    };
+    // x' rows of band bid from its slots (fragment order, see the band end):
+    // thread t takes float4 f = t + 512 m (m = 0..3) of every slot -- row 32
+    // (m >> 1) + (t & 31) of the band, samples 64 (m & 1) + 32 j + 4 h + 8 qg +
+    // e (e = 0..3) with (j, qg) = ((t >> 8) & 1, (t >> 6) & 3), h = (t >> 5) & 1.
+    // Runs after the walk, where the walk's registers are free: mean / sd, eps'
+    // and the first four slots' loads in flight together.
+    auto band_combine = [&](int bid) __attribute__((always_inline)) {
+        const FwdRowBlock rb = a.rbs[bid];
+        const int nk = __builtin_amdgcn_readfirstlane(rb.nk), slot0 = __builtin_amdgcn_readfirstlane(rb.slot0);
+        const int R = __builtin_amdgcn_readfirstlane(rb.R), xcol = __builtin_amdgcn_readfirstlane(rb.xcol);
+        const int l = __builtin_amdgcn_readfirstlane(rb.layer), r0 = __builtin_amdgcn_readfirstlane(rb.r0);
+        const int n = a.lay[l].n;
+        const float* const bm = a.bms + 128 * (int64_t)bid;
+        const int lt = tid & 31, hh = (tid >> 5) & 1, qg = (tid >> 6) & 3, jj = (tid >> 8) & 1;
+        // rows rr[w] = 32 w + lt (w = m >> 1): the band's new mean and softplus(sd)
+        float mu[2], dg[2], ev[4][4];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            mu[w] = __hip_atomic_load(bm + 32 * w + lt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dg[w] = __hip_atomic_load(bm + 64 + 32 * w + lt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        auto smp = [&](int m, int e) { return 64 * (m & 1) + 32 * jj + 4 * hh + 8 * qg + e; };
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float* ec = a.eps_next + a.lay[l].eoff + r0 + min(32 * (m >> 1) + lt, R - 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ev[m][e] = ec[(int64_t)smp(m, e) * n];
+        }
+        const rsrc_t rs_p = make_rsrc(a.part, 0x7fffffff);
+        f32x4 A[4][4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) A[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // slot k into partial k mod 4, in slot order (mvn_fwd_reduce_kernel's sum)
+        for (int k0 = 0; k0 < nk; k0 += 4) {  // uniform
+            f32x4 v[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int so = __builtin_amdgcn_readfirstlane((slot0 + min(k0 + i, nk - 1)) * S * 64 * 4);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    v[m][i] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, (uint32_t)((tid + 512 * m) * 16), so, 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (k0 + i < nk)  // uniform
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) A[m][i] += v[m][i];
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const f32x4 t = (A[m][0] + A[m][1]) + (A[m][2] + A[m][3]);
+            const int rr = 32 * (m >> 1) + lt;
+            if (rr < R) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    a.x[(int64_t)smp(m, e) * a.ldx + xcol + rr] =
+                        (mu[m >> 1] + mul_unfused(dg[m >> 1], ev[m][e])) + t[e];  // mvn_fwd_reduce_kernel's rounding
+            }
+        }
+    };
+
     auto tile = [&](const StrTile& nxt, auto has_next_c, auto newband_c) __attribute__((always_inline)) {
         constexpr bool has_next = decltype(has_next_c)::value;
         constexpr bool newband = decltype(newband_c)::value;
@@ -2468,14 +2587,28 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
                     kld += a.log_s0 - logf(sp) + 0.5f * ((sp * sp + mu * mu) * a.inv_s0sq - 1.f);
                 }
                 float mm = a.m[pm], vv = a.v[pm];
-                a.params[pm] = adam_apply(a.adam, mu, gmean, mm, vv);
+                const float mun = adam_apply(a.adam, mu, gmean, mm, vv);
                 a.m[pm] = mm;
                 a.v[pm] = vv;
                 mm = a.m[ps];
                 vv = a.v[ps];
-                a.params[ps] = adam_apply(a.adam, sdr, gsd, mm, vv);
+                const float sdn = adam_apply(a.adam, sdr, gsd, mm, vv);
                 a.m[ps] = mm;
                 a.v[ps] = vv;
+                a.params[pm] = mun;
+                a.params[ps] = sdn;
+                if constexpr (FOLD) {
+                    // the band's new mean and softplus(sd) for its combine, on
+                    // lines of the band's own, write-through: the combine may
+                    // run on another XCD, and the params lines are shared with
+                    // the neighbouring bands, whose diagonal tiles and combines
+                    // load them (an sc1 load is served by the reader's L2, so a
+                    // line another band's reader brought there would be stale)
+                    float* const bm = a.bms + 128 * (int64_t)band_id(cur);
+                    __hip_atomic_store(bm + 32 * wr + l32, mun, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(bm + 64 + 32 * wr + l32, softplus_f(sdn), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
         ph(3);
@@ -2574,22 +2707,41 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
                 // buffer stores: a scalar slot base, a per-lane 32-bit offset
                 const rsrc_t rs_p = make_rsrc(a.part, 0x7fffffff);
                 const int sob = __builtin_amdgcn_readfirstlane(slot * S * 64 * 4);
-                const uint32_t vb = (uint32_t)((32 * wr + l32 + 64 * (64 * hk + 4 * h)) * 4);
+                if constexpr (FOLD) {
+                    // fragment order, 16-byte write-through stores (a 4-byte sc1
+                    // store is one fabric write each): float4 ((((wr 2 + hk) 2 +
+                    // j) 4 + qg) 64 + lane) holds accumulators 4 qg .. 4 qg + 3
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < 2; ++j)
 #pragma unroll
-                    for (int qq = 0; qq < 16; ++qq) {
-                        const int sl = 32 * j + (qq & 3) + 8 * (qq >> 2);  // sample - 64 hk - 4 h
-                        const float v = xacc[j][qq] + Xs[(((wr * 2 + hk) * 2 + j) * 16 + qq) * 64 + lane];
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rs_p,
-                                                              vb + (uint32_t)(sl * 256), sob, 0);
-                    }
+                        for (int qg = 0; qg < 4; ++qg) {
+                            u32x4 v4;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                v4[e] = __float_as_uint(xacc[j][4 * qg + e] +
+                                                        Xs[(((wr * 2 + hk) * 2 + j) * 16 + 4 * qg + e) * 64 + lane]);
+                            BSTORE128(v4, rs_p, (uint32_t)((((((wr * 2 + hk) * 2 + j) * 4 + qg) * 64 + lane)) * 16),
+                                      sob, 16);
+                        }
+                } else {
+                    const uint32_t vb = (uint32_t)((32 * wr + l32 + 64 * (64 * hk + 4 * h)) * 4);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int qq = 0; qq < 16; ++qq) {
+                            const int sl = 32 * j + (qq & 3) + 8 * (qq >> 2);  // sample - 64 hk - 4 h
+                            const float v = xacc[j][qq] + Xs[(((wr * 2 + hk) * 2 + j) * 16 + qq) * 64 + lane];
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rs_p,
+                                                                  vb + (uint32_t)(sl * 256), sob, 0);
+                        }
+                }
             }
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int qq = 0; qq < 16; ++qq) xacc[j][qq] = 0.f;
             ++slot;
+            if constexpr (FOLD) band_arrive();
         }
         ph(6);
         __syncthreads();  // every wave done with the eps' image
@@ -2624,12 +2776,18 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         cur = nxt;
     }
     tile(cur, F_{}, F_{});
+    if constexpr (FOLD) {
+        ph(-1);
+        for (int i = 0; i < nfold; ++i) band_combine(__builtin_amdgcn_readfirstlane(fold_list[i]));
+        ph(10);  // DIAG: the combines' clocks (stamp slot 12)
+    }
     if (DIAG && tid == 0) {
         unsigned long long* o = a.stamps + (size_t)blockIdx.x * 16;
 #pragma unroll
         for (int qq = 0; qq < 10; ++qq) o[qq] = tph[qq];
         o[10] = __builtin_amdgcn_s_memtime();
         o[11] = __builtin_amdgcn_s_memrealtime();
+        o[12] = tph[10];
     }
     float klp = (kl2[0] + kl2[1]) * (0.5f * a.inv_s0sq) + kld;
     if (a.kl_out && a.include_kl) {
@@ -2645,7 +2803,8 @@ int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked k
 int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
 int g_ks_bf_off = 0;   // psvi_debug_set(PSVI_DBG_KSTREAM_BF_OFF, 1): the fp32 K-split update (A/B)
 int g_fs_bf_off = 0;   // psvi_debug_set(PSVI_DBG_FWD_SEG_BF_OFF, 1): the fp32 segmented sample (A/B)
-int g_fwd_pair_fp32 = 0;  // psvi_debug_set(PSVI_DBG_FWD_PAIR_FP32, 1): the HVP's sample pair on the fp32 item grid (A/B)
+int g_fwd_pair_bf = 0;  // psvi_debug_set(PSVI_DBG_FWD_PAIR_BF, 1): the HVP's sample pair as two bf16-piece segmented samples (A/B)
+int g_stream_fold_off = 0;  // psvi_debug_set(PSVI_DBG_STREAM_FOLD_OFF, 1): the band combine as mvn_fwd_reduce_kernel (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
 unsigned long long* g_upd_stamps = nullptr;  // psvi_debug_set_ptr(PSVI_DBG_UPD_STAMPS, buf)
@@ -3003,10 +3162,12 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float* params,
                                float* x, const float* vec, float* x2, float* part2,
                                hipStream_t st) {
-    if (p.n_fswg > 0 && !g_fs_off && !g_fs_bf_off && !g_fwd_pair_fp32) {
-        // the segmented sample on bf16 pieces (fp32-faithful), twice on the
-        // plan's slots: x, then the tangent x2 with the diagonal from params
-        // (C3: 2 x (seg + reduce) against the fp32 item-grid pair's 38.5 + 7.6 us)
+    if (p.n_fswg > 0 && !g_fs_off && !g_fs_bf_off && g_fwd_pair_bf) {
+        // (A/B) the segmented sample on bf16 pieces (fp32-faithful), twice on
+        // the plan's slots: x, then the tangent x2 with the diagonal from
+        // params.  Measured at C3: 2 x (20.1 + 6.8) us against the fp32
+        // item-grid pair's one launch of both (39.4 + 7 us), so the pair stays
+        // on the item grid
         if (hipError_t e = launch_mvn_fwd(p, eps, params, x, st)) return e;
         return launch_mvn_fwd(p, eps, vec, x2, st, params);
     }
@@ -3138,12 +3299,23 @@ hipError_t launch_mvn_update(const psvi_plan& p, const float* eps, const float* 
                     b.npad[l] = p.eps_planes.npad[l];
                 }
                 const dim3 b8(512);
-                if (b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
-                    hipLaunchKernelGGL((mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER, true>), sg, b8, 0, st, b);
+                const bool fold = p.d_str_cnt && p.d_str_bms && p.str_max_ends <= kFoldMax && !g_stream_fold_off;
+                b.rbs = p.d_sfrb;
+                b.bcnt = p.d_str_cnt;
+                b.bms = p.d_str_bms;
+                b.x = x_next;
+                b.ldx = p.rows_tot[p.rank];
+                if (fold && b.stamps && b.adam.kind == PSVI_ADAM_HIGHER)
+                    hipLaunchKernelGGL((mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER, true, true>), sg, b8, 0, st, b);
+                else if (fold && b.adam.kind == PSVI_ADAM_HIGHER)
+                    hipLaunchKernelGGL((mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER, false, true>), sg, b8, 0, st, b);
+                else if (fold)
+                    hipLaunchKernelGGL((mvn_stream_bf2_kernel<PSVI_ADAM_HYPERGRAD, false, true>), sg, b8, 0, st, b);
                 else if (b.adam.kind == PSVI_ADAM_HIGHER)
                     hipLaunchKernelGGL(mvn_stream_bf2_kernel<PSVI_ADAM_HIGHER>, sg, b8, 0, st, b);
                 else
                     hipLaunchKernelGGL(mvn_stream_bf2_kernel<PSVI_ADAM_HYPERGRAD>, sg, b8, 0, st, b);
+                if (fold) return hipGetLastError();
             } else if (b.stamps && a.S == 128 && b.adam.kind == PSVI_ADAM_HIGHER)
                 hipLaunchKernelGGL((mvn_stream_kernel<4, PSVI_ADAM_HIGHER, true>), sg, block, 0, st, b);
             else

@@ -17,6 +17,14 @@ constexpr int kMaxWorld = 8;      // ranks per node (xGMI)
 constexpr int kWave = 64;
 
 // ---------------------------------------------------------------- numerics
+// a * b rounded on its own: never fused into an fma with the add that uses it
+// (hipcc contracts a * b + c across statements and through __fmul_rn), for
+// two kernels that must give the same bits from the same operands
+__device__ __forceinline__ float mul_unfused(float a, float b) {
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // torch.nn.functional.softplus(beta=1, threshold=20)
 __device__ __forceinline__ float softplus_f(float x) {
     return x > 20.f ? x : log1pf(expf(x));
@@ -483,6 +491,9 @@ struct psvi_plan {
     psvi::StreamRange* d_str = nullptr;
     psvi::FwdRowBlock* d_sfrb = nullptr;
     float* d_str_part = nullptr;
+    int* d_str_cnt = nullptr;  // the in-kernel band combine's arrival counters (n_sfrb)
+    float* d_str_bms = nullptr;  // per band: new mean + softplus(sd), 128 floats (n_sfrb)
+    int str_max_ends = 0;      // most band ends (slots) in one run of the stream
     int n_str = 0, n_sfrb = 0, n_sslots = 0;
     int n_upd = 0;
     int upd_tiles = 0;  // c-blocks over all chunks (work measure)

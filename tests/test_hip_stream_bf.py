@@ -157,3 +157,37 @@ def test_bf_stream_at_the_bench_inputs(kind):
         assert e_b < 2 * e_f + 1e-7, (tag, e_b, e_f)
     assert l2rel(pb, o_traj[-1]) < 1e-4
     assert np.abs(pb - pf).max() < 2 * T * 1e-3
+
+
+FOLD_OFF = 32  # PSVI_DBG_STREAM_FOLD_OFF
+
+
+@pytest.mark.parametrize("layers", SHAPES)
+@pytest.mark.parametrize("kind", ["higher", "hypergrad"])
+def test_band_combine_in_kernel_equals_reduce(layers, kind):
+    """The streaming update's in-kernel band combine (the last segment of a
+    band to arrive adds the band's slots into x') against the separate
+    mvn_fwd_reduce_kernel: bitwise equal (same sum order), T = 4 steps so the
+    combined x' feeds three later steps, and run twice so the arrival counters
+    are seen to reset."""
+    from psvi.runtime import InnerLoopPlan
+    from psvi.runtime import _lib as L
+
+    lib = L.load()
+    S, M, T, seed = 128, 24, 4, 31
+    plan = InnerLoopPlan("fullcov", layers, S, M)
+    rng, p0 = _case(layers, 5)
+    t = lambda a, d=torch.float32: torch.tensor(a, dtype=d, device=DEV)
+    u = t(rng.standard_normal((M, layers[0][0])).astype(np.float32))
+    z = t(rng.integers(0, layers[-1][1], M).astype(np.int32), torch.int32)
+    w = t(O.coreset_weights(0.3 * rng.standard_normal(M), 800).astype(np.float32))
+    fold = _loop(plan, u, z, w, p0, T, kind, seed, True)
+    fold2 = _loop(plan, u, z, w, p0, T, kind, seed, True)
+    assert lib.psvi_debug_set(FOLD_OFF, 1) == 0
+    try:
+        red = _loop(plan, u, z, w, p0, T, kind, seed, True)
+    finally:
+        lib.psvi_debug_set(FOLD_OFF, 0)
+    for a, b, c in zip(fold, fold2, red):
+        assert np.array_equal(a, b)
+        assert np.array_equal(a, c)
