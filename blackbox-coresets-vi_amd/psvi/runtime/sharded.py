@@ -294,6 +294,37 @@ class ShardedInnerLoop:
         self.phase_net_half(u, z, w, h, draw=nxt if (nxt is not None and self.x_recv.is_cuda)
                             else None)
 
+    def _net_half_launcher(self, u, z, w):
+        """psvi_mvn_phase_net_part for the two halves with the argument checks
+        done once: f(h, eps_out or None, seed, offset, stream handle) -- the
+        overlap schedule's per-step host cost (two launches where the plain
+        schedule has one)."""
+        import ctypes
+
+        from ._lib import check
+        plan = self.plan
+        hv = self._views()
+        for t, d in ((u, None), (z, torch.int32), (w, None)):
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("u / z / w must be contiguous device tensors")
+        plan_checked = (u.numel() == plan.M * plan.in_features and z.numel() == plan.M
+                        and z.dtype == torch.int32 and w.numel() == plan.M)
+        if not plan_checked:
+            raise ValueError("u / z / w do not match the plan")
+        lib, fn = plan.lib, plan.lib.psvi_mvn_phase_net_part
+        base = (plan.handle, u.data_ptr(), z.data_ptr(), w.data_ptr(), self.x_recv.data_ptr(),
+                self.g_send.data_ptr(), self.parts.data_ptr())
+        rng = [(hv[h]["lo"], hv[h]["n"]) for h in range(2)]
+        n_eps = plan.eps_count
+
+        def launch(h, out, seed, offset, stream):
+            lo, n = rng[h]
+            rc = fn(*base, lo, n, out.data_ptr() if out is not None else None,
+                    n_eps if out is not None else 0, seed, offset, h, 2, ctypes.c_void_p(stream))
+            if rc:
+                check(rc, "psvi_mvn_phase_net_part")
+        return launch
+
     def run(self, u, z, w, params, m, v, T, lr, kind="higher", step0=1, seed=0, offset=0,
             elbo_parts=None, phase_events=None, overlap=False):
         """T chained inner steps on this rank with in-library Philox draws
@@ -312,14 +343,17 @@ class ShardedInnerLoop:
         [4 events]} recorded around the exchanges + network, the update and
         the sample (diagnostics; they sit between launches).
 
-        overlap=True (full-cov): the rank's samples in two halves A, B and each
-        exchange in two (list all_to_alls of per-peer views, no copies):
-          x(A) -> net(A) on the compute stream, x(B) beside it on a side stream;
-          net(B) once x(B) is in, G(A) beside it on the side stream (after
-          net(A)); G(B), then the update once G(A) is in.
-        The per-sample work and the exchanged bytes are those of the plain
-        schedule (the same parameters bit for bit; the NLL's atomic adds come in
-        another order); the draw is split between the two network launches."""
+        overlap=True (full-cov): the rank's samples in two halves A, B, each
+        with its own chain of exchange -> network -> exchange (list
+        all_to_alls of per-peer views, no copies): A on the compute stream, B
+        on a side stream, issued x(A), x(B), net(A), net(B), G(A), G(B) -- the
+        order a serialising transport (one RCCL stream) runs them in -- so x(B)
+        travels during net(A), G(A) during net(B), and the two network halves
+        (half the workgroups each) run side by side; the update waits for both
+        chains.  The per-sample work and the exchanged bytes are those of the
+        plain schedule (the same parameters bit for bit; the NLL's atomic adds
+        come in another order); the draw is split between the two network
+        launches, which share no plan scratch (net_part_ok)."""
         T = int(T)
         if T <= 0:
             return
@@ -382,6 +416,10 @@ class ShardedInnerLoop:
             cs = self._cs
             main = torch.cuda.current_stream(e_cur.device)
         side = (lambda: torch.cuda.stream(cs)) if cuda else contextlib.nullcontext
+        a2a = self.comm.all_to_all_list
+        net = self._net_half_launcher(u, z, w) if cuda else None
+        if cuda:
+            hm, hs = main.cuda_stream, cs.cuda_stream
         for t in range(T):
             ev = phase_events.get(t) if phase_events else None
             last = t + 1 == T
@@ -390,24 +428,23 @@ class ShardedInnerLoop:
                 self.draw(*nxt)
             if ev: ev[0].record()
             self.parts.zero_()
-            self.comm.all_to_all_list(hv[0]["xo"], hv[0]["xi"])          # x(A)
             if cuda:
-                cs.wait_stream(main)        # x_shard written by the last update
+                cs.wait_stream(main)        # x_shard from the last update, parts zeroed
+            a2a(hv[0]["xo"], hv[0]["xi"])                                # x(A)
             with side():
-                self.comm.all_to_all_list(hv[1]["xo"], hv[1]["xi"])      # x(B) beside net(A)
-            self._net_half(u, z, w, 0, nxt)
+                a2a(hv[1]["xo"], hv[1]["xi"])                            # x(B)
             if cuda:
-                ev_a = torch.cuda.Event()
-                ev_a.record(main)
-                main.wait_stream(cs)        # x(B) in
-            self._net_half(u, z, w, 1, nxt)
+                d = (None, 0, 0) if nxt is None else nxt
+                net(0, d[0], d[1], d[2], hm)                             # net(A)
+                net(1, d[0], d[1], d[2], hs)                             # net(B), side stream
+            else:
+                self._net_half(u, z, w, 0, nxt)
+                self._net_half(u, z, w, 1, nxt)
+            a2a(hv[0]["go"], hv[0]["gi"])                                # G(A)
             with side():
-                if cuda:
-                    cs.wait_event(ev_a)     # G(A) written by net(A)
-                self.comm.all_to_all_list(hv[0]["go"], hv[0]["gi"])      # G(A) beside net(B)
-            self.comm.all_to_all_list(hv[1]["go"], hv[1]["gi"])          # G(B)
+                a2a(hv[1]["go"], hv[1]["gi"])                            # G(B)
             if cuda:
-                main.wait_stream(cs)        # G(A) in
+                main.wait_stream(cs)        # chain B done
             if ev: ev[1].record()
             if last:
                 self.phase_update(e_cur, params, m, v, step0 + t, lr, kind)

@@ -2,11 +2,11 @@
 """The sharded step's exchange overlap on ONE GPU: rank r of a W-rank C4 plan
 runs ShardedInnerLoop.run() -- plain (x all_to_all, network, G all_to_all,
 update) and overlap=True (sample halves: x(B) beside net(A), G(A) beside
-net(B)) -- with each all_to_all replaced by device copies of the blocks rank r
-receives plus a spin of D us on the stream that issues it (standing in for
-the xGMI transfer).  Per-step device time (HIP events around T steps) against
-D: the plain schedule pays both exchanges' D, the overlapped one the x(A) and
-G(B) halves only.
+net(B)) -- with each all_to_all replaced by a device copy of the bytes rank r receives
+plus a spin of D us per whole exchange (a half exchange: D times its share of
+the bytes) on the stream that issues it (standing in for the xGMI transfer).
+Per-step device time (HIP events around T steps) against D, and the host's
+issue time per step.
 
   python tools/overlap_timing.py [--world 8] [--rank 0] [--delays 0,10,20,40] [--T 30]
 """
@@ -31,6 +31,7 @@ class SpinComm:
         self.us, self.cpu = us, cycles_per_us
         self.scratch = torch.randn(1 << 22, device=dev) * 0.1
         self.sink = torch.empty(1 << 22, device=dev)
+        self.full = None  # numel of a whole x exchange (set by the caller)
 
     def _spin(self):
         if self.us > 0:
@@ -42,11 +43,14 @@ class SpinComm:
 
     def all_to_all_list(self, outs, ins):
         # one copy of the list's total bytes (timing only: the contents are
-        # scratch either way; a per-block copy would time the host, not the GPU)
+        # scratch either way; a per-block copy would time the host, not the
+        # GPU), the spin scaled by the share of a whole exchange's bytes
         tot = sum(o.numel() for o in outs)
         if tot:
             self.sink[:tot].copy_(self.scratch[:tot])
-        self._spin()
+        if self.us > 0:
+            frac = tot / self.full if self.full else 1.0
+            torch.cuda._sleep(int(self.us * frac * self.cpu))
 
     def all_reduce(self, t):
         pass
@@ -85,6 +89,7 @@ def main():
         for overlap in (False, True):
             comm = SpinComm(dev, us, cpu)
             loop = ShardedInnerLoop("fullcov", layers, S, M, a.world, a.rank, device=dev, comm=comm)
+            comm.full = loop.x_recv.numel()
             p = reference_init_params(layers, dev)
             m, v = torch.zeros_like(p), torch.zeros_like(p)
             loop.run(u, z, w, p, m, v, 5, LR, seed=1, overlap=overlap)
