@@ -729,9 +729,10 @@ def run(rt, args, shapes=None):
     else:
         S, Mh, layers = c4sh["S"], c4sh["M"], c4sh["layers"]
         # two complete schedules of the same step (ShardedInnerLoop.run): the
-        # exchanges in series with the network, and overlapped with it (sample
-        # halves, x(B) beside net(A), G(A) beside net(B)); the headline is the
-        # faster, both are reported
+        # exchanges in series with the network, and overlapped with it (two
+        # sample halves, each its own x -> network -> G chain, the second on a
+        # side stream); the headline is the faster (the same pick on every
+        # rank: the times are maxima over ranks), both are reported
         sched = {}
         for ov in (False, True):
             log(f"C4 headline over {world} ranks ({'overlapped' if ov else 'plain'} exchanges)")
