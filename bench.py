@@ -751,11 +751,11 @@ def run(rt, args, shapes=None):
     value = steps_per_s  # one step = one inner step of ALL S samples, on every N
     if world == 1:
         upd_s = max(avg_ms["update"], 1e-9) * 1e-3
-        # dominant kernel: the update with the fused next-step sample (plus its
-        # small slot-reduce kernel, inside the same event pair)
+        # dominant kernel: the update with the fused next-step sample (its
+        # band combine in the same launch since round 6)
         wk = algorithmic_work_fused(S)
-        kname = ("mvn_stream_bf2_kernel (fused update + next-step sample, tiled state; "
-                 "fp32-faithful bf16-piece MFMA, eight waves) + mvn_fwd_reduce_kernel")
+        kname = ("mvn_stream_bf2_kernel (fused update + next-step sample with the band "
+                 "combine, tiled state; fp32-faithful bf16-piece MFMA, eight waves)")
         kernels = {kname: dict(avg_us=avg_ms["update"] * 1e3, gbs=wk["bytes"] / upd_s / 1e9,
                                tflops=wk["flops"] / upd_s / 1e12),
                    "net_kernel (+ next-step Philox draw)": dict(avg_us=avg_ms["exchange+net"] * 1e3)}
@@ -779,7 +779,7 @@ def run(rt, args, shapes=None):
         roofline = dict(bound="mfma", achieved=round(wk["flops"] / upd_s / 1e12, 2),
                         peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s")
     roofline.update(frac=round(roofline["achieved"] / roofline["peak"], 4),
-                    traffic=pmc_traffic(["mvn_stream_bf2_kernel", "mvn_fwd_reduce_kernel"])
+                    traffic=pmc_traffic(["mvn_stream_bf2_kernel"])
                     if world == 1 else None,
                     traffic_source=dict(PMC_TRAFFIC, measured_in_this_run=False,
                                         method="rocprofv3 --pmc FETCH_SIZE, then --pmc "

@@ -170,5 +170,6 @@ def test_pmc_traffic_matches_template_keys(tmp_path):
         "mvn_fwd_reduce_kernel_x": {"hbm_bytes_per_launch": 1000}}}))
     assert b.pmc_traffic(["mvn_stream_kernel", "mvn_fwd_reduce_kernel"], str(f)) == 107
     assert b.pmc_traffic(["mvn_update_kernel"], str(f)) is None
-    # the committed summary the bench line reads (the eight-wave bf16-piece kernel)
-    assert b.pmc_traffic(["mvn_stream_bf2_kernel", "mvn_fwd_reduce_kernel"]) > 122379280
+    # the committed summary the bench line reads (the eight-wave bf16-piece
+    # kernel, its band combine in the launch): at least the algorithmic bytes
+    assert b.pmc_traffic(["mvn_stream_bf2_kernel"]) > 122379280
