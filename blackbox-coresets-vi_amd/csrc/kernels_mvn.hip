@@ -2275,6 +2275,7 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
     const int S = a.S;  // 128
     unsigned long long tph[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
     // (wave 0 as a whole: the stamps stay wave-uniform, in scalar registers)
+    if (DIAG && tid == 0) a.stamps[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime();
     auto ph = [&](int qq) __attribute__((always_inline)) {
         if (DIAG && wv == 0) {
             const unsigned long long tt = __builtin_amdgcn_s_memtime();
@@ -2457,22 +2458,26 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int i = 0; i < 4; ++i) A[m][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // slot k into partial k mod 4, in slot order (mvn_fwd_reduce_kernel's sum)
-        for (int k0 = 0; k0 < nk; k0 += 4) {  // uniform
-            f32x4 v[4][4];
+        // slot k into partial k mod 4, in slot order (mvn_fwd_reduce_kernel's
+        // sum); eight slots' loads in flight per round (the walk's registers
+        // are free here): a round trip of sc1 loads is the combine's cost
+        for (int k0 = 0; k0 < nk; k0 += 8) {  // uniform
+            f32x4 v[4][8];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < 8; ++i) {
                 const int so = __builtin_amdgcn_readfirstlane((slot0 + min(k0 + i, nk - 1)) * S * 64 * 4);
+                if (k0 + i < nk || i == 0) {  // uniform
 #pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    v[m][i] = __builtin_bit_cast(
-                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, (uint32_t)((tid + 512 * m) * 16), so, 16));
+                    for (int m = 0; m < 4; ++m)
+                        v[m][i] = __builtin_bit_cast(
+                            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, (uint32_t)((tid + 512 * m) * 16), so, 16));
+                }
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 8; ++i)
                 if (k0 + i < nk)  // uniform
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) A[m][i] += v[m][i];
+                    for (int m = 0; m < 4; ++m) A[m][i & 3] += v[m][i];
         }
 #pragma unroll
         for (int m = 0; m < 4; ++m) {

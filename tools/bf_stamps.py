@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase shader clocks of the bf16-piece streaming update
-(mvn_stream_bf_kernel, DIAG build through PSVI_DBG_UPD_STAMPS): one C3
+(mvn_stream_bf2_kernel, DIAG build through PSVI_DBG_BF_STAMPS): one C3
 inner loop in Philox mode (its first step runs the kernel), clocks summed over
 each workgroup's tiles, median over workgroups, per tile.
 
@@ -47,8 +47,15 @@ def main():
         tot += per
         print(f"  {name:28s} {per:8.0f} clocks / tile")
     print(f"  {'sum':28s} {tot:8.0f}")
-    life = np.median(a[:, 10] - a[:, 12])
+    life = np.median(a[:, 10] - a[:, 13])
     print(f"  workgroup life {life:.0f} clocks ({life / np.median(tiles):.0f} / tile)")
+    comb = a[:, 12]
+    print(f"  band combines after the walk: {int((comb > 0).sum())} workgroups, clocks median "
+          f"{np.median(comb[comb > 0]) if (comb > 0).any() else 0:.0f}, max {comb.max():.0f}")
+    end = a[:, 10] - a[:, 13]
+    k = np.argsort(end)[-8:]
+    print("  the 8 longest-lived workgroups: life / combine clocks / tiles: " +
+          ", ".join(f"{end[i]:.0f}/{comb[i]:.0f}/{tiles[i]:.0f}" for i in k))
 
 
 if __name__ == "__main__":
