@@ -53,6 +53,7 @@ namespace {
 thread_local std::string g_err;
 int g_stream_wgs = 0;       // psvi_debug_set(PSVI_DBG_STREAM_WGS, n): streaming-update workgroups (0 = 256)
 int g_stream_rr = 0;        // psvi_debug_set(PSVI_DBG_STREAM_RR, 1): runs dealt round-robin over XCDs (A/B)
+int g_stream_cost = -1;     // psvi_debug_set(PSVI_DBG_STREAM_COST, first% + 1000 diag%): tile cost weights (tuning)
 int g_upd_chunk_tiles = 0;  // psvi_debug_set(PSVI_DBG_UPD_CHUNK, n): c-blocks per update chunk (0 = auto)
 
 int fail(int code, const std::string& msg) {
@@ -512,13 +513,21 @@ int build_plan(psvi_plan& p) {
                     }
             const int T = (int)tmap.size();
             const int nwg = std::max(1, std::min(g_stream_wgs > 0 ? g_stream_wgs : 256, T));
-            // equal-cost runs: a diagonal tile also updates its band's mean / sd,
-            // a band's first tile follows a slot flush and a G reload (measured
-            // shader clocks: about 0.35 and 0.4 of a plain tile)
+            // equal-cost runs: a band's diagonal (last) tile also updates the
+            // band's mean / sd, flushes its slot, drains and takes the band's
+            // ticket (and, for the last arriver, the combine after the walk); a
+            // band's first tile follows a G reload and split.  Weights 1.5 and
+            // 1.0 of a plain tile: the fastest of a sweep at C3
+            // (tools/stream_cost_sweep.py: 55.7 - 56.3 us per step against 58.4
+            // at the round-5 weights 0.35 / 0.4, which predate the in-kernel
+            // combine); workgroup stamps (tools/bf_stamps.py) show the slowest
+            // workgroups are the ones with band boundaries
             std::vector<double> cum(T + 1, 0.0);
             for (int t = 0; t < T; ++t) {
                 const uint32_t k = tmap[t] & 0x3fff, b = (tmap[t] >> 14) & 0x3fff;
-                cum[t + 1] = cum[t] + 1.0 + (k == b ? 0.35 : 0.0) + (k == 0 ? 0.4 : 0.0);
+                const double wd = g_stream_cost >= 0 ? (g_stream_cost / 1000) * 0.01 : 1.5;
+                const double wf = g_stream_cost >= 0 ? (g_stream_cost % 1000) * 0.01 : 1.0;
+                cum[t + 1] = cum[t] + 1.0 + (k == b ? wd : 0.0) + (k == 0 ? wf : 0.0);
             }
             std::vector<int> cut(nwg + 1, 0);
             cut[nwg] = T;
@@ -636,6 +645,7 @@ int psvi_debug_set(int32_t key, int32_t value) {
         case PSVI_DBG_NET_MLOOP_OFF: g_net_mloop_off = value; return 0;
         case PSVI_DBG_NET_GEO_OFF: g_net_geo_off = value; return 0;
         case PSVI_DBG_STREAM_WGS: g_stream_wgs = value; return 0;
+        case PSVI_DBG_STREAM_COST: g_stream_cost = value; return 0;
         case PSVI_DBG_STREAM_RR: g_stream_rr = value; return 0;
         case PSVI_DBG_LENET_ABLATION: g_lenet_abl = value; return 0;
         case PSVI_DBG_NET_THREADS:

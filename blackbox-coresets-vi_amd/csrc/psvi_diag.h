@@ -114,6 +114,11 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
 #define PSVI_DBG_NET_GEO_OFF 30      /* value: 1 = the network kernel's run-time
                                     geometry for the fn2 64-40-40-2 stack too,
                                     instead of its compile-time one (A/B)      */
+#define PSVI_DBG_STREAM_COST 34      /* value: first-tile% + 1000 x diagonal-tile%:
+                                    the streaming update's extra cost weights of
+                                    a band's first and diagonal (last) tiles in
+                                    the run partition (-1: the defaults; set
+                                    before creating the plan; tuning)          */
 #define PSVI_DBG_STREAM_FOLD_OFF 32  /* value: 1 = the streaming update's band
                                     combine (x' = mean + softplus(sd) eps' + the
                                     band's slots) as mvn_fwd_reduce_kernel

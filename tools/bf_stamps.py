@@ -56,6 +56,30 @@ def main():
     k = np.argsort(end)[-8:]
     print("  the 8 longest-lived workgroups: life / combine clocks / tiles: " +
           ", ".join(f"{end[i]:.0f}/{comb[i]:.0f}/{tiles[i]:.0f}" for i in k))
+    # by XCD (workgroup w on XCD w % 8) and by place in the run list (the
+    # host deals XCD x the contiguous eighth x of the runs: w // 8 is the
+    # run's place within its XCD's eighth)
+    full = st.cpu().numpy().reshape(nwg, 16).astype(np.float64)
+    life_all = full[:, 10] - full[:, 13]
+    xcd = np.arange(nwg) % 8
+    print("  life by XCD (median / max): " + ", ".join(
+        f"{x}: {np.median(life_all[xcd == x]):.0f}/{life_all[xcd == x].max():.0f}" for x in range(8)))
+    pos = np.arange(nwg) // 8
+    q = np.array_split(np.arange(nwg // 8), 4)
+    print("  life by place in the XCD's eighth (quarters, median / max): " + ", ".join(
+        f"{i}: {np.median(life_all[np.isin(pos, qq)]):.0f}/{life_all[np.isin(pos, qq)].max():.0f}"
+        for i, qq in enumerate(q)))
+    # the phases of the slowest and the fastest workgroups (clocks summed over their tiles)
+    order = np.argsort(life_all)
+    hdr = "  " + " ".join(f"{n[:9]:>9s}" for n in PH) + "   combine      life tiles"
+    for tag, idx in (("fastest", order[:6]), ("slowest", order[-10:])):
+        print(f"  {tag}:")
+        print(hdr)
+        for i in idx:
+            print("  " + " ".join(f"{full[i, qq]:9.0f}" for qq in range(len(PH))) +
+                  f" {full[i, 12]:9.0f} {life_all[i]:9.0f} {full[i, 9]:5.0f}  wg {i}")
+    rt = full[:, 11] - full[:, 11].min()
+    print(f"  end (realtime, 100 MHz ticks from the first end): p50 {np.median(rt):.0f} max {rt.max():.0f}")
 
 
 if __name__ == "__main__":
