@@ -2461,10 +2461,12 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         // slot k into partial k mod 4, in slot order (mvn_fwd_reduce_kernel's
         // sum); eight slots' loads in flight per round (the walk's registers
         // are free here): a round trip of sc1 loads is the combine's cost
-        for (int k0 = 0; k0 < nk; k0 += 8) {  // uniform
-            f32x4 v[4][8];
+        // (four in the stamps build, whose stamp registers would spill)
+        constexpr int KR = DIAG ? 4 : 8;
+        for (int k0 = 0; k0 < nk; k0 += KR) {  // uniform
+            f32x4 v[4][KR];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < KR; ++i) {
                 const int so = __builtin_amdgcn_readfirstlane((slot0 + min(k0 + i, nk - 1)) * S * 64 * 4);
                 if (k0 + i < nk || i == 0) {  // uniform
 #pragma unroll
@@ -2474,7 +2476,7 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
                 }
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < KR; ++i)
                 if (k0 + i < nk)  // uniform
 #pragma unroll
                     for (int m = 0; m < 4; ++m) A[m][i & 3] += v[m][i];
