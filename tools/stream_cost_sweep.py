@@ -19,6 +19,8 @@ def main():
     from psvi.runtime import InnerLoopPlan
     from psvi.runtime import _lib as L
 
+    if os.environ.get("PSVI_LIB_AB"):  # A/B against another build of the library
+        L.LIB_PATH = os.environ["PSVI_LIB_AB"]
     lib = L.load()
     dev = torch.device("cuda", 0)
     u, z, w = synthetic_inputs(dev)
