@@ -280,7 +280,10 @@ void build_kstream(psvi_plan& p) {
 // CU; a run's piece of one (row block, pass) is a segment writing its own
 // slot, and the reduce adds a (row block, pass)'s slots in segment order.
 // XCD placement as the K-split update: workgroup w -> run (w % 8) (nwg / 8) + w / 8.
-void build_fseg(psvi_plan& p) {
+// One table for nwg_max workgroups (into segs / off / rbs and the counts).
+static void build_fseg_table(const psvi_plan& p, int nwg_max, std::vector<FsSeg>& segs,
+                             std::vector<int>& off, std::vector<FwdRowBlock>& rbs, int& n_wg,
+                             int& n_slots, int& n_rb) {
     const int r = p.rank, np = (p.d.S + kKsPass - 1) / kKsPass;
     struct Blk {
         int layer, r0, r1, xcol, nkb;
@@ -294,16 +297,16 @@ void build_fseg(psvi_plan& p) {
             blks.push_back(Blk{run.layer, r0, r1, run.col + (r0 - run.lo), (kmax + 63) / 64});
         }
     }
-    p.h_fs_segs.clear();
-    p.h_fs_off.clear();
-    p.h_fs_rb.clear();
-    p.n_fswg = p.n_fs_slots = p.n_fs_rb = 0;
+    segs.clear();
+    off.clear();
+    rbs.clear();
+    n_wg = n_slots = n_rb = 0;
     const int B = (int)blks.size();
     std::vector<int64_t> ub(B + 1, 0);
     for (int b = 0; b < B; ++b) ub[b + 1] = ub[b] + (int64_t)blks[b].nkb * np;
     const int64_t U = ub[B];
     if (U == 0) return;
-    int nwg = (int)std::min<int64_t>(U, 512);
+    int nwg = (int)std::min<int64_t>(U, nwg_max);
     if (nwg >= 8) nwg -= nwg % 8;
     std::vector<int64_t> cut(nwg + 1);
     for (int w = 0; w <= nwg; ++w) cut[w] = U * w / nwg;
@@ -329,24 +332,31 @@ void build_fseg(psvi_plan& p) {
     for (int b = 0; b < B; ++b)
         for (int q = 0; q < np; ++q) {
             const size_t g = (size_t)b * np + q;
-            slot0[g] = p.n_fs_slots;
-            p.n_fs_slots += nseg[g];
-            p.h_fs_rb.push_back(FwdRowBlock{nseg[g] > 0 ? slot0[g] : 0, nseg[g], blks[b].r1 - blks[b].r0,
+            slot0[g] = n_slots;
+            n_slots += nseg[g];
+            rbs.push_back(FwdRowBlock{nseg[g] > 0 ? slot0[g] : 0, nseg[g], blks[b].r1 - blks[b].r0,
                                             blks[b].xcol, blks[b].layer, blks[b].r0, kKsPass * q});
         }
-    p.h_fs_off.push_back(0);
+    off.push_back(0);
     for (int w = 0; w < nwg; ++w) {
         const int run = (nwg % 8 == 0) ? (w % 8) * (nwg / 8) + w / 8 : w;
         for (const Piece& pc : per[run]) {
             const Blk& bk = blks[pc.b];
             const size_t g = (size_t)pc.b * np + pc.pass;
-            p.h_fs_segs.push_back(FsSeg{bk.layer, bk.r0, bk.r1, pc.pass, 64 * pc.kb0, 64 * pc.kb1,
-                                        slot0[g] + seen[g]++, 0});
+            segs.push_back(FsSeg{bk.layer, bk.r0, bk.r1, pc.pass, 64 * pc.kb0, 64 * pc.kb1,
+                                 slot0[g] + seen[g]++, 0});
         }
-        p.h_fs_off.push_back((int)p.h_fs_segs.size());
+        off.push_back((int)segs.size());
     }
-    p.n_fswg = nwg;
-    p.n_fs_rb = (int)p.h_fs_rb.size();
+    n_wg = nwg;
+    n_rb = (int)rbs.size();
+}
+
+// The sample's table over 512 workgroups (two per CU), and the HVP pair's over
+// 256 (one eight-wave workgroup per CU: runs twice as long, fewer slots).
+void build_fseg(psvi_plan& p) {
+    build_fseg_table(p, 512, p.h_fs_segs, p.h_fs_off, p.h_fs_rb, p.n_fswg, p.n_fs_slots, p.n_fs_rb);
+    build_fseg_table(p, 256, p.h_fp_segs, p.h_fp_off, p.h_fp_rb, p.n_fpwg, p.n_fp_slots, p.n_fp_rb);
 }
 
 // make_lenet (neural_net.py:334-359): five mean-field-style layers, the first
@@ -776,7 +786,11 @@ int psvi_plan_create(int32_t family, const psvi_net_desc* d, int32_t world, int3
         if (!rc && p->n_fswg > 0) {
             if (!(rc = upload(p->h_fs_segs, &p->d_fs_segs)) && !(rc = upload(p->h_fs_off, &p->d_fs_off)))
                 rc = upload(p->h_fs_rb, &p->d_fs_rb);
-            const size_t sb = sizeof(float) * (size_t)std::max(1, p->n_fs_slots) * kKsPass * kFwdRows;
+            if (!rc && !(rc = upload(p->h_fp_segs, &p->d_fp_segs)) && !(rc = upload(p->h_fp_off, &p->d_fp_off)))
+                rc = upload(p->h_fp_rb, &p->d_fp_rb);
+            // (the slots serve both tables)
+            const size_t sb = sizeof(float) * (size_t)std::max({1, p->n_fs_slots, p->n_fp_slots}) * kKsPass *
+                              kFwdRows;
             if (!rc && hipMalloc((void**)&p->d_fs_part, sb) != hipSuccess)
                 rc = fail(PSVI_EUNSUP, "cannot allocate the segmented sample's slots");
         }
@@ -848,6 +862,9 @@ int psvi_plan_destroy(psvi_plan* p) {
     if (p->d_fs_segs) (void)hipFree(p->d_fs_segs);
     if (p->d_fs_off) (void)hipFree(p->d_fs_off);
     if (p->d_fs_rb) (void)hipFree(p->d_fs_rb);
+    if (p->d_fp_segs) (void)hipFree(p->d_fp_segs);
+    if (p->d_fp_off) (void)hipFree(p->d_fp_off);
+    if (p->d_fp_rb) (void)hipFree(p->d_fp_rb);
     if (p->d_fs_part) (void)hipFree(p->d_fs_part);
     if (p->d_net_bands) (void)hipFree(p->d_net_bands);
     if (p->d_eps_planes) (void)hipFree(p->d_eps_planes);
@@ -899,7 +916,10 @@ static HvpWs hvp_ws(const psvi_plan* p, void* ws) {
     o.du = (float*)take(sizeof(float) * S * M * D);
     o.nlld = (float*)take(sizeof(float) * S * M);
     if (p->family == PSVI_FAMILY_FULLCOV)
-        o.part2 = (float*)take(sizeof(float) * (size_t)p->n_fwd * S * kFwdRows);
+        o.part2 = (float*)take(sizeof(float) *
+                               std::max({(size_t)p->n_fwd * S, (size_t)p->n_fp_slots * kKsPass,
+                                         (size_t)p->n_fs_slots * kKsPass}) *
+                               kFwdRows);  // item-grid or either segment table's slots
     o.bytes = off;
     return o;
 }

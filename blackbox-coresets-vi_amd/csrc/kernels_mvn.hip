@@ -47,6 +47,15 @@ constexpr int FST = 128;   // samples per pass: 4 waves x 32
 constexpr int FLD = FBK + 4;  // LDS row stride: 16-byte rows (float4 stores, ds_read_b128)
 
 // bf16 pieces (fp32-faithful products on v_mfma_f32_32x32x16_bf16): the
+// cache policy of mvn_stream_bf2_kernel's tiled-state loads: read once per
+// launch, so nt (2) -- the L2 keeps the eps planes, which every tile of a
+// column re-reads.  C3 (tools/gpu_g25.sh): 180.8 -> 175.7 MB per launch
+// (FETCH_SIZE x 2 + WRITE_SIZE), kernel time unchanged (38.3 us); sc1 nt (18)
+// the same.  Other values: A/B builds only.
+#ifndef PSVI_STATE_LOAD_AUX
+#define PSVI_STATE_LOAD_AUX 2
+#endif
+
 // helpers of mvn_stream_bf2_kernel, mvn_fwd_seg_bf_kernel and the bf16 K-split update
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short bf8v __attribute__((ext_vector_type(8)));
@@ -124,6 +133,7 @@ struct FwdArgs {
     int64_t pcount;
     int slot_rows;
     int slot_frag;  // slots in MFMA fragment order (the segmented sample)
+    int seg_nrun;  // runs in seg_off (one per workgroup)
     MvnLayerArgs lay[kMaxL];
 };
 
@@ -2377,7 +2387,10 @@ __global__ __launch_bounds__(512, 1) void mvn_stream_bf2_kernel(StrArgs a) {
         if (qi < 6) {
             const int gi = qi / 3, which = qi % 3;
             const int so = __builtin_amdgcn_readfirstlane((int)(cur.tb * 4));
-            const u32x4 x = ldb(rs_t, vo_f + 1024 * gi, which == 0 ? so : which == 1 ? so + tmb : so + tvb);
+            const u32x4 x = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_t, vo_f + 1024 * gi,
+                                                             which == 0 ? so : which == 1 ? so + tmb : so + tvb,
+                                                             PSVI_STATE_LOAD_AUX));
             if (which == 0) P[gi] = __builtin_bit_cast(f32x4, x);
             else if (which == 1) M4[gi] = __builtin_bit_cast(f32x4, x);
             else V4[gi] = __builtin_bit_cast(f32x4, x);
@@ -2810,7 +2823,7 @@ int g_ks_off = 0;      // psvi_debug_set(PSVI_DBG_KSTREAM_OFF, 1): the chunked k
 int g_fs_off = 0;      // psvi_debug_set(PSVI_DBG_FWD_SEG_OFF, 1): the item-grid sample kernel at S > 128 (A/B)
 int g_ks_bf_off = 0;   // psvi_debug_set(PSVI_DBG_KSTREAM_BF_OFF, 1): the fp32 K-split update (A/B)
 int g_fs_bf_off = 0;   // psvi_debug_set(PSVI_DBG_FWD_SEG_BF_OFF, 1): the fp32 segmented sample (A/B)
-int g_fwd_pair_bf = 0;  // psvi_debug_set(PSVI_DBG_FWD_PAIR_BF, 1): the HVP's sample pair as two bf16-piece segmented samples (A/B)
+int g_fwd_pair_bf = 1;  // psvi_debug_set(PSVI_DBG_FWD_PAIR_BF, 0): the HVP's sample pair on the fp32 item grid (A/B)
 int g_stream_fold_off = 0;  // psvi_debug_set(PSVI_DBG_STREAM_FOLD_OFF, 1): the band combine as mvn_fwd_reduce_kernel (A/B)
 
 int g_upd_ablation = 0;                      // psvi_debug_set(PSVI_DBG_UPD_ABLATION, mask)
@@ -2834,22 +2847,34 @@ static void fill_layers(const psvi_plan& p, MvnLayerArgs* la) {
 // + 7 of row l32 -- the same k order for A (eps, M = samples) and B (L, N =
 // rows), so the accumulators, slots and reduce are mvn_fwd_seg_kernel's.
 // 72 KB of LDS: two workgroups per CU, as the fp32 kernel.
+//
+// PAIR (psvi_hvp's sample pair, launch_mvn_fwd_pair): x = L eps and the
+// tangent x2 = Lv eps in one launch on the same segments.  Eight waves: wave
+// group g = wv >> 2 stages and multiplies group g's matrix (g 0: params, 1:
+// params2) into its own L image and writes its own slots (part / part2); the
+// eps stage is shared, each group staging half of its rows.  96 KB of LDS, one
+// workgroup per CU (the same eight waves per CU as two single workgroups).
 constexpr int kSegEImg = FST * 128;       // bytes per eps plane image
 constexpr int kSegLImg = kFwdRows * 128;  // bytes per L plane image
 __device__ __forceinline__ int seg_img(int s, int chunk) {
     return s * 128 + ((chunk ^ ((s >> 1) & 7)) << 4);
 }
-__global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t smb[3 * kSegEImg + 3 * kSegLImg];
-    uint8_t* const Eb = smb;
-    uint8_t* const Lb = smb + 3 * kSegEImg;
+template <bool PAIR>
+__global__ __launch_bounds__(PAIR ? 512 : 256, PAIR ? 1 : 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
+    constexpr int NG = PAIR ? 2 : 1;  // matrices (wave groups)
+    __shared__ __attribute__((aligned(16))) uint8_t smb[3 * kSegEImg + NG * 3 * kSegLImg];
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    const int tid = threadIdx.x, lane = tid & 63, wv = wave_id(), h = lane >> 5, l32 = lane & 31;
-    const int col4 = tid & 15, srow = tid >> 4;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int gw = PAIR ? __builtin_amdgcn_readfirstlane(wave_id() >> 2) : 0;  // wave group
+    const int wv = wave_id() & 3, tl = tid & 255;
+    const int col4 = tl & 15, srow = tl >> 4;
+    uint8_t* const Eb = smb;
+    uint8_t* const Lb = smb + 3 * kSegEImg + gw * 3 * kSegLImg;
     constexpr int FT = kFwdRows / 32, LJ = kFwdRows / 16;
+    constexpr int EJ = 8 / NG;  // eps rows staged per thread: rows srow + 16 (EJ gw + j)
     const rsrc_t re = make_rsrc(a.eps, 4 * a.e_total);
-    const rsrc_t rp = make_rsrc(a.params, 4 * a.pcount);
-    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[blockIdx.x + 1];
+    const rsrc_t rp = make_rsrc(gw ? a.params2 : a.params, 4 * a.pcount);
+    const int sbeg = a.seg_off[blockIdx.x], send = a.seg_off[min((int)blockIdx.x + 1, a.seg_nrun)];
     if (sbeg >= send) return;  // uniform, before any barrier
     // a stage: column block kb of segment si (si == send: past the run's end)
     struct St {
@@ -2883,8 +2908,8 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
         return d.kb + FBK < d.k1 ? stage_at(d.si, d.kb + FBK) : stage_at(d.si + 1, -1);
     };
     // two register sets: stage i + 2 is loaded behind stage i's MFMAs
-    float4 lreg[2][LJ], ereg[2][8];
-    auto fetch = [&](const St& d, float4 (&lr)[LJ], float4 (&er)[8]) __attribute__((always_inline)) {
+    float4 lreg[2][LJ], ereg[2][EJ];
+    auto fetch = [&](const St& d, float4 (&lr)[LJ], float4 (&er)[EJ]) __attribute__((always_inline)) {
         if (d.si >= send) return;  // uniform
 #pragma unroll
         for (int j = 0; j < LJ; ++j) {
@@ -2894,8 +2919,8 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
                 float4, __builtin_amdgcn_raw_buffer_load_b128(rp, (uint32_t)(d.corr + ro + d.kb + 4 * col4) * 4u, 0, 0));
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int sr = d.s0 + srow + 16 * j;
+        for (int j = 0; j < EJ; ++j) {
+            const int sr = d.s0 + srow + 16 * (EJ * gw + j);
             const uint32_t eo = sr < a.S ? (uint32_t)(d.eoff + sr * d.n + d.kb + 4 * col4) * 4u : kOOB;
             er[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(re, eo, 0, 0));
         }
@@ -2911,7 +2936,7 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
         *reinterpret_cast<u32x2*>(q + pbytes) = u32x2{x1[0], x1[1]};
         *reinterpret_cast<u32x2*>(q + 2 * pbytes) = u32x2{x2[0], x2[1]};
     };
-    auto stage = [&](const St& d, const float4 (&lr)[LJ], const float4 (&er)[8]) __attribute__((always_inline)) {
+    auto stage = [&](const St& d, const float4 (&lr)[LJ], const float4 (&er)[EJ]) __attribute__((always_inline)) {
         const int c = d.kb + 4 * col4;
 #pragma unroll
         for (int j = 0; j < LJ; ++j) {
@@ -2927,7 +2952,7 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
             put(Lb, kSegLImg, srow + 16 * j, o);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) put(Eb, kSegEImg, srow + 16 * j, er[j]);
+        for (int j = 0; j < EJ; ++j) put(Eb, kSegEImg, srow + 16 * (EJ * gw + j), er[j]);
     };
     // operand bases: A row 32 wv + l32 of the eps image, B rows 32 t + l32 of
     // the L image; K-step t, half h -> chunk 2 t + h (the swizzle of row s
@@ -2974,7 +2999,7 @@ __global__ __launch_bounds__(256, 2) void mvn_fwd_seg_bf_kernel(FwdArgs a) {
             // the accumulators in fragment order, as mvn_fwd_seg_kernel
             if (wave_live) {
                 const FsSeg g = a.segs[cur.si];
-                float* slot = a.part + (size_t)g.slot * FST * kFwdRows + (size_t)wv * FT * 16 * 64 + lane;
+                float* slot = (gw ? a.part2 : a.part) + (size_t)g.slot * FST * kFwdRows + (size_t)wv * FT * 16 * 64 + lane;
 #pragma unroll
                 for (int t = 0; t < FT; ++t)
 #pragma unroll
@@ -3145,11 +3170,12 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
         a.part = p.d_fs_part;
         a.slot_rows = FST;
         a.slot_frag = 1;
+        a.seg_nrun = p.n_fswg;
         a.abl = 0;
         if (g_fs_bf_off || a.stamps)
             hipLaunchKernelGGL(mvn_fwd_seg_kernel, dim3(p.n_fswg), dim3(256), 0, st, a);
         else
-            hipLaunchKernelGGL(mvn_fwd_seg_bf_kernel, dim3(p.n_fswg), dim3(256), 0, st, a);
+            hipLaunchKernelGGL(mvn_fwd_seg_bf_kernel<false>, dim3(p.n_fswg), dim3(256), 0, st, a);
         hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_fs_rb, FST / kRedSpb), dim3(256), 0, st,
                            p.d_fs_rb, p.d_fs_part, a, x_shard);
         return hipGetLastError();
@@ -3169,14 +3195,34 @@ hipError_t launch_mvn_fwd(const psvi_plan& p, const float* eps, const float* par
 hipError_t launch_mvn_fwd_pair(const psvi_plan& p, const float* eps, const float* params,
                                float* x, const float* vec, float* x2, float* part2,
                                hipStream_t st) {
-    if (p.n_fswg > 0 && !g_fs_off && !g_fs_bf_off && g_fwd_pair_bf) {
-        // (A/B) the segmented sample on bf16 pieces (fp32-faithful), twice on
-        // the plan's slots: x, then the tangent x2 with the diagonal from
-        // params.  Measured at C3: 2 x (20.1 + 6.8) us against the fp32
-        // item-grid pair's one launch of both (39.4 + 7 us), so the pair stays
-        // on the item grid
-        if (hipError_t e = launch_mvn_fwd(p, eps, params, x, st)) return e;
-        return launch_mvn_fwd(p, eps, vec, x2, st, params);
+    if (p.n_fpwg > 0 && !g_fs_off && !g_fs_bf_off && g_fwd_pair_bf) {
+        // the segmented sample's units over the pair table (256 workgroups of
+        // eight waves), both matrices per unit (the eps stage shared), then the
+        // pair reduce over the two slot sets.  Measured at C3: 25.4 + 7.5 us
+        // against the fp32 item grid's 39.2 + 7.9 (psvi_hvp 0.120 -> 0.107 ms);
+        // the two bf16-piece samples one after the other took 2 x (20.1 + 6.8),
+        // the pair on the sample's 512-run table (two runs per workgroup) 29.5 + 9.3
+        FwdArgs a{};
+        a.params = params;
+        a.eps = eps;
+        a.params2 = vec;
+        a.diag_of2 = params;
+        a.part = p.d_fs_part;
+        a.part2 = part2;
+        a.ldx = p.rows_tot[p.rank];
+        a.S = p.d.S;
+        a.e_total = p.Peps;
+        a.segs = p.d_fp_segs;
+        a.seg_off = p.d_fp_off;
+        a.pcount = p.P;
+        a.slot_rows = FST;
+        a.slot_frag = 1;
+        a.seg_nrun = p.n_fpwg;
+        fill_layers(p, a.lay);
+        hipLaunchKernelGGL(mvn_fwd_seg_bf_kernel<true>, dim3(p.n_fpwg), dim3(512), 0, st, a);
+        hipLaunchKernelGGL(mvn_fwd_reduce_kernel, dim3(p.n_fp_rb, FST / kRedSpb, 2), dim3(256), 0, st, p.d_fp_rb,
+                           p.d_fs_part, a, x, x2);
+        return hipGetLastError();
     }
     FwdArgs a{};
     a.items = p.d_fwd;

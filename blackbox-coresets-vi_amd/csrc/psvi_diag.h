@@ -107,10 +107,10 @@ int psvi_debug_set_ptr(int32_t key, void* ptr);
                                     forward and R-backward) on the VALU kernel
                                     (the form for row blocks past the LDS)
                                     instead of the matrix-core one (A/B)       */
-#define PSVI_DBG_FWD_PAIR_BF 31      /* value: 1 = psvi_hvp's sample pair (x and its
-                                    tangent) as two bf16-piece segmented samples
-                                    instead of one fp32 item-grid launch of both
-                                    (A/B; measured slower at C3) */
+#define PSVI_DBG_FWD_PAIR_BF 31      /* value: 0 = psvi_hvp's sample pair (x and its
+                                    tangent) on the fp32 item grid instead of
+                                    the paired bf16-piece segmented launch
+                                    (default 1; A/B)            */
 #define PSVI_DBG_NET_GEO_OFF 30      /* value: 1 = the network kernel's run-time
                                     geometry for the fn2 64-40-40-2 stack too,
                                     instead of its compile-time one (A/B)      */

@@ -519,6 +519,15 @@ struct psvi_plan {
     psvi::FwdRowBlock* d_fs_rb = nullptr;
     float* d_fs_part = nullptr;
     int n_fswg = 0, n_fs_slots = 0, n_fs_rb = 0;
+    // psvi_hvp's sample pair (one eight-wave workgroup per CU): the same units
+    // over 256 workgroups, slots in d_fs_part (sized for both tables)
+    std::vector<psvi::FsSeg> h_fp_segs;
+    std::vector<int> h_fp_off;
+    std::vector<psvi::FwdRowBlock> h_fp_rb;
+    psvi::FsSeg* d_fp_segs = nullptr;
+    int* d_fp_off = nullptr;
+    psvi::FwdRowBlock* d_fp_rb = nullptr;
+    int n_fpwg = 0, n_fp_slots = 0, n_fp_rb = 0;
     // net kernel geometry
     int mchunks = 1, mc = 0, net_threads = 256, net_roles = 1;
     bool net_mloop = false;  // full-cov inner objective: the LDS-forced chunks looped in a workgroup

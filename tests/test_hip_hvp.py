@@ -76,6 +76,8 @@ def test_hvp_fullsize_vs_oracle(case):
     assert l2rel(dw, dw_o) < 1e-4, l2rel(dw, dw_o)
 
 
+
+
 @pytest.mark.parametrize("family,layers,S,M", [
     ("fullcov", [(64, 40), (40, 40), (40, 2)], 128, 100),   # C3: 50-row blocks
     ("fullcov", [(33, 17), (17, 5)], 6, 37),                # ragged: 19 / 18 rows, K not a 16-multiple
@@ -87,7 +89,9 @@ def test_hvp_kernel_forms_agree(family, layers, S, M):
     """The matrix-core R-op (net_rop_mfma_kernel, the default where a row block
     fits the LDS) against the VALU kernel (PSVI_DBG_ROP_VALU A/B), and the
     full-cov J^T G_dot on the bf16-piece K-split kernel's gradient mode (the
-    default) against the chunked fp32 kernel (PSVI_DBG_KSTREAM_OFF A/B): H vec
+    default) against the chunked fp32 kernel (PSVI_DBG_KSTREAM_OFF A/B), and
+    the sample pair (x and its tangent) on the paired bf16-piece launch (the
+    default) against the fp32 item grid (PSVI_DBG_FWD_PAIR_BF 0): H vec
     and both mixed products within 1e-5 relative (l2) -- fp32 sums in another
     order -- and the default result bitwise run to run."""
     from psvi.runtime import InnerLoopPlan
@@ -114,14 +118,19 @@ def test_hvp_kernel_forms_agree(family, layers, S, M):
 
     a, b = run(), run()
     alt = []
-    for key in (29, 19):   # the VALU R-op; the chunked gradient-mode update
-        plan.lib.psvi_debug_set(key, 1)
+    # the VALU R-op; the chunked gradient-mode update; (full-cov) the sample
+    # pair on the fp32 item grid instead of the paired bf16-piece launch
+    forms = [(29, 1, 0), (19, 1, 0)]
+    if family == "fullcov":
+        forms.append((31, 0, 1))
+    for key, val, dflt in forms:
+        plan.lib.psvi_debug_set(key, val)
         try:
             alt.append(run())
         finally:
-            plan.lib.psvi_debug_set(key, 0)
-    for x, y, r, c in zip(a, b, *alt):
+            plan.lib.psvi_debug_set(key, dflt)
+    for i, (x, y) in enumerate(zip(a, b)):
         assert np.isfinite(x).all()
         assert np.array_equal(x, y)
-        assert l2rel(x, r) < 1e-5, l2rel(x, r)
-        assert l2rel(x, c) < 1e-5, l2rel(x, c)
+        for f, r in zip(forms, alt):
+            assert l2rel(x, r[i]) < 1e-5, (f, l2rel(x, r[i]))
