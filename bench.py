@@ -92,7 +92,7 @@ def algorithmic_work(S, rows_frac=1.0, layers=LAYERS):
 # The PMC summary the roofline's `traffic` is read from, and the commit whose
 # bench it profiled (tools/round_session.sh pmc step: separate FETCH_SIZE /
 # WRITE_SIZE rocprofv3 passes of this bench); reported as `traffic_source`
-PMC_TRAFFIC = dict(file="profiles/r06_pmc_traffic.json", head="d33f79d")
+PMC_TRAFFIC = dict(file="profiles/r06_pmc_traffic.json", head="72299d8")
 
 
 def pmc_traffic(kernels, path=os.path.join(ROOT, PMC_TRAFFIC["file"])):
