@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase device timing of the inner step (HIP events around N back-to-back
-launches of one phase).  Usage: python tools/kernel_bench.py [c3|c4|c2] [iters]"""
+launches of one phase).  Usage: python tools/kernel_bench.py [c3|c4|c2] [iters]
+[KEY=VALUE ...] (psvi_debug_set keys, A/B)"""
 import json
 import math
 import os
@@ -34,6 +35,10 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c3"
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     fam, layers, S, M = CFG[name]
+    from psvi.runtime import _lib
+    for kv in sys.argv[3:]:  # KEY=VALUE: psvi_debug_set before the plan (A/B)
+        k, v = kv.split("=")
+        _lib.load().psvi_debug_set(int(k), int(v))
     dev = "cuda"
     plan = InnerLoopPlan(fam, layers, S, M)
     g = torch.Generator().manual_seed(0)

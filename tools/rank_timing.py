@@ -50,9 +50,13 @@ def main():
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--schedule", choices=("phases", "run"), default="phases")
+    ap.add_argument("--dbg", action="append", default=[], help="KEY=VALUE psvi_debug_set before the plans (A/B)")
     a = ap.parse_args()
     from bench import LR, fn2_inputs, reference_init_params
-    from psvi.runtime import randn_
+    from psvi.runtime import _lib, randn_
+    for kv in a.dbg:
+        k, v = kv.split("=")
+        _lib.load().psvi_debug_set(int(k), int(v))
     from psvi.runtime.sharded import ShardedInnerLoop
 
     W = a.world
