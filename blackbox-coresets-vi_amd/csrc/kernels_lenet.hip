@@ -1106,29 +1106,6 @@ __global__ __launch_bounds__(kThreads) void lenet_loss_tan_kernel(int rows, int 
     for (int c = 0; c < 10; ++c) ld[c] = out[c];
 }
 
-// 2x2 block of a transposed 5x5 conv: acc[q] += sum_ij w[i][j] Q[4 - i + dy][4 - j + dx]
-// over a 6x6 patch at q (row stride ld) of a zero-bordered plane
-// PAR > 0: q is a parity-split plane (da2_at layout, odd columns PAR words on)
-template <int PAR = 0>
-__device__ __forceinline__ void convT_block(const float* q, int ld, const float* wk,
-                                            float (&acc)[4]) {
-    float Q[6][6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Q[i][j] = PAR ? q[(j & 1) * PAR + i * ld + (j >> 1)] : q[i * ld + j];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const float wv = wk[i * 5 + j];
-            acc[0] += wv * Q[4 - i][4 - j];
-            acc[1] += wv * Q[4 - i][5 - j];
-            acc[2] += wv * Q[5 - i][4 - j];
-            acc[3] += wv * Q[5 - i][5 - j];
-        }
-}
-
 // The tangent backward on the matrix cores (d/du, when asked for, by
 // lenet_du_tan_kernel afterwards).  Per image, as lenet_conv_bwd_mfma_kernel:
 //   d P1_dot patches  U_dot = [A_dot | A] [B(W2) ; B(W2_dot)]   (K = 2 x 64),
@@ -1351,12 +1328,45 @@ __global__ __launch_bounds__(kTThreads, 4) void lenet_conv_bwd_tan_mfma_kernel(T
 // primal and tangent d P1 the backward kernels left in HBM:
 //   du_dot = convT(routed d P1_dot, W1) + convT(routed d P1, W1_dot)
 // (each routed value placed at its conv1 position of a zero-bordered 32 x 32
-// plane per channel, 2x2 output blocks per thread).
+// plane per channel, 2x2 output blocks per thread).  Each pooled value
+// writes its whole 2x2 conv1 block (the routed position, zeros elsewhere),
+// so the planes need no clearing between images, and the next image's
+// routes and values are loaded into registers behind this image's
+// convolution.  Planes with 46-float rows, read as float2: a wave's 16-lane
+// groups (2x2 blocks of rows yy = 0, 2, 4, ... at even columns) then cover
+// distinct banks (2 x 46 = 28 mod 32) -- the 32-float rows put every block
+// row on the same banks (3-way conflicts at ds_read_b32).  C5 (rocprof,
+// tools/gpu_g32.sh): 3.39 ms -> 3.08 (prefetch, no clearing) -> 2.41 (the
+// planes) -> 1.77 (packed fma); a second pair of accumulators: no change.
+constexpr int kDuLd = 46, kDuPlane = 32 * kDuLd;
+// 2x2 block of a transposed 5x5 conv: acc[q] += sum_ij w[i][j] Q[4 - i + dy][4 - j + dx]
+// over a 6x6 patch at q (row stride kDuLd, q 8-byte aligned) of a zero-bordered plane
+// (acc as two column pairs: each update one packed fma, v_pk_fma_f32 -- the
+// same per-element fma as the scalar form)
+typedef float duf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void convT_block2(const float* q, const float* wk, duf2 (&acc)[2]) {
+    float Q[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; j += 2) {
+            const float2 v = *reinterpret_cast<const float2*>(q + i * kDuLd + j);
+            Q[i][j] = v.x;
+            Q[i][j + 1] = v.y;
+        }
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const float wv = wk[i * 5 + j];
+            acc[0] = __builtin_elementwise_fma(duf2{wv, wv}, duf2{Q[4 - i][4 - j], Q[4 - i][5 - j]}, acc[0]);
+            acc[1] = __builtin_elementwise_fma(duf2{wv, wv}, duf2{Q[5 - i][4 - j], Q[5 - i][5 - j]}, acc[1]);
+        }
+}
 __global__ __launch_bounds__(kThreads) void lenet_du_tan_kernel(TanArgs a, const float* __restrict__ g1p,
                                                                const float* __restrict__ g1t) {
     __shared__ float w1[150], wd1[150];
-    __shared__ float da1[6 * 1024], da1d[6 * 1024];
-    __shared__ int off1[kP1];
+    __shared__ __attribute__((aligned(16))) float da1[6 * kDuPlane], da1d[6 * kDuPlane];
     const int tid = threadIdx.x, s = blockIdx.y;
     const float* ws = a.wsamp + (int64_t)s * a.n_tot;
     const float* wds = a.wdot + (int64_t)s * a.n_tot;
@@ -1364,36 +1374,53 @@ __global__ __launch_bounds__(kThreads) void lenet_du_tan_kernel(TanArgs a, const
         w1[i] = ws[i];
         wd1[i] = wds[i];
     }
-    for (int i = tid; i < 6 * 1024; i += kThreads) da1[i] = da1d[i] = 0.f;
+    for (int i = tid; i < 6 * kDuPlane; i += kThreads) da1[i] = da1d[i] = 0.f;  // the borders stay 0
     const int m0 = blockIdx.x * a.chunk, m1 = min(a.M, m0 + a.chunk);
+    constexpr int kLP = (kP1 + kThreads - 1) / kThreads;
+    int pr[kLP];
+    float pg[kLP], pt[kLP];
+    auto fetch = [&](int m) __attribute__((always_inline)) {
+        const int64_t row = (int64_t)s * a.M + m;
+#pragma unroll
+        for (int k = 0; k < kLP; ++k) {
+            const int o = min(tid + k * kThreads, kP1 - 1);
+            pr[k] = a.r1[row * kP1 + o];
+            pg[k] = g1p[row * kP1 + o];
+            pt[k] = g1t[row * kP1 + o];
+        }
+    };
+    if (m0 < m1) fetch(m0);
     for (int m = m0; m < m1; ++m) {
         const int64_t row = (int64_t)s * a.M + m;
-        __syncthreads();
-        for (int o = tid; o < kP1; o += kThreads) {
-            const int r = a.r1[row * kP1 + o], rr = r >= 0 ? r : 0;
-            const int c = o / 196, py = (o % 196) / 14, px = o % 14;
-            const int q = c * 1024 + (2 * py + (rr >> 1) + 2) * 32 + 2 * px + (rr & 1) + 2;
-            off1[o] = q;
-            da1[q] = g1p[row * kP1 + o];  // 0 where relu / pool drop it
-            da1d[q] = g1t[row * kP1 + o];
+        __syncthreads();  // the previous image's convolution is done with the planes
+#pragma unroll
+        for (int k = 0; k < kLP; ++k) {
+            const int o = tid + k * kThreads;
+            if (o < kP1) {
+                const int rr = pr[k] >= 0 ? pr[k] : 0;  // a dropped value (0) at offset 0
+                const int c = o / 196, py = (o % 196) / 14, px = o % 14;
+                const int q = c * kDuPlane + (2 * py + 2) * kDuLd + 2 * px + 2;
+                const float g = pg[k], t = pt[k];
+                *reinterpret_cast<float2*>(da1 + q) = make_float2(rr == 0 ? g : 0.f, rr == 1 ? g : 0.f);
+                *reinterpret_cast<float2*>(da1 + q + kDuLd) = make_float2(rr == 2 ? g : 0.f, rr == 3 ? g : 0.f);
+                *reinterpret_cast<float2*>(da1d + q) = make_float2(rr == 0 ? t : 0.f, rr == 1 ? t : 0.f);
+                *reinterpret_cast<float2*>(da1d + q + kDuLd) = make_float2(rr == 2 ? t : 0.f, rr == 3 ? t : 0.f);
+            }
         }
+        if (m + 1 < m1) fetch(m + 1);
         __syncthreads();
         if (tid < 196) {
             const int yy = 2 * (tid / 14), xx = 2 * (tid % 14);
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            duf2 acc[2] = {duf2{0.f, 0.f}, duf2{0.f, 0.f}};
 #pragma unroll 1
             for (int c = 0; c < 6; ++c) {
-                convT_block(da1d + c * 1024 + yy * 32 + xx, 32, w1 + c * 25, acc);
-                convT_block(da1 + c * 1024 + yy * 32 + xx, 32, wd1 + c * 25, acc);
+                convT_block2(da1d + c * kDuPlane + yy * kDuLd + xx, w1 + c * 25, acc);
+                convT_block2(da1 + c * kDuPlane + yy * kDuLd + xx, wd1 + c * 25, acc);
             }
             float* out = a.du + row * 784 + yy * 28 + xx;
-            out[0] = acc[0];
-            out[1] = acc[1];
-            out[28] = acc[2];
-            out[29] = acc[3];
+            *reinterpret_cast<float2*>(out) = make_float2(acc[0].x, acc[0].y);
+            *reinterpret_cast<float2*>(out + 28) = make_float2(acc[1].x, acc[1].y);
         }
-        __syncthreads();
-        for (int o = tid; o < kP1; o += kThreads) da1[off1[o]] = da1d[off1[o]] = 0.f;
     }
 }
 
