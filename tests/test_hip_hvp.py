@@ -82,6 +82,7 @@ def test_hvp_fullsize_vs_oracle(case):
     ("fullcov", [(64, 40), (40, 40), (40, 2)], 128, 100),   # C3: 50-row blocks
     ("fullcov", [(33, 17), (17, 5)], 6, 37),                # ragged: 19 / 18 rows, K not a 16-multiple
     ("fullcov", [(7, 5), (5, 3)], 4, 3),                    # 2 / 1 rows
+    ("fullcov", [(33, 17), (17, 5)], 300, 11),              # three sample passes, the last ragged
     ("meanfield", [(2, 100), (100, 4)], 32, 50),            # C2
     ("meanfield", [(5, 7), (7, 7), (7, 3)], 6, 70),
 ])
