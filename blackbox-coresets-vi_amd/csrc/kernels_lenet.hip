@@ -1117,9 +1117,9 @@ __global__ __launch_bounds__(kThreads) void lenet_loss_tan_kernel(int rows, int 
 // Eight waves: waves 0..5 own d P1 column tiles wv, wv + 8 and conv2 weight
 // tile wv; waves 6, 7 own d P1 tile wv and conv2 weight tiles 6 + 2 (wv - 6)
 // + {0, 1} (178 / 164 MFMAs per image).  LDS: P1 | P1_dot, then U_dot (the
-// weight-gradient GEMM is done before the patches are written); W2's B
-// fragments in registers, W2_dot's read from LDS per k-step (128 VGPRs: four
-// waves per SIMD, two workgroups per CU).
+// weight-gradient GEMM is done before the patches are written); W2's and
+// W2_dot's B fragments in registers (122 VGPRs: four waves per SIMD, two
+// workgroups per CU; W2_dot's read from LDS per k-step took 2 % longer).
 constexpr int kTW = 8, kTThreads = 64 * kTW;
 constexpr int kTPP = 2 * 6 * kP1C;
 static_assert(kTPP >= 25 * kUS + 1, "P1 | P1_dot region holds U_dot");
@@ -1142,19 +1142,20 @@ __global__ __launch_bounds__(kTThreads, 4) void lenet_conv_bwd_tan_mfma_kernel(T
     }
     for (int i = tid; i < 4 * kGQ; i += kTThreads) ga[i] = gad[i] = 0.f;
     __syncthreads();
-    // B fragments of the d P1 column tiles wv + 8 j: k-steps 0..15 W2 (in
-    // registers), 16..31 W2_dot (read from LDS at wo, masked by okf)
-    float bf[2][16], okf[2];
-    int wo[2];
+    // B fragments of the d P1 column tiles wv + 8 j: k-steps 0..15 W2,
+    // 16..31 W2_dot (both in registers, 0 off the tile)
+    float bf[2][16], bfd[2][16];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int tile = wv + 8 * j, n = 16 * tile + r16;
         const int c = n / 36, ay = (n % 36) / 6 - (kq >> 1), ax = n % 6 - (kq & 1);
         const bool ok = tile < 14 && n < 216 && ay >= 0 && ay < 5 && ax >= 0 && ax < 5;
-        wo[j] = ok ? c * 25 + ay * 5 + ax : 0;
-        okf[j] = ok ? 1.f : 0.f;
+        const int wo = ok ? c * 25 + ay * 5 + ax : 0;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) bf[j][t] = ok ? pp[t * 150 + wo[j]] : 0.f;
+        for (int t = 0; t < 16; ++t) {
+            bf[j][t] = ok ? pp[t * 150 + wo] : 0.f;
+            bfd[j][t] = ok ? wd2[t * 150 + wo] : 0.f;
+        }
     }
     const bool hi = wv >= 6;  // wave-uniform
     int nb2[2];
@@ -1214,8 +1215,7 @@ __global__ __launch_bounds__(kTThreads, 4) void lenet_conv_bwd_tan_mfma_kernel(T
                 const float av = ap[t * kGK];
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
-                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wd2[wo[j] + t * 150] * okf[j],
-                                                                  acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bfd[j][t], acc[j], 0, 0, 0);
             }
 #pragma unroll
             for (int j = 0; j < NT; ++j) {
